@@ -1,0 +1,64 @@
+# Native build: HIP kernels (hipcc, gfx950 only) + C++17 host runtime (g++) +
+# pybind11 module + mcg-cg CLI.   `make -j8`  (also driven by __graft_entry__.build()).
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+PYTHON    ?= python3
+
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include())")
+EXT_SUFFIX:= $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+BUILD     := build
+PKG       := cuda_mpi_parallel_amd
+PYMOD     := $(PKG)/_C$(EXT_SUFFIX)
+CLI       := bin/mcg-cg
+TESTBIN   := $(BUILD)/test_host
+
+COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-function
+HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
+CXXFLAGS  := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -pthread
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -pthread
+
+HIP_SRC   := $(wildcard csrc/gpu/*.hip)
+HOST_SRC  := $(wildcard csrc/host/*.cpp)
+GPU_CPP   := $(wildcard csrc/gpu/*.cpp)
+
+HIP_OBJ   := $(patsubst csrc/%.hip,$(BUILD)/%.o,$(HIP_SRC))
+HOST_OBJ  := $(patsubst csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(GPU_CPP))
+CORE_OBJ  := $(HIP_OBJ) $(HOST_OBJ)
+HEADERS   := $(wildcard csrc/include/mcg/*.hpp)
+
+all: $(PYMOD) $(CLI) $(TESTBIN)
+
+$(BUILD)/%.o: csrc/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/python/bindings.o: csrc/python/bindings.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -c $< -o $@
+
+$(PYMOD): $(CORE_OBJ) $(BUILD)/python/bindings.o
+	$(CXX) -shared -o $@ $^ $(LDLIBS)
+
+$(CLI): $(CORE_OBJ) $(BUILD)/cli/main.o
+	@mkdir -p bin
+	$(CXX) -o $@ $^ $(LDLIBS)
+
+$(TESTBIN): $(HOST_OBJ:$(BUILD)/gpu/%=) $(BUILD)/tests/test_host.o
+	$(CXX) -o $@ $(filter-out $(BUILD)/gpu/%,$(HOST_OBJ)) $(BUILD)/tests/test_host.o -pthread
+
+$(BUILD)/tests/test_host.o: tests/native/test_host.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+clean:
+	rm -rf $(BUILD) $(PYMOD) $(CLI)
+
+.PHONY: all clean

@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Headline benchmark: CG iterations/sec (whole node), 5-pt Poisson N=16384^2, fp64.
+
+Metric and config come from BASELINE.json: one linear system (n = 268,435,456
+rows, nnz = 1,342,111,744) solved jointly by N GPUs of one node (strong
+scaling: total work fixed), matrix 1-D row-partitioned, generated on device
+(synthetic — no dataset exists for this), random RHS.  A "step" is one full CG
+iteration: fused SpMV + pAp all-reduce + residual update + r.r all-reduce, halo
+exchange when N > 1.  tol is disabled so every timed step does real work; the
+device-side iteration counter is checked after the run.
+
+  python bench.py                      # N=1
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+      --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+import cuda_mpi_parallel_amd as mcg
+from cuda_mpi_parallel_amd.parallel import dist as pdist
+
+METRIC = "CG iterations/sec (whole node), 5-pt Poisson N=16384², 1/2/4/8 MI355X"
+BASELINE_IT_PER_S = 65.0  # BASELINE.md "Bar to clear": reference algorithm's H100 roofline (derived; nothing published)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--problem", default="poisson2d")
+    ap.add_argument("--format", default="csr", choices=["csr", "sell"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--blocks-per-cu", type=int, default=8)
+    ap.add_argument("--verify", action="store_true", help="also compute the true residual ||b-Ax|| after the run")
+    args = ap.parse_args()
+
+    env = pdist.dist_env()
+    n_gpus = args.gpus if args.gpus is not None else env.world
+    if env.world != n_gpus:
+        print(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={env.world}; launch with torchrun --nproc-per-node {n_gpus}",
+              file=sys.stderr)
+        return 2
+    pdist.set_device(env)
+    if env.world > 1:
+        pdist.init_process_group(env, backend="gloo")
+    comm = pdist.bootstrap_comm(env)
+
+    spec = mcg.make_problem(args.problem, n=args.n, rhs="random")
+    C = mcg.native()
+    opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
+                       use_graph=not args.no_graph, force_comm=False, format=args.format,
+                       blocks_per_cu=args.blocks_per_cu)
+    t_setup = time.perf_counter()
+    solver = C.Solver(spec.native(), opts, env.rank, env.world, comm)
+    solver.setup()
+    solver.reset()
+    setup_s = time.perf_counter() - t_setup
+
+    def barrier():
+        if env.world > 1:
+            dist.barrier()
+
+    solver.run_iterations(args.warmup)
+    solver.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    solver.run_iterations(args.steps)
+    solver.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+
+    if env.world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    res = solver.result()
+    ok = res["iterations"] == args.warmup + args.steps and not res["breakdown"] and math.isfinite(res["rnorm"])
+    extra = {}
+    if args.verify:
+        extra["true_rnorm"] = solver.true_residual_norm()
+    info = solver.info
+    value = args.steps / dt
+    if env.rank == 0:
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "iterations/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / BASELINE_IT_PER_S, 4),
+            "dtype": "fp64",
+            "data": "synthetic (on-device generated 5-pt Poisson matrix, random RHS)",
+            "config": {
+                "model": f"{args.problem}_N{args.n}",
+                "problem": args.problem,
+                "N": args.n,
+                "rows": spec.n_rows,
+                "nnz": spec.nnz,
+                "global_batch": 1,
+                "seq_len": spec.n_rows,
+                "parallelism": f"rowpart{n_gpus}",
+                "format": info["format"],
+                "hipgraph": not args.no_graph,
+                "halo_overlap": (not args.no_overlap) and n_gpus > 1,
+            },
+            "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
+                      "setup_s": round(setup_s, 3), "model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
+                      "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3), **extra},
+        }), flush=True)
+    if env.world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,250 @@
+// mcg-cg : command-line entry point.
+//
+// With NO arguments it behaves exactly like the reference binary
+// (CUDACG.cu:41-366): solve the built-in 3x3 system on GPU 0 with maxit=2000,
+// tol=1e-7 (absolute), print x one "%f\n" per entry, then "Success", exit 0.
+// Any failure prints a one-line message to stdout (the reference prints
+// everything through printf, CUDACG.cu:11) and exits 1; details go to stderr.
+//
+// Flags (all additive):
+//   --problem demo|poisson2d|poisson3d|randspd   --n N   --rows R --band W --density q
+//   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
+//   --maxit M  --tol T  --check-every K  --fixed-iters K  --warmup W
+//   --format csr|sell  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
+//   --print-x auto|yes|no  --report text|json  --verify
+// Multi-GPU runs use one host thread per GPU inside this process (no MPI in
+// this image); the two RCCL unique ids are shared in memory.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mcg/cg.hpp"
+#include "mcg/check.hpp"
+#include "mcg/comm.hpp"
+#include "mcg/solver.hpp"
+
+using namespace mcg;
+
+namespace {
+
+struct Args {
+  ProblemSpec spec;
+  CgOptions opt;
+  int gpus = 1;
+  bool cpu = false;
+  int sim_ranks = 1;
+  int fixed_iters = 0;
+  int warmup = 0;
+  std::string print_x = "auto";
+  std::string report = "text";
+  bool verify = false;
+  bool rhs_set = false;
+};
+
+[[noreturn]] void usage_error(const std::string& m) { fail("invalid arguments: " + m); }
+
+Args parse(int argc, char** argv) {
+  Args a;
+  auto need = [&](int& i) -> std::string {
+    if (i + 1 >= argc) usage_error(std::string("missing value for ") + argv[i]);
+    return argv[++i];
+  };
+  for (int i = 1; i < argc; ++i) {
+    std::string f = argv[i];
+    if (f == "--problem") a.spec.kind = parse_problem_kind(need(i));
+    else if (f == "--n") a.spec.N = std::stoll(need(i));
+    else if (f == "--rows") a.spec.rows = std::stoll(need(i));
+    else if (f == "--band") a.spec.band = std::stoll(need(i));
+    else if (f == "--density") a.spec.density = std::stod(need(i));
+    else if (f == "--rhs") { a.spec.rhs = parse_rhs_kind(need(i)); a.rhs_set = true; }
+    else if (f == "--seed") a.spec.seed = std::stoull(need(i));
+    else if (f == "--gpus") a.gpus = std::stoi(need(i));
+    else if (f == "--device") { std::string d = need(i); if (d == "cpu") a.cpu = true; else if (d != "gpu") usage_error(d); }
+    else if (f == "--sim-ranks") a.sim_ranks = std::stoi(need(i));
+    else if (f == "--maxit") a.opt.maxit = std::stoi(need(i));
+    else if (f == "--tol") a.opt.tol = std::stod(need(i));
+    else if (f == "--check-every") a.opt.check_every = std::stoi(need(i));
+    else if (f == "--fixed-iters") a.fixed_iters = std::stoi(need(i));
+    else if (f == "--warmup") a.warmup = std::stoi(need(i));
+    else if (f == "--format") { std::string v = need(i); a.opt.format = (v == "sell" || v == "sell64") ? 1 : 0; }
+    else if (f == "--no-overlap") a.opt.overlap = false;
+    else if (f == "--no-graph") a.opt.use_graph = false;
+    else if (f == "--force-comm") a.opt.force_comm = true;
+    else if (f == "--blocks-per-cu") a.opt.blocks_per_cu = std::stoi(need(i));
+    else if (f == "--print-x") a.print_x = need(i);
+    else if (f == "--report") a.report = need(i);
+    else if (f == "--verify") a.verify = true;
+    else if (f == "-h" || f == "--help") {
+      std::fprintf(stderr, "see csrc/cli/main.cpp header for flags\n");
+      std::exit(0);
+    } else usage_error(f);
+  }
+  if (a.spec.kind == ProblemKind::RandomSPD) {
+    if (a.spec.rows <= 0) a.spec.rows = 100000;
+    if (a.spec.band <= 0) a.spec.band = 64;
+  }
+  if (a.spec.kind != ProblemKind::Demo && !a.rhs_set) a.spec.rhs = RhsKind::Random;
+  if (a.spec.kind != ProblemKind::Demo && a.spec.N == 3 && a.spec.kind != ProblemKind::RandomSPD) a.spec.N = 1024;
+  return a;
+}
+
+class Barrier {
+ public:
+  explicit Barrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    const int gen = gen_;
+    if (++count_ == n_) { count_ = 0; ++gen_; cv_.notify_all(); return; }
+    cv_.wait(lk, [&] { return gen != gen_; });
+  }
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, gen_ = 0;
+};
+
+struct RankOut {
+  CgResult res;
+  SolverInfo info;
+  double true_rnorm = -1;
+  double bench_seconds = 0;
+  std::vector<double> x;
+  int64_t row_begin = 0;
+  std::string error, detail;
+};
+
+void run_rank(const Args& a, int rank, int world, const std::string& id_red, const std::string& id_halo,
+              Barrier& bar, bool want_x, RankOut& out) {
+  try {
+    if (hipSetDevice(rank) != hipSuccess) fail("Device Set failed");  // CUDACG.cu:87-91
+    std::unique_ptr<Comm> comm;
+    if (world > 1 || a.opt.force_comm)
+      comm.reset(new Comm(rank, world, unique_id_from_bytes(id_red), unique_id_from_bytes(id_halo)));
+    CgOptions opt = a.opt;
+    if (a.fixed_iters > 0) { opt.tol = -1.0; opt.maxit = a.fixed_iters; }
+    GpuCgSolver solver(a.spec, opt, rank, world, comm.get());
+    solver.setup();
+    out.info = solver.info();
+    out.row_begin = solver.layout().row_begin;
+    if (a.fixed_iters > 0) {
+      solver.reset();
+      solver.run_iterations(a.warmup);
+      solver.synchronize();
+      bar.wait();
+      const auto t0 = std::chrono::steady_clock::now();
+      solver.run_iterations(a.fixed_iters);
+      solver.synchronize();
+      bar.wait();
+      out.bench_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      solver.finalize();
+      out.res = solver.result();
+      out.res.solve_seconds = out.bench_seconds;
+    } else {
+      out.res = solver.solve();
+    }
+    if (a.verify) out.true_rnorm = solver.true_residual_norm();
+    if (want_x) out.x = solver.x_local();
+  } catch (const Error& e) {
+    out.error = e.what();
+    out.detail = e.detail();
+  } catch (const std::exception& e) {
+    out.error = e.what();
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  try {
+    a = parse(argc, argv);
+  } catch (const Error& e) {
+    std::printf("%s\n", e.what());
+    return EXIT_FAILURE;
+  } catch (const std::exception& e) {
+    std::printf("invalid arguments: %s\n", e.what());
+    return EXIT_FAILURE;
+  }
+  const int64_t n = global_rows(a.spec);
+  const bool want_x = a.print_x == "yes" || (a.print_x == "auto" && n <= 1000);
+  std::vector<double> x;
+  CgResult res;
+  SolverInfo info;
+  double true_rnorm = -1;
+  int world = a.cpu ? a.sim_ranks : a.gpus;
+
+  try {
+    if (a.cpu) {
+      CgOptions opt = a.opt;
+      if (a.fixed_iters > 0) { opt.tol = -1.0; opt.maxit = a.fixed_iters; }
+      res = a.sim_ranks > 1 ? cpu_cg_partitioned(a.spec, a.sim_ranks, opt, &x) : cpu_cg(a.spec, opt, &x);
+      info.n_global = n;
+    } else {
+      int ndev = 0;
+      if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) fail("Device Set failed", "no HIP device");
+      if (a.gpus < 1 || a.gpus > ndev) fail("Device Set failed", "requested more GPUs than present");
+      std::string id_red, id_halo;
+      if (a.gpus > 1 || a.opt.force_comm) {
+        id_red = unique_id_bytes();
+        id_halo = unique_id_bytes();
+      }
+      Barrier bar(a.gpus);
+      std::vector<RankOut> outs(a.gpus);
+      std::vector<std::thread> ts;
+      for (int r = 0; r < a.gpus; ++r)
+        ts.emplace_back(run_rank, std::cref(a), r, a.gpus, std::cref(id_red), std::cref(id_halo), std::ref(bar),
+                        want_x, std::ref(outs[r]));
+      for (auto& t : ts) t.join();
+      for (auto& o : outs)
+        if (!o.error.empty()) fail(o.error, o.detail);
+      res = outs[0].res;
+      info = outs[0].info;
+      true_rnorm = outs[0].true_rnorm;
+      for (auto& o : outs) {
+        res.solve_seconds = std::max(res.solve_seconds, o.res.solve_seconds);
+        res.setup_seconds = std::max(res.setup_seconds, o.res.setup_seconds);
+      }
+      if (want_x)
+        for (auto& o : outs) x.insert(x.end(), o.x.begin(), o.x.end());
+    }
+  } catch (const Error& e) {
+    std::printf("%s\n", e.what());
+    if (!e.detail().empty()) std::fprintf(stderr, "[mcg] %s\n", e.detail().c_str());
+    std::fflush(stdout);
+    (void)hipDeviceReset();
+    return EXIT_FAILURE;
+  }
+
+  if (want_x)
+    for (double v : x) std::printf("%f\n", v);  // CUDACG.cu:361-364
+
+  const double itps = res.iters_per_second();
+  if (a.report == "json") {
+    std::printf("{\"problem\": \"%s\", \"n\": %lld, \"nnz_rank0\": %lld, \"ranks\": %d, \"device\": \"%s\", "
+                "\"format\": \"%s\", \"iterations\": %d, \"converged\": %s, \"breakdown\": %s, \"rnorm\": %.6e, "
+                "\"true_rnorm\": %.6e, \"setup_s\": %.6f, \"solve_s\": %.6f, \"it_per_s\": %.3f, "
+                "\"device_bytes_rank0\": %zu}\n",
+                problem_name(a.spec).c_str(), (long long)n, (long long)info.nnz_local, world,
+                a.cpu ? "cpu" : "gpu", a.opt.format == 1 ? "sell64" : "csr", res.iterations,
+                res.converged ? "true" : "false", res.breakdown ? "true" : "false", res.rnorm, true_rnorm,
+                res.setup_seconds, res.solve_seconds, itps, info.device_bytes);
+  } else if (!want_x || n > 3) {
+    std::fprintf(stderr,
+                 "[mcg] problem=%s n=%lld ranks=%d iterations=%d converged=%d rnorm=%.3e solve=%.4fs "
+                 "(%.2f it/s) setup=%.3fs\n",
+                 problem_name(a.spec).c_str(), (long long)n, world, res.iterations, (int)res.converged, res.rnorm,
+                 res.solve_seconds, itps, res.setup_seconds);
+  }
+  std::printf("Success\n");  // CUDACG.cu:365 CLEANUP("Success")
+  return 0;
+}

@@ -1,0 +1,456 @@
+// CG hot-path kernels for gfx950 (CDNA4): wave64, 256 CUs / 8 XCDs, HBM3E.
+//
+// One CG iteration k of the reference (CUDACG.cu:269-352: SpMV, dot, 2 AXPY,
+// nrm2, SCAL+AXPY = 7 library launches, 2 blocking D2H reads) becomes
+//
+//   cg_spmv_fused  (K_A)  p_k  = r_k + beta_{k-1} p_{k-1}          [on the fly]
+//                         Ap   = A p_k                              [CSR/SELL]
+//                         x   += alpha_{k-1} p_{k-1}                [deferred x update]
+//                         partial(p_k . Ap)
+//   cg_reduce(A)          rho <- rr_new ; pAp <- sum partials   (+ RCCL all-reduce)
+//   cg_update_r    (K_B)  r   -= alpha_k Ap ; partial(r . r)
+//   cg_reduce(B)          rr_new <- sum partials ; iter++      (+ RCCL all-reduce)
+//
+// i.e. two streaming passes (136 B/row for a 5-pt CSR row instead of the
+// reference's ~192 B/row) and two 1-block reductions; all
+// scalars stay on the device.  The p_k values a row needs from its neighbours
+// are recomputed from r and p_{k-1} (bit-identical to what the owner stores),
+// so the separate AYPX pass disappears; p is double-buffered by iteration parity.
+//
+// Reductions are fixed-order (block partials -> one block), so results are
+// bitwise reproducible run to run at fixed grid size and rank count.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "mcg/check.hpp"
+#include "mcg/kernels.hpp"
+
+namespace mcg {
+
+TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1, int64_t e1) {
+  TileRanges t;
+  t.b0 = b0; t.e0 = e0 > b0 ? e0 : b0;
+  t.b1 = b1; t.e1 = e1 > b1 ? e1 : b1;
+  t.nt0 = (t.e0 - t.b0 + kTileRows - 1) / kTileRows;
+  t.ntiles = t.nt0 + (t.e1 - t.b1 + kTileRows - 1) / kTileRows;
+  return t;
+}
+
+namespace kern {
+namespace {
+
+constexpr int kBS = 256;             // threads per block = rows per CSR tile
+constexpr int kWaves = kBS / 64;
+constexpr int kCap = 2048;           // nnz staged in LDS per chunk (16 KB vals + 8 KB cols)
+constexpr int kReduceBS = 1024;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// fixed-order block reduction -> *out (thread 0)
+template <int BS>
+__device__ __forceinline__ void block_partial(double v, double* sh, double* out) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / 64; ++w) s += sh[w];
+    *out = s;
+  }
+}
+
+__device__ __forceinline__ void tile_rows(const TileRanges& tr, int64_t t, int64_t& r0, int64_t& r1) {
+  if (t < tr.nt0) {
+    r0 = tr.b0 + t * kTileRows;
+    r1 = r0 + kTileRows < tr.e0 ? r0 + kTileRows : tr.e0;
+  } else {
+    t -= tr.nt0;
+    r0 = tr.b1 + t * kTileRows;
+    r1 = r0 + kTileRows < tr.e1 ? r0 + kTileRows : tr.e1;
+  }
+}
+
+// CSR row-tile engine: a 256-row tile's rowptr slice, then its contiguous
+// nnz range in chunks of kCap, are staged through LDS with 16-B-per-lane loads
+// (coalesced 1 KiB wave accesses); each thread then walks its own row out of
+// LDS (stride-5 doubles / ints across lanes: conflict-free for ds_read_b64 and
+// ds_read_b32) and gathers x through L2/MALL.  Rows longer than kCap simply
+// span several chunks.
+template <typename IdxT, class Gather, class Epi>
+__device__ __forceinline__ void csr_tiles(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather,
+                                          Epi&& epi) {
+  __shared__ __attribute__((aligned(16))) double s_v[kCap + 2];
+  __shared__ __attribute__((aligned(16))) int32_t s_c[kCap + 4];
+  __shared__ int64_t s_rp[kBS + 1];
+  const int t = threadIdx.x;
+  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+    int64_t r0, r1;
+    tile_rows(tr, tile, r0, r1);
+    const int nr = (int)(r1 - r0);
+    if (t <= nr) s_rp[t] = (int64_t)A.rowptr[r0 + t];
+    __syncthreads();
+    const int64_t rs = s_rp[0], re = s_rp[nr];
+    int64_t my_b = 0, my_e = 0;
+    if (t < nr) {
+      my_b = s_rp[t];
+      my_e = s_rp[t + 1];
+    }
+    double sum = 0.0;
+    for (int64_t cs = rs; cs < re; cs += kCap) {
+      const int64_t ce = re < cs + kCap ? re : cs + kCap;
+      const int64_t vb = cs & ~(int64_t)1, cb = cs & ~(int64_t)3;
+      const int nv2 = (int)((ce - vb + 1) >> 1), nc4 = (int)((ce - cb + 3) >> 2);
+      const double2* gv = reinterpret_cast<const double2*>(A.vals + vb);
+      const int4* gc = reinterpret_cast<const int4*>(A.cols + cb);
+      for (int c = t; c < nv2; c += kBS) reinterpret_cast<double2*>(s_v)[c] = gv[c];
+      for (int c = t; c < nc4; c += kBS) reinterpret_cast<int4*>(s_c)[c] = gc[c];
+      __syncthreads();
+      const int64_t jb = my_b > cs ? my_b : cs, je = my_e < ce ? my_e : ce;
+      for (int64_t j = jb; j < je; ++j) sum = fma(s_v[j - vb], gather(s_c[j - cb]), sum);
+      __syncthreads();
+    }
+    if (t < nr) epi(r0 + t, sum);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K_A: fused SpMV (CSR)
+template <typename IdxT>
+__global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const double* __restrict__ r,
+                                                       const double* __restrict__ pold,
+                                                       double* __restrict__ pnew, double* __restrict__ x,
+                                                       double* __restrict__ Ap, int64_t own, TileRanges tr,
+                                                       double* __restrict__ partials,
+                                                       const CgState* __restrict__ st, double tol, int first,
+                                                       int final_mode) {
+  __shared__ double s_red[kWaves];
+  if (st->done) return;
+  const double rr = st->rr_new, rho = st->rho, pAp = st->pAp;
+  const bool conv = final_mode || (!first && sqrt(rr) < tol);
+  const double alpha = first ? 0.0 : rho / pAp;
+  const double beta = first ? 0.0 : rr / rho;
+  if (conv) {
+    // the loop exits (CUDACG.cu:333): only the deferred x += alpha_{k-1} p_{k-1}
+    for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+      int64_t r0, r1;
+      tile_rows(tr, tile, r0, r1);
+      const int64_t i = r0 + threadIdx.x;
+      if (i < r1) x[i] = fma(alpha, pold[own + i], x[i]);
+    }
+    return;
+  }
+  double acc = 0.0;
+  csr_tiles(
+      A, tr, [&](int32_t c) { return fma(beta, pold[c], r[c]); },
+      [&](int64_t i, double sum) {
+        const double po = pold[own + i];
+        const double pi = fma(beta, po, r[own + i]);
+        pnew[own + i] = pi;
+        Ap[i] = sum;
+        x[i] = fma(alpha, po, x[i]);
+        acc = fma(pi, sum, acc);
+      });
+  block_partial<kBS>(acc, s_red, partials + blockIdx.x);
+}
+
+// K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries)
+__global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const double* __restrict__ r,
+                                                            const double* __restrict__ pold,
+                                                            double* __restrict__ pnew, double* __restrict__ x,
+                                                            double* __restrict__ Ap, int64_t own, TileRanges sr,
+                                                            double* __restrict__ partials,
+                                                            const CgState* __restrict__ st, double tol,
+                                                            int first, int final_mode) {
+  __shared__ double s_red[kWaves];
+  if (st->done) return;
+  const double rr = st->rr_new, rho = st->rho, pAp = st->pAp;
+  const bool conv = final_mode || (!first && sqrt(rr) < tol);
+  const double alpha = first ? 0.0 : rho / pAp;
+  const double beta = first ? 0.0 : rr / rho;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  double acc = 0.0;
+  for (int64_t t = wid; t < sr.ntiles; t += nw) {
+    const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
+    const int64_t i = sl * 64 + lane;
+    if (conv) {
+      if (i < A.n_rows) x[i] = fma(alpha, pold[own + i], x[i]);
+      continue;
+    }
+    const int64_t base = A.slice_ptr[sl];
+    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
+    const int32_t* __restrict__ cp = A.cols + base + lane;
+    const double* __restrict__ vp = A.vals + base + lane;
+    double sum = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < w; ++j) {
+      const int32_t c = cp[64 * j];
+      sum = fma(vp[64 * j], fma(beta, pold[c], r[c]), sum);
+    }
+    if (i < A.n_rows) {
+      const double po = pold[own + i];
+      const double pi = fma(beta, po, r[own + i]);
+      pnew[own + i] = pi;
+      Ap[i] = sum;
+      x[i] = fma(alpha, po, x[i]);
+      acc = fma(pi, sum, acc);
+    }
+  }
+  if (conv) return;
+  block_partial<kBS>(acc, s_red, partials + blockIdx.x);
+}
+
+// K_B: r -= alpha Ap ; partial(r . r)      (16-B per lane)
+__global__ __launch_bounds__(kBS) void k_cg_update_r(double* __restrict__ r, const double* __restrict__ Ap,
+                                                     int64_t n, double* __restrict__ partials,
+                                                     const CgState* __restrict__ st) {
+  __shared__ double s_red[kWaves];
+  if (st->done) return;
+  const double alpha = st->rho / st->pAp;
+  const double na = -alpha;  // CUDACG.cu:320-321 : axpy with tmp2 = -alpha
+  double acc = 0.0;
+  const int64_t n2 = n >> 1;
+  double2* __restrict__ r2 = reinterpret_cast<double2*>(r);
+  const double2* __restrict__ a2 = reinterpret_cast<const double2*>(Ap);
+  const int64_t stride = (int64_t)gridDim.x * kBS;
+  for (int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x; k < n2; k += stride) {
+    double2 v = r2[k];
+    const double2 a = a2[k];
+    v.x = fma(na, a.x, v.x);
+    v.y = fma(na, a.y, v.y);
+    r2[k] = v;
+    acc = fma(v.x, v.x, acc);
+    acc = fma(v.y, v.y, acc);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const double v = fma(na, Ap[n - 1], r[n - 1]);
+    r[n - 1] = v;
+    acc = fma(v, v, acc);
+  }
+  block_partial<kBS>(acc, s_red, partials + blockIdx.x);
+}
+
+__global__ __launch_bounds__(kBS) void k_dot_partials(const double* __restrict__ a, const double* __restrict__ b,
+                                                      int64_t n, double* __restrict__ partials) {
+  __shared__ double s_red[kWaves];
+  double acc = 0.0;
+  const int64_t n2 = n >> 1;
+  const double2* __restrict__ a2 = reinterpret_cast<const double2*>(a);
+  const double2* __restrict__ b2 = reinterpret_cast<const double2*>(b);
+  const int64_t stride = (int64_t)gridDim.x * kBS;
+  for (int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x; k < n2; k += stride) {
+    const double2 u = a2[k], v = b2[k];
+    acc = fma(u.x, v.x, acc);
+    acc = fma(u.y, v.y, acc);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) acc = fma(a[n - 1], b[n - 1], acc);
+  block_partial<kBS>(acc, s_red, partials + blockIdx.x);
+}
+
+__device__ __forceinline__ double reduce_partials_1block(const double* __restrict__ p, int np, double* sh) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += kReduceBS) s += p[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  double tot = 0.0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < kReduceBS / 64; ++w) tot += sh[w];
+  }
+  return tot;  // valid in thread 0
+}
+
+__global__ __launch_bounds__(kReduceBS) void k_cg_reduce(const double* __restrict__ partials, int np,
+                                                         CgState* __restrict__ st, int mode, int first,
+                                                         double tol) {
+  __shared__ double sh[kReduceBS / 64];
+  const double tot = reduce_partials_1block(partials, np, sh);
+  if (threadIdx.x != 0) return;
+  switch (mode) {
+    case kReduceInit:
+      st->rr_new = tot;
+      st->rr0 = tot;
+      st->rho = 0.0;
+      st->pAp = 0.0;
+      st->rr_final = 0.0;
+      st->iter = 0;
+      st->done = 0;
+      st->conv_iter = 0;
+      st->converged = 0;
+      st->breakdown = 0;
+      break;
+    case kReduceA: {
+      if (st->done) { st->pAp = 0.0; break; }  // keep no-op all-reduces finite
+      const double rr = st->rr_new;
+      if (!first && sqrt(rr) < tol) {  // CUDACG.cu:333 — break after x/r update
+        st->done = 1;
+        st->converged = 1;
+        st->conv_iter = st->iter;
+        st->rr_final = rr;
+        st->pAp = 0.0;
+        break;
+      }
+      if (!isfinite(rr)) {
+        st->done = 3;
+        st->breakdown = 1;
+        st->conv_iter = st->iter;
+        st->rr_final = rr;
+        st->pAp = 0.0;
+        break;
+      }
+      st->rho = rr;
+      st->pAp = tot;
+      break;
+    }
+    case kReduceB:
+      if (st->done) { st->rr_new = 0.0; break; }
+      st->rr_new = tot;
+      st->iter += 1;
+      break;
+    case kReduceFinal:
+      if (st->done) break;
+      st->done = 2;
+      st->converged = sqrt(st->rr_new) < tol ? 1 : 0;
+      st->conv_iter = st->iter;
+      st->rr_final = st->rr_new;
+      break;
+    default: break;
+  }
+}
+
+__global__ __launch_bounds__(kReduceBS) void k_sum_partials(const double* __restrict__ partials, int np,
+                                                            double* __restrict__ out) {
+  __shared__ double sh[kReduceBS / 64];
+  const double tot = reduce_partials_1block(partials, np, sh);
+  if (threadIdx.x == 0) *out = tot;
+}
+
+// ---------------------------------------------------------------------------
+// unfused building blocks
+template <typename IdxT>
+__global__ __launch_bounds__(kBS) void k_spmv_csr(CsrDev<IdxT> A, const double* __restrict__ xv,
+                                                  double* __restrict__ y, TileRanges tr) {
+  csr_tiles(A, tr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
+}
+
+__global__ __launch_bounds__(kBS) void k_spmv_sell(SellDev A, const double* __restrict__ xv,
+                                                   double* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  const int64_t ns = (A.n_rows + 63) / 64;
+  for (int64_t sl = wid; sl < ns; sl += nw) {
+    const int64_t base = A.slice_ptr[sl];
+    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
+    double sum = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < w; ++j) sum = fma(A.vals[base + 64 * j + lane], xv[A.cols[base + 64 * j + lane]], sum);
+    const int64_t i = sl * 64 + lane;
+    if (i < A.n_rows) y[i] = sum;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_axpy(double alpha, const double* __restrict__ xv,
+                                              double* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBS;
+  for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += stride) y[i] = fma(alpha, xv[i], y[i]);
+}
+
+__global__ __launch_bounds__(kBS) void k_xpby(const double* __restrict__ xv, double beta,
+                                              double* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBS;
+  for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += stride) y[i] = fma(beta, y[i], xv[i]);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launchers
+template <typename IdxT>
+void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pold_ext, double* pnew_ext,
+                   double* x, double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int grid,
+                   const CgState* st, double tol, int first, int final_mode, hipStream_t stream) {
+  if (tr.ntiles == 0) return;
+  hipLaunchKernelGGL(k_cg_spmv_fused<IdxT>, dim3(grid), dim3(kBS), 0, stream, A, r_ext, pold_ext, pnew_ext, x,
+                     Ap, own_off, tr, partials, st, tol, first, final_mode);
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+template void cg_spmv_fused<int32_t>(const CsrDev<int32_t>&, const double*, const double*, double*, double*,
+                                     double*, int64_t, const TileRanges&, double*, int, const CgState*, double,
+                                     int, int, hipStream_t);
+template void cg_spmv_fused<int64_t>(const CsrDev<int64_t>&, const double*, const double*, double*, double*,
+                                     double*, int64_t, const TileRanges&, double*, int, const CgState*, double,
+                                     int, int, hipStream_t);
+
+void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pold_ext, double* pnew_ext,
+                        double* x, double* Ap, int64_t own_off, const TileRanges& slices, double* partials,
+                        int grid, const CgState* st, double tol, int first, int final_mode, hipStream_t stream) {
+  if (slices.ntiles == 0) return;
+  hipLaunchKernelGGL(k_cg_spmv_fused_sell, dim3(grid), dim3(kBS), 0, stream, A, r_ext, pold_ext, pnew_ext, x,
+                     Ap, own_off, slices, partials, st, tol, first, final_mode);
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+
+void cg_update_r(double* r_own, const double* Ap, int64_t n, double* partials, int grid, const CgState* st,
+                 hipStream_t stream) {
+  hipLaunchKernelGGL(k_cg_update_r, dim3(grid), dim3(kBS), 0, stream, r_own, Ap, n, partials, st);
+  MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
+}
+
+void cg_reduce(const double* partials, int np, CgState* st, int mode, int first, double tol,
+               hipStream_t stream) {
+  hipLaunchKernelGGL(k_cg_reduce, dim3(1), dim3(kReduceBS), 0, stream, partials, np, st, mode, first, tol);
+  MCG_HIP(hipGetLastError(), "compute dot failed(tmp)");
+}
+
+void dot_partials(const double* a, const double* b, int64_t n, double* partials, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(k_dot_partials, dim3(grid), dim3(kBS), 0, stream, a, b, n, partials);
+  MCG_HIP(hipGetLastError(), "compute norm2 failed(r)");
+}
+
+void sum_partials(const double* partials, int np, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kReduceBS), 0, stream, partials, np, out);
+  MCG_HIP(hipGetLastError(), "compute dot failed");
+}
+
+template <typename IdxT>
+void spmv_csr(const CsrDev<IdxT>& A, const double* x, double* y, hipStream_t stream) {
+  const TileRanges tr = make_tiles(0, A.n_rows);
+  if (tr.ntiles == 0) return;
+  const int grid = grid_for(tr.ntiles * kTileRows, kBS, 8);
+  hipLaunchKernelGGL(k_spmv_csr<IdxT>, dim3(grid), dim3(kBS), 0, stream, A, x, y, tr);
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+template void spmv_csr<int32_t>(const CsrDev<int32_t>&, const double*, double*, hipStream_t);
+template void spmv_csr<int64_t>(const CsrDev<int64_t>&, const double*, double*, hipStream_t);
+
+void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream) {
+  const int64_t ns = (A.n_rows + 63) / 64;
+  if (ns == 0) return;
+  const int grid = grid_for(ns * 64, kBS, 8);
+  hipLaunchKernelGGL(k_spmv_sell, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+
+void axpy(double alpha, const double* x, double* y, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_axpy, dim3(grid_for(n, kBS, 8)), dim3(kBS), 0, stream, alpha, x, y, n);
+  MCG_HIP(hipGetLastError(), "compute axpy failed");
+}
+
+void xpby(const double* x, double beta, double* y, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_xpby, dim3(grid_for(n, kBS, 8)), dim3(kBS), 0, stream, x, beta, y, n);
+  MCG_HIP(hipGetLastError(), "compute axpy failed(p)");
+}
+
+}  // namespace kern
+}  // namespace mcg

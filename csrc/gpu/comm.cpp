@@ -1,0 +1,82 @@
+#include "mcg/comm.hpp"
+
+#include <cstring>
+
+#include "mcg/check.hpp"
+
+namespace mcg {
+
+std::string unique_id_bytes() {
+  ncclUniqueId id;
+  MCG_RCCL(ncclGetUniqueId(&id), "RCCL unique id failed");
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+ncclUniqueId unique_id_from_bytes(const std::string& b) {
+  MCG_CHECK(b.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
+  ncclUniqueId id;
+  std::memcpy(id.internal, b.data(), sizeof(id.internal));
+  return id;
+}
+
+Comm::Comm(int rank, int world, const ncclUniqueId& reduce_id, const ncclUniqueId& halo_id)
+    : rank_(rank), world_(world) {
+  MCG_CHECK(world >= 1 && rank >= 0 && rank < world, "invalid rank/world");
+  MCG_RCCL(ncclCommInitRank(&reduce_, world, reduce_id, rank), "RCCL communicator init failed(reduce)");
+  MCG_RCCL(ncclCommInitRank(&halo_, world, halo_id, rank), "RCCL communicator init failed(halo)");
+}
+
+Comm::~Comm() {
+  if (aborted_) return;
+  if (halo_) (void)ncclCommDestroy(halo_);
+  if (reduce_) (void)ncclCommDestroy(reduce_);
+}
+
+void Comm::allreduce_sum(double* buf, size_t count, hipStream_t stream) {
+  MCG_RCCL(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, reduce_, stream), "RCCL allreduce failed");
+}
+
+void Comm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) {
+  if (!L.has_halo()) return;
+  MCG_RCCL(ncclGroupStart(), "RCCL group failed");
+  // Matching rule: for each (me, peer) pair both sides post their messages in the
+  // same order — vector-major, then ascending global row (make_layout builds
+  // sends/recvs in ascending order).
+  for (int v = 0; v < nvec; ++v) {
+    for (const HaloRange& h : L.sends)
+      MCG_RCCL(ncclSend(ext_vecs[v] + L.ext_index(h.gbegin), (size_t)h.count, ncclFloat64, h.peer, halo_, stream),
+               "RCCL halo send failed");
+    for (const HaloRange& h : L.recvs)
+      MCG_RCCL(ncclRecv(ext_vecs[v] + L.ext_index(h.gbegin), (size_t)h.count, ncclFloat64, h.peer, halo_, stream),
+               "RCCL halo recv failed");
+  }
+  MCG_RCCL(ncclGroupEnd(), "RCCL group failed");
+}
+
+void Comm::allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream) {
+  MCG_RCCL(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, reduce_, stream), "RCCL allgather failed");
+}
+
+void Comm::broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream) {
+  MCG_RCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, root, reduce_, stream), "RCCL broadcast failed");
+}
+
+void Comm::check_async() {
+  for (ncclComm_t c : {reduce_, halo_}) {
+    ncclResult_t async = ncclSuccess;
+    MCG_RCCL(ncclCommGetAsyncError(c, &async), "RCCL async error query failed");
+    if (async != ncclSuccess) {
+      abort();
+      fail("RCCL asynchronous error", ncclGetErrorString(async));
+    }
+  }
+}
+
+void Comm::abort() {
+  if (aborted_) return;
+  aborted_ = true;
+  if (halo_) (void)ncclCommAbort(halo_);
+  if (reduce_) (void)ncclCommAbort(reduce_);
+}
+
+}  // namespace mcg

@@ -1,0 +1,252 @@
+// On-device matrix/RHS generation for each rank's owned rows (SURVEY.md §2.7
+// N1-N4): count -> scan -> fill, so a 200 GB/GPU matrix never passes through
+// host memory (the reference builds its 3x3 matrix on the host and copies it,
+// CUDACG.cu:93-134).  Also CSR -> SELL-64 conversion.
+#include <hip/hip_runtime.h>
+
+#include "mcg/check.hpp"
+#include "mcg/kernels.hpp"
+
+namespace mcg {
+namespace kern {
+
+namespace {
+
+constexpr int kGenBlock = 256;
+constexpr int kScanItems = 16;                       // items per thread
+constexpr int kScanChunk = kGenBlock * kScanItems;   // 4096 items per block
+
+__global__ __launch_bounds__(kGenBlock) void k_rowlen(ProblemSpec s, int64_t row_begin, int64_t n,
+                                                      int64_t* __restrict__ rowptr) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    rowptr[i + 1] = row_length(s, row_begin + i);
+  if (blockIdx.x == 0 && threadIdx.x == 0) rowptr[0] = 0;
+}
+
+// block-wide inclusive scan of one value per thread (256 threads), returns the
+// inclusive prefix for this thread and writes the block total to *total.
+__device__ int64_t block_scan_inclusive(int64_t v, int64_t* sh, int64_t* total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int off = 1; off < kGenBlock; off <<= 1) {
+    const int64_t add = t >= off ? sh[t - off] : 0;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  const int64_t r = sh[t];
+  if (total) *total = sh[kGenBlock - 1];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kGenBlock) void k_scan_blocksums(const int64_t* __restrict__ a,
+                                                              int64_t n, int64_t* __restrict__ sums) {
+  __shared__ int64_t sh[kGenBlock];
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) s += a[base + k];
+  int64_t tot;
+  block_scan_inclusive(s, sh, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// single block: exclusive scan of nb block sums in place
+__global__ __launch_bounds__(kGenBlock) void k_scan_sums(int64_t* __restrict__ sums, int64_t nb) {
+  __shared__ int64_t sh[kGenBlock];
+  const int64_t per = (nb + kGenBlock - 1) / kGenBlock;
+  const int64_t b0 = threadIdx.x * per;
+  int64_t s = 0;
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < nb) s += sums[b0 + k];
+  const int64_t incl = block_scan_inclusive(s, sh, nullptr);
+  int64_t run = incl - s;
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < nb) {
+      const int64_t v = sums[b0 + k];
+      sums[b0 + k] = run;
+      run += v;
+    }
+}
+
+__global__ __launch_bounds__(kGenBlock) void k_scan_apply(int64_t* __restrict__ a, int64_t n,
+                                                          const int64_t* __restrict__ sums) {
+  __shared__ int64_t sh[kGenBlock];
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+  int64_t v[kScanItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = (base + k < n) ? a[base + k] : 0;
+    s += v[k];
+  }
+  const int64_t incl = block_scan_inclusive(s, sh, nullptr);
+  int64_t run = sums[blockIdx.x] + incl - s;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    run += v[k];
+    if (base + k < n) a[base + k] = run;
+  }
+}
+
+template <typename IdxT>
+__global__ __launch_bounds__(kGenBlock) void k_fill(ProblemSpec s, int64_t row_begin, int64_t n,
+                                                    int64_t col_lo, int64_t pad,
+                                                    const int64_t* __restrict__ rp64,
+                                                    IdxT* __restrict__ rp_out,
+                                                    int32_t* __restrict__ cols,
+                                                    double* __restrict__ vals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t k = rp64[i];
+    const int64_t len = rp64[i + 1] - k;
+    if (rp_out) {
+      rp_out[i] = (IdxT)k;
+      if (i == n - 1) rp_out[n] = (IdxT)rp64[n];
+    }
+    for_each_entry(s, row_begin + i, [&](int64_t c, double v) {
+      cols[k] = (int32_t)(c - col_lo + pad);
+      vals[k] = v;
+      ++k;
+    }, len);
+  }
+}
+
+__global__ __launch_bounds__(kGenBlock) void k_rhs(ProblemSpec s, int64_t row_begin, int64_t n,
+                                                   double* __restrict__ b) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    b[i] = rhs_value(s, row_begin + i);
+}
+
+// one thread per 64-row slice: slice_ptr[s+1] = 64 * max row length
+__global__ __launch_bounds__(kGenBlock) void k_sell_widths(const int64_t* __restrict__ rp, int64_t n,
+                                                           int64_t* __restrict__ sp) {
+  const int64_t ns = (n + 63) / 64;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t sl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < ns; sl += stride) {
+    int64_t w = 0;
+    const int64_t r1 = (sl + 1) * 64 < n ? (sl + 1) * 64 : n;
+    for (int64_t r = sl * 64; r < r1; ++r) {
+      const int64_t len = rp[r + 1] - rp[r];
+      w = len > w ? len : w;
+    }
+    sp[sl + 1] = 64 * w;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) sp[0] = 0;
+}
+
+template <typename IdxT>
+__global__ __launch_bounds__(kGenBlock) void k_csr_to_sell(const IdxT* __restrict__ rp,
+                                                           const int32_t* __restrict__ cols,
+                                                           const double* __restrict__ vals, int64_t n,
+                                                           int64_t own_off, const int64_t* __restrict__ sp,
+                                                           int32_t* __restrict__ scols,
+                                                           double* __restrict__ svals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t sl = i >> 6, l = i & 63;
+    const int64_t base = sp[sl], w = (sp[sl + 1] - base) >> 6;
+    const int64_t rs = rp[i], len = (int64_t)rp[i + 1] - rs;
+    for (int64_t j = 0; j < w; ++j) {
+      const int64_t dst = base + 64 * j + l;
+      if (j < len) {
+        scols[dst] = cols[rs + j];
+        svals[dst] = vals[rs + j];
+      } else {
+        scols[dst] = (int32_t)(own_off + i);
+        svals[dst] = 0.0;
+      }
+    }
+  }
+}
+
+int gen_grid(int64_t n) {
+  int64_t g = (n + kGenBlock - 1) / kGenBlock;
+  const int64_t cap = (int64_t)num_cus() * 16;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+int num_cus() {
+  static int cached = -1;
+  if (cached < 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cached = prop.multiProcessorCount;
+    else
+      cached = 256;
+  }
+  return cached;
+}
+
+int grid_for(int64_t work_items, int block, int blocks_per_cu) {
+  int64_t g = (work_items + block - 1) / block;
+  const int64_t cap = (int64_t)num_cus() * blocks_per_cu;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void gen_rowlen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t* rowptr, hipStream_t st) {
+  hipLaunchKernelGGL(k_rowlen, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, rowptr);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(gen_rowlen)");
+}
+
+int64_t scan_tmp_elems(int64_t n) { return (n + kScanChunk - 1) / kScanChunk + 1; }
+
+void scan_inclusive_i64(int64_t* a, int64_t n, int64_t* tmp, hipStream_t st) {
+  if (n <= 0) return;
+  const int64_t nb = (n + kScanChunk - 1) / kScanChunk;
+  MCG_CHECK(nb < (int64_t)1 << 31, "scan too large");
+  hipLaunchKernelGGL(k_scan_blocksums, dim3((unsigned)nb), dim3(kGenBlock), 0, st, a, n, tmp);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kGenBlock), 0, st, tmp, nb);
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(kGenBlock), 0, st, a, n, tmp);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(scan)");
+}
+
+template <typename IdxT>
+void gen_fill(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
+              const int64_t* rowptr64, IdxT* rowptr_out, int32_t* cols, double* vals, hipStream_t st) {
+  hipLaunchKernelGGL(k_fill<IdxT>, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, col_lo,
+                     pad, rowptr64, rowptr_out, cols, vals);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(gen_fill)");
+}
+template void gen_fill<int32_t>(const ProblemSpec&, int64_t, int64_t, int64_t, int64_t, const int64_t*,
+                                int32_t*, int32_t*, double*, hipStream_t);
+template void gen_fill<int64_t>(const ProblemSpec&, int64_t, int64_t, int64_t, int64_t, const int64_t*,
+                                int64_t*, int32_t*, double*, hipStream_t);
+
+void gen_rhs(const ProblemSpec& s, int64_t row_begin, int64_t n, double* b, hipStream_t st) {
+  hipLaunchKernelGGL(k_rhs, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, b);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(gen_rhs)");
+}
+
+void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr, hipStream_t st) {
+  const int64_t ns = (n + 63) / 64;
+  hipLaunchKernelGGL(k_sell_widths, dim3(gen_grid(ns)), dim3(kGenBlock), 0, st, rowptr64, n, slice_ptr);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(sell_widths)");
+}
+
+template <typename IdxT>
+void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
+                 const int64_t* slice_ptr, int32_t* scols, double* svals, hipStream_t st) {
+  hipLaunchKernelGGL(k_csr_to_sell<IdxT>, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, rowptr, cols, vals,
+                     n, own_off, slice_ptr, scols, svals);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(csr_to_sell)");
+}
+template void csr_to_sell<int32_t>(const int32_t*, const int32_t*, const double*, int64_t, int64_t,
+                                   const int64_t*, int32_t*, double*, hipStream_t);
+template void csr_to_sell<int64_t>(const int64_t*, const int32_t*, const double*, int64_t, int64_t,
+                                   const int64_t*, int32_t*, double*, hipStream_t);
+
+}  // namespace kern
+}  // namespace mcg

@@ -1,0 +1,382 @@
+#include "mcg/solver.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+
+#include "mcg/check.hpp"
+
+namespace mcg {
+
+namespace {
+constexpr int kCsrBlocksPerCuCap = 6;  // LDS-limited residency of the CSR tile kernel (26.7 KB/block)
+}
+
+GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank, int world, Comm* comm)
+    : spec_(spec), opt_(opt), rank_(rank), world_(world), comm_(comm) {
+  MCG_CHECK(world >= 1 && rank >= 0 && rank < world, "invalid rank/world");
+  MCG_CHECK(world == 1 || comm != nullptr, "multi-rank solver needs a communicator");
+  RowPartition part = partition_rows(spec_, world_);
+  L_ = make_layout(spec_, part, rank_);
+  use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
+  use_halo_ = use_comm_ && L_.has_halo();
+  s0_ = Stream(true, 0);
+  s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
+  ev_r_ = Event(true);
+  ev_h_ = Event(true);
+  ev_t0_ = Event(true, true);
+  ev_t1_ = Event(true, true);
+  ev_poll_[0] = Event(true);
+  ev_poll_[1] = Event(true);
+  host_st_ = PinnedBuffer<CgState>(2);
+}
+
+GpuCgSolver::~GpuCgSolver() {
+  if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
+  if (s0_.get()) (void)hipStreamSynchronize(s0_);
+  if (s1_.get()) (void)hipStreamSynchronize(s1_);
+}
+
+template <typename IdxT>
+void GpuCgSolver::build_csr_(DeviceBuffer<int64_t>& rp64) {
+  const int64_t n = L_.n_local();
+  if constexpr (sizeof(IdxT) == 4) {
+    rp32_.allocate(n + 1, "A");
+    kern::gen_fill<int32_t>(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), rp32_.get(), cols_.get(),
+                            vals_.get(), s0_);
+  } else {
+    kern::gen_fill<int64_t>(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), nullptr, cols_.get(),
+                            vals_.get(), s0_);
+  }
+}
+
+void GpuCgSolver::setup() {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  const int64_t n = L_.n_local();
+  info_.n_global = L_.n_global;
+  info_.n_local = n;
+  info_.ext_len = L_.ext_len;
+  info_.halo_in = L_.halo_rows_in();
+  info_.halo_out = L_.halo_rows_out();
+  info_.interior_rows = L_.interior_end - L_.interior_begin;
+  info_.format = opt_.format;
+
+  // ---- A: count -> scan -> fill (owned rows, ext-local columns) ----
+  DeviceBuffer<int64_t> rp64(n + 1, "A");
+  kern::gen_rowlen(spec_, L_.row_begin, n, rp64.get(), s0_);
+  {
+    DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(n), "A");
+    kern::scan_inclusive_i64(rp64.get() + 1, n, tmp.get(), s0_);
+    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+  }
+  int64_t nnz = 0;
+  MCG_HIP(hipMemcpy(&nnz, rp64.get() + n, sizeof(int64_t), hipMemcpyDeviceToHost),
+          "memcpy from device to host failed(A)");
+  info_.nnz_local = nnz;
+  info_.idx64 = nnz >= ((int64_t)1 << 31) - 64;
+  cols_.allocate(nnz, "A", 8);
+  vals_.allocate(nnz, "A", 8);
+  if (info_.idx64) build_csr_<int64_t>(rp64); else build_csr_<int32_t>(rp64);
+
+  size_t matrix_bytes = 0;
+  int64_t stored_entries = nnz;
+  if (opt_.format == 1) {
+    // ---- CSR -> SELL-64 ----
+    const int64_t ns = (n + 63) / 64;
+    slice_ptr_.allocate(ns + 1, "A");
+    kern::sell_slice_widths(rp64.get(), n, slice_ptr_.get(), s0_);
+    DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ns), "A");
+    kern::scan_inclusive_i64(slice_ptr_.get() + 1, ns, tmp.get(), s0_);
+    int64_t total = 0;
+    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    MCG_HIP(hipMemcpy(&total, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(A)");
+    DeviceBuffer<int32_t> scols(total, "A", 8);
+    DeviceBuffer<double> svals(total, "A", 8);
+    if (info_.idx64)
+      kern::csr_to_sell<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
+                                 scols.get(), svals.get(), s0_);
+    else
+      kern::csr_to_sell<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
+                                 scols.get(), svals.get(), s0_);
+    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    cols_ = std::move(scols);
+    vals_ = std::move(svals);
+    rp32_.release();
+    stored_entries = total;
+    matrix_bytes = total * 12 + (ns + 1) * 8;
+  } else {
+    matrix_bytes = nnz * 12 + (n + 1) * (info_.idx64 ? 8 : 4);
+    if (info_.idx64) rp64_ = std::move(rp64);
+  }
+  (void)stored_entries;
+
+  // ---- vectors ----
+  x_.allocate(n, "x", 8);
+  Ap_.allocate(n, "Ap", 8);
+  b_.allocate(n, "b", 8);
+  r_.allocate(L_.ext_len, "r", 8);
+  p_[0].allocate(L_.ext_len, "p", 8);
+  p_[1].allocate(L_.ext_len, "p", 8);
+  kern::gen_rhs(spec_, L_.row_begin, n, b_.get(), s0_);
+
+  // ---- launch geometry ----
+  const int bpc = std::max(1, opt_.blocks_per_cu);
+  auto grid_a = [&](const TileRanges& t) {
+    if (t.ntiles == 0) return 0;
+    if (opt_.format == 1) return kern::grid_for(t.ntiles * 64, 256, bpc);
+    return kern::grid_for(t.ntiles * kTileRows, 256, std::min(bpc, kCsrBlocksPerCuCap));
+  };
+  auto ranges = [&](int64_t b0, int64_t e0, int64_t b1, int64_t e1) {
+    if (opt_.format == 1) {  // slice units; rows [b,e) -> whole slices
+      return make_tiles(b0 / 64, (e0 + 63) / 64, b1 / 64, (e1 + 63) / 64);
+    }
+    return make_tiles(b0, e0, b1, e1);
+  };
+  tr_all_ = ranges(0, n, 0, 0);
+  g_all_ = grid_a(tr_all_);
+  if (use_halo_ && opt_.overlap) {
+    int64_t ib = L_.interior_begin, ie = L_.interior_end;
+    if (opt_.format == 1) {  // interior launch takes only whole slices inside the interior
+      const int64_t sb = (ib + 63) / 64, se = ie / 64;
+      if (se > sb) {
+        tr_int_ = make_tiles(sb, se);
+        tr_bnd_ = make_tiles(0, sb, se, (n + 63) / 64);
+      } else {
+        tr_int_ = make_tiles(0, 0);
+        tr_bnd_ = make_tiles(0, (n + 63) / 64);
+      }
+    } else {
+      tr_int_ = make_tiles(ib, ie);
+      tr_bnd_ = make_tiles(0, ib, ie, n);
+    }
+    g_int_ = grid_a(tr_int_);
+    g_bnd_ = grid_a(tr_bnd_);
+  }
+  g_b_ = kern::grid_for((n + 1) / 2, 256, bpc);
+  info_.grid_a = g_all_;
+  info_.grid_b = g_b_;
+  const int np = std::max({g_all_, g_int_ + g_bnd_, g_b_, 1});
+  partials_.allocate(np + 64, "partials");
+  st_.allocate(1, "state");
+  MCG_HIP(hipMemsetAsync(partials_.get(), 0, partials_.bytes(), s0_), "device memset failed");
+  MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s0_), "device memset failed");
+  MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
+
+  info_.device_bytes = matrix_bytes + (size_t)(3 * n + 3 * L_.ext_len) * 8 + (rp64_.bytes());
+  const double vec_a = 8.0 * (1 + 1 + 1 + 2 + 1);  // r, pold gathers (ideal), pnew, x rw, Ap
+  const double vec_b = 24.0;                        // r rw, Ap
+  info_.bytes_per_iter_model = (double)matrix_bytes + (vec_a + vec_b) * n;
+  setup_done_ = true;
+  setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
+}
+
+void GpuCgSolver::reset() {
+  MCG_CHECK(setup_done_, "solver not set up");
+  const int64_t n = L_.n_local();
+  hipStream_t s = s0_;
+  MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
+  MCG_HIP(hipMemsetAsync(Ap_.get(), 0, Ap_.bytes(), s), "device memset failed(Ap)");
+  MCG_HIP(hipMemsetAsync(r_.get(), 0, r_.bytes(), s), "device memset failed(r)");
+  MCG_HIP(hipMemsetAsync(p_[0].get(), 0, p_[0].bytes(), s), "device memset failed(p)");
+  MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
+  // r = b  (CUDACG.cu:248; x0 = 0 so r0 = b - A x0 = b, and p0 = r0 is formed by K_A at k = 0)
+  MCG_HIP(hipMemcpyAsync(r_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+          "vector copy failed(r)");
+  kern::dot_partials(b_.get(), b_.get(), n, partials_.get(), g_b_, s);
+  kern::cg_reduce(partials_.get(), g_b_, st_.get(), kReduceInit, 1, opt_.tol, s);
+  if (use_comm_) comm_->allreduce_sum(&st_.get()->rr_new, 1, s);
+  MCG_HIP(hipStreamSynchronize(s), "compute norm2 failed(r)");
+  k_ = 0;
+}
+
+void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
+  const int first = (k == 0) ? 1 : 0;
+  double* pold = p_[(k + 1) & 1].get();
+  double* pnew = p_[k & 1].get();
+  const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
+  const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
+  double* part = partials_.get() + (which == 2 ? g_int_ : 0);
+  if (grid == 0) return;
+  const int64_t n = L_.n_local();
+  if (opt_.format == 1) {
+    SellDev A{slice_ptr_.get(), cols_.get(), vals_.get(), n};
+    kern::cg_spmv_fused_sell(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid, st_.get(),
+                             opt_.tol, first, final_mode, s0_);
+  } else if (info_.idx64) {
+    CsrDev<int64_t> A{rp64_.get(), cols_.get(), vals_.get(), n};
+    kern::cg_spmv_fused<int64_t>(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid,
+                                 st_.get(), opt_.tol, first, final_mode, s0_);
+  } else {
+    CsrDev<int32_t> A{rp32_.get(), cols_.get(), vals_.get(), n};
+    kern::cg_spmv_fused<int32_t>(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid,
+                                 st_.get(), opt_.tol, first, final_mode, s0_);
+  }
+}
+
+void GpuCgSolver::enqueue_iteration_(int k) {
+  const int first = (k == 0) ? 1 : 0;
+  double* pold = p_[(k + 1) & 1].get();
+  int np = g_all_;
+  if (use_halo_) {
+    double* vecs[2] = {r_.get(), pold};
+    if (opt_.overlap) {
+      MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+      MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+      comm_->halo_exchange(L_, vecs, 2, s1_);
+      MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+      enqueue_spmv_(k, 1, 0);
+      MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+      enqueue_spmv_(k, 2, 0);
+      np = g_int_ + g_bnd_;
+    } else {
+      comm_->halo_exchange(L_, vecs, 2, s0_);
+      enqueue_spmv_(k, 0, 0);
+    }
+  } else {
+    enqueue_spmv_(k, 0, 0);
+  }
+  CgState* st = st_.get();
+  kern::cg_reduce(partials_.get(), np, st, kReduceA, first, opt_.tol, s0_);
+  if (use_comm_) comm_->allreduce_sum(&st->pAp, 1, s0_);
+  kern::cg_update_r(r_.get() + L_.own_off, Ap_.get(), L_.n_local(), partials_.get(), g_b_, st, s0_);
+  kern::cg_reduce(partials_.get(), g_b_, st, kReduceB, first, opt_.tol, s0_);
+  if (use_comm_) comm_->allreduce_sum(&st->rr_new, 1, s0_);
+}
+
+void GpuCgSolver::capture_pair_() {
+  hipStream_t s = s0_;
+  MCG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "graph capture failed");
+  try {
+    enqueue_iteration_(k_);
+    enqueue_iteration_(k_ + 1);
+  } catch (...) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(s, &g);
+    if (g) (void)hipGraphDestroy(g);
+    throw;
+  }
+  MCG_HIP(hipStreamEndCapture(s, &graph_), "graph capture failed");
+  MCG_HIP(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0), "graph instantiate failed");
+}
+
+void GpuCgSolver::run_iterations(int count) {
+  MCG_CHECK(setup_done_, "solver not set up");
+  while (count > 0) {
+    if (opt_.use_graph && k_ >= 2 && (k_ % 2) == 0 && count >= 2) {
+      if (!graph_exec_) {
+        try {
+          capture_pair_();
+        } catch (const Error& e) {
+          std::fprintf(stderr, "[mcg] graph capture unavailable (%s: %s); running eagerly\n", e.what(),
+                       e.detail().c_str());
+          (void)hipGetLastError();
+          opt_.use_graph = false;
+          continue;
+        }
+      }
+      MCG_HIP(hipGraphLaunch(graph_exec_, s0_), "graph launch failed");
+      k_ += 2;
+      count -= 2;
+    } else {
+      enqueue_iteration_(k_);
+      ++k_;
+      --count;
+    }
+  }
+}
+
+void GpuCgSolver::finalize() {
+  if (k_ == 0) return;
+  enqueue_spmv_(k_, 0, 1);  // pold = p_{k-1}: the deferred x += alpha p
+  kern::cg_reduce(partials_.get(), 0, st_.get(), kReduceFinal, 0, opt_.tol, s0_);
+}
+
+void GpuCgSolver::synchronize() {
+  MCG_HIP(hipStreamSynchronize(s1_), "device synchronize failed");
+  MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
+  if (use_comm_) comm_->check_async();
+}
+
+CgResult GpuCgSolver::solve() {
+  reset();
+  MCG_HIP(hipEventRecord(ev_t0_, s0_), "event record failed");
+  const int every = std::max(1, opt_.check_every);
+  int c = 0;
+  while (k_ < opt_.maxit) {
+    const int chunk = std::min(every, opt_.maxit - k_);
+    run_iterations(chunk);
+    MCG_HIP(hipMemcpyAsync(&host_st_[c & 1], st_.get(), sizeof(CgState), hipMemcpyDeviceToHost, s0_),
+            "memcpy from device to host failed(state)");
+    MCG_HIP(hipEventRecord(ev_poll_[c & 1], s0_), "event record failed");
+    if (c > 0) {
+      MCG_HIP(hipEventSynchronize(ev_poll_[(c - 1) & 1]), "event synchronize failed");
+      if (host_st_[(c - 1) & 1].done) break;
+      if (use_comm_) comm_->check_async();
+    }
+    ++c;
+  }
+  finalize();
+  MCG_HIP(hipEventRecord(ev_t1_, s0_), "event record failed");
+  synchronize();
+  return result();
+}
+
+CgResult GpuCgSolver::result() {
+  synchronize();
+  CgState st;
+  MCG_HIP(hipMemcpy(&st, st_.get(), sizeof(CgState), hipMemcpyDeviceToHost), "memcpy from device to host failed(state)");
+  CgResult r;
+  r.iterations = st.done ? st.conv_iter : st.iter;
+  r.converged = st.converged != 0;
+  r.breakdown = st.breakdown != 0;
+  r.rnorm = std::sqrt(st.done ? st.rr_final : st.rr_new);
+  r.setup_seconds = setup_seconds_;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, ev_t0_, ev_t1_) == hipSuccess) r.solve_seconds = ms * 1e-3;
+  (void)hipGetLastError();
+  return r;
+}
+
+std::vector<double> GpuCgSolver::x_local() {
+  synchronize();
+  std::vector<double> h(L_.n_local());
+  if (!h.empty())
+    MCG_HIP(hipMemcpy(h.data(), x_.get(), h.size() * sizeof(double), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(x)");
+  return h;
+}
+
+double GpuCgSolver::true_residual_norm() {
+  synchronize();
+  const int64_t n = L_.n_local();
+  DeviceBuffer<double> xe(L_.ext_len, "x", 8), y(n, "Ap", 8), out(1, "scalar");
+  hipStream_t s = s0_;
+  MCG_HIP(hipMemsetAsync(xe.get(), 0, xe.bytes(), s), "device memset failed");
+  MCG_HIP(hipMemcpyAsync(xe.get() + L_.own_off, x_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+          "vector copy failed(x)");
+  if (use_halo_) {
+    double* v[1] = {xe.get()};
+    comm_->halo_exchange(L_, v, 1, s);
+  }
+  if (opt_.format == 1) {
+    kern::spmv_sell(SellDev{slice_ptr_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
+  } else if (info_.idx64) {
+    kern::spmv_csr<int64_t>(CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
+  } else {
+    kern::spmv_csr<int32_t>(CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
+  }
+  kern::xpby(b_.get(), -1.0, y.get(), n, s);  // y = b - A x
+  kern::dot_partials(y.get(), y.get(), n, partials_.get(), g_b_, s);
+  kern::sum_partials(partials_.get(), g_b_, out.get(), s);
+  if (use_comm_) comm_->allreduce_sum(out.get(), 1, s);
+  double h = 0.0;
+  MCG_HIP(hipMemcpyAsync(&h, out.get(), sizeof(double), hipMemcpyDeviceToHost, s), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(s), "device synchronize failed");
+  return std::sqrt(h);
+}
+
+}  // namespace mcg

@@ -1,0 +1,115 @@
+#include "mcg/partition.hpp"
+
+#include <algorithm>
+
+#include "mcg/check.hpp"
+
+namespace mcg {
+
+RowPartition partition_rows(const ProblemSpec& s, int world) {
+  MCG_CHECK(world >= 1, "invalid number of ranks");
+  const int64_t n = global_rows(s);
+  int64_t g = partition_granule(s);
+  if (g < 1 || n / g < world) g = 1;
+  const int64_t units = (n + g - 1) / g;
+  RowPartition p;
+  p.offsets.resize(world + 1);
+  for (int r = 0; r <= world; ++r) {
+    const int64_t u = units * r / world;
+    p.offsets[r] = std::min(n, u * g);
+  }
+  p.offsets[world] = n;
+  return p;
+}
+
+RowPartition partition_by_weight(const std::vector<int64_t>& row_prefix, int world) {
+  MCG_CHECK(world >= 1 && !row_prefix.empty(), "invalid weighted partition input");
+  const int64_t n = (int64_t)row_prefix.size() - 1;
+  const int64_t total = row_prefix.back();
+  RowPartition p;
+  p.offsets.resize(world + 1);
+  p.offsets[0] = 0;
+  for (int r = 1; r < world; ++r) {
+    const int64_t target = (int64_t)((__int128)total * r / world);
+    // first row boundary whose prefix >= target
+    int64_t b = std::lower_bound(row_prefix.begin(), row_prefix.end(), target) - row_prefix.begin();
+    b = std::max(b, p.offsets[r - 1]);
+    p.offsets[r] = std::min(b, n);
+  }
+  p.offsets[world] = n;
+  return p;
+}
+
+void column_window(const ProblemSpec& s, int64_t r0, int64_t r1, int64_t* lo, int64_t* hi) {
+  const int64_t n = global_rows(s), bw = bandwidth(s);
+  if (r1 <= r0) { *lo = r0; *hi = r0; return; }
+  *lo = std::max<int64_t>(0, r0 - bw);
+  *hi = std::min<int64_t>(n, r1 + bw);
+}
+
+int64_t LocalLayout::halo_rows_in() const {
+  int64_t t = 0;
+  for (auto& h : recvs) t += h.count;
+  return t;
+}
+int64_t LocalLayout::halo_rows_out() const {
+  int64_t t = 0;
+  for (auto& h : sends) t += h.count;
+  return t;
+}
+
+static void intersect(int64_t a0, int64_t a1, int64_t b0, int64_t b1, int64_t* c0, int64_t* c1) {
+  *c0 = std::max(a0, b0);
+  *c1 = std::min(a1, b1);
+}
+
+LocalLayout make_layout(const ProblemSpec& s, const RowPartition& part, int rank) {
+  const int P = part.world();
+  MCG_CHECK(rank >= 0 && rank < P, "invalid rank");
+  LocalLayout L;
+  L.rank = rank;
+  L.world = P;
+  L.n_global = global_rows(s);
+  L.row_begin = part.begin(rank);
+  L.row_end = part.end(rank);
+  column_window(s, L.row_begin, L.row_end, &L.col_lo, &L.col_hi);
+  if (L.row_end <= L.row_begin) { L.col_lo = L.col_hi = L.row_begin; }
+  L.col_lo = std::min(L.col_lo, L.row_begin);
+  L.col_hi = std::max(L.col_hi, L.row_end);
+  const int64_t ghost_lo = L.row_begin - L.col_lo;
+  L.pad = (8 - ghost_lo % 8) % 8;
+  L.own_off = L.pad + ghost_lo;
+  L.ext_len = L.pad + (L.col_hi - L.col_lo);
+
+  // interior rows: every column inside [row_begin, row_end)
+  const int64_t bw = bandwidth(s);
+  int64_t ib = (L.row_begin == 0) ? 0 : L.row_begin + bw;
+  int64_t ie = (L.row_end == L.n_global) ? L.n_global : L.row_end - bw;
+  ib = std::max(ib, L.row_begin);
+  ie = std::min(ie, L.row_end);
+  if (ie < ib) ie = ib;
+  L.interior_begin = ib - L.row_begin;
+  L.interior_end = ie - L.row_begin;
+
+  // halo: what I receive = my ghost ranges ∩ peers' owned; what I send = my owned ∩ peers' ghosts
+  for (int q = 0; q < P; ++q) {
+    if (q == rank) continue;
+    const int64_t q0 = part.begin(q), q1 = part.end(q);
+    int64_t c0, c1;
+    intersect(L.col_lo, L.row_begin, q0, q1, &c0, &c1);
+    if (c1 > c0) L.recvs.push_back({q, c0, c1 - c0});
+    intersect(L.row_end, L.col_hi, q0, q1, &c0, &c1);
+    if (c1 > c0) L.recvs.push_back({q, c0, c1 - c0});
+
+    int64_t qlo, qhi;
+    column_window(s, q0, q1, &qlo, &qhi);
+    if (q1 <= q0) continue;
+    intersect(qlo, q0, L.row_begin, L.row_end, &c0, &c1);
+    if (c1 > c0) L.sends.push_back({q, c0, c1 - c0});
+    intersect(q1, qhi, L.row_begin, L.row_end, &c0, &c1);
+    if (c1 > c0) L.sends.push_back({q, c0, c1 - c0});
+  }
+  return L;
+}
+
+}  // namespace mcg

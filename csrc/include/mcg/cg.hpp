@@ -1,0 +1,68 @@
+// Solver options / results shared by the CPU reference path and the GPU solver,
+// plus the CPU reference path itself.
+//
+// Defaults reproduce the reference exactly: maxit = 2000, tol = 1e-7 on the
+// ABSOLUTE residual norm ||r||_2 (CUDACG.cu:244-245,333 — the "relative
+// residual" comment at :238 is not what the code does), x0 = 0, r0 = p0 = b,
+// and no abort on non-positive curvature (the demo matrix is indefinite).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mcg/partition.hpp"
+#include "mcg/problem.hpp"
+
+namespace mcg {
+
+struct CgOptions {
+  int maxit = 2000;          // CUDACG.cu:244
+  double tol = 1e-7;         // CUDACG.cu:245 (absolute ||r||_2)
+  int check_every = 32;      // host polls the device convergence latch every k iterations
+  bool overlap = true;       // halo on a side stream, overlapped with the interior SpMV
+  bool use_graph = true;     // capture iteration pairs into a hipGraph
+  bool force_comm = false;   // run RCCL collectives even with one rank
+  int format = 0;            // 0 = CSR (LDS-staged row tiles), 1 = SELL-64
+  int blocks_per_cu = 8;     // grid sizing for the streaming kernels
+};
+
+struct CgResult {
+  int iterations = 0;        // number of SpMVs performed (= reference loop trips)
+  bool converged = false;
+  bool breakdown = false;    // NaN/Inf in a reduction
+  double rnorm = 0.0;        // final ||r||_2 (recurrence residual)
+  double setup_seconds = 0.0;
+  double solve_seconds = 0.0;
+  double iters_per_second() const { return solve_seconds > 0 ? iterations / solve_seconds : 0.0; }
+};
+
+// Host CSR with int64 row pointers, int32 (ext-local) columns, fp64 values.
+struct HostCsr {
+  int64_t n_rows = 0;
+  std::vector<int64_t> rowptr;
+  std::vector<int32_t> cols;
+  std::vector<double> vals;
+  int64_t nnz() const { return rowptr.empty() ? 0 : rowptr.back(); }
+};
+
+// Owned rows of `L`, columns mapped to L.ext_index().  Multithreaded.
+HostCsr build_local_csr(const ProblemSpec& s, const LocalLayout& L, int threads = 0);
+std::vector<double> build_rhs(const ProblemSpec& s, int64_t r0, int64_t r1);
+// y[i] = sum_j A[i,j] x_ext[j]  (x in ext coordinates)
+void csr_spmv(const HostCsr& A, const double* x_ext, double* y);
+
+// Single-process CPU reference CG: the reference recurrence op-for-op
+// (copy, nrm2, SpMV, dot, axpy, axpy, nrm2, scal, axpy — CUDACG.cu:248-351).
+CgResult cpu_cg(const ProblemSpec& s, const CgOptions& opt, std::vector<double>* x_out,
+                std::vector<double>* rnorm_history = nullptr);
+
+// Same recurrence with P virtual ranks in one process: each rank owns a
+// LocalLayout, builds its local CSR, exchanges halos per the plan (memcpy from
+// the peer's owned block into its ghosts) and reduces dot products in rank
+// order.  Validates the partition + halo plan used by the GPU solver.
+CgResult cpu_cg_partitioned(const ProblemSpec& s, int world, const CgOptions& opt,
+                            std::vector<double>* x_out,
+                            std::vector<double>* rnorm_history = nullptr);
+
+}  // namespace mcg

@@ -1,0 +1,123 @@
+// Hand-written gfx950 kernels (launchers).  Device code lives in
+// csrc/gpu/*.hip; nothing here calls rocBLAS/rocSPARSE — the reference's
+// cuBLAS/cuSPARSE calls are replaced by:
+//
+//   cg_spmv_fused   K6+K8+K9(x)+K12+K13 : p_k = r + beta p_{k-1} (on the fly),
+//                   Ap = A p_k (CSR, LDS-staged row tiles), x += alpha_{k-1} p_{k-1},
+//                   block partials of p_k . Ap
+//   cg_update_r     K10+K11 : r -= alpha Ap, block partials of r . r
+//   cg_reduce       fixed-order sum of block partials + device-side scalar
+//                   bookkeeping (alpha/beta/rho never visit the host; K3/K8/K11's
+//                   blocking D2H reads are gone)
+//   gen_*           on-device generation of each rank's owned rows + RHS
+//   spmv_csr / dot / axpy / xpby   unfused building blocks (ops API, tests)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mcg/problem.hpp"
+
+namespace mcg {
+
+// Device-resident CG scalars.  All fields are written only by the single-block
+// cg_reduce kernel (or by RCCL in-place all-reduces of rr_new / pAp), and read
+// by the streaming kernels, so no intra-launch hand-off is ever needed.
+struct alignas(64) CgState {
+  double rr_new;  // r_k . r_k (global) — the newest residual norm^2 (all-reduce slot)
+  double rho;     // r_{k-1} . r_{k-1} after rotation (the reference's `rho`)
+  double pAp;     // p . Ap of the last SpMV (global after all-reduce; all-reduce slot)
+  double rr0;     // b . b
+  double rr_final;  // rr_new captured when the latch fires (later no-op all-reduces may clobber rr_new)
+  double pad0_[3];
+  int iter;       // completed iterations (SpMVs whose residual update ran)
+  int done;       // latch: 1 = converged in-loop, 2 = maxit finalised, 3 = breakdown
+  int conv_iter;  // iteration count at the latch
+  int converged;  // ||r|| < tol at the end
+  int breakdown;  // NaN/Inf seen
+  int pad_[3];
+};
+
+enum ReduceMode : int { kReduceInit = 0, kReduceA = 1, kReduceB = 2, kReduceFinal = 3, kReduceScalar = 4 };
+
+// Rows of a launch = up to two local row ranges [b0,e0) ∪ [b1,e1), cut in
+// tiles of kTileRows consecutive rows.
+constexpr int kTileRows = 256;
+struct TileRanges {
+  int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
+  int64_t nt0 = 0, ntiles = 0;
+};
+TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0);
+
+template <typename IdxT>
+struct CsrDev {
+  const IdxT* rowptr;
+  const int32_t* cols;
+  const double* vals;
+  int64_t n_rows;
+};
+
+// SELL-C-sigma (C = 64 = one wave, sigma = 1 i.e. no sorting) view: slice s
+// holds rows [64s, 64s+64), width w_s; entry j of row 64s+l is at
+// slice_ptr[s] + 64 j + l (column-major inside the slice -> every lane's load
+// of entry j is one coalesced 512-B wave access).  Padding entries have
+// val 0 and col = the row's own diagonal column.
+struct SellDev {
+  const int64_t* slice_ptr;  // n_slices + 1
+  const int32_t* cols;
+  const double* vals;
+  int64_t n_rows;
+};
+
+namespace kern {
+
+int num_cus();  // of the current device (cached)
+
+// ---- generation (csrc/gpu/gen.hip) ----
+void gen_rowlen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t* rowptr, hipStream_t st);
+void scan_inclusive_i64(int64_t* a, int64_t n, int64_t* tmp, hipStream_t st);  // tmp >= n/4096+1
+int64_t scan_tmp_elems(int64_t n);
+template <typename IdxT>
+void gen_fill(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
+              const int64_t* rowptr64, IdxT* rowptr_out, int32_t* cols, double* vals, hipStream_t st);
+void gen_rhs(const ProblemSpec& s, int64_t row_begin, int64_t n, double* b, hipStream_t st);
+// CSR -> SELL-64 (slice_ptr must be precomputed on the host/device from row lengths)
+void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr /* ns+1 */, hipStream_t st);
+template <typename IdxT>
+void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n,
+                 int64_t own_off, const int64_t* slice_ptr, int32_t* scols, double* svals,
+                 hipStream_t st);
+
+// ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
+template <typename IdxT>
+void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pold_ext,
+                   double* pnew_ext, double* x, double* Ap, int64_t own_off, const TileRanges& tr,
+                   double* partials, int grid, const CgState* st, double tol, int first,
+                   int final_mode, hipStream_t stream);
+// `slices`: TileRanges in units of 64-row slices
+void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pold_ext,
+                        double* pnew_ext, double* x, double* Ap, int64_t own_off,
+                        const TileRanges& slices, double* partials, int grid,
+                        const CgState* st, double tol, int first, int final_mode,
+                        hipStream_t stream);
+void cg_update_r(double* r_own, const double* Ap, int64_t n, double* partials, int grid,
+                 const CgState* st, hipStream_t stream);
+void cg_reduce(const double* partials, int np, CgState* st, int mode, int first, double tol,
+               hipStream_t stream);
+void dot_partials(const double* a, const double* b, int64_t n, double* partials, int grid,
+                  hipStream_t stream);
+// scalar[0] = fixed-order sum of partials
+void sum_partials(const double* partials, int np, double* out, hipStream_t stream);
+
+// ---- unfused ops (ops API / tests) ----
+template <typename IdxT>
+void spmv_csr(const CsrDev<IdxT>& A, const double* x, double* y, hipStream_t stream);
+void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream);
+void axpy(double alpha, const double* x, double* y, int64_t n, hipStream_t stream);  // y += a x
+void xpby(const double* x, double beta, double* y, int64_t n, hipStream_t stream);   // y = x + b y
+
+int grid_for(int64_t work_items, int block, int blocks_per_cu);
+
+}  // namespace kern
+}  // namespace mcg

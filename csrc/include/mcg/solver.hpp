@@ -1,0 +1,109 @@
+// Distributed GPU CG solver (one rank = one GPU).
+//
+// Per rank: the owned rows of A (CSR int32/int64 row pointers, or SELL-64),
+// generated on device; ext-layout r and p (double-buffered) vectors with ghost
+// regions; owned x / Ap / b; a device-resident CgState.  The iteration is a
+// fixed sequence of stream operations with zero host synchronisation:
+//
+//  compute stream S0                              comm stream S1
+//  ─────────────────                              ──────────────
+//  record E_r (r_k, p_{k-1} final) ─────────────► wait E_r; RCCL group{send/recv
+//  K_A interior rows (no ghosts needed)            r and p_{k-1} boundary rows};
+//  wait E_h ◄──────────────────────────────────── record E_h
+//  K_A boundary rows
+//  cg_reduce(A) ; ncclAllReduce(pAp)  (8 B)
+//  K_B (r -= alpha Ap, partial r.r)
+//  cg_reduce(B) ; ncclAllReduce(rr_new) (8 B)
+//
+// The host enqueues iterations (pairs are captured once into a hipGraph and
+// replayed), and polls the device convergence latch every `check_every`
+// iterations through a pinned buffer; iterations enqueued after the latch
+// fires are no-ops, so the iteration count is exactly the reference's.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <vector>
+
+#include "mcg/cg.hpp"
+#include "mcg/comm.hpp"
+#include "mcg/device.hpp"
+#include "mcg/kernels.hpp"
+#include "mcg/partition.hpp"
+
+namespace mcg {
+
+struct SolverInfo {
+  int64_t n_global = 0, n_local = 0, nnz_local = 0;
+  int64_t ext_len = 0, halo_in = 0, halo_out = 0;
+  int64_t interior_rows = 0;
+  bool idx64 = false;
+  int format = 0;
+  size_t device_bytes = 0;
+  double bytes_per_iter_model = 0;  // modelled HBM bytes per iteration (this rank)
+  int grid_a = 0, grid_b = 0;
+};
+
+class GpuCgSolver {
+ public:
+  // `comm` may be null for a single rank; it is not owned.
+  GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank = 0, int world = 1,
+              Comm* comm = nullptr);
+  ~GpuCgSolver();
+  GpuCgSolver(const GpuCgSolver&) = delete;
+  GpuCgSolver& operator=(const GpuCgSolver&) = delete;
+
+  void setup();                     // generate matrix + RHS on device (timed as setup)
+  void reset();                     // x = 0, r = b, p = 0, scalars; iteration counter = 0
+  CgResult solve();                 // reset + iterate to tol/maxit with polling + finalise
+  void run_iterations(int k);       // enqueue k more iterations (benchmark mode), no sync
+  void finalize();                  // enqueue the deferred last x update (if not latched)
+  void synchronize();
+  CgResult result();                // read the device state (syncs)
+  std::vector<double> x_local();    // owned part of x (syncs)
+  double true_residual_norm();      // ||b - A x||_2 over all ranks (syncs)
+
+  const SolverInfo& info() const { return info_; }
+  const LocalLayout& layout() const { return L_; }
+  hipStream_t stream() const { return s0_.get(); }
+  int iterations_enqueued() const { return k_; }
+
+ private:
+  template <typename IdxT> void build_csr_(DeviceBuffer<int64_t>& rp64);
+  void enqueue_iteration_(int k);
+  void enqueue_spmv_(int k, int which, int final_mode);  // which: 0 all, 1 interior, 2 boundary
+  void capture_pair_();
+
+  ProblemSpec spec_;
+  CgOptions opt_;
+  int rank_, world_;
+  Comm* comm_;
+  LocalLayout L_;
+  SolverInfo info_;
+  bool use_comm_ = false, use_halo_ = false;
+  bool setup_done_ = false;
+  int k_ = 0;  // host-side iteration counter (parity of the p double buffer)
+
+  Stream s0_, s1_;
+  Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2];
+  // matrix
+  DeviceBuffer<int32_t> rp32_;
+  DeviceBuffer<int64_t> rp64_;
+  DeviceBuffer<int32_t> cols_;
+  DeviceBuffer<double> vals_;
+  DeviceBuffer<int64_t> slice_ptr_;
+  // vectors
+  DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
+  DeviceBuffer<CgState> st_;
+  PinnedBuffer<CgState> host_st_;
+  // launch geometry
+  TileRanges tr_all_, tr_int_, tr_bnd_;
+  int g_all_ = 1, g_int_ = 1, g_bnd_ = 1, g_b_ = 1;
+  // graph of two iterations (even, odd)
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
+  double setup_seconds_ = 0.0;
+};
+
+}  // namespace mcg

@@ -1,0 +1,311 @@
+// Python bindings (pybind11) for the native mcg runtime:
+//   - problem specs, partition / halo plans, host CSR (CPU tests)
+//   - CPU reference CG (single process and P virtual ranks)
+//   - RCCL communicator + distributed GPU solver
+//   - raw-pointer kernel entry points used by cuda_mpi_parallel_amd.ops (the
+//     Python side passes torch tensors' data_ptr() and the current HIP stream)
+#include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+
+#include "mcg/cg.hpp"
+#include "mcg/check.hpp"
+#include "mcg/comm.hpp"
+#include "mcg/kernels.hpp"
+#include "mcg/partition.hpp"
+#include "mcg/solver.hpp"
+
+namespace py = pybind11;
+using namespace mcg;
+
+namespace {
+
+ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64_t band, double density,
+                      uint64_t seed, const std::string& rhs) {
+  ProblemSpec s;
+  s.kind = parse_problem_kind(problem);
+  s.N = n;
+  s.rows = rows;
+  s.band = band;
+  s.density = density;
+  s.seed = seed;
+  s.rhs = parse_rhs_kind(rhs);
+  if (s.kind == ProblemKind::Demo) s.N = 3;
+  return s;
+}
+
+CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool use_graph, bool force_comm,
+                    const std::string& format, int blocks_per_cu) {
+  CgOptions o;
+  o.maxit = maxit;
+  o.tol = tol;
+  o.check_every = check_every;
+  o.overlap = overlap;
+  o.use_graph = use_graph;
+  o.force_comm = force_comm;
+  if (format == "csr") o.format = 0;
+  else if (format == "sell" || format == "sell64") o.format = 1;
+  else fail("unknown format: " + format);
+  o.blocks_per_cu = blocks_per_cu;
+  return o;
+}
+
+py::dict result_dict(const CgResult& r) {
+  py::dict d;
+  d["iterations"] = r.iterations;
+  d["converged"] = r.converged;
+  d["breakdown"] = r.breakdown;
+  d["rnorm"] = r.rnorm;
+  d["setup_seconds"] = r.setup_seconds;
+  d["solve_seconds"] = r.solve_seconds;
+  d["iters_per_second"] = r.iters_per_second();
+  return d;
+}
+
+py::dict layout_dict(const LocalLayout& L) {
+  py::dict d;
+  d["rank"] = L.rank;
+  d["world"] = L.world;
+  d["n_global"] = L.n_global;
+  d["row_begin"] = L.row_begin;
+  d["row_end"] = L.row_end;
+  d["col_lo"] = L.col_lo;
+  d["col_hi"] = L.col_hi;
+  d["pad"] = L.pad;
+  d["ext_len"] = L.ext_len;
+  d["own_off"] = L.own_off;
+  d["interior_begin"] = L.interior_begin;
+  d["interior_end"] = L.interior_end;
+  py::list sends, recvs;
+  for (auto& h : L.sends) sends.append(py::make_tuple(h.peer, h.gbegin, h.count));
+  for (auto& h : L.recvs) recvs.append(py::make_tuple(h.peer, h.gbegin, h.count));
+  d["sends"] = sends;
+  d["recvs"] = recvs;
+  return d;
+}
+
+template <typename T>
+py::array_t<T> to_numpy(std::vector<T>&& v) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::vector<T>*>(p); });
+  return py::array_t<T>(heap->size(), heap->data(), owner);
+}
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mcg: MI355X-native distributed conjugate-gradient runtime (HIP + RCCL)";
+
+  py::register_exception<Error>(m, "MCGError");
+
+  py::class_<ProblemSpec>(m, "ProblemSpec")
+      .def(py::init(&make_spec), py::arg("problem") = "demo", py::arg("n") = 3, py::arg("rows") = 0,
+           py::arg("band") = 0, py::arg("density") = 0.5, py::arg("seed") = 1234, py::arg("rhs") = "reference")
+      .def_property_readonly("name", [](const ProblemSpec& s) { return problem_name(s); })
+      .def_property_readonly("n_rows", [](const ProblemSpec& s) { return global_rows(s); })
+      .def_property_readonly("bandwidth", [](const ProblemSpec& s) { return bandwidth(s); })
+      .def_property_readonly("closed_form_nnz", [](const ProblemSpec& s) { return closed_form_nnz(s); })
+      .def_readonly("N", &ProblemSpec::N)
+      .def_readonly("rows", &ProblemSpec::rows)
+      .def_readonly("band", &ProblemSpec::band)
+      .def_readonly("density", &ProblemSpec::density)
+      .def_readonly("seed", &ProblemSpec::seed)
+      .def("row_length", [](const ProblemSpec& s, int64_t i) { return row_length(s, i); })
+      .def("rhs_value", [](const ProblemSpec& s, int64_t i) { return rhs_value(s, i); })
+      .def("row", [](const ProblemSpec& s, int64_t i) {
+        py::list cols, vals;
+        for_each_entry(s, i, [&](int64_t c, double v) { cols.append(c); vals.append(v); });
+        return py::make_tuple(cols, vals);
+      });
+
+  py::class_<CgOptions>(m, "CgOptions")
+      .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
+           py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
+           py::arg("format") = "csr", py::arg("blocks_per_cu") = 8)
+      .def_readwrite("maxit", &CgOptions::maxit)
+      .def_readwrite("tol", &CgOptions::tol)
+      .def_readwrite("check_every", &CgOptions::check_every)
+      .def_readwrite("overlap", &CgOptions::overlap)
+      .def_readwrite("use_graph", &CgOptions::use_graph)
+      .def_readwrite("force_comm", &CgOptions::force_comm)
+      .def_readwrite("format", &CgOptions::format)
+      .def_readwrite("blocks_per_cu", &CgOptions::blocks_per_cu);
+
+  // ---- partition / halo plan / host CSR ----
+  m.def("partition_rows", [](const ProblemSpec& s, int world) { return partition_rows(s, world).offsets; });
+  m.def("partition_by_weight", [](const std::vector<int64_t>& prefix, int world) {
+    return partition_by_weight(prefix, world).offsets;
+  });
+  m.def("make_layout", [](const ProblemSpec& s, int world, int rank) {
+    return layout_dict(make_layout(s, partition_rows(s, world), rank));
+  });
+  m.def("host_csr", [](const ProblemSpec& s, int world, int rank) {
+    LocalLayout L = make_layout(s, partition_rows(s, world), rank);
+    HostCsr A = build_local_csr(s, L);
+    return py::make_tuple(to_numpy(std::move(A.rowptr)), to_numpy(std::move(A.cols)), to_numpy(std::move(A.vals)));
+  }, py::arg("spec"), py::arg("world") = 1, py::arg("rank") = 0);
+  m.def("host_rhs", [](const ProblemSpec& s, int64_t r0, int64_t r1) { return to_numpy(build_rhs(s, r0, r1)); });
+
+  // ---- CPU reference path ----
+  m.def("cpu_cg", [](const ProblemSpec& s, const CgOptions& o) {
+    std::vector<double> x, hist;
+    CgResult r;
+    {
+      py::gil_scoped_release rel;
+      r = cpu_cg(s, o, &x, &hist);
+    }
+    py::dict d = result_dict(r);
+    d["x"] = to_numpy(std::move(x));
+    d["rnorm_history"] = to_numpy(std::move(hist));
+    return d;
+  });
+  m.def("cpu_cg_partitioned", [](const ProblemSpec& s, int world, const CgOptions& o) {
+    std::vector<double> x, hist;
+    CgResult r;
+    {
+      py::gil_scoped_release rel;
+      r = cpu_cg_partitioned(s, world, o, &x, &hist);
+    }
+    py::dict d = result_dict(r);
+    d["x"] = to_numpy(std::move(x));
+    d["rnorm_history"] = to_numpy(std::move(hist));
+    return d;
+  });
+
+  // ---- device / RCCL ----
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    (void)hipGetLastError();
+    return n;
+  });
+  m.def("unique_id", []() { return py::bytes(unique_id_bytes()); });
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def(py::init([](int rank, int world, py::bytes id_red, py::bytes id_halo) {
+             std::string a = id_red, b = id_halo;
+             py::gil_scoped_release rel;
+             return std::make_shared<Comm>(rank, world, unique_id_from_bytes(a), unique_id_from_bytes(b));
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("reduce_id"), py::arg("halo_id"))
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def("allreduce_sum_ptr", [](Comm& c, uintptr_t buf, size_t count, uintptr_t stream) {
+        c.allreduce_sum(reinterpret_cast<double*>(buf), count, as_stream(stream));
+      })
+      .def("check_async", &Comm::check_async)
+      .def("abort", &Comm::abort);
+
+  py::class_<GpuCgSolver>(m, "Solver")
+      .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<Comm> comm) {
+             return new GpuCgSolver(s, o, rank, world, comm.get());
+           }),
+           py::arg("spec"), py::arg("opts"), py::arg("rank") = 0, py::arg("world") = 1,
+           py::arg("comm") = nullptr, py::keep_alive<1, 6>())
+      .def("setup", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.setup(); })
+      .def("reset", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.reset(); })
+      .def("solve", [](GpuCgSolver& g) {
+        CgResult r;
+        {
+          py::gil_scoped_release rel;
+          r = g.solve();
+        }
+        return result_dict(r);
+      })
+      .def("run_iterations", [](GpuCgSolver& g, int k) { py::gil_scoped_release rel; g.run_iterations(k); })
+      .def("finalize", &GpuCgSolver::finalize)
+      .def("synchronize", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.synchronize(); })
+      .def("result", [](GpuCgSolver& g) { return result_dict(g.result()); })
+      .def("x_local", [](GpuCgSolver& g) { return to_numpy(g.x_local()); })
+      .def("true_residual_norm", [](GpuCgSolver& g) { py::gil_scoped_release rel; return g.true_residual_norm(); })
+      .def_property_readonly("iterations_enqueued", &GpuCgSolver::iterations_enqueued)
+      .def_property_readonly("stream", [](GpuCgSolver& g) { return reinterpret_cast<uintptr_t>(g.stream()); })
+      .def_property_readonly("layout", [](GpuCgSolver& g) { return layout_dict(g.layout()); })
+      .def_property_readonly("info", [](GpuCgSolver& g) {
+        const SolverInfo& i = g.info();
+        py::dict d;
+        d["n_global"] = i.n_global;
+        d["n_local"] = i.n_local;
+        d["nnz_local"] = i.nnz_local;
+        d["ext_len"] = i.ext_len;
+        d["halo_in"] = i.halo_in;
+        d["halo_out"] = i.halo_out;
+        d["interior_rows"] = i.interior_rows;
+        d["idx64"] = i.idx64;
+        d["format"] = i.format == 1 ? "sell64" : "csr";
+        d["device_bytes"] = i.device_bytes;
+        d["bytes_per_iter_model"] = i.bytes_per_iter_model;
+        d["grid_a"] = i.grid_a;
+        d["grid_b"] = i.grid_b;
+        return d;
+      });
+
+  // ---- raw-pointer kernel entry points (ops API) ----
+  py::module_ k = m.def_submodule("kernels", "hand-written gfx950 kernels on raw device pointers");
+  k.def("spmv_csr", [](uintptr_t rowptr, bool idx64, uintptr_t cols, uintptr_t vals, int64_t n_rows, uintptr_t x,
+                       uintptr_t y, uintptr_t stream) {
+    if (idx64)
+      kern::spmv_csr<int64_t>(CsrDev<int64_t>{reinterpret_cast<const int64_t*>(rowptr),
+                                              reinterpret_cast<const int32_t*>(cols),
+                                              reinterpret_cast<const double*>(vals), n_rows},
+                              reinterpret_cast<const double*>(x), reinterpret_cast<double*>(y), as_stream(stream));
+    else
+      kern::spmv_csr<int32_t>(CsrDev<int32_t>{reinterpret_cast<const int32_t*>(rowptr),
+                                              reinterpret_cast<const int32_t*>(cols),
+                                              reinterpret_cast<const double*>(vals), n_rows},
+                              reinterpret_cast<const double*>(x), reinterpret_cast<double*>(y), as_stream(stream));
+  });
+  k.def("spmv_sell", [](uintptr_t slice_ptr, uintptr_t cols, uintptr_t vals, int64_t n_rows, uintptr_t x,
+                        uintptr_t y, uintptr_t stream) {
+    kern::spmv_sell(SellDev{reinterpret_cast<const int64_t*>(slice_ptr), reinterpret_cast<const int32_t*>(cols),
+                            reinterpret_cast<const double*>(vals), n_rows},
+                    reinterpret_cast<const double*>(x), reinterpret_cast<double*>(y), as_stream(stream));
+  });
+  k.def("csr_to_sell", [](uintptr_t rowptr64, uintptr_t cols, uintptr_t vals, int64_t n, uintptr_t slice_ptr,
+                          uintptr_t scols, uintptr_t svals, uintptr_t stream) {
+    kern::csr_to_sell<int64_t>(reinterpret_cast<const int64_t*>(rowptr64), reinterpret_cast<const int32_t*>(cols),
+                               reinterpret_cast<const double*>(vals), n, 0,
+                               reinterpret_cast<const int64_t*>(slice_ptr), reinterpret_cast<int32_t*>(scols),
+                               reinterpret_cast<double*>(svals), as_stream(stream));
+  });
+  k.def("dot_partials", [](uintptr_t a, uintptr_t b, int64_t n, uintptr_t partials, int grid, uintptr_t stream) {
+    kern::dot_partials(reinterpret_cast<const double*>(a), reinterpret_cast<const double*>(b), n,
+                       reinterpret_cast<double*>(partials), grid, as_stream(stream));
+  });
+  k.def("sum_partials", [](uintptr_t partials, int np, uintptr_t out, uintptr_t stream) {
+    kern::sum_partials(reinterpret_cast<const double*>(partials), np, reinterpret_cast<double*>(out),
+                       as_stream(stream));
+  });
+  k.def("axpy", [](double a, uintptr_t x, uintptr_t y, int64_t n, uintptr_t stream) {
+    kern::axpy(a, reinterpret_cast<const double*>(x), reinterpret_cast<double*>(y), n, as_stream(stream));
+  });
+  k.def("xpby", [](uintptr_t x, double b, uintptr_t y, int64_t n, uintptr_t stream) {
+    kern::xpby(reinterpret_cast<const double*>(x), b, reinterpret_cast<double*>(y), n, as_stream(stream));
+  });
+  k.def("gen_rowlen", [](const ProblemSpec& s, int64_t row_begin, int64_t n, uintptr_t rowptr, uintptr_t stream) {
+    kern::gen_rowlen(s, row_begin, n, reinterpret_cast<int64_t*>(rowptr), as_stream(stream));
+  });
+  k.def("scan_inclusive_i64", [](uintptr_t a, int64_t n, uintptr_t tmp, uintptr_t stream) {
+    kern::scan_inclusive_i64(reinterpret_cast<int64_t*>(a), n, reinterpret_cast<int64_t*>(tmp), as_stream(stream));
+  });
+  k.def("scan_tmp_elems", &kern::scan_tmp_elems);
+  k.def("gen_fill", [](const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
+                       uintptr_t rp64, uintptr_t cols, uintptr_t vals, uintptr_t stream) {
+    kern::gen_fill<int64_t>(s, row_begin, n, col_lo, pad, reinterpret_cast<const int64_t*>(rp64), nullptr,
+                            reinterpret_cast<int32_t*>(cols), reinterpret_cast<double*>(vals), as_stream(stream));
+  });
+  k.def("gen_rhs", [](const ProblemSpec& s, int64_t row_begin, int64_t n, uintptr_t b, uintptr_t stream) {
+    kern::gen_rhs(s, row_begin, n, reinterpret_cast<double*>(b), as_stream(stream));
+  });
+  k.def("sell_slice_widths", [](uintptr_t rp64, int64_t n, uintptr_t sp, uintptr_t stream) {
+    kern::sell_slice_widths(reinterpret_cast<const int64_t*>(rp64), n, reinterpret_cast<int64_t*>(sp),
+                            as_stream(stream));
+  });
+  k.def("grid_for", &kern::grid_for);
+  k.attr("TILE_ROWS") = kTileRows;
+}

@@ -1,0 +1,69 @@
+"""Process-group bootstrap: one process per GPU under torchrun, RCCL for the solver.
+
+``torch.distributed`` (gloo, host side) is used only for rendezvous, barriers and
+shipping the two ``ncclUniqueId``s; the solver's own collectives are native RCCL
+calls issued from C++ on the solver's HIP streams (``csrc/gpu/comm.cpp``), so no
+Python is on the per-iteration path.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from .. import native
+
+
+@dataclass(frozen=True)
+class DistEnv:
+    rank: int
+    world: int
+    local_rank: int
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world > 1
+
+
+def dist_env() -> DistEnv:
+    """RANK / WORLD_SIZE / LOCAL_RANK from the torchrun environment (defaults: single rank)."""
+    return DistEnv(
+        rank=int(os.environ.get("RANK", "0")),
+        world=int(os.environ.get("WORLD_SIZE", "1")),
+        local_rank=int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))),
+    )
+
+
+def init_process_group(env: DistEnv, backend: str = "gloo") -> None:
+    """Initialise torch.distributed if running multi-rank (MASTER_ADDR/PORT from torchrun)."""
+    if env.world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, rank=env.rank, world_size=env.world)
+
+
+def bootstrap_comm(env: DistEnv, force: bool = False):
+    """Create the native RCCL communicator pair for this rank (None for a single rank
+    unless ``force``).  Rank 0 draws the unique ids and broadcasts them over the
+    torch.distributed store-backed process group."""
+    if env.world == 1 and not force:
+        return None
+    C = native()
+    if env.world == 1:
+        return C.Comm(0, 1, C.unique_id(), C.unique_id())
+    if not dist.is_initialized():
+        raise RuntimeError("bootstrap_comm needs torch.distributed initialised (call init_process_group)")
+    ids = [C.unique_id(), C.unique_id()] if env.rank == 0 else [None, None]
+    dist.broadcast_object_list(ids, src=0)
+    return C.Comm(env.rank, env.world, ids[0], ids[1])
+
+
+def set_device(env: DistEnv) -> int:
+    """Bind this process to its GPU (LOCAL_RANK) — like the reference's cudaSetDevice(0)."""
+    n = torch.cuda.device_count()
+    if n == 0:
+        raise RuntimeError("Device Set failed: no HIP device visible")
+    dev = env.local_rank % n
+    torch.cuda.set_device(dev)
+    return dev

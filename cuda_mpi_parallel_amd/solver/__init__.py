@@ -1,0 +1,99 @@
+"""High-level CG drivers.
+
+``CGSolver`` wraps the native distributed GPU solver (``csrc/gpu/solver.cpp``):
+on-device generation of this rank's rows, fused HIP kernels, device-resident
+scalars, RCCL all-reduce + halo on side streams, hipGraph-captured iteration
+pairs.  ``device="cpu"`` runs the CPU reference path instead (single process,
+``sim_ranks`` virtual ranks, or — under torch.distributed/gloo — one process
+per rank).
+
+Semantics follow the reference (CUDACG.cu:235-352): x0 = 0, r0 = p0 = b,
+stop when ||r||_2 < tol (absolute) after the x/r update, at most ``maxit``
+iterations, no abort on non-positive curvature.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+
+from .. import native
+from ..models import ProblemSpec, make_problem
+from ..parallel import dist as _dist
+
+
+def _opts(maxit=2000, tol=1e-7, check_every=32, overlap=True, use_graph=True, force_comm=False,
+          format="csr", blocks_per_cu=8):
+    return native().CgOptions(maxit, tol, check_every, overlap, use_graph, force_comm, format, blocks_per_cu)
+
+
+class CGSolver:
+    """Distributed GPU CG for one rank (one process per GPU, or a single GPU)."""
+
+    def __init__(self, spec: ProblemSpec, maxit: int = 2000, tol: float = 1e-7, check_every: int = 32,
+                 overlap: bool = True, use_graph: bool = True, format: str = "csr", force_comm: bool = False,
+                 blocks_per_cu: int = 8, env: Optional[_dist.DistEnv] = None, comm=None):
+        self.spec = spec
+        self.env = env or _dist.dist_env()
+        _dist.set_device(self.env)
+        if comm is None and (self.env.world > 1 or force_comm):
+            _dist.init_process_group(self.env)
+            comm = _dist.bootstrap_comm(self.env, force=force_comm)
+        self.comm = comm
+        self.opts = _opts(maxit, tol, check_every, overlap, use_graph, force_comm, format, blocks_per_cu)
+        self._s = native().Solver(spec.native(), self.opts, self.env.rank, self.env.world, comm)
+        self._s.setup()
+
+    # --- solve to tolerance (reference semantics) ---
+    def solve(self) -> Dict:
+        res = self._s.solve()
+        res["x_local"] = self._s.x_local()
+        res["row_begin"] = self._s.layout["row_begin"]
+        return res
+
+    # --- fixed-work benchmark mode ---
+    def reset(self) -> None:
+        self._s.reset()
+
+    def run(self, iterations: int) -> None:
+        """Enqueue `iterations` more CG iterations (asynchronous)."""
+        self._s.run_iterations(int(iterations))
+
+    def synchronize(self) -> None:
+        self._s.synchronize()
+
+    def finalize(self) -> None:
+        self._s.finalize()
+
+    def result(self) -> Dict:
+        return self._s.result()
+
+    def x_local(self) -> np.ndarray:
+        return self._s.x_local()
+
+    def true_residual_norm(self) -> float:
+        return self._s.true_residual_norm()
+
+    @property
+    def info(self) -> Dict:
+        return self._s.info
+
+    @property
+    def layout(self) -> Dict:
+        return self._s.layout
+
+
+def solve(problem: str = "demo", device: str = "gpu", sim_ranks: int = 1, maxit: int = 2000, tol: float = 1e-7,
+          **kw) -> Dict:
+    """One-call solve.  ``solve()`` with no arguments is the reference's demo."""
+    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs") if k in kw}
+    spec = make_problem(problem, **spec_kw)
+    if device == "cpu":
+        o = _opts(maxit, tol)
+        C = native()
+        return C.cpu_cg_partitioned(spec.native(), sim_ranks, o) if sim_ranks > 1 else C.cpu_cg(spec.native(), o)
+    s = CGSolver(spec, maxit=maxit, tol=tol, **kw)
+    return s.solve()
+
+
+__all__ = ["CGSolver", "solve"]

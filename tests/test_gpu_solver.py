@@ -1,0 +1,66 @@
+"""GPU solver end-to-end: reference golden output, agreement with the CPU reference path."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_demo_golden(mcg):
+    out = mcg.solve("demo")
+    assert "".join("%f\n" % v for v in out["x_local"]) == "0.500000\n0.750000\n1.000000\n"
+    assert out["iterations"] == 3 and out["converged"]
+    assert out["rnorm"] < 1e-7
+
+
+def test_cli_no_args_golden(mcg):
+    p = subprocess.run([mcg.cli_path()], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout == "0.500000\n0.750000\n1.000000\nSuccess\n"
+
+
+@pytest.mark.parametrize("fmt", ["csr", "sell"])
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20)),
+                                         ("randspd", dict(rows=20000, band=40, density=0.25))])
+def test_matches_cpu_reference(mcg, fmt, graph, problem, kw):
+    spec = mcg.make_problem(problem, **kw)
+    cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions(maxit=2000, tol=1e-7))
+    s = mcg.CGSolver(spec, format=fmt, use_graph=graph, check_every=8)
+    out = s.solve()
+    # same recurrence, different summation order: iteration counts may differ by a step or two
+    assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    assert out["converged"] == cpu["converged"]
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    tr = s.true_residual_norm()
+    assert tr < 1e-6
+
+
+def test_fixed_iterations_counter(mcg):
+    spec = mcg.make_problem("poisson2d", n=512)
+    s = mcg.CGSolver(spec, tol=-1.0, maxit=1 << 30)
+    s.reset()
+    s.run(7)
+    s.run(10)
+    s.synchronize()
+    r = s.result()
+    assert r["iterations"] == 17 and not r["converged"] and np.isfinite(r["rnorm"])
+
+
+def test_maxit_exhaustion_matches_cpu(mcg):
+    spec = mcg.make_problem("poisson2d", n=200)
+    cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions(maxit=50, tol=1e-7))
+    out = mcg.CGSolver(spec, maxit=50).solve()
+    assert out["iterations"] == 50 and not out["converged"]
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-9, atol=1e-12)
+    assert abs(out["rnorm"] - cpu["rnorm"]) <= 1e-8 * cpu["rnorm"]
+
+
+def test_force_comm_single_rank(mcg):
+    """The RCCL code path with one rank (all-reduce degenerates, no halo)."""
+    spec = mcg.make_problem("poisson2d", n=64)
+    out = mcg.CGSolver(spec, force_comm=True).solve()
+    cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions())
+    assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 2
