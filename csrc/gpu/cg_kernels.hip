@@ -28,12 +28,12 @@
 
 namespace mcg {
 
-TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1, int64_t e1) {
+TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1, int64_t e1, int64_t tile) {
   TileRanges t;
   t.b0 = b0; t.e0 = e0 > b0 ? e0 : b0;
   t.b1 = b1; t.e1 = e1 > b1 ? e1 : b1;
-  t.nt0 = (t.e0 - t.b0 + kTileRows - 1) / kTileRows;
-  t.ntiles = t.nt0 + (t.e1 - t.b1 + kTileRows - 1) / kTileRows;
+  t.nt0 = (t.e0 - t.b0 + tile - 1) / tile;
+  t.ntiles = t.nt0 + (t.e1 - t.b1 + tile - 1) / tile;
   return t;
 }
 
@@ -93,7 +93,8 @@ __device__ __forceinline__ void csr_tiles(const CsrDev<IdxT>& A, const TileRange
     int64_t r0, r1;
     tile_rows(tr, tile, r0, r1);
     const int nr = (int)(r1 - r0);
-    if (t <= nr) s_rp[t] = (int64_t)A.rowptr[r0 + t];
+    if (t < nr) s_rp[t] = (int64_t)A.rowptr[r0 + t];
+    if (t == 0) s_rp[nr] = (int64_t)A.rowptr[r0 + nr];
     __syncthreads();
     const int64_t rs = s_rp[0], re = s_rp[nr];
     int64_t my_b = 0, my_e = 0;

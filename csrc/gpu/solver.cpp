@@ -132,7 +132,7 @@ void GpuCgSolver::setup() {
   };
   auto ranges = [&](int64_t b0, int64_t e0, int64_t b1, int64_t e1) {
     if (opt_.format == 1) {  // slice units; rows [b,e) -> whole slices
-      return make_tiles(b0 / 64, (e0 + 63) / 64, b1 / 64, (e1 + 63) / 64);
+      return make_tiles(b0 / 64, (e0 + 63) / 64, b1 / 64, (e1 + 63) / 64, 1);
     }
     return make_tiles(b0, e0, b1, e1);
   };
@@ -143,11 +143,11 @@ void GpuCgSolver::setup() {
     if (opt_.format == 1) {  // interior launch takes only whole slices inside the interior
       const int64_t sb = (ib + 63) / 64, se = ie / 64;
       if (se > sb) {
-        tr_int_ = make_tiles(sb, se);
-        tr_bnd_ = make_tiles(0, sb, se, (n + 63) / 64);
+        tr_int_ = make_tiles(sb, se, 0, 0, 1);
+        tr_bnd_ = make_tiles(0, sb, se, (n + 63) / 64, 1);
       } else {
-        tr_int_ = make_tiles(0, 0);
-        tr_bnd_ = make_tiles(0, (n + 63) / 64);
+        tr_int_ = make_tiles(0, 0, 0, 0, 1);
+        tr_bnd_ = make_tiles(0, (n + 63) / 64, 0, 0, 1);
       }
     } else {
       tr_int_ = make_tiles(ib, ie);

@@ -48,7 +48,8 @@ struct TileRanges {
   int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
   int64_t nt0 = 0, ntiles = 0;
 };
-TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0);
+// `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
+TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);
 
 template <typename IdxT>
 struct CsrDev {
