@@ -11,6 +11,7 @@
 //   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
 //   --maxit M  --tol T  --check-every K  --fixed-iters K  --warmup W
 //   --format csr|sell  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
+//   --spmv-variant 0|1|2  --spmv-param U|G  --update-unroll 1|2|4
 //   --print-x auto|yes|no  --report text|json  --verify
 // Multi-GPU runs use one host thread per GPU inside this process (no MPI in
 // this image); the two RCCL unique ids are shared in memory.
@@ -81,6 +82,9 @@ Args parse(int argc, char** argv) {
     else if (f == "--no-graph") a.opt.use_graph = false;
     else if (f == "--force-comm") a.opt.force_comm = true;
     else if (f == "--blocks-per-cu") a.opt.blocks_per_cu = std::stoi(need(i));
+    else if (f == "--spmv-variant") a.opt.spmv_variant = std::stoi(need(i));
+    else if (f == "--spmv-param") a.opt.spmv_param = std::stoi(need(i));
+    else if (f == "--update-unroll") a.opt.update_unroll = std::stoi(need(i));
     else if (f == "--print-x") a.print_x = need(i);
     else if (f == "--report") a.report = need(i);
     else if (f == "--verify") a.verify = true;

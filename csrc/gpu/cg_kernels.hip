@@ -25,6 +25,7 @@
 
 #include "mcg/check.hpp"
 #include "mcg/kernels.hpp"
+#include "spmv_engines.hpp"
 
 namespace mcg {
 
@@ -40,89 +41,43 @@ TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1, int64_t e1, int64_t ti
 namespace kern {
 namespace {
 
-constexpr int kBS = 256;             // threads per block = rows per CSR tile
-constexpr int kWaves = kBS / 64;
-constexpr int kCap = 2048;           // nnz staged in LDS per chunk (16 KB vals + 8 KB cols)
+using eng::kBS;
+using eng::kWaves;
+using eng::block_partial;
+using eng::tile_rows;
+using eng::wave_sum;
 constexpr int kReduceBS = 1024;
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  return v;
+__device__ __forceinline__ TileRanges make_tiles_dev(int64_t n_units) {
+  TileRanges t;
+  t.b0 = 0;
+  t.e0 = n_units;
+  t.nt0 = n_units;
+  t.ntiles = n_units;
+  return t;
 }
 
-// fixed-order block reduction -> *out (thread 0)
-template <int BS>
-__device__ __forceinline__ void block_partial(double v, double* sh, double* out) {
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < BS / 64; ++w) s += sh[w];
-    *out = s;
-  }
-}
+struct Scalars {
+  double alpha, beta;
+  bool conv;
+};
 
-__device__ __forceinline__ void tile_rows(const TileRanges& tr, int64_t t, int64_t& r0, int64_t& r1) {
-  if (t < tr.nt0) {
-    r0 = tr.b0 + t * kTileRows;
-    r1 = r0 + kTileRows < tr.e0 ? r0 + kTileRows : tr.e0;
-  } else {
-    t -= tr.nt0;
-    r0 = tr.b1 + t * kTileRows;
-    r1 = r0 + kTileRows < tr.e1 ? r0 + kTileRows : tr.e1;
-  }
-}
-
-// CSR row-tile engine: a 256-row tile's rowptr slice, then its contiguous
-// nnz range in chunks of kCap, are staged through LDS with 16-B-per-lane loads
-// (coalesced 1 KiB wave accesses); each thread then walks its own row out of
-// LDS (stride-5 doubles / ints across lanes: conflict-free for ds_read_b64 and
-// ds_read_b32) and gathers x through L2/MALL.  Rows longer than kCap simply
-// span several chunks.
-template <typename IdxT, class Gather, class Epi>
-__device__ __forceinline__ void csr_tiles(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather,
-                                          Epi&& epi) {
-  __shared__ __attribute__((aligned(16))) double s_v[kCap + 2];
-  __shared__ __attribute__((aligned(16))) int32_t s_c[kCap + 4];
-  __shared__ int64_t s_rp[kBS + 1];
-  const int t = threadIdx.x;
-  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
-    int64_t r0, r1;
-    tile_rows(tr, tile, r0, r1);
-    const int nr = (int)(r1 - r0);
-    if (t < nr) s_rp[t] = (int64_t)A.rowptr[r0 + t];
-    if (t == 0) s_rp[nr] = (int64_t)A.rowptr[r0 + nr];
-    __syncthreads();
-    const int64_t rs = s_rp[0], re = s_rp[nr];
-    int64_t my_b = 0, my_e = 0;
-    if (t < nr) {
-      my_b = s_rp[t];
-      my_e = s_rp[t + 1];
-    }
-    double sum = 0.0;
-    for (int64_t cs = rs; cs < re; cs += kCap) {
-      const int64_t ce = re < cs + kCap ? re : cs + kCap;
-      const int64_t vb = cs & ~(int64_t)1, cb = cs & ~(int64_t)3;
-      const int nv2 = (int)((ce - vb + 1) >> 1), nc4 = (int)((ce - cb + 3) >> 2);
-      const double2* gv = reinterpret_cast<const double2*>(A.vals + vb);
-      const int4* gc = reinterpret_cast<const int4*>(A.cols + cb);
-      for (int c = t; c < nv2; c += kBS) reinterpret_cast<double2*>(s_v)[c] = gv[c];
-      for (int c = t; c < nc4; c += kBS) reinterpret_cast<int4*>(s_c)[c] = gc[c];
-      __syncthreads();
-      const int64_t jb = my_b > cs ? my_b : cs, je = my_e < ce ? my_e : ce;
-      for (int64_t j = jb; j < je; ++j) sum = fma(s_v[j - vb], gather(s_c[j - cb]), sum);
-      __syncthreads();
-    }
-    if (t < nr) epi(r0 + t, sum);
-  }
+// alpha_{k-1}, beta_{k-1} and the convergence decision, recomputed by every
+// thread from the device-resident state (identical inputs -> identical values)
+__device__ __forceinline__ Scalars load_scalars(const CgState* __restrict__ st, double tol, int first,
+                                                int final_mode) {
+  const double rr = st->rr_new, rho = st->rho, pAp = st->pAp;
+  Scalars s;
+  s.conv = final_mode || (!first && sqrt(rr) < tol);
+  s.alpha = first ? 0.0 : rho / pAp;
+  s.beta = first ? 0.0 : rr / rho;
+  return s;
 }
 
 // ---------------------------------------------------------------------------
-// K_A: fused SpMV (CSR)
-template <typename IdxT>
+// K_A: fused SpMV (CSR).  ENG: 0 = LDS-staged tiles, 1 = direct, 2 = CSR-vector.
+// P = batch size U (ENG 0/1) or lanes per row G (ENG 2).
+template <int ENG, typename IdxT, int P>
 __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const double* __restrict__ r,
                                                        const double* __restrict__ pold,
                                                        double* __restrict__ pnew, double* __restrict__ x,
@@ -132,11 +87,9 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
                                                        int final_mode) {
   __shared__ double s_red[kWaves];
   if (st->done) return;
-  const double rr = st->rr_new, rho = st->rho, pAp = st->pAp;
-  const bool conv = final_mode || (!first && sqrt(rr) < tol);
-  const double alpha = first ? 0.0 : rho / pAp;
-  const double beta = first ? 0.0 : rr / rho;
-  if (conv) {
+  const Scalars sc = load_scalars(st, tol, first, final_mode);
+  const double alpha = sc.alpha, beta = sc.beta;
+  if (sc.conv) {
     // the loop exits (CUDACG.cu:333): only the deferred x += alpha_{k-1} p_{k-1}
     for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
       int64_t r0, r1;
@@ -147,8 +100,47 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
     return;
   }
   double acc = 0.0;
-  csr_tiles(
-      A, tr, [&](int32_t c) { return fma(beta, pold[c], r[c]); },
+  auto gather = [&](int32_t c) { return fma(beta, pold[c], r[c]); };
+  auto epi = [&](int64_t i, double sum) {
+    const double po = pold[own + i];
+    const double pi = fma(beta, po, r[own + i]);
+    pnew[own + i] = pi;
+    Ap[i] = sum;
+    x[i] = fma(alpha, po, x[i]);
+    acc = fma(pi, sum, acc);
+  };
+  if constexpr (ENG == 0) eng::csr_lds<IdxT, P>(A, tr, gather, epi);
+  else if constexpr (ENG == 1) eng::csr_direct<IdxT, P>(A, tr, gather, epi);
+  else eng::csr_vector<IdxT, P>(A, tr, gather, epi);
+  block_partial<kBS>(acc, s_red, partials + blockIdx.x);
+}
+
+// K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries)
+template <int U>
+__global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const double* __restrict__ r,
+                                                            const double* __restrict__ pold,
+                                                            double* __restrict__ pnew, double* __restrict__ x,
+                                                            double* __restrict__ Ap, int64_t own, TileRanges sr,
+                                                            double* __restrict__ partials,
+                                                            const CgState* __restrict__ st, double tol,
+                                                            int first, int final_mode) {
+  __shared__ double s_red[kWaves];
+  if (st->done) return;
+  const Scalars sc = load_scalars(st, tol, first, final_mode);
+  const double alpha = sc.alpha, beta = sc.beta;
+  if (sc.conv) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = blockIdx.x * kWaves + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * kWaves;
+    for (int64_t t = wid; t < sr.ntiles; t += nw) {
+      const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
+      const int64_t i = sl * 64 + lane;
+      if (i < A.n_rows) x[i] = fma(alpha, pold[own + i], x[i]);
+    }
+    return;
+  }
+  double acc = 0.0;
+  eng::sell<U>(
+      A, sr, [&](int32_t c) { return fma(beta, pold[c], r[c]); },
       [&](int64_t i, double sum) {
         const double po = pold[own + i];
         const double pi = fma(beta, po, r[own + i]);
@@ -160,55 +152,8 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
   block_partial<kBS>(acc, s_red, partials + blockIdx.x);
 }
 
-// K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries)
-__global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const double* __restrict__ r,
-                                                            const double* __restrict__ pold,
-                                                            double* __restrict__ pnew, double* __restrict__ x,
-                                                            double* __restrict__ Ap, int64_t own, TileRanges sr,
-                                                            double* __restrict__ partials,
-                                                            const CgState* __restrict__ st, double tol,
-                                                            int first, int final_mode) {
-  __shared__ double s_red[kWaves];
-  if (st->done) return;
-  const double rr = st->rr_new, rho = st->rho, pAp = st->pAp;
-  const bool conv = final_mode || (!first && sqrt(rr) < tol);
-  const double alpha = first ? 0.0 : rho / pAp;
-  const double beta = first ? 0.0 : rr / rho;
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
-  double acc = 0.0;
-  for (int64_t t = wid; t < sr.ntiles; t += nw) {
-    const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
-    const int64_t i = sl * 64 + lane;
-    if (conv) {
-      if (i < A.n_rows) x[i] = fma(alpha, pold[own + i], x[i]);
-      continue;
-    }
-    const int64_t base = A.slice_ptr[sl];
-    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
-    const int32_t* __restrict__ cp = A.cols + base + lane;
-    const double* __restrict__ vp = A.vals + base + lane;
-    double sum = 0.0;
-#pragma unroll 8
-    for (int j = 0; j < w; ++j) {
-      const int32_t c = cp[64 * j];
-      sum = fma(vp[64 * j], fma(beta, pold[c], r[c]), sum);
-    }
-    if (i < A.n_rows) {
-      const double po = pold[own + i];
-      const double pi = fma(beta, po, r[own + i]);
-      pnew[own + i] = pi;
-      Ap[i] = sum;
-      x[i] = fma(alpha, po, x[i]);
-      acc = fma(pi, sum, acc);
-    }
-  }
-  if (conv) return;
-  block_partial<kBS>(acc, s_red, partials + blockIdx.x);
-}
-
-// K_B: r -= alpha Ap ; partial(r . r)      (16-B per lane)
+// K_B: r -= alpha Ap ; partial(r . r)      (16 B per lane per load, UNR double2 in flight)
+template <int UNR>
 __global__ __launch_bounds__(kBS) void k_cg_update_r(double* __restrict__ r, const double* __restrict__ Ap,
                                                      int64_t n, double* __restrict__ partials,
                                                      const CgState* __restrict__ st) {
@@ -221,7 +166,24 @@ __global__ __launch_bounds__(kBS) void k_cg_update_r(double* __restrict__ r, con
   double2* __restrict__ r2 = reinterpret_cast<double2*>(r);
   const double2* __restrict__ a2 = reinterpret_cast<const double2*>(Ap);
   const int64_t stride = (int64_t)gridDim.x * kBS;
-  for (int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x; k < n2; k += stride) {
+  int64_t k = (int64_t)blockIdx.x * kBS + threadIdx.x;
+  for (; k + (UNR - 1) * stride < n2; k += UNR * stride) {
+    double2 v[UNR], a[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      v[u] = r2[k + u * stride];
+      a[u] = a2[k + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      v[u].x = fma(na, a[u].x, v[u].x);
+      v[u].y = fma(na, a[u].y, v[u].y);
+      r2[k + u * stride] = v[u];
+      acc = fma(v[u].x, v[u].x, acc);
+      acc = fma(v[u].y, v[u].y, acc);
+    }
+  }
+  for (; k < n2; k += stride) {
     double2 v = r2[k];
     const double2 a = a2[k];
     v.x = fma(na, a.x, v.x);
@@ -336,27 +298,19 @@ __global__ __launch_bounds__(kReduceBS) void k_sum_partials(const double* __rest
 
 // ---------------------------------------------------------------------------
 // unfused building blocks
-template <typename IdxT>
+template <int ENG, typename IdxT>
 __global__ __launch_bounds__(kBS) void k_spmv_csr(CsrDev<IdxT> A, const double* __restrict__ xv,
                                                   double* __restrict__ y, TileRanges tr) {
-  csr_tiles(A, tr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
+  auto gather = [&](int32_t c) { return xv[c]; };
+  auto epi = [&](int64_t i, double sum) { y[i] = sum; };
+  if constexpr (ENG == 0) eng::csr_lds<IdxT, 8>(A, tr, gather, epi);
+  else eng::csr_direct<IdxT, 8>(A, tr, gather, epi);
 }
 
 __global__ __launch_bounds__(kBS) void k_spmv_sell(SellDev A, const double* __restrict__ xv,
                                                    double* __restrict__ y) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
-  const int64_t ns = (A.n_rows + 63) / 64;
-  for (int64_t sl = wid; sl < ns; sl += nw) {
-    const int64_t base = A.slice_ptr[sl];
-    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
-    double sum = 0.0;
-#pragma unroll 8
-    for (int j = 0; j < w; ++j) sum = fma(A.vals[base + 64 * j + lane], xv[A.cols[base + 64 * j + lane]], sum);
-    const int64_t i = sl * 64 + lane;
-    if (i < A.n_rows) y[i] = sum;
-  }
+  const TileRanges sr = make_tiles_dev((A.n_rows + 63) / 64);
+  eng::sell<8>(A, sr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
 }
 
 __global__ __launch_bounds__(kBS) void k_axpy(double alpha, const double* __restrict__ xv,
@@ -375,34 +329,67 @@ __global__ __launch_bounds__(kBS) void k_xpby(const double* __restrict__ xv, dou
 
 // ---------------------------------------------------------------------------
 // launchers
+namespace {
+template <typename IdxT, int ENG, int P>
+void launch_fused(const CsrDev<IdxT>& A, const double* r, const double* po, double* pn, double* x, double* Ap,
+                  int64_t own, const TileRanges& tr, double* partials, int grid, const CgState* st, double tol,
+                  int first, int final_mode, hipStream_t stream) {
+  hipLaunchKernelGGL((k_cg_spmv_fused<ENG, IdxT, P>), dim3(grid), dim3(kBS), 0, stream, A, r, po, pn, x, Ap, own,
+                     tr, partials, st, tol, first, final_mode);
+}
+}  // namespace
+
+int spmv_param_for(int variant, int64_t max_row_len) {
+  if (variant == 2) return max_row_len <= 4 ? 4 : (max_row_len <= 8 ? 8 : 16);
+  return max_row_len <= 4 ? 4 : (max_row_len <= 6 ? 6 : 8);
+}
+
 template <typename IdxT>
 void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pold_ext, double* pnew_ext,
                    double* x, double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int grid,
-                   const CgState* st, double tol, int first, int final_mode, hipStream_t stream) {
+                   const CgState* st, double tol, int first, int final_mode, int variant, int param,
+                   hipStream_t stream) {
   if (tr.ntiles == 0) return;
-  hipLaunchKernelGGL(k_cg_spmv_fused<IdxT>, dim3(grid), dim3(kBS), 0, stream, A, r_ext, pold_ext, pnew_ext, x,
-                     Ap, own_off, tr, partials, st, tol, first, final_mode);
+#define MCG_FUSED(E, P) \
+  launch_fused<IdxT, E, P>(A, r_ext, pold_ext, pnew_ext, x, Ap, own_off, tr, partials, grid, st, tol, first, final_mode, stream)
+  if (variant == 0) {
+    if (param <= 4) MCG_FUSED(0, 4); else if (param <= 6) MCG_FUSED(0, 6); else MCG_FUSED(0, 8);
+  } else if (variant == 1) {
+    if (param <= 4) MCG_FUSED(1, 4); else if (param <= 6) MCG_FUSED(1, 6); else MCG_FUSED(1, 8);
+  } else {
+    if (param <= 4) MCG_FUSED(2, 4); else if (param <= 8) MCG_FUSED(2, 8); else MCG_FUSED(2, 16);
+  }
+#undef MCG_FUSED
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 template void cg_spmv_fused<int32_t>(const CsrDev<int32_t>&, const double*, const double*, double*, double*,
                                      double*, int64_t, const TileRanges&, double*, int, const CgState*, double,
-                                     int, int, hipStream_t);
+                                     int, int, int, int, hipStream_t);
 template void cg_spmv_fused<int64_t>(const CsrDev<int64_t>&, const double*, const double*, double*, double*,
                                      double*, int64_t, const TileRanges&, double*, int, const CgState*, double,
-                                     int, int, hipStream_t);
+                                     int, int, int, int, hipStream_t);
 
 void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pold_ext, double* pnew_ext,
                         double* x, double* Ap, int64_t own_off, const TileRanges& slices, double* partials,
-                        int grid, const CgState* st, double tol, int first, int final_mode, hipStream_t stream) {
+                        int grid, const CgState* st, double tol, int first, int final_mode, int param,
+                        hipStream_t stream) {
   if (slices.ntiles == 0) return;
-  hipLaunchKernelGGL(k_cg_spmv_fused_sell, dim3(grid), dim3(kBS), 0, stream, A, r_ext, pold_ext, pnew_ext, x,
-                     Ap, own_off, slices, partials, st, tol, first, final_mode);
+#define MCG_SELL(U)                                                                                              \
+  hipLaunchKernelGGL(k_cg_spmv_fused_sell<U>, dim3(grid), dim3(kBS), 0, stream, A, r_ext, pold_ext, pnew_ext, x, \
+                     Ap, own_off, slices, partials, st, tol, first, final_mode)
+  if (param <= 4) MCG_SELL(4); else if (param <= 6) MCG_SELL(6); else MCG_SELL(8);
+#undef MCG_SELL
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 
 void cg_update_r(double* r_own, const double* Ap, int64_t n, double* partials, int grid, const CgState* st,
-                 hipStream_t stream) {
-  hipLaunchKernelGGL(k_cg_update_r, dim3(grid), dim3(kBS), 0, stream, r_own, Ap, n, partials, st);
+                 int unroll, hipStream_t stream) {
+  if (unroll >= 4)
+    hipLaunchKernelGGL(k_cg_update_r<4>, dim3(grid), dim3(kBS), 0, stream, r_own, Ap, n, partials, st);
+  else if (unroll == 2)
+    hipLaunchKernelGGL(k_cg_update_r<2>, dim3(grid), dim3(kBS), 0, stream, r_own, Ap, n, partials, st);
+  else
+    hipLaunchKernelGGL(k_cg_update_r<1>, dim3(grid), dim3(kBS), 0, stream, r_own, Ap, n, partials, st);
   MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
 }
 
@@ -423,15 +410,18 @@ void sum_partials(const double* partials, int np, double* out, hipStream_t strea
 }
 
 template <typename IdxT>
-void spmv_csr(const CsrDev<IdxT>& A, const double* x, double* y, hipStream_t stream) {
+void spmv_csr(const CsrDev<IdxT>& A, const double* x, double* y, hipStream_t stream, int variant) {
   const TileRanges tr = make_tiles(0, A.n_rows);
   if (tr.ntiles == 0) return;
   const int grid = grid_for(tr.ntiles * kTileRows, kBS, 8);
-  hipLaunchKernelGGL(k_spmv_csr<IdxT>, dim3(grid), dim3(kBS), 0, stream, A, x, y, tr);
+  if (variant == 1)
+    hipLaunchKernelGGL((k_spmv_csr<1, IdxT>), dim3(grid), dim3(kBS), 0, stream, A, x, y, tr);
+  else
+    hipLaunchKernelGGL((k_spmv_csr<0, IdxT>), dim3(grid), dim3(kBS), 0, stream, A, x, y, tr);
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
-template void spmv_csr<int32_t>(const CsrDev<int32_t>&, const double*, double*, hipStream_t);
-template void spmv_csr<int64_t>(const CsrDev<int64_t>&, const double*, double*, hipStream_t);
+template void spmv_csr<int32_t>(const CsrDev<int32_t>&, const double*, double*, hipStream_t, int);
+template void spmv_csr<int64_t>(const CsrDev<int64_t>&, const double*, double*, hipStream_t, int);
 
 void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream) {
   const int64_t ns = (A.n_rows + 63) / 64;

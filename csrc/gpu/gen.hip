@@ -165,6 +165,18 @@ __global__ __launch_bounds__(kGenBlock) void k_csr_to_sell(const IdxT* __restric
   }
 }
 
+__global__ __launch_bounds__(kGenBlock) void k_max_i64(const int64_t* __restrict__ a, int64_t n,
+                                                       unsigned long long* __restrict__ out) {
+  int64_t m = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) m = a[i] > m ? a[i] : m;
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t o = __shfl_down(m, off, 64);
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)m);
+}
+
 int gen_grid(int64_t n) {
   int64_t g = (n + kGenBlock - 1) / kGenBlock;
   const int64_t cap = (int64_t)num_cus() * 16;
@@ -228,6 +240,18 @@ template void gen_fill<int64_t>(const ProblemSpec&, int64_t, int64_t, int64_t, i
 void gen_rhs(const ProblemSpec& s, int64_t row_begin, int64_t n, double* b, hipStream_t st) {
   hipLaunchKernelGGL(k_rhs, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, b);
   MCG_HIP(hipGetLastError(), "kernel launch failed(gen_rhs)");
+}
+
+int64_t max_i64(const int64_t* a, int64_t n, hipStream_t st) {
+  unsigned long long* d = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(unsigned long long), st), "device malloc failed(max)");
+  MCG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), st), "device memset failed");
+  if (n > 0) hipLaunchKernelGGL(k_max_i64, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, a, n, d);
+  unsigned long long h = 0;
+  MCG_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(st), "device synchronize failed");
+  (void)hipFreeAsync(d, st);
+  return (int64_t)h;
 }
 
 void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr, hipStream_t st) {

@@ -67,6 +67,7 @@ void GpuCgSolver::setup() {
   // ---- A: count -> scan -> fill (owned rows, ext-local columns) ----
   DeviceBuffer<int64_t> rp64(n + 1, "A");
   kern::gen_rowlen(spec_, L_.row_begin, n, rp64.get(), s0_);
+  info_.max_row_len = kern::max_i64(rp64.get() + 1, n, s0_);  // row lengths, before the scan
   {
     DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(n), "A");
     kern::scan_inclusive_i64(rp64.get() + 1, n, tmp.get(), s0_);
@@ -75,6 +76,10 @@ void GpuCgSolver::setup() {
   int64_t nnz = 0;
   MCG_HIP(hipMemcpy(&nnz, rp64.get() + n, sizeof(int64_t), hipMemcpyDeviceToHost),
           "memcpy from device to host failed(A)");
+  // engine choice: short rows -> thread-per-row engines, long rows -> CSR-vector
+  info_.spmv_variant = opt_.spmv_variant >= 0 ? opt_.spmv_variant : (info_.max_row_len > 16 ? 2 : 1);
+  info_.spmv_param = opt_.spmv_param > 0 ? opt_.spmv_param
+                                         : kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
   info_.nnz_local = nnz;
   info_.idx64 = nnz >= ((int64_t)1 << 31) - 64;
   cols_.allocate(nnz, "A", 8);
@@ -128,7 +133,9 @@ void GpuCgSolver::setup() {
   auto grid_a = [&](const TileRanges& t) {
     if (t.ntiles == 0) return 0;
     if (opt_.format == 1) return kern::grid_for(t.ntiles * 64, 256, bpc);
-    return kern::grid_for(t.ntiles * kTileRows, 256, std::min(bpc, kCsrBlocksPerCuCap));
+    if (info_.spmv_variant == 0)  // LDS-limited residency
+      return kern::grid_for(t.ntiles * kTileRows, 256, std::min(bpc, kCsrBlocksPerCuCap));
+    return kern::grid_for(t.ntiles * kTileRows, 256, bpc);
   };
   auto ranges = [&](int64_t b0, int64_t e0, int64_t b1, int64_t e1) {
     if (opt_.format == 1) {  // slice units; rows [b,e) -> whole slices
@@ -205,15 +212,17 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
   if (opt_.format == 1) {
     SellDev A{slice_ptr_.get(), cols_.get(), vals_.get(), n};
     kern::cg_spmv_fused_sell(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid, st_.get(),
-                             opt_.tol, first, final_mode, s0_);
+                             opt_.tol, first, final_mode, info_.spmv_param, s0_);
   } else if (info_.idx64) {
     CsrDev<int64_t> A{rp64_.get(), cols_.get(), vals_.get(), n};
     kern::cg_spmv_fused<int64_t>(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid,
-                                 st_.get(), opt_.tol, first, final_mode, s0_);
+                                 st_.get(), opt_.tol, first, final_mode, info_.spmv_variant, info_.spmv_param,
+                                 s0_);
   } else {
     CsrDev<int32_t> A{rp32_.get(), cols_.get(), vals_.get(), n};
     kern::cg_spmv_fused<int32_t>(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid,
-                                 st_.get(), opt_.tol, first, final_mode, s0_);
+                                 st_.get(), opt_.tol, first, final_mode, info_.spmv_variant, info_.spmv_param,
+                                 s0_);
   }
 }
 
@@ -242,7 +251,8 @@ void GpuCgSolver::enqueue_iteration_(int k) {
   CgState* st = st_.get();
   kern::cg_reduce(partials_.get(), np, st, kReduceA, first, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(&st->pAp, 1, s0_);
-  kern::cg_update_r(r_.get() + L_.own_off, Ap_.get(), L_.n_local(), partials_.get(), g_b_, st, s0_);
+  kern::cg_update_r(r_.get() + L_.own_off, Ap_.get(), L_.n_local(), partials_.get(), g_b_, st, opt_.update_unroll,
+                    s0_);
   kern::cg_reduce(partials_.get(), g_b_, st, kReduceB, first, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(&st->rr_new, 1, s0_);
 }

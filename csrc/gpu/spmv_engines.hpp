@@ -1,0 +1,254 @@
+// Device-side SpMV "engines" shared by the fused CG kernel and the plain SpMV op.
+//
+// Each engine walks the rows of a launch (TileRanges: up to two local row ranges)
+// and calls  epi(row, sum)  with  sum = sum_j A[row,j] * gather(col_j).  The
+// gather functor is where the fused CG kernel recomputes p_k = r + beta p_{k-1}
+// for neighbouring rows.  All engines issue their loads in batches (clamped
+// indices + selects instead of per-element branches) so that a wave keeps many
+// independent loads in flight — a dependent load chain per nonzero is what
+// bounded the first version of the kernel (one L2 round trip per nnz).
+//
+//   csr_lds     256-row tiles; the tile's rowptr and its contiguous nnz range are
+//               staged through LDS with 16-B loads (4 double2 + 2 int4 per lane,
+//               all issued before the first LDS write), then each thread walks
+//               its row out of LDS in batches of U entries.
+//   csr_direct  thread per row, no LDS: U clamped loads of cols/vals per batch,
+//               then U gathers (L1 absorbs the stride-U*8 B access pattern).
+//   csr_vector  G lanes per row (CSR-vector), all G/passes of a 256-row tile
+//               batched, group reduction with xor-shuffles, LDS transpose so the
+//               epilogue is thread-per-row and fully coalesced.
+//   sell        one wave per 64-row SELL slice, entries column-major (every load
+//               is one coalesced 512-B / 256-B wave access), U per batch.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "mcg/kernels.hpp"
+
+namespace mcg {
+namespace kern {
+namespace eng {
+
+constexpr int kBS = 256;  // threads per block = rows per CSR tile
+constexpr int kWaves = kBS / 64;
+// LDS stager capacity per chunk: 1023 double2 + 511 int4 fit one 4+2 load batch per lane
+constexpr int kCap = 2044;
+constexpr int kV2 = 4;  // double2 per lane per chunk  (kCap/2 + 1 <= 4*256)
+constexpr int kC4 = 2;  // int4 per lane per chunk     (kCap/4 + 1 <= 2*256)
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+// fixed-order block reduction -> *out (thread 0)
+template <int BS>
+__device__ __forceinline__ void block_partial(double v, double* sh, double* out) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / 64; ++w) s += sh[w];
+    *out = s;
+  }
+}
+
+__device__ __forceinline__ void tile_rows(const TileRanges& tr, int64_t t, int64_t& r0, int64_t& r1) {
+  if (t < tr.nt0) {
+    r0 = tr.b0 + t * kTileRows;
+    r1 = r0 + kTileRows < tr.e0 ? r0 + kTileRows : tr.e0;
+  } else {
+    t -= tr.nt0;
+    r0 = tr.b1 + t * kTileRows;
+    r1 = r0 + kTileRows < tr.e1 ? r0 + kTileRows : tr.e1;
+  }
+}
+
+__device__ __forceinline__ int64_t imin(int64_t a, int64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
+
+// ---------------------------------------------------------------------------
+template <typename IdxT, int U, class Gather, class Epi>
+__device__ __forceinline__ void csr_lds(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather, Epi&& epi) {
+  __shared__ __attribute__((aligned(16))) double2 s_v2[kV2 * kBS];
+  __shared__ __attribute__((aligned(16))) int4 s_c4[kC4 * kBS];
+  __shared__ int64_t s_rp[kBS + 1];
+  const double* s_v = reinterpret_cast<const double*>(s_v2);
+  const int32_t* s_c = reinterpret_cast<const int32_t*>(s_c4);
+  const int t = threadIdx.x;
+  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+    int64_t r0, r1;
+    tile_rows(tr, tile, r0, r1);
+    const int nr = (int)(r1 - r0);
+    if (t < nr) s_rp[t] = (int64_t)A.rowptr[r0 + t];
+    if (t == 0) s_rp[nr] = (int64_t)A.rowptr[r0 + nr];
+    __syncthreads();
+    const int64_t rs = s_rp[0], re = s_rp[nr];
+    int64_t my_b = 0, my_e = 0;
+    if (t < nr) {
+      my_b = s_rp[t];
+      my_e = s_rp[t + 1];
+    }
+    double sum = 0.0;
+    for (int64_t cs = rs; cs < re; cs += kCap) {
+      const int64_t ce = imin(re, cs + kCap);
+      const int64_t vb = cs & ~(int64_t)1, cb = cs & ~(int64_t)3;
+      const int nv2 = (int)((ce - vb + 1) >> 1), nc4 = (int)((ce - cb + 3) >> 2);
+      const double2* gv = reinterpret_cast<const double2*>(A.vals + vb);
+      const int4* gc = reinterpret_cast<const int4*>(A.cols + cb);
+      double2 vr[kV2];
+      int4 cr[kC4];
+#pragma unroll
+      for (int u = 0; u < kV2; ++u) vr[u] = gv[imin(t + u * kBS, nv2 - 1)];
+#pragma unroll
+      for (int u = 0; u < kC4; ++u) cr[u] = gc[imin(t + u * kBS, nc4 - 1)];
+#pragma unroll
+      for (int u = 0; u < kV2; ++u)
+        if (t + u * kBS < nv2) s_v2[t + u * kBS] = vr[u];
+#pragma unroll
+      for (int u = 0; u < kC4; ++u)
+        if (t + u * kBS < nc4) s_c4[t + u * kBS] = cr[u];
+      __syncthreads();
+      const int64_t jb = imax(my_b, cs), je = imin(my_e, ce);
+      for (int64_t j0 = jb; j0 < je; j0 += U) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = imin(j0 + u, je - 1);
+          c[u] = s_c[j - cb];
+          v[u] = s_v[j - vb];
+        }
+        double g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) sum = (j0 + u < je) ? fma(v[u], g[u], sum) : sum;
+      }
+      __syncthreads();
+    }
+    if (t < nr) epi(r0 + t, sum);
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename IdxT, int U, class Gather, class Epi>
+__device__ __forceinline__ void csr_direct(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather, Epi&& epi) {
+  const int t = threadIdx.x;
+  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+    int64_t r0, r1;
+    tile_rows(tr, tile, r0, r1);
+    if (r0 + t >= r1) continue;
+    const int64_t i = r0 + t;
+    const int64_t rs = (int64_t)A.rowptr[i], re = (int64_t)A.rowptr[i + 1];
+    double sum = 0.0;
+    for (int64_t j0 = rs; j0 < re; j0 += U) {
+      int32_t c[U];
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = imin(j0 + u, re - 1);
+        c[u] = A.cols[j];
+        v[u] = A.vals[j];
+      }
+      double g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum = (j0 + u < re) ? fma(v[u], g[u], sum) : sum;
+    }
+    epi(i, sum);
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename IdxT, int G, class Gather, class Epi>
+__device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather, Epi&& epi) {
+  static_assert(G == 4 || G == 8 || G == 16, "lanes per row");
+  constexpr int RPP = kBS / G;  // rows per pass; G passes cover a 256-row tile
+  __shared__ double s_sum[kBS];
+  const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
+  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+    int64_t r0, r1;
+    tile_rows(tr, tile, r0, r1);
+    const int nr = (int)(r1 - r0);
+    int64_t rs[G], re[G];
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      const int lr = p * RPP + grp;
+      const int64_t ii = r0 + (lr < nr ? lr : nr - 1);
+      rs[p] = (int64_t)A.rowptr[ii];
+      re[p] = lr < nr ? (int64_t)A.rowptr[ii + 1] : rs[p];
+    }
+    int32_t c[G];
+    double v[G];
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      const int64_t j = rs[p] + sub;
+      const int64_t jj = re[p] > rs[p] ? imin(j, re[p] - 1) : 0;
+      c[p] = A.cols[jj];
+      v[p] = A.vals[jj];
+    }
+    double s[G];
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      const double g = gather(c[p]);
+      s[p] = (rs[p] + sub < re[p]) ? v[p] * g : 0.0;
+    }
+    // rows longer than G: rare remainder
+#pragma unroll
+    for (int p = 0; p < G; ++p)
+      for (int64_t j = rs[p] + sub + G; j < re[p]; j += G) s[p] = fma(A.vals[j], gather(A.cols[j]), s[p]);
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      double x = s[p];
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, G);
+      if (sub == 0) s_sum[p * RPP + grp] = x;
+    }
+    __syncthreads();
+    if (t < nr) epi(r0 + t, s_sum[t]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SELL-64: `sr` in slice units; one wave per slice.
+template <int U, class Gather, class Epi>
+__device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t t = wid; t < sr.ntiles; t += nw) {
+    const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
+    const int64_t base = A.slice_ptr[sl];
+    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
+    const int32_t* __restrict__ cp = A.cols + base + lane;
+    const double* __restrict__ vp = A.vals + base + lane;
+    double sum = 0.0;
+    for (int j0 = 0; j0 < w; j0 += U) {
+      int32_t c[U];
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = (j0 + u < w ? j0 + u : w - 1) * 64;
+        c[u] = cp[j];
+        v[u] = vp[j];
+      }
+      double g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum = (j0 + u < w) ? fma(v[u], g[u], sum) : sum;
+    }
+    const int64_t i = sl * 64 + lane;
+    if (i < A.n_rows) epi(i, sum);
+  }
+}
+
+}  // namespace eng
+}  // namespace kern
+}  // namespace mcg

@@ -23,8 +23,11 @@ struct CgOptions {
   bool overlap = true;       // halo on a side stream, overlapped with the interior SpMV
   bool use_graph = true;     // capture iteration pairs into a hipGraph
   bool force_comm = false;   // run RCCL collectives even with one rank
-  int format = 0;            // 0 = CSR (LDS-staged row tiles), 1 = SELL-64
+  int format = 0;            // 0 = CSR, 1 = SELL-64
   int blocks_per_cu = 8;     // grid sizing for the streaming kernels
+  int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector; -1 = auto
+  int spmv_param = 0;        // batch U (engines 0/1, SELL) or lanes/row G (engine 2); 0 = auto
+  int update_unroll = 2;     // double2 loads in flight per lane in the residual update
 };
 
 struct CgResult {

@@ -83,6 +83,8 @@ template <typename IdxT>
 void gen_fill(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
               const int64_t* rowptr64, IdxT* rowptr_out, int32_t* cols, double* vals, hipStream_t st);
 void gen_rhs(const ProblemSpec& s, int64_t row_begin, int64_t n, double* b, hipStream_t st);
+// max over a[0..n) (synchronous; setup only)
+int64_t max_i64(const int64_t* a, int64_t n, hipStream_t st);
 // CSR -> SELL-64 (slice_ptr must be precomputed on the host/device from row lengths)
 void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr /* ns+1 */, hipStream_t st);
 template <typename IdxT>
@@ -91,19 +93,22 @@ void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, in
                  hipStream_t st);
 
 // ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
+// variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row);
+// param: batch size U in {4,6,8} (variants 0/1) or G in {4,8,16} (variant 2)
 template <typename IdxT>
 void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pold_ext,
                    double* pnew_ext, double* x, double* Ap, int64_t own_off, const TileRanges& tr,
                    double* partials, int grid, const CgState* st, double tol, int first,
-                   int final_mode, hipStream_t stream);
+                   int final_mode, int variant, int param, hipStream_t stream);
+int spmv_param_for(int variant, int64_t max_row_len);
 // `slices`: TileRanges in units of 64-row slices
 void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pold_ext,
                         double* pnew_ext, double* x, double* Ap, int64_t own_off,
                         const TileRanges& slices, double* partials, int grid,
-                        const CgState* st, double tol, int first, int final_mode,
+                        const CgState* st, double tol, int first, int final_mode, int param,
                         hipStream_t stream);
 void cg_update_r(double* r_own, const double* Ap, int64_t n, double* partials, int grid,
-                 const CgState* st, hipStream_t stream);
+                 const CgState* st, int unroll, hipStream_t stream);
 void cg_reduce(const double* partials, int np, CgState* st, int mode, int first, double tol,
                hipStream_t stream);
 void dot_partials(const double* a, const double* b, int64_t n, double* partials, int grid,
@@ -113,7 +118,7 @@ void sum_partials(const double* partials, int np, double* out, hipStream_t strea
 
 // ---- unfused ops (ops API / tests) ----
 template <typename IdxT>
-void spmv_csr(const CsrDev<IdxT>& A, const double* x, double* y, hipStream_t stream);
+void spmv_csr(const CsrDev<IdxT>& A, const double* x, double* y, hipStream_t stream, int variant = 0);
 void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream);
 void axpy(double alpha, const double* x, double* y, int64_t n, hipStream_t stream);  // y += a x
 void xpby(const double* x, double beta, double* y, int64_t n, hipStream_t stream);   // y = x + b y

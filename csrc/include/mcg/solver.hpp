@@ -43,6 +43,8 @@ struct SolverInfo {
   size_t device_bytes = 0;
   double bytes_per_iter_model = 0;  // modelled HBM bytes per iteration (this rank)
   int grid_a = 0, grid_b = 0;
+  int64_t max_row_len = 0;
+  int spmv_variant = 0, spmv_param = 0;
 };
 
 class GpuCgSolver {

@@ -38,7 +38,8 @@ ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64
 }
 
 CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool use_graph, bool force_comm,
-                    const std::string& format, int blocks_per_cu) {
+                    const std::string& format, int blocks_per_cu, int spmv_variant, int spmv_param,
+                    int update_unroll) {
   CgOptions o;
   o.maxit = maxit;
   o.tol = tol;
@@ -50,6 +51,9 @@ CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool u
   else if (format == "sell" || format == "sell64") o.format = 1;
   else fail("unknown format: " + format);
   o.blocks_per_cu = blocks_per_cu;
+  o.spmv_variant = spmv_variant;
+  o.spmv_param = spmv_param;
+  o.update_unroll = update_unroll;
   return o;
 }
 
@@ -126,7 +130,11 @@ PYBIND11_MODULE(_C, m) {
   py::class_<CgOptions>(m, "CgOptions")
       .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
-           py::arg("format") = "csr", py::arg("blocks_per_cu") = 8)
+           py::arg("format") = "csr", py::arg("blocks_per_cu") = 8, py::arg("spmv_variant") = -1,
+           py::arg("spmv_param") = 0, py::arg("update_unroll") = 2)
+      .def_readwrite("spmv_variant", &CgOptions::spmv_variant)
+      .def_readwrite("spmv_param", &CgOptions::spmv_param)
+      .def_readwrite("update_unroll", &CgOptions::update_unroll)
       .def_readwrite("maxit", &CgOptions::maxit)
       .def_readwrite("tol", &CgOptions::tol)
       .def_readwrite("check_every", &CgOptions::check_every)
@@ -242,6 +250,9 @@ PYBIND11_MODULE(_C, m) {
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
         d["grid_b"] = i.grid_b;
+        d["max_row_len"] = i.max_row_len;
+        d["spmv_variant"] = i.spmv_variant;
+        d["spmv_param"] = i.spmv_param;
         return d;
       });
 
