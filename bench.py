@@ -39,7 +39,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--problem", default="poisson2d")
-    ap.add_argument("--format", default="csr", choices=["csr", "sell"])
+    ap.add_argument("--format", default="csr", choices=["csr", "sell", "sell16"])
+    ap.add_argument("--recurrence", type=int, default=-1, help="0 two-reduction, 1 single-reduction, -1 auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--blocks-per-cu", type=int, default=8)
@@ -61,7 +62,7 @@ def main() -> int:
     C = mcg.native()
     opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
                        use_graph=not args.no_graph, force_comm=False, format=args.format,
-                       blocks_per_cu=args.blocks_per_cu)
+                       blocks_per_cu=args.blocks_per_cu, recurrence=args.recurrence)
     t_setup = time.perf_counter()
     solver = C.Solver(spec.native(), opts, env.rank, env.world, comm)
     solver.setup()

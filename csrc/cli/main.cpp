@@ -77,7 +77,10 @@ Args parse(int argc, char** argv) {
     else if (f == "--check-every") a.opt.check_every = std::stoi(need(i));
     else if (f == "--fixed-iters") a.fixed_iters = std::stoi(need(i));
     else if (f == "--warmup") a.warmup = std::stoi(need(i));
-    else if (f == "--format") { std::string v = need(i); a.opt.format = (v == "sell" || v == "sell64") ? 1 : 0; }
+    else if (f == "--format") {
+      std::string v = need(i);
+      a.opt.format = (v == "sell" || v == "sell64") ? 1 : ((v == "sell16" || v == "sell64-d16") ? 2 : 0);
+    }
     else if (f == "--no-overlap") a.opt.overlap = false;
     else if (f == "--no-graph") a.opt.use_graph = false;
     else if (f == "--force-comm") a.opt.force_comm = true;
@@ -85,6 +88,13 @@ Args parse(int argc, char** argv) {
     else if (f == "--spmv-variant") a.opt.spmv_variant = std::stoi(need(i));
     else if (f == "--spmv-param") a.opt.spmv_param = std::stoi(need(i));
     else if (f == "--update-unroll") a.opt.update_unroll = std::stoi(need(i));
+    else if (f == "--nt-loads") a.opt.nt_loads = std::stoi(need(i));
+    else if (f == "--xcd-map") a.opt.xcd_map = std::stoi(need(i));
+    else if (f == "--sell-slices") a.opt.sell_slices = std::stoi(need(i));
+    else if (f == "--recurrence") {
+      std::string v = need(i);
+      a.opt.recurrence = (v == "single" || v == "fused1" || v == "1") ? 1 : 0;
+    }
     else if (f == "--print-x") a.print_x = need(i);
     else if (f == "--report") a.report = need(i);
     else if (f == "--verify") a.verify = true;

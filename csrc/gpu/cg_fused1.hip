@@ -1,0 +1,232 @@
+// Single-reduction fused CG iteration (one streaming pass + one reduction + one
+// 32-byte all-reduce per iteration).  See kernels.hpp "cg_fused1" for the math.
+//
+// Compared with the two-pass form in cg_kernels.hip (K_A SpMV pass + K_B residual
+// pass, two reductions, two all-reduces), the residual update r_k = r_{k-1} -
+// a Ap_{k-1} moves into the next SpMV pass, where the neighbours' p_k values are
+// recomputed from (r_{k-1}, Ap_{k-1}, p_{k-1}) exactly as their owners compute them.
+// HBM traffic per 5-pt SELL row drops from ~132 B to ~124 B, the per-iteration
+// kernel count from 4 to 2, and — what matters for multi-GPU strong scaling —
+// the latency-bound all-reduces from two to one.  r, Ap and p are
+// double-buffered by iteration parity because neighbours gather the old values
+// while the owner writes the new ones.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "mcg/check.hpp"
+#include "mcg/kernels.hpp"
+#include "spmv_engines.hpp"
+
+namespace mcg {
+namespace kern {
+namespace {
+
+using eng::kBS;
+using eng::kWaves;
+constexpr int kReduceBS = 1024;
+
+struct F1Scalars {
+  double alpha, beta;
+  bool conv;
+};
+
+__device__ __forceinline__ F1Scalars f1_scalars(const CgState* __restrict__ st, double tol, int first, int check) {
+  F1Scalars s;
+  const double pAp = st->red[0], rAp = st->red[1], ApAp = st->red[2], rr = st->red[3];
+  s.conv = check && sqrt(rr) < tol;  // ||r_{k-1}|| < tol : the reference's break (CUDACG.cu:333)
+  if (first) {
+    s.alpha = 0.0;
+    s.beta = 0.0;
+  } else {
+    s.alpha = rr / pAp;
+    double est = fma(s.alpha * s.alpha, ApAp, fma(-2.0 * s.alpha, rAp, rr));  // ||r_{k-1} - a Ap_{k-1}||^2
+    est = est > 0.0 ? est : 0.0;
+    s.beta = est / rr;
+  }
+  return s;
+}
+
+// four fixed-order block partials -> partials[q * pstride + blockIdx.x]
+__device__ __forceinline__ void block_partial4(double a0, double a1, double a2, double a3, double* __restrict__ out,
+                                               int pstride) {
+  __shared__ double sh[4][kWaves];
+  a0 = eng::wave_sum(a0);
+  a1 = eng::wave_sum(a1);
+  a2 = eng::wave_sum(a2);
+  a3 = eng::wave_sum(a3);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = a0;
+    sh[1][w] = a1;
+    sh[2][w] = a2;
+    sh[3][w] = a3;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) s += sh[threadIdx.x][k];
+    out[threadIdx.x * pstride + blockIdx.x] = s;
+  }
+}
+
+template <int FMT, typename IdxT, int U>
+__global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+                                               double* __restrict__ partials, int pstride,
+                                               const CgState* __restrict__ st, double tol, int first, int check,
+                                               int final_mode) {
+  if (st->done) return;
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (sc.conv) return;  // x_{k-1} is the answer; the reduce latches
+  const double a = sc.alpha, b = sc.beta, na = -a;
+  const double* __restrict__ ro = v.r_old;
+  const double* __restrict__ apo = v.ap_old;
+  const double* __restrict__ po = v.p_old;
+  double* __restrict__ rn = v.r_new;
+  double* __restrict__ apn = v.ap_new;
+  double* __restrict__ pn = v.p_new;
+  double* __restrict__ x = v.x;
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+  if (final_mode) {
+    // last iteration's r and x updates only (no SpMV): r_m, x_m, partial ||r_m||^2
+    const int64_t n = FMT == 0 ? A.n_rows : S.n_rows;
+    const int64_t unit = FMT == 0 ? kTileRows : 64;
+    const int64_t sub = FMT == 0 ? 0 : (threadIdx.x >> 6), nsub = FMT == 0 ? 1 : kWaves;
+    const int64_t lane = FMT == 0 ? threadIdx.x : (threadIdx.x & 63);
+    for (eng::TileCursor cur = eng::tile_cursor(tr, sub, nsub); cur.t < cur.end; cur.t += cur.step) {
+      const int64_t t = cur.t;
+      const int64_t u0 = t < tr.nt0 ? tr.b0 + t * (FMT == 0 ? kTileRows : 1)
+                                    : tr.b1 + (t - tr.nt0) * (FMT == 0 ? kTileRows : 1);
+      const int64_t row0 = FMT == 0 ? u0 : u0 * unit;
+      const int64_t i = row0 + lane;
+      const int64_t lim = FMT == 0 ? (t < tr.nt0 ? tr.e0 : tr.e1) : n;
+      if (i < lim && i < n) {
+        const double rk = fma(na, apo[own + i], ro[own + i]);
+        rn[own + i] = rk;
+        x[i] = fma(a, po[own + i], x[i]);
+        s_rr = fma(rk, rk, s_rr);
+      }
+    }
+    block_partial4(0.0, 0.0, 0.0, s_rr, partials, pstride);
+    return;
+  }
+  auto gather = [&](int32_t c) { return fma(b, po[c], fma(na, apo[c], ro[c])); };
+  auto epi = [&](int64_t i, double sum) {
+    const int64_t e = own + i;
+    const double rk = fma(na, apo[e], ro[e]);
+    const double pold = po[e];
+    const double pk = fma(b, pold, rk);
+    rn[e] = rk;
+    pn[e] = pk;
+    apn[e] = sum;
+    x[i] = fma(a, pold, x[i]);
+    s_pap = fma(pk, sum, s_pap);
+    s_rap = fma(rk, sum, s_rap);
+    s_apap = fma(sum, sum, s_apap);
+    s_rr = fma(rk, rk, s_rr);
+  };
+  if constexpr (FMT == 0) eng::csr_direct<IdxT, U, false>(A, tr, gather, epi);
+  else if constexpr (FMT == 1) eng::sell<U, false, false>(S, tr, gather, epi);
+  else if constexpr (FMT == 3) eng::sell<U, false, true>(S, tr, gather, epi);
+  else eng::sell2<U, false>(S, tr, gather, epi);
+  block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
+}
+
+__global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __restrict__ partials, int pstride, int np,
+                                                            CgState* __restrict__ st, int mode, int check,
+                                                            double tol) {
+  __shared__ double sh[4][kReduceBS / 64];
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < np; i += kReduceBS) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] += partials[q * pstride + i];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double w = eng::wave_sum(s[q]);
+    if ((threadIdx.x & 63) == 0) sh[q][threadIdx.x >> 6] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double tot[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    tot[q] = 0.0;
+    for (int w = 0; w < kReduceBS / 64; ++w) tot[q] += sh[q][w];
+  }
+  auto zero = [&] {
+    for (int q = 0; q < 4; ++q) st->red[q] = 0.0;
+  };
+  if (mode == 2) {  // latch after the final pass's all-reduce
+    if (st->done) return;
+    st->done = 2;
+    st->rr_final = st->red[3];
+    st->converged = sqrt(st->red[3]) < tol ? 1 : 0;
+    st->conv_iter = st->iter;
+    return;
+  }
+  if (st->done) { zero(); return; }
+  const double rr_prev = st->red[3];
+  if (check && sqrt(rr_prev) < tol) {
+    st->done = 1;
+    st->converged = 1;
+    st->conv_iter = st->iter - 1;
+    st->rr_final = rr_prev;
+    zero();
+    return;
+  }
+  if (check && !isfinite(rr_prev)) {
+    st->done = 3;
+    st->breakdown = 1;
+    st->conv_iter = st->iter - 1;
+    st->rr_final = rr_prev;
+    zero();
+    return;
+  }
+  if (mode == 1) {
+    st->red[0] = st->red[1] = st->red[2] = 0.0;
+    st->red[3] = tot[3];
+    return;
+  }
+  for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
+  st->rr_new = tot[3];
+  st->iter += 1;
+}
+
+}  // namespace
+
+template <typename IdxT>
+void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
+               const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
+               int first, int check, int final_mode, hipStream_t stream) {
+  if (tr.ntiles == 0 || grid == 0) return;
+#define MCG_F1(F, U)                                                                                              \
+  hipLaunchKernelGGL((k_cg_f1<F, IdxT, U>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, partials, \
+                     pstride, st, tol, first, check, final_mode)
+#define MCG_F1U(F) \
+  do { if (param <= 4) MCG_F1(F, 4); else if (param <= 6) MCG_F1(F, 6); else MCG_F1(F, 8); } while (0)
+  if (fmt == 0) MCG_F1U(0);
+  else if (fmt == 1) MCG_F1U(1);
+  else if (fmt == 2) MCG_F1U(2);
+  else MCG_F1U(3);
+#undef MCG_F1U
+#undef MCG_F1
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+template void cg_fused1<int32_t>(int, int, const CsrDev<int32_t>&, const SellDev&, const F1Vectors&, int64_t,
+                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int,
+                                 hipStream_t);
+template void cg_fused1<int64_t>(int, int, const CsrDev<int64_t>&, const SellDev&, const F1Vectors&, int64_t,
+                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int,
+                                 hipStream_t);
+
+void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, double tol,
+                  hipStream_t stream) {
+  hipLaunchKernelGGL(k_cg_reduce_f1, dim3(1), dim3(kReduceBS), 0, stream, partials, pstride, np, st, mode, check,
+                     tol);
+  MCG_HIP(hipGetLastError(), "compute dot failed(tmp)");
+}
+
+}  // namespace kern
+}  // namespace mcg

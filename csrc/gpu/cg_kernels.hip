@@ -110,13 +110,15 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
     acc = fma(pi, sum, acc);
   };
   if constexpr (ENG == 0) eng::csr_lds<IdxT, P>(A, tr, gather, epi);
-  else if constexpr (ENG == 1) eng::csr_direct<IdxT, P>(A, tr, gather, epi);
+  else if constexpr (ENG == 1) eng::csr_direct<IdxT, P, false>(A, tr, gather, epi);
+  else if constexpr (ENG == 3) eng::csr_direct<IdxT, P, true>(A, tr, gather, epi);
   else eng::csr_vector<IdxT, P>(A, tr, gather, epi);
   block_partial<kBS>(acc, s_red, partials + blockIdx.x);
 }
 
-// K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries)
-template <int U>
+// K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries).
+// S = 2: two slices in flight per wave; D16: 16-bit column offsets.
+template <int U, int S, bool D16>
 __global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const double* __restrict__ r,
                                                             const double* __restrict__ pold,
                                                             double* __restrict__ pnew, double* __restrict__ x,
@@ -139,16 +141,17 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const dou
     return;
   }
   double acc = 0.0;
-  eng::sell<U>(
-      A, sr, [&](int32_t c) { return fma(beta, pold[c], r[c]); },
-      [&](int64_t i, double sum) {
-        const double po = pold[own + i];
-        const double pi = fma(beta, po, r[own + i]);
-        pnew[own + i] = pi;
-        Ap[i] = sum;
-        x[i] = fma(alpha, po, x[i]);
-        acc = fma(pi, sum, acc);
-      });
+  auto gather = [&](int32_t c) { return fma(beta, pold[c], r[c]); };
+  auto epi = [&](int64_t i, double sum) {
+    const double po = pold[own + i];
+    const double pi = fma(beta, po, r[own + i]);
+    pnew[own + i] = pi;
+    Ap[i] = sum;
+    x[i] = fma(alpha, po, x[i]);
+    acc = fma(pi, sum, acc);
+  };
+  if constexpr (S == 2) eng::sell2<U, false>(A, sr, gather, epi);
+  else eng::sell<U, false, D16>(A, sr, gather, epi);
   block_partial<kBS>(acc, s_red, partials + blockIdx.x);
 }
 
@@ -304,13 +307,14 @@ __global__ __launch_bounds__(kBS) void k_spmv_csr(CsrDev<IdxT> A, const double* 
   auto gather = [&](int32_t c) { return xv[c]; };
   auto epi = [&](int64_t i, double sum) { y[i] = sum; };
   if constexpr (ENG == 0) eng::csr_lds<IdxT, 8>(A, tr, gather, epi);
-  else eng::csr_direct<IdxT, 8>(A, tr, gather, epi);
+  else eng::csr_direct<IdxT, 8, false>(A, tr, gather, epi);
 }
 
+template <bool D16>
 __global__ __launch_bounds__(kBS) void k_spmv_sell(SellDev A, const double* __restrict__ xv,
                                                    double* __restrict__ y) {
   const TileRanges sr = make_tiles_dev((A.n_rows + 63) / 64);
-  eng::sell<8>(A, sr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
+  eng::sell<8, false, D16>(A, sr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
 }
 
 __global__ __launch_bounds__(kBS) void k_axpy(double alpha, const double* __restrict__ xv,
@@ -356,6 +360,8 @@ void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pol
     if (param <= 4) MCG_FUSED(0, 4); else if (param <= 6) MCG_FUSED(0, 6); else MCG_FUSED(0, 8);
   } else if (variant == 1) {
     if (param <= 4) MCG_FUSED(1, 4); else if (param <= 6) MCG_FUSED(1, 6); else MCG_FUSED(1, 8);
+  } else if (variant == 3) {
+    if (param <= 4) MCG_FUSED(3, 4); else if (param <= 6) MCG_FUSED(3, 6); else MCG_FUSED(3, 8);
   } else {
     if (param <= 4) MCG_FUSED(2, 4); else if (param <= 8) MCG_FUSED(2, 8); else MCG_FUSED(2, 16);
   }
@@ -372,11 +378,20 @@ template void cg_spmv_fused<int64_t>(const CsrDev<int64_t>&, const double*, cons
 void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pold_ext, double* pnew_ext,
                         double* x, double* Ap, int64_t own_off, const TileRanges& slices, double* partials,
                         int grid, const CgState* st, double tol, int first, int final_mode, int param,
-                        hipStream_t stream) {
+                        int flags, hipStream_t stream) {
   if (slices.ntiles == 0) return;
-#define MCG_SELL(U)                                                                                              \
-  hipLaunchKernelGGL(k_cg_spmv_fused_sell<U>, dim3(grid), dim3(kBS), 0, stream, A, r_ext, pold_ext, pnew_ext, x, \
-                     Ap, own_off, slices, partials, st, tol, first, final_mode)
+#define MCG_SELL(U)                                                                                     \
+  do {                                                                                                  \
+    if (flags & 4)                                                                                      \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, true>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,    \
+                         pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
+    else if (flags & 2)                                                                                 \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 2, false>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,   \
+                         pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
+    else                                                                                                \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, false>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,   \
+                         pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
+  } while (0)
   if (param <= 4) MCG_SELL(4); else if (param <= 6) MCG_SELL(6); else MCG_SELL(8);
 #undef MCG_SELL
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
@@ -427,7 +442,10 @@ void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream)
   const int64_t ns = (A.n_rows + 63) / 64;
   if (ns == 0) return;
   const int grid = grid_for(ns * 64, kBS, 8);
-  hipLaunchKernelGGL(k_spmv_sell, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+  if (A.dcols)
+    hipLaunchKernelGGL(k_spmv_sell<true>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+  else
+    hipLaunchKernelGGL(k_spmv_sell<false>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 

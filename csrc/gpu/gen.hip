@@ -146,7 +146,8 @@ __global__ __launch_bounds__(kGenBlock) void k_csr_to_sell(const IdxT* __restric
                                                            const double* __restrict__ vals, int64_t n,
                                                            int64_t own_off, const int64_t* __restrict__ sp,
                                                            int32_t* __restrict__ scols,
-                                                           double* __restrict__ svals) {
+                                                           double* __restrict__ svals,
+                                                           int16_t* __restrict__ dcols) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t sl = i >> 6, l = i & 63;
@@ -154,13 +155,10 @@ __global__ __launch_bounds__(kGenBlock) void k_csr_to_sell(const IdxT* __restric
     const int64_t rs = rp[i], len = (int64_t)rp[i + 1] - rs;
     for (int64_t j = 0; j < w; ++j) {
       const int64_t dst = base + 64 * j + l;
-      if (j < len) {
-        scols[dst] = cols[rs + j];
-        svals[dst] = vals[rs + j];
-      } else {
-        scols[dst] = (int32_t)(own_off + i);
-        svals[dst] = 0.0;
-      }
+      const int32_t c = j < len ? cols[rs + j] : (int32_t)(own_off + i);  // padding: own column, value 0
+      if (dcols) dcols[dst] = (int16_t)(c - (own_off + i));
+      else scols[dst] = c;
+      svals[dst] = j < len ? vals[rs + j] : 0.0;
     }
   }
 }
@@ -262,15 +260,15 @@ void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr, h
 
 template <typename IdxT>
 void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
-                 const int64_t* slice_ptr, int32_t* scols, double* svals, hipStream_t st) {
+                 const int64_t* slice_ptr, int32_t* scols, double* svals, hipStream_t st, int16_t* dcols) {
   hipLaunchKernelGGL(k_csr_to_sell<IdxT>, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, rowptr, cols, vals,
-                     n, own_off, slice_ptr, scols, svals);
+                     n, own_off, slice_ptr, scols, svals, dcols);
   MCG_HIP(hipGetLastError(), "kernel launch failed(csr_to_sell)");
 }
 template void csr_to_sell<int32_t>(const int32_t*, const int32_t*, const double*, int64_t, int64_t,
-                                   const int64_t*, int32_t*, double*, hipStream_t);
+                                   const int64_t*, int32_t*, double*, hipStream_t, int16_t*);
 template void csr_to_sell<int64_t>(const int64_t*, const int32_t*, const double*, int64_t, int64_t,
-                                   const int64_t*, int32_t*, double*, hipStream_t);
+                                   const int64_t*, int32_t*, double*, hipStream_t, int16_t*);
 
 }  // namespace kern
 }  // namespace mcg

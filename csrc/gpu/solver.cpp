@@ -19,6 +19,11 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   MCG_CHECK(world == 1 || comm != nullptr, "multi-rank solver needs a communicator");
   RowPartition part = partition_rows(spec_, world_);
   L_ = make_layout(spec_, part, rank_);
+  if (opt_.format == 2) {  // SELL-64 with 16-bit column offsets, if the bandwidth fits int16
+    d16_ = bandwidth(spec_) <= 32767;
+    opt_.format = 1;
+  }
+  if (opt_.recurrence < 0) opt_.recurrence = world_ > 1 ? 1 : 0;  // auto: one all-reduce per iteration when P > 1
   use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
   use_halo_ = use_comm_ && L_.has_halo();
   s0_ = Stream(true, 0);
@@ -62,7 +67,8 @@ void GpuCgSolver::setup() {
   info_.halo_in = L_.halo_rows_in();
   info_.halo_out = L_.halo_rows_out();
   info_.interior_rows = L_.interior_end - L_.interior_begin;
-  info_.format = opt_.format;
+  info_.format = d16_ ? 2 : opt_.format;
+  info_.recurrence = opt_.recurrence;
 
   // ---- A: count -> scan -> fill (owned rows, ext-local columns) ----
   DeviceBuffer<int64_t> rp64(n + 1, "A");
@@ -80,6 +86,7 @@ void GpuCgSolver::setup() {
   info_.spmv_variant = opt_.spmv_variant >= 0 ? opt_.spmv_variant : (info_.max_row_len > 16 ? 2 : 1);
   info_.spmv_param = opt_.spmv_param > 0 ? opt_.spmv_param
                                          : kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
+  if (opt_.nt_loads && info_.spmv_variant == 1) info_.spmv_variant = 3;
   info_.nnz_local = nnz;
   info_.idx64 = nnz >= ((int64_t)1 << 31) - 64;
   cols_.allocate(nnz, "A", 8);
@@ -99,20 +106,21 @@ void GpuCgSolver::setup() {
     MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
     MCG_HIP(hipMemcpy(&total, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
             "memcpy from device to host failed(A)");
-    DeviceBuffer<int32_t> scols(total, "A", 8);
+    DeviceBuffer<int32_t> scols(d16_ ? 0 : total, "A", 8);
     DeviceBuffer<double> svals(total, "A", 8);
+    if (d16_) dcols_.allocate(total, "A", 16);
     if (info_.idx64)
       kern::csr_to_sell<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                 scols.get(), svals.get(), s0_);
+                                 scols.get(), svals.get(), s0_, dcols_.get());
     else
       kern::csr_to_sell<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                 scols.get(), svals.get(), s0_);
+                                 scols.get(), svals.get(), s0_, dcols_.get());
     MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
     cols_ = std::move(scols);
     vals_ = std::move(svals);
     rp32_.release();
     stored_entries = total;
-    matrix_bytes = total * 12 + (ns + 1) * 8;
+    matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
   } else {
     matrix_bytes = nnz * 12 + (n + 1) * (info_.idx64 ? 8 : 4);
     if (info_.idx64) rp64_ = std::move(rp64);
@@ -121,9 +129,15 @@ void GpuCgSolver::setup() {
 
   // ---- vectors ----
   x_.allocate(n, "x", 8);
-  Ap_.allocate(n, "Ap", 8);
   b_.allocate(n, "b", 8);
   r_.allocate(L_.ext_len, "r", 8);
+  if (opt_.recurrence == 1) {  // single-reduction form: r and Ap are gathered -> ext layout, double-buffered
+    Ap_.allocate(L_.ext_len, "Ap", 8);
+    Ap1_.allocate(L_.ext_len, "Ap", 8);
+    r1_.allocate(L_.ext_len, "r", 8);
+  } else {
+    Ap_.allocate(n, "Ap", 8);
+  }
   p_[0].allocate(L_.ext_len, "p", 8);
   p_[1].allocate(L_.ext_len, "p", 8);
   kern::gen_rhs(spec_, L_.row_begin, n, b_.get(), s0_);
@@ -163,11 +177,13 @@ void GpuCgSolver::setup() {
     g_int_ = grid_a(tr_int_);
     g_bnd_ = grid_a(tr_bnd_);
   }
+  if (opt_.xcd_map) tr_all_.xcd = tr_int_.xcd = tr_bnd_.xcd = 8;
   g_b_ = kern::grid_for((n + 1) / 2, 256, bpc);
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
   const int np = std::max({g_all_, g_int_ + g_bnd_, g_b_, 1});
-  partials_.allocate(np + 64, "partials");
+  pstride_ = np + 64;
+  partials_.allocate((size_t)pstride_ * (opt_.recurrence == 1 ? 4 : 1), "partials");
   st_.allocate(1, "state");
   MCG_HIP(hipMemsetAsync(partials_.get(), 0, partials_.bytes(), s0_), "device memset failed");
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s0_), "device memset failed");
@@ -177,6 +193,9 @@ void GpuCgSolver::setup() {
   const double vec_a = 8.0 * (1 + 1 + 1 + 2 + 1);  // r, pold gathers (ideal), pnew, x rw, Ap
   const double vec_b = 24.0;                        // r rw, Ap
   info_.bytes_per_iter_model = (double)matrix_bytes + (vec_a + vec_b) * n;
+  // single-reduction pass: gathers r, Ap, p (ideal 24), x rw 16, writes r, p, Ap 24
+  if (opt_.recurrence == 1) info_.bytes_per_iter_model = (double)matrix_bytes + 64.0 * n;
+  if (opt_.recurrence == 1) info_.device_bytes += (size_t)(3 * L_.ext_len - n) * 8;
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
 }
@@ -191,8 +210,17 @@ void GpuCgSolver::reset() {
   MCG_HIP(hipMemsetAsync(p_[0].get(), 0, p_[0].bytes(), s), "device memset failed(p)");
   MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
   // r = b  (CUDACG.cu:248; x0 = 0 so r0 = b - A x0 = b, and p0 = r0 is formed by K_A at k = 0)
-  MCG_HIP(hipMemcpyAsync(r_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
-          "vector copy failed(r)");
+  MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s), "device memset failed");
+  if (opt_.recurrence == 1) {
+    // iteration 0 reads parity-1 buffers: r_{-1} = b, Ap_{-1} = 0, p_{-1} = 0
+    MCG_HIP(hipMemsetAsync(r1_.get(), 0, r1_.bytes(), s), "device memset failed(r)");
+    MCG_HIP(hipMemsetAsync(Ap1_.get(), 0, Ap1_.bytes(), s), "device memset failed(Ap)");
+    MCG_HIP(hipMemcpyAsync(r1_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+            "vector copy failed(r)");
+  } else {
+    MCG_HIP(hipMemcpyAsync(r_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+            "vector copy failed(r)");
+  }
   kern::dot_partials(b_.get(), b_.get(), n, partials_.get(), g_b_, s);
   kern::cg_reduce(partials_.get(), g_b_, st_.get(), kReduceInit, 1, opt_.tol, s);
   if (use_comm_) comm_->allreduce_sum(&st_.get()->rr_new, 1, s);
@@ -210,9 +238,10 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
   if (grid == 0) return;
   const int64_t n = L_.n_local();
   if (opt_.format == 1) {
-    SellDev A{slice_ptr_.get(), cols_.get(), vals_.get(), n};
+    const SellDev A = sell_view();
     kern::cg_spmv_fused_sell(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid, st_.get(),
-                             opt_.tol, first, final_mode, info_.spmv_param, s0_);
+                             opt_.tol, first, final_mode, info_.spmv_param,
+                             (opt_.nt_loads ? 1 : 0) | (opt_.sell_slices == 2 ? 2 : 0) | (d16_ ? 4 : 0), s0_);
   } else if (info_.idx64) {
     CsrDev<int64_t> A{rp64_.get(), cols_.get(), vals_.get(), n};
     kern::cg_spmv_fused<int64_t>(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid,
@@ -226,7 +255,62 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
   }
 }
 
+void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
+  const int first = (k == 0) ? 1 : 0;
+  const int check = (k >= 2) ? 1 : 0;  // the reference never tests r_0
+  const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
+  const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
+  double* part = partials_.get() + (which == 2 ? g_int_ : 0);
+  if (grid == 0) return;
+  const int64_t n = L_.n_local();
+  const bool odd = (k & 1) != 0;
+  DeviceBuffer<double>& r_new = odd ? r1_ : r_;
+  DeviceBuffer<double>& r_old = odd ? r_ : r1_;
+  DeviceBuffer<double>& ap_new = odd ? Ap1_ : Ap_;
+  DeviceBuffer<double>& ap_old = odd ? Ap_ : Ap1_;
+  kern::F1Vectors v{r_old.get(), ap_old.get(), p_[(k + 1) & 1].get(), r_new.get(), ap_new.get(), p_[k & 1].get(),
+                    x_.get()};
+  const SellDev S = sell_view();
+  const int fmt = opt_.format == 1 ? (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1)) : 0;
+  if (info_.idx64)
+    kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,
+                             L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, s0_);
+  else
+    kern::cg_fused1<int32_t>(fmt, info_.spmv_param, CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, S, v,
+                             L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, s0_);
+}
+
+void GpuCgSolver::enqueue_iteration_f1_(int k) {
+  int np = g_all_;
+  if (use_halo_) {
+    const bool odd = (k & 1) != 0;
+    double* vecs[3] = {(odd ? r_ : r1_).get(), (odd ? Ap_ : Ap1_).get(), p_[(k + 1) & 1].get()};
+    if (opt_.overlap) {
+      MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+      MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+      comm_->halo_exchange(L_, vecs, 3, s1_);
+      MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+      enqueue_f1_(k, 1, 0);
+      MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+      enqueue_f1_(k, 2, 0);
+      np = g_int_ + g_bnd_;
+    } else {
+      comm_->halo_exchange(L_, vecs, 3, s0_);
+      enqueue_f1_(k, 0, 0);
+    }
+  } else {
+    enqueue_f1_(k, 0, 0);
+  }
+  CgState* st = st_.get();
+  kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, opt_.tol, s0_);
+  if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
+}
+
 void GpuCgSolver::enqueue_iteration_(int k) {
+  if (opt_.recurrence == 1) {
+    enqueue_iteration_f1_(k);
+    return;
+  }
   const int first = (k == 0) ? 1 : 0;
   double* pold = p_[(k + 1) & 1].get();
   int np = g_all_;
@@ -301,6 +385,14 @@ void GpuCgSolver::run_iterations(int count) {
 
 void GpuCgSolver::finalize() {
   if (k_ == 0) return;
+  if (opt_.recurrence == 1) {
+    // r_m = r_{m-1} - a Ap_{m-1}, x_m = x_{m-1} + a p_{m-1}, exact ||r_m||^2, then latch
+    enqueue_f1_(k_, 0, 1);
+    kern::cg_reduce_f1(partials_.get(), pstride_, g_all_, st_.get(), 1, k_ >= 2 ? 1 : 0, opt_.tol, s0_);
+    if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
+    kern::cg_reduce_f1(partials_.get(), pstride_, 0, st_.get(), 2, 0, opt_.tol, s0_);
+    return;
+  }
   enqueue_spmv_(k_, 0, 1);  // pold = p_{k-1}: the deferred x += alpha p
   kern::cg_reduce(partials_.get(), 0, st_.get(), kReduceFinal, 0, opt_.tol, s0_);
 }
@@ -343,7 +435,7 @@ CgResult GpuCgSolver::result() {
   r.iterations = st.done ? st.conv_iter : st.iter;
   r.converged = st.converged != 0;
   r.breakdown = st.breakdown != 0;
-  r.rnorm = std::sqrt(st.done ? st.rr_final : st.rr_new);
+  r.rnorm = std::sqrt(st.done ? st.rr_final : (opt_.recurrence == 1 ? st.red[3] : st.rr_new));
   r.setup_seconds = setup_seconds_;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, ev_t0_, ev_t1_) == hipSuccess) r.solve_seconds = ms * 1e-3;
@@ -373,7 +465,7 @@ double GpuCgSolver::true_residual_norm() {
     comm_->halo_exchange(L_, v, 1, s);
   }
   if (opt_.format == 1) {
-    kern::spmv_sell(SellDev{slice_ptr_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
+    kern::spmv_sell(sell_view(), xe.get(), y.get(), s);
   } else if (info_.idx64) {
     kern::spmv_csr<int64_t>(CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
   } else {

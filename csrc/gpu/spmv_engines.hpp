@@ -70,6 +70,41 @@ __device__ __forceinline__ void tile_rows(const TileRanges& tr, int64_t t, int64
 __device__ __forceinline__ int64_t imin(int64_t a, int64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
 
+// Work distribution over tiles.  Plain: unit u takes tiles u, u+U, u+2U, ...
+// XCD-aware (tr.xcd = X > 1, grid divisible by X): blocks b and b+X are observed
+// to land on the same XCD, so the blocks with b % X == x sweep a contiguous 1/X
+// of the tiles together; the stencil neighbours of a tile (i +- N rows) are then
+// read by blocks on the same XCD at about the same time and hit that XCD's L2.
+// Speed only: every tile is visited exactly once for any placement.
+struct TileCursor {
+  int64_t t, end, step;
+};
+__device__ __forceinline__ TileCursor tile_cursor(const TileRanges& tr, int64_t sub, int64_t nsub) {
+  const int64_t blk = blockIdx.x, nblk = gridDim.x;
+  TileCursor c;
+  if (tr.xcd > 1 && nblk % tr.xcd == 0) {
+    const int64_t X = tr.xcd, x = blk % X, lb = blk / X, nb = nblk / X;
+    const int64_t per = (tr.ntiles + X - 1) / X;
+    const int64_t start = x * per;
+    c.end = imin(tr.ntiles, start + per);
+    c.t = start + lb * nsub + sub;
+    c.step = nb * nsub;
+  } else {
+    c.t = blk * nsub + sub;
+    c.end = tr.ntiles;
+    c.step = nblk * nsub;
+  }
+  return c;
+}
+
+// matrix streams are read once per SpMV: non-temporal loads keep them from
+// evicting the gathered vectors out of L2 / the Infinity Cache
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // ---------------------------------------------------------------------------
 template <typename IdxT, int U, class Gather, class Epi>
 __device__ __forceinline__ void csr_lds(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather, Epi&& epi) {
@@ -79,9 +114,9 @@ __device__ __forceinline__ void csr_lds(const CsrDev<IdxT>& A, const TileRanges&
   const double* s_v = reinterpret_cast<const double*>(s_v2);
   const int32_t* s_c = reinterpret_cast<const int32_t*>(s_c4);
   const int t = threadIdx.x;
-  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+  for (TileCursor cur = tile_cursor(tr, 0, 1); cur.t < cur.end; cur.t += cur.step) {
     int64_t r0, r1;
-    tile_rows(tr, tile, r0, r1);
+    tile_rows(tr, cur.t, r0, r1);
     const int nr = (int)(r1 - r0);
     if (t < nr) s_rp[t] = (int64_t)A.rowptr[r0 + t];
     if (t == 0) s_rp[nr] = (int64_t)A.rowptr[r0 + nr];
@@ -135,15 +170,15 @@ __device__ __forceinline__ void csr_lds(const CsrDev<IdxT>& A, const TileRanges&
 }
 
 // ---------------------------------------------------------------------------
-template <typename IdxT, int U, class Gather, class Epi>
+template <typename IdxT, int U, bool NT, class Gather, class Epi>
 __device__ __forceinline__ void csr_direct(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather, Epi&& epi) {
   const int t = threadIdx.x;
-  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+  for (TileCursor cur = tile_cursor(tr, 0, 1); cur.t < cur.end; cur.t += cur.step) {
     int64_t r0, r1;
-    tile_rows(tr, tile, r0, r1);
+    tile_rows(tr, cur.t, r0, r1);
     if (r0 + t >= r1) continue;
     const int64_t i = r0 + t;
-    const int64_t rs = (int64_t)A.rowptr[i], re = (int64_t)A.rowptr[i + 1];
+    const int64_t rs = (int64_t)ld<NT>(A.rowptr + i), re = (int64_t)ld<NT>(A.rowptr + i + 1);
     double sum = 0.0;
     for (int64_t j0 = rs; j0 < re; j0 += U) {
       int32_t c[U];
@@ -151,8 +186,8 @@ __device__ __forceinline__ void csr_direct(const CsrDev<IdxT>& A, const TileRang
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t j = imin(j0 + u, re - 1);
-        c[u] = A.cols[j];
-        v[u] = A.vals[j];
+        c[u] = ld<NT>(A.cols + j);
+        v[u] = ld<NT>(A.vals + j);
       }
       double g[U];
 #pragma unroll
@@ -171,9 +206,9 @@ __device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRang
   constexpr int RPP = kBS / G;  // rows per pass; G passes cover a 256-row tile
   __shared__ double s_sum[kBS];
   const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
-  for (int64_t tile = blockIdx.x; tile < tr.ntiles; tile += gridDim.x) {
+  for (TileCursor cur = tile_cursor(tr, 0, 1); cur.t < cur.end; cur.t += cur.step) {
     int64_t r0, r1;
-    tile_rows(tr, tile, r0, r1);
+    tile_rows(tr, cur.t, r0, r1);
     const int nr = (int)(r1 - r0);
     int64_t rs[G], re[G];
 #pragma unroll
@@ -217,16 +252,19 @@ __device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRang
 
 // ---------------------------------------------------------------------------
 // SELL-64: `sr` in slice units; one wave per slice.
-template <int U, class Gather, class Epi>
+// D16: columns stored as int16 offsets from the row's own ext column (SellDev::dcols).
+template <int U, bool NT, bool D16, class Gather, class Epi>
 __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
   const int lane = threadIdx.x & 63;
-  const int64_t wid = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
-  for (int64_t t = wid; t < sr.ntiles; t += nw) {
+  const int64_t w_in_blk = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (TileCursor cur = tile_cursor(sr, w_in_blk, kWaves); cur.t < cur.end; cur.t += cur.step) {
+    const int64_t t = cur.t;
     const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
     const int64_t base = A.slice_ptr[sl];
     const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
     const int32_t* __restrict__ cp = A.cols + base + lane;
+    const int16_t* __restrict__ dp = A.dcols + base + lane;
+    const int32_t rowcol = (int32_t)(A.own_off + sl * 64 + lane);
     const double* __restrict__ vp = A.vals + base + lane;
     double sum = 0.0;
     for (int j0 = 0; j0 < w; j0 += U) {
@@ -235,8 +273,9 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = (j0 + u < w ? j0 + u : w - 1) * 64;
-        c[u] = cp[j];
-        v[u] = vp[j];
+        if constexpr (D16) c[u] = rowcol + (int32_t)ld<NT>(dp + j);
+        else c[u] = ld<NT>(cp + j);
+        v[u] = ld<NT>(vp + j);
       }
       double g[U];
 #pragma unroll
@@ -246,6 +285,57 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
     }
     const int64_t i = sl * 64 + lane;
     if (i < A.n_rows) epi(i, sum);
+  }
+}
+
+// SELL-64, two slices per wave iteration: two independent load -> gather chains
+// in flight per wave (memory-level parallelism without more waves).
+template <int U, bool NT, class Gather, class Epi>
+__device__ __forceinline__ void sell2(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w_in_blk = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  TileCursor cur = tile_cursor(sr, w_in_blk, kWaves);
+  for (; cur.t < cur.end; cur.t += 2 * cur.step) {
+    const int64_t ta = cur.t, tb = cur.t + cur.step;
+    const bool has_b = tb < cur.end;
+    const int64_t sa = ta < sr.nt0 ? sr.b0 + ta : sr.b1 + (ta - sr.nt0);
+    const int64_t sb = has_b ? (tb < sr.nt0 ? sr.b0 + tb : sr.b1 + (tb - sr.nt0)) : sa;
+    const int64_t base_a = A.slice_ptr[sa], base_b = A.slice_ptr[sb];
+    const int wa = (int)((A.slice_ptr[sa + 1] - base_a) >> 6);
+    const int wb = (int)((A.slice_ptr[sb + 1] - base_b) >> 6);
+    const int w = wa > wb ? wa : wb;
+    const int32_t* __restrict__ cpa = A.cols + base_a + lane;
+    const double* __restrict__ vpa = A.vals + base_a + lane;
+    const int32_t* __restrict__ cpb = A.cols + base_b + lane;
+    const double* __restrict__ vpb = A.vals + base_b + lane;
+    double suma = 0.0, sumb = 0.0;
+    for (int j0 = 0; j0 < w; j0 += U) {
+      int32_t ca[U], cb[U];
+      double va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int ja = (j0 + u < wa ? j0 + u : wa - 1) * 64;
+        const int jb = (j0 + u < wb ? j0 + u : wb - 1) * 64;
+        ca[u] = ld<NT>(cpa + ja);
+        va[u] = ld<NT>(vpa + ja);
+        cb[u] = ld<NT>(cpb + jb);
+        vb[u] = ld<NT>(vpb + jb);
+      }
+      double ga[U], gb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ga[u] = gather(ca[u]);
+        gb[u] = gather(cb[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        suma = (j0 + u < wa) ? fma(va[u], ga[u], suma) : suma;
+        sumb = (j0 + u < wb) ? fma(vb[u], gb[u], sumb) : sumb;
+      }
+    }
+    const int64_t ia = sa * 64 + lane, ib = sb * 64 + lane;
+    if (ia < A.n_rows) epi(ia, suma);
+    if (has_b && ib < A.n_rows) epi(ib, sumb);
   }
 }
 

@@ -28,6 +28,10 @@ struct CgOptions {
   int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector; -1 = auto
   int spmv_param = 0;        // batch U (engines 0/1, SELL) or lanes/row G (engine 2); 0 = auto
   int update_unroll = 2;     // double2 loads in flight per lane in the residual update
+  int nt_loads = 0;          // non-temporal loads for the matrix streams (direct CSR / SELL engines)
+  int xcd_map = 0;           // XCD-aware contiguous tile regions for the SpMV grid
+  int sell_slices = 1;       // SELL engine: slices in flight per wave (1 or 2)
+  int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass
 };
 
 struct CgResult {

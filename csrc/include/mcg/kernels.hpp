@@ -31,7 +31,10 @@ struct alignas(64) CgState {
   double rr0;     // b . b
   double rr_final;  // rr_new captured when the latch fires (later no-op all-reduces may clobber rr_new)
   double pad0_[3];
-  int iter;       // completed iterations (SpMVs whose residual update ran)
+  // single-reduction recurrence: {p.Ap, r.Ap, Ap.Ap, r.r} of the last fused pass
+  // (one contiguous 32-B all-reduce slot)
+  double red[4];
+  int iter;      // completed iterations (SpMVs whose residual update ran)
   int done;       // latch: 1 = converged in-loop, 2 = maxit finalised, 3 = breakdown
   int conv_iter;  // iteration count at the latch
   int converged;  // ||r|| < tol at the end
@@ -47,6 +50,8 @@ constexpr int kTileRows = 256;
 struct TileRanges {
   int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
   int64_t nt0 = 0, ntiles = 0;
+  int32_t xcd = 0;  // > 1: XCD-aware contiguous tile regions (see spmv_engines.hpp tile_cursor)
+  int32_t pad_ = 0;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);
@@ -69,6 +74,11 @@ struct SellDev {
   const int32_t* cols;
   const double* vals;
   int64_t n_rows;
+  // SELL-64/d16: 16-bit column offsets relative to the row's own ext column
+  // (col = own_off + row + dcols[k]); used when the matrix bandwidth fits int16.
+  // Index bytes per entry 4 -> 2.
+  const int16_t* dcols = nullptr;
+  int64_t own_off = 0;
 };
 
 namespace kern {
@@ -90,10 +100,11 @@ void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr /*
 template <typename IdxT>
 void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n,
                  int64_t own_off, const int64_t* slice_ptr, int32_t* scols, double* svals,
-                 hipStream_t st);
+                 hipStream_t st, int16_t* dcols = nullptr /* write 16-bit deltas instead of scols */);
 
 // ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
-// variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row);
+// variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row),
+//          3 = direct with non-temporal matrix loads;
 // param: batch size U in {4,6,8} (variants 0/1) or G in {4,8,16} (variant 2)
 template <typename IdxT>
 void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pold_ext,
@@ -106,6 +117,7 @@ void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pol
                         double* pnew_ext, double* x, double* Ap, int64_t own_off,
                         const TileRanges& slices, double* partials, int grid,
                         const CgState* st, double tol, int first, int final_mode, int param,
+                        int flags /* bit0: non-temporal matrix loads, bit1: two slices per wave */,
                         hipStream_t stream);
 void cg_update_r(double* r_own, const double* Ap, int64_t n, double* partials, int grid,
                  const CgState* st, int unroll, hipStream_t stream);
@@ -115,6 +127,29 @@ void dot_partials(const double* a, const double* b, int64_t n, double* partials,
                   hipStream_t stream);
 // scalar[0] = fixed-order sum of partials
 void sum_partials(const double* partials, int np, double* out, hipStream_t stream);
+
+// ---- single-reduction fused CG iteration (csrc/gpu/cg_fused1.hip) ----
+// One streaming pass per iteration k:
+//   r_k = r_{k-1} - a_{k-1} Ap_{k-1};  p_k = r_k + b_{k-1} p_{k-1};  x += a_{k-1} p_{k-1};
+//   Ap_k = A p_k;  partials of {p_k.Ap_k, r_k.Ap_k, Ap_k.Ap_k, r_k.r_k}
+// then ONE reduction (+ one 32-B all-reduce).  a_k = rr_k / pAp_k (exact norms);
+// b_k = rr_{k+1} / rr_k with rr_{k+1} = rr_k - 2 a_k (r_k.Ap_k) + a_k^2 (Ap_k.Ap_k)
+// (an exact expansion of ||r_k - a_k Ap_k||^2 over the actual vectors; convergence is
+// tested on the exact rr_k of the stored residual, as in the reference).
+// `fmt`: 0 CSR direct (param U), 1 SELL-64 (U), 2 SELL-64 two slices/wave (U).
+struct F1Vectors {
+  const double *r_old, *ap_old, *p_old;  // ext layout, iteration k-1
+  double *r_new, *ap_new, *p_new;        // ext layout, iteration k
+  double* x;                             // owned
+};
+template <typename IdxT>
+void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
+               const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
+               int first, int check, int final_mode, hipStream_t stream);
+// modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),
+//        1 = after the final pass (sum rr only), 2 = latch after the final all-reduce
+void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, double tol,
+                  hipStream_t stream);
 
 // ---- unfused ops (ops API / tests) ----
 template <typename IdxT>

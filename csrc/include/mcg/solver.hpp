@@ -45,6 +45,7 @@ struct SolverInfo {
   int grid_a = 0, grid_b = 0;
   int64_t max_row_len = 0;
   int spmv_variant = 0, spmv_param = 0;
+  int recurrence = 0;
 };
 
 class GpuCgSolver {
@@ -75,6 +76,8 @@ class GpuCgSolver {
   template <typename IdxT> void build_csr_(DeviceBuffer<int64_t>& rp64);
   void enqueue_iteration_(int k);
   void enqueue_spmv_(int k, int which, int final_mode);  // which: 0 all, 1 interior, 2 boundary
+  void enqueue_f1_(int k, int which, int final_mode);    // single-reduction fused pass
+  void enqueue_iteration_f1_(int k);
   void capture_pair_();
 
   ProblemSpec spec_;
@@ -95,8 +98,18 @@ class GpuCgSolver {
   DeviceBuffer<int32_t> cols_;
   DeviceBuffer<double> vals_;
   DeviceBuffer<int64_t> slice_ptr_;
+  DeviceBuffer<int16_t> dcols_;  // SELL-64/d16 column offsets
+  bool d16_ = false;
+  SellDev sell_view() const {
+    SellDev s{slice_ptr_.get(), cols_.get(), vals_.get(), L_.n_local()};
+    s.dcols = dcols_.get();
+    s.own_off = L_.own_off;
+    return s;
+  }
   // vectors
   DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
+  DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
+  int pstride_ = 0;                // partial-array stride (4 arrays in the single-reduction form)
   DeviceBuffer<CgState> st_;
   PinnedBuffer<CgState> host_st_;
   // launch geometry

@@ -39,7 +39,7 @@ ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64
 
 CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool use_graph, bool force_comm,
                     const std::string& format, int blocks_per_cu, int spmv_variant, int spmv_param,
-                    int update_unroll) {
+                    int update_unroll, int nt_loads, int xcd_map, int sell_slices, int recurrence) {
   CgOptions o;
   o.maxit = maxit;
   o.tol = tol;
@@ -49,11 +49,16 @@ CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool u
   o.force_comm = force_comm;
   if (format == "csr") o.format = 0;
   else if (format == "sell" || format == "sell64") o.format = 1;
+  else if (format == "sell16" || format == "sell64-d16") o.format = 2;
   else fail("unknown format: " + format);
   o.blocks_per_cu = blocks_per_cu;
   o.spmv_variant = spmv_variant;
   o.spmv_param = spmv_param;
   o.update_unroll = update_unroll;
+  o.nt_loads = nt_loads;
+  o.xcd_map = xcd_map;
+  o.sell_slices = sell_slices;
+  o.recurrence = recurrence;
   return o;
 }
 
@@ -131,7 +136,12 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
            py::arg("format") = "csr", py::arg("blocks_per_cu") = 8, py::arg("spmv_variant") = -1,
-           py::arg("spmv_param") = 0, py::arg("update_unroll") = 2)
+           py::arg("spmv_param") = 0, py::arg("update_unroll") = 2, py::arg("nt_loads") = 0,
+           py::arg("xcd_map") = 0, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
+      .def_readwrite("recurrence", &CgOptions::recurrence)
+      .def_readwrite("sell_slices", &CgOptions::sell_slices)
+      .def_readwrite("nt_loads", &CgOptions::nt_loads)
+      .def_readwrite("xcd_map", &CgOptions::xcd_map)
       .def_readwrite("spmv_variant", &CgOptions::spmv_variant)
       .def_readwrite("spmv_param", &CgOptions::spmv_param)
       .def_readwrite("update_unroll", &CgOptions::update_unroll)
@@ -245,7 +255,8 @@ PYBIND11_MODULE(_C, m) {
         d["halo_out"] = i.halo_out;
         d["interior_rows"] = i.interior_rows;
         d["idx64"] = i.idx64;
-        d["format"] = i.format == 1 ? "sell64" : "csr";
+        d["format"] = i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr");
+        d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;

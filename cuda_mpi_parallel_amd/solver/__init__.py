@@ -22,9 +22,10 @@ from ..models import ProblemSpec, make_problem
 from ..parallel import dist as _dist
 
 
-def _opts(maxit=2000, tol=1e-7, check_every=32, overlap=True, use_graph=True, force_comm=False,
-          format="csr", blocks_per_cu=8):
-    return native().CgOptions(maxit, tol, check_every, overlap, use_graph, force_comm, format, blocks_per_cu)
+def _opts(maxit=2000, tol=1e-7, **kw):
+    """Native CgOptions; keyword names as in csrc/include/mcg/cg.hpp (format, blocks_per_cu,
+    spmv_variant, spmv_param, update_unroll, nt_loads, xcd_map, sell_slices, recurrence, ...)."""
+    return native().CgOptions(maxit=maxit, tol=tol, **kw)
 
 
 class CGSolver:
@@ -32,7 +33,7 @@ class CGSolver:
 
     def __init__(self, spec: ProblemSpec, maxit: int = 2000, tol: float = 1e-7, check_every: int = 32,
                  overlap: bool = True, use_graph: bool = True, format: str = "csr", force_comm: bool = False,
-                 blocks_per_cu: int = 8, env: Optional[_dist.DistEnv] = None, comm=None):
+                 blocks_per_cu: int = 8, env: Optional[_dist.DistEnv] = None, comm=None, **tuning):
         self.spec = spec
         self.env = env or _dist.dist_env()
         _dist.set_device(self.env)
@@ -40,7 +41,8 @@ class CGSolver:
             _dist.init_process_group(self.env)
             comm = _dist.bootstrap_comm(self.env, force=force_comm)
         self.comm = comm
-        self.opts = _opts(maxit, tol, check_every, overlap, use_graph, force_comm, format, blocks_per_cu)
+        self.opts = _opts(maxit, tol, check_every=check_every, overlap=overlap, use_graph=use_graph,
+                          force_comm=force_comm, format=format, blocks_per_cu=blocks_per_cu, **tuning)
         self._s = native().Solver(spec.native(), self.opts, self.env.rank, self.env.world, comm)
         self._s.setup()
 

@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU-box check: each GPU step under its own time limit; stop at the first fault/abort/timeout.
+# GPU-box check: each GPU step under its own time limit; stop at the first failing step
+# (a failed test may be a device fault: nothing more runs on the GPU in this call).
 set -u
 mkdir -p gpurun_out
 step() {  # name timeout cmd...
@@ -9,6 +10,6 @@ step() {  # name timeout cmd...
   local rc=$?
   echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
   tail -5 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "stopping after rc=$rc"; exit $rc; fi
   return 0
 }

@@ -21,7 +21,7 @@ def test_cli_no_args_golden(mcg):
     assert p.stdout == "0.500000\n0.750000\n1.000000\nSuccess\n"
 
 
-@pytest.mark.parametrize("fmt", ["csr", "sell"])
+@pytest.mark.parametrize("fmt", ["csr", "sell", "sell16"])
 @pytest.mark.parametrize("graph", [True, False])
 @pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20)),
                                          ("randspd", dict(rows=20000, band=40, density=0.25))])
@@ -36,6 +36,32 @@ def test_matches_cpu_reference(mcg, fmt, graph, problem, kw):
     np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
     tr = s.true_residual_norm()
     assert tr < 1e-6
+
+
+@pytest.mark.parametrize("fmt,slices", [("csr", 1), ("sell", 1), ("sell", 2), ("sell16", 1)])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20)),
+                                         ("randspd", dict(rows=20000, band=40, density=0.25))])
+def test_single_reduction_matches_cpu(mcg, fmt, slices, problem, kw):
+    spec = mcg.make_problem(problem, **kw)
+    cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions(maxit=2000, tol=1e-7))
+    s = mcg.CGSolver(spec, format=fmt, sell_slices=slices, recurrence=1, check_every=8)
+    out = s.solve()
+    assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    assert out["converged"] == cpu["converged"]
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    assert s.true_residual_norm() < 1e-6
+
+
+def test_single_reduction_demo_and_maxit(mcg):
+    out = mcg.CGSolver(mcg.make_problem("demo"), recurrence=1).solve()
+    assert "".join("%f\n" % v for v in out["x_local"]) == "0.500000\n0.750000\n1.000000\n"
+    assert out["iterations"] == 3 and out["converged"]
+    spec = mcg.make_problem("poisson2d", n=200)
+    cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions(maxit=50, tol=1e-7))
+    out = mcg.CGSolver(spec, maxit=50, recurrence=1, format="sell").solve()
+    assert out["iterations"] == 50 and not out["converged"]
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-8, atol=1e-12)
+    assert abs(out["rnorm"] - cpu["rnorm"]) <= 1e-6 * cpu["rnorm"]
 
 
 def test_fixed_iterations_counter(mcg):
