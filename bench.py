@@ -37,7 +37,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--grid", type=int, default=16384, help="grid edge N (N^2 rows for poisson2d)")
     ap.add_argument("--problem", default="poisson2d")
     ap.add_argument("--format", default="csr", choices=["csr", "sell", "sell16"])
     ap.add_argument("--recurrence", type=int, default=-1, help="0 two-reduction, 1 single-reduction, -1 auto")
@@ -58,7 +58,7 @@ def main() -> int:
         pdist.init_process_group(env, backend="gloo")
     comm = pdist.bootstrap_comm(env)
 
-    spec = mcg.make_problem(args.problem, n=args.n, rhs="random")
+    spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
     C = mcg.native()
     opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
                        use_graph=not args.no_graph, force_comm=False, format=args.format,
@@ -116,9 +116,9 @@ def main() -> int:
             "dtype": "fp64",
             "data": "synthetic (on-device generated 5-pt Poisson matrix, random RHS)",
             "config": {
-                "model": f"{args.problem}_N{args.n}",
+                "model": f"{args.problem}_N{args.grid}",
                 "problem": args.problem,
-                "N": args.n,
+                "N": args.grid,
                 "rows": spec.n_rows,
                 "nnz": spec.nnz,
                 "global_batch": 1,

@@ -149,13 +149,16 @@ __global__ __launch_bounds__(kGenBlock) void k_csr_to_sell(const IdxT* __restric
                                                            double* __restrict__ svals,
                                                            int16_t* __restrict__ dcols) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  const int64_t n_pad = (n + 63) / 64 * 64;  // lanes past the last row of the last slice get padding too
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
     const int64_t sl = i >> 6, l = i & 63;
     const int64_t base = sp[sl], w = (sp[sl + 1] - base) >> 6;
-    const int64_t rs = rp[i], len = (int64_t)rp[i + 1] - rs;
+    const bool row = i < n;
+    const int64_t rs = row ? (int64_t)rp[i] : 0, len = row ? (int64_t)rp[i + 1] - rs : 0;
+    const int64_t own_col = own_off + (row ? i : n - 1);  // a valid ext column for padding gathers
     for (int64_t j = 0; j < w; ++j) {
       const int64_t dst = base + 64 * j + l;
-      const int32_t c = j < len ? cols[rs + j] : (int32_t)(own_off + i);  // padding: own column, value 0
+      const int32_t c = j < len ? cols[rs + j] : (int32_t)own_col;  // padding: valid column, value 0
       if (dcols) dcols[dst] = (int16_t)(c - (own_off + i));
       else scols[dst] = c;
       svals[dst] = j < len ? vals[rs + j] : 0.0;

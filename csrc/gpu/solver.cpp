@@ -13,7 +13,7 @@ namespace {
 constexpr int kCsrBlocksPerCuCap = 6;  // LDS-limited residency of the CSR tile kernel (26.7 KB/block)
 }
 
-GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank, int world, Comm* comm)
+GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank, int world, Communicator* comm)
     : spec_(spec), opt_(opt), rank_(rank), world_(world), comm_(comm) {
   MCG_CHECK(world >= 1 && rank >= 0 && rank < world, "invalid rank/world");
   MCG_CHECK(world == 1 || comm != nullptr, "multi-rank solver needs a communicator");
@@ -26,6 +26,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   if (opt_.recurrence < 0) opt_.recurrence = world_ > 1 ? 1 : 0;  // auto: one all-reduce per iteration when P > 1
   use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
   use_halo_ = use_comm_ && L_.has_halo();
+  if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
   s0_ = Stream(true, 0);
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);

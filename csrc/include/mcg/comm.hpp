@@ -1,25 +1,34 @@
-// RCCL communicator over xGMI (one rank per GPU).
+// Communicators for the distributed CG solver (one rank = one GPU).
 //
 // The reference has no communication at all; the north star
 // (BASELINE.json:5) moves the per-iteration global dot products and the
-// boundary-row halo exchange onto RCCL.  Two communicators are used so the
-// halo (side stream) and the scalar all-reduces (compute stream) can be in
-// flight at the same time without sharing one communicator's FIFO:
+// boundary-row halo exchange onto RCCL over xGMI.
 //
-//   reduce comm : ncclAllReduce(sum, f64) of the 8-byte CG scalars, in place
-//                 on device memory (CgState::pAp / rr_new) — no host round trip
-//   halo comm   : ncclSend/ncclRecv inside ncclGroupStart/End straight from the
-//                 owner's owned block into the receiver's ghost block (the
-//                 LocalLayout plan: contiguous ranges, no packing)
-//
-// Bootstrap needs only the two ncclUniqueIds to reach every rank: the Python
-// layer ships them over the torch.distributed store (torchrun), the native CLI
-// shares them between its per-GPU threads.
+//   Comm (RCCL)   two communicators so the halo (side stream) and the scalar
+//                 all-reduces (compute stream) can be in flight together:
+//                 - reduce comm: ncclAllReduce(sum, f64) of the CG scalars, in place
+//                   on device memory (CgState) — no host round trip
+//                 - halo comm: ncclSend/ncclRecv inside ncclGroupStart/End straight
+//                   from the owner's owned block into the receiver's ghost block
+//                   (LocalLayout plan: contiguous ranges, no packing)
+//                 Bootstrap needs only the two ncclUniqueIds on every rank (the
+//                 Python layer ships them over the torch.distributed store; the
+//                 native CLI shares them between its per-GPU threads).
+//   LocalComm     P ranks as host threads of ONE process sharing ONE device:
+//                 all-reduce = D2D copies into a shared staging area + a fixed-order
+//                 sum kernel; halo = D2D copies from the peer's owned block; stream
+//                 ordering through events exchanged at host barriers.  RCCL refuses
+//                 several ranks on one GPU, so this is how the multi-rank solver
+//                 (partition, halo plan, interior/boundary split, overlap streams,
+//                 collective placement) is exercised on a single MI355X.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -27,28 +36,39 @@
 
 namespace mcg {
 
-std::string unique_id_bytes();                    // ncclGetUniqueId -> 128 raw bytes
+std::string unique_id_bytes();  // ncclGetUniqueId -> 128 raw bytes
 ncclUniqueId unique_id_from_bytes(const std::string& b);
 
-class Comm {
+class Communicator {
+ public:
+  virtual ~Communicator() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  // in-place sum all-reduce of `count` doubles on `stream`
+  virtual void allreduce_sum(double* buf, size_t count, hipStream_t stream) = 0;
+  // exchange the halo rows of every vector in `ext_vecs` (ext layout of `L`)
+  virtual void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) = 0;
+  // poll for asynchronous errors; throws mcg::Error
+  virtual void check_async() {}
+  // whether the solver may capture this communicator's calls into a hipGraph
+  virtual bool graph_capturable() const { return true; }
+};
+
+class Comm final : public Communicator {
  public:
   Comm(int rank, int world, const ncclUniqueId& reduce_id, const ncclUniqueId& halo_id);
-  ~Comm();
+  ~Comm() override;
   Comm(const Comm&) = delete;
   Comm& operator=(const Comm&) = delete;
 
-  int rank() const { return rank_; }
-  int world() const { return world_; }
-
-  // in-place sum all-reduce of `count` doubles on `stream`
-  void allreduce_sum(double* buf, size_t count, hipStream_t stream);
-  // exchange the halo rows of every vector in `ext_vecs` (ext layout of `L`)
-  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream);
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void allreduce_sum(double* buf, size_t count, hipStream_t stream) override;
+  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) override;
+  void check_async() override;
   // generic device-buffer collectives used by gathers / tests
   void allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream);
   void broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream);
-  // poll for asynchronous RCCL errors; throws mcg::Error
-  void check_async();
   void abort();
 
  private:
@@ -56,6 +76,42 @@ class Comm {
   ncclComm_t reduce_ = nullptr;
   ncclComm_t halo_ = nullptr;
   bool aborted_ = false;
+};
+
+// Shared state of P in-process ranks on one device.
+class LocalGroup {
+ public:
+  explicit LocalGroup(int world, size_t max_allreduce = 64);
+  ~LocalGroup();
+  int world() const { return world_; }
+
+ private:
+  friend class LocalComm;
+  void barrier();
+  int world_;
+  size_t max_n_;
+  double* staging_ = nullptr;  // [2 parities][world][max_n]
+  std::vector<hipEvent_t> ev_copy_[2], ev_done_[2], ev_pre_, ev_post_;
+  std::vector<double* const*> halo_vecs_;
+  std::vector<const LocalLayout*> halo_layouts_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  int count_ = 0, gen_ = 0;
+};
+
+class LocalComm final : public Communicator {
+ public:
+  LocalComm(std::shared_ptr<LocalGroup> group, int rank);
+  int rank() const override { return rank_; }
+  int world() const override { return group_->world(); }
+  void allreduce_sum(double* buf, size_t count, hipStream_t stream) override;
+  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) override;
+  bool graph_capturable() const override { return false; }
+
+ private:
+  std::shared_ptr<LocalGroup> group_;
+  int rank_;
+  long calls_ = 0;
 };
 
 }  // namespace mcg

@@ -52,7 +52,7 @@ class GpuCgSolver {
  public:
   // `comm` may be null for a single rank; it is not owned.
   GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank = 0, int world = 1,
-              Comm* comm = nullptr);
+              Communicator* comm = nullptr);
   ~GpuCgSolver();
   GpuCgSolver(const GpuCgSolver&) = delete;
   GpuCgSolver& operator=(const GpuCgSolver&) = delete;
@@ -83,7 +83,7 @@ class GpuCgSolver {
   ProblemSpec spec_;
   CgOptions opt_;
   int rank_, world_;
-  Comm* comm_;
+  Communicator* comm_;
   LocalLayout L_;
   SolverInfo info_;
   bool use_comm_ = false, use_halo_ = false;

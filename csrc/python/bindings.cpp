@@ -15,6 +15,7 @@
 #include "mcg/check.hpp"
 #include "mcg/comm.hpp"
 #include "mcg/kernels.hpp"
+#include "mcg/local_ranks.hpp"
 #include "mcg/partition.hpp"
 #include "mcg/solver.hpp"
 
@@ -110,7 +111,15 @@ hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 PYBIND11_MODULE(_C, m) {
   m.doc() = "mcg: MI355X-native distributed conjugate-gradient runtime (HIP + RCCL)";
 
-  py::register_exception<Error>(m, "MCGError");
+  static py::exception<Error> mcg_error(m, "MCGError");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const Error& e) {
+      const std::string msg = e.detail().empty() ? std::string(e.what()) : std::string(e.what()) + " [" + e.detail() + "]";
+      py::set_error(mcg_error, msg.c_str());
+    }
+  });
 
   py::class_<ProblemSpec>(m, "ProblemSpec")
       .def(py::init(&make_spec), py::arg("problem") = "demo", py::arg("n") = 3, py::arg("rows") = 0,
@@ -266,6 +275,28 @@ PYBIND11_MODULE(_C, m) {
         d["spmv_param"] = i.spmv_param;
         return d;
       });
+
+  m.def("run_local_ranks", [](const ProblemSpec& s, const CgOptions& o, int world, int fixed_iters, bool verify) {
+    LocalRunResult lr;
+    {
+      py::gil_scoped_release rel;
+      lr = run_local_ranks(s, o, world, fixed_iters, verify);
+    }
+    py::list ranks;
+    std::vector<double> x;
+    for (auto& rr : lr.ranks) {
+      py::dict d = result_dict(rr.res);
+      d["row_begin"] = rr.row_begin;
+      d["true_rnorm"] = rr.true_rnorm;
+      ranks.append(d);
+      x.insert(x.end(), rr.x.begin(), rr.x.end());
+    }
+    py::dict out;
+    out["ranks"] = ranks;
+    out["x"] = to_numpy(std::move(x));
+    return out;
+  }, py::arg("spec"), py::arg("opts"), py::arg("world"), py::arg("fixed_iters") = 0, py::arg("verify") = false,
+     "P ranks as threads on the current device with the in-process LocalComm (multi-rank test harness)");
 
   // ---- raw-pointer kernel entry points (ops API) ----
   py::module_ k = m.def_submodule("kernels", "hand-written gfx950 kernels on raw device pointers");
