@@ -39,9 +39,11 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--grid", type=int, default=16384, help="grid edge N (N^2 rows for poisson2d)")
     ap.add_argument("--problem", default="poisson2d")
-    ap.add_argument("--format", default="csr", choices=["csr", "sell", "sell16"])
+    ap.add_argument("--format", default="sell16", choices=["csr", "sell", "sell16"],
+                    help="sparse storage: CSR, SELL-64 or SELL-64 with 16-bit column offsets (default)")
     ap.add_argument("--recurrence", type=int, default=-1, help="0 two-reduction, 1 single-reduction, -1 auto")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="capture iteration pairs into a hipGraph also when N > 1")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--blocks-per-cu", type=int, default=8)
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
@@ -60,8 +62,11 @@ def main() -> int:
 
     spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
     C = mcg.native()
+    # hipGraph replay of iteration pairs at N = 1; at N > 1 the host enqueue runs far ahead of the
+    # ~1 ms iterations anyway, so RCCL-in-graph capture is opt-in (--graph)
+    use_graph = not args.no_graph and (env.world == 1 or args.graph)
     opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
-                       use_graph=not args.no_graph, force_comm=False, format=args.format,
+                       use_graph=use_graph, force_comm=False, format=args.format,
                        blocks_per_cu=args.blocks_per_cu, recurrence=args.recurrence)
     t_setup = time.perf_counter()
     solver = C.Solver(spec.native(), opts, env.rank, env.world, comm)
@@ -125,7 +130,8 @@ def main() -> int:
                 "seq_len": spec.n_rows,
                 "parallelism": f"rowpart{n_gpus}",
                 "format": info["format"],
-                "hipgraph": not args.no_graph,
+                "recurrence": info["recurrence"],
+                "hipgraph": use_graph,
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output (kernel stats + optional PMC runs) into markdown.
+
+  python bench/prof_summary.py --stats gpurun_out/prof/run_kernel_stats.csv \
+      --pmc gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/xxx.md
+"""
+import argparse
+import collections
+import csv
+import re
+
+
+def short(name: str) -> str:
+    m = re.search(r"(k_\w+(<[^>]*>)?)", name)
+    return m.group(1) if m else name[:48]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stats")
+    ap.add_argument("--pmc", nargs="*", default=[])
+    ap.add_argument("--title", default="rocprofv3 summary")
+    a = ap.parse_args()
+    print(f"# {a.title}\n")
+    if a.stats:
+        rows = list(csv.DictReader(open(a.stats)))
+        print("| kernel | calls | avg µs | total ms | % |")
+        print("|---|---|---|---|---|")
+        for r in rows:
+            print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
+                  f"{float(r['TotalDurationNs'])/1e6:.2f} | {float(r['Percentage']):.1f} |")
+        print()
+    if a.pmc:
+        agg = collections.defaultdict(lambda: collections.defaultdict(list))
+        dur = collections.defaultdict(list)
+        for d in a.pmc:
+            for r in csv.DictReader(open(d + "/run_counter_collection.csv")):
+                k = short(r["Kernel_Name"])
+                agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        print("| kernel | median µs | FETCH_SIZE GB | WRITE_SIZE GB | TCC hit % |")
+        print("|---|---|---|---|---|")
+        for k, v in agg.items():
+            if not k.startswith("k_cg") and not k.startswith("k_dot"):
+                continue
+            f = v.get("FETCH_SIZE")
+            w = v.get("WRITE_SIZE")
+            h = v.get("TCC_HIT_sum")
+            m = v.get("TCC_MISS_sum")
+            fs = f"{sum(f)/len(f)/1e6:.3f}" if f else "-"
+            ws = f"{sum(w)/len(w)/1e6:.3f}" if w else "-"
+            hr = f"{100*sum(h)/(sum(h)+sum(m)):.1f}" if h and m else "-"
+            ds = sorted(dur[k])
+            print(f"| `{k}` | {ds[len(ds)//2]:.1f} | {fs} | {ws} | {hr} |")
+        print("\nFETCH_SIZE/WRITE_SIZE are reported in KB by rocprofv3 (shown here as GB). On gfx950 FETCH_SIZE"
+              " reads ~1/2 of the bytes of 16-B/lane streaming loads (MI355X_MICROARCH.md §HBM); compare ratios.")
+
+
+if __name__ == "__main__":
+    main()
