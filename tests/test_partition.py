@@ -1,0 +1,80 @@
+"""1-D row partition and halo plan (csrc/host/partition.cpp) — the data structures the
+RCCL halo exchange is driven by.  Property tests over problems and rank counts."""
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+
+def _layouts(mcg, spec, world):
+    return [mcg.parallel.layout(spec, world, r) for r in range(world)]
+
+
+@settings(max_examples=60, deadline=None)
+@given(problem=st.sampled_from(["poisson2d", "poisson3d", "randspd", "demo"]), n=st.integers(2, 24),
+       world=st.integers(1, 9))
+def test_plan_properties(mcg, problem, n, world):
+    kw = {"poisson2d": dict(n=n), "poisson3d": dict(n=max(2, n // 3)),
+          "randspd": dict(rows=n * 37, band=max(1, n // 2), density=0.4), "demo": {}}[problem]
+    spec = mcg.make_problem(problem, **kw)
+    Ls = _layouts(mcg, spec, world)
+    # partition covers [0, n) contiguously
+    assert Ls[0].row_begin == 0 and Ls[-1].row_end == spec.n_rows
+    for a, b in zip(Ls, Ls[1:]):
+        assert a.row_end == b.row_begin
+    for L in Ls:
+        assert L.own_off % 8 == 0 and L.ext_len >= L.own_off + L.n_local
+        # sends of r to q == recvs of q from r, same ranges in the same order (RCCL matching rule)
+        for q in range(world):
+            s = [(g, c) for (p, g, c) in L.sends if p == q]
+            r = [(g, c) for (p, g, c) in Ls[q].recvs if p == L.rank]
+            assert s == r
+        # every column of every owned row is owned or arrives by exactly one recv
+        cover = np.zeros(spec.n_rows, dtype=int)
+        for (_, g, c) in L.recvs:
+            cover[g:g + c] += 1
+        assert cover.max(initial=0) <= 1
+        nat = spec.native()
+        for i in range(L.row_begin, L.row_end):
+            cols, _ = nat.row(i)
+            local = i - L.row_begin
+            interior = L.interior_begin <= local < L.interior_end
+            for c in cols:
+                owned = L.row_begin <= c < L.row_end
+                assert owned or cover[c] == 1
+                if interior:
+                    assert owned
+                assert 0 <= L.ext_index(c) < L.ext_len
+
+
+def test_stencil_partition_is_line_aligned(mcg):
+    spec = mcg.make_problem("poisson2d", n=16384)
+    offs = mcg.parallel.partition_rows(spec, 8)
+    assert all(o % 16384 == 0 for o in offs)
+    L = mcg.parallel.layout(spec, 8, 3)
+    # neighbours only, one grid line (N rows = 128 KiB of doubles) each way
+    assert sorted(p for p, _, _ in L.recvs) == [2, 4]
+    assert all(c == 16384 for _, _, c in L.recvs + L.sends)
+    assert L.interior_end - L.interior_begin == L.n_local - 2 * 16384
+
+
+def test_3d_partition_plane_aligned(mcg):
+    spec = mcg.make_problem("poisson3d", n=512)
+    offs = mcg.parallel.partition_rows(spec, 8)
+    assert all(o % (512 * 512) == 0 for o in offs)
+    L = mcg.parallel.layout(spec, 8, 0)
+    assert L.recvs == ((1, 64 * 512 * 512, 512 * 512),)
+
+
+def test_more_ranks_than_lines_falls_back_to_rows(mcg):
+    spec = mcg.make_problem("poisson2d", n=4)  # 16 rows, 4 lines
+    offs = mcg.parallel.partition_rows(spec, 8)
+    assert offs[0] == 0 and offs[-1] == 16 and all(b - a == 2 for a, b in zip(offs, offs[1:]))
+
+
+def test_partition_by_weight(C):
+    prefix = np.concatenate([[0], np.cumsum([1] * 50 + [100] * 10)]).tolist()
+    offs = C.partition_by_weight(prefix, 4)
+    w = [prefix[b] - prefix[a] for a, b in zip(offs, offs[1:])]
+    assert offs[0] == 0 and offs[-1] == 60
+    assert max(w) <= 2 * (prefix[-1] / 4)
