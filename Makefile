@@ -19,7 +19,7 @@ TESTBIN   := $(BUILD)/test_host
 COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-function
 HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
 CXXFLAGS  := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -pthread
-LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -pthread
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -pthread -ldl
 
 HIP_SRC   := $(wildcard csrc/gpu/*.hip)
 HOST_SRC  := $(wildcard csrc/host/*.cpp)
@@ -52,7 +52,7 @@ $(CLI): $(CORE_OBJ) $(BUILD)/cli/main.o
 	$(CXX) -o $@ $^ $(LDLIBS)
 
 $(TESTBIN): $(HOST_OBJ:$(BUILD)/gpu/%=) $(BUILD)/tests/test_host.o
-	$(CXX) -o $@ $(filter-out $(BUILD)/gpu/%,$(HOST_OBJ)) $(BUILD)/tests/test_host.o -pthread
+	$(CXX) -o $@ $(filter-out $(BUILD)/gpu/%,$(HOST_OBJ)) $(BUILD)/tests/test_host.o -pthread -ldl
 
 $(BUILD)/tests/test_host.o: tests/native/test_host.cpp $(HEADERS)
 	@mkdir -p $(dir $@)

@@ -50,6 +50,7 @@ struct Args {
   std::string report = "text";
   bool verify = false;
   bool rhs_set = false;
+  std::string resume;  // checkpoint prefix to resume from
 };
 
 [[noreturn]] void usage_error(const std::string& m) { fail("invalid arguments: " + m); }
@@ -91,6 +92,10 @@ Args parse(int argc, char** argv) {
     else if (f == "--nt-loads") a.opt.nt_loads = std::stoi(need(i));
     else if (f == "--xcd-map") a.opt.xcd_map = std::stoi(need(i));
     else if (f == "--sell-slices") a.opt.sell_slices = std::stoi(need(i));
+    else if (f == "--checkpoint") a.opt.checkpoint_path = need(i);
+    else if (f == "--checkpoint-every") a.opt.checkpoint_every = std::stoi(need(i));
+    else if (f == "--resume") a.resume = need(i);
+    else if (f == "--inject-nan-at") a.opt.inject_nan_at = std::stoi(need(i));
     else if (f == "--recurrence") {
       std::string v = need(i);
       a.opt.recurrence = (v == "single" || v == "fused1" || v == "1") ? 1 : 0;
@@ -163,6 +168,9 @@ void run_rank(const Args& a, int rank, int world, const std::string& id_red, con
       solver.finalize();
       out.res = solver.result();
       out.res.solve_seconds = out.bench_seconds;
+    } else if (!a.resume.empty()) {
+      solver.load_checkpoint(a.resume);  // continue from the saved iteration
+      out.res = solver.solve(true);
     } else {
       out.res = solver.solve();
     }

@@ -4,8 +4,11 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
+#include <limits>
 
 #include "mcg/check.hpp"
+#include "mcg/trace.hpp"
 
 namespace mcg {
 
@@ -27,6 +30,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
   use_halo_ = use_comm_ && L_.has_halo();
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
+  if (opt_.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
   s0_ = Stream(true, 0);
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);
@@ -59,6 +63,7 @@ void GpuCgSolver::build_csr_(DeviceBuffer<int64_t>& rp64) {
 }
 
 void GpuCgSolver::setup() {
+  trace::Range tr_("mcg.setup");
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   const int64_t n = L_.n_local();
@@ -89,7 +94,7 @@ void GpuCgSolver::setup() {
                                          : kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
   if (opt_.nt_loads && info_.spmv_variant == 1) info_.spmv_variant = 3;
   info_.nnz_local = nnz;
-  info_.idx64 = nnz >= ((int64_t)1 << 31) - 64;
+  info_.idx64 = nnz >= ((int64_t)1 << 31) - 64 || opt_.force_idx64;
   cols_.allocate(nnz, "A", 8);
   vals_.allocate(nnz, "A", 8);
   if (info_.idx64) build_csr_<int64_t>(rp64); else build_csr_<int32_t>(rp64);
@@ -202,6 +207,7 @@ void GpuCgSolver::setup() {
 }
 
 void GpuCgSolver::reset() {
+  trace::Range tr_("mcg.reset");
   MCG_CHECK(setup_done_, "solver not set up");
   const int64_t n = L_.n_local();
   hipStream_t s = s0_;
@@ -282,6 +288,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
 }
 
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
+  trace::Range tr_("mcg.iteration.single_reduction");
   int np = g_all_;
   if (use_halo_) {
     const bool odd = (k & 1) != 0;
@@ -308,6 +315,7 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
 }
 
 void GpuCgSolver::enqueue_iteration_(int k) {
+  trace::Range tr_("mcg.iteration");
   if (opt_.recurrence == 1) {
     enqueue_iteration_f1_(k);
     return;
@@ -377,11 +385,23 @@ void GpuCgSolver::run_iterations(int count) {
       k_ += 2;
       count -= 2;
     } else {
+      if (k_ == opt_.inject_nan_at) inject_fault_(k_);
       enqueue_iteration_(k_);
       ++k_;
       --count;
     }
   }
+}
+
+// Fault-injection hook: poison the residual entry of this rank's first row
+// with a NaN just before iteration k (the r the iteration reads).  The NaN
+// reaches the global dot products, every rank latches "breakdown" at the same
+// iteration, and the run ends instead of silently iterating on garbage.
+void GpuCgSolver::inject_fault_(int k) {
+  static const double nan = std::numeric_limits<double>::quiet_NaN();
+  if (L_.n_local() == 0 || rank_ != 0) return;
+  double* r = (opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get();
+  MCG_HIP(hipMemcpyAsync(r + L_.own_off, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
 }
 
 void GpuCgSolver::finalize() {
@@ -404,11 +424,13 @@ void GpuCgSolver::synchronize() {
   if (use_comm_) comm_->check_async();
 }
 
-CgResult GpuCgSolver::solve() {
-  reset();
+CgResult GpuCgSolver::solve(bool resume) {
+  trace::Range tr_("mcg.solve");
+  if (!resume) reset();
   MCG_HIP(hipEventRecord(ev_t0_, s0_), "event record failed");
   const int every = std::max(1, opt_.check_every);
   int c = 0;
+  int next_ckpt = opt_.checkpoint_every > 0 ? k_ + opt_.checkpoint_every : -1;
   while (k_ < opt_.maxit) {
     const int chunk = std::min(every, opt_.maxit - k_);
     run_iterations(chunk);
@@ -420,12 +442,90 @@ CgResult GpuCgSolver::solve() {
       if (host_st_[(c - 1) & 1].done) break;
       if (use_comm_) comm_->check_async();
     }
+    if (next_ckpt >= 0 && k_ >= next_ckpt && k_ < opt_.maxit) {
+      save_checkpoint(opt_.checkpoint_path);  // synchronises: a consistent state after k_ iterations
+      next_ckpt = k_ + opt_.checkpoint_every;
+    }
     ++c;
   }
   finalize();
   MCG_HIP(hipEventRecord(ev_t1_, s0_), "event record failed");
   synchronize();
   return result();
+}
+
+// ---- checkpoint / resume ----------------------------------------------------
+namespace {
+constexpr char kCkptMagic[8] = {'M', 'C', 'G', 'C', 'K', 'P', 'T', '1'};
+struct CkptHeader {
+  char magic[8];
+  int32_t rank, world, recurrence, format;
+  int64_t n_local, ext_len, row_begin, k;
+  int64_t n_global;
+  uint64_t seed;
+};
+}  // namespace
+
+void GpuCgSolver::save_checkpoint(const std::string& prefix) {
+  MCG_CHECK(setup_done_, "solver not set up");
+  MCG_CHECK(!prefix.empty(), "checkpoint path not set");
+  synchronize();
+  const std::string path = prefix + ".rank" + std::to_string(rank_);
+  const std::string tmp = path + ".tmp";
+  std::FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) fail("checkpoint write failed", tmp);
+  CkptHeader h{};
+  std::memcpy(h.magic, kCkptMagic, 8);
+  h.rank = rank_;
+  h.world = world_;
+  h.recurrence = opt_.recurrence;
+  h.format = info_.format;
+  h.n_local = L_.n_local();
+  h.ext_len = L_.ext_len;
+  h.row_begin = L_.row_begin;
+  h.k = k_;
+  h.n_global = L_.n_global;
+  h.seed = spec_.seed;
+  bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
+  std::vector<char> host;
+  auto dump = [&](const void* dev, size_t bytes) {
+    if (!ok || bytes == 0) return;
+    host.resize(bytes);
+    MCG_HIP(hipMemcpy(host.data(), dev, bytes, hipMemcpyDeviceToHost), "memcpy from device to host failed(ckpt)");
+    ok = std::fwrite(host.data(), 1, bytes, f) == bytes;
+  };
+  dump(st_.get(), sizeof(CgState));
+  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_}) dump(b->get(), b->bytes());
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) fail("checkpoint write failed", path);
+}
+
+void GpuCgSolver::load_checkpoint(const std::string& prefix) {
+  MCG_CHECK(setup_done_, "solver not set up");
+  const std::string path = prefix + ".rank" + std::to_string(rank_);
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) fail("checkpoint read failed", path);
+  CkptHeader h{};
+  bool ok = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, 8) == 0;
+  ok = ok && h.rank == rank_ && h.world == world_ && h.recurrence == opt_.recurrence && h.format == info_.format &&
+       h.n_local == L_.n_local() && h.ext_len == L_.ext_len && h.row_begin == L_.row_begin &&
+       h.n_global == L_.n_global && h.seed == spec_.seed;
+  if (!ok) {
+    std::fclose(f);
+    fail("checkpoint does not match this problem/layout", path);
+  }
+  std::vector<char> host;
+  auto load = [&](void* dev, size_t bytes) {
+    if (!ok || bytes == 0) return;
+    host.resize(bytes);
+    ok = std::fread(host.data(), 1, bytes, f) == bytes;
+    if (ok) MCG_HIP(hipMemcpy(dev, host.data(), bytes, hipMemcpyHostToDevice), "memcpy from host to device failed(ckpt)");
+  };
+  load(st_.get(), sizeof(CgState));
+  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_}) load(b->get(), b->bytes());
+  std::fclose(f);
+  if (!ok) fail("checkpoint truncated", path);
+  k_ = (int)h.k;
 }
 
 CgResult GpuCgSolver::result() {
@@ -454,6 +554,7 @@ std::vector<double> GpuCgSolver::x_local() {
 }
 
 double GpuCgSolver::true_residual_norm() {
+  trace::Range tr_("mcg.true_residual");
   synchronize();
   const int64_t n = L_.n_local();
   DeviceBuffer<double> xe(L_.ext_len, "x", 8), y(n, "Ap", 8), out(1, "scalar");

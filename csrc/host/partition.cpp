@@ -6,9 +6,44 @@
 
 namespace mcg {
 
+namespace {
+// randspd: nnz-balanced partition from the EXPECTED row lengths per 1024-row
+// density region (the generator draws densities per region, so row lengths vary
+// by up to 7x between regions; exact counting would cost 2W hashes per row).
+RowPartition partition_randspd(const ProblemSpec& s, int world) {
+  const int64_t n = s.rows, W = s.band, R = 1024;
+  const int64_t nreg = (n + R - 1) / R;
+  std::vector<double> q(nreg);
+  for (int64_t g = 0; g < nreg; ++g) q[g] = randspd_density(s, g * R);
+  // prefix of q over rows (region-constant) to average the density of a row window
+  std::vector<double> qpre(nreg + 1, 0.0);
+  for (int64_t g = 0; g < nreg; ++g) qpre[g + 1] = qpre[g] + q[g] * (double)std::min(R, n - g * R);
+  auto qsum_rows = [&](int64_t a, int64_t b) {  // sum of q over rows [a, b)
+    a = std::max<int64_t>(0, a);
+    b = std::min(n, b);
+    if (b <= a) return 0.0;
+    const int64_t ga = a / R, gb = (b - 1) / R;
+    if (ga == gb) return q[ga] * (double)(b - a);
+    return q[ga] * (double)((ga + 1) * R - a) + (qpre[gb] - qpre[ga + 1]) + q[gb] * (double)(b - gb * R);
+  };
+  std::vector<int64_t> prefix(nreg + 1, 0);
+  for (int64_t g = 0; g < nreg; ++g) {
+    const int64_t r0 = g * R, r1 = std::min(n, r0 + R), mid = (r0 + r1) / 2;
+    // pairs {i-d, i} use the density of i-d's region; pairs {i, i+d} that of i's
+    const double left = qsum_rows(mid - W, mid), right = q[g] * (double)std::min(W, n - 1 - mid);
+    prefix[g + 1] = prefix[g] + (int64_t)((double)(r1 - r0) * (1.0 + left + right));
+  }
+  RowPartition pr = partition_by_weight(prefix, world);
+  for (auto& o : pr.offsets) o = std::min(n, o * R);
+  pr.offsets.back() = n;
+  return pr;
+}
+}  // namespace
+
 RowPartition partition_rows(const ProblemSpec& s, int world) {
   MCG_CHECK(world >= 1, "invalid number of ranks");
   const int64_t n = global_rows(s);
+  if (s.kind == ProblemKind::RandomSPD && world > 1 && n / 1024 >= world) return partition_randspd(s, world);
   int64_t g = partition_granule(s);
   if (g < 1 || n / g < world) g = 1;
   const int64_t units = (n + g - 1) / g;

@@ -59,7 +59,11 @@ class GpuCgSolver {
 
   void setup();                     // generate matrix + RHS on device (timed as setup)
   void reset();                     // x = 0, r = b, p = 0, scalars; iteration counter = 0
-  CgResult solve();                 // reset + iterate to tol/maxit with polling + finalise
+  CgResult solve(bool resume = false);  // [reset +] iterate to tol/maxit with polling + finalise
+  // checkpoint / resume of the full iteration state (x, r, p, Ap, device scalars,
+  // iteration counter) of this rank; the file is "<prefix>.rank<r>"
+  void save_checkpoint(const std::string& prefix);
+  void load_checkpoint(const std::string& prefix);
   void run_iterations(int k);       // enqueue k more iterations (benchmark mode), no sync
   void finalize();                  // enqueue the deferred last x update (if not latched)
   void synchronize();
@@ -79,6 +83,7 @@ class GpuCgSolver {
   void enqueue_f1_(int k, int which, int final_mode);    // single-reduction fused pass
   void enqueue_iteration_f1_(int k);
   void capture_pair_();
+  void inject_fault_(int k);
 
   ProblemSpec spec_;
   CgOptions opt_;

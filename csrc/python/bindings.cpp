@@ -148,6 +148,10 @@ PYBIND11_MODULE(_C, m) {
            py::arg("spmv_param") = 0, py::arg("update_unroll") = 2, py::arg("nt_loads") = 0,
            py::arg("xcd_map") = 0, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
+      .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
+      .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
+      .def_readwrite("force_idx64", &CgOptions::force_idx64)
+      .def_readwrite("inject_nan_at", &CgOptions::inject_nan_at)
       .def_readwrite("sell_slices", &CgOptions::sell_slices)
       .def_readwrite("nt_loads", &CgOptions::nt_loads)
       .def_readwrite("xcd_map", &CgOptions::xcd_map)
@@ -236,14 +240,16 @@ PYBIND11_MODULE(_C, m) {
            py::arg("comm") = nullptr, py::keep_alive<1, 6>())
       .def("setup", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.setup(); })
       .def("reset", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.reset(); })
-      .def("solve", [](GpuCgSolver& g) {
+      .def("solve", [](GpuCgSolver& g, bool resume) {
         CgResult r;
         {
           py::gil_scoped_release rel;
-          r = g.solve();
+          r = g.solve(resume);
         }
         return result_dict(r);
-      })
+      }, py::arg("resume") = false)
+      .def("save_checkpoint", [](GpuCgSolver& g, const std::string& p) { py::gil_scoped_release rel; g.save_checkpoint(p); })
+      .def("load_checkpoint", [](GpuCgSolver& g, const std::string& p) { py::gil_scoped_release rel; g.load_checkpoint(p); })
       .def("run_iterations", [](GpuCgSolver& g, int k) { py::gil_scoped_release rel; g.run_iterations(k); })
       .def("finalize", &GpuCgSolver::finalize)
       .def("synchronize", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.synchronize(); })

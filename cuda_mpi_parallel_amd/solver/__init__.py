@@ -25,7 +25,15 @@ from ..parallel import dist as _dist
 def _opts(maxit=2000, tol=1e-7, **kw):
     """Native CgOptions; keyword names as in csrc/include/mcg/cg.hpp (format, blocks_per_cu,
     spmv_variant, spmv_param, update_unroll, nt_loads, xcd_map, sell_slices, recurrence, ...)."""
-    return native().CgOptions(maxit=maxit, tol=tol, **kw)
+    ctor = {"check_every", "overlap", "use_graph", "force_comm", "format", "blocks_per_cu", "spmv_variant",
+            "spmv_param", "update_unroll", "nt_loads", "xcd_map", "sell_slices", "recurrence"}
+    o = native().CgOptions(maxit=maxit, tol=tol, **{k: v for k, v in kw.items() if k in ctor})
+    for k, v in kw.items():
+        if k not in ctor:
+            if not hasattr(o, k):
+                raise TypeError(f"unknown solver option {k!r}")
+            setattr(o, k, v)
+    return o
 
 
 class CGSolver:
@@ -47,8 +55,10 @@ class CGSolver:
         self._s.setup()
 
     # --- solve to tolerance (reference semantics) ---
-    def solve(self) -> Dict:
-        res = self._s.solve()
+    def solve(self, resume: bool = False) -> Dict:
+        """Solve to tol / maxit.  ``resume=True`` continues from the state loaded by
+        :meth:`load_checkpoint` instead of restarting from x0 = 0."""
+        res = self._s.solve(resume)
         res["x_local"] = self._s.x_local()
         res["row_begin"] = self._s.layout["row_begin"]
         return res
@@ -75,6 +85,13 @@ class CGSolver:
 
     def true_residual_norm(self) -> float:
         return self._s.true_residual_norm()
+
+    # --- checkpoint / resume (per-rank files "<prefix>.rank<r>") ---
+    def save_checkpoint(self, prefix: str) -> None:
+        self._s.save_checkpoint(prefix)
+
+    def load_checkpoint(self, prefix: str) -> None:
+        self._s.load_checkpoint(prefix)
 
     @property
     def info(self) -> Dict:

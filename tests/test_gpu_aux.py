@@ -1,0 +1,98 @@
+"""Auxiliary subsystems on the GPU: checkpoint/resume, fault injection / breakdown
+detection, int64 row pointers, race detection (serialised vs. concurrent launch
+order must give bitwise-identical results), roctx tracing."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("recurrence", [0, 1])
+def test_checkpoint_resume_matches_uninterrupted(mcg, tmp_path, recurrence):
+    spec = mcg.make_problem("poisson2d", n=128)
+    full = mcg.CGSolver(spec, recurrence=recurrence, format="sell16", check_every=8).solve()
+    # first leg: stop at maxit=40 with a checkpoint every 16 iterations
+    prefix = str(tmp_path / "ckpt")
+    a = mcg.CGSolver(spec, recurrence=recurrence, format="sell16", check_every=8, maxit=40,
+                     checkpoint_every=16, checkpoint_path=prefix)
+    a.solve()
+    assert os.path.exists(prefix + ".rank0")
+    # second leg: fresh solver (new process state), resume from the last checkpoint
+    b = mcg.CGSolver(spec, recurrence=recurrence, format="sell16", check_every=8)
+    b.load_checkpoint(prefix)
+    out = b.solve(resume=True)
+    assert out["converged"] and out["iterations"] == full["iterations"]
+    np.testing.assert_array_equal(out["x_local"], full["x_local"])
+
+
+def test_checkpoint_rejects_other_problem(mcg, tmp_path):
+    prefix = str(tmp_path / "c")
+    s = mcg.CGSolver(mcg.make_problem("poisson2d", n=64), maxit=5)
+    s.solve()
+    s.save_checkpoint(prefix)
+    t = mcg.CGSolver(mcg.make_problem("poisson2d", n=32))
+    with pytest.raises(Exception, match="does not match"):
+        t.load_checkpoint(prefix)
+
+
+@pytest.mark.parametrize("recurrence", [0, 1])
+def test_fault_injection_latches_breakdown(mcg, recurrence):
+    spec = mcg.make_problem("poisson2d", n=64)
+    out = mcg.CGSolver(spec, recurrence=recurrence, inject_nan_at=5, check_every=4).solve()
+    assert out["breakdown"] and not out["converged"]
+    assert out["iterations"] <= 8
+
+
+def test_int64_row_pointers(mcg):
+    spec = mcg.make_problem("randspd", rows=20000, band=40, density=0.25)
+    a = mcg.CGSolver(spec, format="csr").solve()
+    b = mcg.CGSolver(spec, format="csr", force_idx64=1).solve()
+    assert a["iterations"] == b["iterations"]
+    np.testing.assert_array_equal(a["x_local"], b["x_local"])
+
+
+_RUN = r"""
+import json, sys
+sys.path.insert(0, %r)
+import torch, numpy as np
+import cuda_mpi_parallel_amd as m
+torch.cuda.set_device(0)
+s = m.CGSolver(m.make_problem("poisson2d", n=96), format="sell16", check_every=4, recurrence=%d)
+out = s.solve()
+print(json.dumps({"it": out["iterations"], "x": out["x_local"].tolist()}))
+"""
+
+
+@pytest.mark.parametrize("recurrence", [0, 1])
+def test_serialised_launches_bitwise_identical(mcg, recurrence):
+    """Race detection: AMD_SERIALIZE_KERNEL=3 (+ blocking launches) must not change one bit."""
+    code = _RUN % (ROOT, recurrence)
+    normal = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, AMD_SERIALIZE_KERNEL="3", AMD_SERIALIZE_COPY="3", HIP_LAUNCH_BLOCKING="1")
+    serial = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert normal.returncode == 0, normal.stderr
+    assert serial.returncode == 0, serial.stderr
+    a = json.loads(normal.stdout.strip().splitlines()[-1])
+    b = json.loads(serial.stdout.strip().splitlines()[-1])
+    assert a["it"] == b["it"] and a["x"] == b["x"]
+
+
+def test_run_to_run_bitwise_reproducible(mcg):
+    spec = mcg.make_problem("poisson3d", n=24)
+    a = mcg.CGSolver(spec, format="sell16").solve()
+    b = mcg.CGSolver(spec, format="sell16").solve()
+    np.testing.assert_array_equal(a["x_local"], b["x_local"])
+
+
+def test_roctx_tracing_enabled_run(mcg):
+    code = _RUN % (ROOT, 0)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MCG_TRACE="1"))
+    assert p.returncode == 0, p.stderr
