@@ -58,7 +58,17 @@ $(BUILD)/tests/test_host.o: tests/native/test_host.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
+# host-only sanitizer build of the CPU reference path / partitioner / halo plan tests
+# (GPU sanitizers are not available on this pool: host code only)
+ASAN_SRC  := $(wildcard csrc/host/*.cpp) tests/native/test_host.cpp
+$(BUILD)/test_host_asan: $(ASAN_SRC) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) -O1 -g -std=c++17 -Icsrc/include -fsanitize=address,undefined -fno-omit-frame-pointer \
+	  -fno-sanitize-recover=undefined $(ASAN_SRC) -o $@ -pthread -ldl
+
+asan: $(BUILD)/test_host_asan
+
 clean:
 	rm -rf $(BUILD) $(PYMOD) $(CLI)
 
-.PHONY: all clean
+.PHONY: all clean asan

@@ -63,7 +63,7 @@ def set_device(env: DistEnv) -> int:
     """Bind this process to its GPU (LOCAL_RANK) — like the reference's cudaSetDevice(0)."""
     n = torch.cuda.device_count()
     if n == 0:
-        raise RuntimeError("Device Set failed: no HIP device visible")
+        raise RuntimeError("Device Set failed")  # CUDACG.cu:88-91 wording; no HIP device visible
     dev = env.local_rank % n
     torch.cuda.set_device(dev)
     return dev

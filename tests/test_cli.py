@@ -49,3 +49,11 @@ def test_fixed_iterations_cpu(mcg):
     p = run(mcg, "--device", "cpu", "--problem", "poisson2d", "--n", "64", "--fixed-iters", "17", "--report", "json")
     rep = json.loads(p.stdout.strip().splitlines()[-2])
     assert rep["iterations"] == 17 and not rep["converged"]
+
+
+def test_python_module_cli_cpu_golden(mcg):
+    import sys
+
+    p = subprocess.run([sys.executable, "-m", "cuda_mpi_parallel_amd", "--device", "cpu"], capture_output=True,
+                       text=True, timeout=300, cwd=mcg.repo_root())
+    assert p.returncode == 0 and p.stdout == "0.500000\n0.750000\n1.000000\nSuccess\n"
