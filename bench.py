@@ -45,7 +45,7 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture iteration pairs into a hipGraph also when N > 1")
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--blocks-per-cu", type=int, default=8)
+    ap.add_argument("--blocks-per-cu", type=int, default=0, help="SpMV grid; 0 = auto")
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
     args = ap.parse_args()
 

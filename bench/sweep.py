@@ -21,7 +21,7 @@ import cuda_mpi_parallel_amd as mcg  # noqa: E402
 
 def parse_cfg(s):
     parts = s.split(":")
-    d = {"format": parts[0], "v": -1, "p": 0, "b": 8, "u": 2, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0}
+    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0}
     for q in parts[1:]:
         d[q[0]] = int(q[1:])
     return d
@@ -46,6 +46,7 @@ def main():
             c = parse_cfg(cs)
             o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, use_graph=bool(c["g"]), format=c["format"],
                             blocks_per_cu=c["b"], spmv_variant=c["v"], spmv_param=c["p"], update_unroll=c["u"], nt_loads=c["n"], xcd_map=c["x"], sell_slices=c["s"], recurrence=c["r"])
+            o.update_blocks_per_cu = c.get("B", 0)
             s = C.Solver(spec.native(), o, 0, 1, None)
             s.setup()
             s.reset()

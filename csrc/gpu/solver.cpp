@@ -149,7 +149,7 @@ void GpuCgSolver::setup() {
   kern::gen_rhs(spec_, L_.row_begin, n, b_.get(), s0_);
 
   // ---- launch geometry ----
-  const int bpc = std::max(1, opt_.blocks_per_cu);
+  const int bpc = opt_.blocks_per_cu > 0 ? opt_.blocks_per_cu : (opt_.format == 1 ? 48 : 8);
   auto grid_a = [&](const TileRanges& t) {
     if (t.ntiles == 0) return 0;
     if (opt_.format == 1) return kern::grid_for(t.ntiles * 64, 256, bpc);
@@ -184,7 +184,7 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (opt_.xcd_map) tr_all_.xcd = tr_int_.xcd = tr_bnd_.xcd = 8;
-  g_b_ = kern::grid_for((n + 1) / 2, 256, bpc);
+  g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
   const int np = std::max({g_all_, g_int_ + g_bnd_, g_b_, 1});

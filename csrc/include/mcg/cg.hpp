@@ -24,10 +24,11 @@ struct CgOptions {
   bool use_graph = true;     // capture iteration pairs into a hipGraph
   bool force_comm = false;   // run RCCL collectives even with one rank
   int format = 0;            // 0 = CSR, 1 = SELL-64
-  int blocks_per_cu = 8;     // grid sizing for the streaming kernels
+  int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
   int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector; -1 = auto
   int spmv_param = 0;        // batch U (engines 0/1, SELL) or lanes/row G (engine 2); 0 = auto
-  int update_unroll = 2;     // double2 loads in flight per lane in the residual update
+  int update_unroll = 1;     // double2 loads in flight per lane in the residual update
+  int update_blocks_per_cu = 4;  // grid of the residual update / dot kernels (1024 blocks: best measured)
   int nt_loads = 0;          // non-temporal loads for the matrix streams (direct CSR / SELL engines)
   int xcd_map = 0;           // XCD-aware contiguous tile regions for the SpMV grid
   int sell_slices = 1;       // SELL engine: slices in flight per wave (1 or 2)

@@ -144,13 +144,14 @@ PYBIND11_MODULE(_C, m) {
   py::class_<CgOptions>(m, "CgOptions")
       .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
-           py::arg("format") = "csr", py::arg("blocks_per_cu") = 8, py::arg("spmv_variant") = -1,
-           py::arg("spmv_param") = 0, py::arg("update_unroll") = 2, py::arg("nt_loads") = 0,
+           py::arg("format") = "csr", py::arg("blocks_per_cu") = 0, py::arg("spmv_variant") = -1,
+           py::arg("spmv_param") = 0, py::arg("update_unroll") = 1, py::arg("nt_loads") = 0,
            py::arg("xcd_map") = 0, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
+      .def_readwrite("update_blocks_per_cu", &CgOptions::update_blocks_per_cu)
       .def_readwrite("inject_nan_at", &CgOptions::inject_nan_at)
       .def_readwrite("sell_slices", &CgOptions::sell_slices)
       .def_readwrite("nt_loads", &CgOptions::nt_loads)
