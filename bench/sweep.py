@@ -2,8 +2,9 @@
 """Kernel-variant / launch-geometry sweep on one GPU (one process, configs interleaved
 over rounds so clock drift hits every config alike).
 
-A config is  fmt:vV:pP:bB:uU  (format csr|sell, SpMV engine V, batch/lanes P,
-blocks per CU B, residual-update unroll U), e.g.
+A config is  fmt:vV:pP:bB:uU  (format csr|sell|sell16, SpMV engine V, batch/lanes P,
+blocks per CU B, residual-update unroll U; also nN non-temporal, xX XCD map, sS slices/wave,
+rR recurrence, iI interleaved r/Ap pairs, BN update blocks per CU), e.g.
 
   python bench/sweep.py --n 16384 --steps 30 --cfg csr:v1:p6:b8:u2 csr:v0:p6:b6:u2 sell:v1:p6:b8:u2
 """
@@ -21,7 +22,7 @@ import cuda_mpi_parallel_amd as mcg  # noqa: E402
 
 def parse_cfg(s):
     parts = s.split(":")
-    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0}
+    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0, "i": -1}
     for q in parts[1:]:
         d[q[0]] = int(q[1:])
     return d
@@ -47,6 +48,7 @@ def main():
             o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, use_graph=bool(c["g"]), format=c["format"],
                             blocks_per_cu=c["b"], spmv_variant=c["v"], spmv_param=c["p"], update_unroll=c["u"], nt_loads=c["n"], xcd_map=c["x"], sell_slices=c["s"], recurrence=c["r"])
             o.update_blocks_per_cu = c.get("B", 0)
+            o.interleave = c["i"]
             s = C.Solver(spec.native(), o, 0, 1, None)
             s.setup()
             s.reset()

@@ -10,8 +10,10 @@
 //   --problem demo|poisson2d|poisson3d|randspd   --n N   --rows R --band W --density q
 //   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
 //   --maxit M  --tol T  --check-every K  --fixed-iters K  --warmup W
-//   --format csr|sell  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
-//   --spmv-variant 0|1|2  --spmv-param U|G  --update-unroll 1|2|4
+//   --format csr|sell|sell16  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
+//   --spmv-variant 0|1|2|3  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
+//   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off
+//   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
 //   --print-x auto|yes|no  --report text|json  --verify
 // Multi-GPU runs use one host thread per GPU inside this process (no MPI in
 // this image); the two RCCL unique ids are shared in memory.
@@ -99,6 +101,10 @@ Args parse(int argc, char** argv) {
     else if (f == "--recurrence") {
       std::string v = need(i);
       a.opt.recurrence = (v == "single" || v == "fused1" || v == "1") ? 1 : 0;
+    }
+    else if (f == "--interleave") {
+      std::string v = need(i);
+      a.opt.interleave = v == "auto" ? -1 : ((v == "on" || v == "1") ? 1 : 0);
     }
     else if (f == "--print-x") a.print_x = need(i);
     else if (f == "--report") a.report = need(i);

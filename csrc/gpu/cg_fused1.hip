@@ -71,7 +71,7 @@ __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, 
   }
 }
 
-template <int FMT, typename IdxT, int U>
+template <int FMT, typename IdxT, int U, bool RA>
 __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                double* __restrict__ partials, int pstride,
                                                const CgState* __restrict__ st, double tol, int first, int check,
@@ -87,6 +87,17 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
   double* __restrict__ apn = v.ap_new;
   double* __restrict__ pn = v.p_new;
   double* __restrict__ x = v.x;
+  const double2* __restrict__ rao = v.ra_old;
+  double2* __restrict__ ran = v.ra_new;
+  // r_k = r_{k-1} - a Ap_{k-1} at ext index e (one 16-B load in the interleaved layout)
+  auto r_next = [&](int64_t e) -> double {
+    if constexpr (RA) {
+      const double2 q = rao[e];
+      return fma(na, q.y, q.x);
+    } else {
+      return fma(na, apo[e], ro[e]);
+    }
+  };
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
   if (final_mode) {
     // last iteration's r and x updates only (no SpMV): r_m, x_m, partial ||r_m||^2
@@ -102,8 +113,9 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
       const int64_t i = row0 + lane;
       const int64_t lim = FMT == 0 ? (t < tr.nt0 ? tr.e0 : tr.e1) : n;
       if (i < lim && i < n) {
-        const double rk = fma(na, apo[own + i], ro[own + i]);
-        rn[own + i] = rk;
+        const double rk = r_next(own + i);
+        if constexpr (RA) ran[own + i] = make_double2(rk, 0.0);
+        else rn[own + i] = rk;
         x[i] = fma(a, po[own + i], x[i]);
         s_rr = fma(rk, rk, s_rr);
       }
@@ -111,15 +123,19 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
     block_partial4(0.0, 0.0, 0.0, s_rr, partials, pstride);
     return;
   }
-  auto gather = [&](int32_t c) { return fma(b, po[c], fma(na, apo[c], ro[c])); };
+  auto gather = [&](int32_t c) { return fma(b, po[c], r_next(c)); };
   auto epi = [&](int64_t i, double sum) {
     const int64_t e = own + i;
-    const double rk = fma(na, apo[e], ro[e]);
+    const double rk = r_next(e);
     const double pold = po[e];
     const double pk = fma(b, pold, rk);
-    rn[e] = rk;
+    if constexpr (RA) {
+      ran[e] = make_double2(rk, sum);
+    } else {
+      rn[e] = rk;
+      apn[e] = sum;
+    }
     pn[e] = pk;
-    apn[e] = sum;
     x[i] = fma(a, pold, x[i]);
     s_pap = fma(pk, sum, s_pap);
     s_rap = fma(rk, sum, s_rap);
@@ -194,22 +210,35 @@ __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __rest
   st->iter += 1;
 }
 
+__global__ void k_pack_pairs(const double* __restrict__ a, double2* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = make_double2(a[i], 0.0);
+}
+
 }  // namespace
+
+void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pack_pairs, dim3(grid_for(n, 256, 4)), dim3(256), 0, stream, a, out, n);
+  MCG_HIP(hipGetLastError(), "vector copy failed(r)");
+}
 
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
                int first, int check, int final_mode, hipStream_t stream) {
   if (tr.ntiles == 0 || grid == 0) return;
-#define MCG_F1(F, U)                                                                                              \
-  hipLaunchKernelGGL((k_cg_f1<F, IdxT, U>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, partials, \
-                     pstride, st, tol, first, check, final_mode)
-#define MCG_F1U(F) \
-  do { if (param <= 4) MCG_F1(F, 4); else if (param <= 6) MCG_F1(F, 6); else MCG_F1(F, 8); } while (0)
-  if (fmt == 0) MCG_F1U(0);
-  else if (fmt == 1) MCG_F1U(1);
-  else if (fmt == 2) MCG_F1U(2);
-  else MCG_F1U(3);
+#define MCG_F1(F, U, RA)                                                                                   \
+  hipLaunchKernelGGL((k_cg_f1<F, IdxT, U, RA>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, \
+                     partials, pstride, st, tol, first, check, final_mode)
+#define MCG_F1U(F, RA) \
+  do { if (param <= 4) MCG_F1(F, 4, RA); else if (param <= 6) MCG_F1(F, 6, RA); else MCG_F1(F, 8, RA); } while (0)
+  const bool ra = v.ra_old != nullptr;
+  MCG_CHECK(!ra || fmt == 1 || fmt == 3, "interleaved r/Ap layout needs a SELL format");
+  if (fmt == 0) MCG_F1U(0, false);
+  else if (fmt == 1) { if (ra) MCG_F1U(1, true); else MCG_F1U(1, false); }
+  else if (fmt == 2) MCG_F1U(2, false);
+  else { if (ra) MCG_F1U(3, true); else MCG_F1U(3, false); }
 #undef MCG_F1U
 #undef MCG_F1
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");

@@ -36,18 +36,22 @@ void Comm::allreduce_sum(double* buf, size_t count, hipStream_t stream) {
   MCG_RCCL(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, reduce_, stream), "RCCL allreduce failed");
 }
 
-void Comm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) {
+void Comm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                         const int* widths) {
   if (!L.has_halo()) return;
   MCG_RCCL(ncclGroupStart(), "RCCL group failed");
   // Matching rule: for each (me, peer) pair both sides post their messages in the
   // same order — vector-major, then ascending global row (make_layout builds
   // sends/recvs in ascending order).
   for (int v = 0; v < nvec; ++v) {
+    const int64_t w = widths ? widths[v] : 1;
     for (const HaloRange& h : L.sends)
-      MCG_RCCL(ncclSend(ext_vecs[v] + L.ext_index(h.gbegin), (size_t)h.count, ncclFloat64, h.peer, halo_, stream),
+      MCG_RCCL(ncclSend(ext_vecs[v] + w * L.ext_index(h.gbegin), (size_t)(w * h.count), ncclFloat64, h.peer, halo_,
+                        stream),
                "RCCL halo send failed");
     for (const HaloRange& h : L.recvs)
-      MCG_RCCL(ncclRecv(ext_vecs[v] + L.ext_index(h.gbegin), (size_t)h.count, ncclFloat64, h.peer, halo_, stream),
+      MCG_RCCL(ncclRecv(ext_vecs[v] + w * L.ext_index(h.gbegin), (size_t)(w * h.count), ncclFloat64, h.peer, halo_,
+                        stream),
                "RCCL halo recv failed");
   }
   MCG_RCCL(ncclGroupEnd(), "RCCL group failed");

@@ -89,7 +89,8 @@ void LocalComm::allreduce_sum(double* buf, size_t count, hipStream_t stream) {
   MCG_HIP(hipEventRecord(g.ev_done_[par][rank_], stream), "event record failed");
 }
 
-void LocalComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) {
+void LocalComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                              const int* widths) {
   LocalGroup& g = *group_;
   const int P = g.world_;
   MCG_HIP(hipEventRecord(g.ev_pre_[rank_], stream), "event record failed");
@@ -99,10 +100,13 @@ void LocalComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
   for (const HaloRange& h : L.recvs) {
     MCG_HIP(hipStreamWaitEvent(stream, g.ev_pre_[h.peer], 0), "stream wait failed");
     const LocalLayout& Lp = *g.halo_layouts_[h.peer];
-    for (int v = 0; v < nvec; ++v)
-      MCG_HIP(hipMemcpyAsync(ext_vecs[v] + L.ext_index(h.gbegin), g.halo_vecs_[h.peer][v] + Lp.ext_index(h.gbegin),
-                             h.count * sizeof(double), hipMemcpyDeviceToDevice, stream),
+    for (int v = 0; v < nvec; ++v) {
+      const int64_t w = widths ? widths[v] : 1;
+      MCG_HIP(hipMemcpyAsync(ext_vecs[v] + w * L.ext_index(h.gbegin),
+                             g.halo_vecs_[h.peer][v] + w * Lp.ext_index(h.gbegin), w * h.count * sizeof(double),
+                             hipMemcpyDeviceToDevice, stream),
               "local halo copy failed");
+    }
   }
   MCG_HIP(hipEventRecord(g.ev_post_[rank_], stream), "event record failed");
   g.barrier();

@@ -26,7 +26,14 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
     d16_ = bandwidth(spec_) <= 32767;
     opt_.format = 1;
   }
-  if (opt_.recurrence < 0) opt_.recurrence = world_ > 1 ? 1 : 0;  // auto: one all-reduce per iteration when P > 1
+  // auto: the single-reduction form (one pass, one all-reduce per iteration) when P > 1 or on
+  // SELL, where its interleaved {r, Ap} gathers make it the faster pass (profiles/sweep_ra_*)
+  if (opt_.recurrence < 0) opt_.recurrence = (world_ > 1 || opt_.format == 1) ? 1 : 0;
+  {
+    const bool ra_ok = opt_.recurrence == 1 && opt_.format == 1 && opt_.sell_slices != 2;
+    if (opt_.interleave < 0) opt_.interleave = ra_ok ? 1 : 0;
+    MCG_CHECK(!opt_.interleave || ra_ok, "interleaved r/Ap layout needs the single-reduction recurrence on SELL");
+  }
   use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
   use_halo_ = use_comm_ && L_.has_halo();
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
@@ -75,6 +82,7 @@ void GpuCgSolver::setup() {
   info_.interior_rows = L_.interior_end - L_.interior_begin;
   info_.format = d16_ ? 2 : opt_.format;
   info_.recurrence = opt_.recurrence;
+  info_.interleave = opt_.interleave == 1;
 
   // ---- A: count -> scan -> fill (owned rows, ext-local columns) ----
   DeviceBuffer<int64_t> rp64(n + 1, "A");
@@ -136,12 +144,16 @@ void GpuCgSolver::setup() {
   // ---- vectors ----
   x_.allocate(n, "x", 8);
   b_.allocate(n, "b", 8);
-  r_.allocate(L_.ext_len, "r", 8);
-  if (opt_.recurrence == 1) {  // single-reduction form: r and Ap are gathered -> ext layout, double-buffered
+  if (opt_.interleave == 1) {  // single-reduction form, {r, Ap} pairs, double-buffered by parity
+    ra_[0].allocate(2 * L_.ext_len, "r", 8);
+    ra_[1].allocate(2 * L_.ext_len, "r", 8);
+  } else if (opt_.recurrence == 1) {  // single-reduction form: r and Ap are gathered -> ext layout, double-buffered
+    r_.allocate(L_.ext_len, "r", 8);
     Ap_.allocate(L_.ext_len, "Ap", 8);
     Ap1_.allocate(L_.ext_len, "Ap", 8);
     r1_.allocate(L_.ext_len, "r", 8);
   } else {
+    r_.allocate(L_.ext_len, "r", 8);
     Ap_.allocate(n, "Ap", 8);
   }
   p_[0].allocate(L_.ext_len, "p", 8);
@@ -212,13 +224,16 @@ void GpuCgSolver::reset() {
   const int64_t n = L_.n_local();
   hipStream_t s = s0_;
   MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
-  MCG_HIP(hipMemsetAsync(Ap_.get(), 0, Ap_.bytes(), s), "device memset failed(Ap)");
-  MCG_HIP(hipMemsetAsync(r_.get(), 0, r_.bytes(), s), "device memset failed(r)");
+  for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1]})
+    if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
   MCG_HIP(hipMemsetAsync(p_[0].get(), 0, p_[0].bytes(), s), "device memset failed(p)");
   MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
   // r = b  (CUDACG.cu:248; x0 = 0 so r0 = b - A x0 = b, and p0 = r0 is formed by K_A at k = 0)
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s), "device memset failed");
-  if (opt_.recurrence == 1) {
+  if (opt_.interleave == 1) {
+    // iteration 0 reads the parity-1 pairs: {r_{-1}, Ap_{-1}} = {b, 0}
+    kern::pack_pairs(b_.get(), reinterpret_cast<double2*>(ra_[1].get()) + L_.own_off, n, s);
+  } else if (opt_.recurrence == 1) {
     // iteration 0 reads parity-1 buffers: r_{-1} = b, Ap_{-1} = 0, p_{-1} = 0
     MCG_HIP(hipMemsetAsync(r1_.get(), 0, r1_.bytes(), s), "device memset failed(r)");
     MCG_HIP(hipMemsetAsync(Ap1_.get(), 0, Ap1_.bytes(), s), "device memset failed(Ap)");
@@ -277,6 +292,10 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   DeviceBuffer<double>& ap_old = odd ? Ap_ : Ap1_;
   kern::F1Vectors v{r_old.get(), ap_old.get(), p_[(k + 1) & 1].get(), r_new.get(), ap_new.get(), p_[k & 1].get(),
                     x_.get()};
+  if (opt_.interleave == 1) {
+    v.ra_old = reinterpret_cast<const double2*>(ra_[(k + 1) & 1].get());
+    v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
+  }
   const SellDev S = sell_view();
   const int fmt = opt_.format == 1 ? (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1)) : 0;
   if (info_.idx64)
@@ -293,17 +312,26 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
   if (use_halo_) {
     const bool odd = (k & 1) != 0;
     double* vecs[3] = {(odd ? r_ : r1_).get(), (odd ? Ap_ : Ap1_).get(), p_[(k + 1) & 1].get()};
+    int nv = 3;
+    const int widths[3] = {2, 1, 1};
+    const int* w = nullptr;
+    if (opt_.interleave == 1) {  // {r, Ap} pairs of iteration k-1, then p_{k-1}
+      vecs[0] = ra_[(k + 1) & 1].get();
+      vecs[1] = p_[(k + 1) & 1].get();
+      nv = 2;
+      w = widths;
+    }
     if (opt_.overlap) {
       MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
       MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
-      comm_->halo_exchange(L_, vecs, 3, s1_);
+      comm_->halo_exchange(L_, vecs, nv, s1_, w);
       MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
       enqueue_f1_(k, 1, 0);
       MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
       enqueue_f1_(k, 2, 0);
       np = g_int_ + g_bnd_;
     } else {
-      comm_->halo_exchange(L_, vecs, 3, s0_);
+      comm_->halo_exchange(L_, vecs, nv, s0_, w);
       enqueue_f1_(k, 0, 0);
     }
   } else {
@@ -400,8 +428,9 @@ void GpuCgSolver::run_iterations(int count) {
 void GpuCgSolver::inject_fault_(int k) {
   static const double nan = std::numeric_limits<double>::quiet_NaN();
   if (L_.n_local() == 0 || rank_ != 0) return;
-  double* r = (opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get();
-  MCG_HIP(hipMemcpyAsync(r + L_.own_off, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
+  double* r = opt_.interleave == 1 ? ra_[(k + 1) & 1].get() + 2 * L_.own_off  // .x of the first owned pair
+               : ((opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get()) + L_.own_off;
+  MCG_HIP(hipMemcpyAsync(r, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
 }
 
 void GpuCgSolver::finalize() {
@@ -495,7 +524,8 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
     ok = std::fwrite(host.data(), 1, bytes, f) == bytes;
   };
   dump(st_.get(), sizeof(CgState));
-  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_}) dump(b->get(), b->bytes());
+  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1]})
+    dump(b->get(), b->bytes());
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) fail("checkpoint write failed", path);
 }
@@ -522,7 +552,8 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
     if (ok) MCG_HIP(hipMemcpy(dev, host.data(), bytes, hipMemcpyHostToDevice), "memcpy from host to device failed(ckpt)");
   };
   load(st_.get(), sizeof(CgState));
-  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_}) load(b->get(), b->bytes());
+  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1]})
+    load(b->get(), b->bytes());
   std::fclose(f);
   if (!ok) fail("checkpoint truncated", path);
   k_ = (int)h.k;

@@ -46,8 +46,10 @@ class Communicator {
   virtual int world() const = 0;
   // in-place sum all-reduce of `count` doubles on `stream`
   virtual void allreduce_sum(double* buf, size_t count, hipStream_t stream) = 0;
-  // exchange the halo rows of every vector in `ext_vecs` (ext layout of `L`)
-  virtual void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) = 0;
+  // exchange the halo rows of every vector in `ext_vecs` (ext layout of `L`);
+  // `widths[v]` = doubles per row of vector v (nullptr: all 1; 2 = interleaved pairs)
+  virtual void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                             const int* widths = nullptr) = 0;
   // poll for asynchronous errors; throws mcg::Error
   virtual void check_async() {}
   // whether the solver may capture this communicator's calls into a hipGraph
@@ -64,7 +66,8 @@ class Comm final : public Communicator {
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   void allreduce_sum(double* buf, size_t count, hipStream_t stream) override;
-  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) override;
+  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                     const int* widths = nullptr) override;
   void check_async() override;
   // generic device-buffer collectives used by gathers / tests
   void allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream);
@@ -105,7 +108,8 @@ class LocalComm final : public Communicator {
   int rank() const override { return rank_; }
   int world() const override { return group_->world(); }
   void allreduce_sum(double* buf, size_t count, hipStream_t stream) override;
-  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream) override;
+  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                     const int* widths = nullptr) override;
   bool graph_capturable() const override { return false; }
 
  private:

@@ -141,11 +141,17 @@ struct F1Vectors {
   const double *r_old, *ap_old, *p_old;  // ext layout, iteration k-1
   double *r_new, *ap_new, *p_new;        // ext layout, iteration k
   double* x;                             // owned
+  // interleaved layout: {r, Ap} pairs in one 16-B element per row, so a neighbour
+  // gather is one 16-B load (+ the 8-B p load) instead of three 8-B loads
+  const double2* ra_old = nullptr;
+  double2* ra_new = nullptr;
 };
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
                int first, int check, int final_mode, hipStream_t stream);
+// out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
+void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),
 //        1 = after the final pass (sum rr only), 2 = latch after the final all-reduce
 void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, double tol,

@@ -46,6 +46,7 @@ struct SolverInfo {
   int64_t max_row_len = 0;
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
+  bool interleave = false;
 };
 
 class GpuCgSolver {
@@ -114,6 +115,7 @@ class GpuCgSolver {
   // vectors
   DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
+  DeviceBuffer<double> ra_[2];     // interleaved {r, Ap} pairs by parity (2 * ext_len doubles each)
   int pstride_ = 0;                // partial-array stride (4 arrays in the single-reduction form)
   DeviceBuffer<CgState> st_;
   PinnedBuffer<CgState> host_st_;

@@ -148,6 +148,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("spmv_param") = 0, py::arg("update_unroll") = 1, py::arg("nt_loads") = 0,
            py::arg("xcd_map") = 0, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
+      .def_readwrite("interleave", &CgOptions::interleave)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
@@ -273,6 +274,7 @@ PYBIND11_MODULE(_C, m) {
         d["idx64"] = i.idx64;
         d["format"] = i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr");
         d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
+        d["interleave"] = i.interleave;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;

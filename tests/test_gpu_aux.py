@@ -42,10 +42,10 @@ def test_checkpoint_rejects_other_problem(mcg, tmp_path):
         t.load_checkpoint(prefix)
 
 
-@pytest.mark.parametrize("recurrence", [0, 1])
-def test_fault_injection_latches_breakdown(mcg, recurrence):
+@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "csr"), (1, "sell16")])
+def test_fault_injection_latches_breakdown(mcg, recurrence, fmt):
     spec = mcg.make_problem("poisson2d", n=64)
-    out = mcg.CGSolver(spec, recurrence=recurrence, inject_nan_at=5, check_every=4).solve()
+    out = mcg.CGSolver(spec, recurrence=recurrence, format=fmt, inject_nan_at=5, check_every=4).solve()
     assert out["breakdown"] and not out["converged"]
     assert out["iterations"] <= 8
 

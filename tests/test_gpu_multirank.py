@@ -50,6 +50,20 @@ def test_local_ranks_fixed_iterations_agree_with_single_rank(mcg, recurrence):
     np.testing.assert_allclose(four["x"], one["x"], rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_ranks_interleaved_halo_bitwise(mcg, world):
+    """Halo exchange of the 16-B {r, Ap} pairs (width-2 messages) vs split vectors."""
+    spec = mcg.make_problem("poisson3d", n=16)
+    C = mcg.native()
+    outs = []
+    for il in (1, 0):
+        o = _opts(mcg, format="sell16", recurrence=1, check_every=4)
+        o.interleave = il
+        outs.append(C.run_local_ranks(spec.native(), o, world, 0, True))
+    assert [r["iterations"] for r in outs[0]["ranks"]] == [r["iterations"] for r in outs[1]["ranks"]]
+    np.testing.assert_array_equal(outs[0]["x"], outs[1]["x"])
+
+
 def test_local_ranks_demo_more_ranks_than_rows_per_rank(mcg):
     """3x3 demo on 2 ranks (halo covers most of the matrix) still prints the golden x."""
     C = mcg.native()

@@ -52,6 +52,24 @@ def test_single_reduction_matches_cpu(mcg, fmt, slices, problem, kw):
     assert s.true_residual_norm() < 1e-6
 
 
+@pytest.mark.parametrize("fmt", ["sell", "sell16"])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("randspd", dict(rows=20000, band=40, density=0.25))])
+def test_interleaved_pairs_bitwise_equal_split_vectors(mcg, fmt, problem, kw):
+    """{r, Ap} stored as 16-B pairs vs separate r / Ap arrays: same arithmetic, same bits."""
+    spec = mcg.make_problem(problem, **kw)
+    a = mcg.CGSolver(spec, format=fmt, recurrence=1, interleave=1, check_every=8)
+    b = mcg.CGSolver(spec, format=fmt, recurrence=1, interleave=0, check_every=8)
+    assert a.info["interleave"] and not b.info["interleave"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+
+
+def test_interleave_requires_single_reduction_sell(mcg):
+    with pytest.raises(Exception, match="interleaved"):
+        mcg.CGSolver(mcg.make_problem("poisson2d", n=32), format="csr", recurrence=1, interleave=1)
+
+
 def test_single_reduction_demo_and_maxit(mcg):
     out = mcg.CGSolver(mcg.make_problem("demo"), recurrence=1).solve()
     assert "".join("%f\n" % v for v in out["x_local"]) == "0.500000\n0.750000\n1.000000\n"
