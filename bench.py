@@ -39,8 +39,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--grid", type=int, default=16384, help="grid edge N (N^2 rows for poisson2d)")
     ap.add_argument("--problem", default="poisson2d")
-    ap.add_argument("--format", default="sell16", choices=["csr", "sell", "sell16"],
-                    help="sparse storage: CSR, SELL-64 or SELL-64 with 16-bit column offsets (default)")
+    ap.add_argument("--format", default="sellc8", choices=["csr", "sell", "sell16", "sellc8"],
+                    help="sparse storage: CSR, SELL-64, SELL-64/d16 (16-bit column offsets) or SELL-64/c8 "
+                         "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
     ap.add_argument("--recurrence", type=int, default=-1, help="0 two-reduction, 1 single-reduction, -1 auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture iteration pairs into a hipGraph also when N > 1")

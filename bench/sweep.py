@@ -2,7 +2,7 @@
 """Kernel-variant / launch-geometry sweep on one GPU (one process, configs interleaved
 over rounds so clock drift hits every config alike).
 
-A config is  fmt:vV:pP:bB:uU  (format csr|sell|sell16, SpMV engine V, batch/lanes P,
+A config is  fmt:vV:pP:bB:uU  (format csr|sell|sell16|sellc8, SpMV engine V, batch/lanes P,
 blocks per CU B, residual-update unroll U; also nN non-temporal, xX XCD map, sS slices/wave,
 rR recurrence, iI interleaved r/Ap pairs, BN update blocks per CU), e.g.
 

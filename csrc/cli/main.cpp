@@ -10,7 +10,7 @@
 //   --problem demo|poisson2d|poisson3d|randspd   --n N   --rows R --band W --density q
 //   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
 //   --maxit M  --tol T  --check-every K  --fixed-iters K  --warmup W
-//   --format csr|sell|sell16  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
+//   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
 //   --spmv-variant 0|1|2|3  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
 //   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
@@ -82,7 +82,10 @@ Args parse(int argc, char** argv) {
     else if (f == "--warmup") a.warmup = std::stoi(need(i));
     else if (f == "--format") {
       std::string v = need(i);
-      a.opt.format = (v == "sell" || v == "sell64") ? 1 : ((v == "sell16" || v == "sell64-d16") ? 2 : 0);
+      a.opt.format = (v == "sell" || v == "sell64") ? 1
+                     : (v == "sell16" || v == "sell64-d16") ? 2
+                     : (v == "sellc8" || v == "sell64-c8") ? 3
+                                                            : 0;
     }
     else if (f == "--no-overlap") a.opt.overlap = false;
     else if (f == "--no-graph") a.opt.use_graph = false;
@@ -263,7 +266,11 @@ int main(int argc, char** argv) {
                 "\"true_rnorm\": %.6e, \"setup_s\": %.6f, \"solve_s\": %.6f, \"it_per_s\": %.3f, "
                 "\"device_bytes_rank0\": %zu}\n",
                 problem_name(a.spec).c_str(), (long long)n, (long long)info.nnz_local, world,
-                a.cpu ? "cpu" : "gpu", a.opt.format == 1 ? "sell64" : "csr", res.iterations,
+                a.cpu ? "cpu" : "gpu",
+                a.cpu ? "csr"
+                      : (info.format == 3 ? "sell64-c8"
+                                          : (info.format == 2 ? "sell64-d16" : (info.format == 1 ? "sell64" : "csr"))),
+                res.iterations,
                 res.converged ? "true" : "false", res.breakdown ? "true" : "false", res.rnorm, true_rnorm,
                 res.setup_seconds, res.solve_seconds, itps, info.device_bytes);
   } else if (!want_x || n > 3) {

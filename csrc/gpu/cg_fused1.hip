@@ -143,8 +143,9 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
     s_rr = fma(rk, rk, s_rr);
   };
   if constexpr (FMT == 0) eng::csr_direct<IdxT, U, false>(A, tr, gather, epi);
-  else if constexpr (FMT == 1) eng::sell<U, false, false>(S, tr, gather, epi);
-  else if constexpr (FMT == 3) eng::sell<U, false, true>(S, tr, gather, epi);
+  else if constexpr (FMT == 1) eng::sell<U, false, 0>(S, tr, gather, epi);
+  else if constexpr (FMT == 3) eng::sell<U, false, 1>(S, tr, gather, epi);
+  else if constexpr (FMT == 4) eng::sell<U, false, 2>(S, tr, gather, epi);
   else eng::sell2<U, false>(S, tr, gather, epi);
   block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
 }
@@ -231,14 +232,22 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 #define MCG_F1(F, U, RA)                                                                                   \
   hipLaunchKernelGGL((k_cg_f1<F, IdxT, U, RA>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, \
                      partials, pstride, st, tol, first, check, final_mode)
-#define MCG_F1U(F, RA) \
-  do { if (param <= 4) MCG_F1(F, 4, RA); else if (param <= 6) MCG_F1(F, 6, RA); else MCG_F1(F, 8, RA); } while (0)
+// SELL engines take U = 4..8 (U = the slice width avoids clamped duplicate gathers)
+#define MCG_F1U(F, RA)                                  \
+  do {                                                  \
+    if (param <= 4) MCG_F1(F, 4, RA);                   \
+    else if (param == 5 && F >= 3) MCG_F1(F, 5, RA);    \
+    else if (param <= 6) MCG_F1(F, 6, RA);              \
+    else if (param == 7 && F >= 3) MCG_F1(F, 7, RA);    \
+    else MCG_F1(F, 8, RA);                              \
+  } while (0)
   const bool ra = v.ra_old != nullptr;
-  MCG_CHECK(!ra || fmt == 1 || fmt == 3, "interleaved r/Ap layout needs a SELL format");
+  MCG_CHECK(!ra || fmt == 1 || fmt == 3 || fmt == 4, "interleaved r/Ap layout needs a SELL format");
   if (fmt == 0) MCG_F1U(0, false);
   else if (fmt == 1) { if (ra) MCG_F1U(1, true); else MCG_F1U(1, false); }
   else if (fmt == 2) MCG_F1U(2, false);
-  else { if (ra) MCG_F1U(3, true); else MCG_F1U(3, false); }
+  else if (fmt == 3) { if (ra) MCG_F1U(3, true); else MCG_F1U(3, false); }
+  else { if (ra) MCG_F1U(4, true); else MCG_F1U(4, false); }
 #undef MCG_F1U
 #undef MCG_F1
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");

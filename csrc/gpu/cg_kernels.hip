@@ -117,8 +117,8 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
 }
 
 // K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries).
-// S = 2: two slices in flight per wave; D16: 16-bit column offsets.
-template <int U, int S, bool D16>
+// S = 2: two slices in flight per wave; CM: column mode of eng::sell (0 int32, 1 d16, 2 c8).
+template <int U, int S, int CM>
 __global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const double* __restrict__ r,
                                                             const double* __restrict__ pold,
                                                             double* __restrict__ pnew, double* __restrict__ x,
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const dou
     acc = fma(pi, sum, acc);
   };
   if constexpr (S == 2) eng::sell2<U, false>(A, sr, gather, epi);
-  else eng::sell<U, false, D16>(A, sr, gather, epi);
+  else eng::sell<U, false, CM>(A, sr, gather, epi);
   block_partial<kBS>(acc, s_red, partials + blockIdx.x);
 }
 
@@ -310,11 +310,11 @@ __global__ __launch_bounds__(kBS) void k_spmv_csr(CsrDev<IdxT> A, const double* 
   else eng::csr_direct<IdxT, 8, false>(A, tr, gather, epi);
 }
 
-template <bool D16>
+template <int CM>
 __global__ __launch_bounds__(kBS) void k_spmv_sell(SellDev A, const double* __restrict__ xv,
                                                    double* __restrict__ y) {
   const TileRanges sr = make_tiles_dev((A.n_rows + 63) / 64);
-  eng::sell<8, false, D16>(A, sr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
+  eng::sell<8, false, CM>(A, sr, [&](int32_t c) { return xv[c]; }, [&](int64_t i, double sum) { y[i] = sum; });
 }
 
 __global__ __launch_bounds__(kBS) void k_axpy(double alpha, const double* __restrict__ xv,
@@ -382,17 +382,24 @@ void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pol
   if (slices.ntiles == 0) return;
 #define MCG_SELL(U)                                                                                     \
   do {                                                                                                  \
-    if (flags & 4)                                                                                      \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, true>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,    \
+    if (flags & 8)                                                                                      \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, 2>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
+                         pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
+    else if (flags & 4)                                                                                 \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, 1>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
                          pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
     else if (flags & 2)                                                                                 \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 2, false>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,   \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 2, 0>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
                          pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
     else                                                                                                \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, false>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,   \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, 0>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
                          pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
   } while (0)
-  if (param <= 4) MCG_SELL(4); else if (param <= 6) MCG_SELL(6); else MCG_SELL(8);
+  if (param <= 4) MCG_SELL(4);
+  else if (param == 5) MCG_SELL(5);
+  else if (param <= 6) MCG_SELL(6);
+  else if (param == 7) MCG_SELL(7);
+  else MCG_SELL(8);
 #undef MCG_SELL
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
@@ -442,10 +449,12 @@ void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream)
   const int64_t ns = (A.n_rows + 63) / 64;
   if (ns == 0) return;
   const int grid = grid_for(ns * 64, kBS, 8);
-  if (A.dcols)
-    hipLaunchKernelGGL(k_spmv_sell<true>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+  if (A.codes)
+    hipLaunchKernelGGL(k_spmv_sell<2>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+  else if (A.dcols)
+    hipLaunchKernelGGL(k_spmv_sell<1>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
   else
-    hipLaunchKernelGGL(k_spmv_sell<false>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+    hipLaunchKernelGGL(k_spmv_sell<0>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 

@@ -22,8 +22,9 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   MCG_CHECK(world == 1 || comm != nullptr, "multi-rank solver needs a communicator");
   RowPartition part = partition_rows(spec_, world_);
   L_ = make_layout(spec_, part, rank_);
-  if (opt_.format == 2) {  // SELL-64 with 16-bit column offsets, if the bandwidth fits int16
+  if (opt_.format == 2 || opt_.format == 3) {  // SELL-64 with 16-bit column offsets, if the bandwidth fits int16
     d16_ = bandwidth(spec_) <= 32767;
+    c8_ = opt_.format == 3;  // dictionary codes: decided in setup() from the actual entries (fallback d16)
     opt_.format = 1;
   }
   // auto: the single-reduction form (one pass, one all-reduce per iteration) when P > 1 or on
@@ -100,6 +101,9 @@ void GpuCgSolver::setup() {
   info_.spmv_variant = opt_.spmv_variant >= 0 ? opt_.spmv_variant : (info_.max_row_len > 16 ? 2 : 1);
   info_.spmv_param = opt_.spmv_param > 0 ? opt_.spmv_param
                                          : kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
+  // SELL: one batch = the slice width when it is 4..8 (no clamped duplicate gathers)
+  if (opt_.format == 1 && opt_.spmv_param <= 0)
+    info_.spmv_param = (int)std::max<int64_t>(4, std::min<int64_t>(8, info_.max_row_len));
   if (opt_.nt_loads && info_.spmv_variant == 1) info_.spmv_variant = 3;
   info_.nnz_local = nnz;
   info_.idx64 = nnz >= ((int64_t)1 << 31) - 64 || opt_.force_idx64;
@@ -120,21 +124,49 @@ void GpuCgSolver::setup() {
     MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
     MCG_HIP(hipMemcpy(&total, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
             "memcpy from device to host failed(A)");
-    DeviceBuffer<int32_t> scols(d16_ ? 0 : total, "A", 8);
-    DeviceBuffer<double> svals(total, "A", 8);
-    if (d16_) dcols_.allocate(total, "A", 16);
-    if (info_.idx64)
-      kern::csr_to_sell<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                 scols.get(), svals.get(), s0_, dcols_.get());
-    else
-      kern::csr_to_sell<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                 scols.get(), svals.get(), s0_, dcols_.get());
-    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
-    cols_ = std::move(scols);
-    vals_ = std::move(svals);
+    if (c8_) {  // SELL-64/c8 when the (value, offset) dictionary fits one byte
+      std::vector<double2> dict;
+      int nv = 0, nd = 0;
+      c8_ = info_.idx64 ? kern::sell_dict_build<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, dict,
+                                                          nv, nd, s0_)
+                        : kern::sell_dict_build<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, dict,
+                                                          nv, nd, s0_);
+      if (c8_) {
+        ndict_ = (int)dict.size();
+        dict_.allocate(dict.size(), "A");
+        MCG_HIP(hipMemcpy(dict_.get(), dict.data(), dict.size() * sizeof(double2), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(A)");
+        codes_.allocate(total, "A", 64);
+        if (info_.idx64)
+          kern::csr_to_sell_c8<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
+                                        dict_.get(), nv, nd, codes_.get(), s0_);
+        else
+          kern::csr_to_sell_c8<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
+                                        dict_.get(), nv, nd, codes_.get(), s0_);
+        MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+        cols_.release();
+        vals_.release();
+        info_.format = 3;
+        matrix_bytes = total + (ns + 1) * 8;
+      }
+    }
+    if (!c8_) {
+      DeviceBuffer<int32_t> scols(d16_ ? 0 : total, "A", 8);
+      DeviceBuffer<double> svals(total, "A", 8);
+      if (d16_) dcols_.allocate(total, "A", 16);
+      if (info_.idx64)
+        kern::csr_to_sell<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
+                                   scols.get(), svals.get(), s0_, dcols_.get());
+      else
+        kern::csr_to_sell<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
+                                   scols.get(), svals.get(), s0_, dcols_.get());
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+      cols_ = std::move(scols);
+      vals_ = std::move(svals);
+      matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
+    }
     rp32_.release();
     stored_entries = total;
-    matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
   } else {
     matrix_bytes = nnz * 12 + (n + 1) * (info_.idx64 ? 8 : 4);
     if (info_.idx64) rp64_ = std::move(rp64);
@@ -263,7 +295,9 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
     const SellDev A = sell_view();
     kern::cg_spmv_fused_sell(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid, st_.get(),
                              opt_.tol, first, final_mode, info_.spmv_param,
-                             (opt_.nt_loads ? 1 : 0) | (opt_.sell_slices == 2 ? 2 : 0) | (d16_ ? 4 : 0), s0_);
+                             (opt_.nt_loads ? 1 : 0) | (opt_.sell_slices == 2 ? 2 : 0) | (d16_ ? 4 : 0) |
+                                 (c8_ ? 8 : 0),
+                             s0_);
   } else if (info_.idx64) {
     CsrDev<int64_t> A{rp64_.get(), cols_.get(), vals_.get(), n};
     kern::cg_spmv_fused<int64_t>(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid,
@@ -297,7 +331,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
   }
   const SellDev S = sell_view();
-  const int fmt = opt_.format == 1 ? (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1)) : 0;
+  const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1))) : 0;
   if (info_.idx64)
     kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,
                              L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, s0_);

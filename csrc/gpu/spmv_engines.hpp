@@ -252,10 +252,18 @@ __device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRang
 
 // ---------------------------------------------------------------------------
 // SELL-64: `sr` in slice units; one wave per slice.
-// D16: columns stored as int16 offsets from the row's own ext column (SellDev::dcols).
-template <int U, bool NT, bool D16, class Gather, class Epi>
+// CM (column mode): 0 int32 ext columns, 1 int16 offsets from the row's own ext
+// column (SellDev::dcols), 2 one-byte dictionary codes (SellDev::codes) looked up
+// in an LDS copy of the {value, offset} table — every lane of a stencil slice reads
+// the same code at entry j, so the LDS read is a broadcast.
+template <int U, bool NT, int CM, class Gather, class Epi>
 __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
   const int lane = threadIdx.x & 63;
+  __shared__ double2 s_dict[CM == 2 ? 256 : 1];
+  if constexpr (CM == 2) {
+    for (int k = threadIdx.x; k < A.ndict; k += kBS) s_dict[k] = A.dict[k];
+    __syncthreads();
+  }
   const int64_t w_in_blk = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   for (TileCursor cur = tile_cursor(sr, w_in_blk, kWaves); cur.t < cur.end; cur.t += cur.step) {
     const int64_t t = cur.t;
@@ -264,6 +272,7 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
     const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
     const int32_t* __restrict__ cp = A.cols + base + lane;
     const int16_t* __restrict__ dp = A.dcols + base + lane;
+    const uint8_t* __restrict__ kp = A.codes + base + lane;
     const int32_t rowcol = (int32_t)(A.own_off + sl * 64 + lane);
     const double* __restrict__ vp = A.vals + base + lane;
     double sum = 0.0;
@@ -273,9 +282,15 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = (j0 + u < w ? j0 + u : w - 1) * 64;
-        if constexpr (D16) c[u] = rowcol + (int32_t)ld<NT>(dp + j);
-        else c[u] = ld<NT>(cp + j);
-        v[u] = ld<NT>(vp + j);
+        if constexpr (CM == 2) {
+          const double2 q = s_dict[ld<NT>(kp + j)];
+          c[u] = rowcol + (int32_t)__double_as_longlong(q.y);
+          v[u] = q.x;
+        } else {
+          if constexpr (CM == 1) c[u] = rowcol + (int32_t)ld<NT>(dp + j);
+          else c[u] = ld<NT>(cp + j);
+          v[u] = ld<NT>(vp + j);
+        }
       }
       double g[U];
 #pragma unroll

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "mcg/problem.hpp"
 
@@ -79,6 +80,12 @@ struct SellDev {
   // Index bytes per entry 4 -> 2.
   const int16_t* dcols = nullptr;
   int64_t own_off = 0;
+  // SELL-64/c8 (csrc/gpu/dict.hip): one byte per entry indexing `dict`, pairs
+  // {value, int64 column offset bits}; used when the matrix has <= 256 distinct
+  // (value, offset) combinations.  Index + value bytes per entry 10 -> 1.
+  const uint8_t* codes = nullptr;
+  const double2* dict = nullptr;
+  int32_t ndict = 0;
 };
 
 namespace kern {
@@ -102,6 +109,15 @@ void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, in
                  int64_t own_off, const int64_t* slice_ptr, int32_t* scols, double* svals,
                  hipStream_t st, int16_t* dcols = nullptr /* write 16-bit deltas instead of scols */);
 
+// SELL-64/c8 dictionary (csrc/gpu/dict.hip): false if the matrix has too many distinct
+// values / offsets (or an offset outside int16).  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
+template <typename IdxT>
+bool sell_dict_build(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
+                     std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
+template <typename IdxT>
+void csr_to_sell_c8(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
+                    const int64_t* slice_ptr, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st);
+
 // ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
 // variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row),
 //          3 = direct with non-temporal matrix loads;
@@ -117,7 +133,8 @@ void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pol
                         double* pnew_ext, double* x, double* Ap, int64_t own_off,
                         const TileRanges& slices, double* partials, int grid,
                         const CgState* st, double tol, int first, int final_mode, int param,
-                        int flags /* bit0: non-temporal matrix loads, bit1: two slices per wave */,
+                        int flags /* bit0: non-temporal matrix loads, bit1: two slices per wave,
+                                     bit2: d16 column offsets, bit3: c8 dictionary codes */,
                         hipStream_t stream);
 void cg_update_r(double* r_own, const double* Ap, int64_t n, double* partials, int grid,
                  const CgState* st, int unroll, hipStream_t stream);
@@ -136,7 +153,8 @@ void sum_partials(const double* partials, int np, double* out, hipStream_t strea
 // b_k = rr_{k+1} / rr_k with rr_{k+1} = rr_k - 2 a_k (r_k.Ap_k) + a_k^2 (Ap_k.Ap_k)
 // (an exact expansion of ||r_k - a_k Ap_k||^2 over the actual vectors; convergence is
 // tested on the exact rr_k of the stored residual, as in the reference).
-// `fmt`: 0 CSR direct (param U), 1 SELL-64 (U), 2 SELL-64 two slices/wave (U).
+// `fmt`: 0 CSR direct (param U), 1 SELL-64 (U), 2 SELL-64 two slices/wave (U), 3 SELL-64/d16,
+// 4 SELL-64/c8.
 struct F1Vectors {
   const double *r_old, *ap_old, *p_old;  // ext layout, iteration k-1
   double *r_new, *ap_new, *p_new;        // ext layout, iteration k

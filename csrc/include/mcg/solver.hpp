@@ -106,10 +106,17 @@ class GpuCgSolver {
   DeviceBuffer<int64_t> slice_ptr_;
   DeviceBuffer<int16_t> dcols_;  // SELL-64/d16 column offsets
   bool d16_ = false;
+  DeviceBuffer<uint8_t> codes_;  // SELL-64/c8 dictionary codes
+  DeviceBuffer<double2> dict_;
+  int ndict_ = 0;
+  bool c8_ = false;
   SellDev sell_view() const {
     SellDev s{slice_ptr_.get(), cols_.get(), vals_.get(), L_.n_local()};
     s.dcols = dcols_.get();
     s.own_off = L_.own_off;
+    s.codes = codes_.get();
+    s.dict = dict_.get();
+    s.ndict = ndict_;
     return s;
   }
   // vectors

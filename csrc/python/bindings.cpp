@@ -51,6 +51,7 @@ CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool u
   if (format == "csr") o.format = 0;
   else if (format == "sell" || format == "sell64") o.format = 1;
   else if (format == "sell16" || format == "sell64-d16") o.format = 2;
+  else if (format == "sellc8" || format == "sell64-c8") o.format = 3;
   else fail("unknown format: " + format);
   o.blocks_per_cu = blocks_per_cu;
   o.spmv_variant = spmv_variant;
@@ -272,7 +273,7 @@ PYBIND11_MODULE(_C, m) {
         d["halo_out"] = i.halo_out;
         d["interior_rows"] = i.interior_rows;
         d["idx64"] = i.idx64;
-        d["format"] = i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr");
+        d["format"] = i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
         d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["interleave"] = i.interleave;
         d["device_bytes"] = i.device_bytes;

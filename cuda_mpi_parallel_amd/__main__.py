@@ -27,7 +27,7 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--maxit", type=int, default=2000)
     ap.add_argument("--tol", type=float, default=1e-7)
     ap.add_argument("--check-every", type=int, default=32)
-    ap.add_argument("--format", default="csr", choices=["csr", "sell", "sell16"])
+    ap.add_argument("--format", default="csr", choices=["csr", "sell", "sell16", "sellc8"])
     ap.add_argument("--recurrence", type=int, default=-1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")

@@ -18,7 +18,7 @@ def _opts(mcg, **kw):
 
 @pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("recurrence", [0, 1])
-@pytest.mark.parametrize("fmt,overlap", [("csr", True), ("sell16", True), ("sell", False)])
+@pytest.mark.parametrize("fmt,overlap", [("csr", True), ("sell16", True), ("sell", False), ("sellc8", True)])
 @pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=64)), ("poisson3d", dict(n=16)),
                                          ("randspd", dict(rows=6000, band=30, density=0.3))])
 def test_local_ranks_match_cpu(mcg, world, recurrence, fmt, overlap, problem, kw):

@@ -21,7 +21,7 @@ def test_cli_no_args_golden(mcg):
     assert p.stdout == "0.500000\n0.750000\n1.000000\nSuccess\n"
 
 
-@pytest.mark.parametrize("fmt", ["csr", "sell", "sell16"])
+@pytest.mark.parametrize("fmt", ["csr", "sell", "sell16", "sellc8"])
 @pytest.mark.parametrize("graph", [True, False])
 @pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20)),
                                          ("randspd", dict(rows=20000, band=40, density=0.25))])
@@ -38,7 +38,7 @@ def test_matches_cpu_reference(mcg, fmt, graph, problem, kw):
     assert tr < 1e-6
 
 
-@pytest.mark.parametrize("fmt,slices", [("csr", 1), ("sell", 1), ("sell", 2), ("sell16", 1)])
+@pytest.mark.parametrize("fmt,slices", [("csr", 1), ("sell", 1), ("sell", 2), ("sell16", 1), ("sellc8", 1)])
 @pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20)),
                                          ("randspd", dict(rows=20000, band=40, density=0.25))])
 def test_single_reduction_matches_cpu(mcg, fmt, slices, problem, kw):
@@ -63,6 +63,24 @@ def test_interleaved_pairs_bitwise_equal_split_vectors(mcg, fmt, problem, kw):
     ra, rb = a.solve(), b.solve()
     assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
     np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+
+
+@pytest.mark.parametrize("recurrence", [0, 1])
+@pytest.mark.parametrize("problem,kw,plain,expect", [("poisson2d", dict(n=96), "sell16", "sell64-c8"),
+                                                    ("poisson3d", dict(n=20), "sell", "sell64-c8"),
+                                                    ("randspd", dict(rows=20000, band=40, density=0.25), "sell16",
+                                                     "sell64-d16")])
+def test_dictionary_codes_bitwise_equal_plain_sell(mcg, recurrence, problem, kw, plain, expect):
+    """SELL-64/c8 stores the same entries in the same slot order as SELL-64(/d16): same bits out.
+    Matrices with too many distinct (value, offset) pairs fall back to d16."""
+    spec = mcg.make_problem(problem, **kw)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=recurrence, check_every=8)
+    b = mcg.CGSolver(spec, format=plain, recurrence=recurrence, check_every=8)
+    assert a.info["format"] == expect
+    ra, rb = a.solve(), b.solve()
+    assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+    assert a.true_residual_norm() == b.true_residual_norm()
 
 
 def test_interleave_requires_single_reduction_sell(mcg):
