@@ -64,6 +64,18 @@ def test_local_ranks_interleaved_halo_bitwise(mcg, world):
     np.testing.assert_array_equal(outs[0]["x"], outs[1]["x"])
 
 
+@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "sellc8"), (1, "sell16")])
+def test_local_ranks_dense_halo_full_replica(mcg, recurrence, fmt):
+    """band >= rows: each rank gathers every other rank's rows (all-gather-shaped halo)."""
+    spec = mcg.make_problem("randspd", rows=3000, band=3000, density=0.01)
+    C = mcg.native()
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=1e-7))
+    out = C.run_local_ranks(spec.native(), _opts(mcg, format=fmt, recurrence=recurrence, check_every=4), 3, 0, True)
+    assert abs(out["ranks"][0]["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
+
+
 def test_local_ranks_demo_more_ranks_than_rows_per_rank(mcg):
     """3x3 demo on 2 ranks (halo covers most of the matrix) still prints the golden x."""
     C = mcg.native()
