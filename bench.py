@@ -38,7 +38,10 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--grid", type=int, default=16384, help="grid edge N (N^2 rows for poisson2d)")
-    ap.add_argument("--problem", default="poisson2d")
+    ap.add_argument("--problem", default="poisson2d", choices=["poisson2d", "poisson3d", "randspd"])
+    ap.add_argument("--rows", type=int, default=100_000_000, help="randspd: global rows")
+    ap.add_argument("--band", type=int, default=4096, help="randspd: half bandwidth")
+    ap.add_argument("--density", type=float, default=0.16, help="randspd: candidate-pair density")
     ap.add_argument("--format", default="sellc8", choices=["csr", "sell", "sell16", "sellc8"],
                     help="sparse storage: CSR, SELL-64, SELL-64/d16 (16-bit column offsets) or SELL-64/c8 "
                          "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
@@ -61,7 +64,10 @@ def main() -> int:
         pdist.init_process_group(env, backend="gloo")
     comm = pdist.bootstrap_comm(env)
 
-    spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
+    if args.problem == "randspd":
+        spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, rhs="random")
+    else:
+        spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
     C = mcg.native()
     # hipGraph replay of iteration pairs at N = 1; at N > 1 the host enqueue runs far ahead of the
     # ~1 ms iterations anyway, so RCCL-in-graph capture is opt-in (--graph)
@@ -107,9 +113,18 @@ def main() -> int:
         ok = ok and abs(tr - res["rnorm"]) <= 1e-2 * max(tr, 1e-300) + 1e-9
     info = solver.info
     value = args.steps / dt
+    nnz = spec.nnz
+    if nnz is None:  # randspd: no closed form; sum the ranks' generated counts
+        t = torch.tensor([info["nnz_local"]], dtype=torch.int64)
+        if env.world > 1:
+            dist.all_reduce(t)
+        nnz = int(t.item())
+    headline = args.problem == "poisson2d" and args.grid == 16384
+    model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" if args.problem == "randspd"
+             else f"{args.problem}_N{args.grid}")
     if env.rank == 0:
         print(json.dumps({
-            "metric": METRIC,
+            "metric": METRIC if headline else "CG iterations/sec (whole node), %s" % model,
             "value": round(value, 4),
             "unit": "iterations/s",
             "n_gpus": n_gpus,
@@ -118,15 +133,16 @@ def main() -> int:
             "ms_per_step": round(1e3 * dt / args.steps, 5),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(value / BASELINE_IT_PER_S, 4),
+            "vs_baseline": round(value / BASELINE_IT_PER_S, 4) if headline else None,
             "dtype": "fp64",
-            "data": "synthetic (on-device generated 5-pt Poisson matrix, random RHS)",
+            "data": "synthetic (on-device generated %s matrix, random RHS)" % {
+                "poisson2d": "5-pt Poisson", "poisson3d": "7-pt Poisson", "randspd": "random SPD banded"}[args.problem],
             "config": {
-                "model": f"{args.problem}_N{args.grid}",
+                "model": model,
                 "problem": args.problem,
                 "N": args.grid,
                 "rows": spec.n_rows,
-                "nnz": spec.nnz,
+                "nnz": nnz,
                 "global_batch": 1,
                 "seq_len": spec.n_rows,
                 "parallelism": f"rowpart{n_gpus}",

@@ -4,7 +4,7 @@ over rounds so clock drift hits every config alike).
 
 A config is  fmt:vV:pP:bB:uU  (format csr|sell|sell16|sellc8, SpMV engine V, batch/lanes P,
 blocks per CU B, residual-update unroll U; also nN non-temporal, xX XCD map, sS slices/wave,
-rR recurrence, iI interleaved r/Ap pairs, BN update blocks per CU), e.g.
+rR recurrence, iI interleaved r/Ap pairs, wW LDS-window pass, BN update blocks per CU), e.g.
 
   python bench/sweep.py --n 16384 --steps 30 --cfg csr:v1:p6:b8:u2 csr:v0:p6:b6:u2 sell:v1:p6:b8:u2
 """
@@ -22,7 +22,7 @@ import cuda_mpi_parallel_amd as mcg  # noqa: E402
 
 def parse_cfg(s):
     parts = s.split(":")
-    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0, "i": -1}
+    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0, "i": -1, "w": -1}
     for q in parts[1:]:
         d[q[0]] = int(q[1:])
     return d
@@ -32,6 +32,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--problem", default="poisson2d")
+    ap.add_argument("--rows", type=int, default=4_000_000)
+    ap.add_argument("--band", type=int, default=4096)
+    ap.add_argument("--density", type=float, default=0.16)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--cfg", nargs="+", default=["csr:v1:p6:b8:u2"])
@@ -39,7 +42,10 @@ def main():
     args = ap.parse_args()
     torch.cuda.set_device(0)
     C = mcg.native()
-    spec = mcg.make_problem(args.problem, n=args.n)
+    if args.problem == "randspd":
+        spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density)
+    else:
+        spec = mcg.make_problem(args.problem, n=args.n)
     results = {}
     ref_rnorm = None
     for rnd in range(args.rounds):
@@ -49,6 +55,7 @@ def main():
                             blocks_per_cu=c["b"], spmv_variant=c["v"], spmv_param=c["p"], update_unroll=c["u"], nt_loads=c["n"], xcd_map=c["x"], sell_slices=c["s"], recurrence=c["r"])
             o.update_blocks_per_cu = c.get("B", 0)
             o.interleave = c["i"]
+            o.window = c["w"]
             s = C.Solver(spec.native(), o, 0, 1, None)
             s.setup()
             s.reset()

@@ -211,12 +211,195 @@ __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __rest
   st->iter += 1;
 }
 
+// ---------------------------------------------------------------------------
+// Windowed single-reduction pass for long banded rows (random-SPD family).
+//
+// The plain pass recomputes p_k = r_k + b p_{k-1} at EVERY gather (one 16-B {r, Ap}
+// load + one 8-B p load per nonzero, scattered over a +-band window — for ~1000
+// nonzeros per row that L2->L1 gather traffic, not HBM, bounds the kernel).  Here a
+// 1024-thread block owns a chunk of 16 consecutive slices (1024 rows), computes
+// p_k ONCE for every ext column the chunk touches into an LDS window
+// [win_lo, win_hi), and the 16 waves gather from LDS.  Applies when every chunk's
+// window fits the LDS budget (band <= ~4-9K at 1-2 blocks per CU).
+constexpr int kWinWaves = kWinRows / 64;
+constexpr int kWinBS = kWinRows;
+
+template <int CM, int U, bool RA>
+__global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+                                                      const int32_t* __restrict__ win,
+                                                      double* __restrict__ partials, int pstride,
+                                                      const CgState* __restrict__ st, double tol, int first,
+                                                      int check) {
+  extern __shared__ double s_win[];
+  __shared__ double s_part[4][kWinWaves];
+  if (st->done) return;
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (sc.conv) return;
+  const double a = sc.alpha, b = sc.beta, na = -a;
+  const double* __restrict__ ro = v.r_old;
+  const double* __restrict__ apo = v.ap_old;
+  const double* __restrict__ po = v.p_old;
+  double* __restrict__ rn = v.r_new;
+  double* __restrict__ apn = v.ap_new;
+  double* __restrict__ pn = v.p_new;
+  double* __restrict__ x = v.x;
+  const double2* __restrict__ rao = v.ra_old;
+  double2* __restrict__ ran = v.ra_new;
+  auto r_next = [&](int64_t e) -> double {
+    if constexpr (RA) {
+      const double2 q = rao[e];
+      return fma(na, q.y, q.x);
+    } else {
+      return fma(na, apo[e], ro[e]);
+    }
+  };
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+  // chunks of kWinWaves slices touched by the (up to two) slice ranges of this launch
+  const int64_t c0 = tr.b0 / kWinWaves, n0 = tr.e0 > tr.b0 ? (tr.e0 + kWinWaves - 1) / kWinWaves - c0 : 0;
+  const int64_t c1 = tr.b1 / kWinWaves, n1 = tr.e1 > tr.b1 ? (tr.e1 + kWinWaves - 1) / kWinWaves - c1 : 0;
+  for (int64_t q = blockIdx.x; q < n0 + n1; q += gridDim.x) {
+    const bool r0 = q < n0;
+    const int64_t chunk = r0 ? c0 + q : c1 + (q - n0);
+    const int64_t lo = win[2 * chunk], hi = win[2 * chunk + 1];
+    for (int64_t e = lo + threadIdx.x; e < hi; e += kWinBS) s_win[e - lo] = fma(b, po[e], r_next(e));
+    __syncthreads();
+    const int64_t sl = chunk * kWinWaves + wave;
+    if (sl >= (r0 ? tr.b0 : tr.b1) && sl < (r0 ? tr.e0 : tr.e1)) {
+      const double* __restrict__ wl = s_win - lo;
+      const double sum = eng::sell_slice<U, false, CM>(S, sl, nullptr, [&](int32_t c) { return wl[c]; });
+      const int64_t i = sl * 64 + lane;
+      if (i < S.n_rows) {
+        const int64_t e = own + i;
+        const double rk = r_next(e);
+        const double pold = po[e];
+        const double pk = wl[e];  // = fma(b, pold, rk), staged above
+        if constexpr (RA) {
+          ran[e] = make_double2(rk, sum);
+        } else {
+          rn[e] = rk;
+          apn[e] = sum;
+        }
+        pn[e] = pk;
+        x[i] = fma(a, pold, x[i]);
+        s_pap = fma(pk, sum, s_pap);
+        s_rap = fma(rk, sum, s_rap);
+        s_apap = fma(sum, sum, s_apap);
+        s_rr = fma(rk, rk, s_rr);
+      }
+    }
+    __syncthreads();
+  }
+  s_pap = eng::wave_sum(s_pap);
+  s_rap = eng::wave_sum(s_rap);
+  s_apap = eng::wave_sum(s_apap);
+  s_rr = eng::wave_sum(s_rr);
+  if (lane == 0) {
+    s_part[0][wave] = s_pap;
+    s_part[1][wave] = s_rap;
+    s_part[2][wave] = s_apap;
+    s_part[3][wave] = s_rr;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < kWinWaves; ++k) t += s_part[threadIdx.x][k];
+    partials[threadIdx.x * pstride + blockIdx.x] = t;
+  }
+}
+
+// per-chunk [lo, hi) ext-column window: one block per chunk, one thread per row
+template <typename IdxT>
+__global__ __launch_bounds__(kWinRows) void k_chunk_windows(const IdxT* __restrict__ rp, const int32_t* __restrict__ cols,
+                                                            int64_t n, int64_t own_off, int32_t* __restrict__ win) {
+  __shared__ int s_lo, s_hi;
+  if (threadIdx.x == 0) {
+    s_lo = 0x7fffffff;
+    s_hi = -1;
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kWinRows + threadIdx.x;
+  const int64_t n_pad = (n + 63) / 64 * 64;
+  if (i < n_pad) {
+    // the row's own column is always gathered (SELL padding; tail lanes use row n - 1)
+    int lo = (int)(own_off + (i < n ? i : n - 1)), hi = lo;
+    if (i < n)
+      for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+        lo = min(lo, cols[k]);
+        hi = max(hi, cols[k]);
+      }
+    atomicMin(&s_lo, lo);
+    atomicMax(&s_hi, hi);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    win[2 * blockIdx.x] = s_lo;
+    win[2 * blockIdx.x + 1] = s_hi + 1;
+  }
+}
+
 __global__ void k_pack_pairs(const double* __restrict__ a, double2* __restrict__ out, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = make_double2(a[i], 0.0);
 }
 
 }  // namespace
+
+int64_t win_chunks(const TileRanges& tr) {
+  const int64_t n0 = tr.e0 > tr.b0 ? (tr.e0 + kWinWaves - 1) / kWinWaves - tr.b0 / kWinWaves : 0;
+  const int64_t n1 = tr.e1 > tr.b1 ? (tr.e1 + kWinWaves - 1) / kWinWaves - tr.b1 / kWinWaves : 0;
+  return n0 + n1;
+}
+
+template <typename IdxT>
+void chunk_windows(const IdxT* rowptr, const int32_t* cols, int64_t n, int64_t own_off, int32_t* win,
+                   hipStream_t stream) {
+  const int64_t nch = (n + kWinRows - 1) / kWinRows;
+  if (nch == 0) return;
+  MCG_CHECK(nch < ((int64_t)1 << 31), "too many window chunks");
+  hipLaunchKernelGGL(k_chunk_windows<IdxT>, dim3((unsigned)nch), dim3(kWinRows), 0, stream, rowptr, cols, n, own_off,
+                     win);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(chunk_windows)");
+}
+template void chunk_windows<int32_t>(const int32_t*, const int32_t*, int64_t, int64_t, int32_t*, hipStream_t);
+template void chunk_windows<int64_t>(const int64_t*, const int32_t*, int64_t, int64_t, int32_t*, hipStream_t);
+
+// raise the dynamic-LDS limit of every windowed instantiation (setup time, not per launch)
+void cg_fused1_win_prepare(int win_doubles) {
+  const int lds = win_doubles * (int)sizeof(double);
+  MCG_CHECK((size_t)lds <= kWinMaxLds, "window exceeds the LDS budget");
+  const void* fns[] = {
+      reinterpret_cast<const void*>(&k_cg_f1_win<0, 4, false>), reinterpret_cast<const void*>(&k_cg_f1_win<0, 6, false>),
+      reinterpret_cast<const void*>(&k_cg_f1_win<0, 8, false>), reinterpret_cast<const void*>(&k_cg_f1_win<0, 4, true>),
+      reinterpret_cast<const void*>(&k_cg_f1_win<0, 6, true>),  reinterpret_cast<const void*>(&k_cg_f1_win<0, 8, true>),
+      reinterpret_cast<const void*>(&k_cg_f1_win<1, 4, false>), reinterpret_cast<const void*>(&k_cg_f1_win<1, 6, false>),
+      reinterpret_cast<const void*>(&k_cg_f1_win<1, 8, false>), reinterpret_cast<const void*>(&k_cg_f1_win<1, 4, true>),
+      reinterpret_cast<const void*>(&k_cg_f1_win<1, 6, true>),  reinterpret_cast<const void*>(&k_cg_f1_win<1, 8, true>)};
+  for (const void* f : fns)
+    MCG_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds), "kernel attribute failed(LDS)");
+}
+
+void cg_fused1_win(int cm, int param, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
+                   const int32_t* win, int win_doubles, double* partials, int pstride, int grid, const CgState* st,
+                   double tol, int first, int check, hipStream_t stream) {
+  if (tr.ntiles == 0 || grid == 0) return;
+  const size_t lds = (size_t)win_doubles * sizeof(double);
+  MCG_CHECK(lds <= kWinMaxLds, "window exceeds the LDS budget");
+  MCG_CHECK(cm == 0 || cm == 1, "windowed pass supports SELL-64 and SELL-64/d16");
+#define MCG_W(CM, U, RA)                                                                                      \
+  hipLaunchKernelGGL((k_cg_f1_win<CM, U, RA>), dim3(grid), dim3(kWinBS), lds, stream, S, v, own_off, tr, win, \
+                     partials, pstride, st, tol, first, check)
+#define MCG_WU(CM, RA) \
+  do { if (param <= 4) MCG_W(CM, 4, RA); else if (param <= 6) MCG_W(CM, 6, RA); else MCG_W(CM, 8, RA); } while (0)
+  const bool ra = v.ra_old != nullptr;
+  if (cm == 0) { if (ra) MCG_WU(0, true); else MCG_WU(0, false); }
+  else { if (ra) MCG_WU(1, true); else MCG_WU(1, false); }
+#undef MCG_WU
+#undef MCG_W
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
 
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream) {
   if (n <= 0) return;

@@ -150,6 +150,28 @@ void GpuCgSolver::setup() {
         matrix_bytes = total + (ns + 1) * 8;
       }
     }
+    if (!c8_ && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 && n > 0) {
+      // windowed pass: per-chunk column windows, measured from the CSR before conversion
+      const int64_t nch = (n + kern::kWinRows - 1) / kern::kWinRows;
+      win_.allocate(2 * nch, "A");
+      if (info_.idx64) kern::chunk_windows<int64_t>(rp64.get(), cols_.get(), n, L_.own_off, win_.get(), s0_);
+      else kern::chunk_windows<int32_t>(rp32_.get(), cols_.get(), n, L_.own_off, win_.get(), s0_);
+      std::vector<int32_t> w(2 * nch);
+      MCG_HIP(hipMemcpyAsync(w.data(), win_.get(), w.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s0_),
+              "memcpy from device to host failed(A)");
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+      int64_t width = 0;
+      for (int64_t c = 0; c < nch; ++c) width = std::max<int64_t>(width, (int64_t)w[2 * c + 1] - w[2 * c]);
+      const bool fits = width * (int64_t)sizeof(double) <= (int64_t)kern::kWinMaxLds;
+      const bool dense_rows = nnz >= 32 * n;
+      MCG_CHECK(opt_.window != 1 || fits, "windowed pass: a chunk's column window exceeds the LDS budget");
+      if (fits && (opt_.window == 1 || dense_rows)) {
+        win_doubles_ = (int)width;
+        kern::cg_fused1_win_prepare(win_doubles_);
+      } else {
+        win_.release();
+      }
+    }
     if (!c8_) {
       DeviceBuffer<int32_t> scols(d16_ ? 0 : total, "A", 8);
       DeviceBuffer<double> svals(total, "A", 8);
@@ -194,8 +216,13 @@ void GpuCgSolver::setup() {
 
   // ---- launch geometry ----
   const int bpc = opt_.blocks_per_cu > 0 ? opt_.blocks_per_cu : (opt_.format == 1 ? 48 : 8);
+  info_.window = win_doubles_;
   auto grid_a = [&](const TileRanges& t) {
     if (t.ntiles == 0) return 0;
+    if (win_doubles_ > 0) {  // 1024-thread chunk blocks: 2 per CU while the window fits half the LDS
+      const int per_cu = win_doubles_ * 8 <= 75 * 1024 ? 2 : 1;
+      return (int)std::max<int64_t>(1, std::min<int64_t>(kern::win_chunks(t), (int64_t)kern::num_cus() * per_cu));
+    }
     if (opt_.format == 1) return kern::grid_for(t.ntiles * 64, 256, bpc);
     if (info_.spmv_variant == 0)  // LDS-limited residency
       return kern::grid_for(t.ntiles * kTileRows, 256, std::min(bpc, kCsrBlocksPerCuCap));
@@ -331,6 +358,11 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
   }
   const SellDev S = sell_view();
+  if (win_doubles_ > 0 && !final_mode) {
+    kern::cg_fused1_win(d16_ ? 1 : 0, info_.spmv_param, S, v, L_.own_off, tr, win_.get(), win_doubles_, part,
+                        pstride_, grid, st_.get(), opt_.tol, first, check, s0_);
+    return;
+  }
   const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1))) : 0;
   if (info_.idx64)
     kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,

@@ -251,11 +251,48 @@ __device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRang
 }
 
 // ---------------------------------------------------------------------------
-// SELL-64: `sr` in slice units; one wave per slice.
+// SELL-64: one wave computes the 64 row sums of slice `sl` (lane = row in slice).
 // CM (column mode): 0 int32 ext columns, 1 int16 offsets from the row's own ext
 // column (SellDev::dcols), 2 one-byte dictionary codes (SellDev::codes) looked up
-// in an LDS copy of the {value, offset} table — every lane of a stencil slice reads
-// the same code at entry j, so the LDS read is a broadcast.
+// in `dict` (an LDS copy of the {value, offset} table) — every lane of a stencil
+// slice reads the same code at entry j, so the LDS read is a broadcast.
+template <int U, bool NT, int CM, class Gather>
+__device__ __forceinline__ double sell_slice(const SellDev& A, int64_t sl, const double2* dict, Gather&& gather) {
+  const int lane = threadIdx.x & 63;
+  const int64_t base = A.slice_ptr[sl];
+  const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
+  const int32_t* __restrict__ cp = A.cols + base + lane;
+  const int16_t* __restrict__ dp = A.dcols + base + lane;
+  const uint8_t* __restrict__ kp = A.codes + base + lane;
+  const int32_t rowcol = (int32_t)(A.own_off + sl * 64 + lane);
+  const double* __restrict__ vp = A.vals + base + lane;
+  double sum = 0.0;
+  for (int j0 = 0; j0 < w; j0 += U) {
+    int32_t c[U];
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = (j0 + u < w ? j0 + u : w - 1) * 64;
+      if constexpr (CM == 2) {
+        const double2 q = dict[ld<NT>(kp + j)];
+        c[u] = rowcol + (int32_t)__double_as_longlong(q.y);
+        v[u] = q.x;
+      } else {
+        if constexpr (CM == 1) c[u] = rowcol + (int32_t)ld<NT>(dp + j);
+        else c[u] = ld<NT>(cp + j);
+        v[u] = ld<NT>(vp + j);
+      }
+    }
+    double g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) sum = (j0 + u < w) ? fma(v[u], g[u], sum) : sum;
+  }
+  return sum;
+}
+
+// SELL-64: `sr` in slice units; one wave per slice.
 template <int U, bool NT, int CM, class Gather, class Epi>
 __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
   const int lane = threadIdx.x & 63;
@@ -268,36 +305,7 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
   for (TileCursor cur = tile_cursor(sr, w_in_blk, kWaves); cur.t < cur.end; cur.t += cur.step) {
     const int64_t t = cur.t;
     const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
-    const int64_t base = A.slice_ptr[sl];
-    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
-    const int32_t* __restrict__ cp = A.cols + base + lane;
-    const int16_t* __restrict__ dp = A.dcols + base + lane;
-    const uint8_t* __restrict__ kp = A.codes + base + lane;
-    const int32_t rowcol = (int32_t)(A.own_off + sl * 64 + lane);
-    const double* __restrict__ vp = A.vals + base + lane;
-    double sum = 0.0;
-    for (int j0 = 0; j0 < w; j0 += U) {
-      int32_t c[U];
-      double v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = (j0 + u < w ? j0 + u : w - 1) * 64;
-        if constexpr (CM == 2) {
-          const double2 q = s_dict[ld<NT>(kp + j)];
-          c[u] = rowcol + (int32_t)__double_as_longlong(q.y);
-          v[u] = q.x;
-        } else {
-          if constexpr (CM == 1) c[u] = rowcol + (int32_t)ld<NT>(dp + j);
-          else c[u] = ld<NT>(cp + j);
-          v[u] = ld<NT>(vp + j);
-        }
-      }
-      double g[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) sum = (j0 + u < w) ? fma(v[u], g[u], sum) : sum;
-    }
+    const double sum = sell_slice<U, NT, CM>(A, sl, s_dict, gather);
     const int64_t i = sl * 64 + lane;
     if (i < A.n_rows) epi(i, sum);
   }

@@ -120,7 +120,7 @@ LocalLayout make_layout(const ProblemSpec& s, const RowPartition& part, int rank
   const int64_t bw = bandwidth(s);
   int64_t ib = (L.row_begin == 0) ? 0 : L.row_begin + bw;
   int64_t ie = (L.row_end == L.n_global) ? L.n_global : L.row_end - bw;
-  ib = std::max(ib, L.row_begin);
+  ib = std::min(std::max(ib, L.row_begin), L.row_end);  // band wider than the block: no interior rows
   ie = std::min(ie, L.row_end);
   if (ie < ib) ie = ib;
   L.interior_begin = ib - L.row_begin;

@@ -34,6 +34,8 @@ struct CgOptions {
   int sell_slices = 1;       // SELL engine: slices in flight per wave (1 or 2)
   int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
+  int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
+                             // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   int force_idx64 = 0;       // test hook: int64 row pointers even when int32 would do

@@ -168,6 +168,18 @@ template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
                int first, int check, int final_mode, hipStream_t stream);
+// Windowed variant for long banded rows: 1024-row chunks (16 slices) stage p_k for their
+// column window [win[2c], win[2c+1]) in LDS once, the SpMV gathers from LDS.
+constexpr int kWinRows = 1024;
+constexpr size_t kWinMaxLds = 150 * 1024;  // dynamic LDS budget per block (gfx950: 160 KB per CU)
+template <typename IdxT>
+void chunk_windows(const IdxT* rowptr, const int32_t* cols, int64_t n, int64_t own_off, int32_t* win /* 2 per chunk */,
+                   hipStream_t stream);
+int64_t win_chunks(const TileRanges& slices);  // chunks touched by a launch (grid sizing)
+void cg_fused1_win_prepare(int win_doubles);     // setup: dynamic-LDS limit of the windowed kernels
+void cg_fused1_win(int cm /* 0 SELL-64, 1 SELL-64/d16 */, int param, const SellDev& S, const F1Vectors& v,
+                   int64_t own_off, const TileRanges& slices, const int32_t* win, int win_doubles, double* partials,
+                   int pstride, int grid, const CgState* st, double tol, int first, int check, hipStream_t stream);
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),

@@ -47,6 +47,7 @@ struct SolverInfo {
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
   bool interleave = false;
+  int window = 0;  // LDS window width (doubles) of the windowed pass; 0 = off
 };
 
 class GpuCgSolver {
@@ -110,6 +111,8 @@ class GpuCgSolver {
   DeviceBuffer<double2> dict_;
   int ndict_ = 0;
   bool c8_ = false;
+  DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
+  int win_doubles_ = 0;         // 0 = windowed pass off
   SellDev sell_view() const {
     SellDev s{slice_ptr_.get(), cols_.get(), vals_.get(), L_.n_local()};
     s.dcols = dcols_.get();

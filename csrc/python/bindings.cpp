@@ -150,6 +150,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("xcd_map") = 0, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
       .def_readwrite("interleave", &CgOptions::interleave)
+      .def_readwrite("window", &CgOptions::window)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
@@ -276,6 +277,7 @@ PYBIND11_MODULE(_C, m) {
         d["format"] = i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
         d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["interleave"] = i.interleave;
+        d["window"] = i.window;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;

@@ -76,6 +76,21 @@ def test_local_ranks_dense_halo_full_replica(mcg, recurrence, fmt):
     assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_ranks_window_pass_bitwise(mcg, world):
+    """Windowed pass with interior/boundary split + halo overlap vs the plain pass."""
+    spec = mcg.make_problem("randspd", rows=9000, band=50, density=0.7)
+    C = mcg.native()
+    outs = []
+    for w in (1, 0):
+        o = _opts(mcg, format="sell16", recurrence=1, check_every=4)
+        o.window = w
+        outs.append(C.run_local_ranks(spec.native(), o, world, 0, True))
+    assert [r["iterations"] for r in outs[0]["ranks"]] == [r["iterations"] for r in outs[1]["ranks"]]
+    np.testing.assert_array_equal(outs[0]["x"], outs[1]["x"])
+    assert all(r["converged"] for r in outs[0]["ranks"])
+
+
 def test_local_ranks_demo_more_ranks_than_rows_per_rank(mcg):
     """3x3 demo on 2 ranks (halo covers most of the matrix) still prints the golden x."""
     C = mcg.native()

@@ -83,6 +83,24 @@ def test_dictionary_codes_bitwise_equal_plain_sell(mcg, recurrence, problem, kw,
     assert a.true_residual_norm() == b.true_residual_norm()
 
 
+@pytest.mark.parametrize("fmt", ["sell", "sell16"])
+@pytest.mark.parametrize("interleave", [0, 1])
+def test_window_pass_bitwise_equal_plain(mcg, fmt, interleave):
+    """LDS-window pass (p_k staged once per 1024-row chunk) vs per-gather recomputation: same bits."""
+    spec = mcg.make_problem("randspd", rows=30000, band=60, density=0.6)
+    a = mcg.CGSolver(spec, format=fmt, recurrence=1, interleave=interleave, window=-1, check_every=8)
+    b = mcg.CGSolver(spec, format=fmt, recurrence=1, interleave=interleave, window=0, check_every=8)
+    assert a.info["window"] > 0 and b.info["window"] == 0  # mean row length ~73 -> auto on
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+
+
+def test_window_pass_off_for_stencils(mcg):
+    s = mcg.CGSolver(mcg.make_problem("poisson2d", n=256), format="sell16", recurrence=1)
+    assert s.info["window"] == 0  # 5 nonzeros per row: per-gather recomputation is cheaper
+
+
 def test_interleave_requires_single_reduction_sell(mcg):
     with pytest.raises(Exception, match="interleaved"):
         mcg.CGSolver(mcg.make_problem("poisson2d", n=32), format="csr", recurrence=1, interleave=1)

@@ -24,6 +24,7 @@ def test_plan_properties(mcg, problem, n, world):
         assert a.row_end == b.row_begin
     for L in Ls:
         assert L.own_off % 8 == 0 and L.ext_len >= L.own_off + L.n_local
+        assert 0 <= L.interior_begin <= L.interior_end <= L.n_local
         # sends of r to q == recvs of q from r, same ranges in the same order (RCCL matching rule)
         for q in range(world):
             s = [(g, c) for (p, g, c) in L.sends if p == q]
@@ -115,5 +116,7 @@ def test_partitioned_spmv_with_ghost_copies_is_bitwise_global(mcg, problem, kw, 
         rp_l, cols_l, vals_l = C.host_csr(spec.native(), world, L.rank)
         y[L.row_begin:L.row_end] = _spmv_rows(rp_l, cols_l, vals_l, xe)
     np.testing.assert_array_equal(y, y_global)
+    for L in Ls:
+        assert 0 <= L.interior_begin <= L.interior_end <= L.n_local
     if kw.get("band", 0) >= n:
         assert any(sum(c for (_, _, c) in L.recvs) == n - L.n_local for L in Ls)  # full replica
