@@ -310,26 +310,28 @@ __global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, in
   }
 }
 
-// per-chunk [lo, hi) ext-column window: one block per chunk, one thread per row
-template <typename IdxT>
-__global__ __launch_bounds__(kWinRows) void k_chunk_windows(const IdxT* __restrict__ rp, const int32_t* __restrict__ cols,
-                                                            int64_t n, int64_t own_off, int32_t* __restrict__ win) {
+// per-chunk [lo, hi) ext-column window: one block per chunk, one thread per padded row
+__global__ __launch_bounds__(kWinRows) void k_chunk_windows(SellDev S, int32_t* __restrict__ win) {
   __shared__ int s_lo, s_hi;
   if (threadIdx.x == 0) {
     s_lo = 0x7fffffff;
     s_hi = -1;
   }
   __syncthreads();
+  const int64_t n = S.n_rows;
   const int64_t i = (int64_t)blockIdx.x * kWinRows + threadIdx.x;
   const int64_t n_pad = (n + 63) / 64 * 64;
   if (i < n_pad) {
-    // the row's own column is always gathered (SELL padding; tail lanes use row n - 1)
-    int lo = (int)(own_off + (i < n ? i : n - 1)), hi = lo;
-    if (i < n)
-      for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-        lo = min(lo, cols[k]);
-        hi = max(hi, cols[k]);
-      }
+    const int64_t sl = i >> 6, l = i & 63;
+    const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
+    // the row's own column is always gathered (the epilogue; tail lanes stand in for row n - 1)
+    int lo = (int)(S.own_off + (i < n ? i : n - 1)), hi = lo;
+    for (int64_t j = 0; j < w; ++j) {
+      const int64_t dst = base + 64 * j + l;
+      const int c = S.dcols ? (int)(S.own_off + i + S.dcols[dst]) : S.cols[dst];
+      lo = min(lo, c);
+      hi = max(hi, c);
+    }
     atomicMin(&s_lo, lo);
     atomicMax(&s_hi, hi);
   }
@@ -353,18 +355,13 @@ int64_t win_chunks(const TileRanges& tr) {
   return n0 + n1;
 }
 
-template <typename IdxT>
-void chunk_windows(const IdxT* rowptr, const int32_t* cols, int64_t n, int64_t own_off, int32_t* win,
-                   hipStream_t stream) {
-  const int64_t nch = (n + kWinRows - 1) / kWinRows;
+void chunk_windows(const SellDev& S, int32_t* win, hipStream_t stream) {
+  const int64_t nch = (S.n_rows + kWinRows - 1) / kWinRows;
   if (nch == 0) return;
   MCG_CHECK(nch < ((int64_t)1 << 31), "too many window chunks");
-  hipLaunchKernelGGL(k_chunk_windows<IdxT>, dim3((unsigned)nch), dim3(kWinRows), 0, stream, rowptr, cols, n, own_off,
-                     win);
+  hipLaunchKernelGGL(k_chunk_windows, dim3((unsigned)nch), dim3(kWinRows), 0, stream, S, win);
   MCG_HIP(hipGetLastError(), "kernel launch failed(chunk_windows)");
 }
-template void chunk_windows<int32_t>(const int32_t*, const int32_t*, int64_t, int64_t, int32_t*, hipStream_t);
-template void chunk_windows<int64_t>(const int64_t*, const int32_t*, int64_t, int64_t, int32_t*, hipStream_t);
 
 // raise the dynamic-LDS limit of every windowed instantiation (setup time, not per launch)
 void cg_fused1_win_prepare(int win_doubles) {

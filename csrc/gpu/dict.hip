@@ -7,6 +7,7 @@
 // (e.g. the random-SPD family) keep SELL-64/d16 (2-B offset + 8-B value) or SELL-64.
 // Offsets are any int32 (the 7-pt operator's +-N^2 planes do not fit d16).
 //
+// Built from the generated SELL-64(/d16) arrays, which it then replaces.
 // This is value/index compression of a stored matrix (CSR-VI / CSR-DU style):
 // every nonzero is still stored, read and multiplied; it only shrinks the matrix
 // stream from 10 B to 1 B per entry, which is what bounds a memory-bound CG pass.
@@ -63,17 +64,25 @@ __device__ __forceinline__ bool set_insert(DictScratch* __restrict__ d, int t, u
   return false;
 }
 
-// collect the distinct value bit patterns and column offsets (from the row's own ext column)
-template <typename IdxT>
-__global__ __launch_bounds__(kBlock) void k_dict_collect(const IdxT* __restrict__ rp, const int32_t* __restrict__ cols,
-                                                         const double* __restrict__ vals, int64_t n, int64_t own_off,
-                                                         DictScratch* __restrict__ d) {
+// column of SELL entry `dst` of padded row i (ext index)
+__device__ __forceinline__ int64_t sell_col(const SellDev& S, int64_t dst, int64_t i) {
+  return S.dcols ? S.own_off + i + S.dcols[dst] : (int64_t)S.cols[dst];
+}
+
+// collect the distinct value bit patterns and column offsets (from the row's own ext
+// column) over every stored SELL entry, padding included (value 0, offset 0)
+__global__ __launch_bounds__(kBlock) void k_dict_collect(SellDev S, DictScratch* __restrict__ d) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  const int64_t n_pad = (S.n_rows + 63) / 64 * 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
     if (d->overflow) return;
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-      const unsigned long long off = (unsigned long long)((int64_t)cols[k] - (own_off + i));
-      const unsigned long long key = (unsigned long long)__double_as_longlong(vals[k]);
+    const int64_t sl = i >> 6, l = i & 63;
+    const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
+    const int64_t own = S.own_off + (i < S.n_rows ? i : S.n_rows - 1);
+    for (int64_t j = 0; j < w; ++j) {
+      const int64_t dst = base + 64 * j + l;
+      const unsigned long long off = (unsigned long long)(sell_col(S, dst, i) - own);
+      const unsigned long long key = (unsigned long long)__double_as_longlong(S.vals[dst]);
       if (key == kEmpty) {
         atomicOr(&d->overflow, 4u);
         return;
@@ -89,45 +98,30 @@ __global__ void k_dict_init(DictScratch* d) {
   if (blockIdx.x == 0 && threadIdx.x == 0) d->count[0] = d->count[1] = d->overflow = 0;
 }
 
-// one thread per row of the padded slice set: write the codes of row i, entry j
-// at base + 64 j + lane (column-major, like the other SELL arrays)
-template <typename IdxT>
-__global__ __launch_bounds__(kBlock) void k_csr_to_sell_c8(const IdxT* __restrict__ rp, const int32_t* __restrict__ cols,
-                                                           const double* __restrict__ vals, int64_t n, int64_t own_off,
-                                                           const int64_t* __restrict__ sp,
-                                                           const double2* __restrict__ dict, int nv, int nd,
-                                                           uint8_t* __restrict__ codes) {
+// one thread per padded row: code of SELL entry (i, j) at the same slot (base + 64 j + lane)
+__global__ __launch_bounds__(kBlock) void k_sell_to_c8(SellDev S, const double2* __restrict__ dict, int nv, int nd,
+                                                       uint8_t* __restrict__ codes) {
   __shared__ unsigned long long s_v[kMaxValues];
-  __shared__ int32_t s_d[kMaxValues];
+  __shared__ int64_t s_d[kMaxValues];
   for (int k = threadIdx.x; k < nv; k += kBlock) s_v[k] = (unsigned long long)__double_as_longlong(dict[k * nd].x);
-  for (int k = threadIdx.x; k < nd; k += kBlock) s_d[k] = (int32_t)__double_as_longlong(dict[k].y);
+  for (int k = threadIdx.x; k < nd; k += kBlock) s_d[k] = (int64_t)__double_as_longlong(dict[k].y);
   __syncthreads();
-  int pad_v = 0, pad_d = 0;  // padding = (offset 0, value +0.0); both are in the dictionary by construction
-  for (int k = 0; k < nv; ++k)
-    if (s_v[k] == 0ull) pad_v = k;
-  for (int k = 0; k < nd; ++k)
-    if (s_d[k] == 0) pad_d = k;
-  const uint8_t pad_code = (uint8_t)(pad_v * nd + pad_d);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n_pad = (n + 63) / 64 * 64;
+  const int64_t n_pad = (S.n_rows + 63) / 64 * 64;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
     const int64_t sl = i >> 6, l = i & 63;
-    const int64_t base = sp[sl], w = (sp[sl + 1] - base) >> 6;
-    const bool row = i < n;
-    const int64_t rs = row ? (int64_t)rp[i] : 0, len = row ? (int64_t)rp[i + 1] - rs : 0;
+    const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
+    const int64_t own = S.own_off + (i < S.n_rows ? i : S.n_rows - 1);
     for (int64_t j = 0; j < w; ++j) {
-      uint8_t code = pad_code;
-      if (j < len) {
-        const unsigned long long key = (unsigned long long)__double_as_longlong(vals[rs + j]);
-        const int32_t off = (int32_t)((int64_t)cols[rs + j] - (own_off + i));
-        int vi = 0, di = 0;
-        for (int k = 0; k < nv; ++k)
-          if (s_v[k] == key) vi = k;
-        for (int k = 0; k < nd; ++k)
-          if (s_d[k] == off) di = k;
-        code = (uint8_t)(vi * nd + di);
-      }
-      codes[base + 64 * j + l] = code;
+      const int64_t dst = base + 64 * j + l;
+      const unsigned long long key = (unsigned long long)__double_as_longlong(S.vals[dst]);
+      const int64_t off = sell_col(S, dst, i) - own;
+      int vi = 0, di = 0;
+      for (int k = 0; k < nv; ++k)
+        if (s_v[k] == key) vi = k;
+      for (int k = 0; k < nd; ++k)
+        if (s_d[k] == off) di = k;
+      codes[dst] = (uint8_t)(vi * nd + di);
     }
   }
 }
@@ -140,15 +134,11 @@ int dict_grid(int64_t n) {
 
 }  // namespace
 
-template <typename IdxT>
-bool sell_dict_build(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
-                     std::vector<double2>& dict, int& nv, int& nd, hipStream_t st) {
+bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st) {
   DictScratch* d = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(DictScratch), st), "device malloc failed(dict)");
   hipLaunchKernelGGL(k_dict_init, dim3(8), dim3(kBlock), 0, st, d);
-  if (n > 0)
-    hipLaunchKernelGGL(k_dict_collect<IdxT>, dim3(dict_grid(n)), dim3(kBlock), 0, st, rowptr, cols, vals, n, own_off,
-                       d);
+  if (S.n_rows > 0) hipLaunchKernelGGL(k_dict_collect, dim3(dict_grid(S.n_rows)), dim3(kBlock), 0, st, S, d);
   MCG_HIP(hipGetLastError(), "kernel launch failed(dict)");
   std::vector<unsigned char> raw(sizeof(DictScratch));
   MCG_HIP(hipMemcpyAsync(raw.data(), d, raw.size(), hipMemcpyDeviceToHost, st), "memcpy from device to host failed");
@@ -173,32 +163,20 @@ bool sell_dict_build(const IdxT* rowptr, const int32_t* cols, const double* vals
   dict.resize(v.size() * o.size());
   for (int a = 0; a < nv; ++a)
     for (int b = 0; b < nd; ++b) {
-      double val;
+      double val, offbits;
       std::memcpy(&val, &v[a], 8);
-      long long off = o[b];
-      double offbits;
+      const long long off = o[b];
       std::memcpy(&offbits, &off, 8);
       dict[a * nd + b] = make_double2(val, offbits);  // .y holds the int64 offset's bits
     }
   return true;
 }
-template bool sell_dict_build<int32_t>(const int32_t*, const int32_t*, const double*, int64_t, int64_t,
-                                       std::vector<double2>&, int&, int&, hipStream_t);
-template bool sell_dict_build<int64_t>(const int64_t*, const int32_t*, const double*, int64_t, int64_t,
-                                       std::vector<double2>&, int&, int&, hipStream_t);
 
-template <typename IdxT>
-void csr_to_sell_c8(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
-                    const int64_t* slice_ptr, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_csr_to_sell_c8<IdxT>, dim3(dict_grid(n)), dim3(kBlock), 0, st, rowptr, cols, vals, n, own_off,
-                     slice_ptr, dict, nv, nd, codes);
-  MCG_HIP(hipGetLastError(), "kernel launch failed(csr_to_sell_c8)");
+void sell_to_c8(const SellDev& S, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st) {
+  if (S.n_rows <= 0) return;
+  hipLaunchKernelGGL(k_sell_to_c8, dim3(dict_grid(S.n_rows)), dim3(kBlock), 0, st, S, dict, nv, nd, codes);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(sell_to_c8)");
 }
-template void csr_to_sell_c8<int32_t>(const int32_t*, const int32_t*, const double*, int64_t, int64_t,
-                                      const int64_t*, const double2*, int, int, uint8_t*, hipStream_t);
-template void csr_to_sell_c8<int64_t>(const int64_t*, const int32_t*, const double*, int64_t, int64_t,
-                                      const int64_t*, const double2*, int, int, uint8_t*, hipStream_t);
 
 }  // namespace kern
 }  // namespace mcg

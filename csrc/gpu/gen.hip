@@ -166,6 +166,41 @@ __global__ __launch_bounds__(kGenBlock) void k_csr_to_sell(const IdxT* __restric
   }
 }
 
+// direct SELL-64 fill: one thread per padded row, entries generated in the same order as
+// k_fill (so the SELL matrix equals the CSR -> SELL conversion entry for entry)
+__global__ __launch_bounds__(kGenBlock) void k_fill_sell(ProblemSpec s, int64_t row_begin, int64_t n, int64_t col_lo,
+                                                         int64_t pad, int64_t own_off,
+                                                         const int64_t* __restrict__ rp64,
+                                                         const int64_t* __restrict__ sp,
+                                                         int32_t* __restrict__ scols, int16_t* __restrict__ dcols,
+                                                         double* __restrict__ svals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n_pad = (n + 63) / 64 * 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
+    const int64_t sl = i >> 6, l = i & 63;
+    const int64_t base = sp[sl], w = (sp[sl + 1] - base) >> 6;
+    const bool row = i < n;
+    const int64_t len = row ? rp64[i + 1] - rp64[i] : 0;
+    const int64_t own_col = own_off + (row ? i : n - 1);  // a valid ext column for padding gathers
+    int64_t j = 0;
+    if (row)
+      for_each_entry(s, row_begin + i, [&](int64_t c, double v) {
+        const int64_t dst = base + 64 * j + l;
+        const int64_t ec = c - col_lo + pad;
+        if (dcols) dcols[dst] = (int16_t)(ec - (own_off + i));
+        else scols[dst] = (int32_t)ec;
+        svals[dst] = v;
+        ++j;
+      }, len);
+    for (; j < w; ++j) {
+      const int64_t dst = base + 64 * j + l;
+      if (dcols) dcols[dst] = (int16_t)(own_col - (own_off + i));
+      else scols[dst] = (int32_t)own_col;
+      svals[dst] = 0.0;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kGenBlock) void k_max_i64(const int64_t* __restrict__ a, int64_t n,
                                                        unsigned long long* __restrict__ out) {
   int64_t m = 0;
@@ -253,6 +288,16 @@ int64_t max_i64(const int64_t* a, int64_t n, hipStream_t st) {
   MCG_HIP(hipStreamSynchronize(st), "device synchronize failed");
   (void)hipFreeAsync(d, st);
   return (int64_t)h;
+}
+
+void gen_fill_sell(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad, int64_t own_off,
+                   const int64_t* rowptr64, const int64_t* slice_ptr, int32_t* scols, int16_t* dcols, double* svals,
+                   hipStream_t st) {
+  if (n <= 0) return;
+  MCG_CHECK((scols == nullptr) != (dcols == nullptr), "gen_fill_sell: exactly one column array");
+  hipLaunchKernelGGL(k_fill_sell, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, col_lo, pad, own_off,
+                     rowptr64, slice_ptr, scols, dcols, svals);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(gen_fill_sell)");
 }
 
 void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr, hipStream_t st) {

@@ -107,55 +107,51 @@ void GpuCgSolver::setup() {
   if (opt_.nt_loads && info_.spmv_variant == 1) info_.spmv_variant = 3;
   info_.nnz_local = nnz;
   info_.idx64 = nnz >= ((int64_t)1 << 31) - 64 || opt_.force_idx64;
-  cols_.allocate(nnz, "A", 8);
-  vals_.allocate(nnz, "A", 8);
-  if (info_.idx64) build_csr_<int64_t>(rp64); else build_csr_<int32_t>(rp64);
 
   size_t matrix_bytes = 0;
-  int64_t stored_entries = nnz;
   if (opt_.format == 1) {
-    // ---- CSR -> SELL-64 ----
+    // ---- SELL-64, generated directly (no CSR intermediate: peak memory = the SELL arrays) ----
     const int64_t ns = (n + 63) / 64;
     slice_ptr_.allocate(ns + 1, "A");
     kern::sell_slice_widths(rp64.get(), n, slice_ptr_.get(), s0_);
-    DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ns), "A");
-    kern::scan_inclusive_i64(slice_ptr_.get() + 1, ns, tmp.get(), s0_);
+    {
+      DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ns), "A");
+      kern::scan_inclusive_i64(slice_ptr_.get() + 1, ns, tmp.get(), s0_);
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    }
     int64_t total = 0;
-    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
     MCG_HIP(hipMemcpy(&total, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
             "memcpy from device to host failed(A)");
+    if (d16_) dcols_.allocate(total, "A", 16);
+    else cols_.allocate(total, "A", 8);
+    vals_.allocate(total, "A", 8);
+    kern::gen_fill_sell(spec_, L_.row_begin, n, L_.col_lo, L_.pad, L_.own_off, rp64.get(), slice_ptr_.get(),
+                        cols_.get(), dcols_.get(), vals_.get(), s0_);
+    matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
     if (c8_) {  // SELL-64/c8 when the (value, offset) dictionary fits one byte
       std::vector<double2> dict;
       int nv = 0, nd = 0;
-      c8_ = info_.idx64 ? kern::sell_dict_build<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, dict,
-                                                          nv, nd, s0_)
-                        : kern::sell_dict_build<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, dict,
-                                                          nv, nd, s0_);
+      c8_ = kern::sell_dict_build(sell_view(), dict, nv, nd, s0_);
       if (c8_) {
         ndict_ = (int)dict.size();
         dict_.allocate(dict.size(), "A");
         MCG_HIP(hipMemcpy(dict_.get(), dict.data(), dict.size() * sizeof(double2), hipMemcpyHostToDevice),
                 "memcpy from host to device failed(A)");
         codes_.allocate(total, "A", 64);
-        if (info_.idx64)
-          kern::csr_to_sell_c8<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                        dict_.get(), nv, nd, codes_.get(), s0_);
-        else
-          kern::csr_to_sell_c8<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                        dict_.get(), nv, nd, codes_.get(), s0_);
+        kern::sell_to_c8(sell_view(), dict_.get(), nv, nd, codes_.get(), s0_);
         MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
         cols_.release();
+        dcols_.release();
         vals_.release();
         info_.format = 3;
         matrix_bytes = total + (ns + 1) * 8;
       }
     }
     if (!c8_ && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 && n > 0) {
-      // windowed pass: per-chunk column windows, measured from the CSR before conversion
+      // windowed pass: per-chunk column windows of the generated matrix
       const int64_t nch = (n + kern::kWinRows - 1) / kern::kWinRows;
       win_.allocate(2 * nch, "A");
-      if (info_.idx64) kern::chunk_windows<int64_t>(rp64.get(), cols_.get(), n, L_.own_off, win_.get(), s0_);
-      else kern::chunk_windows<int32_t>(rp32_.get(), cols_.get(), n, L_.own_off, win_.get(), s0_);
+      kern::chunk_windows(sell_view(), win_.get(), s0_);
       std::vector<int32_t> w(2 * nch);
       MCG_HIP(hipMemcpyAsync(w.data(), win_.get(), w.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s0_),
               "memcpy from device to host failed(A)");
@@ -172,28 +168,14 @@ void GpuCgSolver::setup() {
         win_.release();
       }
     }
-    if (!c8_) {
-      DeviceBuffer<int32_t> scols(d16_ ? 0 : total, "A", 8);
-      DeviceBuffer<double> svals(total, "A", 8);
-      if (d16_) dcols_.allocate(total, "A", 16);
-      if (info_.idx64)
-        kern::csr_to_sell<int64_t>(rp64.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                   scols.get(), svals.get(), s0_, dcols_.get());
-      else
-        kern::csr_to_sell<int32_t>(rp32_.get(), cols_.get(), vals_.get(), n, L_.own_off, slice_ptr_.get(),
-                                   scols.get(), svals.get(), s0_, dcols_.get());
-      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
-      cols_ = std::move(scols);
-      vals_ = std::move(svals);
-      matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
-    }
-    rp32_.release();
-    stored_entries = total;
+    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
   } else {
+    cols_.allocate(nnz, "A", 8);
+    vals_.allocate(nnz, "A", 8);
+    if (info_.idx64) build_csr_<int64_t>(rp64); else build_csr_<int32_t>(rp64);
     matrix_bytes = nnz * 12 + (n + 1) * (info_.idx64 ? 8 : 4);
     if (info_.idx64) rp64_ = std::move(rp64);
   }
-  (void)stored_entries;
 
   // ---- vectors ----
   x_.allocate(n, "x", 8);

@@ -109,14 +109,16 @@ void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, in
                  int64_t own_off, const int64_t* slice_ptr, int32_t* scols, double* svals,
                  hipStream_t st, int16_t* dcols = nullptr /* write 16-bit deltas instead of scols */);
 
-// SELL-64/c8 dictionary (csrc/gpu/dict.hip): false if the matrix has too many distinct
-// values / offsets (or an offset outside int16).  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
-template <typename IdxT>
-bool sell_dict_build(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
-                     std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
-template <typename IdxT>
-void csr_to_sell_c8(const IdxT* rowptr, const int32_t* cols, const double* vals, int64_t n, int64_t own_off,
-                    const int64_t* slice_ptr, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st);
+// direct SELL-64(/d16) generation — no CSR intermediate (peak memory = the SELL arrays):
+// rowptr64 = inclusive-scanned row lengths, slice_ptr from sell_slice_widths + scan;
+// exactly one of scols (int32 ext columns) / dcols (int16 offsets from the row's own column)
+void gen_fill_sell(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad, int64_t own_off,
+                   const int64_t* rowptr64, const int64_t* slice_ptr, int32_t* scols, int16_t* dcols, double* svals,
+                   hipStream_t st);
+// SELL-64/c8 dictionary (csrc/gpu/dict.hip) from a generated SELL-64(/d16) matrix: false if
+// it has too many distinct values / offsets.  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
+bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
+void sell_to_c8(const SellDev& S, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st);
 
 // ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
 // variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row),
@@ -172,9 +174,7 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 // column window [win[2c], win[2c+1]) in LDS once, the SpMV gathers from LDS.
 constexpr int kWinRows = 1024;
 constexpr size_t kWinMaxLds = 150 * 1024;  // dynamic LDS budget per block (gfx950: 160 KB per CU)
-template <typename IdxT>
-void chunk_windows(const IdxT* rowptr, const int32_t* cols, int64_t n, int64_t own_off, int32_t* win /* 2 per chunk */,
-                   hipStream_t stream);
+void chunk_windows(const SellDev& S, int32_t* win /* 2 per chunk */, hipStream_t stream);
 int64_t win_chunks(const TileRanges& slices);  // chunks touched by a launch (grid sizing)
 void cg_fused1_win_prepare(int win_doubles);     // setup: dynamic-LDS limit of the windowed kernels
 void cg_fused1_win(int cm /* 0 SELL-64, 1 SELL-64/d16 */, int param, const SellDev& S, const F1Vectors& v,
