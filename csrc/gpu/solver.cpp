@@ -252,8 +252,9 @@ void GpuCgSolver::setup() {
   const double vec_a = 8.0 * (1 + 1 + 1 + 2 + 1);  // r, pold gathers (ideal), pnew, x rw, Ap
   const double vec_b = 24.0;                        // r rw, Ap
   info_.bytes_per_iter_model = (double)matrix_bytes + (vec_a + vec_b) * n;
-  // single-reduction pass: gathers r, Ap, p (ideal 24), x rw 16, writes r, p, Ap 24
-  if (opt_.recurrence == 1) info_.bytes_per_iter_model = (double)matrix_bytes + 64.0 * n;
+  // single-reduction pass: gathers r, Ap, p (ideal 24), writes r, p, Ap 24; x rw 16 + p_{k-2} 8
+  // every second pass (paired x updates) = 12 per pass
+  if (opt_.recurrence == 1) info_.bytes_per_iter_model = (double)matrix_bytes + 60.0 * n;
   if (opt_.recurrence == 1) info_.device_bytes += (size_t)(3 * L_.ext_len - n) * 8;
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
@@ -289,6 +290,7 @@ void GpuCgSolver::reset() {
   if (use_comm_) comm_->allreduce_sum(&st_.get()->rr_new, 1, s);
   MCG_HIP(hipStreamSynchronize(s), "compute norm2 failed(r)");
   k_ = 0;
+  finalized_ = false;
 }
 
 void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
@@ -335,6 +337,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   DeviceBuffer<double>& ap_old = odd ? Ap_ : Ap1_;
   kern::F1Vectors v{r_old.get(), ap_old.get(), p_[(k + 1) & 1].get(), r_new.get(), ap_new.get(), p_[k & 1].get(),
                     x_.get()};
+  v.p_fix = p_[1].get();
   if (opt_.interleave == 1) {
     v.ra_old = reinterpret_cast<const double2*>(ra_[(k + 1) & 1].get());
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
@@ -342,16 +345,18 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   const SellDev S = sell_view();
   if (win_doubles_ > 0 && !final_mode) {
     kern::cg_fused1_win(d16_ ? 1 : 0, info_.spmv_param, S, v, L_.own_off, tr, win_.get(), win_doubles_, part,
-                        pstride_, grid, st_.get(), opt_.tol, first, check, s0_);
+                        pstride_, grid, st_.get(), opt_.tol, first, check, k, s0_);
     return;
   }
   const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1))) : 0;
   if (info_.idx64)
     kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,
-                             L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, s0_);
+                             L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
+                             s0_);
   else
     kern::cg_fused1<int32_t>(fmt, info_.spmv_param, CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, S, v,
-                             L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, s0_);
+                             L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
+                             s0_);
 }
 
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
@@ -386,7 +391,7 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     enqueue_f1_(k, 0, 0);
   }
   CgState* st = st_.get();
-  kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, opt_.tol, s0_);
+  kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
 }
 
@@ -482,13 +487,14 @@ void GpuCgSolver::inject_fault_(int k) {
 }
 
 void GpuCgSolver::finalize() {
-  if (k_ == 0) return;
+  if (k_ == 0 || finalized_) return;
+  finalized_ = true;  // the single-reduction catch-up of a pending x term must run once
   if (opt_.recurrence == 1) {
     // r_m = r_{m-1} - a Ap_{m-1}, x_m = x_{m-1} + a p_{m-1}, exact ||r_m||^2, then latch
     enqueue_f1_(k_, 0, 1);
-    kern::cg_reduce_f1(partials_.get(), pstride_, g_all_, st_.get(), 1, k_ >= 2 ? 1 : 0, opt_.tol, s0_);
+    kern::cg_reduce_f1(partials_.get(), pstride_, g_all_, st_.get(), 1, k_ >= 2 ? 1 : 0, 0, opt_.tol, s0_);
     if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
-    kern::cg_reduce_f1(partials_.get(), pstride_, 0, st_.get(), 2, 0, opt_.tol, s0_);
+    kern::cg_reduce_f1(partials_.get(), pstride_, 0, st_.get(), 2, 0, 0, opt_.tol, s0_);
     return;
   }
   enqueue_spmv_(k_, 0, 1);  // pold = p_{k-1}: the deferred x += alpha p
@@ -605,6 +611,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   std::fclose(f);
   if (!ok) fail("checkpoint truncated", path);
   k_ = (int)h.k;
+  finalized_ = false;
 }
 
 CgResult GpuCgSolver::result() {

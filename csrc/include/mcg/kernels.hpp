@@ -31,7 +31,8 @@ struct alignas(64) CgState {
   double pAp;     // p . Ap of the last SpMV (global after all-reduce; all-reduce slot)
   double rr0;     // b . b
   double rr_final;  // rr_new captured when the latch fires (later no-op all-reduces may clobber rr_new)
-  double pad0_[3];
+  double a_prev;    // single-reduction form: alpha of the pass before the last (paired x updates)
+  double pad0_[2];
   // single-reduction recurrence: {p.Ap, r.Ap, Ap.Ap, r.r} of the last fused pass
   // (one contiguous 32-B all-reduce slot)
   double red[4];
@@ -165,11 +166,16 @@ struct F1Vectors {
   // gather is one 16-B load (+ the 8-B p load) instead of three 8-B loads
   const double2* ra_old = nullptr;
   double2* ra_new = nullptr;
+  // x is updated in pairs: pass k odd applies a_{k-2} p_{k-2} (read from p_new before it is
+  // overwritten) and a_{k-1} p_{k-1}; even passes leave x alone (-4 B/row/iteration).  p_fix =
+  // the parity-1 p buffer, for the one-term catch-up when convergence latches after an even pass.
+  const double* p_fix = nullptr;
 };
+// `k`: pass index (its parity selects the paired x update; final mode: m = k)
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
-               int first, int check, int final_mode, hipStream_t stream);
+               int first, int check, int final_mode, int k, hipStream_t stream);
 // Windowed variant for long banded rows: 1024-row chunks (16 slices) stage p_k for their
 // column window [win[2c], win[2c+1]) in LDS once, the SpMV gathers from LDS.
 constexpr int kWinRows = 1024;
@@ -179,13 +185,15 @@ int64_t win_chunks(const TileRanges& slices);  // chunks touched by a launch (gr
 void cg_fused1_win_prepare(int win_doubles);     // setup: dynamic-LDS limit of the windowed kernels
 void cg_fused1_win(int cm /* 0 SELL-64, 1 SELL-64/d16 */, int param, const SellDev& S, const F1Vectors& v,
                    int64_t own_off, const TileRanges& slices, const int32_t* win, int win_doubles, double* partials,
-                   int pstride, int grid, const CgState* st, double tol, int first, int check, hipStream_t stream);
+                   int pstride, int grid, const CgState* st, double tol, int first, int check, int k,
+                   hipStream_t stream);
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),
 //        1 = after the final pass (sum rr only), 2 = latch after the final all-reduce
-void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, double tol,
-                  hipStream_t stream);
+// `first`: after pass 0 (a_prev := 0)
+void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, int first,
+                  double tol, hipStream_t stream);
 
 // ---- unfused ops (ops API / tests) ----
 template <typename IdxT>

@@ -96,6 +96,7 @@ class GpuCgSolver {
   bool use_comm_ = false, use_halo_ = false;
   bool setup_done_ = false;
   int k_ = 0;  // host-side iteration counter (parity of the p double buffer)
+  bool finalized_ = false;
 
   Stream s0_, s1_;
   Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2];
