@@ -39,6 +39,8 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   use_halo_ = use_comm_ && L_.has_halo();
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
   if (opt_.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
+  // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only
+  prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph;
   s0_ = Stream(true, 0);
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);
@@ -291,6 +293,7 @@ void GpuCgSolver::reset() {
   MCG_HIP(hipStreamSynchronize(s), "compute norm2 failed(r)");
   k_ = 0;
   finalized_ = false;
+  halo_ready_for_ = -1;
 }
 
 void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
@@ -359,34 +362,49 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
                              s0_);
 }
 
+void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
+  // ghosts read by iteration k: {r, Ap} (or r and Ap) and p of iteration k-1 (parity (k+1)&1)
+  const bool odd = (k & 1) != 0;
+  double* vecs[3] = {(odd ? r_ : r1_).get(), (odd ? Ap_ : Ap1_).get(), p_[(k + 1) & 1].get()};
+  int nv = 3;
+  static const int widths[2] = {2, 1};
+  const int* w = nullptr;
+  if (opt_.interleave == 1) {
+    vecs[0] = ra_[(k + 1) & 1].get();
+    vecs[1] = p_[(k + 1) & 1].get();
+    nv = 2;
+    w = widths;
+  }
+  comm_->halo_exchange(L_, vecs, nv, s, w);
+}
+
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
   trace::Range tr_("mcg.iteration.single_reduction");
   int np = g_all_;
-  if (use_halo_) {
-    const bool odd = (k & 1) != 0;
-    double* vecs[3] = {(odd ? r_ : r1_).get(), (odd ? Ap_ : Ap1_).get(), p_[(k + 1) & 1].get()};
-    int nv = 3;
-    const int widths[3] = {2, 1, 1};
-    const int* w = nullptr;
-    if (opt_.interleave == 1) {  // {r, Ap} pairs of iteration k-1, then p_{k-1}
-      vecs[0] = ra_[(k + 1) & 1].get();
-      vecs[1] = p_[(k + 1) & 1].get();
-      nv = 2;
-      w = widths;
-    }
-    if (opt_.overlap) {
+  if (use_halo_ && opt_.overlap) {
+    if (halo_ready_for_ != k) {
       MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
       MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
-      comm_->halo_exchange(L_, vecs, nv, s1_, w);
+      enqueue_halo_f1_(k, s1_);
       MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
-      enqueue_f1_(k, 1, 0);
-      MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
-      enqueue_f1_(k, 2, 0);
-      np = g_int_ + g_bnd_;
-    } else {
-      comm_->halo_exchange(L_, vecs, nv, s0_, w);
-      enqueue_f1_(k, 0, 0);
     }
+    enqueue_f1_(k, 1, 0);  // interior rows || halo on the side stream
+    MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+    enqueue_f1_(k, 2, 0);  // boundary rows
+    np = g_int_ + g_bnd_;
+    halo_ready_for_ = -1;
+    if (prefetch_halo_) {
+      // the next iteration's ghosts are this iteration's outputs, final now: exchange them while
+      // this iteration's reduction + all-reduce and the next interior pass run
+      MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+      MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+      enqueue_halo_f1_(k + 1, s1_);
+      MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+      halo_ready_for_ = k + 1;
+    }
+  } else if (use_halo_) {
+    enqueue_halo_f1_(k, s0_);
+    enqueue_f1_(k, 0, 0);
   } else {
     enqueue_f1_(k, 0, 0);
   }
@@ -612,6 +630,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   if (!ok) fail("checkpoint truncated", path);
   k_ = (int)h.k;
   finalized_ = false;
+  halo_ready_for_ = -1;
 }
 
 CgResult GpuCgSolver::result() {

@@ -83,6 +83,7 @@ class GpuCgSolver {
   void enqueue_iteration_(int k);
   void enqueue_spmv_(int k, int which, int final_mode);  // which: 0 all, 1 interior, 2 boundary
   void enqueue_f1_(int k, int which, int final_mode);    // single-reduction fused pass
+  void enqueue_halo_f1_(int k, hipStream_t s);            // ghosts iteration k of the single-reduction form reads
   void enqueue_iteration_f1_(int k);
   void capture_pair_();
   void inject_fault_(int k);
@@ -97,6 +98,8 @@ class GpuCgSolver {
   bool setup_done_ = false;
   int k_ = 0;  // host-side iteration counter (parity of the p double buffer)
   bool finalized_ = false;
+  bool prefetch_halo_ = false;  // single-reduction form: next iteration's halo right after the boundary pass
+  int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
 
   Stream s0_, s1_;
   Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2];
