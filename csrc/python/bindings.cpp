@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <cstring>
 #include <pybind11/stl.h>
 
 #include <memory>
@@ -330,6 +331,39 @@ PYBIND11_MODULE(_C, m) {
     kern::spmv_sell(SellDev{reinterpret_cast<const int64_t*>(slice_ptr), reinterpret_cast<const int32_t*>(cols),
                             reinterpret_cast<const double*>(vals), n_rows},
                     reinterpret_cast<const double*>(x), reinterpret_cast<double*>(y), as_stream(stream));
+  });
+  // SELL-64/c8 (dictionary codes) from a SELL-64 matrix with int32 columns (own_off = 0):
+  // returns (dict as float64 [nv*nd, 2] = {value, int64 offset bits}, nv, nd) or None if it does not fit
+  k.def("sell_dict_build", [](uintptr_t slice_ptr, uintptr_t cols, uintptr_t vals, int64_t n_rows,
+                              uintptr_t stream) -> py::object {
+    SellDev S{reinterpret_cast<const int64_t*>(slice_ptr), reinterpret_cast<const int32_t*>(cols),
+              reinterpret_cast<const double*>(vals), n_rows};
+    std::vector<double2> dict;
+    int nv = 0, nd = 0;
+    bool ok;
+    {
+      py::gil_scoped_release rel;
+      ok = kern::sell_dict_build(S, dict, nv, nd, as_stream(stream));
+    }
+    if (!ok) return py::none();
+    py::array_t<double> d({(py::ssize_t)dict.size(), (py::ssize_t)2});
+    std::memcpy(d.mutable_data(), dict.data(), dict.size() * sizeof(double2));
+    return py::make_tuple(d, nv, nd);
+  });
+  k.def("sell_to_c8", [](uintptr_t slice_ptr, uintptr_t cols, uintptr_t vals, int64_t n_rows, uintptr_t dict, int nv,
+                         int nd, uintptr_t codes, uintptr_t stream) {
+    SellDev S{reinterpret_cast<const int64_t*>(slice_ptr), reinterpret_cast<const int32_t*>(cols),
+              reinterpret_cast<const double*>(vals), n_rows};
+    kern::sell_to_c8(S, reinterpret_cast<const double2*>(dict), nv, nd, reinterpret_cast<uint8_t*>(codes),
+                     as_stream(stream));
+  });
+  k.def("spmv_sell_c8", [](uintptr_t slice_ptr, uintptr_t codes, uintptr_t dict, int ndict, int64_t n_rows,
+                           uintptr_t x, uintptr_t y, uintptr_t stream) {
+    SellDev S{reinterpret_cast<const int64_t*>(slice_ptr), nullptr, nullptr, n_rows};
+    S.codes = reinterpret_cast<const uint8_t*>(codes);
+    S.dict = reinterpret_cast<const double2*>(dict);
+    S.ndict = ndict;
+    kern::spmv_sell(S, reinterpret_cast<const double*>(x), reinterpret_cast<double*>(y), as_stream(stream));
   });
   k.def("csr_to_sell", [](uintptr_t rowptr64, uintptr_t cols, uintptr_t vals, int64_t n, uintptr_t slice_ptr,
                           uintptr_t scols, uintptr_t svals, uintptr_t stream) {

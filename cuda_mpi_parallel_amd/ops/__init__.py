@@ -96,6 +96,40 @@ def spmv_sell(slice_ptr: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n
     return y
 
 
+def sell_compress_c8(slice_ptr: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows: int
+                     ) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """SELL-64 -> SELL-64/c8: one byte per stored entry indexing a table of distinct
+    (value, column offset) pairs (csrc/gpu/dict.hip).  Returns (codes uint8, dict float64 [k, 2])
+    or None when the matrix has more than 256 distinct pairs."""
+    _req(slice_ptr, torch.int64, "slice_ptr")
+    _req(cols, torch.int32, "cols")
+    _req(vals, torch.float64, "vals")
+    r = _k().sell_dict_build(slice_ptr.data_ptr(), cols.data_ptr(), vals.data_ptr(), n_rows, _stream())
+    if r is None:
+        return None
+    d, nv, nd = r
+    dict_t = torch.from_numpy(d).to(vals.device)
+    codes = torch.empty(vals.numel(), dtype=torch.uint8, device=vals.device)
+    _k().sell_to_c8(slice_ptr.data_ptr(), cols.data_ptr(), vals.data_ptr(), n_rows, dict_t.data_ptr(), nv, nd,
+                    codes.data_ptr(), _stream())
+    return codes, dict_t
+
+
+def spmv_sell_c8(slice_ptr: torch.Tensor, codes: torch.Tensor, dict_t: torch.Tensor, n_rows: int, x: torch.Tensor,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = A x for SELL-64/c8 storage (codes from :func:`sell_compress_c8`)."""
+    _req(slice_ptr, torch.int64, "slice_ptr")
+    _req(codes, torch.uint8, "codes")
+    _req(dict_t, torch.float64, "dict")
+    _req(x, torch.float64, "x")
+    if dict_t.dim() != 2 or dict_t.shape[1] != 2 or dict_t.shape[0] > 256:
+        raise ValueError("dict must be [k <= 256, 2]")
+    y = out if out is not None else torch.empty(n_rows, dtype=torch.float64, device=x.device)
+    _k().spmv_sell_c8(slice_ptr.data_ptr(), codes.data_ptr(), dict_t.data_ptr(), dict_t.shape[0], n_rows,
+                      x.data_ptr(), y.data_ptr(), _stream())
+    return y
+
+
 def dot(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """Fixed-order two-stage dot product (block partials -> one block); returns a 1-element tensor."""
     _req(a, torch.float64, "a")
@@ -152,4 +186,4 @@ def generate_rhs(spec, row_begin: int = 0, n: Optional[int] = None, device: str 
     return b
 
 
-__all__ = ["spmv_csr", "spmv_sell", "csr_to_sell", "dot", "axpy", "xpby", "generate_csr", "generate_rhs"]
+__all__ = ["spmv_csr", "spmv_sell", "csr_to_sell", "sell_compress_c8", "spmv_sell_c8", "dot", "axpy", "xpby", "generate_csr", "generate_rhs"]

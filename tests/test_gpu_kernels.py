@@ -49,6 +49,30 @@ def test_spmv_sell_matches_csr(mcg):
     np.testing.assert_allclose(y.cpu().numpy(), _ref_spmv(rowptr, cols, vals, x), rtol=1e-12, atol=1e-12)
 
 
+def test_spmv_sell_c8_matches_fp64_reference(mcg):
+    """Dictionary-coded SELL (1 byte per entry) on a 5-pt stencil with a ragged tail slice
+    vs a plain fp64 PyTorch SpMV; a random matrix (too many distinct values) is refused."""
+    spec = mcg.make_problem("poisson2d", n=45)  # 2025 rows: last slice has 41 live rows
+    rowptr, cols, vals = mcg.native().host_csr(spec.native(), 1, 0)
+    n = len(rowptr) - 1
+    d = "cuda"
+    rp, c, v = (torch.tensor(rowptr, device=d), torch.tensor(cols, device=d), torch.tensor(vals, device=d))
+    sp, sc, sv = mcg.ops.csr_to_sell(rp, c, v)
+    codes, dict_t = mcg.ops.sell_compress_c8(sp, sc, sv, n)
+    assert codes.dtype == torch.uint8 and dict_t.shape[0] <= 256
+    x = torch.tensor(np.random.default_rng(3).standard_normal(n), device=d)
+    y = mcg.ops.spmv_sell_c8(sp, codes, dict_t, n, x)
+    ref = torch.sparse_csr_tensor(torch.tensor(rowptr), torch.tensor(cols), torch.tensor(vals), (n, n)) @ x.cpu()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(y.cpu().numpy(), ref.numpy(), rtol=1e-13, atol=1e-13)
+    # bit-identical to the uncompressed SELL kernel (same entries, same order)
+    assert torch.equal(y, mcg.ops.spmv_sell(sp, sc, sv, n, x))
+    rowptr, cols, vals = _rand_csr(3001, 9, seed=7)
+    rp, c, v = (torch.tensor(rowptr, device=d), torch.tensor(cols, device=d), torch.tensor(vals, device=d))
+    sp, sc, sv = mcg.ops.csr_to_sell(rp, c, v)
+    assert mcg.ops.sell_compress_c8(sp, sc, sv, 3001) is None
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 1001, 1 << 20])
 def test_dot_axpy_xpby(mcg, n):
     g = torch.Generator().manual_seed(n)
