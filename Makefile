@@ -17,7 +17,7 @@ CLI       := bin/mcg-cg
 TESTBIN   := $(BUILD)/test_host
 
 COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-function
-HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
+HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 CXXFLAGS  := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -pthread
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -pthread -ldl
 

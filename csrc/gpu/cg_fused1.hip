@@ -71,6 +71,27 @@ __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, 
   }
 }
 
+// non-temporal stores for the vectors the pass writes: they are re-read only by the next pass,
+// after ~GBs of other traffic, so caching them is useless (A/B on 16384^2: +1.5-2 %,
+// profiles/ab_nt_stores.log; -DMCG_NT_STORES=0 restores plain stores)
+#ifndef MCG_NT_STORES
+#define MCG_NT_STORES 1
+#endif
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+  if constexpr (MCG_NT_STORES) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void st_stream(double2* p, double2 v) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  if constexpr (MCG_NT_STORES) {
+    d2v w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<d2v*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 template <int FMT, typename IdxT, int U, bool RA>
 __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                double* __restrict__ partials, int pstride,
@@ -143,13 +164,13 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
     const double pold = po[e];
     const double pk = fma(b, pold, rk);
     if constexpr (RA) {
-      ran[e] = make_double2(rk, sum);
+      st_stream(&ran[e], make_double2(rk, sum));
     } else {
       rn[e] = rk;
       apn[e] = sum;
     }
-    if (pair) x[i] = fma(a, pold, fma(ap, pn[e], x[i]));  // pn[e] = p_{k-2} until overwritten below
-    pn[e] = pk;
+    if (pair) st_stream(&x[i], fma(a, pold, fma(ap, pn[e], x[i])));  // pn[e] = p_{k-2} until overwritten below
+    st_stream(&pn[e], pk);
     s_pap = fma(pk, sum, s_pap);
     s_rap = fma(rk, sum, s_rap);
     s_apap = fma(sum, sum, s_apap);
