@@ -188,8 +188,21 @@ __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __rest
                                                             CgState* __restrict__ st, int mode, int check, int first,
                                                             double tol) {
   __shared__ double sh[4][kReduceBS / 64];
+  // 4 x 4 independent loads in flight per thread (a latency-bound single block); fixed order
   double s[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int i = threadIdx.x; i < np; i += kReduceBS) {
+  int i = threadIdx.x;
+  for (; i + 3 * kReduceBS < np; i += 4 * kReduceBS) {
+    double v[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[q][u] = partials[q * pstride + i + u * kReduceBS];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[q] += v[q][u];
+  }
+  for (; i < np; i += kReduceBS) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) s[q] += partials[q * pstride + i];
   }

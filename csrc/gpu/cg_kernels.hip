@@ -221,8 +221,18 @@ __global__ __launch_bounds__(kBS) void k_dot_partials(const double* __restrict__
 }
 
 __device__ __forceinline__ double reduce_partials_1block(const double* __restrict__ p, int np, double* sh) {
+  // 8 independent loads in flight per thread (a latency-bound single block); the order of the
+  // additions depends only on np, so the sum is bitwise reproducible
   double s = 0.0;
-  for (int i = threadIdx.x; i < np; i += kReduceBS) s += p[i];
+  int i = threadIdx.x;
+  for (; i + 7 * kReduceBS < np; i += 8 * kReduceBS) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[i + u * kReduceBS];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; i < np; i += kReduceBS) s += p[i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
