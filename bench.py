@@ -51,6 +51,9 @@ def main() -> int:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="SpMV grid; 0 = auto")
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
+    ap.add_argument("--phases", type=int, default=10,
+                    help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
+                         "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
     args = ap.parse_args()
 
     env = pdist.dist_env()
@@ -101,9 +104,14 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    phases = None
+    if args.phases > 0 and solver.info["recurrence"] == "single-reduction":
+        phases = solver.phase_profile(args.phases)  # untimed diagnostics: per-phase mean microseconds
+        phases = {k: round(v, 2) for k, v in phases.items()}
+    n_extra = args.phases if phases is not None else 0
     solver.finalize()  # untimed: completes x_m (the single-reduction form pairs x updates) and latches
     res = solver.result()
-    ok = res["iterations"] == args.warmup + args.steps and not res["breakdown"] and math.isfinite(res["rnorm"])
+    ok = res["iterations"] == args.warmup + args.steps + n_extra and not res["breakdown"] and math.isfinite(res["rnorm"])
     extra = {}
     if not args.no_verify:
         # the recurrence residual must track the true residual ||b - A x|| (catches a kernel
@@ -121,6 +129,13 @@ def main() -> int:
             dist.all_reduce(t)
         nnz = int(t.item())
     headline = args.problem == "poisson2d" and args.grid == 16384
+    if phases is not None:
+        extra["phase_us"] = phases
+        if env.world > 1:  # slowest rank per phase
+            keys = sorted(phases)
+            t = torch.tensor([phases[k] for k in keys], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            extra["phase_us_max"] = {k: round(float(v), 2) for k, v in zip(keys, t.tolist())}
     model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" if args.problem == "randspd"
              else f"{args.problem}_N{args.grid}")
     if env.rank == 0:

@@ -633,6 +633,64 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   halo_ready_for_ = -1;
 }
 
+std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters) {
+  MCG_CHECK(setup_done_, "solver not set up");
+  MCG_CHECK(opt_.recurrence == 1, "phase_profile: single-reduction form only");
+  trace::Range tr_("mcg.phase_profile");
+  synchronize();
+  halo_ready_for_ = -1;
+  Event e[6], h[2];
+  for (Event& v : e) v = Event(true, true);
+  for (Event& v : h) v = Event(true, true);
+  const char* names[] = {"interior_or_all", "halo_side_stream", "boundary_wait", "boundary", "reduce", "allreduce",
+                         "iteration"};
+  double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  auto ms = [](const Event& a, const Event& b) {
+    float t = 0.f;
+    MCG_HIP(hipEventElapsedTime(&t, a.get(), b.get()), "event elapsed failed");
+    return (double)t;
+  };
+  const bool split = use_halo_ && opt_.overlap;
+  for (int it = 0; it < iters; ++it) {
+    const int k = k_;
+    MCG_HIP(hipEventRecord(e[0].get(), s0_), "event record failed");
+    if (split) {
+      MCG_HIP(hipStreamWaitEvent(s1_, e[0].get(), 0), "stream wait failed");
+      MCG_HIP(hipEventRecord(h[0].get(), s1_), "event record failed");
+      enqueue_halo_f1_(k, s1_);
+      MCG_HIP(hipEventRecord(h[1].get(), s1_), "event record failed");
+      enqueue_f1_(k, 1, 0);
+      MCG_HIP(hipEventRecord(e[1].get(), s0_), "event record failed");
+      MCG_HIP(hipStreamWaitEvent(s0_, h[1].get(), 0), "stream wait failed");
+      MCG_HIP(hipEventRecord(e[2].get(), s0_), "event record failed");
+      enqueue_f1_(k, 2, 0);
+    } else {
+      if (use_halo_) enqueue_halo_f1_(k, s0_);
+      enqueue_f1_(k, 0, 0);
+      MCG_HIP(hipEventRecord(e[1].get(), s0_), "event record failed");
+      MCG_HIP(hipEventRecord(e[2].get(), s0_), "event record failed");
+    }
+    MCG_HIP(hipEventRecord(e[3].get(), s0_), "event record failed");
+    const int np = split ? g_int_ + g_bnd_ : g_all_;
+    kern::cg_reduce_f1(partials_.get(), pstride_, np, st_.get(), 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
+    MCG_HIP(hipEventRecord(e[4].get(), s0_), "event record failed");
+    if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
+    MCG_HIP(hipEventRecord(e[5].get(), s0_), "event record failed");
+    synchronize();
+    acc[0] += ms(e[0], e[1]);
+    acc[1] += split ? ms(h[0], h[1]) : 0.0;
+    acc[2] += ms(e[1], e[2]);
+    acc[3] += ms(e[2], e[3]);
+    acc[4] += ms(e[3], e[4]);
+    acc[5] += ms(e[4], e[5]);
+    acc[6] += ms(e[0], e[5]);
+    ++k_;
+  }
+  std::vector<std::pair<std::string, double>> out;
+  for (int q = 0; q < 7; ++q) out.emplace_back(names[q], iters > 0 ? 1e3 * acc[q] / iters : 0.0);
+  return out;
+}
+
 CgResult GpuCgSolver::result() {
   synchronize();
   CgState st;

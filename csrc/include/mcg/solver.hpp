@@ -72,6 +72,10 @@ class GpuCgSolver {
   CgResult result();                // read the device state (syncs)
   std::vector<double> x_local();    // owned part of x (syncs)
   double true_residual_norm();      // ||b - A x||_2 over all ranks (syncs)
+  // Diagnostic: run `iters` more single-reduction iterations eagerly with hipEvents at every
+  // phase boundary (halo on the side stream, interior / boundary passes, reduce, all-reduce) and
+  // return the mean microseconds per phase.  Advances the solver like run_iterations().
+  std::vector<std::pair<std::string, double>> phase_profile(int iters);
 
   const SolverInfo& info() const { return info_; }
   const LocalLayout& layout() const { return L_; }

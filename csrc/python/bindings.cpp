@@ -261,6 +261,16 @@ PYBIND11_MODULE(_C, m) {
       .def("result", [](GpuCgSolver& g) { return result_dict(g.result()); })
       .def("x_local", [](GpuCgSolver& g) { return to_numpy(g.x_local()); })
       .def("true_residual_norm", [](GpuCgSolver& g) { py::gil_scoped_release rel; return g.true_residual_norm(); })
+      .def("phase_profile", [](GpuCgSolver& g, int iters) {
+        std::vector<std::pair<std::string, double>> r;
+        {
+          py::gil_scoped_release rel;
+          r = g.phase_profile(iters);
+        }
+        py::dict d;
+        for (auto& kv : r) d[py::str(kv.first)] = kv.second;
+        return d;
+      })
       .def_property_readonly("iterations_enqueued", &GpuCgSolver::iterations_enqueued)
       .def_property_readonly("stream", [](GpuCgSolver& g) { return reinterpret_cast<uintptr_t>(g.stream()); })
       .def_property_readonly("layout", [](GpuCgSolver& g) { return layout_dict(g.layout()); })

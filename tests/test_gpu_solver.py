@@ -146,3 +146,18 @@ def test_force_comm_single_rank(mcg):
     out = mcg.CGSolver(spec, force_comm=True).solve()
     cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions())
     assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 2
+
+
+def test_phase_profile_diagnostic(mcg):
+    """Per-phase hipEvent timing of the single-reduction iteration (bench.py check.phase_us)."""
+    spec = mcg.make_problem("poisson2d", n=512)
+    s = mcg.CGSolver(spec, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, force_comm=True)
+    s.reset()
+    s.run(4)
+    ph = s._s.phase_profile(6)
+    assert set(ph) == {"interior_or_all", "halo_side_stream", "boundary_wait", "boundary", "reduce", "allreduce",
+                       "iteration"}
+    assert ph["iteration"] > 0 and ph["interior_or_all"] > 0 and ph["allreduce"] > 0
+    assert ph["iteration"] >= ph["interior_or_all"]
+    s.synchronize()
+    assert s.result()["iterations"] == 10
