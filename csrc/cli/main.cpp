@@ -9,7 +9,8 @@
 // Flags (all additive):
 //   --problem demo|poisson2d|poisson3d|randspd   --n N   --rows R --band W --density q
 //   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
-//   --maxit M  --tol T  --check-every K  --fixed-iters K  --warmup W
+//   --maxit M  --tol T  --rtol R (||r|| < R ||b||)  --check-every K  --fixed-iters K  --warmup W
+//   --nnz-per-row m (random-spd: density = (m - 1) / (2 band))
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
 //   --spmv-variant 0|1|2|3  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
 //   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off  --window auto|on|off
@@ -48,6 +49,7 @@ struct Args {
   int sim_ranks = 1;
   int fixed_iters = 0;
   int warmup = 0;
+  double nnz_per_row = 0.0;  // random-spd: mean nonzeros per row (sets the density)
   std::string print_x = "auto";
   std::string report = "text";
   bool verify = false;
@@ -77,6 +79,8 @@ Args parse(int argc, char** argv) {
     else if (f == "--sim-ranks") a.sim_ranks = std::stoi(need(i));
     else if (f == "--maxit") a.opt.maxit = std::stoi(need(i));
     else if (f == "--tol") a.opt.tol = std::stod(need(i));
+    else if (f == "--rtol") a.opt.rtol = std::stod(need(i));
+    else if (f == "--nnz-per-row") a.nnz_per_row = std::stod(need(i));
     else if (f == "--check-every") a.opt.check_every = std::stoi(need(i));
     else if (f == "--fixed-iters") a.fixed_iters = std::stoi(need(i));
     else if (f == "--warmup") a.warmup = std::stoi(need(i));
@@ -124,6 +128,7 @@ Args parse(int argc, char** argv) {
   if (a.spec.kind == ProblemKind::RandomSPD) {
     if (a.spec.rows <= 0) a.spec.rows = 100000;
     if (a.spec.band <= 0) a.spec.band = 64;
+    if (a.nnz_per_row > 0) a.spec.density = std::min(1.0, std::max(0.0, (a.nnz_per_row - 1.0) / (2.0 * a.spec.band)));
   }
   if (a.spec.kind != ProblemKind::Demo && !a.rhs_set) a.spec.rhs = RhsKind::Random;
   if (a.spec.kind != ProblemKind::Demo && a.spec.N == 3 && a.spec.kind != ProblemKind::RandomSPD) a.spec.N = 1024;

@@ -291,6 +291,19 @@ void GpuCgSolver::reset() {
   kern::cg_reduce(partials_.get(), g_b_, st_.get(), kReduceInit, 1, opt_.tol, s);
   if (use_comm_) comm_->allreduce_sum(&st_.get()->rr_new, 1, s);
   MCG_HIP(hipStreamSynchronize(s), "compute norm2 failed(r)");
+  if (opt_.rtol > 0) {  // relative stopping: tol = rtol * ||b|| (kernels take tol by value: re-capture)
+    double rr0 = 0.0;
+    MCG_HIP(hipMemcpy(&rr0, &st_.get()->rr_new, sizeof(double), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(state)");
+    const double tol = opt_.rtol * std::sqrt(rr0);
+    if (tol != opt_.tol && graph_exec_) {
+      (void)hipGraphExecDestroy(graph_exec_);
+      (void)hipGraphDestroy(graph_);
+      graph_exec_ = nullptr;
+      graph_ = nullptr;
+    }
+    opt_.tol = tol;
+  }
   k_ = 0;
   finalized_ = false;
   halo_ready_for_ = -1;

@@ -102,6 +102,7 @@ CgResult cpu_cg(const ProblemSpec& s, const CgOptions& opt, std::vector<double>*
   std::copy(b.begin(), b.end(), r.begin());
   std::copy(b.begin(), b.end(), pown);
   double rho = std::sqrt(dot(r.data(), r.data(), n));
+  const double tol = opt.rtol > 0 ? opt.rtol * rho : opt.tol;  // r0 = b
   rho = rho * rho;
   int it = 0;
   for (; it < opt.maxit;) {
@@ -115,7 +116,7 @@ CgResult cpu_cg(const ProblemSpec& s, const CgOptions& opt, std::vector<double>*
     rho = std::sqrt(dot(r.data(), r.data(), n));               // :328
     if (hist) hist->push_back(rho);
     if (!std::isfinite(rho)) { res.breakdown = true; break; }
-    if (rho < opt.tol) { res.converged = true; break; }        // :333
+    if (rho < tol) { res.converged = true; break; }            // :333
     rho = rho * rho;                                           // :336
     const double beta = rho / rhop;                            // :339
     for (int64_t i = 0; i < n; ++i) pown[i] = beta * pown[i];  // :342
@@ -171,6 +172,7 @@ CgResult cpu_cg_partitioned(const ProblemSpec& s, int world, const CgOptions& op
   };
 
   double rho = std::sqrt(allreduce([](Rank& k) { return dot(k.r.data(), k.r.data(), k.L.n_local()); }));
+  const double tol = opt.rtol > 0 ? opt.rtol * rho : opt.tol;
   rho = rho * rho;
   int it = 0;
   for (; it < opt.maxit;) {
@@ -190,7 +192,7 @@ CgResult cpu_cg_partitioned(const ProblemSpec& s, int world, const CgOptions& op
     rho = std::sqrt(allreduce([](Rank& k) { return dot(k.r.data(), k.r.data(), k.L.n_local()); }));
     if (hist) hist->push_back(rho);
     if (!std::isfinite(rho)) { res.breakdown = true; break; }
-    if (rho < opt.tol) { res.converged = true; break; }
+    if (rho < tol) { res.converged = true; break; }
     rho = rho * rho;
     const double beta = rho / rhop;
     for (auto& k : R) {

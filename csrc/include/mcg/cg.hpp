@@ -19,6 +19,7 @@ namespace mcg {
 struct CgOptions {
   int maxit = 2000;          // CUDACG.cu:244
   double tol = 1e-7;         // CUDACG.cu:245 (absolute ||r||_2)
+  double rtol = 0.0;         // > 0: stop on ||r||_2 < rtol * ||b||_2 instead (the "relative" of the comment at :238)
   int check_every = 32;      // host polls the device convergence latch every k iterations
   bool overlap = true;       // halo on a side stream, overlapped with the interior SpMV
   bool use_graph = true;     // capture iteration pairs into a hipGraph

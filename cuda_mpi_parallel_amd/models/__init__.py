@@ -61,6 +61,7 @@ class ProblemSpec:
 def make_problem(name: str = "demo", **kw) -> ProblemSpec:
     """``make_problem("poisson2d", n=4096)``; non-demo problems default to a random RHS
     (BASELINE.json:5 "random RHS"); randspd defaults to rows=100000, band=64."""
+    name = {"random-spd": "randspd", "random": "randspd"}.get(name, name)
     if name not in PROBLEMS:
         raise ValueError(f"unknown problem {name!r}; choose from {PROBLEMS}")
     if name != "demo":
@@ -68,6 +69,9 @@ def make_problem(name: str = "demo", **kw) -> ProblemSpec:
     if name == "randspd":
         kw.setdefault("rows", 100000)
         kw.setdefault("band", 64)
+        m = kw.pop("nnz_per_row", None)  # mean nonzeros per row -> candidate-pair density
+        if m is not None:
+            kw["density"] = min(1.0, max(0.0, (float(m) - 1.0) / (2.0 * kw["band"])))
     if name in ("poisson2d", "poisson3d"):
         kw.setdefault("n", 1024 if name == "poisson2d" else 128)
     return ProblemSpec(problem=name, **kw)

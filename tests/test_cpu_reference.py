@@ -74,3 +74,23 @@ def test_rhs_independent_of_partition(mcg):
     parts = [mcg.models.rhs(spec, a, b) for a, b in [(0, 500), (500, 1111), (1111, 1600)]]
     np.testing.assert_array_equal(np.concatenate(parts), full)
     assert 0.0 <= full.min() and full.max() < 1.0 and full.std() > 0.2
+
+
+def test_relative_tolerance_option(mcg):
+    """--rtol R stops on ||r|| < R ||b|| (the reference's comment says "relative", its code is absolute)."""
+    C = mcg.native()
+    spec = mcg.make_problem("poisson2d", n=64)
+    bn = float(np.linalg.norm(mcg.models.rhs(spec)))
+    o = C.CgOptions(maxit=2000, tol=1e-30)
+    o.rtol = 1e-6
+    r = C.cpu_cg(spec.native(), o)
+    assert r["converged"] and r["rnorm"] < 1e-6 * bn
+    o2 = C.CgOptions(maxit=2000, tol=1e-6 * bn)
+    assert C.cpu_cg(spec.native(), o2)["iterations"] == r["iterations"]
+    v = C.cpu_cg_partitioned(spec.native(), 3, o)
+    assert abs(v["iterations"] - r["iterations"]) <= 1
+
+
+def test_problem_aliases_and_nnz_per_row(mcg):
+    s = mcg.make_problem("random-spd", rows=2000, band=40, nnz_per_row=17)
+    assert s.problem == "randspd" and abs(s.density - 0.2) < 1e-12

@@ -161,3 +161,14 @@ def test_phase_profile_diagnostic(mcg):
     assert ph["iteration"] >= ph["interior_or_all"]
     s.synchronize()
     assert s.result()["iterations"] == 10
+
+
+@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "sellc8")])
+def test_relative_tolerance_matches_cpu(mcg, recurrence, fmt):
+    spec = mcg.make_problem("poisson2d", n=96)
+    C = mcg.native()
+    o = C.CgOptions(maxit=2000, tol=1e-30)
+    o.rtol = 1e-8
+    cpu = C.cpu_cg(spec.native(), o)
+    out = mcg.CGSolver(spec, format=fmt, recurrence=recurrence, tol=1e-30, rtol=1e-8, check_every=8).solve()
+    assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 2
