@@ -51,6 +51,8 @@ def main() -> int:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="SpMV grid; 0 = auto")
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="experiment: set a native CgOptions field (e.g. xcd_map=1, spmv_param=6)")
     ap.add_argument("--phases", type=int, default=10,
                     help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
@@ -78,6 +80,11 @@ def main() -> int:
     opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
                        use_graph=use_graph, force_comm=False, format=args.format,
                        blocks_per_cu=args.blocks_per_cu, recurrence=args.recurrence)
+    for kv in args.set:
+        k, v = kv.split("=", 1)
+        if not hasattr(opts, k):
+            raise SystemExit(f"bench.py: unknown option {k!r}")
+        setattr(opts, k, type(getattr(opts, k))(v))
     t_setup = time.perf_counter()
     solver = C.Solver(spec.native(), opts, env.rank, env.world, comm)
     solver.setup()

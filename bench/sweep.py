@@ -22,7 +22,7 @@ import cuda_mpi_parallel_amd as mcg  # noqa: E402
 
 def parse_cfg(s):
     parts = s.split(":")
-    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0, "i": -1, "w": -1}
+    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": 0, "s": 1, "r": 0, "i": -1, "w": -1, "P": -1, "S": -1}
     for q in parts[1:]:
         d[q[0]] = int(q[1:])
     return d
@@ -56,6 +56,8 @@ def main():
             o.update_blocks_per_cu = c.get("B", 0)
             o.interleave = c["i"]
             o.window = c["w"]
+            o.pipeline = c["P"]
+            o.strip = c["S"]
             s = C.Solver(spec.native(), o, 0, 1, None)
             s.setup()
             s.reset()

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "mcg/check.hpp"
 #include "mcg/kernels.hpp"
@@ -130,8 +131,8 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
       const int64_t lane = FMT == 0 ? threadIdx.x : (threadIdx.x & 63);
       for (eng::TileCursor cur = eng::tile_cursor(tr, sub, nsub); cur.t < cur.end; cur.t += cur.step) {
         const int64_t t = cur.t;
-        const int64_t u0 = t < tr.nt0 ? tr.b0 + t * (FMT == 0 ? kTileRows : 1)
-                                      : tr.b1 + (t - tr.nt0) * (FMT == 0 ? kTileRows : 1);
+        const int64_t u0 = FMT == 0 ? (t < tr.nt0 ? tr.b0 + t * kTileRows : tr.b1 + (t - tr.nt0) * kTileRows)
+                                    : eng::tile_unit(tr, t);
         const int64_t i = (FMT == 0 ? u0 : u0 * unit) + lane;
         const int64_t lim = FMT == 0 ? (t < tr.nt0 ? tr.e0 : tr.e1) : n;
         if (i < lim && i < n) f(i);
@@ -181,6 +182,135 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
   else if constexpr (FMT == 3) eng::sell<U, false, 1>(S, tr, gather, epi);
   else if constexpr (FMT == 4) eng::sell<U, false, 2>(S, tr, gather, epi);
   else eng::sell2<U, false>(S, tr, gather, epi);
+  block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
+}
+
+// ---------------------------------------------------------------------------
+// Software-pipelined single-reduction pass for short-row SELL-64/d16 and /c8 matrices with
+// the interleaved {r, Ap} layout (the stencil path: every slice fits ONE batch, w <= U).
+//
+// The generic engine walks a slice as load codes -> gather -> sum -> epilogue loads -> stores:
+// three dependent memory round trips per slice, ~7 us per slice per wave under load, so the
+// pass was latency bound (~9 cycles/row/CU against ~3 of L1 bandwidth).  Here a wave issues,
+// at the top of slice s: its own-row operands ({r, Ap}, p_{k-1}, and for paired x updates
+// p_{k-2} and x), the NEXT slice's slice pointers and codes, then the gathers of slice s.  The
+// arithmetic (sum order, every fma) is exactly the generic kernel's, so results are bitwise
+// identical (tests/test_gpu_solver.py).
+template <int CM, int U>
+__global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+                                                    double* __restrict__ partials, int pstride,
+                                                    const CgState* __restrict__ st, double tol, int first,
+                                                    int check, int k) {
+  __shared__ double2 s_dict[CM == 2 ? 256 : 1];
+  if (st->done) return;
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (sc.conv) return;
+  if constexpr (CM == 2) {
+    for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
+    __syncthreads();
+  }
+  const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  const bool pair = (k & 1) != 0;
+  const double* __restrict__ po = v.p_old;
+  double* __restrict__ pn = v.p_new;
+  double* __restrict__ x = v.x;
+  const double2* __restrict__ rao = v.ra_old;
+  double2* __restrict__ ran = v.ra_new;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t n = S.n_rows;
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+  using CodeT = typename std::conditional<CM == 2, uint8_t, int16_t>::type;
+  const CodeT* __restrict__ codes = CM == 2 ? reinterpret_cast<const CodeT*>(S.codes)
+                                            : reinterpret_cast<const CodeT*>(S.dcols);
+  const double* __restrict__ svals = S.vals;
+  auto slice_of = [&](int64_t t) { return eng::tile_unit(tr, t); };
+  eng::TileCursor cur = eng::tile_cursor(tr, wave, kWaves);
+  if (cur.t < cur.end) {
+    int64_t sl = slice_of(cur.t);
+    int64_t base = S.slice_ptr[sl];
+    int w = (int)((S.slice_ptr[sl + 1] - base) >> 6);
+    CodeT K[U];
+    double V[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = base + lane + 64 * (u < w ? u : w - 1);
+      K[u] = codes[j];
+      if constexpr (CM != 2) V[u] = svals[j];
+    }
+    for (;;) {
+      const int64_t i = sl * 64 + lane;
+      const bool live = i < n;
+      const int64_t e = own + (live ? i : n - 1);
+      // own-row operands: independent of the gathers, issued first
+      const double2 qo = rao[e];
+      const double pold = po[e];
+      const double pkm2 = pair ? pn[e] : 0.0;
+      const double xo = (pair && live) ? x[i] : 0.0;
+      // next slice: pointers + codes (one round trip ahead)
+      const int64_t tn = cur.t + cur.step;
+      const bool has_next = tn < cur.end;
+      int64_t sl_n = sl, base_n = base;
+      int w_n = w;
+      CodeT Kn[U];
+      double Vn[U];
+      if (has_next) {
+        sl_n = slice_of(tn);
+        base_n = S.slice_ptr[sl_n];
+        w_n = (int)((S.slice_ptr[sl_n + 1] - base_n) >> 6);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = base_n + lane + 64 * (u < w_n ? u : w_n - 1);
+          Kn[u] = codes[j];
+          if constexpr (CM != 2) Vn[u] = svals[j];
+        }
+      }
+      // this slice: decode, gather p_k = r_k + b p_{k-1} of every column, row sums
+      const int32_t rowcol = (int32_t)(own + i);
+      int32_t c[U];
+      double val[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (CM == 2) {
+          const double2 q = s_dict[K[u]];
+          c[u] = rowcol + (int32_t)__double_as_longlong(q.y);
+          val[u] = q.x;
+        } else {
+          c[u] = rowcol + (int32_t)K[u];
+          val[u] = V[u];
+        }
+      }
+      double g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double2 q = rao[c[u]];
+        g[u] = fma(b, po[c[u]], fma(na, q.y, q.x));
+      }
+      double sum = 0.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum = (u < w) ? fma(val[u], g[u], sum) : sum;
+      if (live) {
+        const double rk = fma(na, qo.y, qo.x);
+        const double pk = fma(b, pold, rk);
+        st_stream(&ran[e], make_double2(rk, sum));
+        if (pair) st_stream(&x[i], fma(a, pold, fma(ap, pkm2, xo)));
+        st_stream(&pn[e], pk);
+        s_pap = fma(pk, sum, s_pap);
+        s_rap = fma(rk, sum, s_rap);
+        s_apap = fma(sum, sum, s_apap);
+        s_rr = fma(rk, rk, s_rr);
+      }
+      if (!has_next) break;
+      cur.t = tn;
+      sl = sl_n;
+      base = base_n;
+      w = w_n;
+      for (int u = 0; u < U; ++u) {  // register renames after full unrolling of the body
+        K[u] = Kn[u];
+        if constexpr (CM != 2) V[u] = Vn[u];
+      }
+    }
+  }
   block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
 }
 
@@ -458,7 +588,7 @@ void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream) {
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
-               int first, int check, int final_mode, int k, hipStream_t stream) {
+               int first, int check, int final_mode, int k, hipStream_t stream, bool pipe) {
   if (tr.ntiles == 0 || grid == 0) return;
 #define MCG_F1(F, U, RA)                                                                                   \
   hipLaunchKernelGGL((k_cg_f1<F, IdxT, U, RA>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, \
@@ -474,6 +604,25 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
   } while (0)
   const bool ra = v.ra_old != nullptr;
   MCG_CHECK(!ra || fmt == 1 || fmt == 3 || fmt == 4, "interleaved r/Ap layout needs a SELL format");
+  if (pipe && !final_mode && ra && (fmt == 3 || fmt == 4) && param >= 4 && param <= 8) {
+#define MCG_PIPE(CM, U)                                                                                        \
+  hipLaunchKernelGGL((k_cg_f1_pipe<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, partials, pstride, \
+                     st, tol, first, check, k)
+#define MCG_PIPEU(CM)                          \
+  do {                                         \
+    if (param == 4) MCG_PIPE(CM, 4);           \
+    else if (param == 5) MCG_PIPE(CM, 5);      \
+    else if (param == 6) MCG_PIPE(CM, 6);      \
+    else if (param == 7) MCG_PIPE(CM, 7);      \
+    else MCG_PIPE(CM, 8);                      \
+  } while (0)
+    if (fmt == 4) MCG_PIPEU(2);
+    else MCG_PIPEU(1);
+#undef MCG_PIPEU
+#undef MCG_PIPE
+    MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+    return;
+  }
   if (fmt == 0) MCG_F1U(0, false);
   else if (fmt == 1) { if (ra) MCG_F1U(1, true); else MCG_F1U(1, false); }
   else if (fmt == 2) MCG_F1U(2, false);
@@ -485,10 +634,10 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 }
 template void cg_fused1<int32_t>(int, int, const CsrDev<int32_t>&, const SellDev&, const F1Vectors&, int64_t,
                                  const TileRanges&, double*, int, int, const CgState*, double, int, int, int, int,
-                                 hipStream_t);
+                                 hipStream_t, bool);
 template void cg_fused1<int64_t>(int, int, const CsrDev<int64_t>&, const SellDev&, const F1Vectors&, int64_t,
                                  const TileRanges&, double*, int, int, const CgState*, double, int, int, int, int,
-                                 hipStream_t);
+                                 hipStream_t, bool);
 
 void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, int first,
                   double tol, hipStream_t stream) {

@@ -201,6 +201,10 @@ void GpuCgSolver::setup() {
   // ---- launch geometry ----
   const int bpc = opt_.blocks_per_cu > 0 ? opt_.blocks_per_cu : (opt_.format == 1 ? 48 : 8);
   info_.window = win_doubles_;
+  pipe_ = opt_.pipeline != 0 && opt_.format == 1 && (d16_ || c8_) && opt_.interleave == 1 &&
+          opt_.sell_slices != 2 && info_.max_row_len <= 8 && info_.spmv_param >= info_.max_row_len;
+  MCG_CHECK(opt_.pipeline != 1 || pipe_, "pipelined pass needs SELL d16/c8, interleave and rows <= param <= 8");
+  info_.pipeline = pipe_;
   auto grid_a = [&](const TileRanges& t) {
     if (t.ntiles == 0) return 0;
     if (win_doubles_ > 0) {  // 1024-thread chunk blocks: 2 per CU while the window fits half the LDS
@@ -239,6 +243,17 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (opt_.xcd_map) tr_all_.xcd = tr_int_.xcd = tr_bnd_.xcd = 8;
+  if (opt_.format == 1 && opt_.sell_slices != 2 && win_doubles_ == 0) {
+    // vertical-strip slice order: S = slices per grid line (2-D stencil, whole-slice lines)
+    int64_t S = opt_.strip > 0 ? opt_.strip : 0;
+    if (opt_.strip < 0 && spec_.kind == ProblemKind::Poisson2D && spec_.N % 64 == 0) S = spec_.N / 64;
+    auto apply = [&](TileRanges& t) {
+      if (S > 0 && t.ntiles > 0 && t.nt0 == t.ntiles && t.ntiles % S == 0 && t.ntiles / S >= 2) t.strip = (int32_t)S;
+    };
+    apply(tr_all_);
+    apply(tr_int_);
+    info_.strip = tr_all_.strip;
+  }
   g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
@@ -368,11 +383,11 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   if (info_.idx64)
     kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,
                              L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
-                             s0_);
+                             s0_, pipe_);
   else
     kern::cg_fused1<int32_t>(fmt, info_.spmv_param, CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, S, v,
                              L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
-                             s0_);
+                             s0_, pipe_);
 }
 
 void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {

@@ -82,7 +82,13 @@ struct TileCursor {
 __device__ __forceinline__ TileCursor tile_cursor(const TileRanges& tr, int64_t sub, int64_t nsub) {
   const int64_t blk = blockIdx.x, nblk = gridDim.x;
   TileCursor c;
-  if (tr.xcd > 1 && nblk % tr.xcd == 0) {
+  if (tr.strip > 0) {  // contiguous run of (permuted) units per wave, see TileRanges::strip
+    const int64_t nw = nblk * nsub, gw = blk * nsub + sub;
+    const int64_t chunk = (tr.ntiles + nw - 1) / nw;
+    c.t = gw * chunk;
+    c.end = imin(tr.ntiles, c.t + chunk);
+    c.step = 1;
+  } else if (tr.xcd > 1 && nblk % tr.xcd == 0) {
     const int64_t X = tr.xcd, x = blk % X, lb = blk / X, nb = nblk / X;
     const int64_t per = (tr.ntiles + X - 1) / X;
     const int64_t start = x * per;
@@ -95,6 +101,15 @@ __device__ __forceinline__ TileCursor tile_cursor(const TileRanges& tr, int64_t 
     c.step = nblk * nsub;
   }
   return c;
+}
+
+// unit (slice / row tile) visited at cursor position t
+__device__ __forceinline__ int64_t tile_unit(const TileRanges& tr, int64_t t) {
+  if (tr.strip > 0) {
+    const int64_t L = tr.nt0 / tr.strip;
+    return tr.b0 + (t % L) * tr.strip + t / L;
+  }
+  return t < tr.nt0 ? tr.b0 + t : tr.b1 + (t - tr.nt0);
 }
 
 // matrix streams are read once per SpMV: non-temporal loads keep them from
@@ -303,8 +318,7 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
   }
   const int64_t w_in_blk = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   for (TileCursor cur = tile_cursor(sr, w_in_blk, kWaves); cur.t < cur.end; cur.t += cur.step) {
-    const int64_t t = cur.t;
-    const int64_t sl = t < sr.nt0 ? sr.b0 + t : sr.b1 + (t - sr.nt0);
+    const int64_t sl = tile_unit(sr, cur.t);
     const double sum = sell_slice<U, NT, CM>(A, sl, s_dict, gather);
     const int64_t i = sl * 64 + lane;
     if (i < A.n_rows) epi(i, sum);

@@ -35,6 +35,11 @@ struct CgOptions {
   int sell_slices = 1;       // SELL engine: slices in flight per wave (1 or 2)
   int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
+  int strip = 0;             // SELL: visit slices in vertical strips of this many slices per grid line (each wave
+                             // walks down one column); -1 = 2-D stencil line width.  Off by default: measured
+                             // slower (241 vs 248 it/s at 16384^2, profiles/sweep_strip_order.log)
+  int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
+                             // pass (next slice's codes + own-row operands issued ahead); -1 = auto
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)

@@ -53,7 +53,12 @@ struct TileRanges {
   int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
   int64_t nt0 = 0, ntiles = 0;
   int32_t xcd = 0;  // > 1: XCD-aware contiguous tile regions (see spmv_engines.hpp tile_cursor)
-  int32_t pad_ = 0;
+  // > 0 (single range, nt0 % strip == 0): units are visited in "vertical strips" — unit
+  // index u = col * L + line maps to b0 + line * strip + col (L = nt0 / strip), and every wave
+  // takes a contiguous run of u.  With strip = slices per grid line, a wave walks one column of
+  // slices down the grid, so a row's +-N (next/previous line) neighbours are the wave's own
+  // previous/next slices: cache hits instead of a second/third HBM read of the same vector rows.
+  int32_t strip = 0;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);
@@ -175,7 +180,9 @@ struct F1Vectors {
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
                const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
-               int first, int check, int final_mode, int k, hipStream_t stream);
+               int first, int check, int final_mode, int k, hipStream_t stream,
+               bool pipe = false /* software-pipelined stencil pass: SELL d16/c8 + interleaved, every slice
+                                    width <= param */);
 // Windowed variant for long banded rows: 1024-row chunks (16 slices) stage p_k for their
 // column window [win[2c], win[2c+1]) in LDS once, the SpMV gathers from LDS.
 constexpr int kWinRows = 1024;

@@ -48,6 +48,8 @@ struct SolverInfo {
   int recurrence = 0;
   bool interleave = false;
   int window = 0;  // LDS window width (doubles) of the windowed pass; 0 = off
+  bool pipeline = false;
+  int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
 };
 
 class GpuCgSolver {
@@ -121,6 +123,7 @@ class GpuCgSolver {
   bool c8_ = false;
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
   int win_doubles_ = 0;         // 0 = windowed pass off
+  bool pipe_ = false;           // software-pipelined stencil pass
   SellDev sell_view() const {
     SellDev s{slice_ptr_.get(), cols_.get(), vals_.get(), L_.n_local()};
     s.dcols = dcols_.get();

@@ -152,6 +152,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("recurrence", &CgOptions::recurrence)
       .def_readwrite("interleave", &CgOptions::interleave)
       .def_readwrite("window", &CgOptions::window)
+      .def_readwrite("pipeline", &CgOptions::pipeline)
+      .def_readwrite("strip", &CgOptions::strip)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
@@ -290,6 +292,8 @@ PYBIND11_MODULE(_C, m) {
         d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["interleave"] = i.interleave;
         d["window"] = i.window;
+        d["pipeline"] = i.pipeline;
+        d["strip"] = i.strip;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;

@@ -92,6 +92,19 @@ def test_local_ranks_window_pass_bitwise(mcg, world):
     assert all(r["converged"] for r in outs[0]["ranks"])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_ranks_pipelined_pass_bitwise(mcg, world):
+    spec = mcg.make_problem("poisson2d", n=200)
+    C = mcg.native()
+    outs = []
+    for pp in (1, 0):
+        o = _opts(mcg, format="sellc8", recurrence=1, check_every=4)
+        o.pipeline = pp
+        outs.append(C.run_local_ranks(spec.native(), o, world, 0, True))
+    assert [r["iterations"] for r in outs[0]["ranks"]] == [r["iterations"] for r in outs[1]["ranks"]]
+    np.testing.assert_array_equal(outs[0]["x"], outs[1]["x"])
+
+
 def test_local_ranks_demo_more_ranks_than_rows_per_rank(mcg):
     """3x3 demo on 2 ranks (halo covers most of the matrix) still prints the golden x."""
     C = mcg.native()

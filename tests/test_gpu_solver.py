@@ -103,6 +103,19 @@ def test_window_pass_off_for_stencils(mcg):
     assert s.info["window"] == 0  # 5 nonzeros per row: per-gather recomputation is cheaper
 
 
+@pytest.mark.parametrize("fmt", ["sell16", "sellc8"])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20))])
+def test_pipelined_pass_bitwise_equal_generic(mcg, fmt, problem, kw):
+    """Software-pipelined stencil pass vs the generic engine: same arithmetic, same bits."""
+    spec = mcg.make_problem(problem, **kw)
+    a = mcg.CGSolver(spec, format=fmt, recurrence=1, pipeline=-1, check_every=8)
+    b = mcg.CGSolver(spec, format=fmt, recurrence=1, pipeline=0, check_every=8)
+    assert a.info["pipeline"] and not b.info["pipeline"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+
+
 def test_interleave_requires_single_reduction_sell(mcg):
     with pytest.raises(Exception, match="interleaved"):
         mcg.CGSolver(mcg.make_problem("poisson2d", n=32), format="csr", recurrence=1, interleave=1)
