@@ -38,8 +38,9 @@ struct CgOptions {
   int strip = 0;             // SELL: visit slices in vertical strips of this many slices per grid line (each wave
                              // walks down one column); -1 = 2-D stencil line width.  Off by default: measured
                              // slower (241 vs 248 it/s at 16384^2, profiles/sweep_strip_order.log)
-  int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
-                             // pass (next slice's codes + own-row operands issued ahead); -1 = auto
+  int pipeline = 0;          // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
+                             // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
+                             // Off by default: 2-D equal, 3-D slower (310 vs 336 it/s, profiles/sweep_pipeline.log)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)

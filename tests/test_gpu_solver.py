@@ -108,7 +108,7 @@ def test_window_pass_off_for_stencils(mcg):
 def test_pipelined_pass_bitwise_equal_generic(mcg, fmt, problem, kw):
     """Software-pipelined stencil pass vs the generic engine: same arithmetic, same bits."""
     spec = mcg.make_problem(problem, **kw)
-    a = mcg.CGSolver(spec, format=fmt, recurrence=1, pipeline=-1, check_every=8)
+    a = mcg.CGSolver(spec, format=fmt, recurrence=1, pipeline=1, check_every=8)
     b = mcg.CGSolver(spec, format=fmt, recurrence=1, pipeline=0, check_every=8)
     assert a.info["pipeline"] and not b.info["pipeline"]
     ra, rb = a.solve(), b.solve()
