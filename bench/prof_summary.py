@@ -38,8 +38,8 @@ def main():
                 k = short(r["Kernel_Name"])
                 agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-        print("| kernel | median µs | FETCH_SIZE GB | WRITE_SIZE GB | TCC hit % |")
-        print("|---|---|---|---|---|")
+        print("| kernel | median µs | FETCH_SIZE GB | WRITE_SIZE GB | TCC hit % | L2->fabric read GB | fabric write GB |")
+        print("|---|---|---|---|---|---|---|")
         for k, v in agg.items():
             if not k.startswith("k_cg") and not k.startswith("k_dot"):
                 continue
@@ -50,10 +50,16 @@ def main():
             fs = f"{sum(f)/len(f)/1e6:.3f}" if f else "-"
             ws = f"{sum(w)/len(w)/1e6:.3f}" if w else "-"
             hr = f"{100*sum(h)/(sum(h)+sum(m)):.1f}" if h and m else "-"
+            rd = v.get("TCC_EA0_RDREQ_DRAM_32B_sum")
+            wd = v.get("TCC_EA0_WRREQ_WRITE_DRAM_32B_sum")
+            rds = f"{32*sum(rd)/len(rd)/1e9:.2f}" if rd else "-"
+            wds = f"{32*sum(wd)/len(wd)/1e9:.2f}" if wd else "-"
             ds = sorted(dur[k])
-            print(f"| `{k}` | {ds[len(ds)//2]:.1f} | {fs} | {ws} | {hr} |")
+            print(f"| `{k}` | {ds[len(ds)//2]:.1f} | {fs} | {ws} | {hr} | {rds} | {wds} |")
         print("\nFETCH_SIZE/WRITE_SIZE are reported in KB by rocprofv3 (shown here as GB). On gfx950 FETCH_SIZE"
-              " reads ~1/2 of the bytes of 16-B/lane streaming loads (MI355X_MICROARCH.md §HBM); compare ratios.")
+              " reads ~1/2 of the bytes of 16-B/lane streaming loads (MI355X_MICROARCH.md §HBM); compare ratios."
+              " L2->fabric columns: TCC_EA0_{RDREQ,WRREQ_WRITE}_DRAM_32B x 32 B (calibrated exact on a copy kernel;"
+              " includes Infinity-Cache hits), averaged over the profiled passes.")
 
 
 if __name__ == "__main__":
