@@ -54,6 +54,7 @@ struct Args {
   std::string report = "text";
   bool verify = false;
   bool rhs_set = false;
+  bool format_set = false, recurrence_set = false;
   std::string resume;  // checkpoint prefix to resume from
 };
 
@@ -90,6 +91,7 @@ Args parse(int argc, char** argv) {
                      : (v == "sell16" || v == "sell64-d16") ? 2
                      : (v == "sellc8" || v == "sell64-c8") ? 3
                                                             : 0;
+      a.format_set = true;
     }
     else if (f == "--no-overlap") a.opt.overlap = false;
     else if (f == "--no-graph") a.opt.use_graph = false;
@@ -108,6 +110,7 @@ Args parse(int argc, char** argv) {
     else if (f == "--recurrence") {
       std::string v = need(i);
       a.opt.recurrence = (v == "single" || v == "fused1" || v == "1") ? 1 : 0;
+      a.recurrence_set = true;
     }
     else if (f == "--window") {
       std::string v = need(i);
@@ -131,6 +134,10 @@ Args parse(int argc, char** argv) {
     if (a.nnz_per_row > 0) a.spec.density = std::min(1.0, std::max(0.0, (a.nnz_per_row - 1.0) / (2.0 * a.spec.band)));
   }
   if (a.spec.kind != ProblemKind::Demo && !a.rhs_set) a.spec.rhs = RhsKind::Random;
+  // generated problems default to the fast path (SELL-64/c8, falls back to d16 / plain SELL; the
+  // single-reduction form); the built-in demo keeps the reference's CSR and two-reduction order
+  if (a.spec.kind != ProblemKind::Demo && !a.format_set) a.opt.format = 3;
+  if (a.spec.kind != ProblemKind::Demo && !a.recurrence_set) a.opt.recurrence = -1;
   if (a.spec.kind != ProblemKind::Demo && a.spec.N == 3 && a.spec.kind != ProblemKind::RandomSPD) a.spec.N = 1024;
   return a;
 }

@@ -27,7 +27,9 @@ def _parser() -> argparse.ArgumentParser:
     ap.add_argument("--maxit", type=int, default=2000)
     ap.add_argument("--tol", type=float, default=1e-7)
     ap.add_argument("--check-every", type=int, default=32)
-    ap.add_argument("--format", default="csr", choices=["csr", "sell", "sell16", "sellc8"])
+    ap.add_argument("--format", default=None, choices=["csr", "sell", "sell16", "sellc8"],
+                    help="default: csr for the demo (reference layout), sellc8 for generated problems")
+    ap.add_argument("--rtol", type=float, default=0.0, help="> 0: stop on ||r|| < rtol * ||b||")
     ap.add_argument("--recurrence", type=int, default=-1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
@@ -58,14 +60,16 @@ def main(argv=None) -> int:
         if args.device == "cpu":
             C = mcg.native()
             o = C.CgOptions(maxit=args.maxit, tol=args.tol)
+            o.rtol = args.rtol
             res = (C.cpu_cg_partitioned(spec.native(), args.sim_ranks, o) if args.sim_ranks > 1
                    else C.cpu_cg(spec.native(), o))
             x = res["x"]
             rank = 0
         else:
             s = mcg.CGSolver(spec, maxit=args.maxit, tol=args.tol, check_every=args.check_every,
-                             overlap=not args.no_overlap, use_graph=not args.no_graph, format=args.format,
-                             recurrence=args.recurrence, checkpoint_every=args.checkpoint_every,
+                             overlap=not args.no_overlap, use_graph=not args.no_graph,
+                             format=args.format or ("csr" if args.problem == "demo" else "sellc8"),
+                             recurrence=args.recurrence, rtol=args.rtol, checkpoint_every=args.checkpoint_every,
                              checkpoint_path=args.checkpoint)
             if args.resume:
                 s.load_checkpoint(args.resume)
