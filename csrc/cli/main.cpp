@@ -81,6 +81,7 @@ Args parse(int argc, char** argv) {
     else if (f == "--maxit") a.opt.maxit = std::stoi(need(i));
     else if (f == "--tol") a.opt.tol = std::stod(need(i));
     else if (f == "--rtol") a.opt.rtol = std::stod(need(i));
+    else if (f == "--watchdog") a.opt.watchdog_seconds = std::stod(need(i));
     else if (f == "--nnz-per-row") a.nnz_per_row = std::stod(need(i));
     else if (f == "--check-every") a.opt.check_every = std::stoi(need(i));
     else if (f == "--fixed-iters") a.fixed_iters = std::stoi(need(i));

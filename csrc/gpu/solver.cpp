@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <thread>
 
 #include "mcg/check.hpp"
 #include "mcg/trace.hpp"
@@ -553,6 +554,29 @@ void GpuCgSolver::synchronize() {
   if (use_comm_) comm_->check_async();
 }
 
+// Host wait on a poll event.  With a watchdog it polls (checking RCCL async errors) and gives
+// up after opt_.watchdog_seconds without the event completing: a hung peer or collective then
+// surfaces as an error on every rank instead of a silent hang.
+void GpuCgSolver::wait_bounded_(hipEvent_t ev) {
+  if (opt_.watchdog_seconds <= 0) {
+    MCG_HIP(hipEventSynchronize(ev), "event synchronize failed");
+    return;
+  }
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) MCG_HIP(q, "event synchronize failed");
+    if (use_comm_) comm_->check_async();
+    if (std::chrono::duration<double>(clk::now() - t0).count() > opt_.watchdog_seconds) {
+      if (use_comm_) comm_->abort();
+      fail("watchdog: no progress", "poll interval exceeded " + std::to_string(opt_.watchdog_seconds) + " s");
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 CgResult GpuCgSolver::solve(bool resume) {
   trace::Range tr_("mcg.solve");
   if (!resume) reset();
@@ -567,7 +591,7 @@ CgResult GpuCgSolver::solve(bool resume) {
             "memcpy from device to host failed(state)");
     MCG_HIP(hipEventRecord(ev_poll_[c & 1], s0_), "event record failed");
     if (c > 0) {
-      MCG_HIP(hipEventSynchronize(ev_poll_[(c - 1) & 1]), "event synchronize failed");
+      wait_bounded_(ev_poll_[(c - 1) & 1]);
       if (host_st_[(c - 1) & 1].done) break;
       if (use_comm_) comm_->check_async();
     }

@@ -47,6 +47,8 @@ struct CgOptions {
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   int force_idx64 = 0;       // test hook: int64 row pointers even when int32 would do
   int inject_nan_at = -1;    // fault-injection hook: poison r at this iteration (breakdown detection test)
+  double watchdog_seconds = 0.0;  // > 0: solve() fails (and aborts the communicator) if one poll interval
+                                  // makes no progress for this long (bounded host wait)
 };
 
 struct CgResult {

@@ -54,6 +54,8 @@ class Communicator {
   virtual void check_async() {}
   // whether the solver may capture this communicator's calls into a hipGraph
   virtual bool graph_capturable() const { return true; }
+  // tear down outstanding collectives after a fatal error (watchdog)
+  virtual void abort() {}
 };
 
 class Comm final : public Communicator {
@@ -72,7 +74,7 @@ class Comm final : public Communicator {
   // generic device-buffer collectives used by gathers / tests
   void allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream);
   void broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream);
-  void abort();
+  void abort() override;
 
  private:
   int rank_, world_;

@@ -90,6 +90,7 @@ class GpuCgSolver {
   void enqueue_spmv_(int k, int which, int final_mode);  // which: 0 all, 1 interior, 2 boundary
   void enqueue_f1_(int k, int which, int final_mode);    // single-reduction fused pass
   void enqueue_halo_f1_(int k, hipStream_t s);            // ghosts iteration k of the single-reduction form reads
+  void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
   void capture_pair_();
   void inject_fault_(int k);

@@ -168,6 +168,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("maxit", &CgOptions::maxit)
       .def_readwrite("tol", &CgOptions::tol)
       .def_readwrite("rtol", &CgOptions::rtol)
+      .def_readwrite("watchdog_seconds", &CgOptions::watchdog_seconds)
       .def_readwrite("check_every", &CgOptions::check_every)
       .def_readwrite("overlap", &CgOptions::overlap)
       .def_readwrite("use_graph", &CgOptions::use_graph)

@@ -96,3 +96,14 @@ def test_roctx_tracing_enabled_run(mcg):
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, MCG_TRACE="1"))
     assert p.returncode == 0, p.stderr
+
+
+def test_watchdog_bounded_wait(mcg):
+    """--watchdog: a poll interval that makes no progress within the bound fails loudly; a
+    generous bound changes nothing."""
+    spec = mcg.make_problem("poisson2d", n=2048)
+    ok = mcg.CGSolver(spec, maxit=64, check_every=16, watchdog_seconds=600.0).solve()
+    ref = mcg.CGSolver(spec, maxit=64, check_every=16).solve()
+    assert ok["iterations"] == ref["iterations"] == 64 and ok["rnorm"] == ref["rnorm"]
+    with pytest.raises(Exception, match="watchdog"):
+        mcg.CGSolver(spec, maxit=2000, check_every=256, watchdog_seconds=1e-9, use_graph=False).solve()
