@@ -14,6 +14,7 @@
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
 //   --spmv-variant 0|1|2|3  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
 //   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off  --window auto|on|off
+//   --carry auto|on|off (line-carry stencil pass)
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
 //   --print-x auto|yes|no  --report text|json  --verify
 // Multi-GPU runs use one host thread per GPU inside this process (no MPI in
@@ -116,6 +117,10 @@ Args parse(int argc, char** argv) {
     else if (f == "--window") {
       std::string v = need(i);
       a.opt.window = v == "auto" ? -1 : ((v == "on" || v == "1") ? 1 : 0);
+    }
+    else if (f == "--carry") {
+      std::string v = need(i);
+      a.opt.carry = v == "auto" ? -1 : ((v == "on" || v == "1") ? 1 : 0);
     }
     else if (f == "--interleave") {
       std::string v = need(i);

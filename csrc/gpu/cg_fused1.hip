@@ -314,6 +314,272 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int6
   block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
 }
 
+// ---------------------------------------------------------------------------
+// Line-carry single-reduction pass: SELL-64/d16 or /c8 with the interleaved {r, Ap} layout,
+// every slice width <= U, the launch's slices whole grid lines of S slices (structured-grid
+// stencils: S = line (2-D) or plane (3-D) length / 64).
+//
+// In the generic pass every row's vector operands are read three times: as the +L neighbour
+// of the row one line up (L = 64 S rows), as the row itself, and as the -L neighbour of the
+// row one line down.  Those reads are L rows apart, issued by waves anywhere on the chip, and
+// about half of them miss the XCD's L2 (profiles/r1_poisson16384_1gpu_final.md: 16 GB of
+// L2->fabric reads per pass against 7.8 GB of model traffic).  Here a wave walks DOWN one
+// column of slices (s, s + S, s + 2S, ...): the slice it reads as the +L neighbour at line l
+// is its own slice at line l + 1 and the -L neighbour at line l + 2, so p_k of the previous,
+// current and next line stay in registers and each row's operands come from memory once.
+// The +-1 neighbours are the neighbouring lanes' p_k (a shuffle; lanes 0 / 63 load the row
+// across the slice edge with the line's operands).  So in the steady state every operand is
+// in registers and the only loads are the prefetches (operands PD lines ahead, codes two):
+// gathering +-1 from memory read each vector line twice from the fabric (the line, loaded PD
+// steps earlier, had left the XCD's L2) and exposed a memory latency per step.  Offsets that
+// are not carried (a run's first / last line, +-N in 3-D) take a slow path that gathers from
+// memory.
+// Every value is the generic pass's fma sequence; only the blocking of the dot-product
+// partials differs (fixed per launch geometry: still bitwise reproducible run to run).
+template <int CM, int U, int PD, bool PAIR, bool GEN>
+__global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+                                                     double* __restrict__ partials, int pstride,
+                                                     const CgState* __restrict__ st, double tol, int first,
+                                                     int check) {
+  __shared__ double2 s_dict[CM == 2 ? 256 : 1];
+  if (st->done) return;
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (sc.conv) return;
+  if constexpr (CM == 2) {
+    for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
+    __syncthreads();
+  }
+  const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  const double* __restrict__ po = v.p_old;
+  double* __restrict__ pn = v.p_new;
+  double* __restrict__ x = v.x;
+  const double2* __restrict__ rao = v.ra_old;
+  double2* __restrict__ ran = v.ra_new;
+  const double* __restrict__ svals = S.vals;
+  const int lane = threadIdx.x & 63;
+  const int64_t SS = tr.strip;              // slices per line
+  const int32_t LO = (int32_t)(SS * 64);    // the carried column offset: one line
+  const int64_t nl = tr.nt0 / SS;           // lines in the launch
+  const int64_t ext = v.ext_len;
+  // XCD-aware wave numbering (speed only): blocks b and b + 8 are observed to share an XCD, so
+  // consecutive logical waves -- neighbouring columns of the same lines -- run on one XCD
+  const int64_t nb = gridDim.x, blk = blockIdx.x;
+  const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;
+  const int64_t nw = nb * kWaves;
+  const int64_t gw = lb * kWaves + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t runs = nw > SS ? nw / SS : 1;  // line chunks per column
+  const int64_t chunk = (nl + runs - 1) / runs;
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+  // operands of a line (prefetched PD lines ahead): {r_{k-1}, Ap_{k-1}} and p_{k-1}
+  struct Raw {
+    double2 q;
+    double pold;
+  };
+  // the rows just before / after a slice (the +-1 neighbours of lanes 0 / 63, in the adjacent
+  // slice column): wave-uniform addresses through a constant-address-space view -> scalar loads
+  // (SGPRs, the lgkm counter: no vector registers, no queueing behind the vector prefetches)
+  struct Edge {
+    double2 qd, qu;
+    double pd, pu;
+  };
+  // paired x updates (odd passes): p_{k-2} (read before this pass overwrites it) and x
+  struct XP {
+    double pkm2, xo;
+  };
+  // a slice's codes: c8 bytes packed four per register (the dictionary is re-read from LDS
+  // when the row sums are formed); d16 offsets + values
+  struct Codes {
+    uint32_t pk[CM == 2 ? (U + 3) / 4 : 1];
+    int16_t d[CM == 2 ? 1 : U];
+    double v[CM == 2 ? 1 : U];
+    int w;
+  };
+  typedef __attribute__((address_space(4))) const double KD;
+  KD* __restrict__ k_ra = (KD*)rao;
+  KD* __restrict__ k_po = (KD*)po;
+  // p_k = r_k + b p_{k-1} from the old values (the generic pass's gather, bit for bit)
+  auto pk_of = [&](double2 q, double pold) { return fma(b, pold, fma(na, q.y, q.x)); };
+  // entry u of a slice: {value, column offset from the row's own column}
+  auto entry = [&](const Codes& c, int u, double& val) -> int32_t {
+    if constexpr (CM == 2) {
+      const double2 q = s_dict[(c.pk[u >> 2] >> (8 * (u & 3))) & 255u];
+      val = q.x;
+      return (int32_t)__double_as_longlong(q.y);
+    } else {
+      val = c.v[u];
+      return (int32_t)c.d[u];
+    }
+  };
+  // Addressing: every per-line access is a wave-uniform base (SGPRs) + the lane, so the loads
+  // are saddr + voffset forms and the per-step scalar work is a few adds.  Loads are never
+  // conditional: line indices are clamped to lines that exist (values past the run are unused).
+  const int32_t ext32 = (int32_t)v.ext_len;
+  for (int64_t job = gw; job < SS * runs; job += nw) {
+    const int64_t col = job % SS, l0 = (job / SS) * chunk;
+    const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
+    if (l0 >= l1) continue;
+    const int64_t sl0 = tr.b0 + l0 * SS + col;
+    const int32_t e0 = (int32_t)(own + sl0 * 64);  // ext index of lane 0's row at line l0
+    const int32_t i0 = (int32_t)(sl0 * 64);        // owned index of the same row
+    const int32_t n_run = (int32_t)(l1 - l0);
+    // lines (relative to l0) whose operands exist: [-1 if the line before exists, la]
+    const int32_t la = (e0 + n_run * LO + 63 < ext32) ? n_run : n_run - 1;
+    const bool prev_exists = e0 - LO >= 0;
+    auto ebase = [&](int32_t m) { return e0 + m * LO; };             // ext index, line l0 + m
+    auto sbase = [&](int32_t m) { return sl0 + (int64_t)m * SS; };   // slice, line l0 + m
+    auto load_raw = [&](int32_t m, Raw& r) {
+      const int32_t eb = ebase(m < la ? m : la);
+      r.q = (rao + eb)[lane];
+      r.pold = (po + eb)[lane];
+    };
+    auto load_edge = [&](int32_t m, Edge& r) {  // m <= n_run - 1 (owned lines)
+      const int32_t eb = ebase(m);
+      const int32_t dn = eb >= 1 ? eb - 1 : 0, up = eb + 64 < ext32 ? eb + 64 : ext32 - 1;
+      r.qd = make_double2(k_ra[2 * dn], k_ra[2 * dn + 1]);
+      r.pd = k_po[dn];
+      r.qu = make_double2(k_ra[2 * up], k_ra[2 * up + 1]);
+      r.pu = k_po[up];
+    };
+    auto edge_ok = [&](int32_t m) {  // lanes 0 / 63: the row across the slice edge exists
+      const int32_t eb = ebase(m);
+      return lane == 0 ? eb >= 1 : eb + 64 < ext32;
+    };
+    auto load_xp = [&](int32_t m, XP& r) {  // owned lines only
+      if constexpr (PAIR) {
+        const int32_t mm = m < n_run - 1 ? m : n_run - 1;
+        r.pkm2 = (pn + ebase(mm))[lane];
+        r.xo = (x + i0 + mm * LO)[lane];
+      }
+    };
+    auto load_codes = [&](int32_t m, Codes& c) {  // owned lines only
+      const int64_t sl = sbase(m < n_run - 1 ? m : n_run - 1);
+      const int64_t base = S.slice_ptr[sl];
+      c.w = (int)((S.slice_ptr[sl + 1] - base) >> 6);
+      if constexpr (CM == 2) {
+        const uint8_t* __restrict__ cp = S.codes + base;
+#pragma unroll
+        for (int q = 0; q < (U + 3) / 4; ++q) c.pk[q] = 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) c.pk[u >> 2] |= (uint32_t)cp[64 * u + lane] << (8 * (u & 3));
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = base + lane + 64 * (u < c.w ? u : c.w - 1);
+          c.d[u] = S.dcols[j];
+          c.v[u] = svals[j];
+        }
+      }
+    };
+    // prologue: the line before the run (if it exists), operands of lines 0 .. PD, codes of
+    // lines 0, 1, edges + x / p_{k-2} of line 0
+    Raw r0, rq[PD];
+    load_raw(0, r0);
+    bool pv = prev_exists;
+    double pr_pk = 0.0;
+    {
+      const int32_t eb = prev_exists ? e0 - LO : e0;
+      pr_pk = pk_of((rao + eb)[lane], (po + eb)[lane]);
+    }
+    Edge ed0;
+    load_edge(0, ed0);
+    XP x0{0.0, 0.0};
+    load_xp(0, x0);
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_raw(1 + d, rq[d]);
+    Codes c0, c1;
+    load_codes(0, c0);
+    load_codes(1, c1);
+    double o_rk = fma(na, r0.q.y, r0.q.x);
+    double o_pk = fma(b, r0.pold, o_rk);
+    double o_pold = r0.pold;
+    double o_epk = lane == 0 ? pk_of(ed0.qd, ed0.pd) : pk_of(ed0.qu, ed0.pu);  // lanes 0 / 63
+    bool o_eok = edge_ok(0);
+    for (int32_t m = 0; m < n_run; ++m) {
+      const bool nv = m + 1 <= la;
+      // 1. loads, in the order they are waited for: the next line's edges (scalar) and
+      //    x / p_{k-2}, then the codes of line m + 2 and the operands of line m + 1 + PD
+      Edge ed1;
+      load_edge(m + 1 < n_run ? m + 1 : m, ed1);
+      XP x1{0.0, 0.0};
+      load_xp(m + 1, x1);
+      Codes c2;
+      load_codes(m + 2, c2);
+      Raw rn;
+      load_raw(m + 1 + PD, rn);
+      // 2. this line's row sums from registers: own row, next / previous line (carried), row
+      //    +- 1 (the neighbouring lanes; lanes 0 / 63 the edge rows).  GEN: an entry that is
+      //    none of these (other offsets such as +-N in 3-D) sends the wave down a slow path
+      //    that redoes the sums with memory gathers; !GEN: the dictionary has no such offset.
+      const double n_pk = pk_of(rq[0].q, rq[0].pold);
+      const double sh_up = __shfl_down(o_pk, 1, 64);
+      const double sh_dn = __shfl_up(o_pk, 1, 64);
+      const double up_pk = lane == 63 ? o_epk : sh_up;  // row + 1
+      const double dn_pk = lane == 0 ? o_epk : sh_dn;   // row - 1
+      const bool up_ok = lane < 63 || o_eok, dn_ok = lane > 0 || o_eok;
+      // branch-free (selects): per-lane if / else chains become exec-mask branches
+      auto reg_value = [&](int32_t off, double& g) -> bool {
+        const bool k0 = off == 0, k1 = (off == 1) & up_ok, k2 = (off == -1) & dn_ok;
+        const bool k3 = nv & (off == LO), k4 = pv & (off == -LO);
+        // each select pinned in a register (an opaque asm operand): left alone, the optimiser
+        // turns the chain into a stack table of the candidates + a computed-address load
+        double t = k3 ? n_pk : pr_pk;
+        asm volatile("" : "+v"(t));
+        t = k2 ? dn_pk : t;
+        asm volatile("" : "+v"(t));
+        t = k1 ? up_pk : t;
+        asm volatile("" : "+v"(t));
+        g = k0 ? o_pk : t;
+        return k0 | k1 | k2 | k3 | k4;
+      };
+      double sum = 0.0;
+      bool all_reg = true;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        double val, g = 0.0;
+        const int32_t off = entry(c0, u, val);
+        all_reg = (u >= c0.w || reg_value(off, g)) && all_reg;
+        sum = (u < c0.w) ? fma(val, g, sum) : sum;
+      }
+      const int32_t eb = ebase(m);
+      if constexpr (GEN) {
+        if (__builtin_expect(!__all(all_reg), 0)) {
+          const int32_t rowcol = eb + lane;
+          sum = 0.0;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            double val, g = 0.0;
+            const int32_t off = entry(c0, u, val);
+            if (u < c0.w && !reg_value(off, g)) g = pk_of(rao[rowcol + off], po[rowcol + off]);
+            sum = (u < c0.w) ? fma(val, g, sum) : sum;
+          }
+        }
+      }
+      st_stream(&(ran + eb)[lane], make_double2(o_rk, sum));
+      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, x0.pkm2, x0.xo)));
+      st_stream(&(pn + eb)[lane], o_pk);
+      s_pap = fma(o_pk, sum, s_pap);
+      s_rap = fma(o_rk, sum, s_rap);
+      s_apap = fma(sum, sum, s_apap);
+      s_rr = fma(o_rk, o_rk, s_rr);
+      // 3. rotate the carried lines and the prefetch pipeline
+      pr_pk = o_pk;
+      pv = true;
+      o_rk = fma(na, rq[0].q.y, rq[0].q.x);
+      o_pk = n_pk;
+      o_pold = rq[0].pold;
+      o_epk = lane == 0 ? pk_of(ed1.qd, ed1.pd) : pk_of(ed1.qu, ed1.pu);
+      o_eok = edge_ok(m + 1);
+#pragma unroll
+      for (int d = 0; d + 1 < PD; ++d) rq[d] = rq[d + 1];
+      rq[PD - 1] = rn;
+      x0 = x1;
+      c0 = c1;
+      c1 = c2;
+    }
+  }
+  block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
+}
+
 __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __restrict__ partials, int pstride, int np,
                                                             CgState* __restrict__ st, int mode, int check, int first,
                                                             double tol) {
@@ -576,6 +842,50 @@ void cg_fused1_win(int cm, int param, const SellDev& S, const F1Vectors& v, int6
   else { if (ra) MCG_WU(1, true); else MCG_WU(1, false); }
 #undef MCG_WU
 #undef MCG_W
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+
+void cg_fused1_carry(int cm, int param, int depth, bool general, const SellDev& S, const F1Vectors& v,
+                     int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
+                     const CgState* st, double tol, int first, int check, int k, hipStream_t stream) {
+  if (tr.ntiles == 0 || grid == 0) return;
+  MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0, "line-carry pass needs whole grid lines");
+  MCG_CHECK(v.ra_old != nullptr && (cm == 1 || cm == 2) && param >= 4 && param <= 8,
+            "line-carry pass needs SELL-64 d16/c8 with interleaved pairs");
+  MCG_CHECK(depth == 2 || depth == 3, "line-carry prefetch depth must be 2 or 3");
+  MCG_CHECK(general || cm == 2, "the specialised line-carry pass needs the c8 dictionary");
+  const bool pair = (k & 1) != 0;
+#define MCG_C(CM, U, PD, PAIR, GEN)                                                                          \
+  hipLaunchKernelGGL((k_cg_f1_carry<CM, U, PD, PAIR, GEN>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
+                     tr, partials, pstride, st, tol, first, check)
+#define MCG_CP(CM, U, PD, GEN)                         \
+  do {                                                 \
+    if (pair) MCG_C(CM, U, PD, true, GEN);             \
+    else MCG_C(CM, U, PD, false, GEN);                 \
+  } while (0)
+#define MCG_CD(CM, U, GEN)                             \
+  do {                                                 \
+    if (depth == 2) MCG_CP(CM, U, 2, GEN);             \
+    else MCG_CP(CM, U, 3, GEN);                        \
+  } while (0)
+#define MCG_CU(CM, GEN)                       \
+  do {                                        \
+    if (param == 4) MCG_CD(CM, 4, GEN);       \
+    else if (param == 5) MCG_CD(CM, 5, GEN);  \
+    else if (param == 6) MCG_CD(CM, 6, GEN);  \
+    else if (param == 7) MCG_CD(CM, 7, GEN);  \
+    else MCG_CD(CM, 8, GEN);                  \
+  } while (0)
+  if (cm == 2) {
+    if (general) MCG_CU(2, true);
+    else MCG_CU(2, false);
+  } else {
+    MCG_CU(1, true);
+  }
+#undef MCG_CU
+#undef MCG_CD
+#undef MCG_CP
+#undef MCG_C
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 

@@ -137,10 +137,16 @@ void GpuCgSolver::setup() {
       c8_ = kern::sell_dict_build(sell_view(), dict, nv, nd, s0_);
       if (c8_) {
         ndict_ = (int)dict.size();
+        dict_offsets_.clear();
+        for (int q = 0; q < nd; ++q) {  // dict[vi * nd + di].y = bits of offset di
+          long long off;
+          std::memcpy(&off, &dict[q].y, sizeof(off));
+          dict_offsets_.push_back((int64_t)off);
+        }
         dict_.allocate(dict.size(), "A");
         MCG_HIP(hipMemcpy(dict_.get(), dict.data(), dict.size() * sizeof(double2), hipMemcpyHostToDevice),
                 "memcpy from host to device failed(A)");
-        codes_.allocate(total, "A", 64);
+        codes_.allocate(total, "A", 512);  // the line-carry pass reads 8 entries past a slice's last
         kern::sell_to_c8(sell_view(), dict_.get(), nv, nd, codes_.get(), s0_);
         MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
         cols_.release();
@@ -254,6 +260,34 @@ void GpuCgSolver::setup() {
     apply(tr_all_);
     apply(tr_int_);
     info_.strip = tr_all_.strip;
+  }
+  {
+    // line-carry pass: whole 64-row slices per grid line (2-D) / plane (3-D), the stencil path's
+    // format and layout; applies to a launch whose slices are one range of whole lines
+    const int64_t gl = partition_granule(spec_);
+    const bool ok = opt_.recurrence == 1 && opt_.format == 1 && (d16_ || c8_) && opt_.interleave == 1 &&
+                    opt_.sell_slices != 2 && win_doubles_ == 0 && info_.max_row_len <= 8 &&
+                    info_.spmv_param >= info_.max_row_len && info_.spmv_param >= 4 && gl > 1 && gl % 64 == 0 &&
+                    n % gl == 0 && L_.row_begin % gl == 0;
+    MCG_CHECK(opt_.carry != 1 || ok,
+              "line-carry pass needs SELL d16/c8, interleaved pairs, rows <= param <= 8 and whole 64-row grid lines");
+    if (ok && opt_.carry != 0) {
+      const int64_t S = gl / 64;
+      const int g = kern::num_cus() * std::max(1, opt_.carry_blocks_per_cu);
+      auto apply = [&](TileRanges& t, int& grid) {
+        if (t.ntiles == 0 || t.nt0 != t.ntiles || t.b0 % S != 0 || t.nt0 % S != 0 || t.nt0 / S < 2) return false;
+        t.strip = (int32_t)S;
+        grid = g;
+        return true;
+      };
+      // the specialised pass (no slow path) when every stored offset is carried: 0, +-1, +-one line
+      carry_general_ = !c8_;
+      for (int64_t off : dict_offsets_)
+        if (off != 0 && off != 1 && off != -1 && off != 64 * S && off != -64 * S) carry_general_ = true;
+      carry_all_ = apply(tr_all_, g_all_);
+      if (use_halo_ && opt_.overlap) carry_int_ = apply(tr_int_, g_int_);
+    }
+    info_.carry = carry_all_ || carry_int_;
   }
   g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
@@ -370,11 +404,17 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   kern::F1Vectors v{r_old.get(), ap_old.get(), p_[(k + 1) & 1].get(), r_new.get(), ap_new.get(), p_[k & 1].get(),
                     x_.get()};
   v.p_fix = p_[1].get();
+  v.ext_len = L_.ext_len;
   if (opt_.interleave == 1) {
     v.ra_old = reinterpret_cast<const double2*>(ra_[(k + 1) & 1].get());
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
   }
   const SellDev S = sell_view();
+  if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
+    kern::cg_fused1_carry(c8_ ? 2 : 1, info_.spmv_param, opt_.carry_depth, carry_general_, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
+                          opt_.tol, first, check, k, s0_);
+    return;
+  }
   if (win_doubles_ > 0 && !final_mode) {
     kern::cg_fused1_win(d16_ ? 1 : 0, info_.spmv_param, S, v, L_.own_off, tr, win_.get(), win_doubles_, part,
                         pstride_, grid, st_.get(), opt_.tol, first, check, k, s0_);

@@ -41,6 +41,11 @@ struct CgOptions {
   int pipeline = 0;          // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
                              // Off by default: 2-D equal, 3-D slower (310 vs 336 it/s, profiles/sweep_pipeline.log)
+  int carry = 0;             // single-reduction SELL d16/c8 + interleave on a structured grid (whole 64-row slices
+                             // per grid line / plane): line-carry pass — a wave walks down a column of slices and
+                             // keeps the +-one-line neighbours' p_k in registers; -1 = when applicable, 1 = on
+  int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
+  int carry_depth = 3;          // line-carry pass: operand prefetch depth in lines (2 or 3; 3 measured faster)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)

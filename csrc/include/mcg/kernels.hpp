@@ -175,6 +175,7 @@ struct F1Vectors {
   // overwritten) and a_{k-1} p_{k-1}; even passes leave x alone (-4 B/row/iteration).  p_fix =
   // the parity-1 p buffer, for the one-term catch-up when convergence latches after an even pass.
   const double* p_fix = nullptr;
+  int64_t ext_len = 0;  // ext-layout length of r / Ap / p (bounds of the line-carry pass's edge loads)
 };
 // `k`: pass index (its parity selects the paired x update; final mode: m = k)
 template <typename IdxT>
@@ -183,6 +184,15 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
                int first, int check, int final_mode, int k, hipStream_t stream,
                bool pipe = false /* software-pipelined stencil pass: SELL d16/c8 + interleaved, every slice
                                     width <= param */);
+// Line-carry variant for structured-grid stencils (SELL d16/c8 + interleaved {r, Ap}, every
+// slice width <= param): `slices.strip` = S slices per grid line (the carried column offset is
+// one line, 64 S rows), the launch one range of whole lines; a wave walks down one column of
+// slices and keeps the previous / current / next line's p_k in registers.
+void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8 */, int param, int depth /* operand prefetch, lines */,
+                     bool general /* false: every dictionary offset is 0, +-1 or +-one line (no slow path) */,
+                     const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& slices,
+                     double* partials, int pstride, int grid, const CgState* st, double tol, int first, int check,
+                     int k, hipStream_t stream);
 // Windowed variant for long banded rows: 1024-row chunks (16 slices) stage p_k for their
 // column window [win[2c], win[2c+1]) in LDS once, the SpMV gathers from LDS.
 constexpr int kWinRows = 1024;

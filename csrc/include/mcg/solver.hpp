@@ -50,6 +50,7 @@ struct SolverInfo {
   int window = 0;  // LDS window width (doubles) of the windowed pass; 0 = off
   bool pipeline = false;
   int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
+  bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
 };
 
 class GpuCgSolver {
@@ -125,6 +126,9 @@ class GpuCgSolver {
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
   int win_doubles_ = 0;         // 0 = windowed pass off
   bool pipe_ = false;           // software-pipelined stencil pass
+  bool carry_all_ = false, carry_int_ = false;  // line-carry pass for the all-rows / interior launch
+  bool carry_general_ = true;                   // line-carry pass with the memory-gather slow path
+  std::vector<int64_t> dict_offsets_;           // SELL-64/c8: the distinct column offsets
   SellDev sell_view() const {
     SellDev s{slice_ptr_.get(), cols_.get(), vals_.get(), L_.n_local()};
     s.dcols = dcols_.get();

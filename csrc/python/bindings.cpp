@@ -154,6 +154,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("window", &CgOptions::window)
       .def_readwrite("pipeline", &CgOptions::pipeline)
       .def_readwrite("strip", &CgOptions::strip)
+      .def_readwrite("carry", &CgOptions::carry)
+      .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
+      .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
@@ -295,6 +298,7 @@ PYBIND11_MODULE(_C, m) {
         d["window"] = i.window;
         d["pipeline"] = i.pipeline;
         d["strip"] = i.strip;
+        d["carry"] = i.carry;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;

@@ -111,3 +111,20 @@ def test_local_ranks_demo_more_ranks_than_rows_per_rank(mcg):
     out = C.run_local_ranks(mcg.make_problem("demo").native(), _opts(mcg), 2, 0, False)
     assert "".join("%f\n" % v for v in out["x"]) == "0.500000\n0.750000\n1.000000\n"
     assert out["ranks"][0]["iterations"] == 3
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_ranks_line_carry_interior(mcg, world):
+    """Line-carry pass on the interior launch (boundary lines through the generic pass after the
+    halo) across ranks vs the CPU reference."""
+    spec = mcg.make_problem("poisson2d", n=192)
+    C = mcg.native()
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=1e-7))
+    o = _opts(mcg, format="sellc8", recurrence=1, check_every=4)
+    o.carry = 1
+    out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    its = {r["iterations"] for r in out["ranks"]}
+    assert len(its) == 1, its
+    assert abs(its.pop() - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])

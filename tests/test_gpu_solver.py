@@ -185,3 +185,39 @@ def test_relative_tolerance_matches_cpu(mcg, recurrence, fmt):
     cpu = C.cpu_cg(spec.native(), o)
     out = mcg.CGSolver(spec, format=fmt, recurrence=recurrence, tol=1e-30, rtol=1e-8, check_every=8).solve()
     assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 2
+
+
+@pytest.mark.parametrize("fmt", ["sell16", "sellc8"])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=128)), ("poisson3d", dict(n=16))])
+def test_line_carry_pass_matches_generic(mcg, fmt, problem, kw):
+    """Line-carry pass (a wave walks down one slice column; the +-one-line neighbours' p_k stay in
+    registers) vs the generic pass: the same per-row arithmetic, dot-product partials blocked
+    differently -> fixed-iteration residuals agree to rounding, solutions to the solver tolerance."""
+    spec = mcg.make_problem(problem, rhs="random", **kw)
+    a = mcg.CGSolver(spec, format=fmt, recurrence=1, carry=1, check_every=8)
+    b = mcg.CGSolver(spec, format=fmt, recurrence=1, carry=0, check_every=8)
+    assert a.info["carry"] and not b.info["carry"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and rb["converged"] and abs(ra["iterations"] - rb["iterations"]) <= 1
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-6, atol=1e-6 * np.abs(rb["x_local"]).max())
+    assert a.true_residual_norm() < 1e-6
+    outs = []
+    for s in (a, b):
+        s.reset()
+        s.run(24)
+        s.finalize()
+        outs.append(s.result())
+    assert outs[0]["iterations"] == outs[1]["iterations"] == 24
+    assert abs(outs[0]["rnorm"] - outs[1]["rnorm"]) <= 1e-9 * outs[1]["rnorm"]
+
+
+def test_line_carry_pass_reproducible_and_auto(mcg):
+    spec = mcg.make_problem("poisson2d", n=256, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=-1).solve()
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=-1).solve()
+    np.testing.assert_array_equal(a["x_local"], b["x_local"])
+    # not applicable (line length not a multiple of 64): auto falls back, on=1 refuses
+    odd = mcg.make_problem("poisson2d", n=100)
+    assert not mcg.CGSolver(odd, format="sellc8", recurrence=1, carry=-1).info["carry"]
+    with pytest.raises(Exception, match="line-carry"):
+        mcg.CGSolver(odd, format="sellc8", recurrence=1, carry=1)
