@@ -284,8 +284,10 @@ void GpuCgSolver::setup() {
       carry_general_ = !c8_;
       for (int64_t off : dict_offsets_)
         if (off != 0 && off != 1 && off != -1 && off != 64 * S && off != -64 * S) carry_general_ = true;
-      carry_all_ = apply(tr_all_, g_all_);
-      if (use_halo_ && opt_.overlap) carry_int_ = apply(tr_int_, g_int_);
+      // auto: only the specialised pass (2-D stencils); with the slow path (3-D's +-N gathers) it
+      // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log)
+      if (opt_.carry == 1 || !carry_general_) carry_all_ = apply(tr_all_, g_all_);
+      if (use_halo_ && opt_.overlap && (opt_.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
     }
     info_.carry = carry_all_ || carry_int_;
   }

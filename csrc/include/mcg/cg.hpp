@@ -41,9 +41,10 @@ struct CgOptions {
   int pipeline = 0;          // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
                              // Off by default: 2-D equal, 3-D slower (310 vs 336 it/s, profiles/sweep_pipeline.log)
-  int carry = 0;             // single-reduction SELL d16/c8 + interleave on a structured grid (whole 64-row slices
+  int carry = -1;            // single-reduction SELL d16/c8 + interleave on a structured grid (whole 64-row slices
                              // per grid line / plane): line-carry pass — a wave walks down a column of slices and
-                             // keeps the +-one-line neighbours' p_k in registers; -1 = when applicable, 1 = on
+                             // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
+                             // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
   int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
   int carry_depth = 3;          // line-carry pass: operand prefetch depth in lines (2 or 3; 3 measured faster)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
