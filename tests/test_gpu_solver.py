@@ -188,7 +188,8 @@ def test_relative_tolerance_matches_cpu(mcg, recurrence, fmt):
 
 
 @pytest.mark.parametrize("fmt", ["sell16", "sellc8"])
-@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=128)), ("poisson3d", dict(n=16))])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=128)), ("poisson2d", dict(n=256)),
+                                        ("poisson3d", dict(n=16))])
 def test_line_carry_pass_matches_generic(mcg, fmt, problem, kw):
     """Line-carry pass (a wave walks down one slice column; the +-one-line neighbours' p_k stay in
     registers) vs the generic pass: the same per-row arithmetic, dot-product partials blocked
