@@ -360,7 +360,6 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int
   const int64_t SS = tr.strip;              // slices per line
   const int32_t LO = (int32_t)(SS * 64);    // the carried column offset: one line
   const int64_t nl = tr.nt0 / SS;           // lines in the launch
-  const int64_t ext = v.ext_len;
   // XCD-aware wave numbering (speed only): blocks b and b + 8 are observed to share an XCD, so
   // consecutive logical waves -- neighbouring columns of the same lines -- run on one XCD
   const int64_t nb = gridDim.x, blk = blockIdx.x;
