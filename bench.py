@@ -171,6 +171,7 @@ def main() -> int:
                 "parallelism": f"rowpart{n_gpus}",
                 "format": info["format"],
                 "recurrence": info["recurrence"],
+                "pass": "line-carry" if info.get("carry") else ("generic, xcd-aware" if info.get("xcd_map") else "generic"),
                 "hipgraph": use_graph,
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,
             },

@@ -31,16 +31,18 @@ struct CgOptions {
   int update_unroll = 1;     // double2 loads in flight per lane in the residual update
   int update_blocks_per_cu = 4;  // grid of the residual update / dot kernels (1024 blocks: best measured)
   int nt_loads = 0;          // non-temporal loads for the matrix streams (direct CSR / SELL engines)
-  int xcd_map = 0;           // XCD-aware contiguous tile regions for the SpMV grid
+  int xcd_map = -1;          // XCD-aware contiguous tile regions for the SpMV grid; -1 = auto (the 3-D stencil's
+                             // generic SELL pass, with a grid sweeping one plane of slices per step)
   int sell_slices = 1;       // SELL engine: slices in flight per wave (1 or 2)
   int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
   int strip = 0;             // SELL: visit slices in vertical strips of this many slices per grid line (each wave
                              // walks down one column); -1 = 2-D stencil line width.  Off by default: measured
                              // slower (241 vs 248 it/s at 16384^2, profiles/sweep_strip_order.log)
-  int pipeline = 0;          // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
+  int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
-                             // Off by default: 2-D equal, 3-D slower (310 vs 336 it/s, profiles/sweep_pipeline.log)
+                             // With the XCD-aware 3-D sweep it is the faster pass (419 vs 383 it/s at 512^3,
+                             // profiles/sweep_xcd_3d.log; in natural order it was slower, sweep_pipeline.log)
   int carry = -1;            // single-reduction SELL d16/c8 + interleave on a structured grid (whole 64-row slices
                              // per grid line / plane): line-carry pass — a wave walks down a column of slices and
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every

@@ -51,6 +51,7 @@ struct SolverInfo {
   bool pipeline = false;
   int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
+  bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
 };
 
 class GpuCgSolver {

@@ -148,7 +148,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
            py::arg("format") = "csr", py::arg("blocks_per_cu") = 0, py::arg("spmv_variant") = -1,
            py::arg("spmv_param") = 0, py::arg("update_unroll") = 1, py::arg("nt_loads") = 0,
-           py::arg("xcd_map") = 0, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
+           py::arg("xcd_map") = -1, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
       .def_readwrite("interleave", &CgOptions::interleave)
       .def_readwrite("window", &CgOptions::window)
@@ -299,6 +299,7 @@ PYBIND11_MODULE(_C, m) {
         d["pipeline"] = i.pipeline;
         d["strip"] = i.strip;
         d["carry"] = i.carry;
+        d["xcd_map"] = i.xcd_map;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
