@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Rehearse the distributed path at the headline size on ONE GPU: P ranks as threads sharing the
+device (LocalComm: D2D halo copies + fixed-order all-reduce), fixed iterations, then every rank's
+true residual ||b - A x|| against the recurrence residual and the P = 1 run.  Correctness only
+(the ranks share one GPU, so no timing is reported).
+
+  python bench/rehearse_ranks.py --n 16384 --iters 40 --world 1 2 8
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import cuda_mpi_parallel_amd as mcg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--problem", default="poisson2d")
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--world", type=int, nargs="+", default=[1, 2, 8])
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    C = mcg.native()
+    spec = mcg.make_problem(args.problem, n=args.n)
+    ref = None
+    for w in args.world:
+        o = C.CgOptions(maxit=1 << 30, tol=-1.0, format="sellc8", recurrence=1, check_every=1 << 30)
+        out = C.run_local_ranks(spec.native(), o, w, args.iters, True)
+        r = out["ranks"]
+        rn = r[0]["rnorm"]
+        tr = max(x["true_rnorm"] for x in r)
+        ok = all(x["iterations"] == args.iters for x in r) and abs(tr - rn) <= 1e-6 * max(tr, 1e-300)
+        if ref is None:
+            ref = rn
+        print(json.dumps({"world": w, "iterations": r[0]["iterations"], "rnorm": rn, "true_rnorm": tr,
+                          "rel_vs_first": abs(rn - ref) / ref, "ok": ok}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
