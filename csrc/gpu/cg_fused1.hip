@@ -336,11 +336,16 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int6
 // memory.
 // Every value is the generic pass's fma sequence; only the blocking of the dot-product
 // partials differs (fixed per launch geometry: still bitwise reproducible run to run).
-template <int CM, int U, int PD, bool PAIR, bool GEN>
+//
+// M2 (3-D stencils, plane carry: the carried "line" is a plane, L = N^2): the +-N neighbours
+// (offset LO2 = N rows: slices N/64 apart in the same plane, worked at the same step by the
+// neighbouring columns' waves on the same XCD) are gathered from the L2 one line ahead, issued
+// before the prefetches, and carried into the step as p_k.
+template <int CM, int U, int PD, bool PAIR, bool GEN, bool M2>
 __global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride,
                                                      const CgState* __restrict__ st, double tol, int first,
-                                                     int check) {
+                                                     int check, int32_t LO2) {
   __shared__ double2 s_dict[CM == 2 ? 256 : 1];
   if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
@@ -469,6 +474,22 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int
         }
       }
     };
+    // M2: p_k of the rows +-LO2 away (clamped indices; values of rows that do not exist are
+    // never used: the matrix has no entry for them)
+    struct Far {
+      double2 qu, qd;
+      double pu, pd;
+    };
+    auto load_far = [&](int32_t m, Far& f) {
+      if constexpr (M2) {
+        const int32_t e = ebase(m < n_run - 1 ? m : n_run - 1) + lane;
+        const int32_t cu = e + LO2 < ext32 ? e + LO2 : ext32 - 1, cd = e - LO2 >= 0 ? e - LO2 : 0;
+        f.qu = rao[cu];
+        f.pu = po[cu];
+        f.qd = rao[cd];
+        f.pd = po[cd];
+      }
+    };
     // prologue: the line before the run (if it exists), operands of lines 0 .. PD, codes of
     // lines 0, 1, edges + x / p_{k-2} of line 0
     Raw r0, rq[PD];
@@ -493,10 +514,20 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int
     double o_pold = r0.pold;
     double o_epk = lane == 0 ? pk_of(ed0.qd, ed0.pd) : pk_of(ed0.qu, ed0.pu);  // lanes 0 / 63
     bool o_eok = edge_ok(0);
+    double o_fu = 0.0, o_fd = 0.0;  // M2: p_k of rows +LO2 / -LO2
+    if constexpr (M2) {
+      Far f0;
+      load_far(0, f0);
+      o_fu = pk_of(f0.qu, f0.pu);
+      o_fd = pk_of(f0.qd, f0.pd);
+    }
     for (int32_t m = 0; m < n_run; ++m) {
       const bool nv = m + 1 <= la;
-      // 1. loads, in the order they are waited for: the next line's edges (scalar) and
-      //    x / p_{k-2}, then the codes of line m + 2 and the operands of line m + 1 + PD
+      // 1. loads, in the order they are waited for: (M2) the next line's +-LO2 rows, its edges
+      //    (scalar) and x / p_{k-2}, then the codes of line m + 2 and the operands of line
+      //    m + 1 + PD
+      Far f1;
+      load_far(m + 1, f1);
       Edge ed1;
       load_edge(m + 1 < n_run ? m + 1 : m, ed1);
       XP x1{0.0, 0.0};
@@ -519,16 +550,23 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int
       auto reg_value = [&](int32_t off, double& g) -> bool {
         const bool k0 = off == 0, k1 = (off == 1) & up_ok, k2 = (off == -1) & dn_ok;
         const bool k3 = nv & (off == LO), k4 = pv & (off == -LO);
+        const bool k5 = M2 && off == LO2, k6 = M2 && off == -LO2;
         // each select pinned in a register (an opaque asm operand): left alone, the optimiser
         // turns the chain into a stack table of the candidates + a computed-address load
         double t = k3 ? n_pk : pr_pk;
         asm volatile("" : "+v"(t));
+        if constexpr (M2) {
+          t = k5 ? o_fu : t;
+          asm volatile("" : "+v"(t));
+          t = k6 ? o_fd : t;
+          asm volatile("" : "+v"(t));
+        }
         t = k2 ? dn_pk : t;
         asm volatile("" : "+v"(t));
         t = k1 ? up_pk : t;
         asm volatile("" : "+v"(t));
         g = k0 ? o_pk : t;
-        return k0 | k1 | k2 | k3 | k4;
+        return k0 | k1 | k2 | k3 | k4 | k5 | k6;
       };
       double sum = 0.0;
       bool all_reg = true;
@@ -568,6 +606,10 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int
       o_pold = rq[0].pold;
       o_epk = lane == 0 ? pk_of(ed1.qd, ed1.pd) : pk_of(ed1.qu, ed1.pu);
       o_eok = edge_ok(m + 1);
+      if constexpr (M2) {
+        o_fu = pk_of(f1.qu, f1.pu);
+        o_fd = pk_of(f1.qd, f1.pd);
+      }
 #pragma unroll
       for (int d = 0; d + 1 < PD; ++d) rq[d] = rq[d + 1];
       rq[PD - 1] = rn;
@@ -844,7 +886,7 @@ void cg_fused1_win(int cm, int param, const SellDev& S, const F1Vectors& v, int6
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 
-void cg_fused1_carry(int cm, int param, int depth, bool general, const SellDev& S, const F1Vectors& v,
+void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, const SellDev& S, const F1Vectors& v,
                      int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
                      const CgState* st, double tol, int first, int check, int k, hipStream_t stream) {
   if (tr.ntiles == 0 || grid == 0) return;
@@ -853,33 +895,35 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, const SellDev& 
             "line-carry pass needs SELL-64 d16/c8 with interleaved pairs");
   MCG_CHECK(depth == 2 || depth == 3, "line-carry prefetch depth must be 2 or 3");
   MCG_CHECK(general || cm == 2, "the specialised line-carry pass needs the c8 dictionary");
+  MCG_CHECK(lo2 == 0 || (cm == 2 && !general && lo2 > 1), "the +-LO2 carry needs the specialised c8 pass");
   const bool pair = (k & 1) != 0;
-#define MCG_C(CM, U, PD, PAIR, GEN)                                                                          \
-  hipLaunchKernelGGL((k_cg_f1_carry<CM, U, PD, PAIR, GEN>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
-                     tr, partials, pstride, st, tol, first, check)
-#define MCG_CP(CM, U, PD, GEN)                         \
+#define MCG_C(CM, U, PD, PAIR, GEN, M2)                                                                         \
+  hipLaunchKernelGGL((k_cg_f1_carry<CM, U, PD, PAIR, GEN, M2>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
+                     tr, partials, pstride, st, tol, first, check, lo2)
+#define MCG_CP(CM, U, PD, GEN, M2)                     \
   do {                                                 \
-    if (pair) MCG_C(CM, U, PD, true, GEN);             \
-    else MCG_C(CM, U, PD, false, GEN);                 \
+    if (pair) MCG_C(CM, U, PD, true, GEN, M2);         \
+    else MCG_C(CM, U, PD, false, GEN, M2);             \
   } while (0)
-#define MCG_CD(CM, U, GEN)                             \
+#define MCG_CD(CM, U, GEN, M2)                         \
   do {                                                 \
-    if (depth == 2) MCG_CP(CM, U, 2, GEN);             \
-    else MCG_CP(CM, U, 3, GEN);                        \
+    if (depth == 2) MCG_CP(CM, U, 2, GEN, M2);         \
+    else MCG_CP(CM, U, 3, GEN, M2);                    \
   } while (0)
-#define MCG_CU(CM, GEN)                       \
-  do {                                        \
-    if (param == 4) MCG_CD(CM, 4, GEN);       \
-    else if (param == 5) MCG_CD(CM, 5, GEN);  \
-    else if (param == 6) MCG_CD(CM, 6, GEN);  \
-    else if (param == 7) MCG_CD(CM, 7, GEN);  \
-    else MCG_CD(CM, 8, GEN);                  \
+#define MCG_CU(CM, GEN, M2)                       \
+  do {                                            \
+    if (param == 4) MCG_CD(CM, 4, GEN, M2);       \
+    else if (param == 5) MCG_CD(CM, 5, GEN, M2);  \
+    else if (param == 6) MCG_CD(CM, 6, GEN, M2);  \
+    else if (param == 7) MCG_CD(CM, 7, GEN, M2);  \
+    else MCG_CD(CM, 8, GEN, M2);                  \
   } while (0)
   if (cm == 2) {
-    if (general) MCG_CU(2, true);
-    else MCG_CU(2, false);
+    if (general) MCG_CU(2, true, false);
+    else if (lo2 > 0) MCG_CU(2, false, true);
+    else MCG_CU(2, false, false);
   } else {
-    MCG_CU(1, true);
+    MCG_CU(1, true, false);
   }
 #undef MCG_CU
 #undef MCG_CD

@@ -301,9 +301,14 @@ void GpuCgSolver::setup() {
         return true;
       };
       // the specialised pass (no slow path) when every stored offset is carried: 0, +-1, +-one line
+      // 3-D: the carried line is a plane (N^2 rows) and +-N is a second carried offset
+      carry_lo2_ = spec_.kind == ProblemKind::Poisson3D && opt_.carry_3d != 0 ? (int32_t)spec_.N : 0;
       carry_general_ = !c8_;
       for (int64_t off : dict_offsets_)
-        if (off != 0 && off != 1 && off != -1 && off != 64 * S && off != -64 * S) carry_general_ = true;
+        if (off != 0 && off != 1 && off != -1 && off != 64 * S && off != -64 * S &&
+            (carry_lo2_ == 0 || (off != carry_lo2_ && off != -carry_lo2_)))
+          carry_general_ = true;
+      if (carry_general_) carry_lo2_ = 0;
       // auto: only the specialised pass (2-D stencils); with the slow path (3-D's +-N gathers) it
       // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log)
       if (opt_.carry == 1 || !carry_general_) carry_all_ = apply(tr_all_, g_all_);
@@ -433,7 +438,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   }
   const SellDev S = sell_view();
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
-    kern::cg_fused1_carry(c8_ ? 2 : 1, info_.spmv_param, opt_.carry_depth, carry_general_, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
+    kern::cg_fused1_carry(c8_ ? 2 : 1, info_.spmv_param, opt_.carry_depth, carry_general_, carry_lo2_, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
                           opt_.tol, first, check, k, s0_);
     return;
   }

@@ -48,6 +48,7 @@ struct CgOptions {
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
   int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
+  int carry_3d = 1;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
   int carry_depth = 3;          // line-carry pass: operand prefetch depth in lines (2 or 3; 3 measured faster)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)

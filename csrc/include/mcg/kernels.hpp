@@ -189,7 +189,8 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 // one line, 64 S rows), the launch one range of whole lines; a wave walks down one column of
 // slices and keeps the previous / current / next line's p_k in registers.
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8 */, int param, int depth /* operand prefetch, lines */,
-                     bool general /* false: every dictionary offset is 0, +-1 or +-one line (no slow path) */,
+                     bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
+                     int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,
                      const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& slices,
                      double* partials, int pstride, int grid, const CgState* st, double tol, int first, int check,
                      int k, hipStream_t stream);

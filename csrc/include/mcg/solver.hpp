@@ -129,6 +129,7 @@ class GpuCgSolver {
   bool pipe_ = false;           // software-pipelined stencil pass
   bool carry_all_ = false, carry_int_ = false;  // line-carry pass for the all-rows / interior launch
   bool carry_general_ = true;                   // line-carry pass with the memory-gather slow path
+  int32_t carry_lo2_ = 0;                       // line-carry pass: second carried offset (3-D: N)
   std::vector<int64_t> dict_offsets_;           // SELL-64/c8: the distinct column offsets
   SellDev sell_view() const {
     SellDev s{slice_ptr_.get(), cols_.get(), vals_.get(), L_.n_local()};

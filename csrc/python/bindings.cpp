@@ -156,6 +156,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("strip", &CgOptions::strip)
       .def_readwrite("carry", &CgOptions::carry)
       .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
+      .def_readwrite("carry_3d", &CgOptions::carry_3d)
       .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
