@@ -23,7 +23,7 @@ import cuda_mpi_parallel_amd as mcg  # noqa: E402
 
 def parse_cfg(s):
     parts = s.split(":")
-    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": -1, "s": 1, "r": 0, "i": -1, "w": -1, "P": -1, "S": -1, "c": 0, "k": 4, "d": 3}
+    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": -1, "s": 1, "r": 0, "i": -1, "w": -1, "P": -1, "S": -1, "c": 0, "k": 4, "d": 0}
     for q in parts[1:]:
         d[q[0]] = int(q[1:])
     return d

@@ -341,8 +341,9 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int6
 // (offset LO2 = N rows: slices N/64 apart in the same plane, worked at the same step by the
 // neighbouring columns' waves on the same XCD) are gathered from the L2 one line ahead, issued
 // before the prefetches, and carried into the step as p_k.
+// (M2: at least 4 waves per SIMD requested -- the +-N rows push the odd pass just past 128 VGPRs)
 template <int CM, int U, int PD, bool PAIR, bool GEN, bool M2>
-__global__ __launch_bounds__(kBS) void k_cg_f1_carry(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+__global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride,
                                                      const CgState* __restrict__ st, double tol, int first,
                                                      int check, int32_t LO2) {
