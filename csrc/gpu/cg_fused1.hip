@@ -894,7 +894,7 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, co
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0, "line-carry pass needs whole grid lines");
   MCG_CHECK(v.ra_old != nullptr && (cm == 1 || cm == 2) && param >= 4 && param <= 8,
             "line-carry pass needs SELL-64 d16/c8 with interleaved pairs");
-  MCG_CHECK(depth == 2 || depth == 3, "line-carry prefetch depth must be 2 or 3");
+  MCG_CHECK(depth >= 1 && depth <= 3, "line-carry prefetch depth must be 1..3");
   MCG_CHECK(general || cm == 2, "the specialised line-carry pass needs the c8 dictionary");
   MCG_CHECK(lo2 == 0 || (cm == 2 && !general && lo2 > 1), "the +-LO2 carry needs the specialised c8 pass");
   const bool pair = (k & 1) != 0;
@@ -908,7 +908,8 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, co
   } while (0)
 #define MCG_CD(CM, U, GEN, M2)                         \
   do {                                                 \
-    if (depth == 2) MCG_CP(CM, U, 2, GEN, M2);         \
+    if (depth == 1) MCG_CP(CM, U, 1, GEN, M2);         \
+    else if (depth == 2) MCG_CP(CM, U, 2, GEN, M2);    \
     else MCG_CP(CM, U, 3, GEN, M2);                    \
   } while (0)
 #define MCG_CU(CM, GEN, M2)                       \

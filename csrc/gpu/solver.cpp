@@ -439,7 +439,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   const SellDev S = sell_view();
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
     kern::cg_fused1_carry(c8_ ? 2 : 1, info_.spmv_param,
-                          opt_.carry_depth > 0 ? opt_.carry_depth : (carry_lo2_ > 0 ? 2 : 3), carry_general_, carry_lo2_, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
+                          opt_.carry_depth > 0 ? opt_.carry_depth : (carry_lo2_ > 0 ? 1 : 3), carry_general_, carry_lo2_, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
                           opt_.tol, first, check, k, s0_);
     return;
   }

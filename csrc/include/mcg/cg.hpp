@@ -49,8 +49,9 @@ struct CgOptions {
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
   int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
   int carry_3d = 1;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
-  int carry_depth = 0;          // line-carry pass: operand prefetch depth in lines (2 or 3); 0 = auto (2-D 3: 318 vs
-                                // 301 it/s; 3-D 2: the deeper pipeline does not fit 4 waves/SIMD with the +-N rows)
+  int carry_depth = 0;          // line-carry pass: operand prefetch depth in lines (1..3); 0 = auto (2-D 3: 318 vs
+                                // 301 it/s at 2; 3-D 1: the +-N rows, gathered one plane ahead, then meet the
+                                // neighbouring column's own prefetch in the L2: 534 vs 518 it/s at 2)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
