@@ -23,6 +23,9 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   MCG_CHECK(world == 1 || comm != nullptr, "multi-rank solver needs a communicator");
   RowPartition part = partition_rows(spec_, world_);
   L_ = make_layout(spec_, part, rank_);
+  // column indices are int32 in every format (CSR cols, SELL cols / ext offsets, kernel gathers)
+  MCG_CHECK(L_.ext_len < ((int64_t)1 << 31) - 64,
+            "a rank's rows + ghosts exceed int32 column indices (2^31): use more ranks");
   if (opt_.format == 2 || opt_.format == 3) {  // SELL-64 with 16-bit column offsets, if the bandwidth fits int16
     d16_ = bandwidth(spec_) <= 32767;
     c8_ = opt_.format == 3;  // dictionary codes: decided in setup() from the actual entries (fallback d16)
