@@ -347,11 +347,11 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
                                                      double* __restrict__ partials, int pstride,
                                                      const CgState* __restrict__ st, double tol, int first,
                                                      int check, int32_t LO2) {
-  __shared__ double2 s_dict[CM == 2 ? 256 : 1];
+  __shared__ double2 s_dict[CM >= 2 ? 256 : 1];
   if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   if (sc.conv) return;
-  if constexpr (CM == 2) {
+  if constexpr (CM >= 2) {
     for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
     __syncthreads();
   }
@@ -394,9 +394,9 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
   // a slice's codes: c8 bytes packed four per register (the dictionary is re-read from LDS
   // when the row sums are formed); d16 offsets + values
   struct Codes {
-    uint32_t pk[CM == 2 ? (U + 3) / 4 : 1];
-    int16_t d[CM == 2 ? 1 : U];
-    double v[CM == 2 ? 1 : U];
+    uint32_t pk[CM >= 2 ? (U + 3) / 4 : 1];
+    int16_t d[CM >= 2 ? 1 : U];
+    double v[CM >= 2 ? 1 : U];
     int w;
   };
   typedef __attribute__((address_space(4))) const double KD;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
   auto pk_of = [&](double2 q, double pold) { return fma(b, pold, fma(na, q.y, q.x)); };
   // entry u of a slice: {value, column offset from the row's own column}
   auto entry = [&](const Codes& c, int u, double& val) -> int32_t {
-    if constexpr (CM == 2) {
+    if constexpr (CM >= 2) {
       const double2 q = s_dict[(c.pk[u >> 2] >> (8 * (u & 3))) & 255u];
       val = q.x;
       return (int32_t)__double_as_longlong(q.y);
@@ -466,6 +466,15 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
         for (int q = 0; q < (U + 3) / 4; ++q) c.pk[q] = 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u) c.pk[u >> 2] |= (uint32_t)cp[64 * u + lane] << (8 * (u & 3));
+      } else if constexpr (CM == 3) {
+        // 4-bit codes (SellDev::codes4): lanes 2i, 2i+1 share a byte, 32 bytes per slice entry
+        const uint8_t* __restrict__ cp = S.codes4 + (base >> 1);
+        const int sh = (lane & 1) * 4;
+#pragma unroll
+        for (int q = 0; q < (U + 3) / 4; ++q) c.pk[q] = 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          c.pk[u >> 2] |= (((uint32_t)cp[32 * u + (lane >> 1)] >> sh) & 15u) << (8 * (u & 3));
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -892,10 +901,11 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, co
                      const CgState* st, double tol, int first, int check, int k, hipStream_t stream) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0, "line-carry pass needs whole grid lines");
-  MCG_CHECK(v.ra_old != nullptr && (cm == 1 || cm == 2) && param >= 4 && param <= 8,
-            "line-carry pass needs SELL-64 d16/c8 with interleaved pairs");
+  MCG_CHECK(v.ra_old != nullptr && cm >= 1 && cm <= 3 && param >= 4 && param <= 8,
+            "line-carry pass needs SELL-64 d16/c8/c4 with interleaved pairs");
   MCG_CHECK(depth >= 1 && depth <= 3, "line-carry prefetch depth must be 1..3");
-  MCG_CHECK(general || cm == 2, "the specialised line-carry pass needs the c8 dictionary");
+  MCG_CHECK(general || cm >= 2, "the specialised line-carry pass needs the c8 dictionary");
+  MCG_CHECK(cm != 3 || (!general && lo2 == 0 && S.codes4 != nullptr), "4-bit codes: specialised 2-D pass only");
   MCG_CHECK(lo2 == 0 || (cm == 2 && !general && lo2 > 1), "the +-LO2 carry needs the specialised c8 pass");
   const bool pair = (k & 1) != 0;
 #define MCG_C(CM, U, PD, PAIR, GEN, M2)                                                                         \
@@ -920,7 +930,9 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, co
     else if (param == 7) MCG_CD(CM, 7, GEN, M2);  \
     else MCG_CD(CM, 8, GEN, M2);                  \
   } while (0)
-  if (cm == 2) {
+  if (cm == 3) {
+    MCG_CU(3, false, false);
+  } else if (cm == 2) {
     if (general) MCG_CU(2, true, false);
     else if (lo2 > 0) MCG_CU(2, false, true);
     else MCG_CU(2, false, false);

@@ -155,6 +155,12 @@ void GpuCgSolver::setup() {
         cols_.release();
         dcols_.release();
         vals_.release();
+        if (ndict_ <= 16 && opt_.carry != 0 && opt_.carry_c4 != 0 && opt_.recurrence == 1 && opt_.interleave != 0) {
+          // 4-bit codes for the line-carry pass (half the c8 stream; the generic passes keep c8)
+          codes4_.allocate(total / 2, "A", 256);
+          kern::sell_c8_to_c4(codes_.get(), total, codes4_.get(), s0_);
+          MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+        }
         info_.format = 3;
         matrix_bytes = total + (ns + 1) * 8;
       }
@@ -318,6 +324,8 @@ void GpuCgSolver::setup() {
       if (use_halo_ && opt_.overlap && (opt_.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
     }
     info_.carry = carry_all_ || carry_int_;
+    if (!info_.carry || carry_general_ || carry_lo2_ != 0) codes4_.release();  // only the 2-D carry reads them
+    info_.codes4 = codes4_.get() != nullptr;
   }
   g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
@@ -441,7 +449,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
   }
   const SellDev S = sell_view();
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
-    kern::cg_fused1_carry(c8_ ? 2 : 1, info_.spmv_param,
+    kern::cg_fused1_carry(codes4_.get() && !carry_general_ && carry_lo2_ == 0 ? 3 : (c8_ ? 2 : 1), info_.spmv_param,
                           opt_.carry_depth > 0 ? opt_.carry_depth : (carry_lo2_ > 0 ? 1 : 3), carry_general_, carry_lo2_, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
                           opt_.tol, first, check, k, s0_);
     return;

@@ -48,6 +48,7 @@ struct CgOptions {
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
   int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
+  int carry_c4 = 1;             // line-carry pass on a c8 matrix with <= 16 dictionary entries: 4-bit codes
   int carry_3d = 1;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
   int carry_depth = 0;          // line-carry pass: operand prefetch depth in lines (1..3); 0 = auto (2-D 3: 318 vs
                                 // 301 it/s at 2; 3-D 1: the +-N rows, gathered one plane ahead, then meet the

@@ -92,6 +92,10 @@ struct SellDev {
   const uint8_t* codes = nullptr;
   const double2* dict = nullptr;
   int32_t ndict = 0;
+  // SELL-64/c4 (dictionaries of <= 16 entries, e.g. the 2-D 5-pt operator's 15): the same codes
+  // 4 bits each, lanes 2i / 2i+1 of a slice entry in one byte (byte offset = c8 offset / 2);
+  // read by the line-carry pass (half the matrix stream of c8)
+  const uint8_t* codes4 = nullptr;
 };
 
 namespace kern {
@@ -125,6 +129,8 @@ void gen_fill_sell(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t c
 // it has too many distinct values / offsets.  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
 bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
 void sell_to_c8(const SellDev& S, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st);
+// c8 -> c4 (every code < 16): codes4[i / 2] = codes[i] | codes[i + 1] << 4 for even i
+void sell_c8_to_c4(const uint8_t* codes, int64_t total, uint8_t* codes4, hipStream_t st);
 
 // ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
 // variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row),
@@ -188,7 +194,7 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 // slice width <= param): `slices.strip` = S slices per grid line (the carried column offset is
 // one line, 64 S rows), the launch one range of whole lines; a wave walks down one column of
 // slices and keeps the previous / current / next line's p_k in registers.
-void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8 */, int param, int depth /* operand prefetch, lines */,
+void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,
                      bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,
                      const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& slices,

@@ -52,6 +52,7 @@ struct SolverInfo {
   int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
+  bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
 };
 
 class GpuCgSolver {
@@ -122,6 +123,7 @@ class GpuCgSolver {
   bool d16_ = false;
   DeviceBuffer<uint8_t> codes_;  // SELL-64/c8 dictionary codes
   DeviceBuffer<double2> dict_;
+  DeviceBuffer<uint8_t> codes4_;  // SELL-64/c4 copy of the codes (line-carry pass, <= 16 dictionary entries)
   int ndict_ = 0;
   bool c8_ = false;
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
@@ -138,6 +140,7 @@ class GpuCgSolver {
     s.codes = codes_.get();
     s.dict = dict_.get();
     s.ndict = ndict_;
+    s.codes4 = codes4_.get();
     return s;
   }
   // vectors

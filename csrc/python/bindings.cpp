@@ -157,6 +157,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry", &CgOptions::carry)
       .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
       .def_readwrite("carry_3d", &CgOptions::carry_3d)
+      .def_readwrite("carry_c4", &CgOptions::carry_c4)
       .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -301,6 +302,7 @@ PYBIND11_MODULE(_C, m) {
         d["strip"] = i.strip;
         d["carry"] = i.carry;
         d["xcd_map"] = i.xcd_map;
+        d["codes4"] = i.codes4;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;

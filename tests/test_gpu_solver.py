@@ -222,3 +222,15 @@ def test_line_carry_pass_reproducible_and_auto(mcg):
     assert not mcg.CGSolver(odd, format="sellc8", recurrence=1, carry=-1).info["carry"]
     with pytest.raises(Exception, match="line-carry"):
         mcg.CGSolver(odd, format="sellc8", recurrence=1, carry=1)
+
+
+def test_line_carry_c4_codes_match_c8(mcg):
+    """4-bit dictionary codes (<= 16 entries: the 2-D 5-pt operator's 15) read by the line-carry pass:
+    the same entries as c8, so the same bits."""
+    spec = mcg.make_problem("poisson2d", n=256, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=1, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=0, check_every=8)
+    assert a.info["codes4"] and not b.info["codes4"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
