@@ -5,7 +5,7 @@ over rounds so clock drift hits every config alike).
 A config is  fmt:vV:pP:bB:uU  (format csr|sell|sell16|sellc8, SpMV engine V, batch/lanes P,
 blocks per CU B, residual-update unroll U; also nN non-temporal, xX XCD map, sS slices/wave,
 rR recurrence, iI interleaved r/Ap pairs, wW LDS-window pass, BN update blocks per CU, cC line-carry pass,
-kK line-carry blocks per CU, dD line-carry prefetch depth), e.g.
+kK line-carry blocks per CU, dD line-carry prefetch depth, T1 line-carry non-temporal operand loads), e.g.
 
   python bench/sweep.py --n 16384 --steps 30 --cfg csr:v1:p6:b8:u2 csr:v0:p6:b6:u2 sell:v1:p6:b8:u2
 """
@@ -23,7 +23,7 @@ import cuda_mpi_parallel_amd as mcg  # noqa: E402
 
 def parse_cfg(s):
     parts = s.split(":")
-    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": -1, "s": 1, "r": 0, "i": -1, "w": -1, "P": -1, "S": -1, "c": 0, "k": 4, "d": 0}
+    d = {"format": parts[0], "v": -1, "p": 0, "b": 0, "u": 1, "g": 1, "n": 0, "x": -1, "s": 1, "r": 0, "i": -1, "w": -1, "P": -1, "S": -1, "c": 0, "k": 4, "d": 0, "T": 0}
     for q in parts[1:]:
         d[q[0]] = int(q[1:])
     return d
@@ -62,6 +62,7 @@ def main():
             o.carry = c["c"]
             o.carry_blocks_per_cu = c["k"]
             o.carry_depth = c["d"]
+            o.carry_nt = c["T"]
             s = C.Solver(spec.native(), o, 0, 1, None)
             s.setup()
             s.reset()

@@ -314,6 +314,17 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int6
   block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
 }
 
+// loads of data one wave reads once (line-carry operands): optionally non-temporal
+__device__ __forceinline__ double ld_once(const double* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
+__device__ __forceinline__ double2 ld_once(const double2* p, bool nt) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  if (nt) {
+    const d2v w = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+    return make_double2(w.x, w.y);
+  }
+  return *p;
+}
+
 // ---------------------------------------------------------------------------
 // Line-carry single-reduction pass: SELL-64/d16 or /c8 with the interleaved {r, Ap} layout,
 // every slice width <= U, the launch's slices whole grid lines of S slices (structured-grid
@@ -419,6 +430,7 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
   // are saddr + voffset forms and the per-step scalar work is a few adds.  Loads are never
   // conditional: line indices are clamped to lines that exist (values past the run are unused).
   const int32_t ext32 = (int32_t)v.ext_len;
+  const bool ntl = v.nt_loads != 0;
   for (int64_t job = gw; job < SS * runs; job += nw) {
     const int64_t col = job % SS, l0 = (job / SS) * chunk;
     const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
@@ -434,8 +446,8 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
     auto sbase = [&](int32_t m) { return sl0 + (int64_t)m * SS; };   // slice, line l0 + m
     auto load_raw = [&](int32_t m, Raw& r) {
       const int32_t eb = ebase(m < la ? m : la);
-      r.q = (rao + eb)[lane];
-      r.pold = (po + eb)[lane];
+      r.q = ld_once(rao + eb + lane, ntl);
+      r.pold = ld_once(po + eb + lane, ntl);
     };
     auto load_edge = [&](int32_t m, Edge& r) {  // m <= n_run - 1 (owned lines)
       const int32_t eb = ebase(m);
@@ -452,8 +464,8 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
     auto load_xp = [&](int32_t m, XP& r) {  // owned lines only
       if constexpr (PAIR) {
         const int32_t mm = m < n_run - 1 ? m : n_run - 1;
-        r.pkm2 = (pn + ebase(mm))[lane];
-        r.xo = (x + i0 + mm * LO)[lane];
+        r.pkm2 = ld_once(pn + ebase(mm) + lane, ntl);
+        r.xo = ld_once(x + i0 + mm * LO + lane, ntl);
       }
     };
     auto load_codes = [&](int32_t m, Codes& c) {  // owned lines only

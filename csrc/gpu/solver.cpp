@@ -443,6 +443,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
                     x_.get()};
   v.p_fix = p_[1].get();
   v.ext_len = L_.ext_len;
+  v.nt_loads = opt_.carry_nt;
   if (opt_.interleave == 1) {
     v.ra_old = reinterpret_cast<const double2*>(ra_[(k + 1) & 1].get());
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());

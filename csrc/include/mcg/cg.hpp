@@ -48,6 +48,8 @@ struct CgOptions {
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
   int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
+  int carry_nt = 0;             // line-carry pass: non-temporal loads of the operands each wave reads once (measured
+                                // slower: 281 vs 302 it/s 2-D, 480 vs 531 3-D; the +-1 edge rows are re-read from L2)
   int carry_c4 = 1;             // line-carry pass on a c8 matrix with <= 16 dictionary entries: 4-bit codes
   int carry_3d = 1;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
   int carry_depth = 0;          // line-carry pass: operand prefetch depth in lines (1..3); 0 = auto (2-D 3: 318 vs

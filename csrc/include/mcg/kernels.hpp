@@ -182,6 +182,7 @@ struct F1Vectors {
   // the parity-1 p buffer, for the one-term catch-up when convergence latches after an even pass.
   const double* p_fix = nullptr;
   int64_t ext_len = 0;  // ext-layout length of r / Ap / p (bounds of the line-carry pass's edge loads)
+  int nt_loads = 0;     // line-carry pass: non-temporal loads of the once-read operands
 };
 // `k`: pass index (its parity selects the paired x update; final mode: m = k)
 template <typename IdxT>

@@ -158,6 +158,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
       .def_readwrite("carry_3d", &CgOptions::carry_3d)
       .def_readwrite("carry_c4", &CgOptions::carry_c4)
+      .def_readwrite("carry_nt", &CgOptions::carry_nt)
       .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
