@@ -149,7 +149,7 @@ void GpuCgSolver::setup() {
         dict_.allocate(dict.size(), "A");
         MCG_HIP(hipMemcpy(dict_.get(), dict.data(), dict.size() * sizeof(double2), hipMemcpyHostToDevice),
                 "memcpy from host to device failed(A)");
-        codes_.allocate(total, "A", 512);  // the line-carry pass reads 8 entries past a slice's last
+        codes_.allocate(total, "A", 512);  // the line-carry pass reads all U <= 8 entry slots of a slice
         kern::sell_to_c8(sell_view(), dict_.get(), nv, nd, codes_.get(), s0_);
         MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
         cols_.release();
