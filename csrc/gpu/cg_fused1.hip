@@ -352,13 +352,21 @@ __device__ __forceinline__ double2 ld_once(const double2* p, bool nt) {
 // (offset LO2 = N rows: slices N/64 apart in the same plane, worked at the same step by the
 // neighbouring columns' waves on the same XCD) are gathered from the L2 one line ahead, issued
 // before the prefetches, and carried into the step as p_k.
+// M2 == 1: every wave gathers both.  M2 == 2 (block exchange, LO2 a multiple of 64): the kWaves
+// waves of a block walk the columns of kWaves consecutive grid lines of one plane (same x slice),
+// so the +-N neighbour of wave w's rows is wave w +- 1's rows: each wave puts the next plane's p_k
+// (computed a step ahead from its prefetched operands) in LDS, one barrier per step, and only
+// the block's first / last wave gathers its outer +-N rows from memory.  The gathers missed the
+// L2 about a third of the time (the neighbouring columns' waves drift apart); this is the
+// same p_k values, bit for bit, with 1/kWaves of the gathers.
 // (M2: at least 4 waves per SIMD requested -- the +-N rows push the odd pass just past 128 VGPRs)
-template <int CM, int U, int PD, bool PAIR, bool GEN, bool M2>
+template <int CM, int U, int PD, bool PAIR, bool GEN, int M2>
 __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride,
                                                      const CgState* __restrict__ st, double tol, int first,
                                                      int check, int32_t LO2) {
   __shared__ double2 s_dict[CM >= 2 ? 256 : 1];
+  __shared__ double s_far[M2 == 2 ? 2 * kWaves * 64 : 1];  // [step parity][wave][lane]: p_k of the next plane
   if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   if (sc.conv) return;
@@ -382,9 +390,15 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
   const int64_t nb = gridDim.x, blk = blockIdx.x;
   const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;
   const int64_t nw = nb * kWaves;
-  const int64_t gw = lb * kWaves + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t gw = lb * kWaves + wv;
   const int64_t runs = nw > SS ? nw / SS : 1;  // line chunks per column
   const int64_t chunk = (nl + runs - 1) / runs;
+  // jobs: (column, run of lines).  M2 == 2: one job per block, its waves the columns of kWaves
+  // consecutive grid lines of the plane (G slices per grid line)
+  const int64_t G = M2 == 2 ? LO2 / 64 : 1;
+  const int64_t njobs = M2 == 2 ? SS / kWaves * runs : SS * runs;
+  const bool fu_g = M2 != 2 || wv == kWaves - 1, fd_g = M2 != 2 || wv == 0;  // +-LO2 rows from memory
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
   // operands of a line (prefetched PD lines ahead): {r_{k-1}, Ap_{k-1}} and p_{k-1}
   struct Raw {
@@ -431,8 +445,16 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
   // conditional: line indices are clamped to lines that exist (values past the run are unused).
   const int32_t ext32 = (int32_t)v.ext_len;
   const bool ntl = v.nt_loads != 0;
-  for (int64_t job = gw; job < SS * runs; job += nw) {
-    const int64_t col = job % SS, l0 = (job / SS) * chunk;
+  for (int64_t job = M2 == 2 ? lb : gw; job < njobs; job += M2 == 2 ? nb : nw) {
+    int64_t col, l0;
+    if constexpr (M2 == 2) {
+      const int64_t q = job % (SS / kWaves);
+      col = ((q / G) * kWaves + wv) * G + q % G;
+      l0 = (job / (SS / kWaves)) * chunk;
+    } else {
+      col = job % SS;
+      l0 = (job / SS) * chunk;
+    }
     const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
     if (l0 >= l1) continue;
     const int64_t sl0 = tr.b0 + l0 * SS + col;
@@ -502,14 +524,18 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
       double2 qu, qd;
       double pu, pd;
     };
-    auto load_far = [&](int32_t m, Far& f) {
+    auto load_far = [&](int32_t m, Far& f, bool up, bool dn) {  // up / dn wave-uniform
       if constexpr (M2) {
         const int32_t e = ebase(m < n_run - 1 ? m : n_run - 1) + lane;
         const int32_t cu = e + LO2 < ext32 ? e + LO2 : ext32 - 1, cd = e - LO2 >= 0 ? e - LO2 : 0;
-        f.qu = rao[cu];
-        f.pu = po[cu];
-        f.qd = rao[cd];
-        f.pd = po[cd];
+        if (up) {
+          f.qu = rao[cu];
+          f.pu = po[cu];
+        }
+        if (dn) {
+          f.qd = rao[cd];
+          f.pd = po[cd];
+        }
       }
     };
     // prologue: the line before the run (if it exists), operands of lines 0 .. PD, codes of
@@ -539,7 +565,7 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
     double o_fu = 0.0, o_fd = 0.0;  // M2: p_k of rows +LO2 / -LO2
     if constexpr (M2) {
       Far f0;
-      load_far(0, f0);
+      load_far(0, f0, true, true);
       o_fu = pk_of(f0.qu, f0.pu);
       o_fd = pk_of(f0.qd, f0.pd);
     }
@@ -548,8 +574,8 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
       // 1. loads, in the order they are waited for: (M2) the next line's +-LO2 rows, its edges
       //    (scalar) and x / p_{k-2}, then the codes of line m + 2 and the operands of line
       //    m + 1 + PD
-      Far f1;
-      load_far(m + 1, f1);
+      Far f1{make_double2(0.0, 0.0), make_double2(0.0, 0.0), 0.0, 0.0};
+      load_far(m + 1, f1, fu_g, fd_g);
       Edge ed1;
       load_edge(m + 1 < n_run ? m + 1 : m, ed1);
       XP x1{0.0, 0.0};
@@ -563,6 +589,7 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
       //    none of these (other offsets such as +-N in 3-D) sends the wave down a slow path
       //    that redoes the sums with memory gathers; !GEN: the dictionary has no such offset.
       const double n_pk = pk_of(rq[0].q, rq[0].pold);
+      if constexpr (M2 == 2) s_far[(((m + 1) & 1) * kWaves + wv) * 64 + lane] = n_pk;
       const double sh_up = __shfl_down(o_pk, 1, 64);
       const double sh_dn = __shfl_up(o_pk, 1, 64);
       const double up_pk = lane == 63 ? o_epk : sh_up;  // row + 1
@@ -628,7 +655,14 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
       o_pold = rq[0].pold;
       o_epk = lane == 0 ? pk_of(ed1.qd, ed1.pd) : pk_of(ed1.qu, ed1.pu);
       o_eok = edge_ok(m + 1);
-      if constexpr (M2) {
+      if constexpr (M2 == 2) {
+        // the neighbouring waves' next-plane p_k (written this step; the other parity's slots
+        // were last read before this step's barrier by every wave)
+        __syncthreads();
+        const double* sf = s_far + ((m + 1) & 1) * kWaves * 64 + lane;
+        o_fu = fu_g ? pk_of(f1.qu, f1.pu) : sf[(wv < kWaves - 1 ? wv + 1 : wv) * 64];
+        o_fd = fd_g ? pk_of(f1.qd, f1.pd) : sf[(wv > 0 ? wv - 1 : wv) * 64];
+      } else if constexpr (M2) {
         o_fu = pk_of(f1.qu, f1.pu);
         o_fd = pk_of(f1.qd, f1.pd);
       }
@@ -908,9 +942,13 @@ void cg_fused1_win(int cm, int param, const SellDev& S, const F1Vectors& v, int6
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 
-void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, const SellDev& S, const F1Vectors& v,
-                     int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
-                     const CgState* st, double tol, int first, int check, int k, hipStream_t stream) {
+bool carry_block_exchange_ok(int param, int32_t lo2, int64_t strip) {
+  return lo2 > 0 && lo2 % 64 == 0 && (param == 7 || param == 8) && strip % (kWaves * (lo2 / 64)) == 0;
+}
+
+void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, bool block_exchange, const SellDev& S,
+                     const F1Vectors& v, int64_t own_off, const TileRanges& tr, double* partials, int pstride,
+                     int grid, const CgState* st, double tol, int first, int check, int k, hipStream_t stream) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0, "line-carry pass needs whole grid lines");
   MCG_CHECK(v.ra_old != nullptr && cm >= 1 && cm <= 3 && param >= 4 && param <= 8,
@@ -919,6 +957,8 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, co
   MCG_CHECK(general || cm >= 2, "the specialised line-carry pass needs the c8 dictionary");
   MCG_CHECK(cm != 3 || (!general && lo2 == 0 && S.codes4 != nullptr), "4-bit codes: specialised 2-D pass only");
   MCG_CHECK(lo2 == 0 || (cm == 2 && !general && lo2 > 1), "the +-LO2 carry needs the specialised c8 pass");
+  MCG_CHECK(!block_exchange || carry_block_exchange_ok(param, lo2, tr.strip),
+            "plane-carry block exchange needs +-LO2 whole slices, kWaves | grid lines per plane, 7-8 entries per row");
   const bool pair = (k & 1) != 0;
 #define MCG_C(CM, U, PD, PAIR, GEN, M2)                                                                         \
   hipLaunchKernelGGL((k_cg_f1_carry<CM, U, PD, PAIR, GEN, M2>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
@@ -943,13 +983,16 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, co
     else MCG_CD(CM, 8, GEN, M2);                  \
   } while (0)
   if (cm == 3) {
-    MCG_CU(3, false, false);
+    MCG_CU(3, false, 0);
   } else if (cm == 2) {
-    if (general) MCG_CU(2, true, false);
-    else if (lo2 > 0) MCG_CU(2, false, true);
-    else MCG_CU(2, false, false);
+    if (general) MCG_CU(2, true, 0);
+    else if (lo2 > 0 && block_exchange) {
+      if (param == 7) MCG_CD(2, 7, false, 2);
+      else MCG_CD(2, 8, false, 2);
+    } else if (lo2 > 0) MCG_CU(2, false, 1);
+    else MCG_CU(2, false, 0);
   } else {
-    MCG_CU(1, true, false);
+    MCG_CU(1, true, 0);
   }
 #undef MCG_CU
 #undef MCG_CD

@@ -70,6 +70,7 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         }
         o.x = s.x_local();
         o.row_begin = s.layout().row_begin;
+        o.carry = s.info().carry;
         if (verify) o.true_rnorm = s.true_residual_norm();
       } catch (const Error& e) {
         o.error = std::string(e.what()) + ": " + e.detail();

@@ -51,10 +51,15 @@ struct CgOptions {
   int carry_nt = 0;             // line-carry pass: non-temporal loads of the operands each wave reads once (measured
                                 // slower: 281 vs 302 it/s 2-D, 480 vs 531 3-D; the +-1 edge rows are re-read from L2)
   int carry_c4 = 1;             // line-carry pass on a c8 matrix with <= 16 dictionary entries: 4-bit codes
-  int carry_3d = 1;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
+  int carry_3d = 2;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
+                                // (1); 2 = the block's waves on consecutive grid lines, inner +-N rows exchanged
+                                // through LDS (when N is a multiple of 64); 0 = off
   int carry_depth = 0;          // line-carry pass: operand prefetch depth in lines (1..3); 0 = auto (2-D 3: 318 vs
                                 // 301 it/s at 2; 3-D 1: the +-N rows, gathered one plane ahead, then meet the
                                 // neighbouring column's own prefetch in the L2: 534 vs 518 it/s at 2)
+  int placement_tries = 3;   // single-reduction form: time the pass on this many physical placements of the vector
+                             // set at setup and keep the fastest (1 = off; profiles/r1_placement_probe.md)
+  int vec_skew = 0;         // experiment: stagger the vector buffers' base addresses by i * vec_skew 256-B blocks
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)

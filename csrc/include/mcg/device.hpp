@@ -32,29 +32,34 @@ class DeviceBuffer {
     return *this;
   }
 
-  void allocate(size_t n, const char* what, size_t pad = 0) {
+  // `lead` elements are skipped at the front (the buffer starts `lead` elements past the
+  // allocation: staggers the base addresses of streams read at the same index)
+  void allocate(size_t n, const char* what, size_t pad = 0, size_t lead = 0) {
     release();
-    const size_t bytes = (n + pad) * sizeof(T);
+    const size_t bytes = (lead + n + pad) * sizeof(T);
     if (bytes) {
-      MCG_HIP(hipMalloc(&ptr_, bytes), std::string("device malloc failed(") + what + ")");
+      MCG_HIP(hipMalloc(&base_, bytes), std::string("device malloc failed(") + what + ")");
+      ptr_ = base_ + lead;
       if (pad) MCG_HIP(hipMemset(ptr_ + n, 0, pad * sizeof(T)), "device memset failed");
     }
     n_ = n;
   }
   void release() {
-    if (ptr_) (void)hipFree(ptr_);
-    ptr_ = nullptr;
+    if (base_) (void)hipFree(base_);
+    base_ = ptr_ = nullptr;
     n_ = 0;
   }
   T* get() const { return ptr_; }
   size_t size() const { return n_; }
   size_t bytes() const { return n_ * sizeof(T); }
   void swap(DeviceBuffer& o) noexcept {
+    std::swap(base_, o.base_);
     std::swap(ptr_, o.ptr_);
     std::swap(n_, o.n_);
   }
 
  private:
+  T* base_ = nullptr;
   T* ptr_ = nullptr;
   size_t n_ = 0;
 };

@@ -195,9 +195,12 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 // slice width <= param): `slices.strip` = S slices per grid line (the carried column offset is
 // one line, 64 S rows), the launch one range of whole lines; a wave walks down one column of
 // slices and keeps the previous / current / next line's p_k in registers.
+// The plane carry's block exchange applies: lo2 whole slices, kWaves | grid lines per plane, 7-8 entries
+bool carry_block_exchange_ok(int param, int32_t lo2, int64_t strip);
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,
                      bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,
+                     bool block_exchange /* lo2 rows of a block's inner waves through LDS (carry_block_exchange_ok) */,
                      const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& slices,
                      double* partials, int pstride, int grid, const CgState* st, double tol, int first, int check,
                      int k, hipStream_t stream);

@@ -14,6 +14,7 @@ struct LocalRankResult {
   std::vector<double> x;
   int64_t row_begin = 0;
   double true_rnorm = -1.0;
+  bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)
   std::string error;
 };
 

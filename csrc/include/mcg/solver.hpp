@@ -53,6 +53,9 @@ struct SolverInfo {
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
+  bool carry_xchg = false;
+  int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
+  double placement_gain = 1.0;  // slowest / fastest of them (the fastest is kept)  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
 };
 
 class GpuCgSolver {
@@ -97,6 +100,9 @@ class GpuCgSolver {
   void enqueue_iteration_f1_(int k);
   void capture_pair_();
   void inject_fault_(int k);
+  std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
+  void allocate_vectors_();
+  void probe_placement_();  // keep the fastest of opt_.placement_tries allocations of the vectors
 
   ProblemSpec spec_;
   CgOptions opt_;

@@ -155,6 +155,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("pipeline", &CgOptions::pipeline)
       .def_readwrite("strip", &CgOptions::strip)
       .def_readwrite("carry", &CgOptions::carry)
+      .def_readwrite("vec_skew", &CgOptions::vec_skew)
+      .def_readwrite("placement_tries", &CgOptions::placement_tries)
       .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
       .def_readwrite("carry_3d", &CgOptions::carry_3d)
       .def_readwrite("carry_c4", &CgOptions::carry_c4)
@@ -304,6 +306,9 @@ PYBIND11_MODULE(_C, m) {
         d["carry"] = i.carry;
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;
+        d["carry_xchg"] = i.carry_xchg;
+        d["placement_sets"] = i.placement_sets;
+        d["placement_gain"] = i.placement_gain;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
@@ -326,6 +331,7 @@ PYBIND11_MODULE(_C, m) {
       py::dict d = result_dict(rr.res);
       d["row_begin"] = rr.row_begin;
       d["true_rnorm"] = rr.true_rnorm;
+      d["carry"] = rr.carry;
       ranks.append(d);
       x.insert(x.end(), rr.x.begin(), rr.x.end());
     }

@@ -123,8 +123,27 @@ def test_local_ranks_line_carry_interior(mcg, world):
     o = _opts(mcg, format="sellc8", recurrence=1, check_every=4)
     o.carry = 1
     out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    assert all(r["carry"] for r in out["ranks"])
     its = {r["iterations"] for r in out["ranks"]}
     assert len(its) == 1, its
     assert abs(its.pop() - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
     np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
     assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_local_ranks_plane_carry_interior(mcg, world):
+    """3-D plane carry (the +-N rows gathered a plane ahead) on the interior planes of each rank,
+    the two boundary planes through the generic pass after the halo, vs the same ranks without
+    the carry pass (same row sums: agreement to rounding of the dot-product blocking)."""
+    spec = mcg.make_problem("poisson3d", n=16)  # 16 planes of 256 rows: whole planes per rank
+    C = mcg.native()
+    outs = []
+    for carry in (-1, 0):
+        o = _opts(mcg, format="sellc8", recurrence=1, check_every=4)
+        o.carry = carry
+        outs.append(C.run_local_ranks(spec.native(), o, world, 0, True))
+    assert all(r["carry"] for r in outs[0]["ranks"]) and not any(r["carry"] for r in outs[1]["ranks"])
+    assert [r["iterations"] for r in outs[0]["ranks"]] == [r["iterations"] for r in outs[1]["ranks"]]
+    np.testing.assert_allclose(outs[0]["x"], outs[1]["x"], rtol=1e-10, atol=1e-13)
+    assert all(r["converged"] and r["true_rnorm"] < 1e-6 for r in outs[0]["ranks"])

@@ -212,6 +212,37 @@ def test_line_carry_pass_matches_generic(mcg, fmt, problem, kw):
     assert abs(outs[0]["rnorm"] - outs[1]["rnorm"]) <= 1e-9 * outs[1]["rnorm"]
 
 
+@pytest.mark.parametrize("n", [64, 128])
+def test_plane_carry_block_exchange(mcg, n):
+    """3-D plane carry with the +-N rows of a block's inner waves exchanged through LDS (carry_3d=2)
+    vs every wave gathering them (carry_3d=1) vs the generic pass: the same p_k values in the same
+    fma order, dot-product partials blocked differently."""
+    spec = mcg.make_problem("poisson3d", n=n, rhs="random")
+    solvers = [mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=c, carry_3d=m, check_every=8)
+               for c, m in ((1, 2), (1, 1), (0, 1))]
+    assert [s.info["carry_xchg"] for s in solvers] == [True, False, False]
+    assert [s.info["carry"] for s in solvers] == [True, True, False]
+    res = [s.solve() for s in solvers]
+    assert all(r["converged"] for r in res)
+    assert max(r["iterations"] for r in res) - min(r["iterations"] for r in res) <= 1
+    for r in res[1:]:
+        np.testing.assert_allclose(res[0]["x_local"], r["x_local"], rtol=1e-6,
+                                   atol=1e-6 * np.abs(r["x_local"]).max())
+    assert solvers[0].true_residual_norm() < 1e-6
+    outs = []
+    for s in solvers:
+        s.reset()
+        s.run(24)
+        s.finalize()
+        outs.append(s.result())
+    assert all(o["iterations"] == 24 for o in outs)
+    for o in outs[1:]:
+        assert abs(outs[0]["rnorm"] - o["rnorm"]) <= 1e-9 * o["rnorm"]
+    # run to run: bitwise
+    again = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_3d=2, check_every=8).solve()
+    np.testing.assert_array_equal(again["x_local"], res[0]["x_local"])
+
+
 def test_line_carry_pass_reproducible_and_auto(mcg):
     spec = mcg.make_problem("poisson2d", n=256, rhs="random")
     a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=-1).solve()
