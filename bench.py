@@ -177,7 +177,8 @@ def main() -> int:
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
-                      "placement_gain": round(info.get("placement_gain", 1.0), 4),"model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
+                      "placement_gain": round(info.get("placement_gain", 1.0), 4),
+                      "placement_lead_trial": info.get("placement_lead_trial"),"model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
                       "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3), **extra},
         }), flush=True)
     if env.world > 1:

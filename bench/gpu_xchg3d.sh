@@ -16,6 +16,17 @@ if [ "$1" = "place" ]; then
   done
   exit 0
 fi
+if [ "$1" = "cfg" ]; then
+  # usage: bash bench/gpu_xchg3d.sh cfg REPS "args A" "args B" ...   (bench.py args per config)
+  reps=$2; shift 2
+  for rep in $(seq $reps); do
+    for c in "$@"; do
+      timeout -k 10 200 python bench.py --phases 0 $c > gpurun_out/x.json 2>/dev/null || exit 1
+      echo "$c | $(python3 -c "import json; d=json.load(open('gpurun_out/x.json')); print(d['value'], d['check']['placement_gain'], d['check'].get('placement_lead_trial'), d['check']['setup_s'])")" >> gpurun_out/cfg.log
+    done
+  done
+  exit 0
+fi
 if [ "$1" = "skew" ]; then
   for rep in 1 2 3 4; do
     for k in 0 1 7; do

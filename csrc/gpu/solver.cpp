@@ -346,32 +346,36 @@ std::vector<DeviceBuffer<double>*> GpuCgSolver::vectors_() {
 void GpuCgSolver::allocate_vectors_() {
   const int64_t n = L_.n_local();
   // vec_skew: buffer i of the streams one pass reads / writes at the same row starts i * vec_skew
-  // 256-B blocks past its allocation
+  // 256-B blocks past its allocation.  With the placement probe, every vector gets room for
+  // leads up to kLeadCap (probe_placement_)
   const size_t skew = (size_t)std::max(0, opt_.vec_skew) * 32;
-  x_.allocate(n, "x", 8, 1 * skew);
+  const size_t cap = opt_.placement_tries > 1 && opt_.placement_leads > 1 && opt_.recurrence == 1 ? kLeadCap : 0;
+  x_.allocate(n, "x", 8, 1 * skew, cap);
   if (opt_.interleave == 1) {  // single-reduction form, {r, Ap} pairs, double-buffered by parity
-    ra_[0].allocate(2 * L_.ext_len, "r", 8, 2 * skew);
-    ra_[1].allocate(2 * L_.ext_len, "r", 8, 3 * skew);
+    ra_[0].allocate(2 * L_.ext_len, "r", 8, 2 * skew, cap);
+    ra_[1].allocate(2 * L_.ext_len, "r", 8, 3 * skew, cap);
   } else if (opt_.recurrence == 1) {  // single-reduction form: r and Ap are gathered -> ext layout, double-buffered
-    r_.allocate(L_.ext_len, "r", 8);
-    Ap_.allocate(L_.ext_len, "Ap", 8);
-    Ap1_.allocate(L_.ext_len, "Ap", 8);
-    r1_.allocate(L_.ext_len, "r", 8);
+    r_.allocate(L_.ext_len, "r", 8, 0, cap);
+    Ap_.allocate(L_.ext_len, "Ap", 8, 0, cap);
+    Ap1_.allocate(L_.ext_len, "Ap", 8, 0, cap);
+    r1_.allocate(L_.ext_len, "r", 8, 0, cap);
   } else {
     r_.allocate(L_.ext_len, "r", 8);
     Ap_.allocate(n, "Ap", 8);
   }
-  p_[0].allocate(L_.ext_len, "p", 8, 4 * skew);
-  p_[1].allocate(L_.ext_len, "p", 8, 5 * skew);
+  p_[0].allocate(L_.ext_len, "p", 8, 4 * skew, cap);
+  p_[1].allocate(L_.ext_len, "p", 8, 5 * skew, cap);
 }
 
 // Physical placement of the vector streams.  The same stream kernel on the same sizes runs at
-// 4.7-5.45 TB/s depending on the allocation (stable per allocation, re-drawn by a new one:
-// profiles/r1_placement_probe.md), and the CG benches show the same ~10 % two modes from one
-// process to the next.  Here the single-reduction pass (both parities, full work) is timed on
-// `placement_tries` fresh allocations of the vector set -- each allocated while the earlier ones
-// are still held, so it gets other memory -- and the fastest is kept.  Vector contents are
-// scratch until reset().
+// 4.7-5.45 TB/s depending on the allocation (stable per allocation, re-drawn by a new one), and
+// within one allocation the relative offset of two read streams moves it by ~5 % (4 KiB and
+// 1-3 MiB offsets faster than 0, 32 KiB or 256 KiB: profiles/r1_placement_probe.md); the CG
+// benches show the same ~10 % spread from one process to the next.  Here the single-reduction
+// pass (both parities, full work) is timed on `placement_tries` allocations of the vector set --
+// each allocated while the earlier ones are still held, so it gets other memory -- times
+// `placement_leads` start offsets of each vector inside its allocation (multiples of 4 KiB and
+// 1 MiB), and the fastest combination is kept.  Vector contents are scratch until reset().
 void GpuCgSolver::probe_placement_() {
   info_.placement_sets = 1;
   info_.placement_gain = 1.0;
@@ -380,10 +384,23 @@ void GpuCgSolver::probe_placement_() {
   auto bufs = vectors_();
   size_t set_bytes = 0;
   for (auto* b : bufs) set_bytes += b->bytes();
+  const int leads = std::max(1, opt_.placement_leads);
+  // start offset (doubles) of buffer i in lead trial t: trial 0 all zero, then pseudo-random
+  // multiples of 4 KiB (0..7) + 1 MiB (0..3)
+  auto lead_of = [&](int t, size_t i) -> size_t {
+    if (t == 0 || bufs[i]->lead_capacity() < kLeadCap) return 0;
+    uint32_t h = (uint32_t)(t * 16 + (int)i + 1) * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    return ((size_t)(h & 7) * 4096 + (size_t)((h >> 3) & 3) * (1u << 20)) / sizeof(double);
+  };
+  auto set_leads = [&](int t) {
+    for (size_t i = 0; i < bufs.size(); ++i)
+      if (bufs[i]->get()) bufs[i]->relead(lead_of(t, i));
+  };
   auto time_pairs = [&]() {
     // k = 0, 1: both parities, no convergence test (check = 0), so every launch does its work
-    enqueue_f1_(0, 0, 0);
-    enqueue_f1_(1, 0, 0);
     MCG_HIP(hipEventRecord(ev_t0_, s0_), "event record failed");
     for (int r = 0; r < 2; ++r) {
       enqueue_f1_(0, 0, 0);
@@ -395,7 +412,26 @@ void GpuCgSolver::probe_placement_() {
     MCG_HIP(hipEventElapsedTime(&ms, ev_t0_, ev_t1_), "event elapsed failed");
     return ms;
   };
-  float best = time_pairs(), worst = best;
+  // this set: warm once, then each lead trial; leaves the set at its best trial
+  auto probe_set = [&](int& best_t) {
+    enqueue_f1_(0, 0, 0);
+    enqueue_f1_(1, 0, 0);
+    float b = 0.f;
+    for (int t = 0; t < leads; ++t) {
+      if (leads > 1) set_leads(t);
+      const float ms = time_pairs();
+      info_.placement_worst_ms = std::max(info_.placement_worst_ms, (double)ms);
+      if (t == 0 || ms < b) {
+        b = ms;
+        best_t = t;
+      }
+    }
+    if (leads > 1) set_leads(best_t);
+    return b;
+  };
+  info_.placement_worst_ms = 0.0;
+  int best_t = 0;
+  float best = probe_set(best_t);
   std::vector<std::vector<DeviceBuffer<double>>> held;
   for (int t = 1; t < opt_.placement_tries; ++t) {
     size_t free_b = 0, total_b = 0;
@@ -404,18 +440,21 @@ void GpuCgSolver::probe_placement_() {
     std::vector<DeviceBuffer<double>> prev(bufs.size());
     for (size_t i = 0; i < bufs.size(); ++i) prev[i].swap(*bufs[i]);
     allocate_vectors_();
-    const float ms = time_pairs();
+    int bt = 0;
+    const float ms = probe_set(bt);
     ++info_.placement_sets;
-    worst = std::max(worst, ms);
     if (ms < best) {
       best = ms;
+      best_t = bt;
     } else {
       for (size_t i = 0; i < bufs.size(); ++i) prev[i].swap(*bufs[i]);  // keep the earlier set
     }
     held.push_back(std::move(prev));
   }
   held.clear();
-  info_.placement_gain = best > 0.f ? worst / best : 1.0;
+  info_.placement_best_ms = best;
+  info_.placement_lead_trial = best_t;
+  info_.placement_gain = best > 0.f ? info_.placement_worst_ms / best : 1.0;
   MCG_HIP(hipMemsetAsync(partials_.get(), 0, partials_.bytes(), s0_), "device memset failed");
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s0_), "device memset failed");
   MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");

@@ -33,21 +33,32 @@ class DeviceBuffer {
   }
 
   // `lead` elements are skipped at the front (the buffer starts `lead` elements past the
-  // allocation: staggers the base addresses of streams read at the same index)
-  void allocate(size_t n, const char* what, size_t pad = 0, size_t lead = 0) {
+  // allocation: staggers the base addresses of streams read at the same index); room is left
+  // for leads up to `lead_cap` (relead())
+  void allocate(size_t n, const char* what, size_t pad = 0, size_t lead = 0, size_t lead_cap = 0) {
     release();
-    const size_t bytes = (lead + n + pad) * sizeof(T);
+    lead_cap = lead_cap > lead ? lead_cap : lead;
+    const size_t bytes = (lead_cap + n + pad) * sizeof(T);
     if (bytes) {
       MCG_HIP(hipMalloc(&base_, bytes), std::string("device malloc failed(") + what + ")");
       ptr_ = base_ + lead;
       if (pad) MCG_HIP(hipMemset(ptr_ + n, 0, pad * sizeof(T)), "device memset failed");
     }
     n_ = n;
+    pad_ = pad;
+    cap_ = lead_cap;
   }
+  // move the start within the allocation (contents are not kept; the pad is re-zeroed)
+  void relead(size_t lead) {
+    MCG_CHECK(base_ != nullptr && lead <= cap_, "buffer lead beyond its allocation");
+    ptr_ = base_ + lead;
+    if (pad_) MCG_HIP(hipMemset(ptr_ + n_, 0, pad_ * sizeof(T)), "device memset failed");
+  }
+  size_t lead_capacity() const { return cap_; }
   void release() {
     if (base_) (void)hipFree(base_);
     base_ = ptr_ = nullptr;
-    n_ = 0;
+    n_ = pad_ = cap_ = 0;
   }
   T* get() const { return ptr_; }
   size_t size() const { return n_; }
@@ -56,12 +67,14 @@ class DeviceBuffer {
     std::swap(base_, o.base_);
     std::swap(ptr_, o.ptr_);
     std::swap(n_, o.n_);
+    std::swap(pad_, o.pad_);
+    std::swap(cap_, o.cap_);
   }
 
  private:
   T* base_ = nullptr;
   T* ptr_ = nullptr;
-  size_t n_ = 0;
+  size_t n_ = 0, pad_ = 0, cap_ = 0;
 };
 
 template <typename T>

@@ -53,9 +53,11 @@ struct SolverInfo {
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
-  bool carry_xchg = false;
+  bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
-  double placement_gain = 1.0;  // slowest / fastest of them (the fastest is kept)  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
+  double placement_gain = 1.0;  // slowest / fastest of the timed placements (the fastest is kept)
+  double placement_best_ms = 0.0, placement_worst_ms = 0.0;  // two even/odd pass pairs
+  int placement_lead_trial = 0;  // start-offset trial kept (0 = allocation starts)
 };
 
 class GpuCgSolver {
@@ -102,7 +104,8 @@ class GpuCgSolver {
   void inject_fault_(int k);
   std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
   void allocate_vectors_();
-  void probe_placement_();  // keep the fastest of opt_.placement_tries allocations of the vectors
+  void probe_placement_();  // keep the fastest of several placements of the vectors (CgOptions::placement_*)
+  static constexpr size_t kLeadCap = (4u << 20) / sizeof(double);  // room for vector start offsets (4 MiB)
 
   ProblemSpec spec_;
   CgOptions opt_;

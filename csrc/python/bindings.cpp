@@ -157,6 +157,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry", &CgOptions::carry)
       .def_readwrite("vec_skew", &CgOptions::vec_skew)
       .def_readwrite("placement_tries", &CgOptions::placement_tries)
+      .def_readwrite("placement_leads", &CgOptions::placement_leads)
       .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
       .def_readwrite("carry_3d", &CgOptions::carry_3d)
       .def_readwrite("carry_c4", &CgOptions::carry_c4)
@@ -309,6 +310,8 @@ PYBIND11_MODULE(_C, m) {
         d["carry_xchg"] = i.carry_xchg;
         d["placement_sets"] = i.placement_sets;
         d["placement_gain"] = i.placement_gain;
+        d["placement_best_ms"] = i.placement_best_ms;
+        d["placement_lead_trial"] = i.placement_lead_trial;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
