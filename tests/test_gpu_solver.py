@@ -265,3 +265,20 @@ def test_line_carry_c4_codes_match_c8(mcg):
     ra, rb = a.solve(), b.solve()
     assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
     np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+
+
+@pytest.mark.parametrize("problem,n", [("poisson2d", 256), ("poisson3d", 40)])
+def test_placement_probe_keeps_numerics(mcg, problem, n):
+    """The setup-time placement probe (several vector allocations x start offsets, fastest kept) only
+    moves where the vectors live: the solve is bitwise equal to one without the probe, and the probe
+    leaves no state behind (partials and CgState are cleared)."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, placement_tries=3, placement_leads=4)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, placement_tries=1)
+    assert a.info["placement_sets"] >= 2 and b.info["placement_sets"] == 1
+    assert 0 <= a.info["placement_lead_trial"] < 4
+    assert a.info["placement_gain"] >= 1.0
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and rb["converged"] and ra["iterations"] == rb["iterations"]
+    assert np.array_equal(ra["x_local"], rb["x_local"])
+    assert ra["rnorm"] == rb["rnorm"]
