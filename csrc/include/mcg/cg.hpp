@@ -59,7 +59,7 @@ struct CgOptions {
                                 // neighbouring column's own prefetch in the L2: 534 vs 518 it/s at 2)
   int placement_tries = 3;   // single-reduction form: time the pass on this many physical placements of the vector
                              // set at setup and keep the fastest (1 = off; profiles/r1_placement_probe.md)
-  int placement_leads = 4;   // ... times this many start offsets of the vectors inside their allocations
+  int placement_leads = 8;   // ... times this many start offsets of the vectors inside their allocations
   int vec_skew = 0;         // experiment: stagger the vector buffers' base addresses by i * vec_skew 256-B blocks
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
