@@ -234,6 +234,7 @@ int main(int argc, char** argv) {
   CgResult res;
   SolverInfo info;
   double true_rnorm = -1;
+  std::vector<size_t> rank_bytes;  // device bytes held by each rank's solver
   int world = a.cpu ? a.sim_ranks : a.gpus;
 
   try {
@@ -264,6 +265,7 @@ int main(int argc, char** argv) {
       info = outs[0].info;
       true_rnorm = outs[0].true_rnorm;
       for (auto& o : outs) {
+        rank_bytes.push_back(o.info.device_bytes);
         res.solve_seconds = std::max(res.solve_seconds, o.res.solve_seconds);
         res.setup_seconds = std::max(res.setup_seconds, o.res.setup_seconds);
       }
@@ -283,10 +285,13 @@ int main(int argc, char** argv) {
 
   const double itps = res.iters_per_second();
   if (a.report == "json") {
+    std::string per_rank = "[";
+    for (size_t r = 0; r < rank_bytes.size(); ++r) per_rank += (r ? ", " : "") + std::to_string(rank_bytes[r]);
+    per_rank += "]";
     std::printf("{\"problem\": \"%s\", \"n\": %lld, \"nnz_rank0\": %lld, \"ranks\": %d, \"device\": \"%s\", "
                 "\"format\": \"%s\", \"iterations\": %d, \"converged\": %s, \"breakdown\": %s, \"rnorm\": %.6e, "
                 "\"true_rnorm\": %.6e, \"setup_s\": %.6f, \"solve_s\": %.6f, \"it_per_s\": %.3f, "
-                "\"device_bytes_rank0\": %zu}\n",
+                "\"device_bytes_rank0\": %zu, \"device_bytes_per_rank\": %s}\n",
                 problem_name(a.spec).c_str(), (long long)n, (long long)info.nnz_local, world,
                 a.cpu ? "cpu" : "gpu",
                 a.cpu ? "csr"
@@ -294,7 +299,7 @@ int main(int argc, char** argv) {
                                           : (info.format == 2 ? "sell64-d16" : (info.format == 1 ? "sell64" : "csr"))),
                 res.iterations,
                 res.converged ? "true" : "false", res.breakdown ? "true" : "false", res.rnorm, true_rnorm,
-                res.setup_seconds, res.solve_seconds, itps, info.device_bytes);
+                res.setup_seconds, res.solve_seconds, itps, info.device_bytes, per_rank.c_str());
   } else if (!want_x || n > 3) {
     std::fprintf(stderr,
                  "[mcg] problem=%s n=%lld ranks=%d iterations=%d converged=%d rnorm=%.3e solve=%.4fs "

@@ -43,6 +43,7 @@ def test_json_report_cpu_poisson(mcg):
     rep = json.loads(lines[-2])
     assert rep["problem"] == "poisson2d" and rep["n"] == 4096 and rep["converged"]
     assert rep["rnorm"] < 1e-7
+    assert rep["device_bytes_per_rank"] == []  # CPU path holds no device memory
 
 
 def test_fixed_iterations_cpu(mcg):

@@ -282,3 +282,16 @@ def test_placement_probe_keeps_numerics(mcg, problem, n):
     assert ra["converged"] and rb["converged"] and ra["iterations"] == rb["iterations"]
     assert np.array_equal(ra["x_local"], rb["x_local"])
     assert ra["rnorm"] == rb["rnorm"]
+
+
+def test_cli_json_report_per_rank_memory(mcg):
+    """--report json lists the device bytes each rank's solver holds."""
+    import json
+    p = subprocess.run([mcg.cli_path(), "--problem", "poisson2d", "--n", "128", "--report", "json"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.strip().splitlines()
+    assert lines[-1] == "Success"
+    rep = json.loads(lines[-2])
+    assert rep["converged"] and rep["ranks"] == 1
+    assert rep["device_bytes_per_rank"] == [rep["device_bytes_rank0"]] and rep["device_bytes_rank0"] > 0
