@@ -42,6 +42,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
   use_halo_ = use_comm_ && L_.has_halo();
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
+  MCG_CHECK(opt_.graph_iters >= 2 && opt_.graph_iters % 2 == 0, "graph_iters must be even and >= 2");
   if (opt_.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
   // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only
   prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph;
@@ -57,8 +58,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
 }
 
 GpuCgSolver::~GpuCgSolver() {
-  if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
-  if (graph_) (void)hipGraphDestroy(graph_);
+  drop_graphs_();
   if (s0_.get()) (void)hipStreamSynchronize(s0_);
   if (s1_.get()) (void)hipStreamSynchronize(s1_);
 }
@@ -494,11 +494,8 @@ void GpuCgSolver::reset() {
     MCG_HIP(hipMemcpy(&rr0, &st_.get()->rr_new, sizeof(double), hipMemcpyDeviceToHost),
             "memcpy from device to host failed(state)");
     const double tol = opt_.rtol * std::sqrt(rr0);
-    if (tol != opt_.tol && graph_exec_) {
-      (void)hipGraphExecDestroy(graph_exec_);
-      (void)hipGraphDestroy(graph_);
-      graph_exec_ = nullptr;
-      graph_ = nullptr;
+    if (tol != opt_.tol) {
+      drop_graphs_();
     }
     opt_.tol = tol;
   }
@@ -669,29 +666,42 @@ void GpuCgSolver::enqueue_iteration_(int k) {
   if (use_comm_) comm_->allreduce_sum(&st->rr_new, 1, s0_);
 }
 
-void GpuCgSolver::capture_pair_() {
+void GpuCgSolver::drop_graphs_() {
+  for (int g = 0; g < 2; ++g) {
+    if (graph_exec_[g]) (void)hipGraphExecDestroy(graph_exec_[g]);
+    if (graph_[g]) (void)hipGraphDestroy(graph_[g]);
+    graph_exec_[g] = nullptr;
+    graph_[g] = nullptr;
+  }
+}
+
+// Captures 2 (kind 0) or graph_iters (kind 1) iterations starting at an even k_.  The passes
+// depend on k only through its parity (and k >= 2), so one capture replays for every even k_.
+void GpuCgSolver::capture_pair_(int kind) {
   hipStream_t s = s0_;
+  const int iters = kind == 0 ? 2 : opt_.graph_iters;
   MCG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "graph capture failed");
   try {
-    enqueue_iteration_(k_);
-    enqueue_iteration_(k_ + 1);
+    for (int j = 0; j < iters; ++j) enqueue_iteration_(k_ + j);
   } catch (...) {
     hipGraph_t g = nullptr;
     (void)hipStreamEndCapture(s, &g);
     if (g) (void)hipGraphDestroy(g);
     throw;
   }
-  MCG_HIP(hipStreamEndCapture(s, &graph_), "graph capture failed");
-  MCG_HIP(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0), "graph instantiate failed");
+  MCG_HIP(hipStreamEndCapture(s, &graph_[kind]), "graph capture failed");
+  MCG_HIP(hipGraphInstantiate(&graph_exec_[kind], graph_[kind], nullptr, nullptr, 0), "graph instantiate failed");
 }
 
 void GpuCgSolver::run_iterations(int count) {
   MCG_CHECK(setup_done_, "solver not set up");
+  const int glong = opt_.graph_iters > 2 ? opt_.graph_iters : 0;
   while (count > 0) {
     if (opt_.use_graph && k_ >= 2 && (k_ % 2) == 0 && count >= 2) {
-      if (!graph_exec_) {
+      const int kind = glong && count >= glong ? 1 : 0;
+      if (!graph_exec_[kind]) {
         try {
-          capture_pair_();
+          capture_pair_(kind);
         } catch (const Error& e) {
           std::fprintf(stderr, "[mcg] graph capture unavailable (%s: %s); running eagerly\n", e.what(),
                        e.detail().c_str());
@@ -700,9 +710,10 @@ void GpuCgSolver::run_iterations(int count) {
           continue;
         }
       }
-      MCG_HIP(hipGraphLaunch(graph_exec_, s0_), "graph launch failed");
-      k_ += 2;
-      count -= 2;
+      MCG_HIP(hipGraphLaunch(graph_exec_[kind], s0_), "graph launch failed");
+      const int done = kind == 0 ? 2 : glong;
+      k_ += done;
+      count -= done;
     } else {
       if (k_ == opt_.inject_nan_at) inject_fault_(k_);
       enqueue_iteration_(k_);

@@ -23,6 +23,8 @@ struct CgOptions {
   int check_every = 32;      // host polls the device convergence latch every k iterations
   bool overlap = true;       // halo on a side stream, overlapped with the interior SpMV
   bool use_graph = true;     // capture iteration pairs into a hipGraph
+  int graph_iters = 32;      // iterations per graph launch (even, >= 2); the last < graph_iters run as pairs
+                             // (32 vs 2: 4096^2 4700 -> 5025 it/s, profiles/r1_graph_iters.log)
   bool force_comm = false;   // run RCCL collectives even with one rank
   int format = 0;            // 0 = CSR, 1 = SELL-64
   int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)

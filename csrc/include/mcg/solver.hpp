@@ -100,7 +100,7 @@ class GpuCgSolver {
   void enqueue_halo_f1_(int k, hipStream_t s);            // ghosts iteration k of the single-reduction form reads
   void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
-  void capture_pair_();
+  void capture_pair_(int kind);
   void inject_fault_(int k);
   std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
   void allocate_vectors_();
@@ -163,8 +163,10 @@ class GpuCgSolver {
   TileRanges tr_all_, tr_int_, tr_bnd_;
   int g_all_ = 1, g_int_ = 1, g_bnd_ = 1, g_b_ = 1;
   // graph of two iterations (even, odd)
-  hipGraph_t graph_ = nullptr;
-  hipGraphExec_t graph_exec_ = nullptr;
+  // [0]: one iteration pair, [1]: graph_iters iterations (when > 2)
+  hipGraph_t graph_[2] = {nullptr, nullptr};
+  hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
+  void drop_graphs_();
   double setup_seconds_ = 0.0;
 };
 

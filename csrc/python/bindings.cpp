@@ -181,6 +181,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("check_every", &CgOptions::check_every)
       .def_readwrite("overlap", &CgOptions::overlap)
       .def_readwrite("use_graph", &CgOptions::use_graph)
+      .def_readwrite("graph_iters", &CgOptions::graph_iters)
       .def_readwrite("force_comm", &CgOptions::force_comm)
       .def_readwrite("format", &CgOptions::format)
       .def_readwrite("blocks_per_cu", &CgOptions::blocks_per_cu);

@@ -295,3 +295,22 @@ def test_cli_json_report_per_rank_memory(mcg):
     rep = json.loads(lines[-2])
     assert rep["converged"] and rep["ranks"] == 1
     assert rep["device_bytes_per_rank"] == [rep["device_bytes_rank0"]] and rep["device_bytes_rank0"] > 0
+
+
+@pytest.mark.parametrize("fmt,rec", [("sellc8", 1), ("csr", 0)])
+def test_long_graph_bitwise_equal_pairs(mcg, fmt, rec):
+    """graph_iters=8 replays 8 iterations per hipGraph launch (the tail as pairs / eagerly); the
+    passes depend on k only through its parity, so results are bitwise those of pair graphs."""
+    spec = mcg.make_problem("poisson2d", n=96, rhs="random")
+    a = mcg.CGSolver(spec, format=fmt, recurrence=rec, graph_iters=8, check_every=32)
+    b = mcg.CGSolver(spec, format=fmt, recurrence=rec, graph_iters=2, check_every=32)
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and ra["iterations"] == rb["iterations"]
+    assert np.array_equal(ra["x_local"], rb["x_local"]) and ra["rnorm"] == rb["rnorm"]
+    for s in (a, b):
+        s.reset()
+        s.run(2 + 8 * 3 + 6)  # eager head, long graphs, pair tail
+        s.finalize()
+    assert a.result()["iterations"] == b.result()["iterations"] == 32
+    assert a.result()["rnorm"] == b.result()["rnorm"]
+    assert np.array_equal(a.x_local(), b.x_local())
