@@ -710,7 +710,15 @@ void GpuCgSolver::run_iterations(int count) {
           continue;
         }
       }
-      MCG_HIP(hipGraphLaunch(graph_exec_[kind], s0_), "graph launch failed");
+      const hipError_t le = hipGraphLaunch(graph_exec_[kind], s0_);
+      if (le != hipSuccess) {
+        // nothing was enqueued: run these iterations eagerly from here on
+        std::fprintf(stderr, "[mcg] graph launch failed (%s); running eagerly\n", hipGetErrorString(le));
+        (void)hipGetLastError();
+        drop_graphs_();
+        opt_.use_graph = false;
+        continue;
+      }
       const int done = kind == 0 ? 2 : glong;
       k_ += done;
       count -= done;
