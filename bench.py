@@ -10,8 +10,14 @@ exchange when N > 1.  tol is disabled so every timed step does real work; the
 device-side iteration counter is checked after the run.
 
   python bench.py                      # N=1
+  python bench.py --gpus 8             # starts 8 ranks itself (one process per GPU, RCCL)
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
-      --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+      --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8   # same ranks under torchrun
+
+Launch: without a torchrun environment and --gpus N > 1 (or --spawn), this process
+starts the N ranks as children (cuda_mpi_parallel_amd/parallel/launch.py) BEFORE it
+loads any HIP code, and exits with their status; every rank then runs exactly the
+code it runs under torchrun.
 """
 from __future__ import annotations
 
@@ -22,17 +28,20 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
-import cuda_mpi_parallel_amd as mcg
-from cuda_mpi_parallel_amd.parallel import dist as pdist
-
 METRIC = "CG iterations/sec (whole node), 5-pt Poisson N=16384², 1/2/4/8 MI355X"
 BASELINE_IT_PER_S = 65.0  # BASELINE.md "Bar to clear": reference algorithm's H100 roofline (derived; nothing published)
 
 
-def main() -> int:
+def aggregate(steps, ranks):
+    """(iterations/s, seconds, ok) of the job from the per-rank {dt, ok, iterations} records:
+    the timed region ends when the slowest rank ends, and the run is ok only if every rank is
+    ok and all ranks latched the same iteration count."""
+    dt = max(float(r["dt"]) for r in ranks)
+    ok = all(bool(r["ok"]) for r in ranks) and len({int(r["iterations"]) for r in ranks}) == 1
+    return steps / dt, dt, ok
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=200)
@@ -47,7 +56,7 @@ def main() -> int:
                          "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
     ap.add_argument("--recurrence", type=int, default=-1, help="0 two-reduction, 1 single-reduction, -1 auto")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--graph", action="store_true", help="capture iteration pairs into a hipGraph also when N > 1")
+    ap.add_argument("--graph", action="store_true", help="(default since r2; kept for old command lines)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="SpMV grid; 0 = auto")
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
@@ -56,29 +65,57 @@ def main() -> int:
     ap.add_argument("--phases", type=int, default=10,
                     help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
-    args = ap.parse_args()
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
+    ap.add_argument("--spawn", action="store_true",
+                    help="start the rank(s) as child processes even for --gpus 1 (the --gpus N > 1 launch route)")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    from cuda_mpi_parallel_amd.parallel import launch
+
+    # (a) --gpus N without torchrun: start the ranks and exit with their status.  Only the
+    # parent decides; a child (WORLD_SIZE set) always runs as a rank.
+    rc = launch.launch_or_none(args.gpus, [a for a in argv if a != "--spawn"], force_spawn=args.spawn,
+                               script=os.path.abspath(__file__))
+    if rc is not None:
+        return rc
+    return run_rank(args)
+
+
+def run_rank(args) -> int:
+    import torch
+    import torch.distributed as dist
+
+    import cuda_mpi_parallel_amd as mcg
+    from cuda_mpi_parallel_amd.parallel import dist as pdist
+    from cuda_mpi_parallel_amd.parallel import launch
 
     env = pdist.dist_env()
-    n_gpus = args.gpus if args.gpus is not None else env.world
-    if env.world != n_gpus:
-        print(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={env.world}; launch with torchrun --nproc-per-node {n_gpus}",
-              file=sys.stderr)
-        return 2
+    n_gpus = env.world
+    route = "spawn" if os.environ.get(launch.CHILD_FLAG) else ("torchrun" if launch.under_launcher() else "single")
+    # no user-buffer registration while capturing RCCL calls into graphs (buffers are few and
+    # small; registration would add an IPC-handle path the solver does not need)
+    os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
     pdist.set_device(env)
     if env.world > 1:
         pdist.init_process_group(env, backend="gloo")
-    comm = pdist.bootstrap_comm(env)
+    comm = pdist.bootstrap_comm(env, force=args.force_comm)
 
     if args.problem == "randspd":
         spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, rhs="random")
     else:
         spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
     C = mcg.native()
-    # hipGraph replay of iteration pairs at N = 1; at N > 1 the host enqueue runs far ahead of the
-    # ~1 ms iterations anyway, so RCCL-in-graph capture is opt-in (--graph)
-    use_graph = not args.no_graph and (env.world == 1 or args.graph)
+    # hipGraph replay of 32-iteration blocks at every N: at N > 1 the RCCL all-reduce and the halo
+    # send/recv (forked onto the side stream and joined by events) are captured with the kernels,
+    # so the host enqueues one graph per 32 iterations; a failed capture falls back to eager
+    use_graph = not args.no_graph
     opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
-                       use_graph=use_graph, force_comm=False, format=args.format,
+                       use_graph=use_graph, force_comm=args.force_comm, format=args.format,
                        blocks_per_cu=args.blocks_per_cu, recurrence=args.recurrence)
     for kv in args.set:
         k, v = kv.split("=", 1)
@@ -106,10 +143,6 @@ def main() -> int:
     barrier()
     dt = time.perf_counter() - t0
 
-    if env.world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
 
     phases = None
     if args.phases > 0 and solver.info["recurrence"] == "single-reduction":
@@ -123,12 +156,20 @@ def main() -> int:
     if not args.no_verify:
         # the recurrence residual must track the true residual ||b - A x|| (catches a kernel
         # that does less work than claimed: its residual would drift from the truth by orders
-        # of magnitude; legitimate fp64 drift at kappa ~ 1e8 is ~1e-4 relative)
+        # of magnitude).  Over the bench's few hundred iterations the two agree to ~1e-15
+        # relative (fp64 round-off only), so the guard is tight
         tr = solver.true_residual_norm()
         extra["true_rnorm"] = tr
-        ok = ok and abs(tr - res["rnorm"]) <= 1e-2 * max(tr, 1e-300) + 1e-9
+        extra["true_gap_rel"] = abs(tr - res["rnorm"]) / max(tr, 1e-300)
+        ok = ok and abs(tr - res["rnorm"]) <= 1e-8 * max(tr, 1e-300) + 1e-12
     info = solver.info
-    value = args.steps / dt
+    # whole-job result: the slowest rank's clock, every rank ok and latched at the same count
+    mine = {"dt": dt, "ok": bool(ok), "iterations": int(res["iterations"])}
+    ranks = [mine]
+    if env.world > 1:
+        ranks = [None] * env.world
+        dist.all_gather_object(ranks, mine)
+    value, dt, ok = aggregate(args.steps, ranks)
     nnz = spec.nnz
     if nnz is None:  # randspd: no closed form; sum the ranks' generated counts
         t = torch.tensor([info["nnz_local"]], dtype=torch.int64)
@@ -169,13 +210,18 @@ def main() -> int:
                 "global_batch": 1,
                 "seq_len": spec.n_rows,
                 "parallelism": f"rowpart{n_gpus}",
-                "format": info["format"],
+                # storage the timed pass streams: the 2-D line-carry pass reads 4-bit codes (c4)
+                "format": "sell64-c4" if info.get("codes4") else info["format"],
                 "recurrence": info["recurrence"],
                 "pass": "line-carry" if info.get("carry") else ("generic, xcd-aware" if info.get("xcd_map") else "generic"),
-                "hipgraph": use_graph,
+                "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
+                "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,
+                "launch": route,
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
+                      "comm_world": comm.count if comm is not None else 1,
+                      "graph_fallbacks": info.get("graph_fallbacks", 0),
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
                       "placement_lead_trial": info.get("placement_lead_trial"),"model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),

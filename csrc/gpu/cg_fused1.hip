@@ -32,7 +32,7 @@ struct F1Scalars {
   bool conv;
 };
 
-__device__ __forceinline__ F1Scalars f1_scalars(const CgState* __restrict__ st, double tol, int first, int check) {
+__device__ __forceinline__ F1Scalars f1_scalars(const CgState* st, double tol, int first, int check) {
   F1Scalars s;
   const double pAp = st->red[0], rAp = st->red[1], ApAp = st->red[2], rr = st->red[3];
   s.conv = check && sqrt(rr) < tol;  // ||r_{k-1}|| < tol : the reference's break (CUDACG.cu:333)
@@ -48,9 +48,21 @@ __device__ __forceinline__ F1Scalars f1_scalars(const CgState* __restrict__ st, 
   return s;
 }
 
-// four fixed-order block partials -> partials[q * pstride + blockIdx.x]
+// agent-scope (write-through, L1-bypassing) 8-B accesses for the in-kernel reduction's hand-offs
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// four fixed-order block partials -> partials[q * pstride + blockIdx.x] (write-through when an
+// in-kernel reduction reads them)
 __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, double a3, double* __restrict__ out,
-                                               int pstride) {
+                                               int pstride, bool wt = false) {
   __shared__ double sh[4][kWaves];
   a0 = eng::wave_sum(a0);
   a1 = eng::wave_sum(a1);
@@ -68,8 +80,95 @@ __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, 
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < kWaves; ++k) s += sh[threadIdx.x][k];
-    out[threadIdx.x * pstride + blockIdx.x] = s;
+    if (wt) st_wt(&out[threadIdx.x * pstride + blockIdx.x], s);
+    else out[threadIdx.x * pstride + blockIdx.x] = s;
   }
+}
+
+// CgState update from a fused pass's sums tot[4] (local; the all-reduce that follows makes them
+// global): the convergence / breakdown latch on the previous pass's GLOBAL r.r, a_prev, the new
+// sums, the iteration count.  cg_reduce_f1 mode 0 and the in-kernel reduction share this code.
+__device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int check, int first, double tol) {
+  auto zero = [&] {
+    for (int q = 0; q < 4; ++q) st->red[q] = 0.0;
+  };
+  if (st->done) { zero(); return; }
+  const double rr_prev = st->red[3];
+  if (check && sqrt(rr_prev) < tol) {
+    st->done = 1;
+    st->converged = 1;
+    st->conv_iter = st->iter - 1;
+    st->rr_final = rr_prev;
+    zero();
+    return;
+  }
+  if (check && !isfinite(rr_prev)) {
+    st->done = 3;
+    st->breakdown = 1;
+    st->conv_iter = st->iter - 1;
+    st->rr_final = rr_prev;
+    zero();
+    return;
+  }
+  // alpha of the pass whose (global) sums are being replaced — the pass after next pairs it
+  // into its x update; same division as f1_scalars so the bits agree
+  st->a_prev = first ? 0.0 : st->red[3] / st->red[0];
+  if (!first) {  // the clamp in f1_scalars, re-evaluated on the same global sums: count when it fired
+    const double a = st->red[3] / st->red[0];
+    const double est = fma(a * a, st->red[2], fma(-2.0 * a, st->red[1], st->red[3]));
+    if (!(est > 0.0)) st->clamps += 1;
+  }
+  for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
+  st->rr_new = tot[3];
+  st->iter += 1;
+}
+
+// In-kernel two-level last-arriver reduction (kernels.hpp RedCtl).  Runs in wave 0 after
+// block_partial4(wt = true): lanes 0-3 of that wave stored the block's partials write-through;
+// every hand-off is write-through stores -> s_waitcnt vmcnt(0) -> one relaxed agent-scope atomic
+// add, and the last arriver (told by the value its add returned) reads with write-through (sc1)
+// loads only (MI355X_MICROARCH.md, visibility: valid forms, first table row).
+__device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int g = (rc.base + (int)blockIdx.x) / kRedGroup;
+  const int g0 = g * kRedGroup - rc.base;  // the group's first slot, relative to `out`
+  const int gsize = min(kRedGroup, (int)gridDim.x - g0);
+  unsigned old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != (unsigned)(gsize - 1)) return;
+  if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = eng::wave_sum(v[q]);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st_wt(&rc.lvl2[q * rc.l2s + g], v[q]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[rc.top], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != (unsigned)(rc.ngroups - 1)) return;
+  if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[rc.top], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double t[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j = lane; j < rc.ngroups; j += 64) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] += ld_wt(&rc.lvl2[q * rc.l2s + j]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t[q] = eng::wave_sum(t[q]);
+  if (lane == 0) f1_bookkeep(st, t, rc.check, rc.first, tol);
+}
+
+// end of a fused pass: block partials, then (rc on) the in-kernel reduction
+__device__ __forceinline__ void f1_finish(double a0, double a1, double a2, double a3, double* __restrict__ out,
+                                          int pstride, const RedCtl& rc, CgState* st, double tol) {
+  block_partial4(a0, a1, a2, a3, out, pstride, rc.ngroups > 0);
+  if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
 }
 
 // non-temporal stores for the vectors the pass writes: they are re-read only by the next pass,
@@ -96,12 +195,14 @@ __device__ __forceinline__ void st_stream(double2* p, double2 v) {
 template <int FMT, typename IdxT, int U, bool RA>
 __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                double* __restrict__ partials, int pstride,
-                                               const CgState* __restrict__ st, double tol, int first, int check,
-                                               int final_mode, int k) {
+                                               CgState* st, double tol, int first, int check,
+                                               int final_mode, int k, RedCtl rc) {
   const int done = st->done;
-  if (done && !final_mode) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
-  if (sc.conv && !final_mode) return;  // x_{k-1} is the answer; the reduce latches
+  if ((done || sc.conv) && !final_mode) {  // x_{k-1} is the answer; the reduce latches
+    f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+    return;
+  }
   const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
   const double* __restrict__ ro = v.r_old;
   const double* __restrict__ apo = v.ap_old;
@@ -182,7 +283,7 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
   else if constexpr (FMT == 3) eng::sell<U, false, 1>(S, tr, gather, epi);
   else if constexpr (FMT == 4) eng::sell<U, false, 2>(S, tr, gather, epi);
   else eng::sell2<U, false>(S, tr, gather, epi);
-  block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
+  f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
 // ---------------------------------------------------------------------------
@@ -199,12 +300,14 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
 template <int CM, int U>
 __global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                     double* __restrict__ partials, int pstride,
-                                                    const CgState* __restrict__ st, double tol, int first,
-                                                    int check, int k) {
+                                                    CgState* st, double tol, int first,
+                                                    int check, int k, RedCtl rc) {
   __shared__ double2 s_dict[CM == 2 ? 256 : 1];
-  if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
-  if (sc.conv) return;
+  if (st->done || sc.conv) {
+    f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+    return;
+  }
   if constexpr (CM == 2) {
     for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
     __syncthreads();
@@ -311,7 +414,7 @@ __global__ __launch_bounds__(kBS) void k_cg_f1_pipe(SellDev S, F1Vectors v, int6
       }
     }
   }
-  block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
+  f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
 // loads of data one wave reads once (line-carry operands): optionally non-temporal
@@ -363,13 +466,15 @@ __device__ __forceinline__ double2 ld_once(const double2* p, bool nt) {
 template <int CM, int U, int PD, bool PAIR, bool GEN, int M2>
 __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride,
-                                                     const CgState* __restrict__ st, double tol, int first,
-                                                     int check, int32_t LO2) {
+                                                     CgState* st, double tol, int first,
+                                                     int check, int32_t LO2, RedCtl rc) {
   __shared__ double2 s_dict[CM >= 2 ? 256 : 1];
   __shared__ double s_far[M2 == 2 ? 2 * kWaves * 64 : 1];  // [step parity][wave][lane]: p_k of the next plane
-  if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
-  if (sc.conv) return;
+  if (st->done || sc.conv) {
+    f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+    return;
+  }
   if constexpr (CM >= 2) {
     for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
     __syncthreads();
@@ -674,7 +779,7 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
       c1 = c2;
     }
   }
-  block_partial4(s_pap, s_rap, s_apap, s_rr, partials, pstride);
+  f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
 __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __restrict__ partials, int pstride, int np,
@@ -712,9 +817,6 @@ __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __rest
     tot[q] = 0.0;
     for (int w = 0; w < kReduceBS / 64; ++w) tot[q] += sh[q][w];
   }
-  auto zero = [&] {
-    for (int q = 0; q < 4; ++q) st->red[q] = 0.0;
-  };
   if (mode == 2) {  // latch after the final pass's all-reduce
     if (st->done) return;
     st->done = 2;
@@ -723,35 +825,17 @@ __global__ __launch_bounds__(kReduceBS) void k_cg_reduce_f1(const double* __rest
     st->conv_iter = st->iter;
     return;
   }
-  if (st->done) { zero(); return; }
-  const double rr_prev = st->red[3];
-  if (check && sqrt(rr_prev) < tol) {
-    st->done = 1;
-    st->converged = 1;
-    st->conv_iter = st->iter - 1;
-    st->rr_final = rr_prev;
-    zero();
-    return;
-  }
-  if (check && !isfinite(rr_prev)) {
-    st->done = 3;
-    st->breakdown = 1;
-    st->conv_iter = st->iter - 1;
-    st->rr_final = rr_prev;
-    zero();
-    return;
-  }
   if (mode == 1) {
+    // the final pass: the latch tests exactly as mode 0, then only rr is kept
+    if (st->done || (check && (sqrt(st->red[3]) < tol || !isfinite(st->red[3])))) {
+      f1_bookkeep(st, tot, check, first, tol);
+      return;
+    }
     st->red[0] = st->red[1] = st->red[2] = 0.0;
     st->red[3] = tot[3];
     return;
   }
-  // alpha of the pass whose (global) sums are being replaced — the pass after next pairs it
-  // into its x update; same division as f1_scalars so the bits agree
-  st->a_prev = first ? 0.0 : st->red[3] / st->red[0];
-  for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
-  st->rr_new = tot[3];
-  st->iter += 1;
+  f1_bookkeep(st, tot, check, first, tol);
 }
 
 // ---------------------------------------------------------------------------
@@ -771,13 +855,12 @@ template <int CM, int U, bool RA>
 __global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                       const int32_t* __restrict__ win,
                                                       double* __restrict__ partials, int pstride,
-                                                      const CgState* __restrict__ st, double tol, int first,
-                                                      int check, int k) {
+                                                      CgState* st, double tol, int first,
+                                                      int check, int k, RedCtl rc) {
   extern __shared__ double s_win[];
   __shared__ double s_part[4][kWinWaves];
-  if (st->done) return;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
-  if (sc.conv) return;
+  const bool skip = st->done || sc.conv;
   const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
   const bool pair = (k & 1) != 0;  // paired x updates (see k_cg_f1)
   const double* __restrict__ ro = v.r_old;
@@ -803,7 +886,7 @@ __global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, in
   // chunks of kWinWaves slices touched by the (up to two) slice ranges of this launch
   const int64_t c0 = tr.b0 / kWinWaves, n0 = tr.e0 > tr.b0 ? (tr.e0 + kWinWaves - 1) / kWinWaves - c0 : 0;
   const int64_t c1 = tr.b1 / kWinWaves, n1 = tr.e1 > tr.b1 ? (tr.e1 + kWinWaves - 1) / kWinWaves - c1 : 0;
-  for (int64_t q = blockIdx.x; q < n0 + n1; q += gridDim.x) {
+  for (int64_t q = skip ? n0 + n1 : blockIdx.x; q < n0 + n1; q += gridDim.x) {
     const bool r0 = q < n0;
     const int64_t chunk = r0 ? c0 + q : c1 + (q - n0);
     const int64_t lo = win[2 * chunk], hi = win[2 * chunk + 1];
@@ -850,8 +933,10 @@ __global__ __launch_bounds__(kWinBS) void k_cg_f1_win(SellDev S, F1Vectors v, in
     double t = 0.0;
 #pragma unroll
     for (int k = 0; k < kWinWaves; ++k) t += s_part[threadIdx.x][k];
-    partials[threadIdx.x * pstride + blockIdx.x] = t;
+    if (rc.ngroups > 0) st_wt(&partials[threadIdx.x * pstride + blockIdx.x], t);
+    else partials[threadIdx.x * pstride + blockIdx.x] = t;
   }
+  if (rc.ngroups > 0) f1_reduce_tail(partials, pstride, rc, st, tol);
 }
 
 // per-chunk [lo, hi) ext-column window: one block per chunk, one thread per padded row
@@ -923,15 +1008,16 @@ void cg_fused1_win_prepare(int win_doubles) {
 }
 
 void cg_fused1_win(int cm, int param, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
-                   const int32_t* win, int win_doubles, double* partials, int pstride, int grid, const CgState* st,
-                   double tol, int first, int check, int k, hipStream_t stream) {
+                   const int32_t* win, int win_doubles, double* partials, int pstride, int grid, CgState* st,
+                   double tol, int first, int check, int k, hipStream_t stream, const RedCtl& rc) {
   if (tr.ntiles == 0 || grid == 0) return;
   const size_t lds = (size_t)win_doubles * sizeof(double);
   MCG_CHECK(lds <= kWinMaxLds, "window exceeds the LDS budget");
   MCG_CHECK(cm == 0 || cm == 1, "windowed pass supports SELL-64 and SELL-64/d16");
+  MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
 #define MCG_W(CM, U, RA)                                                                                      \
   hipLaunchKernelGGL((k_cg_f1_win<CM, U, RA>), dim3(grid), dim3(kWinBS), lds, stream, S, v, own_off, tr, win, \
-                     partials, pstride, st, tol, first, check, k)
+                     partials, pstride, st, tol, first, check, k, rc)
 #define MCG_WU(CM, RA) \
   do { if (param <= 4) MCG_W(CM, 4, RA); else if (param <= 6) MCG_W(CM, 6, RA); else MCG_W(CM, 8, RA); } while (0)
   const bool ra = v.ra_old != nullptr;
@@ -948,12 +1034,14 @@ bool carry_block_exchange_ok(int param, int32_t lo2, int64_t strip) {
 
 void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, bool block_exchange, const SellDev& S,
                      const F1Vectors& v, int64_t own_off, const TileRanges& tr, double* partials, int pstride,
-                     int grid, const CgState* st, double tol, int first, int check, int k, hipStream_t stream) {
+                     int grid, CgState* st, double tol, int first, int check, int k, hipStream_t stream,
+                     const RedCtl& rc) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0, "line-carry pass needs whole grid lines");
   MCG_CHECK(v.ra_old != nullptr && cm >= 1 && cm <= 3 && param >= 4 && param <= 8,
             "line-carry pass needs SELL-64 d16/c8/c4 with interleaved pairs");
   MCG_CHECK(depth >= 1 && depth <= 3, "line-carry prefetch depth must be 1..3");
+  MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
   MCG_CHECK(general || cm >= 2, "the specialised line-carry pass needs the c8 dictionary");
   MCG_CHECK(cm != 3 || (!general && lo2 == 0 && S.codes4 != nullptr), "4-bit codes: specialised 2-D pass only");
   MCG_CHECK(lo2 == 0 || (cm == 2 && !general && lo2 > 1), "the +-LO2 carry needs the specialised c8 pass");
@@ -962,7 +1050,7 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, bo
   const bool pair = (k & 1) != 0;
 #define MCG_C(CM, U, PD, PAIR, GEN, M2)                                                                         \
   hipLaunchKernelGGL((k_cg_f1_carry<CM, U, PD, PAIR, GEN, M2>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
-                     tr, partials, pstride, st, tol, first, check, lo2)
+                     tr, partials, pstride, st, tol, first, check, lo2, rc)
 #define MCG_CP(CM, U, PD, GEN, M2)                     \
   do {                                                 \
     if (pair) MCG_C(CM, U, PD, true, GEN, M2);         \
@@ -1009,12 +1097,14 @@ void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream) {
 
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
-               const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
-               int first, int check, int final_mode, int k, hipStream_t stream, bool pipe) {
+               const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol,
+               int first, int check, int final_mode, int k, hipStream_t stream, bool pipe, const RedCtl& rc) {
   if (tr.ntiles == 0 || grid == 0) return;
+  MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
+            "in-kernel reduction: bad control block");
 #define MCG_F1(F, U, RA)                                                                                   \
   hipLaunchKernelGGL((k_cg_f1<F, IdxT, U, RA>), dim3(grid), dim3(kBS), 0, stream, A, S, v, own_off, tr, \
-                     partials, pstride, st, tol, first, check, final_mode, k)
+                     partials, pstride, st, tol, first, check, final_mode, k, rc)
 // SELL engines take U = 4..8 (U = the slice width avoids clamped duplicate gathers)
 #define MCG_F1U(F, RA)                                  \
   do {                                                  \
@@ -1029,7 +1119,7 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
   if (pipe && !final_mode && ra && (fmt == 3 || fmt == 4) && param >= 4 && param <= 8) {
 #define MCG_PIPE(CM, U)                                                                                        \
   hipLaunchKernelGGL((k_cg_f1_pipe<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, partials, pstride, \
-                     st, tol, first, check, k)
+                     st, tol, first, check, k, rc)
 #define MCG_PIPEU(CM)                          \
   do {                                         \
     if (param == 4) MCG_PIPE(CM, 4);           \
@@ -1055,11 +1145,11 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 template void cg_fused1<int32_t>(int, int, const CsrDev<int32_t>&, const SellDev&, const F1Vectors&, int64_t,
-                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int, int,
-                                 hipStream_t, bool);
+                                 const TileRanges&, double*, int, int, CgState*, double, int, int, int, int,
+                                 hipStream_t, bool, const RedCtl&);
 template void cg_fused1<int64_t>(int, int, const CsrDev<int64_t>&, const SellDev&, const F1Vectors&, int64_t,
-                                 const TileRanges&, double*, int, int, const CgState*, double, int, int, int, int,
-                                 hipStream_t, bool);
+                                 const TileRanges&, double*, int, int, CgState*, double, int, int, int, int,
+                                 hipStream_t, bool, const RedCtl&);
 
 void cg_reduce_f1(const double* partials, int pstride, int np, CgState* st, int mode, int check, int first,
                   double tol, hipStream_t stream) {

@@ -65,6 +65,12 @@ void Comm::broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream
   MCG_RCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, root, reduce_, stream), "RCCL broadcast failed");
 }
 
+int Comm::count() const {
+  int n = 0;
+  MCG_RCCL(ncclCommCount(reduce_, &n), "RCCL comm count failed");
+  return n;
+}
+
 void Comm::check_async() {
   for (ncclComm_t c : {reduce_, halo_}) {
     ncclResult_t async = ncclSuccess;

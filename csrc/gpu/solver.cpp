@@ -318,12 +318,29 @@ void GpuCgSolver::setup() {
   g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
-  const int np = std::max({g_all_, g_int_ + g_bnd_, g_b_, 1});
+  const bool split = use_halo_ && opt_.overlap;
+  fused_red_ = opt_.recurrence == 1 && opt_.fused_reduce != 0;
+  auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
+  // the boundary launch's partials start on a reduction-group boundary: round the interior grid up
+  // (the extra blocks find no work in the grid-stride loops and contribute zero partials)
+  if (split && fused_red_ && g_int_ > 0) g_int_ = groups(g_int_) * kern::kRedGroup;
+  bnd_base_ = split ? g_int_ : 0;
+  const int np = std::max({g_all_, split ? g_int_ + g_bnd_ : 0, g_b_, 1});
   pstride_ = np + 64;
   partials_.allocate((size_t)pstride_ * (opt_.recurrence == 1 ? 4 : 1), "partials");
   st_.allocate(1, "state");
   MCG_HIP(hipMemsetAsync(partials_.get(), 0, partials_.bytes(), s0_), "device memset failed");
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s0_), "device memset failed");
+  if (fused_red_) {
+    red_groups_all_ = groups(g_all_);
+    red_groups_split_ = split ? groups(g_int_) + groups(g_bnd_) : 0;
+    red_l2s_ = std::max({red_groups_all_, red_groups_split_, 1});
+    red_cnt_.allocate(red_l2s_ + 1, "partials");
+    red_l2_.allocate((size_t)4 * red_l2s_, "partials");
+    MCG_HIP(hipMemsetAsync(red_cnt_.get(), 0, red_cnt_.bytes(), s0_), "device memset failed");
+    MCG_HIP(hipMemsetAsync(red_l2_.get(), 0, red_l2_.bytes(), s0_), "device memset failed");
+  }
+  info_.fused_reduce = fused_red_;
   MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
 
   info_.device_bytes = matrix_bytes + (size_t)(3 * n + 3 * L_.ext_len) * 8 + (rp64_.bytes());
@@ -510,7 +527,7 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
   double* pnew = p_[k & 1].get();
   const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
   const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
-  double* part = partials_.get() + (which == 2 ? g_int_ : 0);
+  double* part = partials_.get() + (which == 2 ? bnd_base_ : 0);
   if (grid == 0) return;
   const int64_t n = L_.n_local();
   if (opt_.format == 1) {
@@ -533,13 +550,25 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
   }
 }
 
-void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
+void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) {
   const int first = (k == 0) ? 1 : 0;
   const int check = (k >= 2) ? 1 : 0;  // the reference never tests r_0
   const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
   const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
-  double* part = partials_.get() + (which == 2 ? g_int_ : 0);
+  double* part = partials_.get() + (which == 2 ? bnd_base_ : 0);
   if (grid == 0) return;
+  kern::RedCtl rc;
+  if (fused_red) {
+    MCG_CHECK(fused_red_ && !final_mode, "in-kernel reduction not set up");
+    rc.cnt = red_cnt_.get();
+    rc.lvl2 = red_l2_.get();
+    rc.l2s = red_l2s_;
+    rc.top = red_l2s_;
+    rc.base = which == 2 ? bnd_base_ : 0;
+    rc.ngroups = which == 0 ? red_groups_all_ : red_groups_split_;
+    rc.check = check;
+    rc.first = first;
+  }
   const int64_t n = L_.n_local();
   const bool odd = (k & 1) != 0;
   DeviceBuffer<double>& r_new = odd ? r1_ : r_;
@@ -560,23 +589,23 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode) {
     kern::cg_fused1_carry(codes4_.get() && !carry_general_ && carry_lo2_ == 0 ? 3 : (c8_ ? 2 : 1), info_.spmv_param,
                           opt_.carry_depth > 0 ? opt_.carry_depth : (carry_lo2_ > 0 ? 1 : 3), carry_general_,
                           carry_lo2_, info_.carry_xchg, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
-                          opt_.tol, first, check, k, s0_);
+                          opt_.tol, first, check, k, s0_, rc);
     return;
   }
   if (win_doubles_ > 0 && !final_mode) {
     kern::cg_fused1_win(d16_ ? 1 : 0, info_.spmv_param, S, v, L_.own_off, tr, win_.get(), win_doubles_, part,
-                        pstride_, grid, st_.get(), opt_.tol, first, check, k, s0_);
+                        pstride_, grid, st_.get(), opt_.tol, first, check, k, s0_, rc);
     return;
   }
   const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1))) : 0;
   if (info_.idx64)
     kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,
                              L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
-                             s0_, pipe_);
+                             s0_, pipe_, rc);
   else
     kern::cg_fused1<int32_t>(fmt, info_.spmv_param, CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, S, v,
                              L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
-                             s0_, pipe_);
+                             s0_, pipe_, rc);
 }
 
 void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
@@ -598,6 +627,7 @@ void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
   trace::Range tr_("mcg.iteration.single_reduction");
   int np = g_all_;
+  const bool fr = fused_red_;
   if (use_halo_ && opt_.overlap) {
     if (halo_ready_for_ != k) {
       MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
@@ -605,9 +635,9 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
       enqueue_halo_f1_(k, s1_);
       MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
     }
-    enqueue_f1_(k, 1, 0);  // interior rows || halo on the side stream
+    enqueue_f1_(k, 1, 0, fr);  // interior rows || halo on the side stream
     MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
-    enqueue_f1_(k, 2, 0);  // boundary rows
+    enqueue_f1_(k, 2, 0, fr);  // boundary rows (its last arriver finishes the reduction)
     np = g_int_ + g_bnd_;
     halo_ready_for_ = -1;
     if (prefetch_halo_) {
@@ -621,12 +651,12 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     }
   } else if (use_halo_) {
     enqueue_halo_f1_(k, s0_);
-    enqueue_f1_(k, 0, 0);
+    enqueue_f1_(k, 0, 0, fr);
   } else {
-    enqueue_f1_(k, 0, 0);
+    enqueue_f1_(k, 0, 0, fr);
   }
   CgState* st = st_.get();
-  kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
+  if (!fr) kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
 }
 
@@ -707,16 +737,25 @@ void GpuCgSolver::run_iterations(int count) {
                        e.detail().c_str());
           (void)hipGetLastError();
           opt_.use_graph = false;
+          ++info_.graph_fallbacks;
           continue;
         }
       }
-      const hipError_t le = hipGraphLaunch(graph_exec_[kind], s0_);
+      const hipError_t le = (k_ == opt_.fail_graph_launch_at) ? hipErrorInvalidValue  // test hook
+                                                              : hipGraphLaunch(graph_exec_[kind], s0_);
       if (le != hipSuccess) {
-        // nothing was enqueued: run these iterations eagerly from here on
-        std::fprintf(stderr, "[mcg] graph launch failed (%s); running eagerly\n", hipGetErrorString(le));
         (void)hipGetLastError();
+        // Only errors that hipGraphLaunch reports while validating its arguments, before it enqueues
+        // any node, leave the state untouched; anything else may have run part of the graph (x, r, p
+        // updated twice on replay) and is fatal, as is every error on a multi-rank run.
+        const bool nothing_ran = le == hipErrorInvalidValue || le == hipErrorInvalidResourceHandle ||
+                                 le == hipErrorOutOfMemory;
+        if (!nothing_ran || world_ > 1) MCG_HIP(le, "graph launch failed");
+        std::fprintf(stderr, "[mcg] graph launch failed (%s); running eagerly\n", hipGetErrorString(le));
+        MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");  // earlier launches may still run
         drop_graphs_();
         opt_.use_graph = false;
+        ++info_.graph_fallbacks;
         continue;
       }
       const int done = kind == 0 ? 2 : glong;
@@ -961,6 +1000,7 @@ CgResult GpuCgSolver::result() {
   r.iterations = st.done ? st.conv_iter : st.iter;
   r.converged = st.converged != 0;
   r.breakdown = st.breakdown != 0;
+  r.beta_clamps = st.clamps;
   r.rnorm = std::sqrt(st.done ? st.rr_final : (opt_.recurrence == 1 ? st.red[3] : st.rr_new));
   r.setup_seconds = setup_seconds_;
   float ms = 0.f;

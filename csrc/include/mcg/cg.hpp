@@ -65,6 +65,10 @@ struct CgOptions {
   int vec_skew = 0;         // experiment: stagger the vector buffers' base addresses by i * vec_skew 256-B blocks
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
+  int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
+                             // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
+                             // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
+  int fail_graph_launch_at = -1;  // test hook: report the graph launch at this iteration as failed (nothing enqueued)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   int force_idx64 = 0;       // test hook: int64 row pointers even when int32 would do
@@ -78,6 +82,7 @@ struct CgResult {
   bool converged = false;
   bool breakdown = false;    // NaN/Inf in a reduction
   double rnorm = 0.0;        // final ||r||_2 (recurrence residual)
+  int beta_clamps = 0;       // single-reduction form: passes whose expanded ||r_k||^2 estimate was clamped at 0
   double setup_seconds = 0.0;
   double solve_seconds = 0.0;
   double iters_per_second() const { return solve_seconds > 0 ? iterations / solve_seconds : 0.0; }

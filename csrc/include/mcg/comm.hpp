@@ -71,6 +71,8 @@ class Comm final : public Communicator {
   void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
                      const int* widths = nullptr) override;
   void check_async() override;
+  // ranks in the communicator as RCCL sees them (ncclCommCount)
+  int count() const;
   // generic device-buffer collectives used by gathers / tests
   void allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream);
   void broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream);

@@ -41,7 +41,8 @@ struct alignas(64) CgState {
   int conv_iter;  // iteration count at the latch
   int converged;  // ||r|| < tol at the end
   int breakdown;  // NaN/Inf seen
-  int pad_[3];
+  int clamps;     // single-reduction form: passes whose expanded ||r - a Ap||^2 was <= 0 (beta clamped to 0)
+  int pad_[2];
 };
 
 enum ReduceMode : int { kReduceInit = 0, kReduceA = 1, kReduceB = 2, kReduceFinal = 3, kReduceScalar = 4 };
@@ -184,13 +185,32 @@ struct F1Vectors {
   int64_t ext_len = 0;  // ext-layout length of r / Ap / p (bounds of the line-carry pass's edge loads)
   int nt_loads = 0;     // line-carry pass: non-temporal loads of the once-read operands
 };
+// In-kernel reduction of a fused pass's block partials (replaces the cg_reduce_f1 launch, so
+// one iteration is ONE kernel + the 32-B all-reduce).  Two-level last-arriver fan-in: each block
+// stores its 4 partials write-through (sc1) and adds to its group's counter (kRedGroup blocks
+// per group); the group's last arriver sums the group's partials in block order into lvl2 and
+// adds to the top counter; the last group sums lvl2 in group order and updates the CgState
+// exactly as cg_reduce_f1 mode 0 does.  Every sum has a fixed order (bitwise reproducible, and
+// the same value however the blocks are scheduled).  Counters are zeroed at setup and reset by
+// their last arriver.  The launches of one iteration (interior + boundary) share the groups:
+// `base` = the launch's first partial slot, a multiple of kRedGroup.
+constexpr int kRedGroup = 64;
+struct RedCtl {
+  unsigned* cnt = nullptr;  // [top] group counters, cnt[top] = the top counter
+  double* lvl2 = nullptr;   // [4][l2s] group sums
+  int l2s = 0, top = 0;
+  int base = 0;
+  int ngroups = 0;          // groups over every launch of the iteration; 0 = off
+  int check = 0, first = 0; // as cg_reduce_f1 mode 0
+};
 // `k`: pass index (its parity selects the paired x update; final mode: m = k)
 template <typename IdxT>
 void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const F1Vectors& v, int64_t own_off,
-               const TileRanges& tr, double* partials, int pstride, int grid, const CgState* st, double tol,
+               const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol,
                int first, int check, int final_mode, int k, hipStream_t stream,
                bool pipe = false /* software-pipelined stencil pass: SELL d16/c8 + interleaved, every slice
-                                    width <= param */);
+                                    width <= param */,
+               const RedCtl& rc = RedCtl());
 // Line-carry variant for structured-grid stencils (SELL d16/c8 + interleaved {r, Ap}, every
 // slice width <= param): `slices.strip` = S slices per grid line (the carried column offset is
 // one line, 64 S rows), the launch one range of whole lines; a wave walks down one column of
@@ -202,8 +222,8 @@ void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,
                      bool block_exchange /* lo2 rows of a block's inner waves through LDS (carry_block_exchange_ok) */,
                      const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& slices,
-                     double* partials, int pstride, int grid, const CgState* st, double tol, int first, int check,
-                     int k, hipStream_t stream);
+                     double* partials, int pstride, int grid, CgState* st, double tol, int first, int check,
+                     int k, hipStream_t stream, const RedCtl& rc = RedCtl());
 // Windowed variant for long banded rows: 1024-row chunks (16 slices) stage p_k for their
 // column window [win[2c], win[2c+1]) in LDS once, the SpMV gathers from LDS.
 constexpr int kWinRows = 1024;
@@ -213,8 +233,8 @@ int64_t win_chunks(const TileRanges& slices);  // chunks touched by a launch (gr
 void cg_fused1_win_prepare(int win_doubles);     // setup: dynamic-LDS limit of the windowed kernels
 void cg_fused1_win(int cm /* 0 SELL-64, 1 SELL-64/d16 */, int param, const SellDev& S, const F1Vectors& v,
                    int64_t own_off, const TileRanges& slices, const int32_t* win, int win_doubles, double* partials,
-                   int pstride, int grid, const CgState* st, double tol, int first, int check, int k,
-                   hipStream_t stream);
+                   int pstride, int grid, CgState* st, double tol, int first, int check, int k,
+                   hipStream_t stream, const RedCtl& rc = RedCtl());
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),

@@ -51,6 +51,8 @@ struct SolverInfo {
   bool pipeline = false;
   int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
+  bool fused_reduce = false;  // the pass reduces its own block partials (one kernel per iteration)
+  int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
@@ -96,7 +98,8 @@ class GpuCgSolver {
   template <typename IdxT> void build_csr_(DeviceBuffer<int64_t>& rp64);
   void enqueue_iteration_(int k);
   void enqueue_spmv_(int k, int which, int final_mode);  // which: 0 all, 1 interior, 2 boundary
-  void enqueue_f1_(int k, int which, int final_mode);    // single-reduction fused pass
+  // single-reduction fused pass; `fused_red`: this launch takes part in the in-kernel reduction
+  void enqueue_f1_(int k, int which, int final_mode, bool fused_red = false);
   void enqueue_halo_f1_(int k, hipStream_t s);            // ghosts iteration k of the single-reduction form reads
   void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
@@ -157,6 +160,11 @@ class GpuCgSolver {
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
   DeviceBuffer<double> ra_[2];     // interleaved {r, Ap} pairs by parity (2 * ext_len doubles each)
   int pstride_ = 0;                // partial-array stride (4 arrays in the single-reduction form)
+  int bnd_base_ = 0;               // first partial slot of the boundary launch (a multiple of kRedGroup)
+  bool fused_red_ = false;         // in-kernel reduction of the fused pass (CgOptions::fused_reduce)
+  int red_groups_all_ = 0, red_groups_split_ = 0, red_l2s_ = 0;
+  DeviceBuffer<unsigned> red_cnt_;  // group counters + top counter (zeroed at setup, reset by the kernels)
+  DeviceBuffer<double> red_l2_;     // [4][red_l2s_] group sums
   DeviceBuffer<CgState> st_;
   PinnedBuffer<CgState> host_st_;
   // launch geometry

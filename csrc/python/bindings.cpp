@@ -71,6 +71,7 @@ py::dict result_dict(const CgResult& r) {
   d["converged"] = r.converged;
   d["breakdown"] = r.breakdown;
   d["rnorm"] = r.rnorm;
+  d["beta_clamps"] = r.beta_clamps;
   d["setup_seconds"] = r.setup_seconds;
   d["solve_seconds"] = r.solve_seconds;
   d["iters_per_second"] = r.iters_per_second();
@@ -163,6 +164,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry_c4", &CgOptions::carry_c4)
       .def_readwrite("carry_nt", &CgOptions::carry_nt)
       .def_readwrite("carry_depth", &CgOptions::carry_depth)
+      .def_readwrite("fused_reduce", &CgOptions::fused_reduce)
+      .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
@@ -245,6 +248,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("rank"), py::arg("world"), py::arg("reduce_id"), py::arg("halo_id"))
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
+      .def_property_readonly("count", &Comm::count)
       .def("allreduce_sum_ptr", [](Comm& c, uintptr_t buf, size_t count, uintptr_t stream) {
         c.allreduce_sum(reinterpret_cast<double*>(buf), count, as_stream(stream));
       })
@@ -306,6 +310,8 @@ PYBIND11_MODULE(_C, m) {
         d["pipeline"] = i.pipeline;
         d["strip"] = i.strip;
         d["carry"] = i.carry;
+        d["fused_reduce"] = i.fused_reduce;
+        d["graph_fallbacks"] = i.graph_fallbacks;
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;
         d["carry_xchg"] = i.carry_xchg;

@@ -26,29 +26,34 @@ to the same HIP runtime and RCCL (matching SONAMEs) instead of a second copy.
 """
 from __future__ import annotations
 
+import importlib as _importlib
 import os as _os
 
 import torch as _torch  # noqa: F401  (must precede the native extension; see docstring)
 
-try:
-    from . import _C  # type: ignore[attr-defined]
-except ImportError as _e:  # pragma: no cover - exercised only when the build is missing
-    _C = None
-    _IMPORT_ERROR = _e
-else:
-    _IMPORT_ERROR = None
+_C = None  # the native extension, loaded on first use by native()
+_IMPORT_ERROR = None
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"
 
 
 def native():
-    """Return the native extension module, raising loudly if it was not built."""
+    """Return the native extension module, raising loudly if it was not built.
+
+    Loaded lazily so that launchers (``parallel/launch.py``) can start the per-GPU ranks
+    before this process maps any HIP code."""
+    global _C, _IMPORT_ERROR
     if _C is None:
-        raise ImportError(
-            "cuda_mpi_parallel_amd native extension (_C) is not built: run `make -j8` "
-            "or `python -c 'import __graft_entry__ as g; g.build()'` in the repo root "
-            f"({_IMPORT_ERROR})"
-        )
+        try:
+            mod = _importlib.import_module(__name__ + "._C")
+        except ImportError as e:
+            _IMPORT_ERROR = e
+            raise ImportError(
+                "cuda_mpi_parallel_amd native extension (_C) is not built: run `make -j8` "
+                "or `python -c 'import __graft_entry__ as g; g.build()'` in the repo root "
+                f"({_IMPORT_ERROR})"
+            ) from e
+        _C = mod
     return _C
 
 
