@@ -87,6 +87,19 @@ def main(argv=None) -> int:
 
 
 def run_rank(args) -> int:
+    # stdout carries exactly one JSON line: RCCL prints a version banner on stdout at communicator
+    # init, so fd 1 points at stderr until the result is printed
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return _run_rank(args, out_fd)
+    finally:
+        sys.stdout.flush()
+        os.dup2(out_fd, 1)
+        os.close(out_fd)
+
+
+def _run_rank(args, out_fd) -> int:
     import torch
     import torch.distributed as dist
 
@@ -187,7 +200,7 @@ def run_rank(args) -> int:
     model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" if args.problem == "randspd"
              else f"{args.problem}_N{args.grid}")
     if env.rank == 0:
-        print(json.dumps({
+        line = json.dumps({
             "metric": METRIC if headline else "CG iterations/sec (whole node), %s" % model,
             "value": round(value, 4),
             "unit": "iterations/s",
@@ -226,7 +239,9 @@ def run_rank(args) -> int:
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
                       "placement_lead_trial": info.get("placement_lead_trial"),"model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
                       "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3), **extra},
-        }), flush=True)
+        })
+        sys.stdout.flush()
+        os.write(out_fd, (line + "\n").encode())
     if env.world > 1:
         dist.barrier()
         dist.destroy_process_group()
