@@ -28,7 +28,7 @@ GPU_CPP   := $(wildcard csrc/gpu/*.cpp)
 HIP_OBJ   := $(patsubst csrc/%.hip,$(BUILD)/%.o,$(HIP_SRC))
 HOST_OBJ  := $(patsubst csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(GPU_CPP))
 CORE_OBJ  := $(HIP_OBJ) $(HOST_OBJ)
-HEADERS   := $(wildcard csrc/include/mcg/*.hpp)
+HEADERS   := $(wildcard csrc/include/mcg/*.hpp) $(wildcard csrc/gpu/*.hpp)
 
 all: $(PYMOD) $(CLI) $(TESTBIN)
 

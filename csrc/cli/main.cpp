@@ -7,14 +7,16 @@
 // everything through printf, CUDACG.cu:11) and exits 1; details go to stderr.
 //
 // Flags (all additive):
-//   --problem demo|poisson2d|poisson3d|randspd   --n N   --rows R --band W --density q
+//   --problem demo|poisson2d|poisson3d|randspd|csr   --n N   --rows R --band W --density q --spread S
+//   --matrix FILE.mtx (a user matrix, problem csr)  --rhs-file FILE (its b: Matrix Market array / one per line)
 //   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
 //   --maxit M  --tol T  --rtol R (||r|| < R ||b||)  --check-every K  --fixed-iters K  --warmup W
 //   --nnz-per-row m (random-spd: density = (m - 1) / (2 band))
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
 //   --spmv-variant 0|1|2|3  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
 //   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off  --window auto|on|off
-//   --carry auto|on|off (line-carry stencil pass)
+//   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
+//   --fused-reduce auto|on|off  --watchdog SECONDS
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
 //   --print-x auto|yes|no  --report text|json  --verify
 // Multi-GPU runs use one host thread per GPU inside this process (no MPI in
@@ -28,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -36,6 +39,7 @@
 #include "mcg/cg.hpp"
 #include "mcg/check.hpp"
 #include "mcg/comm.hpp"
+#include "mcg/matrix.hpp"
 #include "mcg/solver.hpp"
 
 using namespace mcg;
@@ -57,7 +61,16 @@ struct Args {
   bool rhs_set = false;
   bool format_set = false, recurrence_set = false;
   std::string resume;  // checkpoint prefix to resume from
+  std::string matrix, rhs_file;  // user matrix (Matrix Market) and its right-hand side
+  std::shared_ptr<HostMatrix> mat;
 };
+
+int tri(const std::string& v, const char* flag) {  // auto|on|off -> -1|1|0
+  if (v == "auto" || v == "-1") return -1;
+  if (v == "on" || v == "1" || v == "yes") return 1;
+  if (v == "off" || v == "0" || v == "no") return 0;
+  fail(std::string("invalid arguments: ") + flag + " " + v);
+}
 
 [[noreturn]] void usage_error(const std::string& m) { fail("invalid arguments: " + m); }
 
@@ -69,11 +82,24 @@ Args parse(int argc, char** argv) {
   };
   for (int i = 1; i < argc; ++i) {
     std::string f = argv[i];
-    if (f == "--problem") a.spec.kind = parse_problem_kind(need(i));
+    if (f == "--problem") {
+      std::string v = need(i);
+      if (v == "csr") a.spec.kind = ProblemKind::Csr;
+      else a.spec.kind = parse_problem_kind(v);
+    }
     else if (f == "--n") a.spec.N = std::stoll(need(i));
     else if (f == "--rows") a.spec.rows = std::stoll(need(i));
     else if (f == "--band") a.spec.band = std::stoll(need(i));
     else if (f == "--density") a.spec.density = std::stod(need(i));
+    else if (f == "--spread") a.spec.spread = std::stoll(need(i));
+    else if (f == "--matrix") a.matrix = need(i);
+    else if (f == "--rhs-file") a.rhs_file = need(i);
+    else if (f == "--halo-mode") {
+      std::string v = need(i);
+      a.opt.halo_mode = v == "window" ? 0 : (v == "allgather" ? 1 : tri(v, "--halo-mode"));
+    }
+    else if (f == "--pmat") a.opt.pmat = tri(need(i), "--pmat");
+    else if (f == "--fused-reduce") a.opt.fused_reduce = tri(need(i), "--fused-reduce");
     else if (f == "--rhs") { a.spec.rhs = parse_rhs_kind(need(i)); a.rhs_set = true; }
     else if (f == "--seed") a.spec.seed = std::stoull(need(i));
     else if (f == "--gpus") a.gpus = std::stoi(need(i));
@@ -111,28 +137,32 @@ Args parse(int argc, char** argv) {
     else if (f == "--inject-nan-at") a.opt.inject_nan_at = std::stoi(need(i));
     else if (f == "--recurrence") {
       std::string v = need(i);
-      a.opt.recurrence = (v == "single" || v == "fused1" || v == "1") ? 1 : 0;
+      if (v == "auto" || v == "-1") a.opt.recurrence = -1;
+      else if (v == "single" || v == "fused1" || v == "1") a.opt.recurrence = 1;
+      else if (v == "two" || v == "0") a.opt.recurrence = 0;
+      else usage_error("--recurrence " + v);
       a.recurrence_set = true;
     }
-    else if (f == "--window") {
-      std::string v = need(i);
-      a.opt.window = v == "auto" ? -1 : ((v == "on" || v == "1") ? 1 : 0);
-    }
-    else if (f == "--carry") {
-      std::string v = need(i);
-      a.opt.carry = v == "auto" ? -1 : ((v == "on" || v == "1") ? 1 : 0);
-    }
-    else if (f == "--interleave") {
-      std::string v = need(i);
-      a.opt.interleave = v == "auto" ? -1 : ((v == "on" || v == "1") ? 1 : 0);
-    }
+    else if (f == "--window") a.opt.window = tri(need(i), "--window");
+    else if (f == "--carry") a.opt.carry = tri(need(i), "--carry");
+    else if (f == "--interleave") a.opt.interleave = tri(need(i), "--interleave");
     else if (f == "--print-x") a.print_x = need(i);
     else if (f == "--report") a.report = need(i);
     else if (f == "--verify") a.verify = true;
     else if (f == "-h" || f == "--help") {
-      std::fprintf(stderr, "see csrc/cli/main.cpp header for flags\n");
+      std::fprintf(stderr, "flags: cuda_mpi_parallel_amd/cli_spec.py (shared with python -m cuda_mpi_parallel_amd)\n");
       std::exit(0);
     } else usage_error(f);
+  }
+  if (!a.matrix.empty()) a.spec.kind = ProblemKind::Csr;
+  if (a.spec.kind == ProblemKind::Csr) {
+    if (a.matrix.empty()) usage_error("--problem csr needs --matrix FILE");
+    a.mat.reset(read_matrix_market(a.matrix));
+    if (!a.rhs_file.empty()) a.mat->set_rhs(read_vector(a.rhs_file));
+    if (!a.rhs_set) a.spec.rhs = RhsKind::Reference;  // the file's b, ones without one
+    a.rhs_set = true;
+    a.spec.csr = &a.mat->view();
+    a.spec.N = 0;
   }
   if (a.spec.kind == ProblemKind::RandomSPD) {
     if (a.spec.rows <= 0) a.spec.rows = 100000;
@@ -144,7 +174,9 @@ Args parse(int argc, char** argv) {
   // single-reduction form); the built-in demo keeps the reference's CSR and two-reduction order
   if (a.spec.kind != ProblemKind::Demo && !a.format_set) a.opt.format = 3;
   if (a.spec.kind != ProblemKind::Demo && !a.recurrence_set) a.opt.recurrence = -1;
-  if (a.spec.kind != ProblemKind::Demo && a.spec.N == 3 && a.spec.kind != ProblemKind::RandomSPD) a.spec.N = 1024;
+  // default grids, as make_problem(): 1024^2 (BASELINE config 1's size) and 128^3
+  if (a.spec.kind == ProblemKind::Poisson2D && a.spec.N == 3) a.spec.N = 1024;
+  if (a.spec.kind == ProblemKind::Poisson3D && a.spec.N == 3) a.spec.N = 128;
   return a;
 }
 

@@ -39,6 +39,19 @@ void Comm::allreduce_sum(double* buf, size_t count, hipStream_t stream) {
 void Comm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
                          const int* widths) {
   if (!L.has_halo()) return;
+  if (L.allgather) {
+    // unstructured sparsity: every rank's block to every rank, in place (own_off = rank * block,
+    // the recv buffer is the whole ext vector); one collective per vector in one group
+    MCG_RCCL(ncclGroupStart(), "RCCL group failed");
+    for (int v = 0; v < nvec; ++v) {
+      const int64_t w = widths ? widths[v] : 1;
+      MCG_RCCL(ncclAllGather(ext_vecs[v] + w * L.own_off, ext_vecs[v], (size_t)(w * L.block), ncclFloat64, halo_,
+                             stream),
+               "RCCL allgather failed");
+    }
+    MCG_RCCL(ncclGroupEnd(), "RCCL group failed");
+    return;
+  }
   MCG_RCCL(ncclGroupStart(), "RCCL group failed");
   // Matching rule: for each (me, peer) pair both sides post their messages in the
   // same order — vector-major, then ascending global row (make_layout builds
@@ -55,14 +68,6 @@ void Comm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec
                "RCCL halo recv failed");
   }
   MCG_RCCL(ncclGroupEnd(), "RCCL group failed");
-}
-
-void Comm::allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream) {
-  MCG_RCCL(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, reduce_, stream), "RCCL allgather failed");
-}
-
-void Comm::broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream) {
-  MCG_RCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, root, reduce_, stream), "RCCL broadcast failed");
 }
 
 int Comm::count() const {

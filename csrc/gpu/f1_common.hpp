@@ -1,0 +1,173 @@
+// Device helpers shared by the single-reduction passes (cg_fused1.hip: fused pass; cg_split.hip:
+// the materialized-p split pass): the per-pass scalars, block partials, the in-kernel two-level
+// reduction and the CgState bookkeeping.  Included inside namespace mcg::kern::(anonymous).
+#pragma once
+
+using eng::kBS;
+using eng::kWaves;
+
+struct F1Scalars {
+  double alpha, beta;
+  bool conv;
+};
+
+__device__ __forceinline__ F1Scalars f1_scalars(const CgState* st, double tol, int first, int check) {
+  F1Scalars s;
+  const double pAp = st->red[0], rAp = st->red[1], ApAp = st->red[2], rr = st->red[3];
+  s.conv = check && sqrt(rr) < tol;  // ||r_{k-1}|| < tol : the reference's break (CUDACG.cu:333)
+  if (first) {
+    s.alpha = 0.0;
+    s.beta = 0.0;
+  } else {
+    s.alpha = rr / pAp;
+    double est = fma(s.alpha * s.alpha, ApAp, fma(-2.0 * s.alpha, rAp, rr));  // ||r_{k-1} - a Ap_{k-1}||^2
+    est = est > 0.0 ? est : 0.0;
+    s.beta = est / rr;
+  }
+  return s;
+}
+
+// agent-scope (write-through, L1-bypassing) 8-B accesses for the in-kernel reduction's hand-offs
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// four fixed-order block partials -> partials[q * pstride + blockIdx.x] (write-through when an
+// in-kernel reduction reads them)
+__device__ __forceinline__ void block_partial4(double a0, double a1, double a2, double a3, double* __restrict__ out,
+                                               int pstride, bool wt = false) {
+  __shared__ double sh[4][kWaves];
+  a0 = eng::wave_sum(a0);
+  a1 = eng::wave_sum(a1);
+  a2 = eng::wave_sum(a2);
+  a3 = eng::wave_sum(a3);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = a0;
+    sh[1][w] = a1;
+    sh[2][w] = a2;
+    sh[3][w] = a3;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) s += sh[threadIdx.x][k];
+    if (wt) st_wt(&out[threadIdx.x * pstride + blockIdx.x], s);
+    else out[threadIdx.x * pstride + blockIdx.x] = s;
+  }
+}
+
+// CgState update from a fused pass's sums tot[4] (local; the all-reduce that follows makes them
+// global): the convergence / breakdown latch on the previous pass's GLOBAL r.r, a_prev, the new
+// sums, the iteration count.  cg_reduce_f1 mode 0 and the in-kernel reduction share this code.
+__device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int check, int first, double tol) {
+  auto zero = [&] {
+    for (int q = 0; q < 4; ++q) st->red[q] = 0.0;
+  };
+  if (st->done) { zero(); return; }
+  const double rr_prev = st->red[3];
+  if (check && sqrt(rr_prev) < tol) {
+    st->done = 1;
+    st->converged = 1;
+    st->conv_iter = st->iter - 1;
+    st->rr_final = rr_prev;
+    zero();
+    return;
+  }
+  if (check && !isfinite(rr_prev)) {
+    st->done = 3;
+    st->breakdown = 1;
+    st->conv_iter = st->iter - 1;
+    st->rr_final = rr_prev;
+    zero();
+    return;
+  }
+  // alpha of the pass whose (global) sums are being replaced — the pass after next pairs it
+  // into its x update; same division as f1_scalars so the bits agree
+  st->a_prev = first ? 0.0 : st->red[3] / st->red[0];
+  if (!first) {  // the clamp in f1_scalars, re-evaluated on the same global sums: count when it fired
+    const double a = st->red[3] / st->red[0];
+    const double est = fma(a * a, st->red[2], fma(-2.0 * a, st->red[1], st->red[3]));
+    if (!(est > 0.0)) st->clamps += 1;
+  }
+  for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
+  st->rr_new = tot[3];
+  st->iter += 1;
+}
+
+// In-kernel two-level last-arriver reduction (kernels.hpp RedCtl).  Runs in wave 0 after
+// block_partial4(wt = true): lanes 0-3 of that wave stored the block's partials write-through;
+// every hand-off is write-through stores -> s_waitcnt vmcnt(0) -> one relaxed agent-scope atomic
+// add, and the last arriver (told by the value its add returned) reads with write-through (sc1)
+// loads only (MI355X_MICROARCH.md, visibility: valid forms, first table row).
+__device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int g = (rc.base + (int)blockIdx.x) / kRedGroup;
+  const int g0 = g * kRedGroup - rc.base;  // the group's first slot, relative to `out`
+  const int gsize = min(kRedGroup, (int)gridDim.x - g0);
+  unsigned old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != (unsigned)(gsize - 1)) return;
+  if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = eng::wave_sum(v[q]);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st_wt(&rc.lvl2[q * rc.l2s + g], v[q]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[rc.top], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != (unsigned)(rc.ngroups - 1)) return;
+  if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[rc.top], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double t[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j = lane; j < rc.ngroups; j += 64) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] += ld_wt(&rc.lvl2[q * rc.l2s + j]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t[q] = eng::wave_sum(t[q]);
+  if (lane == 0) f1_bookkeep(st, t, rc.check, rc.first, tol);
+}
+
+// end of a fused pass: block partials, then (rc on) the in-kernel reduction
+__device__ __forceinline__ void f1_finish(double a0, double a1, double a2, double a3, double* __restrict__ out,
+                                          int pstride, const RedCtl& rc, CgState* st, double tol) {
+  block_partial4(a0, a1, a2, a3, out, pstride, rc.ngroups > 0);
+  if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
+}
+
+// non-temporal stores for the vectors the pass writes: they are re-read only by the next pass,
+// after ~GBs of other traffic, so caching them is useless (A/B on 16384^2: +1.5-2 %,
+// profiles/ab_nt_stores.log; -DMCG_NT_STORES=0 restores plain stores)
+#ifndef MCG_NT_STORES
+#define MCG_NT_STORES 1
+#endif
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+  if constexpr (MCG_NT_STORES) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void st_stream(double2* p, double2 v) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  if constexpr (MCG_NT_STORES) {
+    d2v w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<d2v*>(p));
+  } else {
+    *p = v;
+  }
+}
+

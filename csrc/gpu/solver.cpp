@@ -21,7 +21,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
     : spec_(spec), opt_(opt), rank_(rank), world_(world), comm_(comm) {
   MCG_CHECK(world >= 1 && rank >= 0 && rank < world, "invalid rank/world");
   MCG_CHECK(world == 1 || comm != nullptr, "multi-rank solver needs a communicator");
-  RowPartition part = partition_rows(spec_, world_);
+  RowPartition part = partition_rows(spec_, world_, opt_.halo_mode);
   L_ = make_layout(spec_, part, rank_);
   // column indices are int32 in every format (CSR cols, SELL cols / ext offsets, kernel gathers)
   MCG_CHECK(L_.ext_len < ((int64_t)1 << 31) - 64,
@@ -44,8 +44,9 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
   MCG_CHECK(opt_.graph_iters >= 2 && opt_.graph_iters % 2 == 0, "graph_iters must be even and >= 2");
   if (opt_.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
-  // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only
-  prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph;
+  // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only (and not for
+  // the split pass, whose ghosts come from its own update kernel; decided in setup())
+  prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph && !L_.allgather;
   s0_ = Stream(true, 0);
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);
@@ -64,8 +65,24 @@ GpuCgSolver::~GpuCgSolver() {
 }
 
 template <typename IdxT>
-void GpuCgSolver::build_csr_(DeviceBuffer<int64_t>& rp64) {
+void GpuCgSolver::build_csr_(DeviceBuffer<int64_t>& rp64, const HostCsr* user) {
   const int64_t n = L_.n_local();
+  if (user) {  // user matrix: upload this rank's rows (columns already in ext coordinates)
+    const size_t nnz = user->cols.size();
+    if (nnz) {
+      MCG_HIP(hipMemcpy(cols_.get(), user->cols.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(A)");
+      MCG_HIP(hipMemcpy(vals_.get(), user->vals.data(), nnz * sizeof(double), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(A)");
+    }
+    if constexpr (sizeof(IdxT) == 4) {
+      std::vector<int32_t> rp(user->rowptr.begin(), user->rowptr.end());
+      rp32_.allocate(n + 1, "A");
+      MCG_HIP(hipMemcpy(rp32_.get(), rp.data(), rp.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(A)");
+    }
+    return;
+  }
   if constexpr (sizeof(IdxT) == 4) {
     rp32_.allocate(n + 1, "A");
     kern::gen_fill<int32_t>(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), rp32_.get(), cols_.get(),
@@ -92,10 +109,20 @@ void GpuCgSolver::setup() {
   info_.interleave = opt_.interleave == 1;
 
   // ---- A: count -> scan -> fill (owned rows, ext-local columns) ----
+  // generated families on the device; a user matrix (kind Csr) from its host rows
   DeviceBuffer<int64_t> rp64(n + 1, "A");
-  kern::gen_rowlen(spec_, L_.row_begin, n, rp64.get(), s0_);
-  info_.max_row_len = kern::max_i64(rp64.get() + 1, n, s0_);  // row lengths, before the scan
-  {
+  HostCsr user;
+  const bool is_user = spec_.kind == ProblemKind::Csr;
+  if (is_user) {
+    user = build_local_csr(spec_, L_);
+    MCG_HIP(hipMemcpy(rp64.get(), user.rowptr.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice),
+            "memcpy from host to device failed(A)");
+    info_.max_row_len = 0;
+    for (int64_t i = 0; i < n; ++i)
+      info_.max_row_len = std::max<int64_t>(info_.max_row_len, user.rowptr[i + 1] - user.rowptr[i]);
+  } else {
+    kern::gen_rowlen(spec_, L_.row_begin, n, rp64.get(), s0_);
+    info_.max_row_len = kern::max_i64(rp64.get() + 1, n, s0_);  // row lengths, before the scan
     DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(n), "A");
     kern::scan_inclusive_i64(rp64.get() + 1, n, tmp.get(), s0_);
     MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
@@ -131,8 +158,23 @@ void GpuCgSolver::setup() {
     if (d16_) dcols_.allocate(total, "A", 16);
     else cols_.allocate(total, "A", 8);
     vals_.allocate(total, "A", 8);
-    kern::gen_fill_sell(spec_, L_.row_begin, n, L_.col_lo, L_.pad, L_.own_off, rp64.get(), slice_ptr_.get(),
-                        cols_.get(), dcols_.get(), vals_.get(), s0_);
+    if (is_user) {  // host rows -> device CSR (temporary) -> SELL-64(/d16)
+      DeviceBuffer<int32_t> tc(std::max<int64_t>(nnz, 1), "A");
+      DeviceBuffer<double> tv(std::max<int64_t>(nnz, 1), "A");
+      if (nnz) {
+        MCG_HIP(hipMemcpy(tc.get(), user.cols.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(A)");
+        MCG_HIP(hipMemcpy(tv.get(), user.vals.data(), nnz * sizeof(double), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(A)");
+      }
+      if (n > 0)
+        kern::csr_to_sell<int64_t>(rp64.get(), tc.get(), tv.get(), n, L_.own_off, slice_ptr_.get(),
+                                   d16_ ? nullptr : cols_.get(), vals_.get(), s0_, d16_ ? dcols_.get() : nullptr);
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    } else {
+      kern::gen_fill_sell(spec_, L_.row_begin, n, L_.col_lo, L_.pad, L_.own_off, rp64.get(), slice_ptr_.get(),
+                          cols_.get(), dcols_.get(), vals_.get(), s0_);
+    }
     matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
     if (c8_) {  // SELL-64/c8 when the (value, offset) dictionary fits one byte
       std::vector<double2> dict;
@@ -190,15 +232,33 @@ void GpuCgSolver::setup() {
   } else {
     cols_.allocate(nnz, "A", 8);
     vals_.allocate(nnz, "A", 8);
-    if (info_.idx64) build_csr_<int64_t>(rp64); else build_csr_<int32_t>(rp64);
+    if (info_.idx64) build_csr_<int64_t>(rp64, is_user ? &user : nullptr);
+    else build_csr_<int32_t>(rp64, is_user ? &user : nullptr);
     matrix_bytes = nnz * 12 + (n + 1) * (info_.idx64 ? 8 : 4);
     if (info_.idx64) rp64_ = std::move(rp64);
   }
 
+  // ---- iteration form for long / unstructured rows: the materialized-p split pass ----
+  pmat_ = opt_.recurrence == 1 && opt_.pmat != 0 &&
+          (opt_.pmat == 1 || (win_doubles_ == 0 && !c8_ && (L_.allgather || nnz >= 32 * n)));
+  if (pmat_) {
+    opt_.interleave = 0;
+    info_.interleave = false;
+    prefetch_halo_ = false;
+  }
+  info_.pmat = pmat_;
+  info_.allgather = L_.allgather;
+
   // ---- vectors ----
   b_.allocate(n, "b", 8);
   allocate_vectors_();
-  kern::gen_rhs(spec_, L_.row_begin, n, b_.get(), s0_);
+  if (is_user) {  // the user's b (or the spec's rhs kind), built on the host
+    const std::vector<double> hb = build_rhs(spec_, L_.row_begin, L_.row_end);
+    if (n) MCG_HIP(hipMemcpy(b_.get(), hb.data(), n * sizeof(double), hipMemcpyHostToDevice),
+                   "memcpy from host to device failed(b)");
+  } else {
+    kern::gen_rhs(spec_, L_.row_begin, n, b_.get(), s0_);
+  }
 
   // ---- launch geometry ----
   const int bpc = opt_.blocks_per_cu > 0 ? opt_.blocks_per_cu : (opt_.format == 1 ? 48 : 8);
@@ -351,6 +411,10 @@ void GpuCgSolver::setup() {
   // every second pass (paired x updates) = 12 per pass
   if (opt_.recurrence == 1) info_.bytes_per_iter_model = (double)matrix_bytes + 60.0 * n;
   if (opt_.recurrence == 1) info_.device_bytes += (size_t)(3 * L_.ext_len - n) * 8;
+  if (pmat_) {  // U: x rw, r rw, Ap r, p rw = 56 B; S: r, Ap 16 B + one pass over p (ideal gathers) 8 B
+    info_.bytes_per_iter_model = (double)matrix_bytes + 80.0 * n;
+    info_.device_bytes = matrix_bytes + (size_t)(4 * n + L_.ext_len) * 8 + rp64_.bytes();
+  }
   probe_placement_();
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
@@ -362,6 +426,13 @@ std::vector<DeviceBuffer<double>*> GpuCgSolver::vectors_() {
 
 void GpuCgSolver::allocate_vectors_() {
   const int64_t n = L_.n_local();
+  if (pmat_) {  // split pass: r, Ap, x owned only; p once in the ext layout (the only gathered vector)
+    x_.allocate(n, "x", 8);
+    r_.allocate(n, "r", 8);
+    Ap_.allocate(n, "Ap", 8);
+    p_[0].allocate(L_.ext_len, "p", 8);
+    return;
+  }
   // vec_skew: buffer i of the streams one pass reads / writes at the same row starts i * vec_skew
   // 256-B blocks past its allocation.  With the placement probe, every vector gets room for
   // leads up to kLeadCap (probe_placement_)
@@ -396,7 +467,7 @@ void GpuCgSolver::allocate_vectors_() {
 void GpuCgSolver::probe_placement_() {
   info_.placement_sets = 1;
   info_.placement_gain = 1.0;
-  if (opt_.placement_tries <= 1 || opt_.recurrence != 1) return;
+  if (opt_.placement_tries <= 1 || opt_.recurrence != 1 || pmat_) return;
   trace::Range tr_("mcg.placement");
   auto bufs = vectors_();
   size_t set_bytes = 0;
@@ -489,7 +560,11 @@ void GpuCgSolver::reset() {
   MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
   // r = b  (CUDACG.cu:248; x0 = 0 so r0 = b - A x0 = b, and p0 = r0 is formed by K_A at k = 0)
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s), "device memset failed");
-  if (opt_.interleave == 1) {
+  if (pmat_) {
+    // U_0 forms r_0 = b - 0 * Ap and p_0 = r_0 + 0 * p: r = b, Ap = 0, p = 0
+    MCG_HIP(hipMemcpyAsync(r_.get(), b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+            "vector copy failed(r)");
+  } else if (opt_.interleave == 1) {
     // iteration 0 reads the parity-1 pairs: {r_{-1}, Ap_{-1}} = {b, 0}
     kern::pack_pairs(b_.get(), reinterpret_cast<double2*>(ra_[1].get()) + L_.own_off, n, s);
   } else if (opt_.recurrence == 1) {
@@ -624,7 +699,72 @@ void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
   comm_->halo_exchange(L_, vecs, nv, s, w);
 }
 
+void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red) {
+  const int first = (k == 0) ? 1 : 0;
+  const int check = (k >= 2) ? 1 : 0;
+  const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
+  const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
+  double* part = partials_.get() + (which == 2 ? bnd_base_ : 0);
+  if (grid == 0) return;
+  kern::RedCtl rc;
+  if (fused_red) {
+    rc.cnt = red_cnt_.get();
+    rc.lvl2 = red_l2_.get();
+    rc.l2s = red_l2s_;
+    rc.top = red_l2s_;
+    rc.base = which == 2 ? bnd_base_ : 0;
+    rc.ngroups = which == 0 ? red_groups_all_ : red_groups_split_;
+    rc.check = check;
+    rc.first = first;
+  }
+  const int64_t n = L_.n_local();
+  const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : 1)) : (info_.spmv_variant == 2 ? 5 : 0);
+  const SellDev S = sell_view();
+  if (info_.idx64)
+    kern::cg_split_spmv<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S,
+                                 p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, part, pstride_, grid, st_.get(),
+                                 opt_.tol, first, check, s0_, rc);
+  else
+    kern::cg_split_spmv<int32_t>(fmt, info_.spmv_param, CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, S,
+                                 p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, part, pstride_, grid, st_.get(),
+                                 opt_.tol, first, check, s0_, rc);
+}
+
+void GpuCgSolver::enqueue_iteration_split_(int k) {
+  trace::Range tr_("mcg.iteration.split");
+  const int64_t n = L_.n_local();
+  const bool fr = fused_red_;
+  CgState* st = st_.get();
+  double* pv[1] = {p_[0].get()};
+  // U_k: x, r_k, p_k of the owned rows
+  kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, n, st, opt_.tol, k == 0 ? 1 : 0,
+                        k >= 2 ? 1 : 0, 0, partials_.get(), pstride_, g_b_, s0_);
+  int np = g_all_;
+  if (use_halo_ && opt_.overlap && !L_.allgather) {
+    MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+    MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+    comm_->halo_exchange(L_, pv, 1, s1_);
+    MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+    enqueue_split_spmv_(k, 1, fr);  // interior rows || ghosts of p_k on the side stream
+    MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+    enqueue_split_spmv_(k, 2, fr);
+    np = g_int_ + g_bnd_;
+  } else {
+    if (use_halo_) comm_->halo_exchange(L_, pv, 1, s0_);
+    // all-gather layout: no interior rows (g_int_ = 0), every row in the boundary launch
+    const bool split = use_halo_ && opt_.overlap;
+    enqueue_split_spmv_(k, split ? 2 : 0, fr);
+    if (split) np = g_int_ + g_bnd_;
+  }
+  if (!fr) kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
+  if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
+}
+
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
+  if (pmat_) {
+    enqueue_iteration_split_(k);
+    return;
+  }
   trace::Range tr_("mcg.iteration.single_reduction");
   int np = g_all_;
   const bool fr = fused_red_;
@@ -777,14 +917,23 @@ void GpuCgSolver::run_iterations(int count) {
 void GpuCgSolver::inject_fault_(int k) {
   static const double nan = std::numeric_limits<double>::quiet_NaN();
   if (L_.n_local() == 0 || rank_ != 0) return;
-  double* r = opt_.interleave == 1 ? ra_[(k + 1) & 1].get() + 2 * L_.own_off  // .x of the first owned pair
-               : ((opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get()) + L_.own_off;
+  double* r = pmat_ ? r_.get()
+              : opt_.interleave == 1 ? ra_[(k + 1) & 1].get() + 2 * L_.own_off  // .x of the first owned pair
+                                     : ((opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get()) + L_.own_off;
   MCG_HIP(hipMemcpyAsync(r, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
 }
 
 void GpuCgSolver::finalize() {
   if (k_ == 0 || finalized_) return;
   finalized_ = true;  // the single-reduction catch-up of a pending x term must run once
+  if (pmat_) {  // U in final mode: r_m, x_m and ||r_m||^2, then latch
+    kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, L_.n_local(), st_.get(), opt_.tol,
+                          0, k_ >= 2 ? 1 : 0, 1, partials_.get(), pstride_, g_b_, s0_);
+    kern::cg_reduce_f1(partials_.get(), pstride_, g_b_, st_.get(), 1, k_ >= 2 ? 1 : 0, 0, opt_.tol, s0_);
+    if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
+    kern::cg_reduce_f1(partials_.get(), pstride_, 0, st_.get(), 2, 0, 0, opt_.tol, s0_);
+    return;
+  }
   if (opt_.recurrence == 1) {
     // r_m = r_{m-1} - a Ap_{m-1}, x_m = x_{m-1} + a p_{m-1}, exact ||r_m||^2, then latch
     enqueue_f1_(k_, 0, 1);
@@ -940,6 +1089,44 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
   trace::Range tr_("mcg.phase_profile");
   synchronize();
   halo_ready_for_ = -1;
+  if (pmat_) {  // split pass: update | ghosts of p | SpMV (+ in-kernel reduce) | all-reduce, serialised
+    Event q[5];
+    for (Event& v : q) v = Event(true, true);
+    double acc[4] = {0, 0, 0, 0};
+    double* pv[1] = {p_[0].get()};
+    for (int it = 0; it < iters; ++it) {
+      const int k = k_;
+      MCG_HIP(hipEventRecord(q[0].get(), s0_), "event record failed");
+      kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, L_.n_local(), st_.get(),
+                            opt_.tol, k == 0 ? 1 : 0, k >= 2 ? 1 : 0, 0, partials_.get(), pstride_, g_b_, s0_);
+      MCG_HIP(hipEventRecord(q[1].get(), s0_), "event record failed");
+      if (use_halo_) comm_->halo_exchange(L_, pv, 1, s0_);
+      MCG_HIP(hipEventRecord(q[2].get(), s0_), "event record failed");
+      enqueue_split_spmv_(k, 0, fused_red_ && red_groups_all_ > 0);
+      if (!fused_red_)
+        kern::cg_reduce_f1(partials_.get(), pstride_, g_all_, st_.get(), 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol,
+                           s0_);
+      MCG_HIP(hipEventRecord(q[3].get(), s0_), "event record failed");
+      if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
+      MCG_HIP(hipEventRecord(q[4].get(), s0_), "event record failed");
+      synchronize();
+      for (int j = 0; j < 4; ++j) {
+        float t = 0.f;
+        MCG_HIP(hipEventElapsedTime(&t, q[j].get(), q[j + 1].get()), "event elapsed failed");
+        acc[j] += t;
+      }
+      ++k_;
+    }
+    const char* nm[4] = {"update", "halo", "spmv", "allreduce"};
+    std::vector<std::pair<std::string, double>> out;
+    double tot = 0;
+    for (int j = 0; j < 4; ++j) {
+      out.emplace_back(nm[j], iters > 0 ? 1e3 * acc[j] / iters : 0.0);
+      tot += acc[j];
+    }
+    out.emplace_back("iteration", iters > 0 ? 1e3 * tot / iters : 0.0);
+    return out;
+  }
   Event e[6], h[2];
   for (Event& v : e) v = Event(true, true);
   for (Event& v : h) v = Event(true, true);

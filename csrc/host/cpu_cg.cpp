@@ -134,7 +134,7 @@ CgResult cpu_cg_partitioned(const ProblemSpec& s, int world, const CgOptions& op
   using clk = std::chrono::steady_clock;
   CgResult res;
   const auto t0 = clk::now();
-  RowPartition part = partition_rows(s, world);
+  RowPartition part = partition_rows(s, world, opt.halo_mode);
   struct Rank {
     LocalLayout L;
     HostCsr A;

@@ -27,10 +27,13 @@ RowPartition partition_randspd(const ProblemSpec& s, int world) {
     return q[ga] * (double)((ga + 1) * R - a) + (qpre[gb] - qpre[ga + 1]) + q[gb] * (double)(b - gb * R);
   };
   std::vector<int64_t> prefix(nreg + 1, 0);
+  const double qmean = qpre[nreg] / (double)std::max<int64_t>(1, n);
   for (int64_t g = 0; g < nreg; ++g) {
     const int64_t r0 = g * R, r1 = std::min(n, r0 + R), mid = (r0 + r1) / 2;
-    // pairs {i-d, i} use the density of i-d's region; pairs {i, i+d} that of i's
-    const double left = qsum_rows(mid - W, mid), right = q[g] * (double)std::min(W, n - 1 - mid);
+    // pairs {i-d, i} use the density of i-d's region; pairs {i, i+d} that of i's (wide offsets:
+    // the lower partners are spread over the whole matrix -> the mean density)
+    const double left = s.spread > 0 ? qmean * (double)W : qsum_rows(mid - W, mid);
+    const double right = q[g] * (double)std::min(W, n - 1 - mid);
     prefix[g + 1] = prefix[g] + (int64_t)((double)(r1 - r0) * (1.0 + left + right));
   }
   RowPartition pr = partition_by_weight(prefix, world);
@@ -40,10 +43,27 @@ RowPartition partition_randspd(const ProblemSpec& s, int world) {
 }
 }  // namespace
 
-RowPartition partition_rows(const ProblemSpec& s, int world) {
+RowPartition partition_rows(const ProblemSpec& s, int world, int halo_mode) {
   MCG_CHECK(world >= 1, "invalid number of ranks");
+  MCG_CHECK(s.kind != ProblemKind::Csr || s.csr != nullptr, "csr problem without a matrix");
   const int64_t n = global_rows(s);
+  if (world > 1 && halo_mode != 0) {
+    const int64_t other = n - (n + world - 1) / world;  // rows of the other ranks (equal blocks)
+    if (halo_mode == 1 || 8 * bandwidth(s) >= 3 * other) {
+      RowPartition p;
+      p.allgather = true;
+      p.block = ((n + world - 1) / world + 63) / 64 * 64;  // whole 64-row SELL slices per block
+      p.offsets.resize(world + 1);
+      for (int r = 0; r <= world; ++r) p.offsets[r] = std::min(n, (int64_t)r * p.block);
+      return p;
+    }
+  }
   if (s.kind == ProblemKind::RandomSPD && world > 1 && n / 1024 >= world) return partition_randspd(s, world);
+  if (s.kind == ProblemKind::Csr && world > 1) {  // nnz + rows balanced
+    std::vector<int64_t> w(n + 1);
+    for (int64_t i = 0; i <= n; ++i) w[i] = s.csr->rowptr[i] + i;
+    return partition_by_weight(w, world);
+  }
   int64_t g = partition_granule(s);
   if (g < 1 || n / g < world) g = 1;
   const int64_t units = (n + g - 1) / g;
@@ -78,6 +98,17 @@ RowPartition partition_by_weight(const std::vector<int64_t>& row_prefix, int wor
 void column_window(const ProblemSpec& s, int64_t r0, int64_t r1, int64_t* lo, int64_t* hi) {
   const int64_t n = global_rows(s), bw = bandwidth(s);
   if (r1 <= r0) { *lo = r0; *hi = r0; return; }
+  if (s.kind == ProblemKind::Csr) {  // the actual columns of the rows
+    int64_t a = r0, b = r1 - 1;
+    const CsrMatrix& A = *s.csr;
+    for (int64_t k = A.rowptr[r0]; k < A.rowptr[r1]; ++k) {
+      a = std::min(a, A.cols[k]);
+      b = std::max(b, A.cols[k]);
+    }
+    *lo = a;
+    *hi = b + 1;
+    return;
+  }
   *lo = std::max<int64_t>(0, r0 - bw);
   *hi = std::min<int64_t>(n, r1 + bw);
 }
@@ -107,6 +138,25 @@ LocalLayout make_layout(const ProblemSpec& s, const RowPartition& part, int rank
   L.n_global = global_rows(s);
   L.row_begin = part.begin(rank);
   L.row_end = part.end(rank);
+  if (part.allgather) {
+    // ext = the whole vector in global order, P blocks of `block` rows (the last one padded):
+    // own_off = rank * block, so an in-place all-gather of `block` rows fills every ghost
+    L.allgather = true;
+    L.block = part.block;
+    L.col_lo = 0;
+    L.col_hi = (int64_t)P * part.block;
+    L.pad = 0;
+    L.own_off = (int64_t)rank * part.block;  // = row_begin unless the rank is empty (rows ran out)
+    L.ext_len = L.col_hi;
+    L.interior_begin = L.interior_end = 0;
+    if (P == 1) L.interior_end = L.n_local();
+    for (int q = 0; q < P; ++q) {
+      if (q == rank) continue;
+      if (part.end(q) > part.begin(q)) L.recvs.push_back({q, part.begin(q), part.end(q) - part.begin(q)});
+      if (L.n_local() > 0) L.sends.push_back({q, L.row_begin, L.n_local()});
+    }
+    return L;
+  }
   column_window(s, L.row_begin, L.row_end, &L.col_lo, &L.col_hi);
   if (L.row_end <= L.row_begin) { L.col_lo = L.col_hi = L.row_begin; }
   L.col_lo = std::min(L.col_lo, L.row_begin);

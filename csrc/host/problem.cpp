@@ -10,6 +10,7 @@ std::string problem_name(const ProblemSpec& s) {
     case ProblemKind::Poisson2D: return "poisson2d";
     case ProblemKind::Poisson3D: return "poisson3d";
     case ProblemKind::RandomSPD: return "randspd";
+    case ProblemKind::Csr: return "csr";
   }
   return "?";
 }

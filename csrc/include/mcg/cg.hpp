@@ -65,6 +65,11 @@ struct CgOptions {
   int vec_skew = 0;         // experiment: stagger the vector buffers' base addresses by i * vec_skew 256-B blocks
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
+  int halo_mode = -1;        // ghosts: 0 = column-window ranges (p2p send/recv), 1 = all-gather of equal row blocks
+                             // (unstructured sparsity), -1 = auto (partition_rows)
+  int pmat = -1;             // single-reduction form: materialized-p split pass (update kernel + SpMV gathering the
+                             // stored p only; cg_split.hip) — the irregular-sparsity path; -1 = auto (long rows
+                             // without an LDS window, or the all-gather layout), 0 = off, 1 = on
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

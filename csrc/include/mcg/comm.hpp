@@ -10,7 +10,9 @@
 //                   on device memory (CgState) — no host round trip
 //                 - halo comm: ncclSend/ncclRecv inside ncclGroupStart/End straight
 //                   from the owner's owned block into the receiver's ghost block
-//                   (LocalLayout plan: contiguous ranges, no packing)
+//                   (LocalLayout plan: contiguous ranges, no packing); for the
+//                   all-gather layout (unstructured sparsity) one in-place
+//                   ncclAllGather of equal row blocks per vector instead
 //                 Bootstrap needs only the two ncclUniqueIds on every rank (the
 //                 Python layer ships them over the torch.distributed store; the
 //                 native CLI shares them between its per-GPU threads).
@@ -73,9 +75,6 @@ class Comm final : public Communicator {
   void check_async() override;
   // ranks in the communicator as RCCL sees them (ncclCommCount)
   int count() const;
-  // generic device-buffer collectives used by gathers / tests
-  void allgather_bytes(const void* send, void* recv, size_t bytes_per_rank, hipStream_t stream);
-  void broadcast_bytes(void* buf, size_t bytes, int root, hipStream_t stream);
   void abort() override;
 
  private:

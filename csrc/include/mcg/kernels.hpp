@@ -235,6 +235,19 @@ void cg_fused1_win(int cm /* 0 SELL-64, 1 SELL-64/d16 */, int param, const SellD
                    int64_t own_off, const TileRanges& slices, const int32_t* win, int win_doubles, double* partials,
                    int pstride, int grid, CgState* st, double tol, int first, int check, int k,
                    hipStream_t stream, const RedCtl& rc = RedCtl());
+// ---- materialized-p single-reduction iteration (csrc/gpu/cg_split.hip) ----
+// The irregular-sparsity path: U (elementwise x / r / p_k update of the owned rows, same scalars
+// as cg_fused1) then S (SpMV gathering the stored p_k only + the 4 partials, in-kernel reduction).
+// final_mode U: r_m and x_m only + the r.r partials (then cg_reduce_f1 modes 1 / 2).
+void cg_split_update(double* x, double* r, const double* Ap, double* p_own, int64_t n, CgState* st, double tol,
+                     int first, int check, int final_mode, double* partials, int pstride, int grid,
+                     hipStream_t stream);
+// fmt: 0 CSR thread-per-row (param U), 5 CSR-vector (param G lanes per row), 1 SELL-64, 3 SELL-64/d16,
+// 4 SELL-64/c8
+template <typename IdxT>
+void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const double* p_ext, const double* r,
+                   double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
+                   CgState* st, double tol, int first, int check, hipStream_t stream, const RedCtl& rc = RedCtl());
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),

@@ -25,14 +25,22 @@ namespace mcg {
 
 struct RowPartition {
   std::vector<int64_t> offsets;  // size P+1, offsets[0] = 0, offsets[P] = n
+  // all-gather ghost layout: every rank owns `block` rows (the last one fewer) and the ghosts are
+  // every other rank's rows, refreshed by one ncclAllGather of equal blocks per vector
+  bool allgather = false;
+  int64_t block = 0;
   int world() const { return (int)offsets.size() - 1; }
   int64_t begin(int r) const { return offsets[r]; }
   int64_t end(int r) const { return offsets[r + 1]; }
 };
 
 // Equal-rows partition, aligned to the problem's partition granule (grid lines
-// for 2-D, planes for 3-D) whenever there are at least P granules.
-RowPartition partition_rows(const ProblemSpec& s, int world);
+// for 2-D, planes for 3-D) whenever there are at least P granules; nnz-balanced for
+// randspd and user CSR matrices.  halo_mode: 0 = column-window halo (contiguous
+// ghost ranges, point-to-point), 1 = all-gather of equal row blocks, -1 = auto: the
+// all-gather when a rank's column window covers >= 3/4 of the other ranks' rows
+// (unstructured sparsity: p2p ranges would move nearly the whole vector anyway).
+RowPartition partition_rows(const ProblemSpec& s, int world, int halo_mode = -1);
 // nnz-balanced partition from per-row lengths (prefix sums), used for irregular matrices.
 RowPartition partition_by_weight(const std::vector<int64_t>& row_prefix, int world);
 
@@ -52,6 +60,8 @@ struct LocalLayout {
   int64_t own_off = 0;                 // ext index of row_begin
   int64_t interior_begin = 0;          // local row range whose columns are all owned
   int64_t interior_end = 0;
+  bool allgather = false;  // ghosts = all other ranks' rows via all-gather (RowPartition::allgather)
+  int64_t block = 0;       // rows per rank block of the all-gather (own_off = rank * block)
   std::vector<HaloRange> sends;  // owned ranges other ranks need (ascending peer, row)
   std::vector<HaloRange> recvs;  // ghost ranges filled from other ranks (ascending peer, row)
 

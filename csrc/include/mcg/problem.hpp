@@ -17,6 +17,14 @@
 //              counter-based hash of the pair passes a density that varies per
 //              1024-row region; value -w(a,b), w in (0,1]; diagonal = row length
 //              (> sum |off-diagonal|).  BASELINE.json config 5.
+//              spread > 0 ("wide"): the W candidate offsets are not 1..W but W
+//              distinct offsets d_0 < ... < d_{W-1} drawn over [1, spread] (one per
+//              stratum of spread/W), so columns reach +-spread rows away — with
+//              spread ~ n the sparsity is unstructured at every scale (the all-gather
+//              ghost path), and each 64-row slice still reads 2W short runs of p.
+//   csr        a user matrix given as host CSR arrays (CsrMatrix view; Matrix
+//              Market files, SciPy matrices) — the reference's own input form
+//              (cusparseCreateCsr over rowptr/col/val, CUDACG.cu:93-117,213-216).
 #pragma once
 
 #include <cmath>
@@ -31,7 +39,19 @@
 
 namespace mcg {
 
-enum class ProblemKind : int { Demo = 0, Poisson2D = 1, Poisson3D = 2, RandomSPD = 3 };
+enum class ProblemKind : int { Demo = 0, Poisson2D = 1, Poisson3D = 2, RandomSPD = 3, Csr = 4 };
+
+// Host CSR of a user matrix (global rows, 0-based, int64 row pointers and columns).  A view:
+// the arrays are owned by the caller (HostMatrix, a NumPy array, ...).  Only host code reads
+// it: a rank uploads its rows; the device generators never see this kind.
+struct CsrMatrix {
+  int64_t n = 0;
+  const int64_t* rowptr = nullptr;  // n + 1
+  const int64_t* cols = nullptr;    // rowptr[n]
+  const double* vals = nullptr;
+  const double* b = nullptr;        // optional right-hand side (n); null: the spec's rhs kind
+  int64_t bw = 0;                   // max |i - j| over the stored entries
+};
 enum class RhsKind : int { Reference = 0, Random = 1, Ones = 2 };
 
 struct ProblemSpec {
@@ -42,6 +62,8 @@ struct ProblemSpec {
   double density = 0.5;    // randspd: mean probability that a candidate pair is present
   uint64_t seed = 1234;    // matrix + rhs seed
   RhsKind rhs = RhsKind::Reference;
+  int64_t spread = 0;      // randspd: > 0 = wide candidate offsets over [1, spread] (see above)
+  const CsrMatrix* csr = nullptr;  // kind Csr: the matrix (host)
 };
 
 // ---- counter-based hashing (SplitMix64 finaliser); identical on host/device ----
@@ -59,6 +81,7 @@ MCG_HD inline int64_t global_rows(const ProblemSpec& s) {
     case ProblemKind::Poisson2D: return s.N * s.N;
     case ProblemKind::Poisson3D: return s.N * s.N * s.N;
     case ProblemKind::RandomSPD: return s.rows;
+    case ProblemKind::Csr: return s.csr ? s.csr->n : 0;
   }
   return 0;
 }
@@ -70,7 +93,8 @@ MCG_HD inline int64_t bandwidth(const ProblemSpec& s) {
     case ProblemKind::Demo: return 2;
     case ProblemKind::Poisson2D: return s.N;
     case ProblemKind::Poisson3D: return s.N * s.N;
-    case ProblemKind::RandomSPD: return s.band;
+    case ProblemKind::RandomSPD: return s.spread > 0 ? s.spread : s.band;
+    case ProblemKind::Csr: return s.csr ? s.csr->bw : 0;
   }
   return 0;
 }
@@ -101,6 +125,13 @@ MCG_HD inline bool randspd_present(const ProblemSpec& s, int64_t a, int64_t b) {
 MCG_HD inline double randspd_weight(const ProblemSpec& s, int64_t a, int64_t b) {
   // (0,1]: reuse the low bits of the pair hash (independent of the presence test's high bits)
   return 1.0 - (double)(pair_hash(s, a, b) & 0xFFFFFull) * (1.0 / 1048576.0);
+}
+// candidate offset t (0 <= t < W), strictly increasing in t: 1..W (banded) or one offset per
+// stratum [t * step, (t + 1) * step) of [1, spread] (wide)
+MCG_HD inline int64_t randspd_offset(const ProblemSpec& s, int64_t t) {
+  if (s.spread <= 0) return t + 1;
+  const int64_t step = s.spread / s.band > 0 ? s.spread / s.band : 1;
+  return t * step + 1 + (int64_t)(mix64(s.seed * 0xD1B54A32D192ED03ull + (uint64_t)t) % (uint64_t)step);
 }
 
 // Visit the entries of global row i in ascending column order: f(col, val).
@@ -141,16 +172,29 @@ MCG_HD inline void for_each_entry(const ProblemSpec& s, int64_t i, F&& f, int64_
       const int64_t n = s.rows, W = s.band;
       if (rowlen < 0) {
         rowlen = 1;
-        for (int64_t d = 1; d <= W; ++d) {
+        for (int64_t t = 0; t < W; ++t) {
+          const int64_t d = randspd_offset(s, t);
           if (i - d >= 0 && randspd_present(s, i - d, i)) ++rowlen;
           if (i + d < n && randspd_present(s, i, i + d)) ++rowlen;
         }
       }
-      for (int64_t d = (W < i ? W : i); d >= 1; --d)
-        if (randspd_present(s, i - d, i)) f(i - d, -randspd_weight(s, i - d, i));
+      for (int64_t t = W - 1; t >= 0; --t) {
+        const int64_t d = randspd_offset(s, t);
+        if (d <= i && randspd_present(s, i - d, i)) f(i - d, -randspd_weight(s, i - d, i));
+      }
       f(i, (double)rowlen);
-      for (int64_t d = 1; d <= W && i + d < n; ++d)
+      for (int64_t t = 0; t < W; ++t) {
+        const int64_t d = randspd_offset(s, t);
+        if (i + d >= n) break;
         if (randspd_present(s, i, i + d)) f(i + d, -randspd_weight(s, i, i + d));
+      }
+      return;
+    }
+    case ProblemKind::Csr: {
+#if !defined(__HIP_DEVICE_COMPILE__)
+      const CsrMatrix& A = *s.csr;
+      for (int64_t k = A.rowptr[i]; k < A.rowptr[i + 1]; ++k) f(A.cols[k], A.vals[k]);
+#endif
       return;
     }
   }
@@ -171,11 +215,19 @@ MCG_HD inline int64_t row_length(const ProblemSpec& s, int64_t i) {
     case ProblemKind::RandomSPD: {
       int64_t len = 1;
       const int64_t n = s.rows, W = s.band;
-      for (int64_t d = 1; d <= W; ++d) {
+      for (int64_t t = 0; t < W; ++t) {
+        const int64_t d = randspd_offset(s, t);
         if (i - d >= 0 && randspd_present(s, i - d, i)) ++len;
         if (i + d < n && randspd_present(s, i, i + d)) ++len;
       }
       return len;
+    }
+    case ProblemKind::Csr: {
+#if !defined(__HIP_DEVICE_COMPILE__)
+      return s.csr->rowptr[i + 1] - s.csr->rowptr[i];
+#else
+      return 0;
+#endif
     }
   }
   return 0;
@@ -186,6 +238,9 @@ MCG_HD inline double rhs_value(const ProblemSpec& s, int64_t i) {
   switch (s.rhs) {
     case RhsKind::Reference: {
       if (s.kind == ProblemKind::Demo) return i == 0 ? 3.5 : (i == 1 ? 1.5 : 2.0);  // CUDACG.cu:138-140
+#if !defined(__HIP_DEVICE_COMPILE__)
+      if (s.kind == ProblemKind::Csr && s.csr && s.csr->b) return s.csr->b[i];  // the user's b
+#endif
       return 1.0;
     }
     case RhsKind::Random: return u01(mix64(s.seed ^ mix64((uint64_t)i + 0x51ED27ull)));
@@ -200,6 +255,7 @@ inline int64_t closed_form_nnz(const ProblemSpec& s) {
     case ProblemKind::Demo: return 5;
     case ProblemKind::Poisson2D: return 5 * s.N * s.N - 4 * s.N;
     case ProblemKind::Poisson3D: return 7 * s.N * s.N * s.N - 6 * s.N * s.N;
+    case ProblemKind::Csr: return s.csr ? s.csr->rowptr[s.csr->n] : 0;
     default: return -1;
   }
 }

@@ -52,6 +52,8 @@ struct SolverInfo {
   int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool fused_reduce = false;  // the pass reduces its own block partials (one kernel per iteration)
+  bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
+  bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
@@ -95,7 +97,7 @@ class GpuCgSolver {
   int iterations_enqueued() const { return k_; }
 
  private:
-  template <typename IdxT> void build_csr_(DeviceBuffer<int64_t>& rp64);
+  template <typename IdxT> void build_csr_(DeviceBuffer<int64_t>& rp64, const HostCsr* user);
   void enqueue_iteration_(int k);
   void enqueue_spmv_(int k, int which, int final_mode);  // which: 0 all, 1 interior, 2 boundary
   // single-reduction fused pass; `fused_red`: this launch takes part in the in-kernel reduction
@@ -103,6 +105,8 @@ class GpuCgSolver {
   void enqueue_halo_f1_(int k, hipStream_t s);            // ghosts iteration k of the single-reduction form reads
   void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
+  void enqueue_iteration_split_(int k);                   // materialized-p split pass (pmat_)
+  void enqueue_split_spmv_(int k, int which, bool fused_red);
   void capture_pair_(int kind);
   void inject_fault_(int k);
   std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
@@ -162,6 +166,7 @@ class GpuCgSolver {
   int pstride_ = 0;                // partial-array stride (4 arrays in the single-reduction form)
   int bnd_base_ = 0;               // first partial slot of the boundary launch (a multiple of kRedGroup)
   bool fused_red_ = false;         // in-kernel reduction of the fused pass (CgOptions::fused_reduce)
+  bool pmat_ = false;              // materialized-p split pass (CgOptions::pmat)
   int red_groups_all_ = 0, red_groups_split_ = 0, red_l2s_ = 0;
   DeviceBuffer<unsigned> red_cnt_;  // group counters + top counter (zeroed at setup, reset by the kernels)
   DeviceBuffer<double> red_l2_;     // [4][red_l2s_] group sums

@@ -17,6 +17,7 @@
 #include "mcg/comm.hpp"
 #include "mcg/kernels.hpp"
 #include "mcg/local_ranks.hpp"
+#include "mcg/matrix.hpp"
 #include "mcg/partition.hpp"
 #include "mcg/solver.hpp"
 
@@ -26,7 +27,7 @@ using namespace mcg;
 namespace {
 
 ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64_t band, double density,
-                      uint64_t seed, const std::string& rhs) {
+                      uint64_t seed, const std::string& rhs, int64_t spread) {
   ProblemSpec s;
   s.kind = parse_problem_kind(problem);
   s.N = n;
@@ -35,6 +36,7 @@ ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64
   s.density = density;
   s.seed = seed;
   s.rhs = parse_rhs_kind(rhs);
+  s.spread = spread;
   if (s.kind == ProblemKind::Demo) s.N = 3;
   return s;
 }
@@ -92,6 +94,8 @@ py::dict layout_dict(const LocalLayout& L) {
   d["own_off"] = L.own_off;
   d["interior_begin"] = L.interior_begin;
   d["interior_end"] = L.interior_end;
+  d["allgather"] = L.allgather;
+  d["block"] = L.block;
   py::list sends, recvs;
   for (auto& h : L.sends) sends.append(py::make_tuple(h.peer, h.gbegin, h.count));
   for (auto& h : L.recvs) recvs.append(py::make_tuple(h.peer, h.gbegin, h.count));
@@ -126,7 +130,8 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<ProblemSpec>(m, "ProblemSpec")
       .def(py::init(&make_spec), py::arg("problem") = "demo", py::arg("n") = 3, py::arg("rows") = 0,
-           py::arg("band") = 0, py::arg("density") = 0.5, py::arg("seed") = 1234, py::arg("rhs") = "reference")
+           py::arg("band") = 0, py::arg("density") = 0.5, py::arg("seed") = 1234, py::arg("rhs") = "reference",
+           py::arg("spread") = 0)
       .def_property_readonly("name", [](const ProblemSpec& s) { return problem_name(s); })
       .def_property_readonly("n_rows", [](const ProblemSpec& s) { return global_rows(s); })
       .def_property_readonly("bandwidth", [](const ProblemSpec& s) { return bandwidth(s); })
@@ -136,6 +141,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("band", &ProblemSpec::band)
       .def_readonly("density", &ProblemSpec::density)
       .def_readonly("seed", &ProblemSpec::seed)
+      .def_readonly("spread", &ProblemSpec::spread)
       .def("row_length", [](const ProblemSpec& s, int64_t i) { return row_length(s, i); })
       .def("rhs_value", [](const ProblemSpec& s, int64_t i) { return rhs_value(s, i); })
       .def("row", [](const ProblemSpec& s, int64_t i) {
@@ -143,6 +149,41 @@ PYBIND11_MODULE(_C, m) {
         for_each_entry(s, i, [&](int64_t c, double v) { cols.append(c); vals.append(v); });
         return py::make_tuple(cols, vals);
       });
+
+  // ---- user matrices (kind csr) ----
+  py::class_<HostMatrix, std::shared_ptr<HostMatrix>>(m, "HostMatrix")
+      .def(py::init([](py::array_t<int64_t, py::array::c_style | py::array::forcecast> indptr,
+                       py::array_t<int64_t, py::array::c_style | py::array::forcecast> indices,
+                       py::array_t<double, py::array::c_style | py::array::forcecast> data, py::object b) {
+             std::vector<int64_t> rp(indptr.data(), indptr.data() + indptr.size());
+             std::vector<int64_t> ci(indices.data(), indices.data() + indices.size());
+             std::vector<double> v(data.data(), data.data() + data.size());
+             std::vector<double> bv;
+             if (!b.is_none()) {
+               auto ba = py::array_t<double, py::array::c_style | py::array::forcecast>::ensure(b);
+               if (!ba) throw py::value_error("b must be a float64 vector");
+               bv.assign(ba.data(), ba.data() + ba.size());
+             }
+             const int64_t n = (int64_t)rp.size() - 1;
+             py::gil_scoped_release rel;
+             return std::make_shared<HostMatrix>(n, std::move(rp), std::move(ci), std::move(v), std::move(bv));
+           }),
+           py::arg("indptr"), py::arg("indices"), py::arg("data"), py::arg("b") = py::none(),
+           "0-based CSR (int64 row pointers / columns, float64 values), optional right-hand side b")
+      .def_static("read_mtx", [](const std::string& path) {
+        py::gil_scoped_release rel;
+        return std::shared_ptr<HostMatrix>(read_matrix_market(path));
+      }, "Matrix Market coordinate file (general / symmetric / skew-symmetric; real / integer / pattern)")
+      .def_property_readonly("n", &HostMatrix::n)
+      .def_property_readonly("nnz", &HostMatrix::nnz)
+      .def_property_readonly("bandwidth", [](const HostMatrix& a) { return a.view().bw; })
+      .def_property_readonly("has_rhs", [](const HostMatrix& a) { return !a.rhs().empty(); })
+      .def("symmetric", &HostMatrix::symmetric_pattern_and_values)
+      .def("spec", [](const HostMatrix& a, const std::string& rhs, uint64_t seed) {
+        return a.spec(parse_rhs_kind(rhs), seed);
+      }, py::arg("rhs") = "reference", py::arg("seed") = 1234, py::keep_alive<0, 1>(),
+         "ProblemSpec of kind csr over this matrix (the spec keeps the matrix alive)");
+  m.def("read_vector", &read_vector, "dense vector: Matrix Market array file or one value per line");
 
   py::class_<CgOptions>(m, "CgOptions")
       .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
@@ -165,6 +206,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry_nt", &CgOptions::carry_nt)
       .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("fused_reduce", &CgOptions::fused_reduce)
+      .def_readwrite("halo_mode", &CgOptions::halo_mode)
+      .def_readwrite("pmat", &CgOptions::pmat)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -190,13 +233,15 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("blocks_per_cu", &CgOptions::blocks_per_cu);
 
   // ---- partition / halo plan / host CSR ----
-  m.def("partition_rows", [](const ProblemSpec& s, int world) { return partition_rows(s, world).offsets; });
+  m.def("partition_rows", [](const ProblemSpec& s, int world, int halo_mode) {
+    return partition_rows(s, world, halo_mode).offsets;
+  }, py::arg("spec"), py::arg("world"), py::arg("halo_mode") = -1);
   m.def("partition_by_weight", [](const std::vector<int64_t>& prefix, int world) {
     return partition_by_weight(prefix, world).offsets;
   });
-  m.def("make_layout", [](const ProblemSpec& s, int world, int rank) {
-    return layout_dict(make_layout(s, partition_rows(s, world), rank));
-  });
+  m.def("make_layout", [](const ProblemSpec& s, int world, int rank, int halo_mode) {
+    return layout_dict(make_layout(s, partition_rows(s, world, halo_mode), rank));
+  }, py::arg("spec"), py::arg("world"), py::arg("rank"), py::arg("halo_mode") = -1);
   m.def("host_csr", [](const ProblemSpec& s, int world, int rank) {
     LocalLayout L = make_layout(s, partition_rows(s, world), rank);
     HostCsr A = build_local_csr(s, L);
@@ -260,7 +305,7 @@ PYBIND11_MODULE(_C, m) {
              return new GpuCgSolver(s, o, rank, world, comm.get());
            }),
            py::arg("spec"), py::arg("opts"), py::arg("rank") = 0, py::arg("world") = 1,
-           py::arg("comm") = nullptr, py::keep_alive<1, 6>())
+           py::arg("comm") = nullptr, py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
       .def("setup", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.setup(); })
       .def("reset", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.reset(); })
       .def("solve", [](GpuCgSolver& g, bool resume) {
@@ -311,6 +356,8 @@ PYBIND11_MODULE(_C, m) {
         d["strip"] = i.strip;
         d["carry"] = i.carry;
         d["fused_reduce"] = i.fused_reduce;
+        d["pmat"] = i.pmat;
+        d["allgather"] = i.allgather;
         d["graph_fallbacks"] = i.graph_fallbacks;
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;

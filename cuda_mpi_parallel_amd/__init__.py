@@ -18,7 +18,7 @@ Package layout::
     parallel/  partition / halo plans, RCCL bootstrap over torch.distributed,
                multi-process CPU reference (gloo)
     solver/    high-level CG drivers (GPU native solver, CPU reference)
-    utils/     timing, reporting, environment helpers
+    utils/     output helpers (reference x format, JSON result lines)
 
 ``torch`` is imported before the native extension on purpose: torch ships its own
 ``libamdhip64.so.7`` / ``librccl.so.1``; loading it first makes the extension bind
@@ -67,5 +67,5 @@ def cli_path() -> str:
 
 
 from . import models, ops, parallel, solver, utils  # noqa: E402,F401
-from .models import ProblemSpec, make_problem  # noqa: E402,F401
+from .models import CsrProblem, ProblemSpec, csr_problem, make_problem  # noqa: E402,F401
 from .solver import CGSolver, solve  # noqa: E402,F401

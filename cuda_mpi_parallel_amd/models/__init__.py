@@ -11,7 +11,10 @@ name           matrix                                       reference / config
 ``demo``       the reference's 3x3 indefinite system        CUDACG.cu:74-117,136-141
 ``poisson2d``  5-pt Dirichlet Laplacian, n = N^2            BASELINE.json configs 1-3
 ``poisson3d``  7-pt Dirichlet Laplacian, n = N^3            BASELINE.json config 4
-``randspd``    banded, irregular, strictly diag. dominant   BASELINE.json config 5
+``randspd``    banded / wide (spread), irregular, strictly  BASELINE.json config 5
+               diagonally dominant
+``csr``        a user matrix: SciPy / NumPy CSR arrays or a  CUDACG.cu:93-117,213-216
+               Matrix Market file (:func:`csr_problem`)       (the reference's input)
 =============  ===========================================  ==========================
 """
 from __future__ import annotations
@@ -23,7 +26,7 @@ import numpy as np
 
 from .. import native
 
-PROBLEMS = ("demo", "poisson2d", "poisson3d", "randspd")
+PROBLEMS = ("demo", "poisson2d", "poisson3d", "randspd", "csr")
 
 
 @dataclass(frozen=True)
@@ -37,9 +40,11 @@ class ProblemSpec:
     density: float = 0.5  # randspd mean pair density
     seed: int = 1234
     rhs: str = "reference"  # reference | random | ones
+    spread: int = 0       # randspd: > 0 = the band candidate offsets drawn over [1, spread] ("wide")
 
     def native(self):
-        return native().ProblemSpec(self.problem, self.n, self.rows, self.band, self.density, self.seed, self.rhs)
+        return native().ProblemSpec(self.problem, self.n, self.rows, self.band, self.density, self.seed, self.rhs,
+                                    self.spread)
 
     @property
     def n_rows(self) -> int:
@@ -58,12 +63,89 @@ class ProblemSpec:
         return int(nnz / ranks * 12 + per_rank_rows * ((8 if idx64 else 4) + 6 * 8))
 
 
-def make_problem(name: str = "demo", **kw) -> ProblemSpec:
+class CsrProblem:
+    """A user matrix (kind ``csr``): the same interface as :class:`ProblemSpec`.
+
+    The native ``HostMatrix`` owns the arrays; every rank reads the whole matrix on the host and
+    uploads only its own rows (partition and ghost plan from the actual columns).  ``rhs``:
+    ``"reference"`` = the given ``b`` (ones when none is given), ``"ones"``, ``"random"``.
+    ``reorder="rcm"`` applies a reverse Cuthill-McKee permutation (SciPy) first, which turns
+    most mesh matrices into banded ones (column-window halos instead of the all-gather);
+    :meth:`unpermute` maps a solution back to the original numbering.
+    """
+
+    problem = "csr"
+
+    def __init__(self, matrix, rhs: str = "reference", seed: int = 1234, perm: Optional[np.ndarray] = None):
+        self.matrix = matrix
+        self.rhs = rhs
+        self.seed = seed
+        self.perm = perm
+        self._spec = matrix.spec(rhs, seed)
+
+    def native(self):
+        return self._spec
+
+    @property
+    def n_rows(self) -> int:
+        return int(self.matrix.n)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.matrix.nnz)
+
+    def unpermute(self, x: np.ndarray) -> np.ndarray:
+        """Solution of the permuted system -> original row order."""
+        if self.perm is None:
+            return np.asarray(x)
+        out = np.empty_like(np.asarray(x))
+        out[self.perm] = x
+        return out
+
+
+def csr_problem(a, b=None, rhs: str = "reference", seed: int = 1234, reorder: Optional[str] = None) -> CsrProblem:
+    """A :class:`CsrProblem` from a SciPy sparse matrix, an ``(indptr, indices, data)`` triple or
+    a Matrix Market path (``.mtx``)."""
+    perm = None
+    if isinstance(a, str):
+        if reorder is None and b is None:
+            return CsrProblem(native().HostMatrix.read_mtx(a), rhs, seed)
+        import scipy.io
+
+        a = scipy.io.mmread(a)
+    if isinstance(a, tuple):
+        indptr, indices, data = a
+    else:
+        import scipy.sparse as sp
+
+        m = sp.csr_matrix(a)
+        if m.shape[0] != m.shape[1]:
+            raise ValueError("matrix must be square")
+        if reorder == "rcm":
+            from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+            perm = np.asarray(reverse_cuthill_mckee(m, symmetric_mode=True), dtype=np.int64)
+            m = m[perm][:, perm].tocsr()
+            if b is not None:
+                b = np.asarray(b, dtype=np.float64)[perm]
+        elif reorder is not None:
+            raise ValueError(f"unknown reorder {reorder!r}")
+        m.sort_indices()
+        indptr, indices, data = m.indptr, m.indices, m.data
+    H = native().HostMatrix(np.asarray(indptr, dtype=np.int64), np.asarray(indices, dtype=np.int64),
+                            np.asarray(data, dtype=np.float64), None if b is None else np.asarray(b, np.float64))
+    return CsrProblem(H, rhs, seed, perm)
+
+
+def make_problem(name: str = "demo", **kw):
     """``make_problem("poisson2d", n=4096)``; non-demo problems default to a random RHS
-    (BASELINE.json:5 "random RHS"); randspd defaults to rows=100000, band=64."""
-    name = {"random-spd": "randspd", "random": "randspd"}.get(name, name)
+    (BASELINE.json:5 "random RHS"); randspd defaults to rows=100000, band=64;
+    ``make_problem("csr", matrix=A_or_path, b=None)`` wraps a user matrix."""
+    name = {"random-spd": "randspd", "random": "randspd", "mtx": "csr"}.get(name, name)
     if name not in PROBLEMS:
         raise ValueError(f"unknown problem {name!r}; choose from {PROBLEMS}")
+    if name == "csr":
+        return csr_problem(kw.pop("matrix"), **kw)
     if name != "demo":
         kw.setdefault("rhs", "random")
     if name == "randspd":
@@ -96,4 +178,4 @@ def rhs(spec: ProblemSpec, r0: int = 0, r1: Optional[int] = None) -> np.ndarray:
     return native().host_rhs(spec.native(), r0, r1)
 
 
-__all__ = ["PROBLEMS", "ProblemSpec", "make_problem", "host_csr", "to_scipy", "rhs"]
+__all__ = ["PROBLEMS", "ProblemSpec", "CsrProblem", "csr_problem", "make_problem", "host_csr", "to_scipy", "rhs"]

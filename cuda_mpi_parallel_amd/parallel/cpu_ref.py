@@ -48,6 +48,13 @@ def cpu_cg_distributed(spec, maxit: int = 2000, tol: float = 1e-7, group=None) -
     def halo(v_ext: np.ndarray) -> None:
         if world == 1:
             return
+        if L.allgather:  # the RCCL path's ncclAllGather of equal blocks, on gloo
+            blk = torch.from_numpy(np.ascontiguousarray(v_ext[L.own_off:L.own_off + L.block]))
+            parts = [torch.empty(L.block, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, blk, group=group)
+            for q, t in enumerate(parts):
+                v_ext[q * L.block:(q + 1) * L.block] = t.numpy()
+            return
         reqs = []
         bufs = []
         for peer, g0, cnt in L.sends:

@@ -28,6 +28,8 @@ class Layout:
     own_off: int
     interior_begin: int
     interior_end: int
+    allgather: bool  # ghosts = every other rank's block, refreshed by one all-gather (own_off = rank * block)
+    block: int
     sends: Tuple[Tuple[int, int, int], ...]
     recvs: Tuple[Tuple[int, int, int], ...]
 
@@ -39,14 +41,14 @@ class Layout:
         return g - self.col_lo + self.pad
 
 
-def partition_rows(spec, world: int) -> List[int]:
+def partition_rows(spec, world: int, halo_mode: int = -1) -> List[int]:
     ns = spec.native() if hasattr(spec, "native") else spec
-    return list(native().partition_rows(ns, world))
+    return list(native().partition_rows(ns, world, halo_mode))
 
 
-def layout(spec, world: int, rank: int) -> Layout:
+def layout(spec, world: int, rank: int, halo_mode: int = -1) -> Layout:
     ns = spec.native() if hasattr(spec, "native") else spec
-    d = native().make_layout(ns, world, rank)
+    d = native().make_layout(ns, world, rank, halo_mode)
     d["sends"] = tuple(tuple(x) for x in d["sends"])
     d["recvs"] = tuple(tuple(x) for x in d["recvs"])
     return Layout(**d)

@@ -1,0 +1,105 @@
+"""GPU irregular-sparsity path (BASELINE.json config 5): the materialized-p split pass
+(csrc/gpu/cg_split.hip) and the all-gather ghost layout, on one GPU and as P in-process ranks
+(LocalComm; the RCCL all-gather itself runs in tests/test_gpu_rccl.py when >= 2 GPUs are visible).
+
+Anchor: the reference's generic CSR SpMV (CUDACG.cu:213-216, 288) must handle any sparsity.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+WIDE = dict(rows=20000, band=24, density=0.5, spread=20000)
+
+
+def _cpu(mcg, spec, maxit=2000, tol=1e-7):
+    C = mcg.native()
+    return C.cpu_cg(spec.native(), C.CgOptions(maxit=maxit, tol=tol))
+
+
+@pytest.mark.parametrize("fmt", ["csr", "sell", "sell16"])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("randspd", dict(rows=20000, band=40, density=0.25)),
+                                         ("randspd", WIDE)])
+def test_split_pass_matches_cpu(mcg, fmt, problem, kw):
+    spec = mcg.make_problem(problem, **kw)
+    cpu = _cpu(mcg, spec)
+    s = mcg.CGSolver(spec, format=fmt, recurrence=1, pmat=1, check_every=8)
+    assert s.info["pmat"]
+    out = s.solve()
+    assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    assert out["converged"] == cpu["converged"]
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    assert s.true_residual_norm() < 1e-6
+
+
+def test_split_pass_auto_for_wide_rows_and_same_recurrence_as_fused(mcg):
+    spec = mcg.make_problem("randspd", rows=20000, band=64, density=0.5, spread=20000)
+    a = mcg.CGSolver(spec, format="sell", recurrence=1, check_every=8)
+    assert a.info["pmat"]  # >= 32 nonzeros per row and no LDS window: the split pass
+    b = mcg.CGSolver(spec, format="sell", recurrence=1, pmat=0, check_every=8)
+    assert not b.info["pmat"]
+    ra, rb = a.solve(), b.solve()
+    assert abs(ra["iterations"] - rb["iterations"]) <= 1  # same scalars, different sum blocking
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("fused", [-1, 0])
+def test_split_pass_graph_equals_eager_bitwise(mcg, fused):
+    spec = mcg.make_problem("randspd", **WIDE)
+    outs = [mcg.CGSolver(spec, format="sell", recurrence=1, pmat=1, use_graph=g, fused_reduce=fused,
+                         check_every=8).solve() for g in (True, False)]
+    assert outs[0]["iterations"] == outs[1]["iterations"] and outs[0]["rnorm"] == outs[1]["rnorm"]
+    np.testing.assert_array_equal(outs[0]["x_local"], outs[1]["x_local"])
+
+
+def test_split_pass_fixed_iterations_track_fused(mcg):
+    spec = mcg.make_problem("poisson2d", n=256, rhs="random")
+    r = []
+    for pm in (1, 0):
+        s = mcg.CGSolver(spec, format="sell", recurrence=1, pmat=pm, tol=-1.0, maxit=300)
+        r.append(s.solve())
+    assert r[0]["iterations"] == r[1]["iterations"] == 300
+    assert abs(r[0]["rnorm"] - r[1]["rnorm"]) <= 1e-10 * r[1]["rnorm"]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_local_ranks_all_gather_layout(mcg, world):
+    """P ranks on the wide matrix: all-gather layout + split pass, every rank latched together,
+    x equal to the CPU oracle (a reduced-rows rehearsal of config 5)."""
+    spec = mcg.make_problem("randspd", **WIDE)
+    C = mcg.native()
+    cpu = _cpu(mcg, spec)
+    o = C.CgOptions(format="sell", recurrence=1, check_every=4)
+    out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    its = {r["iterations"] for r in out["ranks"]}
+    assert len(its) == 1
+    assert abs(its.pop() - cpu["iterations"]) <= 1
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
+
+
+def test_local_ranks_p8_agrees_with_p1_fixed_iterations(mcg):
+    """Config-5 rehearsal: 8 ranks vs 1 over 200 fixed iterations on the wide matrix."""
+    spec = mcg.make_problem("randspd", rows=40000, band=48, density=0.5, spread=40000)
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sell", recurrence=1)
+    one = C.run_local_ranks(spec.native(), o, 1, 200, True)
+    eight = C.run_local_ranks(spec.native(), o, 8, 200, True)
+    r1, r8 = one["ranks"][0]["rnorm"], eight["ranks"][0]["rnorm"]
+    assert abs(r1 - r8) <= 1e-12 * r1
+    np.testing.assert_allclose(eight["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_local_ranks_split_pass_window_halo(mcg, world, overlap):
+    """The split pass on a stencil with the column-window halo (p only), interior || halo."""
+    spec = mcg.make_problem("poisson2d", n=64)
+    C = mcg.native()
+    cpu = _cpu(mcg, spec)
+    o = C.CgOptions(format="sell16", recurrence=1, overlap=overlap, check_every=4)
+    o.pmat = 1
+    out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    its = {r["iterations"] for r in out["ranks"]}
+    assert len(its) == 1 and abs(its.pop() - cpu["iterations"]) <= 2
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
