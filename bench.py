@@ -51,6 +51,8 @@ def parse_args(argv=None):
     ap.add_argument("--rows", type=int, default=100_000_000, help="randspd: global rows")
     ap.add_argument("--band", type=int, default=4096, help="randspd: half bandwidth")
     ap.add_argument("--density", type=float, default=0.16, help="randspd: candidate-pair density")
+    ap.add_argument("--spread", type=int, default=0,
+                    help="randspd: > 0 = candidate offsets over [1, spread] (unstructured; the all-gather path)")
     ap.add_argument("--format", default="sellc8", choices=["csr", "sell", "sell16", "sellc8"],
                     help="sparse storage: CSR, SELL-64, SELL-64/d16 (16-bit column offsets) or SELL-64/c8 "
                          "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
@@ -119,7 +121,8 @@ def _run_rank(args, out_fd) -> int:
     comm = pdist.bootstrap_comm(env, force=args.force_comm)
 
     if args.problem == "randspd":
-        spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, rhs="random")
+        spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, spread=args.spread,
+                                rhs="random")
     else:
         spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
     C = mcg.native()
@@ -197,8 +200,8 @@ def _run_rank(args, out_fd) -> int:
             t = torch.tensor([phases[k] for k in keys], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             extra["phase_us_max"] = {k: round(float(v), 2) for k, v in zip(keys, t.tolist())}
-    model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" if args.problem == "randspd"
-             else f"{args.problem}_N{args.grid}")
+    model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" + (f"_spread{args.spread}" if args.spread else "")
+             if args.problem == "randspd" else f"{args.problem}_N{args.grid}")
     if env.rank == 0:
         line = json.dumps({
             "metric": METRIC if headline else "CG iterations/sec (whole node), %s" % model,
@@ -213,7 +216,8 @@ def _run_rank(args, out_fd) -> int:
             "vs_baseline": round(value / BASELINE_IT_PER_S, 4) if headline else None,
             "dtype": "fp64",
             "data": "synthetic (on-device generated %s matrix, random RHS)" % {
-                "poisson2d": "5-pt Poisson", "poisson3d": "7-pt Poisson", "randspd": "random SPD banded"}[args.problem],
+                "poisson2d": "5-pt Poisson", "poisson3d": "7-pt Poisson",
+                "randspd": "random SPD " + ("wide/unstructured" if args.spread else "banded")}[args.problem],
             "config": {
                 "model": model,
                 "problem": args.problem,
@@ -226,7 +230,10 @@ def _run_rank(args, out_fd) -> int:
                 # storage the timed pass streams: the 2-D line-carry pass reads 4-bit codes (c4)
                 "format": "sell64-c4" if info.get("codes4") else info["format"],
                 "recurrence": info["recurrence"],
-                "pass": "line-carry" if info.get("carry") else ("generic, xcd-aware" if info.get("xcd_map") else "generic"),
+                "pass": ("line-carry" if info.get("carry") else "split (materialized p)" if info.get("pmat")
+                         else "windowed" if info.get("window") else "generic, xcd-aware" if info.get("xcd_map")
+                         else "generic"),
+                "ghosts": "allgather" if info.get("allgather") else "window",
                 "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,
@@ -238,7 +245,8 @@ def _run_rank(args, out_fd) -> int:
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
                       "placement_lead_trial": info.get("placement_lead_trial"),"model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
-                      "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3), **extra},
+                      "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3),
+                      "device_gb_rank0": round(info["device_bytes"] / 1e9, 2), **extra},
         })
         sys.stdout.flush()
         os.write(out_fd, (line + "\n").encode())

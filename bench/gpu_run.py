@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""One recipe runner for every GPU-box command of this repo (replaces the per-experiment shell
+launchers).  Run on the box:
+
+  gpurun -- 'python bench/gpu_run.py check'            # GPU tests + smoke + headline bench
+  gpurun -- 'python bench/gpu_run.py prof --grid 4096' # rocprofv3 kernel trace + summary
+  python bench/gpu_run.py --list                       # recipes and their steps
+
+Every step runs under its own ``timeout -k 10 <s>``, writes stdout/stderr to
+``gpurun_out/<recipe>_<step>.{out,err}``, and the recipe stops at the first failing step (a GPU
+fault, an abort or a time limit ends the call: no step runs after it).  Counter passes hold at
+most one PMC group per rocprofv3 run (the limits of MI355X_MICROARCH.md: 8 SQ, 4 TCC).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shlex
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PY = sys.executable
+PYTEST = f"{PY} -u -m pytest -x -q --timeout 300 --timeout-method thread"
+PROF = "rocprofv3"
+
+
+def bench(extra: str = "") -> str:
+    return f"{PY} bench.py {extra}".strip()
+
+
+def prof(tag: str, cmd: str, pmc: str = "") -> str:
+    """rocprofv3 around `cmd` (the program itself right after --, never a wrapper)."""
+    what = f"--pmc {pmc}" if pmc else "--kernel-trace --stats"
+    return f"{PROF} {what} -d {OUT}/{tag} -o run -- {cmd}"
+
+
+def recipes(a) -> dict:
+    g = a.grid
+    return {
+        # round-end style check: what the driver runs, in one call
+        "check": [
+            ("pytest_gpu", 900, f"{PYTEST} tests -m gpu"),
+            ("smoke", 300, f"{PY} -c 'import __graft_entry__ as g; g.smoke()'"),
+            ("bench", 200, bench()),
+            ("bench_spawn", 200, bench("--gpus 1 --spawn")),
+            ("bench_3d", 200, bench("--problem poisson3d --grid 512")),
+        ],
+        "tests": [("pytest_gpu", 900, f"{PYTEST} tests -m gpu")],
+        "bench": [
+            ("smoke", 300, f"{PY} -c 'import __graft_entry__ as g; g.smoke()'"),
+            ("bench", 200, bench()),
+            ("bench_spawn", 200, bench("--gpus 1 --spawn")),
+            ("bench_3d", 200, bench("--problem poisson3d --grid 512")),
+            ("bench_4096", 200, bench("--grid 4096 --steps 2000 --warmup 100")),
+        ],
+        # BASELINE.json configs on one GPU (config 5 at its per-GPU share: 12.5 M rows, ~150 GB)
+        "configs": [
+            ("c1_cpu_1024", 900, f"bin/mcg-cg --device cpu --problem poisson2d --n 1024 --fixed-iters 200 "
+                                 f"--report json"),
+            ("c2_4096", 200, bench("--grid 4096 --steps 2000 --warmup 100")),
+            ("c3_16384", 200, bench()),
+            ("c4_512", 200, bench("--problem poisson3d --grid 512")),
+            ("c5_randspd", 600, bench("--problem randspd --rows 12500000 --band 650 --density 1.0 "
+                                      "--spread 12500000 --steps 10 --warmup 2 --phases 3")),
+        ],
+        # variants of the current tree on the same box: every number of the README table
+        "variants": [
+            ("generic_c8", 200, bench("--set carry=0")),
+            ("sell16", 200, bench("--format sell16")),
+            ("csr_two", 200, bench("--format csr --recurrence 0")),
+            ("csr_single", 200, bench("--format csr --recurrence 1")),
+            ("no_fused_reduce", 200, bench("--set fused_reduce=0")),
+            ("force_comm", 200, bench("--force-comm")),
+        ],
+        # kernel trace + per-iteration kernel count / gaps of one grid
+        "prof": [
+            ("trace", 300, prof(f"prof{g}", f"{PY} {ROOT}/bench.py --grid {g} --steps 64 --warmup 8 --phases 0 "
+                                            f"--force-comm")),
+            ("summary", 60, f"{PY} bench/trace_summary.py {OUT}/prof{g}/run_results.db --iters 48"),
+        ],
+        # counter passes (one group per run) of the headline pass
+        "pmc": [
+            ("bytes", 90, prof("pmc_bytes", f"{PY} {ROOT}/bench.py --grid {g} --steps 4 --warmup 2 --phases 0 "
+                                             f"--no-verify", "TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum "
+                                                             "GRBM_GUI_ACTIVE")),
+            ("waves", 90, prof("pmc_waves", f"{PY} {ROOT}/bench.py --grid {g} --steps 4 --warmup 2 --phases 0 "
+                                             f"--no-verify", "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY "
+                                                             "SQ_ACTIVE_INST_ANY SQ_WAVES")),
+        ],
+        # irregular-sparsity path (config 5): split pass, wide matrix, user matrices
+        "irregular": [
+            ("pytest", 900, f"{PYTEST} -v tests/test_gpu_irregular.py tests/test_gpu_user_matrix.py "
+                            f"tests/test_gpu_rccl.py tests/test_gpu_fused_reduce.py"),
+            ("rand200", 600, bench("--problem randspd --rows 12500000 --band 650 --density 1.0 --spread 12500000 "
+                                   "--steps 10 --warmup 2 --phases 3")),
+            ("rand30", 300, bench("--problem randspd --rows 12500000 --band 100 --density 1.0 --spread 12500000 "
+                                  "--steps 20 --warmup 2")),
+            ("rand30_fused", 300, bench("--problem randspd --rows 12500000 --band 100 --density 1.0 "
+                                        "--spread 12500000 --steps 20 --warmup 2 --set pmat=0")),
+            ("prof_rand30", 400, prof("prof_rand30", f"{PY} {ROOT}/bench.py --problem randspd --rows 12500000 "
+                                                     f"--band 100 --density 1.0 --spread 12500000 --steps 10 "
+                                                     f"--warmup 2 --phases 0")),
+        ],
+        # the distributed path at headline sizes as P in-process ranks on one GPU
+        "rehearse": [("ranks", 900, f"{PY} bench/rehearse_ranks.py")],
+    }
+
+
+def run(name: str, steps, dry: bool) -> int:
+    os.makedirs(OUT, exist_ok=True)
+    env = dict(os.environ, TMPDIR="/tmp", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for step, limit, cmd in steps:
+        full = f"timeout -k 10 {limit} {cmd}"
+        print(f"[gpu_run] {name}/{step}: {full}", flush=True)
+        if dry:
+            continue
+        t0 = time.time()
+        base = os.path.join(OUT, f"{name}_{step}")
+        with open(base + ".out", "w") as fo, open(base + ".err", "w") as fe:
+            proc = subprocess.Popen(shlex.split(full), cwd=ROOT, env=env, stdout=fo, stderr=fe)
+            beat = time.time()
+            while proc.poll() is None:  # heartbeat: a silent step must not look hung to the pool
+                time.sleep(1.0)
+                if time.time() - beat >= 60:
+                    beat = time.time()
+                    print(f"[gpu_run] {name}/{step}: running {beat - t0:.0f}s", flush=True)
+            rc = proc.returncode
+        print(f"[gpu_run] {name}/{step}: rc={rc} {time.time() - t0:.1f}s", flush=True)
+        if rc != 0:
+            with open(base + ".err") as fe:
+                sys.stdout.write(fe.read()[-3000:])
+            with open(base + ".out") as fo:
+                sys.stdout.write(fo.read()[-3000:])
+            return rc
+        with open(base + ".out") as fo:
+            tail = fo.read().strip().splitlines()[-3:]
+        for line in tail:
+            print("   " + line[:400])
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("recipe", nargs="*", help="recipe names (in order)")
+    ap.add_argument("--grid", type=int, default=4096, help="grid edge for prof / pmc")
+    ap.add_argument("--list", action="store_true")
+    ap.add_argument("--dry-run", action="store_true")
+    a = ap.parse_args(argv)
+    R = recipes(a)
+    if a.list or not a.recipe:
+        for k, steps in R.items():
+            print(k + ": " + ", ".join(s for s, _, _ in steps))
+        return 0
+    for name in a.recipe:
+        if name not in R:
+            print(f"unknown recipe {name!r}", file=sys.stderr)
+            return 2
+        rc = run(name, R[name], a.dry_run)
+        if rc != 0:
+            return rc
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -185,14 +186,22 @@ class Barrier {
   explicit Barrier(int n) : n_(n) {}
   void wait() {
     std::unique_lock<std::mutex> lk(m_);
+    if (failed_) fail("another rank failed");
     const int gen = gen_;
     if (++count_ == n_) { count_ = 0; ++gen_; cv_.notify_all(); return; }
-    cv_.wait(lk, [&] { return gen != gen_; });
+    cv_.wait(lk, [&] { return gen != gen_ || failed_; });
+    if (gen == gen_) fail("another rank failed");
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m_);
+    failed_ = true;
+    cv_.notify_all();
   }
  private:
   std::mutex m_;
   std::condition_variable cv_;
   int n_, count_ = 0, gen_ = 0;
+  bool failed_ = false;
 };
 
 struct RankOut {
@@ -205,6 +214,29 @@ struct RankOut {
   std::string error, detail;
 };
 
+// Communicators of the ranks of this process: a rank that fails aborts them all, so the others
+// leave their collectives with an error instead of waiting for it forever.
+struct CommRegistry {
+  std::mutex m;
+  std::vector<Comm*> comms;
+  bool failed = false;
+  void add(Comm* c) {
+    std::lock_guard<std::mutex> lk(m);
+    comms.push_back(c);
+    if (failed) c->abort();
+  }
+  void remove(Comm* c) {
+    std::lock_guard<std::mutex> lk(m);
+    comms.erase(std::remove(comms.begin(), comms.end(), c), comms.end());
+  }
+  void abort_all() {
+    std::lock_guard<std::mutex> lk(m);
+    failed = true;
+    for (Comm* c : comms) c->abort();
+  }
+};
+CommRegistry g_comms;
+
 void run_rank(const Args& a, int rank, int world, const std::string& id_red, const std::string& id_halo,
               Barrier& bar, bool want_x, RankOut& out) {
   try {
@@ -212,6 +244,19 @@ void run_rank(const Args& a, int rank, int world, const std::string& id_red, con
     std::unique_ptr<Comm> comm;
     if (world > 1 || a.opt.force_comm)
       comm.reset(new Comm(rank, world, unique_id_from_bytes(id_red), unique_id_from_bytes(id_halo)));
+    if (comm) g_comms.add(comm.get());
+    struct Unreg {
+      Comm* c;
+      ~Unreg() {
+        if (c) g_comms.remove(c);
+      }
+    } unreg{comm.get()};
+    struct AbortOnThrow {  // runs during unwinding, before `comm` is destroyed
+      bool armed = true;
+      ~AbortOnThrow() {
+        if (armed && std::uncaught_exceptions() > 0) g_comms.abort_all();
+      }
+    } guard;
     CgOptions opt = a.opt;
     if (a.fixed_iters > 0) { opt.tol = -1.0; opt.maxit = a.fixed_iters; }
     GpuCgSolver solver(a.spec, opt, rank, world, comm.get());
@@ -245,6 +290,7 @@ void run_rank(const Args& a, int rank, int world, const std::string& id_red, con
   } catch (const std::exception& e) {
     out.error = e.what();
   }
+  if (!out.error.empty()) bar.abort();
 }
 
 }  // namespace

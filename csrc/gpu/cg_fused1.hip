@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <mutex>
 #include <type_traits>
 
 #include "mcg/check.hpp"
@@ -826,10 +827,18 @@ void chunk_windows(const SellDev& S, int32_t* win, hipStream_t stream) {
   MCG_HIP(hipGetLastError(), "kernel launch failed(chunk_windows)");
 }
 
-// raise the dynamic-LDS limit of every windowed instantiation (setup time, not per launch)
+// raise the dynamic-LDS limit of every windowed instantiation (setup time, not per launch).  The
+// attribute is per function and process-wide: solvers of several ranks in one process (LocalComm
+// threads) prepare different widths, so the limit only ever grows (a rank must never lower it
+// under another rank's launch).
 void cg_fused1_win_prepare(int win_doubles) {
   const int lds = win_doubles * (int)sizeof(double);
   MCG_CHECK((size_t)lds <= kWinMaxLds, "window exceeds the LDS budget");
+  static std::mutex mu;
+  static int prepared = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (lds <= prepared) return;
+  prepared = lds;
   const void* fns[] = {
       reinterpret_cast<const void*>(&k_cg_f1_win<0, 4, false>), reinterpret_cast<const void*>(&k_cg_f1_win<0, 6, false>),
       reinterpret_cast<const void*>(&k_cg_f1_win<0, 8, false>), reinterpret_cast<const void*>(&k_cg_f1_win<0, 4, true>),

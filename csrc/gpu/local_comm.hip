@@ -55,6 +55,7 @@ LocalGroup::~LocalGroup() {
 
 void LocalGroup::barrier() {
   std::unique_lock<std::mutex> lk(m_);
+  if (failed_) fail("another local rank failed");
   const int gen = gen_;
   if (++count_ == world_) {
     count_ = 0;
@@ -62,7 +63,14 @@ void LocalGroup::barrier() {
     cv_.notify_all();
     return;
   }
-  cv_.wait(lk, [&] { return gen != gen_; });
+  cv_.wait(lk, [&] { return gen != gen_ || failed_; });
+  if (gen == gen_) fail("another local rank failed");
+}
+
+void LocalGroup::abort() {
+  std::lock_guard<std::mutex> lk(m_);
+  failed_ = true;
+  cv_.notify_all();
 }
 
 LocalComm::LocalComm(std::shared_ptr<LocalGroup> group, int rank) : group_(std::move(group)), rank_(rank) {

@@ -74,15 +74,20 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         if (verify) o.true_rnorm = s.true_residual_norm();
       } catch (const Error& e) {
         o.error = std::string(e.what()) + ": " + e.detail();
+        group->abort();
       } catch (const std::exception& e) {
         o.error = e.what();
+        group->abort();
       }
       if (!passed) setup_barrier(true);
     });
   }
   for (auto& t : ts) t.join();
+  std::string first;
   for (auto& o : out.ranks)
-    if (!o.error.empty()) fail("local rank failed", o.error);
+    if (!o.error.empty() && (first.empty() || first.find("another local rank failed") != std::string::npos))
+      first = o.error;
+  if (!first.empty()) fail("local rank failed", first);
   return out;
 }
 

@@ -241,6 +241,9 @@ void GpuCgSolver::setup() {
   // ---- iteration form for long / unstructured rows: the materialized-p split pass ----
   pmat_ = opt_.recurrence == 1 && opt_.pmat != 0 &&
           (opt_.pmat == 1 || (win_doubles_ == 0 && !c8_ && (L_.allgather || nnz >= 32 * n)));
+  // the pass form decides which ghost vectors are exchanged ({r, Ap} + p, or p alone): every rank
+  // must take the same one, whatever its own rows look like
+  if (use_comm_ && world_ > 1) pmat_ = all_ranks_agree_(pmat_);
   if (pmat_) {
     opt_.interleave = 0;
     info_.interleave = false;
@@ -418,6 +421,18 @@ void GpuCgSolver::setup() {
   probe_placement_();
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
+}
+
+// true iff `mine` is true on every rank (one all-reduce of a flag at setup; not in the loop)
+bool GpuCgSolver::all_ranks_agree_(bool mine) {
+  DeviceBuffer<double> f(1, "state");
+  const double v = mine ? 1.0 : 0.0;
+  MCG_HIP(hipMemcpyAsync(f.get(), &v, sizeof(double), hipMemcpyHostToDevice, s0_), "memcpy from host to device failed");
+  comm_->allreduce_sum(f.get(), 1, s0_);
+  double all = 0.0;
+  MCG_HIP(hipMemcpyAsync(&all, f.get(), sizeof(double), hipMemcpyDeviceToHost, s0_), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
+  return all == (double)world_;
 }
 
 std::vector<DeviceBuffer<double>*> GpuCgSolver::vectors_() {

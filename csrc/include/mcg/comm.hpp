@@ -90,10 +90,14 @@ class LocalGroup {
   explicit LocalGroup(int world, size_t max_allreduce = 64);
   ~LocalGroup();
   int world() const { return world_; }
+  // a rank failed: every rank waiting at (or later reaching) a barrier throws instead of waiting
+  // for it forever (RCCL's ncclCommAbort, for threads)
+  void abort();
 
  private:
   friend class LocalComm;
   void barrier();
+  bool failed_ = false;
   int world_;
   size_t max_n_;
   double* staging_ = nullptr;  // [2 parities][world][max_n]

@@ -111,7 +111,8 @@ class GpuCgSolver {
   void inject_fault_(int k);
   std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
   void allocate_vectors_();
-  void probe_placement_();  // keep the fastest of several placements of the vectors (CgOptions::placement_*)
+  void probe_placement_();
+  bool all_ranks_agree_(bool mine);  // setup-time agreement across ranks (one all-reduce)  // keep the fastest of several placements of the vectors (CgOptions::placement_*)
   static constexpr size_t kLeadCap = (4u << 20) / sizeof(double);  // room for vector start offsets (4 MiB)
 
   ProblemSpec spec_;

@@ -79,14 +79,15 @@ def test_local_ranks_all_gather_layout(mcg, world):
 
 
 def test_local_ranks_p8_agrees_with_p1_fixed_iterations(mcg):
-    """Config-5 rehearsal: 8 ranks vs 1 over 200 fixed iterations on the wide matrix."""
+    """Config-5 rehearsal: 8 ranks vs 1 over 12 fixed iterations on the wide matrix (strictly
+    diagonally dominant: ~0.45x residual per iteration, so 12 keep the residual far above rounding)."""
     spec = mcg.make_problem("randspd", rows=40000, band=48, density=0.5, spread=40000)
     C = mcg.native()
     o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sell", recurrence=1)
-    one = C.run_local_ranks(spec.native(), o, 1, 200, True)
-    eight = C.run_local_ranks(spec.native(), o, 8, 200, True)
+    one = C.run_local_ranks(spec.native(), o, 1, 12, True)
+    eight = C.run_local_ranks(spec.native(), o, 8, 12, True)
     r1, r8 = one["ranks"][0]["rnorm"], eight["ranks"][0]["rnorm"]
-    assert abs(r1 - r8) <= 1e-12 * r1
+    assert abs(r1 - r8) <= 1e-11 * r1
     np.testing.assert_allclose(eight["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
 
 
