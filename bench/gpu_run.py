@@ -105,7 +105,12 @@ def recipes(a) -> dict:
                                                      f"--warmup 2 --phases 0")),
         ],
         # the distributed path at headline sizes as P in-process ranks on one GPU
-        "rehearse": [("ranks", 900, f"{PY} bench/rehearse_ranks.py")],
+        "rehearse": [
+            ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),
+            ("r512", 600, f"{PY} bench/rehearse_ranks.py --problem poisson3d --n 512 --iters 20 --world 1 2 4 8 "
+                          f"--phases 10"),
+            ("rwide", 600, f"{PY} bench/rehearse_ranks.py --problem randspd --iters 20 --world 1 2 4 8 --phases 10"),
+        ],
     }
 
 

@@ -23,22 +23,37 @@ def main():
     ap.add_argument("--problem", default="poisson2d")
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--world", type=int, nargs="+", default=[1, 2, 8])
+    ap.add_argument("--grid", type=int, default=None, help="alias of --n")
+    ap.add_argument("--rows", type=int, default=2_000_000, help="randspd rows")
+    ap.add_argument("--band", type=int, default=100, help="randspd candidate offsets per side")
+    ap.add_argument("--density", type=float, default=1.0)
+    ap.add_argument("--spread", type=int, default=-1, help="randspd spread (-1 = rows: unstructured)")
+    ap.add_argument("--phases", type=int, default=0,
+                    help="> 0: per-rank phase timing (interior || halo, boundary wait) over that many iterations")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     C = mcg.native()
-    spec = mcg.make_problem(args.problem, n=args.n)
+    if args.problem == "randspd":
+        spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density,
+                                spread=args.rows if args.spread < 0 else args.spread)
+    else:
+        spec = mcg.make_problem(args.problem, n=args.grid or args.n)
     ref = None
     for w in args.world:
         o = C.CgOptions(maxit=1 << 30, tol=-1.0, format="sellc8", recurrence=1, check_every=1 << 30)
-        out = C.run_local_ranks(spec.native(), o, w, args.iters, True)
+        out = C.run_local_ranks(spec.native(), o, w, args.iters, True, args.phases)
         r = out["ranks"]
         rn = r[0]["rnorm"]
         tr = max(x["true_rnorm"] for x in r)
-        ok = all(x["iterations"] == args.iters for x in r) and abs(tr - rn) <= 1e-6 * max(tr, 1e-300)
+        ok = all(x["iterations"] == args.iters + args.phases for x in r) and abs(tr - rn) <= 1e-6 * max(tr, 1e-300)
         if ref is None:
             ref = rn
-        print(json.dumps({"world": w, "iterations": r[0]["iterations"], "rnorm": rn, "true_rnorm": tr,
-                          "rel_vs_first": abs(rn - ref) / ref, "ok": ok}), flush=True)
+        line = {"world": w, "iterations": r[0]["iterations"], "rnorm": rn, "true_rnorm": tr,
+                "rel_vs_first": abs(rn - ref) / ref, "ok": ok}
+        if args.phases:  # worst rank per phase (the ranks share one GPU: relative sizes, not speed)
+            keys = sorted(r[0]["phases"])
+            line["phase_us_max"] = {k: round(max(x["phases"][k] for x in r), 2) for k in keys}
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -20,7 +20,7 @@
 namespace mcg {
 
 LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, int world, int fixed_iters,
-                               bool verify) {
+                               bool verify, int phase_iters) {
   MCG_CHECK(world >= 1, "invalid number of local ranks");
   int dev = 0;
   MCG_HIP(hipGetDevice(&dev), "Device Set failed");
@@ -63,6 +63,7 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         if (fixed_iters > 0) {
           s.reset();
           s.run_iterations(fixed_iters);
+          if (phase_iters > 0) o.phases = s.phase_profile(phase_iters);
           s.finalize();
           o.res = s.result();
         } else {

@@ -15,6 +15,7 @@ struct LocalRankResult {
   int64_t row_begin = 0;
   double true_rnorm = -1.0;
   bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)
+  std::vector<std::pair<std::string, double>> phases;  // phase_profile (mean us) when asked for
   std::string error;
 };
 
@@ -23,9 +24,10 @@ struct LocalRunResult {
 };
 
 // fixed_iters > 0: run exactly that many iterations (+ finalise) instead of solving to tol.
-// Note: an exception on one rank while others wait at a LocalComm barrier would hang;
-// errors here are setup-time (allocation) errors, raised before any collective.
+// A rank that throws aborts the LocalGroup: the others leave their barriers with an error.
+// phase_iters > 0 (single-reduction form): afterwards, that many more iterations with hipEvents at
+// every phase boundary on every rank (GpuCgSolver::phase_profile): the overlap rehearsal.
 LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, int world, int fixed_iters = 0,
-                               bool verify = false);
+                               bool verify = false, int phase_iters = 0);
 
 }  // namespace mcg

@@ -376,11 +376,12 @@ PYBIND11_MODULE(_C, m) {
         return d;
       });
 
-  m.def("run_local_ranks", [](const ProblemSpec& s, const CgOptions& o, int world, int fixed_iters, bool verify) {
+  m.def("run_local_ranks", [](const ProblemSpec& s, const CgOptions& o, int world, int fixed_iters, bool verify,
+                              int phase_iters) {
     LocalRunResult lr;
     {
       py::gil_scoped_release rel;
-      lr = run_local_ranks(s, o, world, fixed_iters, verify);
+      lr = run_local_ranks(s, o, world, fixed_iters, verify, phase_iters);
     }
     py::list ranks;
     std::vector<double> x;
@@ -389,6 +390,9 @@ PYBIND11_MODULE(_C, m) {
       d["row_begin"] = rr.row_begin;
       d["true_rnorm"] = rr.true_rnorm;
       d["carry"] = rr.carry;
+      py::dict ph;
+      for (auto& kv : rr.phases) ph[py::str(kv.first)] = kv.second;
+      d["phases"] = ph;
       ranks.append(d);
       x.insert(x.end(), rr.x.begin(), rr.x.end());
     }
@@ -397,6 +401,7 @@ PYBIND11_MODULE(_C, m) {
     out["x"] = to_numpy(std::move(x));
     return out;
   }, py::arg("spec"), py::arg("opts"), py::arg("world"), py::arg("fixed_iters") = 0, py::arg("verify") = false,
+     py::arg("phase_iters") = 0,
      "P ranks as threads on the current device with the in-process LocalComm (multi-rank test harness)");
 
   // ---- raw-pointer kernel entry points (ops API) ----
