@@ -418,6 +418,8 @@ void GpuCgSolver::setup() {
     info_.bytes_per_iter_model = (double)matrix_bytes + 80.0 * n;
     info_.device_bytes = matrix_bytes + (size_t)(4 * n + L_.ext_len) * 8 + rp64_.bytes();
   }
+  // vectors allocated with room for the placement probe's start offsets hold that headroom too
+  for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->lead_capacity() * sizeof(double);
   probe_placement_();
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
@@ -487,7 +489,9 @@ void GpuCgSolver::probe_placement_() {
   auto bufs = vectors_();
   size_t set_bytes = 0;
   for (auto* b : bufs) set_bytes += b->bytes();
-  const int leads = std::max(1, opt_.placement_leads);
+  // start-offset trials re-lead every buffer, which would discard a vec_skew experiment's offsets:
+  // with vec_skew only whole allocations are compared
+  const int leads = opt_.vec_skew > 0 ? 1 : std::max(1, opt_.placement_leads);
   // start offset (doubles) of buffer i in lead trial t: trial 0 all zero, then pseudo-random
   // multiples of 4 KiB (0..7) + 1 MiB (0..3)
   auto lead_of = [&](int t, size_t i) -> size_t {
@@ -554,6 +558,9 @@ void GpuCgSolver::probe_placement_() {
     }
     held.push_back(std::move(prev));
   }
+  info_.placement_peak_bytes = 0;
+  for (auto& set : held)
+    for (auto& b : set) info_.placement_peak_bytes += b.bytes() + b.lead_capacity() * sizeof(double);
   held.clear();
   info_.placement_best_ms = best;
   info_.placement_lead_trial = best_t;

@@ -62,6 +62,7 @@ struct SolverInfo {
   double placement_gain = 1.0;  // slowest / fastest of the timed placements (the fastest is kept)
   double placement_best_ms = 0.0, placement_worst_ms = 0.0;  // two even/odd pass pairs
   int placement_lead_trial = 0;  // start-offset trial kept (0 = allocation starts)
+  size_t placement_peak_bytes = 0;  // extra device bytes held while the probe compared vector sets
 };
 
 class GpuCgSolver {

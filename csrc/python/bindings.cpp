@@ -366,6 +366,7 @@ PYBIND11_MODULE(_C, m) {
         d["placement_gain"] = i.placement_gain;
         d["placement_best_ms"] = i.placement_best_ms;
         d["placement_lead_trial"] = i.placement_lead_trial;
+        d["placement_peak_bytes"] = i.placement_peak_bytes;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
