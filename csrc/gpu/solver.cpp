@@ -15,7 +15,57 @@ namespace mcg {
 
 namespace {
 constexpr int kCsrBlocksPerCuCap = 6;  // LDS-limited residency of the CSR tile kernel (26.7 KB/block)
+
+// stored SELL-64 slots of rows taken in the order `order` (slice = 64 consecutive slots)
+int64_t sell_slots(const HostCsr& A, const std::vector<int32_t>* order) {
+  const int64_t n = A.n_rows;
+  int64_t total = 0;
+  for (int64_t s0 = 0; s0 < n; s0 += 64) {
+    int64_t w = 0;
+    for (int64_t i = s0; i < std::min(n, s0 + 64); ++i) {
+      const int64_t r = order ? (*order)[i] : i;
+      w = std::max<int64_t>(w, A.rowptr[r + 1] - A.rowptr[r]);
+    }
+    total += 64 * w;
+  }
+  return total;
 }
+
+// SELL-C-sigma: rows sorted by length (descending, stable) inside windows of `sigma` rows that
+// never cross a cut (the interior / boundary slice ranges must keep their rows), so each 64-row
+// slice holds rows of similar length.  Rewrites A in slot order; perm[slot] = local row.
+bool sigma_sort(HostCsr& A, int64_t sigma, std::vector<int64_t> cuts, bool force, std::vector<int32_t>& perm) {
+  const int64_t n = A.n_rows;
+  std::vector<int32_t> order(n);
+  for (int64_t i = 0; i < n; ++i) order[i] = (int32_t)i;
+  cuts.push_back(0);
+  cuts.push_back(n);
+  std::sort(cuts.begin(), cuts.end());
+  for (size_t c = 0; c + 1 < cuts.size(); ++c)
+    for (int64_t a = cuts[c]; a < cuts[c + 1]; a += sigma) {
+      const int64_t b = std::min(cuts[c + 1], a + sigma);
+      std::stable_sort(order.begin() + a, order.begin() + b, [&](int32_t x, int32_t y) {
+        return A.rowptr[x + 1] - A.rowptr[x] > A.rowptr[y + 1] - A.rowptr[y];
+      });
+    }
+  const int64_t before = sell_slots(A, nullptr), after = sell_slots(A, &order);
+  if (!force && (double)after > 0.9 * (double)before) return false;
+  HostCsr P;
+  P.n_rows = n;
+  P.rowptr.assign(n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) P.rowptr[i + 1] = P.rowptr[i] + (A.rowptr[order[i] + 1] - A.rowptr[order[i]]);
+  P.cols.resize(A.cols.size());
+  P.vals.resize(A.vals.size());
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = order[i];
+    std::copy(A.cols.begin() + A.rowptr[r], A.cols.begin() + A.rowptr[r + 1], P.cols.begin() + P.rowptr[i]);
+    std::copy(A.vals.begin() + A.rowptr[r], A.vals.begin() + A.rowptr[r + 1], P.vals.begin() + P.rowptr[i]);
+  }
+  A = std::move(P);
+  perm = std::move(order);
+  return true;
+}
+}  // namespace
 
 GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank, int world, Communicator* comm)
     : spec_(spec), opt_(opt), rank_(rank), world_(world), comm_(comm) {
@@ -115,6 +165,25 @@ void GpuCgSolver::setup() {
   const bool is_user = spec_.kind == ProblemKind::Csr;
   if (is_user) {
     user = build_local_csr(spec_, L_);
+    if (opt_.format == 1 && opt_.sell_sigma != 0 && n > 64) {
+      // SELL-C-sigma (int32 columns): the windows never mix interior and boundary slices
+      const int64_t sig = opt_.sell_sigma > 1 ? (opt_.sell_sigma + 63) / 64 * 64 : 4096;
+      std::vector<int64_t> cuts;
+      if (use_halo_ && opt_.overlap && !L_.allgather) {
+        cuts.push_back(std::min<int64_t>(n, (L_.interior_begin + 63) / 64 * 64));
+        cuts.push_back(std::max<int64_t>(0, L_.interior_end / 64 * 64));
+      }
+      std::vector<int32_t> perm;
+      if (sigma_sort(user, sig, cuts, opt_.sell_sigma > 0, perm)) {
+        perm_.allocate(n, "A");
+        MCG_HIP(hipMemcpy(perm_.get(), perm.data(), n * sizeof(int32_t), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(A)");
+        info_.sigma = (int)sig;
+        d16_ = false;  // offsets are relative to the slot's row: plain int32 columns with a permutation
+        c8_ = false;
+        info_.format = 1;
+      }
+    }
     MCG_HIP(hipMemcpy(rp64.get(), user.rowptr.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice),
             "memcpy from host to device failed(A)");
     info_.max_row_len = 0;
@@ -207,7 +276,8 @@ void GpuCgSolver::setup() {
         matrix_bytes = total + (ns + 1) * 8;
       }
     }
-    if (!c8_ && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 && n > 0) {
+    info_.sell_fill = nnz > 0 ? (double)total / (double)nnz : 1.0;
+    if (!c8_ && !perm_.get() && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 && n > 0) {
       // windowed pass: per-chunk column windows of the generated matrix
       const int64_t nch = (n + kern::kWinRows - 1) / kern::kWinRows;
       win_.allocate(2 * nch, "A");

@@ -321,7 +321,7 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
     const int64_t sl = tile_unit(sr, cur.t);
     const double sum = sell_slice<U, NT, CM>(A, sl, s_dict, gather);
     const int64_t i = sl * 64 + lane;
-    if (i < A.n_rows) epi(i, sum);
+    if (i < A.n_rows) epi(A.perm ? (int64_t)A.perm[i] : i, sum);
   }
 }
 
@@ -371,8 +371,8 @@ __device__ __forceinline__ void sell2(const SellDev& A, const TileRanges& sr, Ga
       }
     }
     const int64_t ia = sa * 64 + lane, ib = sb * 64 + lane;
-    if (ia < A.n_rows) epi(ia, suma);
-    if (has_b && ib < A.n_rows) epi(ib, sumb);
+    if (ia < A.n_rows) epi(A.perm ? (int64_t)A.perm[ia] : ia, suma);
+    if (has_b && ib < A.n_rows) epi(A.perm ? (int64_t)A.perm[ib] : ib, sumb);
   }
 }
 

@@ -70,6 +70,9 @@ struct CgOptions {
   int pmat = -1;             // single-reduction form: materialized-p split pass (update kernel + SpMV gathering the
                              // stored p only; cg_split.hip) — the irregular-sparsity path; -1 = auto (long rows
                              // without an LDS window, or the all-gather layout), 0 = off, 1 = on
+  int sell_sigma = -1;       // SELL-C-sigma for user matrices: rows sorted by length inside windows of this many
+                             // rows (multiple of 64) so slices pad less; -1 = auto (4096-row windows when that cuts
+                             // the padded SELL slots by >= 10 %), 0 = off
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

@@ -97,6 +97,9 @@ struct SellDev {
   // 4 bits each, lanes 2i / 2i+1 of a slice entry in one byte (byte offset = c8 offset / 2);
   // read by the line-carry pass (half the matrix stream of c8)
   const uint8_t* codes4 = nullptr;
+  // SELL-C-sigma (user matrices): slot i of the slices holds local row perm[i] (rows sorted by
+  // length inside windows, so a slice pads less); nullptr = identity.  int32 columns only.
+  const int32_t* perm = nullptr;
 };
 
 namespace kern {

@@ -53,6 +53,8 @@ struct SolverInfo {
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool fused_reduce = false;  // the pass reduces its own block partials (one kernel per iteration)
   bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
+  int sigma = 0;              // SELL-C-sigma window (rows) of a user matrix; 0 = slices in row order
+  double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
@@ -142,6 +144,7 @@ class GpuCgSolver {
   DeviceBuffer<uint8_t> codes_;  // SELL-64/c8 dictionary codes
   DeviceBuffer<double2> dict_;
   DeviceBuffer<uint8_t> codes4_;  // SELL-64/c4 copy of the codes (line-carry pass, <= 16 dictionary entries)
+  DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
   int ndict_ = 0;
   bool c8_ = false;
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
@@ -159,6 +162,7 @@ class GpuCgSolver {
     s.dict = dict_.get();
     s.ndict = ndict_;
     s.codes4 = codes4_.get();
+    s.perm = perm_.get();
     return s;
   }
   // vectors

@@ -208,6 +208,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fused_reduce", &CgOptions::fused_reduce)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       .def_readwrite("pmat", &CgOptions::pmat)
+      .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -357,6 +358,8 @@ PYBIND11_MODULE(_C, m) {
         d["carry"] = i.carry;
         d["fused_reduce"] = i.fused_reduce;
         d["pmat"] = i.pmat;
+        d["sigma"] = i.sigma;
+        d["sell_fill"] = i.sell_fill;
         d["allgather"] = i.allgather;
         d["graph_fallbacks"] = i.graph_fallbacks;
         d["xcd_map"] = i.xcd_map;

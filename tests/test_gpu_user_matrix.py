@@ -72,3 +72,58 @@ def test_cli_matrix_on_gpu_golden(mcg, tmp_path):
                        timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout == "0.500000\n0.750000\n1.000000\nSuccess\n"
+
+
+def _skewed(n=6000, seed=7, band=None):
+    """SPD with very uneven row lengths (most rows ~3 nonzeros, every 37th row ~150): SELL in row
+    order pads every slice holding a long row to its length."""
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    for i in range(0, n, 37):
+        lo, hi = (0, n) if band is None else (max(0, i - band), min(n, i + band))
+        c = rng.choice(np.arange(lo, hi), size=min(150, hi - lo), replace=False)
+        rows += [i] * len(c)
+        cols += list(c)
+    for i in range(n):
+        c = rng.integers(max(0, i - 3), min(n, i + 4), size=2)
+        rows += [i] * 2
+        cols += list(c)
+    A = sp.csr_matrix((rng.uniform(0.1, 1.0, len(rows)), (rows, cols)), shape=(n, n))
+    A = A + A.T
+    return (A + sp.diags(np.asarray(abs(A).sum(axis=1)).ravel() + 1.0)).tocsr()
+
+
+@pytest.mark.parametrize("pmat", [0, 1])
+def test_sell_sigma_sorting_user_matrix(mcg, pmat):
+    """SELL-C-sigma: rows sorted by length inside 4096-row windows -> fewer padded slots, same x."""
+    A = _skewed()
+    p = mcg.csr_problem(A, b=np.ones(A.shape[0]))
+    C = mcg.native()
+    cpu = C.cpu_cg(p.native(), C.CgOptions(maxit=2000, tol=1e-9))
+    sig = mcg.CGSolver(p, format="sell", recurrence=1, pmat=pmat, tol=1e-9, check_every=8)
+    plain = mcg.CGSolver(p, format="sell", recurrence=1, pmat=pmat, tol=1e-9, check_every=8, sell_sigma=0)
+    assert sig.info["sigma"] == 4096 and plain.info["sigma"] == 0
+    assert sig.info["sell_fill"] < 0.6 * plain.info["sell_fill"]
+    a, b = sig.solve(), plain.solve()
+    assert a["converged"] and abs(a["iterations"] - b["iterations"]) <= 1
+    np.testing.assert_allclose(a["x_local"], cpu["x"], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(b["x_local"], cpu["x"], rtol=1e-7, atol=1e-9)
+    assert sig.true_residual_norm() < 1e-7
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sell_sigma_local_ranks_keeps_interior_split(mcg, world):
+    """Banded skewed matrix at P ranks (column-window halos, interior || halo): the sorting windows
+    never mix interior and boundary slices."""
+    A = _skewed(band=60)
+    p = mcg.csr_problem(A, b=np.ones(A.shape[0]))
+    assert not mcg.parallel.layout(p, world, 0).allgather
+    C = mcg.native()
+    cpu = C.cpu_cg(p.native(), C.CgOptions(maxit=2000, tol=1e-9))
+    for pm in (0, 1):
+        o = C.CgOptions(maxit=2000, tol=1e-9, format="sell", recurrence=1, check_every=4)
+        o.pmat = pm
+        o.sell_sigma = 256
+        out = C.run_local_ranks(p.native(), o, world, 0, True)
+        assert abs(out["ranks"][0]["iterations"] - cpu["iterations"]) <= 1
+        np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-7, atol=1e-9)
