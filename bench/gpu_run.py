@@ -104,6 +104,21 @@ def recipes(a) -> dict:
                                                      f"--band 100 --density 1.0 --spread 12500000 --steps 10 "
                                                      f"--warmup 2 --phases 0")),
         ],
+        # config 5 at ~200 GB per GPU: bench, XCD-ordered slices, kernel stats, L2->fabric bytes
+        "config5": [
+            ("bench", 900, bench("--problem randspd --rows 12500000 --band 820 --density 1.0 --spread 12500000 "
+                                 "--steps 6 --warmup 1 --phases 2")),
+            ("xcd100", 300, bench("--problem randspd --rows 12500000 --band 100 --density 1.0 --spread 12500000 "
+                                  "--steps 20 --warmup 2 --set xcd_map=1")),
+            ("xcd650", 600, bench("--problem randspd --rows 12500000 --band 650 --density 1.0 --spread 12500000 "
+                                  "--steps 6 --warmup 1 --set xcd_map=1")),
+            ("stats", 900, prof("c5_stats", f"{PY} {ROOT}/bench.py --problem randspd --rows 12500000 --band 820 "
+                                            f"--density 1.0 --spread 12500000 --steps 4 --warmup 1 --phases 0")),
+            ("bytes", 900, prof("c5_bytes", f"{PY} {ROOT}/bench.py --problem randspd --rows 12500000 --band 820 "
+                                            f"--density 1.0 --spread 12500000 --steps 2 --warmup 1 --phases 0 "
+                                            f"--no-verify", "TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum "
+                                                            "GRBM_GUI_ACTIVE")),
+        ],
         # the distributed path at headline sizes as P in-process ranks on one GPU
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),
