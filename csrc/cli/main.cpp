@@ -373,7 +373,7 @@ int main(int argc, char** argv) {
                 problem_name(a.spec).c_str(), (long long)n, (long long)info.nnz_local, world,
                 a.cpu ? "cpu" : "gpu",
                 a.cpu ? "csr"
-                      : (info.format == 3 ? "sell64-c8"
+                      : info.format == 4 ? "sell64-aligned" : (info.format == 3 ? "sell64-c8"
                                           : (info.format == 2 ? "sell64-d16" : (info.format == 1 ? "sell64" : "csr"))),
                 res.iterations,
                 res.converged ? "true" : "false", res.breakdown ? "true" : "false", res.rnorm, true_rnorm,

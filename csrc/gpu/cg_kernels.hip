@@ -459,7 +459,9 @@ void spmv_sell(const SellDev& A, const double* x, double* y, hipStream_t stream)
   const int64_t ns = (A.n_rows + 63) / 64;
   if (ns == 0) return;
   const int grid = grid_for(ns * 64, kBS, 8);
-  if (A.codes)
+  if (A.soffs)
+    hipLaunchKernelGGL(k_spmv_sell<3>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
+  else if (A.codes)
     hipLaunchKernelGGL(k_spmv_sell<2>, dim3(grid), dim3(kBS), 0, stream, A, x, y);
   else if (A.dcols)
     hipLaunchKernelGGL(k_spmv_sell<1>, dim3(grid), dim3(kBS), 0, stream, A, x, y);

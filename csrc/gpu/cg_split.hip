@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kBS) void k_split_update(double* __restrict__ x, do
 }
 
 // FMT: 0 CSR thread-per-row (U), 5 CSR-vector (G = U lanes per row), 1 SELL-64, 3 SELL-64/d16,
-// 4 SELL-64/c8
+// 4 SELL-64/c8, 6 SELL-64/aligned
 template <int FMT, typename IdxT, int U>
 __global__ __launch_bounds__(kBS) void k_split_spmv(CsrDev<IdxT> A, SellDev S, const double* __restrict__ p,
                                                     const double* __restrict__ r, double* __restrict__ Ap,
@@ -77,6 +77,7 @@ __global__ __launch_bounds__(kBS) void k_split_spmv(CsrDev<IdxT> A, SellDev S, c
   else if constexpr (FMT == 5) eng::csr_vector<IdxT, U>(A, tr, gather, epi);
   else if constexpr (FMT == 1) eng::sell<U, false, 0>(S, tr, gather, epi);
   else if constexpr (FMT == 3) eng::sell<U, false, 1>(S, tr, gather, epi);
+  else if constexpr (FMT == 6) eng::sell<U, false, 3>(S, tr, gather, epi);
   else eng::sell<U, false, 2>(S, tr, gather, epi);
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
@@ -118,6 +119,7 @@ void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, 
   } else if (fmt == 0) MCG_SU(0);
   else if (fmt == 1) MCG_SU(1);
   else if (fmt == 3) MCG_SU(3);
+  else if (fmt == 6) MCG_SU(6);
   else MCG_SU(4);
 #undef MCG_SU
 #undef MCG_S

@@ -201,6 +201,70 @@ __global__ __launch_bounds__(kGenBlock) void k_fill_sell(ProblemSpec s, int64_t 
   }
 }
 
+// SELL-64/aligned (wide random SPD): candidate t reaches the matrix from some row of the slice
+// [g0, g0 + 64) (global rows, g0 + 63 clamped to n - 1) iff d_t <= g1 (lower) / d_t <= n - 1 - g0 (upper)
+__device__ __forceinline__ void aligned_counts(const ProblemSpec& s, int64_t g0, int64_t g1, int64_t& nlo,
+                                               int64_t& nhi) {
+  const int64_t n = s.rows, W = s.band;
+  nlo = 0;
+  nhi = 0;
+  for (int64_t t = 0; t < W; ++t) {  // d_t increases with t
+    const int64_t d = randspd_offset(s, t);
+    if (d <= g1) nlo = t + 1;
+    if (d <= n - 1 - g0) nhi = t + 1;
+  }
+}
+
+__global__ __launch_bounds__(kGenBlock) void k_aligned_widths(ProblemSpec s, int64_t row_begin, int64_t n,
+                                                              int64_t* __restrict__ sp) {
+  const int64_t ns = (n + 63) / 64;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t sl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < ns; sl += stride) {
+    const int64_t g0 = row_begin + sl * 64, g1 = row_begin + ((sl + 1) * 64 < n ? (sl + 1) * 64 : n) - 1;
+    int64_t nlo, nhi;
+    aligned_counts(s, g0, g1, nlo, nhi);
+    sp[sl + 1] = 64 * (nlo + 1 + nhi);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) sp[0] = 0;
+}
+
+// one thread per padded row; slots in ascending column order (lower candidates descending, the
+// diagonal, upper ascending): the same entries in the same order as k_fill_sell, plus zeros
+__global__ __launch_bounds__(kGenBlock) void k_fill_aligned(ProblemSpec s, int64_t row_begin, int64_t n,
+                                                            const int64_t* __restrict__ rp64,
+                                                            const int64_t* __restrict__ sp,
+                                                            int32_t* __restrict__ soffs, double* __restrict__ svals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n_pad = (n + 63) / 64 * 64, N = s.rows;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
+    const int64_t sl = i >> 6, l = i & 63;
+    const int64_t base = sp[sl], w = (sp[sl + 1] - base) >> 6;
+    const int64_t g0 = row_begin + sl * 64, g1 = row_begin + ((sl + 1) * 64 < n ? (sl + 1) * 64 : n) - 1;
+    int64_t nlo, nhi;
+    aligned_counts(s, g0, g1, nlo, nhi);
+    const bool row = i < n;
+    const int64_t g = row_begin + i;
+    for (int64_t j = 0; j < w; ++j) {
+      int64_t o;
+      double v = 0.0;
+      if (j < nlo) {  // lower candidate t = nlo - 1 - j
+        o = -randspd_offset(s, nlo - 1 - j);
+        const int64_t c = g + o;
+        if (row && c >= 0 && randspd_present(s, c, g)) v = -randspd_weight(s, c, g);
+      } else if (j == nlo) {
+        o = 0;
+        if (row) v = (double)(rp64[i + 1] - rp64[i]);  // diagonal = row length (problem.hpp)
+      } else {  // upper candidate t = j - nlo - 1
+        o = randspd_offset(s, j - nlo - 1);
+        const int64_t c = g + o;
+        if (row && c < N && randspd_present(s, g, c)) v = -randspd_weight(s, g, c);
+      }
+      if (l == 0) soffs[(base >> 6) + j] = (int32_t)o;
+      svals[base + 64 * j + l] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kGenBlock) void k_max_i64(const int64_t* __restrict__ a, int64_t n,
                                                        unsigned long long* __restrict__ out) {
   int64_t m = 0;
@@ -298,6 +362,23 @@ void gen_fill_sell(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t c
   hipLaunchKernelGGL(k_fill_sell, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, col_lo, pad, own_off,
                      rowptr64, slice_ptr, scols, dcols, svals);
   MCG_HIP(hipGetLastError(), "kernel launch failed(gen_fill_sell)");
+}
+
+void randspd_aligned_widths(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t* slice_ptr,
+                            hipStream_t st) {
+  MCG_CHECK(s.kind == ProblemKind::RandomSPD, "aligned SELL: random-SPD family only");
+  const int64_t ns = (n + 63) / 64;
+  if (ns == 0) return;
+  hipLaunchKernelGGL(k_aligned_widths, dim3(gen_grid(ns)), dim3(kGenBlock), 0, st, s, row_begin, n, slice_ptr);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(aligned_widths)");
+}
+
+void randspd_fill_aligned(const ProblemSpec& s, int64_t row_begin, int64_t n, const int64_t* rowptr64,
+                          const int64_t* slice_ptr, int32_t* soffs, double* svals, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_fill_aligned, dim3(gen_grid(n)), dim3(kGenBlock), 0, st, s, row_begin, n, rowptr64, slice_ptr,
+                     soffs, svals);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(fill_aligned)");
 }
 
 void sell_slice_widths(const int64_t* rowptr64, int64_t n, int64_t* slice_ptr, hipStream_t st) {

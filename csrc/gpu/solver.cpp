@@ -16,6 +16,16 @@ namespace mcg {
 namespace {
 constexpr int kCsrBlocksPerCuCap = 6;  // LDS-limited residency of the CSR tile kernel (26.7 KB/block)
 
+// SELL-64/aligned slots per nonzero expected for a wide random SPD matrix: a slice keeps the
+// ~W candidates that reach the matrix from it; a row holds 1 + (W/2)(q_row + q_mean) of them,
+// q = min(1, density * f) with f uniform on [0.25, 1.75] (problem.hpp randspd_density)
+double randspd_aligned_fill(const ProblemSpec& s) {
+  double qm = 0.0;
+  for (int k = 0; k < 1000; ++k) qm += std::min(1.0, s.density * (0.25 + 1.5 * (k + 0.5) / 1000.0));
+  qm /= 1000.0;
+  return (double)(s.band + 1) / (1.0 + (double)s.band * qm);
+}
+
 // stored SELL-64 slots of rows taken in the order `order` (slice = 64 consecutive slots)
 int64_t sell_slots(const HostCsr& A, const std::vector<int32_t>* order) {
   const int64_t n = A.n_rows;
@@ -215,7 +225,13 @@ void GpuCgSolver::setup() {
     // ---- SELL-64, generated directly (no CSR intermediate: peak memory = the SELL arrays) ----
     const int64_t ns = (n + 63) / 64;
     slice_ptr_.allocate(ns + 1, "A");
-    kern::sell_slice_widths(rp64.get(), n, slice_ptr_.get(), s0_);
+    // SELL-64/aligned: the same decision on every rank (from the spec, not from this rank's rows),
+    // since it implies the split pass and with it the ghost vectors exchanged
+    aligned_ = spec_.kind == ProblemKind::RandomSPD && spec_.spread > 0 && opt_.recurrence == 1 &&
+               opt_.pmat != 0 && opt_.sell_aligned != 0 &&
+               (opt_.sell_aligned == 1 || randspd_aligned_fill(spec_) <= 1.6);
+    if (aligned_) kern::randspd_aligned_widths(spec_, L_.row_begin, n, slice_ptr_.get(), s0_);
+    else kern::sell_slice_widths(rp64.get(), n, slice_ptr_.get(), s0_);
     {
       DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ns), "A");
       kern::scan_inclusive_i64(slice_ptr_.get() + 1, ns, tmp.get(), s0_);
@@ -224,10 +240,19 @@ void GpuCgSolver::setup() {
     int64_t total = 0;
     MCG_HIP(hipMemcpy(&total, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
             "memcpy from device to host failed(A)");
-    if (d16_) dcols_.allocate(total, "A", 16);
+    if (aligned_) {
+      d16_ = false;
+      c8_ = false;
+      info_.format = 4;
+      soffs_.allocate(std::max<int64_t>(total / 64, 1), "A");
+    } else if (d16_) dcols_.allocate(total, "A", 16);
     else cols_.allocate(total, "A", 8);
     vals_.allocate(total, "A", 8);
-    if (is_user) {  // host rows -> device CSR (temporary) -> SELL-64(/d16)
+    if (aligned_) {
+      kern::randspd_fill_aligned(spec_, L_.row_begin, n, rp64.get(), slice_ptr_.get(), soffs_.get(), vals_.get(),
+                                 s0_);
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    } else if (is_user) {  // host rows -> device CSR (temporary) -> SELL-64(/d16)
       DeviceBuffer<int32_t> tc(std::max<int64_t>(nnz, 1), "A");
       DeviceBuffer<double> tv(std::max<int64_t>(nnz, 1), "A");
       if (nnz) {
@@ -244,7 +269,7 @@ void GpuCgSolver::setup() {
       kern::gen_fill_sell(spec_, L_.row_begin, n, L_.col_lo, L_.pad, L_.own_off, rp64.get(), slice_ptr_.get(),
                           cols_.get(), dcols_.get(), vals_.get(), s0_);
     }
-    matrix_bytes = total * (d16_ ? 10 : 12) + (ns + 1) * 8;
+    matrix_bytes = aligned_ ? total * 8 + (total / 64) * 4 + (ns + 1) * 8 : total * (d16_ ? 10 : 12) + (ns + 1) * 8;
     if (c8_) {  // SELL-64/c8 when the (value, offset) dictionary fits one byte
       std::vector<double2> dict;
       int nv = 0, nd = 0;
@@ -277,7 +302,8 @@ void GpuCgSolver::setup() {
       }
     }
     info_.sell_fill = nnz > 0 ? (double)total / (double)nnz : 1.0;
-    if (!c8_ && !perm_.get() && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 && n > 0) {
+    if (!c8_ && !perm_.get() && !aligned_ && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 &&
+        n > 0) {
       // windowed pass: per-chunk column windows of the generated matrix
       const int64_t nch = (n + kern::kWinRows - 1) / kern::kWinRows;
       win_.allocate(2 * nch, "A");
@@ -310,10 +336,11 @@ void GpuCgSolver::setup() {
 
   // ---- iteration form for long / unstructured rows: the materialized-p split pass ----
   pmat_ = opt_.recurrence == 1 && opt_.pmat != 0 &&
-          (opt_.pmat == 1 || (win_doubles_ == 0 && !c8_ && (L_.allgather || nnz >= 32 * n)));
+          (opt_.pmat == 1 || aligned_ || (win_doubles_ == 0 && !c8_ && (L_.allgather || nnz >= 32 * n)));
   // the pass form decides which ghost vectors are exchanged ({r, Ap} + p, or p alone): every rank
   // must take the same one, whatever its own rows look like
   if (use_comm_ && world_ > 1) pmat_ = all_ranks_agree_(pmat_);
+  MCG_CHECK(!aligned_ || pmat_, "aligned SELL needs the split pass");
   if (pmat_) {
     opt_.interleave = 0;
     info_.interleave = false;
@@ -810,7 +837,7 @@ void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red) {
     rc.first = first;
   }
   const int64_t n = L_.n_local();
-  const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : 1)) : (info_.spmv_variant == 2 ? 5 : 0);
+  const int fmt = opt_.format == 1 ? (aligned_ ? 6 : (c8_ ? 4 : (d16_ ? 3 : 1))) : (info_.spmv_variant == 2 ? 5 : 0);
   const SellDev S = sell_view();
   if (info_.idx64)
     kern::cg_split_spmv<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S,

@@ -268,7 +268,8 @@ __device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRang
 // ---------------------------------------------------------------------------
 // SELL-64: one wave computes the 64 row sums of slice `sl` (lane = row in slice).
 // CM (column mode): 0 int32 ext columns, 1 int16 offsets from the row's own ext
-// column (SellDev::dcols), 2 one-byte dictionary codes (SellDev::codes) looked up
+// column (SellDev::dcols), 3 one offset per slot shared by the slice's 64 rows
+// (SellDev::soffs, SELL-64/aligned), 2 one-byte dictionary codes (SellDev::codes) looked up
 // in `dict` (an LDS copy of the {value, offset} table) — every lane of a stencil
 // slice reads the same code at entry j, so the LDS read is a broadcast.
 template <int U, bool NT, int CM, class Gather>
@@ -292,6 +293,11 @@ __device__ __forceinline__ double sell_slice(const SellDev& A, int64_t sl, const
         const double2 q = dict[ld<NT>(kp + j)];
         c[u] = rowcol + (int32_t)__double_as_longlong(q.y);
         v[u] = q.x;
+      } else if constexpr (CM == 3) {
+        // slot offset: one wave-uniform value per slot (the slice's list), clamped column
+        const int64_t cc = (int64_t)rowcol + A.soffs[(base >> 6) + (j >> 6)];
+        c[u] = (int32_t)(cc < 0 ? 0 : (cc >= A.ext_len ? A.ext_len - 1 : cc));
+        v[u] = ld<NT>(vp + j);
       } else {
         if constexpr (CM == 1) c[u] = rowcol + (int32_t)ld<NT>(dp + j);
         else c[u] = ld<NT>(cp + j);

@@ -73,6 +73,8 @@ struct CgOptions {
   int sell_sigma = -1;       // SELL-C-sigma for user matrices: rows sorted by length inside windows of this many
                              // rows (multiple of 64) so slices pad less; -1 = auto (4096-row windows when that cuts
                              // the padded SELL slots by >= 10 %), 0 = off
+  int sell_aligned = -1;     // wide random SPD: SELL-64/aligned (one column offset per slot shared by the slice's
+                             // rows, values only; contiguous gathers); -1 = auto (expected fill <= 1.6), 0 = off
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

@@ -100,6 +100,12 @@ struct SellDev {
   // SELL-C-sigma (user matrices): slot i of the slices holds local row perm[i] (rows sorted by
   // length inside windows, so a slice pads less); nullptr = identity.  int32 columns only.
   const int32_t* perm = nullptr;
+  // SELL-64/aligned (long rows whose slices share their column offsets, e.g. the wide random-SPD
+  // family): entry j of EVERY lane of slice s is the row's own column + soffs[slice_ptr[s] / 64 + j]
+  // (one wave-uniform offset per slot, clamped to [0, ext_len); absent entries hold 0.0), so a
+  // slot's 64 gathers are one contiguous 512-B run and no per-entry column index is stored.
+  const int32_t* soffs = nullptr;
+  int64_t ext_len = 0;
 };
 
 namespace kern {
@@ -129,6 +135,14 @@ void csr_to_sell(const IdxT* rowptr, const int32_t* cols, const double* vals, in
 void gen_fill_sell(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad, int64_t own_off,
                    const int64_t* rowptr64, const int64_t* slice_ptr, int32_t* scols, int16_t* dcols, double* svals,
                    hipStream_t st);
+// SELL-64/aligned for the wide random-SPD family: per 64-row slice, the candidate offsets that
+// reach a column of the matrix for some row of the slice (sorted: the lower candidates descending,
+// 0, the upper ascending); slice_ptr[s+1] = 64 * that count (then scan), and the fill writes the
+// per-slot offsets (soffs[slice_ptr[s] / 64 + j]) and every lane's value (0 when absent)
+void randspd_aligned_widths(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t* slice_ptr,
+                            hipStream_t st);
+void randspd_fill_aligned(const ProblemSpec& s, int64_t row_begin, int64_t n, const int64_t* rowptr64,
+                          const int64_t* slice_ptr, int32_t* soffs, double* svals, hipStream_t st);
 // SELL-64/c8 dictionary (csrc/gpu/dict.hip) from a generated SELL-64(/d16) matrix: false if
 // it has too many distinct values / offsets.  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
 bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
@@ -246,7 +260,7 @@ void cg_split_update(double* x, double* r, const double* Ap, double* p_own, int6
                      int first, int check, int final_mode, double* partials, int pstride, int grid,
                      hipStream_t stream);
 // fmt: 0 CSR thread-per-row (param U), 5 CSR-vector (param G lanes per row), 1 SELL-64, 3 SELL-64/d16,
-// 4 SELL-64/c8
+// 4 SELL-64/c8, 6 SELL-64/aligned
 template <typename IdxT>
 void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const double* p_ext, const double* r,
                    double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,

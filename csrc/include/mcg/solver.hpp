@@ -145,6 +145,8 @@ class GpuCgSolver {
   DeviceBuffer<double2> dict_;
   DeviceBuffer<uint8_t> codes4_;  // SELL-64/c4 copy of the codes (line-carry pass, <= 16 dictionary entries)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
+  DeviceBuffer<int32_t> soffs_;   // SELL-64/aligned per-slot column offsets
+  bool aligned_ = false;
   int ndict_ = 0;
   bool c8_ = false;
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
@@ -163,6 +165,8 @@ class GpuCgSolver {
     s.ndict = ndict_;
     s.codes4 = codes4_.get();
     s.perm = perm_.get();
+    s.soffs = soffs_.get();
+    s.ext_len = L_.ext_len;
     return s;
   }
   // vectors

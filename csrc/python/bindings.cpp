@@ -209,6 +209,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       .def_readwrite("pmat", &CgOptions::pmat)
       .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
+      .def_readwrite("sell_aligned", &CgOptions::sell_aligned)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -349,7 +350,8 @@ PYBIND11_MODULE(_C, m) {
         d["halo_out"] = i.halo_out;
         d["interior_rows"] = i.interior_rows;
         d["idx64"] = i.idx64;
-        d["format"] = i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
+        d["format"] = i.format == 4 ? "sell64-aligned"
+                      : i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
         d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["interleave"] = i.interleave;
         d["window"] = i.window;

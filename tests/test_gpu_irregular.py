@@ -104,3 +104,35 @@ def test_local_ranks_split_pass_window_halo(mcg, world, overlap):
     its = {r["iterations"] for r in out["ranks"]}
     assert len(its) == 1 and abs(its.pop() - cpu["iterations"]) <= 2
     np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+
+
+DENSE_WIDE = dict(rows=30000, band=64, density=1.0, spread=30000)
+
+
+def test_aligned_sell_auto_and_same_row_sums(mcg):
+    """SELL-64/aligned (one offset per slot, values only) stores the entries of SELL-64 in the same
+    order plus zeros: the same recurrence, the CPU oracle's x, fewer matrix bytes per nonzero."""
+    spec = mcg.make_problem("randspd", **DENSE_WIDE)
+    a = mcg.CGSolver(spec, format="sell", recurrence=1, check_every=8)
+    b = mcg.CGSolver(spec, format="sell", recurrence=1, check_every=8, sell_aligned=0)
+    assert a.info["format"] == "sell64-aligned" and a.info["pmat"]
+    assert b.info["format"] == "sell64"
+    ra, rb = a.solve(), b.solve()
+    assert ra["iterations"] == rb["iterations"]
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-13, atol=1e-15)
+    cpu = _cpu(mcg, spec)
+    np.testing.assert_allclose(ra["x_local"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    assert a.true_residual_norm() < 1e-6
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_aligned_sell_local_ranks_all_gather(mcg, world):
+    spec = mcg.make_problem("randspd", **DENSE_WIDE)
+    C = mcg.native()
+    cpu = _cpu(mcg, spec)
+    o = C.CgOptions(format="sell", recurrence=1, check_every=4)
+    out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    assert len({r["iterations"] for r in out["ranks"]}) == 1
+    assert abs(out["ranks"][0]["iterations"] - cpu["iterations"]) <= 1
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
