@@ -69,6 +69,10 @@ def parse_args(argv=None):
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="timing rehearsal: run rank --sim-rank of a P-rank job alone on this GPU (its rows, "
+                         "ghost layout, interior/boundary launches, graphs) with collectives that move nothing")
+    ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank(s) as child processes even for --gpus 1 (the --gpus N > 1 launch route)")
     return ap.parse_args(argv)
@@ -119,6 +123,9 @@ def _run_rank(args, out_fd) -> int:
     if env.world > 1:
         pdist.init_process_group(env, backend="gloo")
     comm = pdist.bootstrap_comm(env, force=args.force_comm)
+    sim = args.sim_world > 1 and env.world == 1
+    if sim:  # per-rank timing rehearsal (not a P-rank solve: see --sim-world)
+        comm = mcg.native().NullComm(args.sim_rank, args.sim_world)
 
     if args.problem == "randspd":
         spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, spread=args.spread,
@@ -139,7 +146,8 @@ def _run_rank(args, out_fd) -> int:
             raise SystemExit(f"bench.py: unknown option {k!r}")
         setattr(opts, k, type(getattr(opts, k))(v))
     t_setup = time.perf_counter()
-    solver = C.Solver(spec.native(), opts, env.rank, env.world, comm)
+    solver = (C.Solver(spec.native(), opts, args.sim_rank, args.sim_world, comm) if sim
+              else C.Solver(spec.native(), opts, env.rank, env.world, comm))
     solver.setup()
     solver.reset()
     setup_s = time.perf_counter() - t_setup
@@ -177,7 +185,7 @@ def _run_rank(args, out_fd) -> int:
         tr = solver.true_residual_norm()
         extra["true_rnorm"] = tr
         extra["true_gap_rel"] = abs(tr - res["rnorm"]) / max(tr, 1e-300)
-        ok = ok and abs(tr - res["rnorm"]) <= 1e-8 * max(tr, 1e-300) + 1e-12
+        ok = ok and (sim or abs(tr - res["rnorm"]) <= 1e-8 * max(tr, 1e-300) + 1e-12)
     info = solver.info
     # whole-job result: the slowest rank's clock, every rank ok and latched at the same count
     mine = {"dt": dt, "ok": bool(ok), "iterations": int(res["iterations"])}
@@ -192,7 +200,7 @@ def _run_rank(args, out_fd) -> int:
         if env.world > 1:
             dist.all_reduce(t)
         nnz = int(t.item())
-    headline = args.problem == "poisson2d" and args.grid == 16384
+    headline = args.problem == "poisson2d" and args.grid == 16384 and not sim
     if phases is not None:
         extra["phase_us"] = phases
         if env.world > 1:  # slowest rank per phase
@@ -204,7 +212,9 @@ def _run_rank(args, out_fd) -> int:
              if args.problem == "randspd" else f"{args.problem}_N{args.grid}")
     if env.rank == 0:
         line = json.dumps({
-            "metric": METRIC if headline else "CG iterations/sec (whole node), %s" % model,
+            "metric": METRIC if headline else (
+                "per-rank iterations/sec, timing rehearsal of rank %d of %d (collectives move nothing), %s"
+                % (args.sim_rank, args.sim_world, model) if sim else "CG iterations/sec (whole node), %s" % model),
             "value": round(value, 4),
             "unit": "iterations/s",
             "n_gpus": n_gpus,
@@ -226,7 +236,7 @@ def _run_rank(args, out_fd) -> int:
                 "nnz": nnz,
                 "global_batch": 1,
                 "seq_len": spec.n_rows,
-                "parallelism": f"rowpart{n_gpus}",
+                "parallelism": f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else f"rowpart{n_gpus}",
                 # storage the timed pass streams: the 2-D line-carry pass reads 4-bit codes (c4)
                 "format": "sell64-c4" if info.get("codes4") else info["format"],
                 "recurrence": info["recurrence"],

@@ -121,6 +121,16 @@ def recipes(a) -> dict:
                                             f"--no-verify", "TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum "
                                                             "GRBM_GUI_ACTIVE")),
         ],
+        # one rank's share of a P-rank run, alone on this GPU (NullComm: collectives move nothing):
+        # the per-rank work the scaling runs will see, without the communication latency
+        "simrank": [
+            (f"p{P}_r{r}", 200, bench(f"--sim-world {P} --sim-rank {r} --steps 400 --warmup 40 --phases 10"))
+            for P, r in ((2, 0), (4, 1), (8, 0), (8, 3), (8, 7))
+        ] + [
+            (f"p{P}_r{r}_3d", 200, bench(f"--problem poisson3d --grid 512 --sim-world {P} --sim-rank {r} "
+                                         f"--steps 400 --warmup 40 --phases 10"))
+            for P, r in ((8, 3),)
+        ],
         # the distributed path at headline sizes as P in-process ranks on one GPU
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),

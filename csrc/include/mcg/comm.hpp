@@ -84,6 +84,23 @@ class Comm final : public Communicator {
   bool aborted_ = false;
 };
 
+// Timing rehearsal of ONE rank of a P-rank run on a single GPU: the solver runs rank r's rows,
+// ghost layout, interior / boundary launches, side-stream fork/join and graphs exactly as at P
+// ranks, but the collectives move nothing (all-reduce: the local sums stay local; halo: no
+// transfer, ghosts keep their values).  The numbers it computes are not the P-rank solve's; the
+// time per iteration is the rank's own work without the communication latency.
+class NullComm final : public Communicator {
+ public:
+  NullComm(int rank, int world) : rank_(rank), world_(world) {}
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void allreduce_sum(double*, size_t, hipStream_t) override {}
+  void halo_exchange(const LocalLayout&, double* const*, int, hipStream_t, const int* = nullptr) override {}
+
+ private:
+  int rank_, world_;
+};
+
 // Shared state of P in-process ranks on one device.
 class LocalGroup {
  public:

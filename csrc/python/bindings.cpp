@@ -302,12 +302,22 @@ PYBIND11_MODULE(_C, m) {
       .def("check_async", &Comm::check_async)
       .def("abort", &Comm::abort);
 
+  py::class_<NullComm, std::shared_ptr<NullComm>>(m, "NullComm",
+                                                  "one rank of a P-rank run with collectives that move nothing "
+                                                  "(per-rank timing rehearsal on one GPU)")
+      .def(py::init<int, int>(), py::arg("rank"), py::arg("world"));
+
   py::class_<GpuCgSolver>(m, "Solver")
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<Comm> comm) {
              return new GpuCgSolver(s, o, rank, world, comm.get());
            }),
            py::arg("spec"), py::arg("opts"), py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("comm") = nullptr, py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
+      .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<NullComm> comm) {
+             return new GpuCgSolver(s, o, rank, world, comm.get());
+           }),
+           py::arg("spec"), py::arg("opts"), py::arg("rank"), py::arg("world"), py::arg("comm"),
+           py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
       .def("setup", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.setup(); })
       .def("reset", [](GpuCgSolver& g) { py::gil_scoped_release rel; g.reset(); })
       .def("solve", [](GpuCgSolver& g, bool resume) {
