@@ -250,7 +250,7 @@ def _run_rank(args, out_fd) -> int:
                 "launch": route,
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
-                      "comm_world": comm.count if comm is not None else 1,
+                      "comm_world": comm.count if (comm is not None and not sim) else 1,
                       "graph_fallbacks": info.get("graph_fallbacks", 0),
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
