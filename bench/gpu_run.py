@@ -131,6 +131,15 @@ def recipes(a) -> dict:
                                          f"--steps 400 --warmup 40 --phases 10"))
             for P, r in ((8, 3),)
         ],
+        # line-carry geometry at a P = 8 rank's share (2046 interior lines of 16384^2)
+        "carrysweep": [
+            (f"b{b}_d{d}", 200, bench(f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 --no-verify "
+                                      f"--set carry_blocks_per_cu={b} --set carry_depth={d}"))
+            for b in (2, 3, 4, 6, 8) for d in (2, 3)
+        ] + [
+            (f"full_b{b}", 200, bench(f"--steps 100 --warmup 10 --phases 0 --no-verify --set carry_blocks_per_cu={b}"))
+            for b in (2, 4, 8)
+        ],
         # the distributed path at headline sizes as P in-process ranks on one GPU
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),
