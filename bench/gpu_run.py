@@ -108,6 +108,8 @@ def recipes(a) -> dict:
         "config5": [
             ("bench", 900, bench("--problem randspd --rows 12500000 --band 820 --density 1.0 --spread 12500000 "
                                  "--steps 6 --warmup 1 --phases 2")),
+            ("bench1640", 900, bench("--problem randspd --rows 12500000 --band 1640 --density 1.0 "
+                                     "--spread 12500000 --steps 4 --warmup 1 --phases 2")),
             ("plain820", 900, bench("--problem randspd --rows 12500000 --band 820 --density 1.0 --spread 12500000 "
                                     "--steps 6 --warmup 1 --phases 2 --set sell_aligned=0")),
             ("xcd100", 300, bench("--problem randspd --rows 12500000 --band 100 --density 1.0 --spread 12500000 "
