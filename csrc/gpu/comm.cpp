@@ -70,6 +70,18 @@ void Comm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec
   MCG_RCCL(ncclGroupEnd(), "RCCL group failed");
 }
 
+void Comm::sendrecv(const double* send, int to, double* recv, int from, size_t n, hipStream_t stream) {
+  MCG_RCCL(ncclGroupStart(), "RCCL group failed");
+  MCG_RCCL(ncclSend(send, n, ncclFloat64, to, halo_, stream), "RCCL halo send failed");
+  MCG_RCCL(ncclRecv(recv, n, ncclFloat64, from, halo_, stream), "RCCL halo recv failed");
+  MCG_RCCL(ncclGroupEnd(), "RCCL group failed");
+}
+
+void Comm::allgather_inplace(double* buf, size_t block, hipStream_t stream) {
+  MCG_RCCL(ncclAllGather(buf + (size_t)rank_ * block, buf, block, ncclFloat64, halo_, stream),
+           "RCCL allgather failed");
+}
+
 int Comm::count() const {
   int n = 0;
   MCG_RCCL(ncclCommCount(reduce_, &n), "RCCL comm count failed");

@@ -75,6 +75,11 @@ class Comm final : public Communicator {
   void check_async() override;
   // ranks in the communicator as RCCL sees them (ncclCommCount)
   int count() const;
+  // one grouped point-to-point exchange on the halo communicator: send n doubles to `to`, receive
+  // n doubles from `from` (either may be this rank: the loopback the 1-GPU tests capture in graphs)
+  void sendrecv(const double* send, int to, double* recv, int from, size_t n, hipStream_t stream);
+  // in-place all-gather of `block` doubles per rank on the halo communicator (buf: world * block)
+  void allgather_inplace(double* buf, size_t block, hipStream_t stream);
   void abort() override;
 
  private:

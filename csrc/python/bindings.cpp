@@ -299,6 +299,13 @@ PYBIND11_MODULE(_C, m) {
       .def("allreduce_sum_ptr", [](Comm& c, uintptr_t buf, size_t count, uintptr_t stream) {
         c.allreduce_sum(reinterpret_cast<double*>(buf), count, as_stream(stream));
       })
+      .def("sendrecv_ptr", [](Comm& c, uintptr_t send, int to, uintptr_t recv, int from, size_t n, uintptr_t stream) {
+        c.sendrecv(reinterpret_cast<const double*>(send), to, reinterpret_cast<double*>(recv), from, n,
+                   as_stream(stream));
+      })
+      .def("allgather_inplace_ptr", [](Comm& c, uintptr_t buf, size_t block, uintptr_t stream) {
+        c.allgather_inplace(reinterpret_cast<double*>(buf), block, as_stream(stream));
+      })
       .def("check_async", &Comm::check_async)
       .def("abort", &Comm::abort);
 

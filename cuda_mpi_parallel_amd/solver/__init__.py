@@ -105,14 +105,24 @@ class CGSolver:
 def solve(problem: str = "demo", device: str = "gpu", sim_ranks: int = 1, maxit: int = 2000, tol: float = 1e-7,
           **kw) -> Dict:
     """One-call solve.  ``solve()`` with no arguments is the reference's demo."""
-    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs") if k in kw}
+    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs", "spread", "nnz_per_row",
+                                      "matrix", "b", "reorder") if k in kw}
+    if "matrix" in spec_kw:  # solve(matrix=A_or_path, b=...): a user matrix (kind csr)
+        problem = "csr"
     spec = make_problem(problem, **spec_kw)
+    perm = getattr(spec, "perm", None)  # reordered user matrix: hand x back in the caller's numbering
     if device == "cpu":
         o = _opts(maxit, tol)
         C = native()
-        return C.cpu_cg_partitioned(spec.native(), sim_ranks, o) if sim_ranks > 1 else C.cpu_cg(spec.native(), o)
+        r = C.cpu_cg_partitioned(spec.native(), sim_ranks, o) if sim_ranks > 1 else C.cpu_cg(spec.native(), o)
+        if perm is not None:
+            r["x"] = spec.unpermute(r["x"])
+        return r
     s = CGSolver(spec, maxit=maxit, tol=tol, **kw)
-    return s.solve()
+    r = s.solve()
+    if perm is not None and s.env.world == 1:
+        r["x_local"] = spec.unpermute(r["x_local"])
+    return r
 
 
 __all__ = ["CGSolver", "solve"]

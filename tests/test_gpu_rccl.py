@@ -134,3 +134,46 @@ def test_single_gpu_pool_skips_cleanly():
         pytest.skip("multi-GPU node: the real tests above ran")
     p = _run([sys.executable, "bench.py", "--gpus", "2"], timeout=120)
     assert p.returncode == 2 and "--gpus 2" in p.stderr
+
+
+def _one_rank_comm(mcg):
+    C = mcg.native()
+    return C.Comm(0, 1, C.unique_id(), C.unique_id())
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rccl_loopback_sendrecv_and_allgather_on_one_gpu(mcg, graph):
+    """On one GPU the grouped ncclSend/ncclRecv (to this rank) and the in-place ncclAllGather run
+    through the same Comm calls the halo uses, eager and captured into a hipGraph."""
+    import torch
+
+    torch.cuda.set_device(0)
+    comm = _one_rank_comm(mcg)
+    n = 1 << 16
+    a = torch.arange(n, dtype=torch.float64, device="cuda") * 0.5
+    b = torch.zeros_like(a)
+    g = torch.arange(n, dtype=torch.float64, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+
+    def step():
+        comm.sendrecv_ptr(a.data_ptr(), 0, b.data_ptr(), 0, n, s.cuda_stream)
+        comm.allgather_inplace_ptr(g.data_ptr(), n, s.cuda_stream)
+
+    if graph:
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            cg.capture_begin()
+            step()
+            cg.capture_end()
+        b.zero_()
+        torch.cuda.synchronize()
+        cg.replay()
+        cg.replay()
+    else:
+        with torch.cuda.stream(s):
+            step()
+    torch.cuda.synchronize()
+    comm.check_async()
+    assert torch.equal(b, a)
+    assert torch.equal(g, torch.arange(n, dtype=torch.float64, device="cuda"))

@@ -164,3 +164,11 @@ def test_cli_matrix_flag_golden(mcg, tmp_path, cli):
                        text=True, timeout=120, cwd=ROOT)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout == "0.500000\n0.750000\n1.000000\nSuccess\n"
+
+
+def test_solve_helper_takes_a_matrix(mcg):
+    A = _spd(300, 0.02)
+    b = np.arange(300, dtype=float) / 300.0
+    for reorder in (None, "rcm"):
+        r = mcg.solve(matrix=A, b=b, device="cpu", tol=1e-10, reorder=reorder)
+        np.testing.assert_allclose(r["x"], sp.linalg.spsolve(A.tocsc(), b), rtol=1e-8, atol=1e-10)
