@@ -243,7 +243,8 @@ def _run_rank(args, out_fd) -> int:
                 "pass": ("line-carry" if info.get("carry") else "split (materialized p)" if info.get("pmat")
                          else "windowed" if info.get("window") else "generic, xcd-aware" if info.get("xcd_map")
                          else "generic"),
-                "ghosts": "allgather" if info.get("allgather") else "window",
+                "ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
+                if info.get("allgather") else "window",
                 "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,
@@ -254,7 +255,9 @@ def _run_rank(args, out_fd) -> int:
                       "graph_fallbacks": info.get("graph_fallbacks", 0),
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
-                      "placement_lead_trial": info.get("placement_lead_trial"),"model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
+                      "placement_lead_trial": info.get("placement_lead_trial"),
+                      **({"ag_local_frac": round(info["ag_local_frac"], 4)} if info.get("ag_overlap") else {}),
+                      "model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
                       "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3),
                       "device_gb_rank0": round(info["device_bytes"] / 1e9, 2), **extra},
         })

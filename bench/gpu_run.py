@@ -133,6 +133,16 @@ def recipes(a) -> dict:
                                          f"--steps 400 --warmup 40 --phases 10"))
             for P, r in ((8, 3),)
         ],
+        # config 5 at a P = 8 rank's share (1e8 rows spread over all rows, 12.5 M per rank): the
+        # all-gather overlap halves (own-block slots || all-gather, then the rest) vs one pass
+        "agoverlap": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'all_gather or aligned'"),
+        ] + [
+            (f"sim8_ag{ag}", 900, bench(f"--problem randspd --rows 100000000 --band 820 --density 1.0 "
+                                        f"--spread 100000000 --sim-world 8 --sim-rank 3 --steps 6 --warmup 1 "
+                                        f"--phases 2 --set ag_overlap={ag}"))
+            for ag in (1, 0)
+        ],
         # line-carry geometry at a P = 8 rank's share (2046 interior lines of 16384^2)
         "carrysweep": [
             (f"b{b}_d{d}", 200, bench(f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 --no-verify "

@@ -18,6 +18,7 @@
 // iteration (no pairing), r and Ap exist only for owned rows, p once (ext layout).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "mcg/check.hpp"
@@ -82,7 +83,76 @@ __global__ __launch_bounds__(kBS) void k_split_spmv(CsrDev<IdxT> A, SellDev S, c
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
+// SELL-64/aligned in two halves around the all-gather of p_k (kernels.hpp cg_split_spmv `part`):
+// LOCAL (part 1) sums the own-block slots and stores the partial row sums in Ap; the remote half
+// (part 2) adds the other slots to them and runs the epilogue of k_split_spmv
+template <int U, bool REMOTE>
+__global__ __launch_bounds__(kBS) void k_split_spmv_aligned_part(SellDev S, const double* __restrict__ p,
+                                                                 const double* __restrict__ r, double* __restrict__ Ap,
+                                                                 int64_t own, TileRanges tr,
+                                                                 double* __restrict__ partials, int pstride,
+                                                                 CgState* st, double tol, int first, int check,
+                                                                 RedCtl rc) {
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (st->done || sc.conv) {
+    if constexpr (REMOTE) f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+    return;
+  }
+  auto gather = [&](int32_t c) { return p[c]; };
+  if constexpr (!REMOTE) {
+    eng::sell_aligned_part<U, false, false>(S, tr, gather, [&](int64_t i, double sum) { Ap[i] = sum; });
+  } else {
+    double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+    eng::sell_aligned_part<U, false, true>(S, tr, gather, [&](int64_t i, double rem) {
+      const double sum = Ap[i] + rem;
+      const double pk = p[own + i], rk = r[i];
+      st_stream(&Ap[i], sum);
+      s_pap = fma(pk, sum, s_pap);
+      s_rap = fma(rk, sum, s_rap);
+      s_apap = fma(sum, sum, s_apap);
+      s_rr = fma(rk, rk, s_rr);
+    });
+    f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+  }
+}
+
+// one thread per slice: binary searches over the slice's ascending slot offsets
+__global__ __launch_bounds__(kBS) void k_aligned_local_slots(SellDev S, int32_t* __restrict__ out) {
+  const int64_t ns = (S.n_rows + 63) / 64;
+  for (int64_t sl = (int64_t)blockIdx.x * kBS + threadIdx.x; sl < ns; sl += (int64_t)gridDim.x * kBS) {
+    const int64_t base = S.slice_ptr[sl];
+    const int w = (int)((S.slice_ptr[sl + 1] - base) >> 6);
+    const int32_t* o = S.soffs + (base >> 6);
+    // lane columns own_off + 64 sl + [0, 64) + o inside [own_off, own_off + n_rows):
+    // o >= -64 sl  and  o < n_rows - 63 - 64 sl
+    const int64_t lo = -64 * sl, hi = S.n_rows - 63 - 64 * sl;
+    auto first_ge = [&](int64_t t) {
+      int a = 0, b = w;
+      while (a < b) {
+        const int m = (a + b) >> 1;
+        if ((int64_t)o[m] < t) a = m + 1;
+        else b = m;
+      }
+      return a;
+    };
+    const int a = first_ge(lo);
+    int b = first_ge(hi);
+    b = b < a ? a : b;
+    out[2 * sl] = a;
+    out[2 * sl + 1] = b;
+  }
+}
+
 }  // namespace
+
+void aligned_local_slots(const SellDev& S, int32_t* out, hipStream_t st) {
+  const int64_t ns = (S.n_rows + 63) / 64;
+  if (ns == 0) return;
+  MCG_CHECK(S.soffs && S.slice_ptr, "aligned_local_slots: not an aligned SELL matrix");
+  const int grid = (int)std::min<int64_t>((ns + kBS - 1) / kBS, 4096);
+  hipLaunchKernelGGL(k_aligned_local_slots, dim3(grid), dim3(kBS), 0, st, S, out);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(aligned_local_slots)");
+}
 
 void cg_split_update(double* x, double* r, const double* Ap, double* p_own, int64_t n, CgState* st, double tol,
                      int first, int check, int final_mode, double* partials, int pstride, int grid,
@@ -100,9 +170,27 @@ void cg_split_update(double* x, double* r, const double* Ap, double* p_own, int6
 template <typename IdxT>
 void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const double* p_ext, const double* r,
                    double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
-                   CgState* st, double tol, int first, int check, hipStream_t stream, const RedCtl& rc) {
+                   CgState* st, double tol, int first, int check, hipStream_t stream, const RedCtl& rc, int part) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
+  if (part != 0) {
+    MCG_CHECK(fmt == 6 && S.local_slots && S.soffs, "split SpMV halves: SELL-64/aligned with local slot runs only");
+#define MCG_P(U, R)                                                                                                   \
+  hipLaunchKernelGGL((k_split_spmv_aligned_part<U, R>), dim3(grid), dim3(kBS), 0, stream, S, p_ext, r, Ap, own_off, \
+                     tr, partials, pstride, st, tol, first, check, rc)
+    if (part == 1) {
+      if (param <= 4) MCG_P(4, false);
+      else if (param <= 6) MCG_P(6, false);
+      else MCG_P(8, false);
+    } else {
+      if (param <= 4) MCG_P(4, true);
+      else if (param <= 6) MCG_P(6, true);
+      else MCG_P(8, true);
+    }
+#undef MCG_P
+    MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+    return;
+  }
 #define MCG_S(F, U)                                                                                             \
   hipLaunchKernelGGL((k_split_spmv<F, IdxT, U>), dim3(grid), dim3(kBS), 0, stream, A, S, p_ext, r, Ap, own_off, tr, \
                      partials, pstride, st, tol, first, check, rc)
@@ -127,10 +215,10 @@ void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, 
 }
 template void cg_split_spmv<int32_t>(int, int, const CsrDev<int32_t>&, const SellDev&, const double*, const double*,
                                      double*, int64_t, const TileRanges&, double*, int, int, CgState*, double, int, int,
-                                     hipStream_t, const RedCtl&);
+                                     hipStream_t, const RedCtl&, int);
 template void cg_split_spmv<int64_t>(int, int, const CsrDev<int64_t>&, const SellDev&, const double*, const double*,
                                      double*, int64_t, const TileRanges&, double*, int, int, CgState*, double, int, int,
-                                     hipStream_t, const RedCtl&);
+                                     hipStream_t, const RedCtl&, int);
 
 }  // namespace kern
 }  // namespace mcg

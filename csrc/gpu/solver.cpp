@@ -348,6 +348,26 @@ void GpuCgSolver::setup() {
   }
   info_.pmat = pmat_;
   info_.allgather = L_.allgather;
+  // all-gather overlap: the own-block slots of each aligned slice are summed while p_k's all-gather
+  // is in flight (aligned_ is decided from the spec and the layout is the same kind on every rank,
+  // so every rank takes the same launches)
+  ag_overlap_ = aligned_ && pmat_ && use_halo_ && L_.allgather && opt_.overlap && opt_.ag_overlap != 0 && n > 0;
+  if (ag_overlap_) {
+    const int64_t ns = (n + 63) / 64;
+    lslots_.allocate(2 * ns, "A");
+    kern::aligned_local_slots(sell_view(), lslots_.get(), s0_);
+    std::vector<int32_t> ab(2 * ns);
+    std::vector<int64_t> sp(ns + 1);
+    MCG_HIP(hipMemcpyAsync(ab.data(), lslots_.get(), ab.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s0_),
+            "memcpy from device to host failed(A)");
+    MCG_HIP(hipMemcpyAsync(sp.data(), slice_ptr_.get(), sp.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s0_),
+            "memcpy from device to host failed(A)");
+    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    int64_t loc = 0;
+    for (int64_t s = 0; s < ns; ++s) loc += ab[2 * s + 1] - ab[2 * s];
+    info_.ag_local_frac = sp[ns] > 0 ? (double)(64 * loc) / (double)sp[ns] : 0.0;
+  }
+  info_.ag_overlap = ag_overlap_;
 
   // ---- vectors ----
   b_.allocate(n, "b", 8);
@@ -818,15 +838,14 @@ void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
   comm_->halo_exchange(L_, vecs, nv, s, w);
 }
 
-void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red) {
+void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red, int part) {
   const int first = (k == 0) ? 1 : 0;
   const int check = (k >= 2) ? 1 : 0;
   const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
   const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
-  double* part = partials_.get() + (which == 2 ? bnd_base_ : 0);
   if (grid == 0) return;
   kern::RedCtl rc;
-  if (fused_red) {
+  if (fused_red && part != 1) {  // the local half (part 1) writes no partials
     rc.cnt = red_cnt_.get();
     rc.lvl2 = red_l2_.get();
     rc.l2s = red_l2s_;
@@ -839,14 +858,15 @@ void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red) {
   const int64_t n = L_.n_local();
   const int fmt = opt_.format == 1 ? (aligned_ ? 6 : (c8_ ? 4 : (d16_ ? 3 : 1))) : (info_.spmv_variant == 2 ? 5 : 0);
   const SellDev S = sell_view();
+  double* pp = partials_.get() + (which == 2 ? bnd_base_ : 0);
   if (info_.idx64)
     kern::cg_split_spmv<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S,
-                                 p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, part, pstride_, grid, st_.get(),
-                                 opt_.tol, first, check, s0_, rc);
+                                 p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, pp, pstride_, grid, st_.get(),
+                                 opt_.tol, first, check, s0_, rc, part);
   else
     kern::cg_split_spmv<int32_t>(fmt, info_.spmv_param, CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, S,
-                                 p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, part, pstride_, grid, st_.get(),
-                                 opt_.tol, first, check, s0_, rc);
+                                 p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, pp, pstride_, grid, st_.get(),
+                                 opt_.tol, first, check, s0_, rc, part);
 }
 
 void GpuCgSolver::enqueue_iteration_split_(int k) {
@@ -867,6 +887,16 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
     enqueue_split_spmv_(k, 1, fr);  // interior rows || ghosts of p_k on the side stream
     MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
     enqueue_split_spmv_(k, 2, fr);
+    np = g_int_ + g_bnd_;
+  } else if (ag_overlap_) {
+    // all-gather of p_k on the side stream || the own-block slots of every row; then the rest
+    MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+    MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+    comm_->halo_exchange(L_, pv, 1, s1_);
+    MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+    enqueue_split_spmv_(k, 2, fr, 1);
+    MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+    enqueue_split_spmv_(k, 2, fr, 2);
     np = g_int_ + g_bnd_;
   } else {
     if (use_halo_) comm_->halo_exchange(L_, pv, 1, s0_);
@@ -1208,11 +1238,14 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
   trace::Range tr_("mcg.phase_profile");
   synchronize();
   halo_ready_for_ = -1;
-  if (pmat_) {  // split pass: update | ghosts of p | SpMV (+ in-kernel reduce) | all-reduce, serialised
-    Event q[5];
+  if (pmat_) {  // split pass: update | ghosts of p | [own-block SpMV half] | SpMV (+ in-kernel reduce) | all-reduce,
+                // serialised (with ag_overlap_ the own-block half runs before the all-gather here, so both
+                // halves and the all-gather are timed on their own)
+    Event q[6];
     for (Event& v : q) v = Event(true, true);
-    double acc[4] = {0, 0, 0, 0};
+    double acc[5] = {0, 0, 0, 0, 0};
     double* pv[1] = {p_[0].get()};
+    const bool fr = fused_red_ && red_groups_all_ > 0;
     for (int it = 0; it < iters; ++it) {
       const int k = k_;
       MCG_HIP(hipEventRecord(q[0].get(), s0_), "event record failed");
@@ -1221,25 +1254,27 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
       MCG_HIP(hipEventRecord(q[1].get(), s0_), "event record failed");
       if (use_halo_) comm_->halo_exchange(L_, pv, 1, s0_);
       MCG_HIP(hipEventRecord(q[2].get(), s0_), "event record failed");
-      enqueue_split_spmv_(k, 0, fused_red_ && red_groups_all_ > 0);
+      if (ag_overlap_) enqueue_split_spmv_(k, 0, false, 1);
+      MCG_HIP(hipEventRecord(q[3].get(), s0_), "event record failed");
+      enqueue_split_spmv_(k, 0, fr, ag_overlap_ ? 2 : 0);
       if (!fused_red_)
         kern::cg_reduce_f1(partials_.get(), pstride_, g_all_, st_.get(), 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol,
                            s0_);
-      MCG_HIP(hipEventRecord(q[3].get(), s0_), "event record failed");
-      if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
       MCG_HIP(hipEventRecord(q[4].get(), s0_), "event record failed");
+      if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
+      MCG_HIP(hipEventRecord(q[5].get(), s0_), "event record failed");
       synchronize();
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 5; ++j) {
         float t = 0.f;
         MCG_HIP(hipEventElapsedTime(&t, q[j].get(), q[j + 1].get()), "event elapsed failed");
         acc[j] += t;
       }
       ++k_;
     }
-    const char* nm[4] = {"update", "halo", "spmv", "allreduce"};
+    const char* nm[5] = {"update", "halo", "spmv_local", "spmv", "allreduce"};
     std::vector<std::pair<std::string, double>> out;
     double tot = 0;
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 5; ++j) {
       out.emplace_back(nm[j], iters > 0 ? 1e3 * acc[j] / iters : 0.0);
       tot += acc[j];
     }

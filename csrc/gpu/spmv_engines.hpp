@@ -331,6 +331,59 @@ __device__ __forceinline__ void sell(const SellDev& A, const TileRanges& sr, Gat
   }
 }
 
+// SELL-64/aligned, slots [j_begin, j_end) of the slice at `base` only, added to `sum`
+template <int U, bool NT, class Gather>
+__device__ __forceinline__ double aligned_run(const SellDev& A, int64_t base, int j_begin, int j_end, int32_t rowcol,
+                                              double sum, Gather&& gather) {
+  const int lane = threadIdx.x & 63;
+  const double* __restrict__ vp = A.vals + base + lane;
+  const int32_t* __restrict__ op = A.soffs + (base >> 6);
+  for (int j0 = j_begin; j0 < j_end; j0 += U) {
+    int32_t c[U];
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u < j_end ? j0 + u : j_end - 1;
+      const int64_t cc = (int64_t)rowcol + op[j];
+      c[u] = (int32_t)(cc < 0 ? 0 : (cc >= A.ext_len ? A.ext_len - 1 : cc));
+      v[u] = ld<NT>(vp + (int64_t)j * 64);
+    }
+    double g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) sum = (j0 + u < j_end) ? fma(v[u], g[u], sum) : sum;
+  }
+  return sum;
+}
+
+// SELL-64/aligned split by column ownership (the all-gather overlap): slots sort by offset, so the
+// slots whose 64 columns all lie in the rank's own block are one run [a, b) per slice
+// (SellDev::local_slots).  REMOTE = false sums that run (before the all-gather lands); REMOTE =
+// true the rest, [0, a) then [b, w).
+template <int U, bool NT, bool REMOTE, class Gather, class Epi>
+__device__ __forceinline__ void sell_aligned_part(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w_in_blk = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int2* __restrict__ ls = reinterpret_cast<const int2*>(A.local_slots);
+  for (TileCursor cur = tile_cursor(sr, w_in_blk, kWaves); cur.t < cur.end; cur.t += cur.step) {
+    const int64_t sl = tile_unit(sr, cur.t);
+    const int64_t base = A.slice_ptr[sl];
+    const int w = (int)((A.slice_ptr[sl + 1] - base) >> 6);
+    const int2 ab = ls[sl];
+    const int32_t rowcol = (int32_t)(A.own_off + sl * 64 + lane);
+    double sum = 0.0;
+    if constexpr (REMOTE) {
+      sum = aligned_run<U, NT>(A, base, 0, ab.x, rowcol, sum, gather);
+      sum = aligned_run<U, NT>(A, base, ab.y, w, rowcol, sum, gather);
+    } else {
+      sum = aligned_run<U, NT>(A, base, ab.x, ab.y, rowcol, sum, gather);
+    }
+    const int64_t i = sl * 64 + lane;
+    if (i < A.n_rows) epi(i, sum);
+  }
+}
+
 // SELL-64, two slices per wave iteration: two independent load -> gather chains
 // in flight per wave (memory-level parallelism without more waves).
 template <int U, bool NT, class Gather, class Epi>

@@ -75,6 +75,9 @@ struct CgOptions {
                              // the padded SELL slots by >= 10 %), 0 = off
   int sell_aligned = -1;     // wide random SPD: SELL-64/aligned (one column offset per slot shared by the slice's
                              // rows, values only; contiguous gathers); -1 = auto (expected fill <= 1.6), 0 = off
+  int ag_overlap = -1;       // SELL-64/aligned on an all-gather ghost layout: sum the own-block column slots while the
+                             // all-gather of p is in flight, the rest after it (two SpMV halves); -1 = auto (on
+                             // when the halo overlap is on), 0 = off
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

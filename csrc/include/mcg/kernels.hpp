@@ -106,6 +106,10 @@ struct SellDev {
   // slot's 64 gathers are one contiguous 512-B run and no per-entry column index is stored.
   const int32_t* soffs = nullptr;
   int64_t ext_len = 0;
+  // SELL-64/aligned with an all-gather ghost layout: per slice {a, b}, the run of slots whose 64
+  // columns all lie in the rank's own block (aligned_local_slots); the split pass sums them while
+  // the all-gather of p is in flight
+  const int32_t* local_slots = nullptr;
 };
 
 namespace kern {
@@ -143,6 +147,10 @@ void randspd_aligned_widths(const ProblemSpec& s, int64_t row_begin, int64_t n, 
                             hipStream_t st);
 void randspd_fill_aligned(const ProblemSpec& s, int64_t row_begin, int64_t n, const int64_t* rowptr64,
                           const int64_t* slice_ptr, int32_t* soffs, double* svals, hipStream_t st);
+// per slice of an aligned matrix (S.slice_ptr, S.soffs, S.own_off, S.n_rows): out[2s..2s+1] = the
+// slot run [a, b) whose columns own_off + 64 s + lane + offset lie in [own_off, own_off + n_rows)
+// for all 64 lanes
+void aligned_local_slots(const SellDev& S, int32_t* out, hipStream_t st);
 // SELL-64/c8 dictionary (csrc/gpu/dict.hip) from a generated SELL-64(/d16) matrix: false if
 // it has too many distinct values / offsets.  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
 bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
@@ -260,11 +268,14 @@ void cg_split_update(double* x, double* r, const double* Ap, double* p_own, int6
                      int first, int check, int final_mode, double* partials, int pstride, int grid,
                      hipStream_t stream);
 // fmt: 0 CSR thread-per-row (param U), 5 CSR-vector (param G lanes per row), 1 SELL-64, 3 SELL-64/d16,
-// 4 SELL-64/c8, 6 SELL-64/aligned
+// 4 SELL-64/c8, 6 SELL-64/aligned.  part (fmt 6 with S.local_slots): 0 every slot; 1 the local-column
+// slots only, Ap := that partial sum (no partials, no reduction); 2 the other slots, Ap += them, then
+// the epilogue / partials / reduction of part 0
 template <typename IdxT>
 void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, const double* p_ext, const double* r,
                    double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
-                   CgState* st, double tol, int first, int check, hipStream_t stream, const RedCtl& rc = RedCtl());
+                   CgState* st, double tol, int first, int check, hipStream_t stream, const RedCtl& rc = RedCtl(),
+                   int part = 0);
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),

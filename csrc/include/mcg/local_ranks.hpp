@@ -15,6 +15,8 @@ struct LocalRankResult {
   int64_t row_begin = 0;
   double true_rnorm = -1.0;
   bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)
+  bool ag_overlap = false;     // SolverInfo::ag_overlap (own-block SpMV half || all-gather)
+  double ag_local_frac = 0.0;  // SolverInfo::ag_local_frac
   std::vector<std::pair<std::string, double>> phases;  // phase_profile (mean us) when asked for
   std::string error;
 };

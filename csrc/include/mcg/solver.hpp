@@ -56,6 +56,8 @@ struct SolverInfo {
   int sigma = 0;              // SELL-C-sigma window (rows) of a user matrix; 0 = slices in row order
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
+  bool ag_overlap = false;    // the own-block SpMV half runs while the all-gather is in flight
+  double ag_local_frac = 0.0; // own-block slots / all slots (the part of the SpMV that hides the all-gather)
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
@@ -109,7 +111,7 @@ class GpuCgSolver {
   void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
   void enqueue_iteration_split_(int k);                   // materialized-p split pass (pmat_)
-  void enqueue_split_spmv_(int k, int which, bool fused_red);
+  void enqueue_split_spmv_(int k, int which, bool fused_red, int part = 0);  // part: cg_split_spmv
   void capture_pair_(int kind);
   void inject_fault_(int k);
   std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
@@ -147,6 +149,8 @@ class GpuCgSolver {
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
   DeviceBuffer<int32_t> soffs_;   // SELL-64/aligned per-slot column offsets
   bool aligned_ = false;
+  DeviceBuffer<int32_t> lslots_;  // SELL-64/aligned + all-gather: per slice the own-block slot run {a, b}
+  bool ag_overlap_ = false;
   int ndict_ = 0;
   bool c8_ = false;
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
@@ -167,6 +171,7 @@ class GpuCgSolver {
     s.perm = perm_.get();
     s.soffs = soffs_.get();
     s.ext_len = L_.ext_len;
+    s.local_slots = lslots_.get();
     return s;
   }
   // vectors

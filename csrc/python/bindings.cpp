@@ -210,6 +210,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("pmat", &CgOptions::pmat)
       .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
       .def_readwrite("sell_aligned", &CgOptions::sell_aligned)
+      .def_readwrite("ag_overlap", &CgOptions::ag_overlap)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -380,6 +381,8 @@ PYBIND11_MODULE(_C, m) {
         d["sigma"] = i.sigma;
         d["sell_fill"] = i.sell_fill;
         d["allgather"] = i.allgather;
+        d["ag_overlap"] = i.ag_overlap;
+        d["ag_local_frac"] = i.ag_local_frac;
         d["graph_fallbacks"] = i.graph_fallbacks;
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;
@@ -413,6 +416,8 @@ PYBIND11_MODULE(_C, m) {
       d["row_begin"] = rr.row_begin;
       d["true_rnorm"] = rr.true_rnorm;
       d["carry"] = rr.carry;
+      d["ag_overlap"] = rr.ag_overlap;
+      d["ag_local_frac"] = rr.ag_local_frac;
       py::dict ph;
       for (auto& kv : rr.phases) ph[py::str(kv.first)] = kv.second;
       d["phases"] = ph;

@@ -136,3 +136,37 @@ def test_aligned_sell_local_ranks_all_gather(mcg, world):
     assert abs(out["ranks"][0]["iterations"] - cpu["iterations"]) <= 1
     np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
     assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_all_gather_overlap_halves_match(mcg, world):
+    """SELL-64/aligned on the all-gather layout: the own-block slots are summed while the all-gather
+    of p is in flight, the rest after it (ag_overlap).  Same iterations and x as the one-pass SpMV
+    and the CPU oracle; about 1/P of the slots are own-block for a matrix spread over all rows."""
+    spec = mcg.make_problem("randspd", **DENSE_WIDE)
+    C = mcg.native()
+    cpu = _cpu(mcg, spec)
+    outs = []
+    for ag in (1, 0):
+        o = C.CgOptions(format="sell", recurrence=1, check_every=4)
+        o.ag_overlap = ag
+        outs.append(C.run_local_ranks(spec.native(), o, world, 0, True))
+    on, off = outs
+    assert all(r["ag_overlap"] for r in on["ranks"]) and not any(r["ag_overlap"] for r in off["ranks"])
+    frac = np.mean([r["ag_local_frac"] for r in on["ranks"]])
+    assert 0.3 / world < frac < 2.0 / world
+    assert len({r["iterations"] for r in on["ranks"]}) == 1
+    assert abs(on["ranks"][0]["iterations"] - off["ranks"][0]["iterations"]) <= 1
+    np.testing.assert_allclose(on["x"], off["x"], rtol=1e-10, atol=1e-12 * np.abs(off["x"]).max())
+    np.testing.assert_allclose(on["x"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in on["ranks"])
+
+
+def test_all_gather_overlap_phase_profile(mcg):
+    """phase_profile of the split pass with the halves: both SpMV halves are timed."""
+    spec = mcg.make_problem("randspd", **DENSE_WIDE)
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sell", recurrence=1)
+    out = C.run_local_ranks(spec.native(), o, 4, 8, False, 4)
+    ph = out["ranks"][0]["phases"]
+    assert ph["spmv_local"] > 0 and ph["spmv"] > 0 and ph["halo"] >= 0
