@@ -544,6 +544,7 @@ void GpuCgSolver::setup() {
 
 // true iff `mine` is true on every rank (one all-reduce of a flag at setup; not in the loop)
 bool GpuCgSolver::all_ranks_agree_(bool mine) {
+  if (!comm_->moves_data()) return mine;
   DeviceBuffer<double> f(1, "state");
   const double v = mine ? 1.0 : 0.0;
   MCG_HIP(hipMemcpyAsync(f.get(), &v, sizeof(double), hipMemcpyHostToDevice, s0_), "memcpy from host to device failed");

@@ -56,6 +56,8 @@ class Communicator {
   virtual void check_async() {}
   // whether the solver may capture this communicator's calls into a hipGraph
   virtual bool graph_capturable() const { return true; }
+  // false for NullComm (per-rank timing rehearsal): setup-time agreements take this rank's own value
+  virtual bool moves_data() const { return true; }
   // tear down outstanding collectives after a fatal error (watchdog)
   virtual void abort() {}
 };
@@ -101,6 +103,7 @@ class NullComm final : public Communicator {
   int world() const override { return world_; }
   void allreduce_sum(double*, size_t, hipStream_t) override {}
   void halo_exchange(const LocalLayout&, double* const*, int, hipStream_t, const int* = nullptr) override {}
+  bool moves_data() const override { return false; }
 
  private:
   int rank_, world_;

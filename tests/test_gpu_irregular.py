@@ -170,3 +170,19 @@ def test_all_gather_overlap_phase_profile(mcg):
     out = C.run_local_ranks(spec.native(), o, 4, 8, False, 4)
     ph = out["ranks"][0]["phases"]
     assert ph["spmv_local"] > 0 and ph["spmv"] > 0 and ph["halo"] >= 0
+
+
+def test_null_comm_rank_share_takes_the_split_pass(mcg):
+    """Per-rank timing rehearsal (NullComm) of the wide family: the setup-time agreement on the pass
+    form takes the rank's own choice, so rank 3 of 8 runs aligned SELL, the split pass and the
+    all-gather halves like a real 8-rank job."""
+    spec = mcg.make_problem("randspd", **DENSE_WIDE)
+    C = mcg.native()
+    comm = C.NullComm(3, 8)
+    s = C.Solver(spec.native(), C.CgOptions(format="sell", recurrence=1), 3, 8, comm)
+    s.setup()
+    info = s.info()
+    assert info["pmat"] and info["allgather"] and info["ag_overlap"] and info["format"] == "sell64-aligned"
+    s.reset()
+    s.run_iterations(6)
+    s.synchronize()
