@@ -143,6 +143,13 @@ def recipes(a) -> dict:
                                         f"--phases 2 --set ag_overlap={ag}"))
             for ag in (1, 0)
         ],
+        # does a halo collective find CUs while the (fully resident) carry pass runs?
+        "corun": [
+            ("graph", 180, f"{PY} bench/corun_probe.py"),
+            ("eager", 180, f"{PY} bench/corun_probe.py --graph 0"),
+            ("b3", 180, f"{PY} bench/corun_probe.py --set carry_blocks_per_cu=3"),
+            ("generic", 180, f"{PY} bench/corun_probe.py --set carry=0"),
+        ],
         # line-carry geometry at a P = 8 rank's share (2046 interior lines of 16384^2)
         "carrysweep": [
             (f"b{b}_d{d}", 200, bench(f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 --no-verify "

@@ -181,7 +181,7 @@ def test_null_comm_rank_share_takes_the_split_pass(mcg):
     comm = C.NullComm(3, 8)
     s = C.Solver(spec.native(), C.CgOptions(format="sell", recurrence=1), 3, 8, comm)
     s.setup()
-    info = s.info()
+    info = s.info
     assert info["pmat"] and info["allgather"] and info["ag_overlap"] and info["format"] == "sell64-aligned"
     s.reset()
     s.run_iterations(6)
