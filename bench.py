@@ -73,6 +73,9 @@ def parse_args(argv=None):
                     help="timing rehearsal: run rank --sim-rank of a P-rank job alone on this GPU (its rows, "
                          "ghost layout, interior/boundary launches, graphs) with collectives that move nothing")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--watchdog", type=float, default=600.0,
+                    help="seconds a host wait may go without progress before the run fails and RCCL is aborted "
+                         "(a hung collective ends the job with a message instead of hanging; 0 = unbounded)")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank(s) as child processes even for --gpus 1 (the --gpus N > 1 launch route)")
     return ap.parse_args(argv)
@@ -140,6 +143,7 @@ def _run_rank(args, out_fd) -> int:
     opts = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=not args.no_overlap,
                        use_graph=use_graph, force_comm=args.force_comm, format=args.format,
                        blocks_per_cu=args.blocks_per_cu, recurrence=args.recurrence)
+    opts.watchdog_seconds = args.watchdog
     for kv in args.set:
         k, v = kv.split("=", 1)
         if not hasattr(opts, k):
@@ -244,7 +248,8 @@ def _run_rank(args, out_fd) -> int:
                          else "windowed" if info.get("window") else "generic, xcd-aware" if info.get("xcd_map")
                          else "generic"),
                 "ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
-                if info.get("allgather") else "window",
+                if info.get("allgather") else ("window, exchanged ahead || all-reduce" if info.get("halo_ahead")
+                                               else "window"),
                 "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,

@@ -150,6 +150,25 @@ def recipes(a) -> dict:
             ("b3", 180, f"{PY} bench/corun_probe.py --set carry_blocks_per_cu=3"),
             ("generic", 180, f"{PY} bench/corun_probe.py --set carry=0"),
         ],
+        # CUs withheld from the compute stream (CU-masked queue) so the collective finds room; the
+        # pass time with the mask (full grid and a P = 8 rank's share) is the price
+        # halo exchanged ahead (next to the all-reduce, one full pass) vs interior || halo + boundary
+        "haloahead": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_multirank.py -k 'halo_ahead'"),
+        ] + [
+            (f"sim{P}_{pr}_ha{ha}", 200, bench(f"{'--problem poisson3d --grid 512 ' if pr == '3d' else ''}"
+                                              f"--sim-world {P} --sim-rank {r} --steps 400 --warmup 40 --phases 10 "
+                                              f"--set halo_ahead={ha}"))
+            for P, r, pr in ((8, 3, "2d"), (4, 1, "2d"), (8, 3, "3d")) for ha in (1, 0)
+        ],
+        # does the pass leave room for RCCL's kernels?  (CU-masked compute queue: negative result,
+        # profiles/r2_corun_probe.md)
+        "corun2": [
+            ("graph", 180, f"{PY} bench/corun_probe.py"),
+            ("eager", 180, f"{PY} bench/corun_probe.py --graph 0"),
+            ("generic", 180, f"{PY} bench/corun_probe.py --set carry=0"),
+            ("m16", 180, f"{PY} bench/corun_probe.py --set comm_cus=16"),
+        ],
         # line-carry geometry at a P = 8 rank's share (2046 interior lines of 16384^2)
         "carrysweep": [
             (f"b{b}_d{d}", 200, bench(f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 --no-verify "

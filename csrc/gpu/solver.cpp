@@ -107,7 +107,25 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only (and not for
   // the split pass, whose ghosts come from its own update kernel; decided in setup())
   prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph && !L_.allgather;
-  s0_ = Stream(true, 0);
+  // Compute stream, optionally on a CU-masked queue that keeps a few CUs free for the side stream's
+  // RCCL kernels.  Measured: the mask slows the pass by 20-33 % and the collective still waits for
+  // the pass (bench/corun_probe.py, profiles/r2_corun_probe.md), so it is off unless asked for.
+  const int all_cus = kern::num_cus();
+  info_.comm_cus = std::max(0, opt_.comm_cus);
+  MCG_CHECK(info_.comm_cus >= 0 && info_.comm_cus < all_cus / 2, "comm_cus must leave at least half the CUs");
+  ncu_ = all_cus - info_.comm_cus;
+  if (info_.comm_cus > 0) {
+    std::vector<uint32_t> mask((all_cus + 31) / 32, 0u);
+    for (int c = 0; c < all_cus; ++c) mask[c / 32] |= 1u << (c % 32);
+    const int w = info_.comm_cus, grp = all_cus / w;
+    for (int j = 0; j < w; ++j) {
+      const int c = opt_.cu_mask_pattern == 1 ? all_cus - 1 - j : j * grp + grp - 1;
+      mask[c / 32] &= ~(1u << (c % 32));
+    }
+    s0_ = Stream::with_cu_mask(mask);
+  } else {
+    s0_ = Stream(true, 0);
+  }
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);
   ev_h_ = Event(true);
@@ -115,6 +133,8 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   ev_t1_ = Event(true, true);
   ev_poll_[0] = Event(true);
   ev_poll_[1] = Event(true);
+  ev_sync_[0] = Event(true);
+  ev_sync_[1] = Event(true);
   host_st_ = PinnedBuffer<CgState>(2);
 }
 
@@ -348,6 +368,10 @@ void GpuCgSolver::setup() {
   }
   info_.pmat = pmat_;
   info_.allgather = L_.allgather;
+  halo_ahead_ = opt_.halo_ahead != 0 && use_halo_ && opt_.overlap && !pmat_ && !L_.allgather && opt_.recurrence == 1;
+  if (halo_ahead_) prefetch_halo_ = false;
+  info_.halo_ahead = halo_ahead_;
+  split_ = use_halo_ && opt_.overlap && !halo_ahead_;
   // all-gather overlap: the own-block slots of each aligned slice are summed while p_k's all-gather
   // is in flight (aligned_ is decided from the spec and the layout is the same kind on every rank,
   // so every rank takes the same launches)
@@ -391,7 +415,7 @@ void GpuCgSolver::setup() {
     if (t.ntiles == 0) return 0;
     if (win_doubles_ > 0) {  // 1024-thread chunk blocks: 2 per CU while the window fits half the LDS
       const int per_cu = win_doubles_ * 8 <= 75 * 1024 ? 2 : 1;
-      return (int)std::max<int64_t>(1, std::min<int64_t>(kern::win_chunks(t), (int64_t)kern::num_cus() * per_cu));
+      return (int)std::max<int64_t>(1, std::min<int64_t>(kern::win_chunks(t), (int64_t)ncu_ * per_cu));
     }
     if (opt_.format == 1) return kern::grid_for(t.ntiles * 64, 256, bpc);
     if (info_.spmv_variant == 0)  // LDS-limited residency
@@ -406,7 +430,7 @@ void GpuCgSolver::setup() {
   };
   tr_all_ = ranges(0, n, 0, 0);
   g_all_ = grid_a(tr_all_);
-  if (use_halo_ && opt_.overlap) {
+  if (split_) {
     int64_t ib = L_.interior_begin, ie = L_.interior_end;
     if (opt_.format == 1) {  // interior launch takes only whole slices inside the interior
       const int64_t sb = (ib + 63) / 64, se = ie / 64;
@@ -433,7 +457,7 @@ void GpuCgSolver::setup() {
     // wave's previous / next slice and hit the L2 (512^3: 400 vs 312 it/s,
     // profiles/sweep_xcd_3d.log).  Speed only: every slice is still visited once.
     const int64_t P = partition_granule(spec_) / 64;
-    const int64_t cus = kern::num_cus();
+    const int64_t cus = ncu_;
     int64_t g = std::min<int64_t>(std::max<int64_t>(2 * P, cus * 4), cus * 64) / 8 * 8;
     auto apply = [&](TileRanges& t, int& grid) {
       if (t.ntiles == 0 || g < 8) return;
@@ -441,7 +465,7 @@ void GpuCgSolver::setup() {
       grid = (int)g;
     };
     apply(tr_all_, g_all_);
-    if (use_halo_ && opt_.overlap) apply(tr_int_, g_int_);
+    if (split_) apply(tr_int_, g_int_);
     info_.xcd_map = true;
   }
   if (opt_.xcd_map > 0) info_.xcd_map = true;
@@ -468,7 +492,7 @@ void GpuCgSolver::setup() {
               "line-carry pass needs SELL d16/c8, interleaved pairs, rows <= param <= 8 and whole 64-row grid lines");
     if (ok && opt_.carry != 0) {
       const int64_t S = gl / 64;
-      const int g = kern::num_cus() * std::max(1, opt_.carry_blocks_per_cu);
+      const int g = ncu_ * std::max(1, opt_.carry_blocks_per_cu);
       auto apply = [&](TileRanges& t, int& grid) {
         if (t.ntiles == 0 || t.nt0 != t.ntiles || t.b0 % S != 0 || t.nt0 % S != 0 || t.nt0 / S < 2) return false;
         t.strip = (int32_t)S;
@@ -487,7 +511,7 @@ void GpuCgSolver::setup() {
       // auto: only the specialised pass (2-D stencils); with the slow path (3-D's +-N gathers) it
       // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log)
       if (opt_.carry == 1 || !carry_general_) carry_all_ = apply(tr_all_, g_all_);
-      if (use_halo_ && opt_.overlap && (opt_.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
+      if (split_ && (opt_.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
     }
     info_.carry = carry_all_ || carry_int_;
     info_.carry_xchg = info_.carry && carry_lo2_ > 0 && opt_.carry_3d == 2 &&
@@ -498,7 +522,7 @@ void GpuCgSolver::setup() {
   g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
-  const bool split = use_halo_ && opt_.overlap;
+  const bool split = split_;
   fused_red_ = opt_.recurrence == 1 && opt_.fused_reduce != 0;
   auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
   // the boundary launch's partials start on a reduction-group boundary: round the interior grid up
@@ -731,9 +755,11 @@ void GpuCgSolver::reset() {
     }
     opt_.tol = tol;
   }
+  join_halo_();
   k_ = 0;
   finalized_ = false;
   halo_ready_for_ = -1;
+  ghosts_for_ = -1;
 }
 
 void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
@@ -918,7 +944,18 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
   trace::Range tr_("mcg.iteration.single_reduction");
   int np = g_all_;
   const bool fr = fused_red_;
-  if (use_halo_ && opt_.overlap) {
+  if (halo_ahead_) {
+    ensure_ghosts_(k);
+    enqueue_f1_(k, 0, 0, fr);  // every owned row in one pass (the line-carry pass at P > 1 too)
+    // the next iteration's ghosts are this pass's outputs, final now: exchange them on the side
+    // stream while the all-reduce runs (the join sits in front of the next pass)
+    MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+    MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+    enqueue_halo_f1_(k + 1, s1_);
+    MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+    ghosts_for_ = k + 1;
+    halo_pending_ = true;
+  } else if (use_halo_ && opt_.overlap) {
     if (halo_ready_for_ != k) {
       MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
       MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
@@ -986,6 +1023,20 @@ void GpuCgSolver::enqueue_iteration_(int k) {
   if (use_comm_) comm_->allreduce_sum(&st->rr_new, 1, s0_);
 }
 
+void GpuCgSolver::join_halo_() {
+  if (!halo_pending_) return;
+  MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+  halo_pending_ = false;
+}
+
+void GpuCgSolver::ensure_ghosts_(int k) {
+  const bool have = ghosts_for_ == k;
+  join_halo_();
+  if (have) return;
+  enqueue_halo_f1_(k, s0_);  // not prefetched (first iteration, after a reset / resume / profile)
+  ghosts_for_ = k;
+}
+
 void GpuCgSolver::drop_graphs_() {
   for (int g = 0; g < 2; ++g) {
     if (graph_exec_[g]) (void)hipGraphExecDestroy(graph_exec_[g]);
@@ -1000,15 +1051,23 @@ void GpuCgSolver::drop_graphs_() {
 void GpuCgSolver::capture_pair_(int kind) {
   hipStream_t s = s0_;
   const int iters = kind == 0 ? 2 : opt_.graph_iters;
+  // halo_ahead: a graph starts with its ghosts in place (joined before the launch) and ends by
+  // joining the prefetch of its last iteration, so every replay sees the same host-side state
+  if (halo_ahead_) ensure_ghosts_(k_);
   MCG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "graph capture failed");
   try {
     for (int j = 0; j < iters; ++j) enqueue_iteration_(k_ + j);
+    join_halo_();
   } catch (...) {
     hipGraph_t g = nullptr;
     (void)hipStreamEndCapture(s, &g);
     if (g) (void)hipGraphDestroy(g);
+    ghosts_for_ = -1;
+    halo_pending_ = false;
     throw;
   }
+  ghosts_for_ = halo_ahead_ ? k_ : -1;  // nothing captured has run yet
+  halo_pending_ = false;
   MCG_HIP(hipStreamEndCapture(s, &graph_[kind]), "graph capture failed");
   MCG_HIP(hipGraphInstantiate(&graph_exec_[kind], graph_[kind], nullptr, nullptr, 0), "graph instantiate failed");
 }
@@ -1031,6 +1090,7 @@ void GpuCgSolver::run_iterations(int count) {
           continue;
         }
       }
+      if (halo_ahead_) ensure_ghosts_(k_);
       const hipError_t le = (k_ == opt_.fail_graph_launch_at) ? hipErrorInvalidValue  // test hook
                                                               : hipGraphLaunch(graph_exec_[kind], s0_);
       if (le != hipSuccess) {
@@ -1051,6 +1111,7 @@ void GpuCgSolver::run_iterations(int count) {
       const int done = kind == 0 ? 2 : glong;
       k_ += done;
       count -= done;
+      if (halo_ahead_) ghosts_for_ = k_;  // prefetched by the graph's last iteration and joined
     } else {
       if (k_ == opt_.inject_nan_at) inject_fault_(k_);
       enqueue_iteration_(k_);
@@ -1076,6 +1137,7 @@ void GpuCgSolver::inject_fault_(int k) {
 void GpuCgSolver::finalize() {
   if (k_ == 0 || finalized_) return;
   finalized_ = true;  // the single-reduction catch-up of a pending x term must run once
+  join_halo_();
   if (pmat_) {  // U in final mode: r_m, x_m and ||r_m||^2, then latch
     kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, L_.n_local(), st_.get(), opt_.tol,
                           0, k_ >= 2 ? 1 : 0, 1, partials_.get(), pstride_, g_b_, s0_);
@@ -1096,7 +1158,16 @@ void GpuCgSolver::finalize() {
   kern::cg_reduce(partials_.get(), 0, st_.get(), kReduceFinal, 0, opt_.tol, s0_);
 }
 
+// Drain both streams.  With a watchdog the wait is bounded like the solve's polls: a collective
+// whose peer never arrives (a dead or diverged rank in a multi-GPU bench) ends in an error that
+// names the stall, and the communicator is aborted, instead of a silent hang.
 void GpuCgSolver::synchronize() {
+  if (opt_.watchdog_seconds > 0) {
+    MCG_HIP(hipEventRecord(ev_sync_[1], s1_), "event record failed");
+    MCG_HIP(hipEventRecord(ev_sync_[0], s0_), "event record failed");
+    wait_bounded_(ev_sync_[1]);
+    wait_bounded_(ev_sync_[0]);
+  }
   MCG_HIP(hipStreamSynchronize(s1_), "device synchronize failed");
   MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
   if (use_comm_) comm_->check_async();
@@ -1231,6 +1302,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   k_ = (int)h.k;
   finalized_ = false;
   halo_ready_for_ = -1;
+  ghosts_for_ = -1;
 }
 
 std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters) {
@@ -1238,7 +1310,9 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
   MCG_CHECK(opt_.recurrence == 1, "phase_profile: single-reduction form only");
   trace::Range tr_("mcg.phase_profile");
   synchronize();
+  join_halo_();
   halo_ready_for_ = -1;
+  ghosts_for_ = -1;
   if (pmat_) {  // split pass: update | ghosts of p | [own-block SpMV half] | SpMV (+ in-kernel reduce) | all-reduce,
                 // serialised (with ag_overlap_ the own-block half runs before the all-gather here, so both
                 // halves and the all-gather are timed on their own)
@@ -1293,7 +1367,7 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
     MCG_HIP(hipEventElapsedTime(&t, a.get(), b.get()), "event elapsed failed");
     return (double)t;
   };
-  const bool split = use_halo_ && opt_.overlap;
+  const bool split = split_;
   for (int it = 0; it < iters; ++it) {
     const int k = k_;
     MCG_HIP(hipEventRecord(e[0].get(), s0_), "event record failed");
@@ -1308,7 +1382,9 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
       MCG_HIP(hipEventRecord(e[2].get(), s0_), "event record failed");
       enqueue_f1_(k, 2, 0);
     } else {
-      if (use_halo_) enqueue_halo_f1_(k, s0_);
+      MCG_HIP(hipEventRecord(h[0].get(), s0_), "event record failed");
+      if (use_halo_) enqueue_halo_f1_(k, s0_);  // serialised here, so it is timed on its own
+      MCG_HIP(hipEventRecord(h[1].get(), s0_), "event record failed");
       enqueue_f1_(k, 0, 0);
       MCG_HIP(hipEventRecord(e[1].get(), s0_), "event record failed");
       MCG_HIP(hipEventRecord(e[2].get(), s0_), "event record failed");
@@ -1320,8 +1396,8 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
     if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
     MCG_HIP(hipEventRecord(e[5].get(), s0_), "event record failed");
     synchronize();
-    acc[0] += ms(e[0], e[1]);
-    acc[1] += split ? ms(h[0], h[1]) : 0.0;
+    acc[0] += split ? ms(e[0], e[1]) : ms(h[1], e[1]);
+    acc[1] += ms(h[0], h[1]);
     acc[2] += ms(e[1], e[2]);
     acc[3] += ms(e[2], e[3]);
     acc[4] += ms(e[3], e[4]);

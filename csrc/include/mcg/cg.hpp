@@ -81,6 +81,16 @@ struct CgOptions {
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
+  int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
+                             // right after pass k wrote it (side stream, next to the all-reduce) and run one
+                             // full pass per iteration instead of interior || halo then boundary.  RCCL's
+                             // kernels cannot start next to a resident pass (profiles/r2_corun_probe.md), so
+                             // the split never overlapped; -1 = auto (on when the halo overlap is on), 0 = off
+  int comm_cus = 0;          // experiment: CUs withheld from the compute stream (CU-masked queue) so RCCL's
+                             // halo / all-gather kernels on the side stream find room next to the resident
+                             // pass; measured slower and without effect (profiles/r2_corun_probe.md), 0 = off
+  int cu_mask_pattern = 0;   // which CUs comm_cus withholds: 0 = the last CU of each of comm_cus equal groups of
+                             // the mask bits, 1 = the last comm_cus bits
   int fail_graph_launch_at = -1;  // test hook: report the graph launch at this iteration as failed (nothing enqueued)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")

@@ -11,6 +11,7 @@
 #include <cstddef>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "mcg/check.hpp"
 
@@ -113,6 +114,12 @@ class Stream {
   explicit Stream(bool create, int priority = 0) {
     if (create)
       MCG_HIP(hipStreamCreateWithPriority(&s_, hipStreamNonBlocking, priority), "stream create failed");
+  }
+  // a stream whose kernels run only on the CUs set in `mask` (32 CUs per word)
+  static Stream with_cu_mask(const std::vector<uint32_t>& mask) {
+    Stream st;
+    MCG_HIP(hipExtStreamCreateWithCUMask(&st.s_, (uint32_t)mask.size(), mask.data()), "stream create failed");
+    return st;
   }
   ~Stream() {
     if (s_) (void)hipStreamDestroy(s_);

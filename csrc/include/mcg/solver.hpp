@@ -57,8 +57,11 @@ struct SolverInfo {
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
   bool ag_overlap = false;    // the own-block SpMV half runs while the all-gather is in flight
+  bool halo_ahead = false;    // multi-rank stencil halo exchanged right after the pass that produced it, next to
+                              // the all-reduce; one full pass per iteration (CgOptions::halo_ahead)
   double ag_local_frac = 0.0; // own-block slots / all slots (the part of the SpMV that hides the all-gather)
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
+  int comm_cus = 0;           // CUs withheld from the compute stream for the side stream's RCCL kernels
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
@@ -113,6 +116,8 @@ class GpuCgSolver {
   void enqueue_iteration_split_(int k);                   // materialized-p split pass (pmat_)
   void enqueue_split_spmv_(int k, int which, bool fused_red, int part = 0);  // part: cg_split_spmv
   void capture_pair_(int kind);
+  void join_halo_();            // s0_ waits for a halo in flight on s1_
+  void ensure_ghosts_(int k);   // ghosts of iteration k in place on s0_ (joins a prefetch or exchanges now)
   void inject_fault_(int k);
   std::vector<DeviceBuffer<double>*> vectors_();  // the per-pass vector streams (x, r / Ap / pairs, p)
   void allocate_vectors_();
@@ -132,9 +137,14 @@ class GpuCgSolver {
   bool finalized_ = false;
   bool prefetch_halo_ = false;  // single-reduction form: next iteration's halo right after the boundary pass
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
+  bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
+  bool split_ = false;          // interior / boundary launches around an overlapped halo
+  int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
+  bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them
 
   Stream s0_, s1_;
-  Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2];
+  int ncu_ = 0;  // CUs the compute stream may use (all, minus CgOptions::comm_cus)
+  Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2], ev_sync_[2];
   // matrix
   DeviceBuffer<int32_t> rp32_;
   DeviceBuffer<int64_t> rp64_;

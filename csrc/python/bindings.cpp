@@ -192,6 +192,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("spmv_param") = 0, py::arg("update_unroll") = 1, py::arg("nt_loads") = 0,
            py::arg("xcd_map") = -1, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
+      .def_readwrite("comm_cus", &CgOptions::comm_cus)
+      .def_readwrite("cu_mask_pattern", &CgOptions::cu_mask_pattern)
       .def_readwrite("interleave", &CgOptions::interleave)
       .def_readwrite("window", &CgOptions::window)
       .def_readwrite("pipeline", &CgOptions::pipeline)
@@ -211,6 +213,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
       .def_readwrite("sell_aligned", &CgOptions::sell_aligned)
       .def_readwrite("ag_overlap", &CgOptions::ag_overlap)
+      .def_readwrite("halo_ahead", &CgOptions::halo_ahead)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -382,8 +385,10 @@ PYBIND11_MODULE(_C, m) {
         d["sell_fill"] = i.sell_fill;
         d["allgather"] = i.allgather;
         d["ag_overlap"] = i.ag_overlap;
+        d["halo_ahead"] = i.halo_ahead;
         d["ag_local_frac"] = i.ag_local_frac;
         d["graph_fallbacks"] = i.graph_fallbacks;
+        d["comm_cus"] = i.comm_cus;
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;
         d["carry_xchg"] = i.carry_xchg;

@@ -147,3 +147,53 @@ def test_local_ranks_plane_carry_interior(mcg, world):
     assert [r["iterations"] for r in outs[0]["ranks"]] == [r["iterations"] for r in outs[1]["ranks"]]
     np.testing.assert_allclose(outs[0]["x"], outs[1]["x"], rtol=1e-10, atol=1e-13)
     assert all(r["converged"] and r["true_rnorm"] < 1e-6 for r in outs[0]["ranks"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("problem,n", [("poisson2d", 256), ("poisson3d", 32)])
+def test_local_ranks_halo_ahead_matches_split(mcg, world, problem, n):
+    """halo_ahead (ghosts of iteration k+1 exchanged right after pass k, one full pass per
+    iteration) against the interior || halo + boundary split and P = 1: same recurrence, so the
+    residuals agree to rounding of the differently grouped partial sums."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    C = mcg.native()
+    outs = {}
+    for ha in (1, 0):
+        o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
+        o.halo_ahead = ha
+        outs[ha] = C.run_local_ranks(spec.native(), o, world, 60, True)
+    one = C.run_local_ranks(spec.native(), _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1),
+                            1, 60, True)
+    r = one["ranks"][0]["rnorm"]
+    for ha, out in outs.items():
+        assert all(q["iterations"] == 60 for q in out["ranks"]), ha
+        assert abs(out["ranks"][0]["rnorm"] - r) <= 1e-11 * r, ha
+        np.testing.assert_allclose(out["x"], one["x"], rtol=1e-10, atol=1e-13)
+        assert all(abs(q["true_rnorm"] - q["rnorm"]) <= 1e-8 * q["true_rnorm"] for q in out["ranks"])
+    if problem == "poisson2d":  # the full pass of every rank is the line-carry pass
+        assert all(q["carry"] for q in outs[1]["ranks"])
+
+
+@pytest.mark.parametrize("problem,n", [("poisson2d", 512), ("poisson3d", 64)])
+def test_null_comm_halo_ahead_graph_equals_eager(mcg, problem, n):
+    """A P = 8 rank's share with collectives that move nothing (NullComm): the captured graphs
+    (prefetch fork + join per iteration, the last one joined inside the graph) run exactly the
+    eager iterations, bit for bit, with no capture fallback."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    C = mcg.native()
+    xs, infos = [], []
+    for graph in (True, False):
+        o = C.CgOptions(tol=-1.0, maxit=1 << 30, check_every=1 << 30, format="sellc8", recurrence=1)
+        o.use_graph = graph
+        s = C.Solver(spec.native(), o, 3, 8, C.NullComm(3, 8))
+        s.setup()
+        s.reset()
+        s.run_iterations(5)   # eager start, then graphs from an even k
+        s.run_iterations(70)  # 32-iteration graphs + pair tail
+        s.synchronize()
+        s.finalize()
+        xs.append(s.x_local())
+        infos.append(dict(s.info, **s.result()))
+    assert infos[0]["halo_ahead"] and infos[0]["graph_fallbacks"] == 0
+    assert infos[0]["iterations"] == infos[1]["iterations"] == 75
+    np.testing.assert_array_equal(xs[0], xs[1])
