@@ -152,6 +152,44 @@ def recipes(a) -> dict:
         ],
         # CUs withheld from the compute stream (CU-masked queue) so the collective finds room; the
         # pass time with the mask (full grid and a P = 8 rank's share) is the price
+        # Ap recomputed by the line-carry pass instead of stored as {r, Ap} pairs
+        "apr": [
+            ("pytest", 900, f"{PYTEST} tests -m gpu"),
+        ] + [
+            (f"b{i}_ar{ar}", 200, bench(f"--set ap_recompute={ar}")) for i, ar in enumerate((-1, 0, -1, 0))
+        ] + [
+            ("b4096_ar", 200, bench("--grid 4096 --steps 2000 --warmup 100")),
+            ("b4096_st", 200, bench("--grid 4096 --steps 2000 --warmup 100 --set ap_recompute=0")),
+            ("sim8_ar", 200, bench("--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 10")),
+            ("sim8_st", 200, bench("--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 10 "
+                                   "--set ap_recompute=0")),
+        ],
+        # quick A/B of the Ap-recomputing carry (numerics tests + 16384^2 / 4096^2 / P = 8 share)
+        "arquick": [
+            ("pytest", 300, f"{PYTEST} tests/test_gpu_solver.py tests/test_gpu_multirank.py -k 'ap_recompute or halo_ahead'"),
+        ] + [
+            (f"{nm}_{g}", 200, bench(f"{'--grid 4096 --steps 2000 --warmup 100 ' if g == 4096 else ''}--phases 0 "
+                                     f"{arg}"))
+            for g in (16384, 4096)
+            for nm, arg in (("ar_d2", "--set carry_depth=2"), ("ar_d3", "--set carry_depth=3"),
+                            ("st", "--set ap_recompute=0"), ("ar_d3b", "--set carry_depth=3"))
+        ],
+        # Ap-recomputing carry: prefetch depth x blocks per CU (16384^2 and 4096^2)
+        "arsweep": [
+            (f"d{d}_b{b}_{g}", 200, bench(f"{'--grid 4096 --steps 2000 --warmup 100 ' if g == 4096 else ''}"
+                                        f"--phases 0 --no-verify --set carry_depth={d} --set carry_blocks_per_cu={b}"))
+            for g in (16384, 4096) for d in (2, 3, 4, 5) for b in (4, 3)
+        ],
+        # issue-side counters of the Ap-recomputing vs the storing carry pass (16384^2)
+        "arpmc": [
+            (f"{tag}_{nm}", 120, prof(f"arpmc_{tag}_{nm}", f"{PY} {ROOT}/bench.py --steps 8 --warmup 2 --phases 0 "
+                                                         f"--no-verify --set ap_recompute={ar}", cnt))
+            for tag, ar in (("ar", -1), ("st", 0))
+            for nm, cnt in (("valu", "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU "
+                                     "SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS"),
+                            ("mem", "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS "
+                                    "SQ_INSTS_SALU SQ_WAIT_ANY GRBM_GUI_ACTIVE"))
+        ],
         # halo exchanged ahead (next to the all-reduce, one full pass) vs interior || halo + boundary
         "haloahead": [
             ("pytest", 600, f"{PYTEST} -v tests/test_gpu_multirank.py -k 'halo_ahead'"),

@@ -16,9 +16,9 @@ for d in sys.argv[1:]:
     for r in cur.execute("select * from counters_collection"):
         row = dict(zip(cols, r))
         name = str(row["kernel_name"])
-        if "k_cg_f1" not in name:
+        if "k_cg_f1" not in name and "k_cg_carry_ar" not in name:
             continue
-        k = re.search(r"(k_cg_f1\w*<[^>]*>)", name).group(1)
+        k = re.search(r"(k_cg_(?:f1|carry_ar)\w*<[^>]*>)", name).group(1)
         agg[k][row["counter_name"]].append(row["value"])
     for k, v in agg.items():
         for cn, vals in sorted(v.items()):

@@ -1,0 +1,419 @@
+// Line-carry single-reduction pass that does not store Ap ("Ap recomputed").
+//
+// The line-carry pass (cg_fused1.hip, k_cg_f1_carry) stores {r_k, Ap_k} as 16-B pairs because
+// pass k+1 forms r_{k+1} = r_k - a_k Ap_k for every row it touches (its own and, through p_{k+1}
+// of the neighbours, the stencil's), and a_k is only known after pass k's global reduction.
+// Per row and iteration that is 16 B read + 16 B written for {r, Ap} next to 8 + 8 B for p.
+//
+// Here Ap_{k-1} is not stored: pass k recomputes it as A p_{k-1} from the p_{k-1} it reads
+// anyway.  The recomputation has the producing pass's exact fma order over the same entries and
+// the same p_{k-1} values (which are the values the owners stored), so r_k, p_k, Ap_k and the
+// dot products are bit for bit those of the storing pass.  A wave walking down a column of
+// slices needs p_k of line m+1 for Ap_k(m); p_k(m+1) needs Ap_{k-1}(m+1), i.e. p_{k-1} of lines
+// m .. m+2: the carried window is one line deeper, and each row's r and p are read once and
+// written once (32 B/row instead of 48 B; the matrix codes once, carried from the recomputation
+// into the row sums one step later).
+//
+// Two places cannot recompute:
+//  * the rows just across a slice edge (the +-1 neighbours of lanes 0 / 63), which belong to
+//    the neighbouring column's wave: their Ap_{k-1} comes from a compact per-slice array of the
+//    two edge rows' Ap (ape: 2 doubles per 64-row slice, 1/4 B per row written);
+//  * the ghost lines of a multi-rank run, whose matrix rows another rank owns: each rank stores
+//    the full Ap of its first and last line (apx, ext layout) and the halo carries {r, Ap, p}
+//    of those lines as before.
+// 2-D stencils with only 0, +-1, +-one-line offsets (the specialised carry: SELL-64/c8 or /c4
+// dictionary codes).  Final mode (finalize(): r_m, x_m, ||r_m||^2) is a plain row-parallel
+// kernel with the same recomputation.
+#include <hip/hip_runtime.h>
+
+#include "mcg/check.hpp"
+#include "mcg/kernels.hpp"
+#include "spmv_engines.hpp"
+
+namespace mcg {
+namespace kern {
+namespace {
+
+#include "f1_common.hpp"
+
+__device__ __forceinline__ double ld_once(const double* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
+
+// a slice's codes for one lane: c4 nibbles / c8 bytes packed into 32-bit registers (entry u at
+// bit CB * u); w = the slice's width
+template <int CM, int U>
+struct ArCodes {
+  static constexpr int CB = CM == 3 ? 4 : 8;
+  uint32_t pk[(U * CB + 31) / 32];
+  int w;
+};
+
+// codes of slice row `lane` from its first slot `base` (slots, multiple of 64) and width w
+template <int CM, int U>
+__device__ __forceinline__ void ar_load_codes(const SellDev& S, int64_t base, int w, int lane, ArCodes<CM, U>& c) {
+  constexpr int CB = ArCodes<CM, U>::CB;
+  c.w = w;
+#pragma unroll
+  for (int q = 0; q < (U * CB + 31) / 32; ++q) c.pk[q] = 0u;
+  if constexpr (CM == 2) {
+    const uint8_t* __restrict__ cp = S.codes + base;
+#pragma unroll
+    for (int u = 0; u < U; ++u) c.pk[(u * CB) >> 5] |= (uint32_t)cp[64 * u + lane] << ((u * CB) & 31);
+  } else {
+    const uint8_t* __restrict__ cp = S.codes4 + (base >> 1);
+    const int sh = (lane & 1) * 4;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      c.pk[(u * CB) >> 5] |= (((uint32_t)cp[32 * u + (lane >> 1)] >> sh) & 15u) << ((u * CB) & 31);
+  }
+}
+
+template <int CM, int U>
+__device__ __forceinline__ int32_t ar_entry(const double2* dict, const ArCodes<CM, U>& c, int u, double& val) {
+  constexpr int CB = ArCodes<CM, U>::CB;
+  const double2 q = dict[(c.pk[(u * CB) >> 5] >> ((u * CB) & 31)) & ((1u << CB) - 1u)];
+  val = q.x;
+  return (int32_t)__double_as_longlong(q.y);
+}
+
+// whole-wave lane shifts through DPP (no LDS, so no lgkmcnt wait): value of lane + 1 / lane - 1
+__device__ __forceinline__ double lane_up(double v) {  // wave_shl:1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_dn(double v) {  // wave_shr:1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// per-slice metadata for the carry's codes loads: first slot / 64 (28 bits) | width << 28
+__global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, uint32_t* __restrict__ meta) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = slice_ptr[s];
+    meta[s] = (uint32_t)(b >> 6) | ((uint32_t)((slice_ptr[s + 1] - b) >> 6) << 28);
+  }
+}
+
+template <int CM, int U, int QD, bool PAIR>
+__global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+                                                     double* __restrict__ partials, int pstride, CgState* st,
+                                                     double tol, int first, int check, RedCtl rc) {
+  __shared__ double2 s_dict[256];
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (st->done || sc.conv) {
+    f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+    return;
+  }
+  for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
+  __syncthreads();
+  const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  const double* __restrict__ ro = v.r_old;
+  const double* __restrict__ po = v.p_old;
+  double* __restrict__ rn = v.r_new;
+  double* __restrict__ pn = v.p_new;
+  double* __restrict__ x = v.x;
+  const double* __restrict__ apx_o = v.ap_old;  // multi-rank: ghost lines' Ap_{k-1}
+  double* __restrict__ apx_n = v.ap_new;        // multi-rank: first / last line's Ap_k for the neighbours
+  double* __restrict__ en = v.ape_new;
+  const int lane = threadIdx.x & 63;
+  const int64_t SS = tr.strip;            // slices per line
+  const int32_t LO = (int32_t)(SS * 64);  // one line
+  const int64_t nl = tr.nt0 / SS;         // the rank's lines (the launch covers them all)
+  const int64_t nsl = tr.nt0;             // the rank's slices
+  const int64_t nb = gridDim.x, blk = blockIdx.x;
+  const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;  // XCD-aware (k_cg_f1_carry)
+  const int64_t nw = nb * kWaves;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t gw = lb * kWaves + wv;
+  const int64_t runs = nw > SS ? nw / SS : 1;
+  const int64_t chunk = (nl + runs - 1) / runs;
+  const int32_t ext32 = (int32_t)v.ext_len;
+  const bool ntl = v.nt_loads != 0;
+  const double* __restrict__ eo = v.ape_old;
+  const uint32_t* __restrict__ meta = S.smeta;
+  // a zero the compiler cannot see through: wave-uniform metadata loads stay vector loads (vmcnt,
+  // in order with the prefetches) instead of scalar loads, whose out-of-order lgkmcnt wait would
+  // also wait for every LDS dictionary read of the step
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+
+  struct Raw {
+    double r, p;
+  };
+  // the row just before (lane 0) / after (lane 63) the slice on a line: r, Ap (the neighbouring
+  // slice's edge row, ape), p -- loaded by those two lanes only; other lanes' values are unused
+  struct Edge {
+    double r, a, p;
+  };
+  struct XP {
+    double pkm2, xo;
+  };
+  // row sum over a slice's entries: p of the row, of row +-1 (neighbouring lanes; lanes 0 / 63
+  // take `edge`), of the next / previous line.  Same select chain and fma order as the storing pass.
+  auto stencil = [&](const ArCodes<CM, U>& c, double mid, double edge, double dnl, double upl) {
+    const double sh_up = lane_up(mid);
+    const double sh_dn = lane_dn(mid);
+    const double upv = lane == 63 ? edge : sh_up;
+    const double dnv = lane == 0 ? edge : sh_dn;
+    double sum = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double val;
+      const int32_t off = ar_entry<CM, U>(s_dict, c, u, val);
+      double t = off == LO ? upl : dnl;
+      asm volatile("" : "+v"(t));
+      t = off == -1 ? dnv : t;
+      asm volatile("" : "+v"(t));
+      t = off == 1 ? upv : t;
+      asm volatile("" : "+v"(t));
+      const double g = off == 0 ? mid : t;
+      sum = (u < c.w) ? fma(val, g, sum) : sum;
+    }
+    return sum;
+  };
+  for (int64_t job = gw; job < SS * runs; job += nw) {
+    const int64_t col = job % SS, l0 = (job / SS) * chunk;
+    const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
+    if (l0 >= l1) continue;
+    const int64_t sl0 = l0 * SS + col;
+    const int32_t e0 = (int32_t)(own + sl0 * 64);
+    const int32_t i0 = (int32_t)(sl0 * 64);
+    const int32_t n_run = (int32_t)(l1 - l0);
+    // lines j (relative to l0) inside the ext vectors: [jmin, jmax]; loads clamp to them (values
+    // of lines that do not exist are never multiplied: the matrix has no entry for them)
+    const int32_t jmax = (ext32 - 64 - e0) / LO;
+    const int32_t jmin = -(e0 / LO);
+    auto ebase = [&](int32_t j) { return e0 + (j < jmin ? jmin : (j > jmax ? jmax : j)) * LO; };
+    auto owned = [&](int32_t j) { return l0 + j >= 0 && l0 + j < nl; };
+    auto oline = [&](int32_t j) {  // clamped to the rank's lines
+      const int64_t L = l0 + j;
+      return L < 0 ? (int64_t)0 : (L >= nl ? nl - 1 : L);
+    };
+    auto load_raw = [&](int32_t j, Raw& q) {
+      const int32_t e = ebase(j) + lane;
+      q.r = ld_once(ro + e, ntl);
+      q.p = ld_once(po + e, ntl);
+    };
+    auto load_edge = [&](int32_t j, Edge& q) {
+      const int32_t e = ebase(j);
+      const int64_t s = oline(j) * SS + col;
+      if (lane == 0) {
+        const int32_t row = e >= 1 ? e - 1 : 0;
+        q.r = ro[row];
+        q.p = po[row];
+        q.a = eo[s >= 1 ? 2 * (s - 1) + 1 : 0];
+      } else if (lane == 63) {
+        const int32_t row = e + 64 < ext32 ? e + 64 : ext32 - 1;
+        q.r = ro[row];
+        q.p = po[row];
+        q.a = eo[s + 1 < nsl ? 2 * (s + 1) : 2 * nsl - 1];
+      }
+    };
+    auto load_xp = [&](int32_t j, XP& q) {
+      if constexpr (PAIR) {
+        const int32_t mm = j < n_run - 1 ? j : n_run - 1;
+        q.pkm2 = ld_once(pn + e0 + mm * LO + lane, ntl);
+        q.xo = ld_once(x + i0 + mm * LO + lane, ntl);
+      }
+    };
+    auto load_meta = [&](int32_t j) { return meta[oline(j) * SS + col + vz]; };
+    auto load_codes = [&](uint32_t mt, ArCodes<CM, U>& c) {
+      ar_load_codes<CM, U>(S, (int64_t)(mt & 0x0fffffffu) << 6, (int)(mt >> 28), lane, c);
+    };
+    auto edge_p = [&](const Edge& q) { return q.p; };
+    auto edge_pk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };  // p_k of the edge row
+    // ghost line: Ap_{k-1} exchanged by the halo (multi-rank only)
+    auto ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jmin && j <= jmax; };
+
+    // prologue: p_k of lines -1 and 0, r_k of line 0; operands of lines 1 .. QD, codes of 0, 1
+    Raw rm2, rm1, r0, rq[QD];
+    load_raw(-2, rm2);
+    load_raw(-1, rm1);
+    load_raw(0, r0);
+#pragma unroll
+    for (int d = 0; d < QD; ++d) load_raw(1 + d, rq[d]);
+    Edge edm1, ed0, ed1;
+    load_edge(-1, edm1);
+    load_edge(0, ed0);
+    load_edge(1, ed1);
+    ArCodes<CM, U> cm1, c0, c1;
+    load_codes(load_meta(-1), cm1);
+    load_codes(load_meta(0), c0);
+    load_codes(load_meta(1), c1);
+    uint32_t mt2 = load_meta(2);  // codes metadata one step ahead of the codes loads
+    XP x0{0.0, 0.0};
+    load_xp(0, x0);
+    double pr_pk = 0.0;
+    if (owned(-1)) {
+      const double t = stencil(cm1, rm1.p, edge_p(edm1), rm2.p, r0.p);
+      pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+    } else if (ghost(-1)) {
+      const double t = apx_o[ebase(-1) + lane];
+      pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+    }
+    double o_pold = r0.p, o_rk, o_pk;
+    {
+      const double t = stencil(c0, r0.p, edge_p(ed0), rm1.p, rq[0].p);
+      o_rk = fma(na, t, r0.r);
+      o_pk = fma(b, r0.p, o_rk);
+    }
+    double o_epk = edge_pk(ed0);
+    for (int32_t m = 0; m < n_run; ++m) {
+      // 1. loads for later steps, in the order they are waited for: metadata of line m + 3, codes
+      //    of line m + 2 (metadata from the previous step), edges of line m + 2, x / p_{k-2} of
+      //    line m + 1, operands of line m + 1 + QD.  All vector loads: the in-order vmcnt lets
+      //    every wait leave the younger prefetches in flight
+      const uint32_t mt3 = load_meta(m + 3);
+      ArCodes<CM, U> c2;
+      load_codes(mt2, c2);
+      Edge ed2;
+      load_edge(m + 2, ed2);
+      XP x1{0.0, 0.0};
+      load_xp(m + 1, x1);
+      Raw rnq;
+      load_raw(m + 1 + QD, rnq);
+      // 2. r_k, p_k of line m + 1: Ap_{k-1} recomputed (owned) or exchanged (ghost line)
+      double rk1 = 0.0, pk1 = 0.0;
+      if (owned(m + 1)) {
+        const double t = stencil(c1, rq[0].p, edge_p(ed1), o_pold, rq[1].p);
+        rk1 = fma(na, t, rq[0].r);
+        pk1 = fma(b, rq[0].p, rk1);
+      } else if (ghost(m + 1)) {
+        const double t = apx_o[ebase(m + 1) + lane];
+        rk1 = fma(na, t, rq[0].r);
+        pk1 = fma(b, rq[0].p, rk1);
+      }
+      // 3. Ap_k of line m, stores, partials
+      const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1);
+      const int32_t eb = e0 + m * LO;
+      st_stream(&(rn + eb)[lane], o_rk);
+      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, x0.pkm2, x0.xo)));
+      st_stream(&(pn + eb)[lane], o_pk);
+      const int64_t s = (l0 + m) * SS + col;
+      if (lane == 0 || lane == 63) en[2 * s + (lane == 63 ? 1 : 0)] = sum;
+      if (apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) apx_n[eb + lane] = sum;
+      s_pap = fma(o_pk, sum, s_pap);
+      s_rap = fma(o_rk, sum, s_rap);
+      s_apap = fma(sum, sum, s_apap);
+      s_rr = fma(o_rk, o_rk, s_rr);
+      // 4. rotate
+      pr_pk = o_pk;
+      o_pk = pk1;
+      o_rk = rk1;
+      o_pold = rq[0].p;
+      o_epk = edge_pk(ed1);
+      ed1 = ed2;
+#pragma unroll
+      for (int d = 0; d + 1 < QD; ++d) rq[d] = rq[d + 1];
+      rq[QD - 1] = rnq;
+      x0 = x1;
+      c0 = c1;
+      c1 = c2;
+      mt2 = mt3;
+    }
+  }
+  f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+}
+
+// finalize(): r_m = r_{m-1} - a A p_{m-1} (recomputed, same fma order), x_m, partial ||r_m||^2;
+// or, when the run latched, the one-term x catch-up of an even m (k_cg_f1's final mode)
+template <int CM, int U>
+__global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_t own, int64_t n,
+                                                  double* __restrict__ partials, int pstride, CgState* st,
+                                                  double tol, int first, int check, int k) {
+  const int done = st->done;
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  const double a = sc.alpha, na = -a, ap = st->a_prev;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (done || sc.conv) {
+    const int64_t m = done ? (done == 1 ? st->conv_iter : -1) : k - 1;
+    if (m >= 2 && (m & 1) == 0)
+      for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        v.x[i] = fma(ap, v.p_fix[own + i], v.x[i]);
+    return;
+  }
+  const bool pair = (k & 1) && k >= 3;
+  double s_rr = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t e = own + i;
+    ArCodes<CM, U> c;
+    const int64_t base = S.slice_ptr[i >> 6];
+    ar_load_codes<CM, U>(S, base, (int)((S.slice_ptr[(i >> 6) + 1] - base) >> 6), (int)(i & 63), c);
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double val;
+      const int32_t off = ar_entry<CM, U>(S.dict, c, u, val);
+      if (u < c.w) t = fma(val, v.p_old[e + off], t);
+    }
+    const double rk = fma(na, t, v.r_old[e]);
+    v.r_new[e] = rk;
+    v.x[i] = pair ? fma(a, v.p_old[e], fma(ap, v.p_new[e], v.x[i])) : fma(a, v.p_old[e], v.x[i]);
+    s_rr = fma(rk, rk, s_rr);
+  }
+  block_partial4(0.0, 0.0, 0.0, s_rr, partials, pstride);
+}
+
+}  // namespace
+
+void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipStream_t stream) {
+  if (n_slices <= 0) return;
+  hipLaunchKernelGGL(k_slice_meta, dim3(grid_for(n_slices, 256, 4)), dim3(256), 0, stream, slice_ptr, n_slices, meta);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(slice_meta)");
+}
+
+void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
+                 const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol, int first,
+                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc) {
+  if (tr.ntiles == 0 || grid == 0) return;
+  MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
+            "Ap-recomputing carry: one launch over the rank's whole grid lines");
+  MCG_CHECK((cm == 2 || cm == 3) && param >= 4 && param <= 5 && S.dict != nullptr,
+            "Ap-recomputing carry: SELL-64/c8 or /c4 rows of at most 5 entries");
+  MCG_CHECK(cm != 3 || S.codes4 != nullptr, "Ap-recomputing carry: 4-bit codes missing");
+  MCG_CHECK(final_mode || S.smeta != nullptr, "Ap-recomputing carry: slice metadata missing");
+  MCG_CHECK(v.ape_old != nullptr && v.ape_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
+            "Ap-recomputing carry: vectors missing");
+  MCG_CHECK((v.ap_old == nullptr) == (v.ap_new == nullptr), "Ap-recomputing carry: boundary Ap buffers");
+  MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
+            "in-kernel reduction: bad control block");
+  if (final_mode) {
+    const int64_t n = tr.nt0 * 64;
+#define MCG_AF(CM, U)                                                                                        \
+  hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, partials, pstride, \
+                     st, tol, first, check, k)
+    if (cm == 3) { if (param == 4) MCG_AF(3, 4); else MCG_AF(3, 5); }
+    else { if (param == 4) MCG_AF(2, 4); else MCG_AF(2, 5); }
+#undef MCG_AF
+    MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
+    return;
+  }
+  const bool pair = (k & 1) != 0;
+  const int qd = depth <= 2 ? 2 : (depth >= 5 ? 5 : depth);
+#define MCG_A(CM, U, QD, PAIR)                                                                                     \
+  hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, partials, \
+                     pstride, st, tol, first, check, rc)
+#define MCG_AP(CM, U, QD)                     \
+  do {                                        \
+    if (pair) MCG_A(CM, U, QD, true);         \
+    else MCG_A(CM, U, QD, false);             \
+  } while (0)
+#define MCG_AQ(CM, U)                         \
+  do {                                        \
+    if (qd == 2) MCG_AP(CM, U, 2);            \
+    else if (qd == 3) MCG_AP(CM, U, 3);       \
+    else if (qd == 4) MCG_AP(CM, U, 4);       \
+    else MCG_AP(CM, U, 5);                    \
+  } while (0)
+  if (cm == 3) { if (param == 4) MCG_AQ(3, 4); else MCG_AQ(3, 5); }
+  else { if (param == 4) MCG_AQ(2, 4); else MCG_AQ(2, 5); }
+#undef MCG_AQ
+#undef MCG_AP
+#undef MCG_A
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+
+}  // namespace kern
+}  // namespace mcg

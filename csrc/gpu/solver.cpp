@@ -395,7 +395,6 @@ void GpuCgSolver::setup() {
 
   // ---- vectors ----
   b_.allocate(n, "b", 8);
-  allocate_vectors_();
   if (is_user) {  // the user's b (or the spec's rhs kind), built on the host
     const std::vector<double> hb = build_rhs(spec_, L_.row_begin, L_.row_end);
     if (n) MCG_HIP(hipMemcpy(b_.get(), hb.data(), n * sizeof(double), hipMemcpyHostToDevice),
@@ -514,11 +513,34 @@ void GpuCgSolver::setup() {
       if (split_ && (opt_.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
     }
     info_.carry = carry_all_ || carry_int_;
+    // Ap recomputed instead of stored: the specialised 2-D pass over every owned line in one launch
+    // (with a split launch the boundary rows' generic pass would need the stored Ap)
+    ar_ = opt_.ap_recompute != 0 && carry_all_ && !carry_general_ && carry_lo2_ == 0 && c8_ && !split_ &&
+          info_.spmv_param <= 5 && tr_all_.b0 == 0 && tr_all_.strip > 0;
+    MCG_CHECK(opt_.ap_recompute != 1 || ar_,
+              "ap_recompute needs the specialised 2-D line-carry pass over all lines (c8, <= 5 entries per row)");
     info_.carry_xchg = info_.carry && carry_lo2_ > 0 && opt_.carry_3d == 2 &&
                        kern::carry_block_exchange_ok(info_.spmv_param, carry_lo2_, gl / 64);
     if (!info_.carry || carry_general_ || carry_lo2_ != 0) codes4_.release();  // only the 2-D carry reads them
     info_.codes4 = codes4_.get() != nullptr;
   }
+  if (ar_) {  // r and p in the plain ext layout (no {r, Ap} pairs); the pipelined generic pass reads pairs
+    opt_.interleave = 0;
+    pipe_ = false;
+    info_.pipeline = false;
+  }
+  info_.ap_recompute = ar_;
+  info_.interleave = opt_.interleave == 1;
+  if (ar_ && n > 0) {
+    const int64_t ns = (n + 63) / 64;
+    int64_t slots = 0;
+    MCG_HIP(hipMemcpy(&slots, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(A)");
+    MCG_CHECK((slots >> 6) < ((int64_t)1 << 28) && info_.max_row_len < 16, "slice metadata overflows 28 bits");
+    smeta_.allocate(ns, "A");
+    kern::slice_meta(slice_ptr_.get(), ns, smeta_.get(), s0_);
+  }
+  allocate_vectors_();
   g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
@@ -559,6 +581,11 @@ void GpuCgSolver::setup() {
     info_.bytes_per_iter_model = (double)matrix_bytes + 80.0 * n;
     info_.device_bytes = matrix_bytes + (size_t)(4 * n + L_.ext_len) * 8 + rp64_.bytes();
   }
+  if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25
+    info_.bytes_per_iter_model = (double)matrix_bytes + 44.25 * n;
+    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes();
+    for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
+  }
   // vectors allocated with room for the placement probe's start offsets hold that headroom too
   for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->lead_capacity() * sizeof(double);
   probe_placement_();
@@ -580,7 +607,7 @@ bool GpuCgSolver::all_ranks_agree_(bool mine) {
 }
 
 std::vector<DeviceBuffer<double>*> GpuCgSolver::vectors_() {
-  return {&x_, &r_, &r1_, &Ap_, &Ap1_, &ra_[0], &ra_[1], &p_[0], &p_[1]};
+  return {&x_, &r_, &r1_, &Ap_, &Ap1_, &ra_[0], &ra_[1], &p_[0], &p_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1]};
 }
 
 void GpuCgSolver::allocate_vectors_() {
@@ -598,7 +625,17 @@ void GpuCgSolver::allocate_vectors_() {
   const size_t skew = (size_t)std::max(0, opt_.vec_skew) * 32;
   const size_t cap = opt_.placement_tries > 1 && opt_.placement_leads > 1 && opt_.recurrence == 1 ? kLeadCap : 0;
   x_.allocate(n, "x", 8, 1 * skew, cap);
-  if (opt_.interleave == 1) {  // single-reduction form, {r, Ap} pairs, double-buffered by parity
+  if (ar_) {  // r, p by parity (ext layout); Ap only for slice edges (+ first / last / ghost lines at P > 1)
+    r_.allocate(L_.ext_len, "r", 8, 2 * skew, cap);
+    r1_.allocate(L_.ext_len, "r", 8, 3 * skew, cap);
+    const int64_t ns = (n + 63) / 64;
+    ape_[0].allocate(2 * std::max<int64_t>(ns, 1), "Ap", 8);
+    ape_[1].allocate(2 * std::max<int64_t>(ns, 1), "Ap", 8);
+    if (use_halo_) {
+      apx_[0].allocate(L_.ext_len, "Ap", 8);
+      apx_[1].allocate(L_.ext_len, "Ap", 8);
+    }
+  } else if (opt_.interleave == 1) {  // single-reduction form, {r, Ap} pairs, double-buffered by parity
     ra_[0].allocate(2 * L_.ext_len, "r", 8, 2 * skew, cap);
     ra_[1].allocate(2 * L_.ext_len, "r", 8, 3 * skew, cap);
   } else if (opt_.recurrence == 1) {  // single-reduction form: r and Ap are gathered -> ext layout, double-buffered
@@ -718,7 +755,7 @@ void GpuCgSolver::reset() {
   const int64_t n = L_.n_local();
   hipStream_t s = s0_;
   MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
-  for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1]})
+  for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1]})
     if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
   MCG_HIP(hipMemsetAsync(p_[0].get(), 0, p_[0].bytes(), s), "device memset failed(p)");
   MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
@@ -734,7 +771,7 @@ void GpuCgSolver::reset() {
   } else if (opt_.recurrence == 1) {
     // iteration 0 reads parity-1 buffers: r_{-1} = b, Ap_{-1} = 0, p_{-1} = 0
     MCG_HIP(hipMemsetAsync(r1_.get(), 0, r1_.bytes(), s), "device memset failed(r)");
-    MCG_HIP(hipMemsetAsync(Ap1_.get(), 0, Ap1_.bytes(), s), "device memset failed(Ap)");
+    if (Ap1_.bytes()) MCG_HIP(hipMemsetAsync(Ap1_.get(), 0, Ap1_.bytes(), s), "device memset failed(Ap)");
     MCG_HIP(hipMemcpyAsync(r1_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
             "vector copy failed(r)");
   } else {
@@ -826,6 +863,18 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
   }
   const SellDev S = sell_view();
+  if (ar_) {
+    MCG_CHECK(which == 0, "Ap-recomputing carry: one launch per iteration");
+    v.ra_old = nullptr;
+    v.ra_new = nullptr;
+    v.ap_old = apx_[(k + 1) & 1].get();
+    v.ap_new = apx_[k & 1].get();
+    v.ape_old = ape_[(k + 1) & 1].get();
+    v.ape_new = ape_[k & 1].get();
+    kern::cg_carry_ar(codes4_.get() ? 3 : 2, info_.spmv_param, opt_.carry_depth > 0 ? opt_.carry_depth : 3, S, v,
+                      L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc);
+    return;
+  }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
     kern::cg_fused1_carry(codes4_.get() && !carry_general_ && carry_lo2_ == 0 ? 3 : (c8_ ? 2 : 1), info_.spmv_param,
                           opt_.carry_depth > 0 ? opt_.carry_depth : (carry_lo2_ > 0 ? 1 : 3), carry_general_,
@@ -862,6 +911,7 @@ void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
     nv = 2;
     w = widths;
   }
+  if (ar_) vecs[1] = apx_[(k + 1) & 1].get();  // Ap of the ghost lines: the owners' stored first / last line
   comm_->halo_exchange(L_, vecs, nv, s, w);
 }
 
@@ -1137,7 +1187,8 @@ void GpuCgSolver::inject_fault_(int k) {
 void GpuCgSolver::finalize() {
   if (k_ == 0 || finalized_) return;
   finalized_ = true;  // the single-reduction catch-up of a pending x term must run once
-  join_halo_();
+  if (ar_ && use_halo_) ensure_ghosts_(k_);  // the final r_m recomputes Ap_{m-1} over the ghost lines too
+  else join_halo_();
   if (pmat_) {  // U in final mode: r_m, x_m and ||r_m||^2, then latch
     kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, L_.n_local(), st_.get(), opt_.tol,
                           0, k_ >= 2 ? 1 : 0, 1, partials_.get(), pstride_, g_b_, s0_);
@@ -1267,7 +1318,8 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
     ok = std::fwrite(host.data(), 1, bytes, f) == bytes;
   };
   dump(st_.get(), sizeof(CgState));
-  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1]})
+  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1], &ape_[0], &ape_[1],
+                                  &apx_[0], &apx_[1]})
     dump(b->get(), b->bytes());
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) fail("checkpoint write failed", path);
@@ -1295,7 +1347,8 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
     if (ok) MCG_HIP(hipMemcpy(dev, host.data(), bytes, hipMemcpyHostToDevice), "memcpy from host to device failed(ckpt)");
   };
   load(st_.get(), sizeof(CgState));
-  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1]})
+  for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1], &ape_[0], &ape_[1],
+                                  &apx_[0], &apx_[1]})
     load(b->get(), b->bytes());
   std::fclose(f);
   if (!ok) fail("checkpoint truncated", path);

@@ -81,6 +81,10 @@ struct CgOptions {
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
+  int ap_recompute = -1;     // 2-D line-carry pass: recompute Ap_{k-1} = A p_{k-1} from the p it reads instead of
+                             // storing {r, Ap} pairs (r and p read once, written once: ~16 B/row less;
+                             // cg_carry_ar.hip); -1 = auto (when the specialised 2-D carry covers every row
+                             // in one launch), 0 = off, 1 = required
   int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
                              // right after pass k wrote it (side stream, next to the all-reduce) and run one
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's

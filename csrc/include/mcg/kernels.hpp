@@ -100,6 +100,8 @@ struct SellDev {
   // SELL-C-sigma (user matrices): slot i of the slices holds local row perm[i] (rows sorted by
   // length inside windows, so a slice pads less); nullptr = identity.  int32 columns only.
   const int32_t* perm = nullptr;
+  // Ap-recomputing line carry: per slice (first slot / 64) | (width << 28) (slice_meta)
+  const uint32_t* smeta = nullptr;
   // SELL-64/aligned (long rows whose slices share their column offsets, e.g. the wide random-SPD
   // family): entry j of EVERY lane of slice s is the row's own column + soffs[slice_ptr[s] / 64 + j]
   // (one wave-uniform offset per slot, clamped to [0, ext_len); absent entries hold 0.0), so a
@@ -209,6 +211,11 @@ struct F1Vectors {
   const double* p_fix = nullptr;
   int64_t ext_len = 0;  // ext-layout length of r / Ap / p (bounds of the line-carry pass's edge loads)
   int nt_loads = 0;     // line-carry pass: non-temporal loads of the once-read operands
+  // Ap-recomputing carry (cg_carry_ar.hip): Ap of each slice's two edge rows (lanes 0 / 63),
+  // 2 doubles per owned slice, iteration k-1 / k; r_old/new, p_old/new as above, ap_old/new the
+  // ext-layout Ap of the rank's first / last line and of its ghost lines (multi-rank, else null)
+  const double* ape_old = nullptr;
+  double* ape_new = nullptr;
 };
 // In-kernel reduction of a fused pass's block partials (replaces the cg_reduce_f1 launch, so
 // one iteration is ONE kernel + the 32-B all-reduce).  Two-level last-arriver fan-in: each block
@@ -242,6 +249,13 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
 // slices and keeps the previous / current / next line's p_k in registers.
 // The plane carry's block exchange applies: lo2 whole slices, kWaves | grid lines per plane, 7-8 entries
 bool carry_block_exchange_ok(int param, int32_t lo2, int64_t strip);
+// Line-carry pass that recomputes Ap_{k-1} = A p_{k-1} instead of storing Ap (cg_carry_ar.hip):
+// 2-D stencils (offsets 0, +-1, +-one line), SELL-64/c8 (cm 2) or /c4 (cm 3), <= 5 entries per
+// row, one launch over the rank's whole lines.  final_mode: finalize()'s r_m / x_m pass.
+void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipStream_t stream);
+void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
+                 const TileRanges& slices, double* partials, int pstride, int grid, CgState* st, double tol,
+                 int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl());
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,
                      bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,

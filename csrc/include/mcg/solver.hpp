@@ -57,6 +57,7 @@ struct SolverInfo {
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
   bool ag_overlap = false;    // the own-block SpMV half runs while the all-gather is in flight
+  bool ap_recompute = false;  // line-carry pass recomputes Ap instead of storing it (CgOptions::ap_recompute)
   bool halo_ahead = false;    // multi-rank stencil halo exchanged right after the pass that produced it, next to
                               // the all-reduce; one full pass per iteration (CgOptions::halo_ahead)
   double ag_local_frac = 0.0; // own-block slots / all slots (the part of the SpMV that hides the all-gather)
@@ -138,6 +139,7 @@ class GpuCgSolver {
   bool prefetch_halo_ = false;  // single-reduction form: next iteration's halo right after the boundary pass
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
+  bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool split_ = false;          // interior / boundary launches around an overlapped halo
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
   bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them
@@ -182,12 +184,16 @@ class GpuCgSolver {
     s.soffs = soffs_.get();
     s.ext_len = L_.ext_len;
     s.local_slots = lslots_.get();
+    s.smeta = smeta_.get();
     return s;
   }
   // vectors
   DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
   DeviceBuffer<double> ra_[2];     // interleaved {r, Ap} pairs by parity (2 * ext_len doubles each)
+  DeviceBuffer<uint32_t> smeta_;  // Ap-recomputing carry: per-slice (first slot / 64 | width << 28)
+  DeviceBuffer<double> ape_[2];    // Ap-recomputing carry: Ap of the slices' edge rows, by parity
+  DeviceBuffer<double> apx_[2];    // ... multi-rank: Ap of the first / last line + ghost lines (ext layout)
   int pstride_ = 0;                // partial-array stride (4 arrays in the single-reduction form)
   int bnd_base_ = 0;               // first partial slot of the boundary launch (a multiple of kRedGroup)
   bool fused_red_ = false;         // in-kernel reduction of the fused pass (CgOptions::fused_reduce)

@@ -214,6 +214,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("sell_aligned", &CgOptions::sell_aligned)
       .def_readwrite("ag_overlap", &CgOptions::ag_overlap)
       .def_readwrite("halo_ahead", &CgOptions::halo_ahead)
+      .def_readwrite("ap_recompute", &CgOptions::ap_recompute)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -386,6 +387,7 @@ PYBIND11_MODULE(_C, m) {
         d["allgather"] = i.allgather;
         d["ag_overlap"] = i.ag_overlap;
         d["halo_ahead"] = i.halo_ahead;
+        d["ap_recompute"] = i.ap_recompute;
         d["ag_local_frac"] = i.ag_local_frac;
         d["graph_fallbacks"] = i.graph_fallbacks;
         d["comm_cus"] = i.comm_cus;
@@ -421,6 +423,7 @@ PYBIND11_MODULE(_C, m) {
       d["row_begin"] = rr.row_begin;
       d["true_rnorm"] = rr.true_rnorm;
       d["carry"] = rr.carry;
+      d["ap_recompute"] = rr.ap_recompute;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;
       py::dict ph;

@@ -151,7 +151,8 @@ def test_local_ranks_plane_carry_interior(mcg, world):
 
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("problem,n", [("poisson2d", 256), ("poisson3d", 32)])
-def test_local_ranks_halo_ahead_matches_split(mcg, world, problem, n):
+@pytest.mark.parametrize("ar", [-1, 0])
+def test_local_ranks_halo_ahead_matches_split(mcg, world, problem, n, ar):
     """halo_ahead (ghosts of iteration k+1 exchanged right after pass k, one full pass per
     iteration) against the interior || halo + boundary split and P = 1: same recurrence, so the
     residuals agree to rounding of the differently grouped partial sums."""
@@ -161,6 +162,7 @@ def test_local_ranks_halo_ahead_matches_split(mcg, world, problem, n):
     for ha in (1, 0):
         o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
         o.halo_ahead = ha
+        o.ap_recompute = ar  # auto: the 2-D carry recomputes Ap (ghost lines' Ap from the halo)
         outs[ha] = C.run_local_ranks(spec.native(), o, world, 60, True)
     one = C.run_local_ranks(spec.native(), _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1),
                             1, 60, True)
@@ -172,6 +174,8 @@ def test_local_ranks_halo_ahead_matches_split(mcg, world, problem, n):
         assert all(abs(q["true_rnorm"] - q["rnorm"]) <= 1e-8 * q["true_rnorm"] for q in out["ranks"])
     if problem == "poisson2d":  # the full pass of every rank is the line-carry pass
         assert all(q["carry"] for q in outs[1]["ranks"])
+        assert all(q["ap_recompute"] == (ar != 0) for q in outs[1]["ranks"])
+        assert not any(q["ap_recompute"] for q in outs[0]["ranks"])  # the split keeps the stored Ap
 
 
 @pytest.mark.parametrize("problem,n", [("poisson2d", 512), ("poisson3d", 64)])

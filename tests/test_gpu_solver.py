@@ -267,6 +267,43 @@ def test_line_carry_c4_codes_match_c8(mcg):
     np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
 
 
+@pytest.mark.parametrize("c4", [1, 0])
+@pytest.mark.parametrize("n", [128, 256])
+def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, c4, n):
+    """The line-carry pass that recomputes Ap_{k-1} = A p_{k-1} (same entries, same fma order, same
+    p values) instead of storing {r, Ap} pairs: every r, p, x and dot product is the same bits, to
+    convergence and at fixed odd / even iteration counts (final pass, paired x updates)."""
+    spec = mcg.make_problem("poisson2d", n=n, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=1, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=0, check_every=8)
+    assert a.info["ap_recompute"] and not a.info["interleave"]
+    assert not b.info["ap_recompute"] and b.info["interleave"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+    for its in (23, 24):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["iterations"] == its and outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
+        np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    assert a.true_residual_norm() == b.true_residual_norm()
+
+
+def test_ap_recompute_auto_and_refusal(mcg):
+    """auto: on for the specialised 2-D carry; off where the carry is off (3-D generic) or the
+    rows are not whole 64-row lines; required (=1) where it cannot apply: a clear error."""
+    s2 = mcg.CGSolver(mcg.make_problem("poisson2d", n=256), format="sellc8", recurrence=1)
+    assert s2.info["ap_recompute"] and s2.info["carry"]
+    s3 = mcg.CGSolver(mcg.make_problem("poisson3d", n=32), format="sellc8", recurrence=1)
+    assert not s3.info["ap_recompute"]
+    with pytest.raises(Exception, match="ap_recompute"):
+        mcg.CGSolver(mcg.make_problem("poisson2d", n=100), format="sellc8", recurrence=1, ap_recompute=1)
+
+
 @pytest.mark.parametrize("problem,n", [("poisson2d", 256), ("poisson3d", 40)])
 def test_placement_probe_keeps_numerics(mcg, problem, n):
     """The setup-time placement probe (several vector allocations x start offsets, fastest kept) only
