@@ -242,7 +242,8 @@ def _run_rank(args, out_fd) -> int:
                 "seq_len": spec.n_rows,
                 "parallelism": f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else f"rowpart{n_gpus}",
                 # storage the timed pass streams: the 2-D line-carry pass reads 4-bit codes (c4)
-                "format": "sell64-c4" if info.get("codes4") else info["format"],
+                "format": ("sell64-dia4" if info.get("dia4") else "sell64-c4" if info.get("codes4")
+                           else info["format"]),
                 "recurrence": info["recurrence"],
                 "pass": ("line-carry" if info.get("carry") else "split (materialized p)" if info.get("pmat")
                          else "windowed" if info.get("window") else "generic, xcd-aware" if info.get("xcd_map")

@@ -217,6 +217,18 @@ def recipes(a) -> dict:
             for b in (2, 4, 8)
         ],
         # the distributed path at headline sizes as P in-process ranks on one GPU
+        "dia": [
+            ("pytest", 600, f"{PY} -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_solver.py "
+                            f"tests/test_gpu_multirank.py tests/test_gpu_fused_reduce.py -m gpu"),
+            ("b_dia", 200, f"{PY} bench.py"),
+            ("b_c4", 200, f"{PY} bench.py --set carry_dia=0"),
+            ("b_dia2", 200, f"{PY} bench.py"),
+            ("b_c4_2", 200, f"{PY} bench.py --set carry_dia=0"),
+            ("b4096_dia", 200, f"{PY} bench.py --grid 4096 --steps 2000 --warmup 100"),
+            ("b4096_c4", 200, f"{PY} bench.py --grid 4096 --steps 2000 --warmup 100 --set carry_dia=0"),
+            ("sim8_dia", 200, f"{PY} bench.py --sim-world 8 --sim-rank 3 --steps 400 --warmup 40"),
+            ("sim8_c4", 200, f"{PY} bench.py --sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --set carry_dia=0"),
+        ],
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),
             ("r512", 600, f"{PY} bench/rehearse_ranks.py --problem poisson3d --n 512 --iters 20 --world 1 2 4 8 "
@@ -272,10 +284,15 @@ def main(argv=None) -> int:
             print(k + ": " + ", ".join(s for s, _, _ in steps))
         return 0
     for name in a.recipe:
+        name, _, only = name.partition("/")  # "recipe/step" runs one step of a recipe
         if name not in R:
             print(f"unknown recipe {name!r}", file=sys.stderr)
             return 2
-        rc = run(name, R[name], a.dry_run)
+        steps = [s for s in R[name] if not only or s[0] == only]
+        if not steps:
+            print(f"unknown step {only!r} of {name!r}", file=sys.stderr)
+            return 2
+        rc = run(name, steps, a.dry_run)
         if rc != 0:
             return rc
     return 0

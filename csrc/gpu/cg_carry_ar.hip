@@ -26,6 +26,11 @@
 // kernel with the same recomputation.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <vector>
+
 #include "mcg/check.hpp"
 #include "mcg/kernels.hpp"
 #include "spmv_engines.hpp"
@@ -42,7 +47,7 @@ __device__ __forceinline__ double ld_once(const double* p, bool nt) { return nt 
 // bit CB * u); w = the slice's width
 template <int CM, int U>
 struct ArCodes {
-  static constexpr int CB = CM == 3 ? 4 : 8;
+  static constexpr int CB = CM >= 3 ? 4 : 8;
   uint32_t pk[(U * CB + 31) / 32];
   int w;
 };
@@ -65,6 +70,18 @@ __device__ __forceinline__ void ar_load_codes(const SellDev& S, int64_t base, in
     for (int u = 0; u < U; ++u)
       c.pk[(u * CB) >> 5] |= (((uint32_t)cp[32 * u + (lane >> 1)] >> sh) & 15u) << ((u * CB) & 31);
   }
+}
+
+// SELL-64/dia4: the 5 value indices of slice row `lane` (slot u at bit 4 u); sp = the slice's 160 B
+template <int U>
+__device__ __forceinline__ void ar_load_dia(const uint8_t* __restrict__ sp, int lane, ArCodes<4, U>& c) {
+  static_assert(U == 5, "dia4: the five canonical 2-D offsets");
+  c.w = U;
+  const int sh = (lane & 1) * 4;
+  uint32_t pk = 0u;
+#pragma unroll
+  for (int u = 0; u < U; ++u) pk |= (((uint32_t)sp[32 * u + (lane >> 1)] >> sh) & 15u) << (4 * u);
+  c.pk[0] = pk;
 }
 
 template <int CM, int U>
@@ -99,13 +116,18 @@ template <int CM, int U, int QD, bool PAIR>
 __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
-  __shared__ double2 s_dict[256];
+  __shared__ double2 s_dict[CM == 4 ? 1 : 256];
+  __shared__ double s_val[16];  // dia4 values
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   if (st->done || sc.conv) {
     f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
     return;
   }
-  for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
+  if constexpr (CM == 4) {
+    if (threadIdx.x < 16) s_val[threadIdx.x] = S.dvals[threadIdx.x];
+  } else {
+    for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
+  }
   __syncthreads();
   const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
   const double* __restrict__ ro = v.r_old;
@@ -158,6 +180,12 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
     const double upv = lane == 63 ? edge : sh_up;
     const double dnv = lane == 0 ? edge : sh_dn;
     double sum = 0.0;
+    if constexpr (CM == 4) {  // slot u = the u-th canonical offset: ascending columns, no selects
+      const double g[5] = {dnl, dnv, mid, upv, upl};
+#pragma unroll
+      for (int u = 0; u < 5; ++u) sum = fma(s_val[(c.pk[0] >> (4 * u)) & 15u], g[u], sum);
+      return sum;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       double val;
@@ -218,9 +246,14 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
         q.xo = ld_once(x + i0 + mm * LO + lane, ntl);
       }
     };
-    auto load_meta = [&](int32_t j) { return meta[oline(j) * SS + col + vz]; };
+    // dia4: the "metadata" is the slice index (fixed 160 B per slice, nothing to load)
+    auto load_meta = [&](int32_t j) {
+      if constexpr (CM == 4) return (uint32_t)(oline(j) * SS + col);
+      else return meta[oline(j) * SS + col + vz];
+    };
     auto load_codes = [&](uint32_t mt, ArCodes<CM, U>& c) {
-      ar_load_codes<CM, U>(S, (int64_t)(mt & 0x0fffffffu) << 6, (int)(mt >> 28), lane, c);
+      if constexpr (CM == 4) ar_load_dia<U>(S.dia4 + (int64_t)mt * 160, lane, c);
+      else ar_load_codes<CM, U>(S, (int64_t)(mt & 0x0fffffffu) << 6, (int)(mt >> 28), lane, c);
     };
     auto edge_p = [&](const Edge& q) { return q.p; };
     auto edge_pk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };  // p_k of the edge row
@@ -320,7 +353,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
 // finalize(): r_m = r_{m-1} - a A p_{m-1} (recomputed, same fma order), x_m, partial ||r_m||^2;
 // or, when the run latched, the one-term x catch-up of an even m (k_cg_f1's final mode)
 template <int CM, int U>
-__global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_t own, int64_t n,
+__global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_t own, int64_t n, int32_t lo,
                                                   double* __restrict__ partials, int pstride, CgState* st,
                                                   double tol, int first, int check, int k) {
   const int done = st->done;
@@ -339,14 +372,25 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const int64_t e = own + i;
     ArCodes<CM, U> c;
-    const int64_t base = S.slice_ptr[i >> 6];
-    ar_load_codes<CM, U>(S, base, (int)((S.slice_ptr[(i >> 6) + 1] - base) >> 6), (int)(i & 63), c);
     double t = 0.0;
+    if constexpr (CM == 4) {  // absent entries: value 0 times a clamped (finite) operand
+      ar_load_dia<U>(S.dia4 + (i >> 6) * 160, (int)(i & 63), c);
+      const int64_t offs[5] = {-(int64_t)lo, -1, 0, 1, (int64_t)lo};
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      double val;
-      const int32_t off = ar_entry<CM, U>(S.dict, c, u, val);
-      if (u < c.w) t = fma(val, v.p_old[e + off], t);
+      for (int u = 0; u < 5; ++u) {
+        int64_t q = e + offs[u];
+        q = q < 0 ? 0 : (q >= v.ext_len ? v.ext_len - 1 : q);
+        t = fma(S.dvals[(c.pk[0] >> (4 * u)) & 15u], v.p_old[q], t);
+      }
+    } else {
+      const int64_t base = S.slice_ptr[i >> 6];
+      ar_load_codes<CM, U>(S, base, (int)((S.slice_ptr[(i >> 6) + 1] - base) >> 6), (int)(i & 63), c);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        double val;
+        const int32_t off = ar_entry<CM, U>(S.dict, c, u, val);
+        if (u < c.w) t = fma(val, v.p_old[e + off], t);
+      }
     }
     const double rk = fma(na, t, v.r_old[e]);
     v.r_new[e] = rk;
@@ -354,6 +398,44 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
     s_rr = fma(rk, rk, s_rr);
   }
   block_partial4(0.0, 0.0, 0.0, s_rr, partials, pstride);
+}
+
+// SELL-64/c8 -> /dia4: one thread per row pair (lanes 2i, 2i+1 of a slice share the bytes).
+// Entries with value +-0 (SELL padding) are skipped; any other entry must sit at a canonical
+// offset, in strictly increasing offset order along the row's slots (else `bad`).
+__global__ __launch_bounds__(256) void k_sell_to_dia4(SellDev S, int nd, int64_t line, int zero_vi,
+                                                      uint8_t* __restrict__ dia, unsigned* __restrict__ bad) {
+  const int64_t npairs = (S.n_rows + 63) / 64 * 32;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < npairs; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sl = t >> 5;
+    const int l0 = (int)(t & 31) * 2;
+    const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
+    uint32_t vi[2][5];
+    for (int h = 0; h < 2; ++h) {
+      for (int u = 0; u < 5; ++u) vi[h][u] = (uint32_t)zero_vi;
+      int prev = -1;
+      for (int64_t j = 0; j < w; ++j) {
+        const int code = S.codes[base + 64 * j + l0 + h];
+        const double2 q = S.dict[code];
+        if ((__double_as_longlong(q.x) & 0x7fffffffffffffffll) == 0) continue;
+        const int64_t off = (int64_t)__double_as_longlong(q.y);
+        const int cls = off == -line ? 0 : off == -1 ? 1 : off == 0 ? 2 : off == 1 ? 3 : off == line ? 4 : -1;
+        if (cls <= prev) {
+          atomicOr(bad, 1u);
+          return;
+        }
+        prev = cls;
+        vi[h][cls] = (uint32_t)(code / nd);
+      }
+    }
+    for (int u = 0; u < 5; ++u) dia[(sl * 5 + u) * 32 + (l0 >> 1)] = (uint8_t)(vi[0][u] | (vi[1][u] << 4));
+  }
+}
+
+// dvals[a] = value a of the c8 dictionary (dict[a * nd].x), zero-padded to 16
+__global__ void k_dia_vals(const double2* __restrict__ dict, int nv, int nd, double* __restrict__ dvals) {
+  const int a = threadIdx.x;
+  if (a < 16) dvals[a] = a < nv ? dict[a * nd].x : 0.0;
 }
 
 }  // namespace
@@ -364,16 +446,46 @@ void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipS
   MCG_HIP(hipGetLastError(), "kernel launch failed(slice_meta)");
 }
 
+bool sell_to_dia4(const SellDev& S, int nd, int64_t line, uint8_t* dia4, double* dvals, hipStream_t stream) {
+  MCG_CHECK(S.codes != nullptr && S.dict != nullptr && nd > 0 && S.ndict % nd == 0, "dia4: c8 dictionary missing");
+  const int nv = S.ndict / nd;
+  if (nv > 16 || line <= 1 || line > INT32_MAX) return false;
+  // the padding value +0.0 is always in the (sorted) value list
+  std::vector<double2> dict(S.ndict);
+  MCG_HIP(hipMemcpyAsync(dict.data(), S.dict, dict.size() * sizeof(double2), hipMemcpyDeviceToHost, stream),
+          "memcpy from device to host failed(A)");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(A)");
+  int zero_vi = -1;
+  for (int a = 0; a < nv; ++a)
+    if (dict[(size_t)a * nd].x == 0.0 && !std::signbit(dict[(size_t)a * nd].x)) zero_vi = a;
+  if (zero_vi < 0) return false;
+  unsigned* bad = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&bad), sizeof(unsigned), stream), "device malloc failed(dia4)");
+  MCG_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), stream), "device memset failed");
+  const int64_t npairs = (S.n_rows + 63) / 64 * 32;
+  if (npairs > 0)
+    hipLaunchKernelGGL(k_sell_to_dia4, dim3((unsigned)std::min<int64_t>((npairs + 255) / 256, 65536)), dim3(256), 0,
+                       stream, S, nd, line, zero_vi, dia4, bad);
+  hipLaunchKernelGGL(k_dia_vals, dim3(1), dim3(64), 0, stream, S.dict, nv, nd, dvals);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(dia4)");
+  unsigned h = 0;
+  MCG_HIP(hipMemcpyAsync(&h, bad, sizeof(unsigned), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(dia4)");
+  (void)hipFreeAsync(bad, stream);
+  return h == 0;
+}
+
 void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol, int first,
                  int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
-  MCG_CHECK((cm == 2 || cm == 3) && param >= 4 && param <= 5 && S.dict != nullptr,
-            "Ap-recomputing carry: SELL-64/c8 or /c4 rows of at most 5 entries");
+  MCG_CHECK((cm == 2 || cm == 3 || cm == 4) && param >= 4 && param <= 5 && S.dict != nullptr,
+            "Ap-recomputing carry: SELL-64/c8, /c4 or /dia4 rows of at most 5 entries");
   MCG_CHECK(cm != 3 || S.codes4 != nullptr, "Ap-recomputing carry: 4-bit codes missing");
-  MCG_CHECK(final_mode || S.smeta != nullptr, "Ap-recomputing carry: slice metadata missing");
+  MCG_CHECK(cm != 4 || (S.dia4 != nullptr && S.dvals != nullptr), "Ap-recomputing carry: dia4 codes missing");
+  MCG_CHECK(final_mode || cm == 4 || S.smeta != nullptr, "Ap-recomputing carry: slice metadata missing");
   MCG_CHECK(v.ape_old != nullptr && v.ape_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
             "Ap-recomputing carry: vectors missing");
   MCG_CHECK((v.ap_old == nullptr) == (v.ap_new == nullptr), "Ap-recomputing carry: boundary Ap buffers");
@@ -382,9 +494,10 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   if (final_mode) {
     const int64_t n = tr.nt0 * 64;
 #define MCG_AF(CM, U)                                                                                        \
-  hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, partials, pstride, \
-                     st, tol, first, check, k)
-    if (cm == 3) { if (param == 4) MCG_AF(3, 4); else MCG_AF(3, 5); }
+  hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, \
+                     (int32_t)(tr.strip * 64), partials, pstride, st, tol, first, check, k)
+    if (cm == 4) MCG_AF(4, 5);
+    else if (cm == 3) { if (param == 4) MCG_AF(3, 4); else MCG_AF(3, 5); }
     else { if (param == 4) MCG_AF(2, 4); else MCG_AF(2, 5); }
 #undef MCG_AF
     MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
@@ -407,7 +520,8 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     else if (qd == 4) MCG_AP(CM, U, 4);       \
     else MCG_AP(CM, U, 5);                    \
   } while (0)
-  if (cm == 3) { if (param == 4) MCG_AQ(3, 4); else MCG_AQ(3, 5); }
+  if (cm == 4) MCG_AQ(4, 5);
+  else if (cm == 3) { if (param == 4) MCG_AQ(3, 4); else MCG_AQ(3, 5); }
   else { if (param == 4) MCG_AQ(2, 4); else MCG_AQ(2, 5); }
 #undef MCG_AQ
 #undef MCG_AP

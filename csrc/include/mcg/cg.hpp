@@ -85,6 +85,10 @@ struct CgOptions {
                              // storing {r, Ap} pairs (r and p read once, written once: ~16 B/row less;
                              // cg_carry_ar.hip); -1 = auto (when the specialised 2-D carry covers every row
                              // in one launch), 0 = off, 1 = required
+  int carry_dia = -1;        // Ap-recomputing 2-D carry: SELL-64/dia4 storage (slot u = the u-th canonical offset
+                             // -line, -1, 0, +1, +line; 4-bit value indices), so the pass neither decodes offsets
+                             // nor selects operands per entry; -1 = auto (when every entry's offset is canonical
+                             // and in ascending order, <= 16 distinct values), 0 = off (c4 codes), 1 = required
   int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
                              // right after pass k wrote it (side stream, next to the all-reduce) and run one
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's

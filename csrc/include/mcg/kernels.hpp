@@ -102,6 +102,13 @@ struct SellDev {
   const int32_t* perm = nullptr;
   // Ap-recomputing line carry: per slice (first slot / 64) | (width << 28) (slice_meta)
   const uint32_t* smeta = nullptr;
+  // SELL-64/dia4 (Ap-recomputing 2-D line carry, sell_to_dia4): every slice has 5 slots, slot u
+  // of a row holding its entry at the u-th canonical column offset (-line, -1, 0, +1, +line) as a
+  // 4-bit index into `dvals` (an absent entry indexes +0.0).  Slice s, slot u: 32 bytes at
+  // (5 s + u) * 32, lanes 2i / 2i+1 in one byte.  Diagonal-slot storage (DIA inside SELL): the
+  // column offset is the slot's, so the pass needs no per-entry offset decode or operand select.
+  const uint8_t* dia4 = nullptr;
+  const double* dvals = nullptr;
   // SELL-64/aligned (long rows whose slices share their column offsets, e.g. the wide random-SPD
   // family): entry j of EVERY lane of slice s is the row's own column + soffs[slice_ptr[s] / 64 + j]
   // (one wave-uniform offset per slot, clamped to [0, ext_len); absent entries hold 0.0), so a
@@ -253,7 +260,14 @@ bool carry_block_exchange_ok(int param, int32_t lo2, int64_t strip);
 // 2-D stencils (offsets 0, +-1, +-one line), SELL-64/c8 (cm 2) or /c4 (cm 3), <= 5 entries per
 // row, one launch over the rank's whole lines.  final_mode: finalize()'s r_m / x_m pass.
 void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipStream_t stream);
-void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
+// SELL-64/c8 (S.codes, S.dict with nd distinct offsets) -> SELL-64/dia4 (`dia4`: 160 B per slice,
+// `dvals`: <= 16 doubles).  False (nothing usable written) when a nonzero entry's offset is not
+// one of 0, +-1, +-line, a row's nonzero offsets are not strictly increasing in slot order (the
+// dia4 sum must add the same products in the same order as the slot-order sum), or there are more
+// than 16 distinct values.
+bool sell_to_dia4(const SellDev& S, int nd, int64_t line, uint8_t* dia4, double* dvals, hipStream_t stream);
+// cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals)
+void cg_carry_ar(int cm,int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& slices, double* partials, int pstride, int grid, CgState* st, double tol,
                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl());
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,

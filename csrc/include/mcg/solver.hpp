@@ -65,6 +65,7 @@ struct SolverInfo {
   int comm_cus = 0;           // CUs withheld from the compute stream for the side stream's RCCL kernels
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
+  bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
   double placement_gain = 1.0;  // slowest / fastest of the timed placements (the fastest is kept)
@@ -97,7 +98,8 @@ class GpuCgSolver {
   double true_residual_norm();      // ||b - A x||_2 over all ranks (syncs)
   // Diagnostic: run `iters` more single-reduction iterations eagerly with hipEvents at every
   // phase boundary (halo on the side stream, interior / boundary passes, reduce, all-reduce) and
-  // return the mean microseconds per phase.  Advances the solver like run_iterations().
+  // return the mean microseconds per phase (the first iteration is an untimed warm-up when iters > 1).
+  // Advances the solver like run_iterations().
   std::vector<std::pair<std::string, double>> phase_profile(int iters);
 
   const SolverInfo& info() const { return info_; }
@@ -158,6 +160,8 @@ class GpuCgSolver {
   DeviceBuffer<uint8_t> codes_;  // SELL-64/c8 dictionary codes
   DeviceBuffer<double2> dict_;
   DeviceBuffer<uint8_t> codes4_;  // SELL-64/c4 copy of the codes (line-carry pass, <= 16 dictionary entries)
+  DeviceBuffer<uint8_t> dia4_;    // SELL-64/dia4 copy (Ap-recomputing carry; 160 B per slice)
+  DeviceBuffer<double> dvals_;    // ... its value table (16 doubles)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
   DeviceBuffer<int32_t> soffs_;   // SELL-64/aligned per-slot column offsets
   bool aligned_ = false;
@@ -185,6 +189,8 @@ class GpuCgSolver {
     s.ext_len = L_.ext_len;
     s.local_slots = lslots_.get();
     s.smeta = smeta_.get();
+    s.dia4 = dia4_.get();
+    s.dvals = dvals_.get();
     return s;
   }
   // vectors

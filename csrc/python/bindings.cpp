@@ -215,6 +215,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ag_overlap", &CgOptions::ag_overlap)
       .def_readwrite("halo_ahead", &CgOptions::halo_ahead)
       .def_readwrite("ap_recompute", &CgOptions::ap_recompute)
+      .def_readwrite("carry_dia", &CgOptions::carry_dia)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
@@ -393,6 +394,7 @@ PYBIND11_MODULE(_C, m) {
         d["comm_cus"] = i.comm_cus;
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;
+        d["dia4"] = i.dia4;
         d["carry_xchg"] = i.carry_xchg;
         d["placement_sets"] = i.placement_sets;
         d["placement_gain"] = i.placement_gain;

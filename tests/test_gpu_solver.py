@@ -259,24 +259,30 @@ def test_line_carry_c4_codes_match_c8(mcg):
     """4-bit dictionary codes (<= 16 entries: the 2-D 5-pt operator's 15) read by the line-carry pass:
     the same entries as c8, so the same bits."""
     spec = mcg.make_problem("poisson2d", n=256, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=1, check_every=8)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=0, check_every=8)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=1, carry_dia=0, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=0, carry_dia=0, check_every=8)
     assert a.info["codes4"] and not b.info["codes4"]
     ra, rb = a.solve(), b.solve()
     assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
     np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
 
 
-@pytest.mark.parametrize("c4", [1, 0])
+@pytest.mark.parametrize("codes", ["dia4", "c4", "c8"])
 @pytest.mark.parametrize("n", [128, 256])
-def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, c4, n):
+def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     """The line-carry pass that recomputes Ap_{k-1} = A p_{k-1} (same entries, same fma order, same
     p values) instead of storing {r, Ap} pairs: every r, p, x and dot product is the same bits, to
-    convergence and at fixed odd / even iteration counts (final pass, paired x updates)."""
+    convergence and at fixed odd / even iteration counts (final pass, paired x updates).  With the
+    SELL-64/dia4 storage (slot = canonical offset, absent entries exact zeros) the row sums add the
+    same products in the same order, so it is bitwise equal too."""
     spec = mcg.make_problem("poisson2d", n=n, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=1, check_every=8)
+    c4 = 0 if codes == "c8" else 1
+    dia = 1 if codes == "dia4" else 0
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=1, carry_dia=dia,
+                     check_every=8)
     b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=0, check_every=8)
     assert a.info["ap_recompute"] and not a.info["interleave"]
+    assert a.info["dia4"] == (codes == "dia4") and a.info["codes4"] == (codes == "c4")
     assert not b.info["ap_recompute"] and b.info["interleave"]
     ra, rb = a.solve(), b.solve()
     assert ra["converged"] and ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
@@ -302,6 +308,9 @@ def test_ap_recompute_auto_and_refusal(mcg):
     assert not s3.info["ap_recompute"]
     with pytest.raises(Exception, match="ap_recompute"):
         mcg.CGSolver(mcg.make_problem("poisson2d", n=100), format="sellc8", recurrence=1, ap_recompute=1)
+    assert s2.info["dia4"]  # auto: the 5-pt operator's entries sit at the canonical offsets
+    with pytest.raises(Exception, match="carry_dia"):
+        mcg.CGSolver(mcg.make_problem("poisson3d", n=32), format="sellc8", recurrence=1, carry_dia=1)
 
 
 @pytest.mark.parametrize("problem,n", [("poisson2d", 256), ("poisson3d", 40)])
