@@ -229,6 +229,28 @@ def recipes(a) -> dict:
             ("sim8_dia", 200, f"{PY} bench.py --sim-world 8 --sim-rank 3 --steps 400 --warmup 40"),
             ("sim8_c4", 200, f"{PY} bench.py --sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --set carry_dia=0"),
         ],
+        # counters of the dia4 pass (VALU issue, wave cycles) and its HBM bytes, one group per run
+        "diapmc": [
+            ("valu", 120, prof("diapmc_valu", f"{PY} {ROOT}/bench.py --steps 8 --warmup 2 --phases 0 --no-verify",
+                               "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU "
+                               "SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS")),
+            ("bytes", 120, prof("diapmc_bytes", f"{PY} {ROOT}/bench.py --steps 8 --warmup 2 --phases 0 --no-verify",
+                                "TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum GRBM_GUI_ACTIVE")),
+            ("trace", 200, prof("diatrace", f"{PY} {ROOT}/bench.py --steps 64 --warmup 8 --phases 0")),
+        ],
+        # 3-D Ap-recomputing plane carry (dia4, +-N rows through LDS): tests, kw sweep, store form, P = 8 share
+        "ar3": [
+            ("pytest", 600, f"{PY} -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_solver.py "
+                            f"tests/test_gpu_multirank.py -m gpu -k 'ap_recompute or halo_ahead or carry'"),
+            ("kw8", 200, bench("--problem poisson3d --grid 512")),
+            ("kw4", 200, bench("--problem poisson3d --grid 512 --set carry3_kw=4")),
+            ("kw16", 200, bench("--problem poisson3d --grid 512 --set carry3_kw=16")),
+            ("store", 200, bench("--problem poisson3d --grid 512 --set ap_recompute=0")),
+            ("kw8_b", 200, bench("--problem poisson3d --grid 512")),
+            ("sim8", 200, bench("--problem poisson3d --grid 512 --sim-world 8 --sim-rank 3 --steps 400 --warmup 40")),
+            ("sim8_store", 200, bench("--problem poisson3d --grid 512 --sim-world 8 --sim-rank 3 --steps 400 "
+                                      "--warmup 40 --set ap_recompute=0")),
+        ],
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),
             ("r512", 600, f"{PY} bench/rehearse_ranks.py --problem poisson3d --n 512 --iters 20 --world 1 2 4 8 "

@@ -72,10 +72,10 @@ __device__ __forceinline__ void ar_load_codes(const SellDev& S, int64_t base, in
   }
 }
 
-// SELL-64/dia4: the 5 value indices of slice row `lane` (slot u at bit 4 u); sp = the slice's 160 B
+// SELL-64/dia4: the U value indices of slice row `lane` (slot u at bit 4 u); sp = the slice's 32 U bytes
 template <int U>
 __device__ __forceinline__ void ar_load_dia(const uint8_t* __restrict__ sp, int lane, ArCodes<4, U>& c) {
-  static_assert(U == 5, "dia4: the five canonical 2-D offsets");
+  static_assert(U == 5 || U == 7, "dia4: the five (2-D) or seven (3-D) canonical offsets");
   c.w = U;
   const int sh = (lane & 1) * 4;
   uint32_t pk = 0u;
@@ -350,10 +350,286 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
+// ---------------------------------------------------------------------------
+// 3-D (7-pt) Ap-recomputing plane carry: the carried "line" is a plane (LO = N^2 rows), the
+// matrix SELL-64/dia4 with the seven canonical offsets (-N^2, -N, -1, 0, +1, +N, +N^2).  A block
+// of KW waves walks KW consecutive grid lines (y) of one x slice down the rank's planes (the 3-D
+// store-form pass's block exchange, k_cg_f1_carry M2 == 2): the +-N neighbours of a wave's rows are
+// the previous / next wave's rows, exchanged through LDS once per step (p_{k-1} of plane m + 1 for
+// the recomputation of Ap_{k-1}, p_k of plane m for Ap_k).  The block's first / last wave take the
+// grid line outside the block from memory -- its r, p and Ap_{k-1}, gathered two planes ahead --
+// so Ap is stored (ext layout, v.ap_new) only where a neighbour needs it: the block's outer lines,
+// the slices' edge rows (lanes 0 / 63, the x neighbours of other blocks' rows) and, at P > 1
+// (gfull), the rank's first / last plane (the halo carries {r, Ap, p} of the ghost planes).
+// Per row and iteration: r, p read + written once (32 B), x every second pass (12 B), Ap of 2 of
+// KW lines written and read (4 B at KW = 8), 3.5 B of codes: ~52 B instead of the store form's 67.
+
+// the KW-wave block's four fixed-order partials (block_partial4 for KW waves) + the in-kernel reduction
+template <int KW>
+__device__ __forceinline__ void ar3_finish(double a0, double a1, double a2, double a3, double* __restrict__ out,
+                                           int pstride, const RedCtl& rc, CgState* st, double tol) {
+  __shared__ double sh[4][KW];
+  a0 = eng::wave_sum(a0);
+  a1 = eng::wave_sum(a1);
+  a2 = eng::wave_sum(a2);
+  a3 = eng::wave_sum(a3);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = a0;
+    sh[1][w] = a1;
+    sh[2][w] = a2;
+    sh[3][w] = a3;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) t += sh[threadIdx.x][k];
+    if (rc.ngroups > 0) st_wt(&out[threadIdx.x * pstride + blockIdx.x], t);
+    else out[threadIdx.x * pstride + blockIdx.x] = t;
+  }
+  if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
+}
+
+template <int QD, bool PAIR, int KW>
+__global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+                                                                  int32_t LN, int gfull,
+                                                                  double* __restrict__ partials, int pstride,
+                                                                  CgState* st, double tol, int first, int check,
+                                                                  RedCtl rc) {
+  static_assert(KW >= 2 && QD >= 2, "3-D carry: >= 2 waves per block, operands >= 2 planes ahead");
+  constexpr int U = 7;
+  __shared__ double s_val[16];
+  __shared__ double s_x[2][2][KW][64];  // [step parity][p_{k-1}(m+1), p_k(m)][wave][lane]
+  const F1Scalars sc = f1_scalars(st, tol, first, check);
+  if (st->done || sc.conv) {
+    ar3_finish<KW>(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+    return;
+  }
+  if (threadIdx.x < 16) s_val[threadIdx.x] = S.dvals[threadIdx.x];
+  __syncthreads();
+  const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  const double* __restrict__ ro = v.r_old;
+  const double* __restrict__ po = v.p_old;
+  double* __restrict__ rn = v.r_new;
+  double* __restrict__ pn = v.p_new;
+  double* __restrict__ x = v.x;
+  const double* __restrict__ apo = v.ap_old;  // Ap_{k-1}: outer lines, edge rows, ghost planes
+  double* __restrict__ apw = v.ap_new;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t SS = tr.strip;            // slices per plane
+  const int32_t LO = (int32_t)(SS * 64);  // one plane
+  const int64_t nl = tr.nt0 / SS;         // the rank's planes
+  const int64_t G = LN / 64;              // slices per grid line
+  const int64_t jpr = (LN / KW) * G;      // jobs (y group, x slice) per run of planes
+  const int64_t nb = gridDim.x, blk = blockIdx.x;
+  const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;  // XCD-aware (k_cg_f1_carry)
+  const int64_t runs = nb > jpr ? nb / jpr : 1;
+  const int64_t chunk = (nl + runs - 1) / runs;
+  const int32_t ext32 = (int32_t)v.ext_len;
+  const bool ntl = v.nt_loads != 0;
+  const bool odn = wv == 0, oup = wv == KW - 1;  // outer waves: the line below / above the block
+  const int32_t fo = odn ? -LN : LN;
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+  struct Raw {
+    double r, p;
+  };
+  struct Edge {
+    double r, a, p;
+  };
+  struct XP {
+    double pkm2, xo;
+  };
+  struct Far {  // the outside line's row (outer waves): r, p, Ap of iteration k-1
+    double r, p, a;
+  };
+  auto stencil = [&](const ArCodes<4, U>& c, double mid, double edge, double dnl, double upl, double dnn, double upn) {
+    const double sh_up = lane_up(mid);
+    const double sh_dn = lane_dn(mid);
+    const double upv = lane == 63 ? edge : sh_up;
+    const double dnv = lane == 0 ? edge : sh_dn;
+    const double g[7] = {dnl, dnn, dnv, mid, upv, upn, upl};
+    double sum = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) sum = fma(s_val[(c.pk[0] >> (4 * u)) & 15u], g[u], sum);
+    return sum;
+  };
+  auto pk_of = [&](double r, double a_, double p) { return fma(b, p, fma(na, a_, r)); };
+  for (int64_t job = lb; job < jpr * runs; job += nb) {
+    const int64_t run = job / jpr, q = job % jpr;
+    const int64_t col = ((q / G) * KW + wv) * G + q % G;  // slice of grid line y = yg KW + wv, x slice q % G
+    const int64_t l0 = run * chunk;
+    const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
+    if (l0 >= l1) continue;  // block-uniform
+    const int64_t sl0 = l0 * SS + col;
+    const int32_t e0 = (int32_t)(own + sl0 * 64);
+    const int32_t i0 = (int32_t)(sl0 * 64);
+    const int32_t n_run = (int32_t)(l1 - l0);
+    const int32_t jmax = (ext32 - 64 - e0) / LO;
+    const int32_t jmin = -(e0 / LO);
+    auto ebase = [&](int32_t j) { return e0 + (j < jmin ? jmin : (j > jmax ? jmax : j)) * LO; };
+    auto owned = [&](int32_t j) { return l0 + j >= 0 && l0 + j < nl; };
+    auto oline = [&](int32_t j) {
+      const int64_t L = l0 + j;
+      return L < 0 ? (int64_t)0 : (L >= nl ? nl - 1 : L);
+    };
+    auto clampr = [&](int32_t e) { return e < 0 ? 0 : (e >= ext32 ? ext32 - 1 : e); };
+    auto load_raw = [&](int32_t j, Raw& r) {
+      const int32_t e = ebase(j) + lane;
+      r.r = ld_once(ro + e, ntl);
+      r.p = ld_once(po + e, ntl);
+    };
+    auto load_edge = [&](int32_t j, Edge& r) {
+      const int32_t e = ebase(j);
+      if (lane == 0 || lane == 63) {
+        const int32_t row = clampr(lane == 0 ? e - 1 : e + 64);
+        r.r = ro[row];
+        r.p = po[row];
+        r.a = apo[row];
+      }
+    };
+    auto load_far = [&](int32_t j, Far& f) {
+      if (odn || oup) {
+        const int32_t row = clampr(ebase(j) + lane + fo);
+        f.r = ro[row];
+        f.p = po[row];
+        f.a = apo[row];
+      }
+    };
+    auto load_xp = [&](int32_t j, XP& r) {
+      if constexpr (PAIR) {
+        const int32_t mm = j < n_run - 1 ? j : n_run - 1;
+        r.pkm2 = ld_once(pn + e0 + mm * LO + lane, ntl);
+        r.xo = ld_once(x + i0 + mm * LO + lane, ntl);
+      }
+    };
+    auto load_codes = [&](int32_t j, ArCodes<4, U>& c) {
+      ar_load_dia<U>(S.dia4 + (oline(j) * SS + col) * (32 * U), lane, c);
+    };
+    auto ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jmin && j <= jmax; };
+    auto edge_pk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
+    // neighbour waves' values through LDS (outer waves: `far` for the side outside the block)
+    auto nbr = [&](int par, int which, double far, double& dn, double& up) {
+      const double* sx = &s_x[par][which][0][lane];
+      const double vd = sx[(odn ? wv : wv - 1) * 64], vu = sx[(oup ? wv : wv + 1) * 64];
+      dn = odn ? far : vd;
+      up = oup ? far : vu;
+    };
+
+    __syncthreads();  // the previous job's last step has read its LDS slots
+    // prologue: planes -2 .. QD, edges / codes of -1 .. 1, the outside rows of -1 .. 1
+    Raw rm2, rm1, r0, rq[QD];
+    load_raw(-2, rm2);
+    load_raw(-1, rm1);
+    load_raw(0, r0);
+#pragma unroll
+    for (int d = 0; d < QD; ++d) load_raw(1 + d, rq[d]);
+    Edge edm1{0.0, 0.0, 0.0}, ed0{0.0, 0.0, 0.0}, ed1{0.0, 0.0, 0.0};
+    load_edge(-1, edm1);
+    load_edge(0, ed0);
+    load_edge(1, ed1);
+    ArCodes<4, U> cm1, c0, c1;
+    load_codes(-1, cm1);
+    load_codes(0, c0);
+    load_codes(1, c1);
+    Far fm1{0.0, 0.0, 0.0}, f0{0.0, 0.0, 0.0}, fa{0.0, 0.0, 0.0};
+    load_far(-1, fm1);
+    load_far(0, f0);
+    load_far(1, fa);
+    XP x0{0.0, 0.0};
+    load_xp(0, x0);
+    // p_{k-1} of planes -1 and 0 for the +-N neighbours of the prologue's recomputations
+    s_x[1][0][wv][lane] = rm1.p;
+    s_x[1][1][wv][lane] = r0.p;
+    __syncthreads();
+    double pr_pk = 0.0;
+    if (owned(-1)) {
+      double dn, up;
+      nbr(1, 0, fm1.p, dn, up);
+      const double t = stencil(cm1, rm1.p, edm1.p, rm2.p, r0.p, dn, up);
+      pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+    } else if (ghost(-1)) {
+      pr_pk = pk_of(rm1.r, apo[ebase(-1) + lane], rm1.p);
+    }
+    double o_pold = r0.p, o_rk, o_pk;
+    {
+      double dn, up;
+      nbr(1, 1, f0.p, dn, up);
+      const double t = stencil(c0, r0.p, ed0.p, rm1.p, rq[0].p, dn, up);
+      o_rk = fma(na, t, r0.r);
+      o_pk = fma(b, r0.p, o_rk);
+    }
+    double o_epk = edge_pk(ed0);
+    double o_fpk = pk_of(f0.r, f0.a, f0.p);  // p_k of the outside row, plane 0
+    for (int32_t m = 0; m < n_run; ++m) {
+      const int par = m & 1;
+      // 1. loads for later steps: codes / edges of plane m + 2, the outside row of m + 2, x / p_{k-2}
+      //    of m + 1, operands of m + 1 + QD
+      ArCodes<4, U> c2;
+      load_codes(m + 2, c2);
+      Edge ed2{0.0, 0.0, 0.0};
+      load_edge(m + 2, ed2);
+      Far fb{0.0, 0.0, 0.0};
+      load_far(m + 2, fb);
+      XP x1{0.0, 0.0};
+      load_xp(m + 1, x1);
+      Raw rnq;
+      load_raw(m + 1 + QD, rnq);
+      // 2. exchange: p_{k-1} of plane m + 1 and p_k of plane m with the neighbouring waves
+      s_x[par][0][wv][lane] = rq[0].p;
+      s_x[par][1][wv][lane] = o_pk;
+      __syncthreads();
+      // 3. r_k, p_k of plane m + 1: Ap_{k-1} recomputed (owned) or exchanged (ghost plane)
+      double rk1 = 0.0, pk1 = 0.0;
+      if (owned(m + 1)) {
+        double dn, up;
+        nbr(par, 0, fa.p, dn, up);
+        const double t = stencil(c1, rq[0].p, ed1.p, o_pold, rq[1].p, dn, up);
+        rk1 = fma(na, t, rq[0].r);
+        pk1 = fma(b, rq[0].p, rk1);
+      } else if (ghost(m + 1)) {
+        const double t = apo[ebase(m + 1) + lane];
+        rk1 = fma(na, t, rq[0].r);
+        pk1 = fma(b, rq[0].p, rk1);
+      }
+      // 4. Ap_k of plane m, stores, partials
+      double kdn, kup;
+      nbr(par, 1, o_fpk, kdn, kup);
+      const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1, kdn, kup);
+      const int32_t eb = e0 + m * LO;
+      st_stream(&(rn + eb)[lane], o_rk);
+      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, x0.pkm2, x0.xo)));
+      st_stream(&(pn + eb)[lane], o_pk);
+      if (odn || oup || lane == 0 || lane == 63 || (gfull && (l0 + m == 0 || l0 + m == nl - 1))) apw[eb + lane] = sum;
+      s_pap = fma(o_pk, sum, s_pap);
+      s_rap = fma(o_rk, sum, s_rap);
+      s_apap = fma(sum, sum, s_apap);
+      s_rr = fma(o_rk, o_rk, s_rr);
+      // 5. rotate
+      pr_pk = o_pk;
+      o_pk = pk1;
+      o_rk = rk1;
+      o_pold = rq[0].p;
+      o_epk = edge_pk(ed1);
+      o_fpk = pk_of(fa.r, fa.a, fa.p);
+      fa = fb;
+      ed1 = ed2;
+#pragma unroll
+      for (int d = 0; d + 1 < QD; ++d) rq[d] = rq[d + 1];
+      rq[QD - 1] = rnq;
+      x0 = x1;
+      c0 = c1;
+      c1 = c2;
+    }
+  }
+  ar3_finish<KW>(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+}
+
 // finalize(): r_m = r_{m-1} - a A p_{m-1} (recomputed, same fma order), x_m, partial ||r_m||^2;
 // or, when the run latched, the one-term x catch-up of an even m (k_cg_f1's final mode)
 template <int CM, int U>
-__global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_t own, int64_t n, int32_t lo,
+__global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_t own, int64_t n, int32_t lo, int32_t ln,
                                                   double* __restrict__ partials, int pstride, CgState* st,
                                                   double tol, int first, int check, int k) {
   const int done = st->done;
@@ -374,11 +650,13 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
     ArCodes<CM, U> c;
     double t = 0.0;
     if constexpr (CM == 4) {  // absent entries: value 0 times a clamped (finite) operand
-      ar_load_dia<U>(S.dia4 + (i >> 6) * 160, (int)(i & 63), c);
-      const int64_t offs[5] = {-(int64_t)lo, -1, 0, 1, (int64_t)lo};
+      ar_load_dia<U>(S.dia4 + (i >> 6) * (32 * U), (int)(i & 63), c);
+      const int64_t o5[5] = {-(int64_t)lo, -1, 0, 1, (int64_t)lo};
+      const int64_t o7[7] = {-(int64_t)lo, -(int64_t)ln, -1, 0, 1, (int64_t)ln, (int64_t)lo};
 #pragma unroll
-      for (int u = 0; u < 5; ++u) {
-        int64_t q = e + offs[u];
+      for (int u = 0; u < U; ++u) {
+        const int64_t off = U == 5 ? o5[u] : o7[u];
+        int64_t q = e + off;
         q = q < 0 ? 0 : (q >= v.ext_len ? v.ext_len - 1 : q);
         t = fma(S.dvals[(c.pk[0] >> (4 * u)) & 15u], v.p_old[q], t);
       }
@@ -403,23 +681,29 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
 // SELL-64/c8 -> /dia4: one thread per row pair (lanes 2i, 2i+1 of a slice share the bytes).
 // Entries with value +-0 (SELL padding) are skipped; any other entry must sit at a canonical
 // offset, in strictly increasing offset order along the row's slots (else `bad`).
-__global__ __launch_bounds__(256) void k_sell_to_dia4(SellDev S, int nd, int64_t line, int zero_vi,
+struct DiaOffs {
+  int64_t o[7];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_sell_to_dia4(SellDev S, int nd, DiaOffs co, int zero_vi,
                                                       uint8_t* __restrict__ dia, unsigned* __restrict__ bad) {
   const int64_t npairs = (S.n_rows + 63) / 64 * 32;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < npairs; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t sl = t >> 5;
     const int l0 = (int)(t & 31) * 2;
     const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
-    uint32_t vi[2][5];
+    uint32_t vi[2][7];
     for (int h = 0; h < 2; ++h) {
-      for (int u = 0; u < 5; ++u) vi[h][u] = (uint32_t)zero_vi;
+      for (int u = 0; u < 7; ++u) vi[h][u] = (uint32_t)zero_vi;
       int prev = -1;
       for (int64_t j = 0; j < w; ++j) {
         const int code = S.codes[base + 64 * j + l0 + h];
         const double2 q = S.dict[code];
         if ((__double_as_longlong(q.x) & 0x7fffffffffffffffll) == 0) continue;
         const int64_t off = (int64_t)__double_as_longlong(q.y);
-        const int cls = off == -line ? 0 : off == -1 ? 1 : off == 0 ? 2 : off == 1 ? 3 : off == line ? 4 : -1;
+        int cls = -1;
+        for (int u = 0; u < co.n; ++u)
+          if (off == co.o[u]) cls = u;
         if (cls <= prev) {
           atomicOr(bad, 1u);
           return;
@@ -428,7 +712,7 @@ __global__ __launch_bounds__(256) void k_sell_to_dia4(SellDev S, int nd, int64_t
         vi[h][cls] = (uint32_t)(code / nd);
       }
     }
-    for (int u = 0; u < 5; ++u) dia[(sl * 5 + u) * 32 + (l0 >> 1)] = (uint8_t)(vi[0][u] | (vi[1][u] << 4));
+    for (int u = 0; u < co.n; ++u) dia[(sl * co.n + u) * 32 + (l0 >> 1)] = (uint8_t)(vi[0][u] | (vi[1][u] << 4));
   }
 }
 
@@ -446,10 +730,21 @@ void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipS
   MCG_HIP(hipGetLastError(), "kernel launch failed(slice_meta)");
 }
 
-bool sell_to_dia4(const SellDev& S, int nd, int64_t line, uint8_t* dia4, double* dvals, hipStream_t stream) {
+bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* dia4, double* dvals,
+                  hipStream_t stream) {
   MCG_CHECK(S.codes != nullptr && S.dict != nullptr && nd > 0 && S.ndict % nd == 0, "dia4: c8 dictionary missing");
   const int nv = S.ndict / nd;
-  if (nv > 16 || line <= 1 || line > INT32_MAX) return false;
+  if (nv > 16 || line <= 1 || line > INT32_MAX || ln < 0 || (ln > 0 && (ln <= 1 || ln >= line))) return false;
+  DiaOffs co{};
+  if (ln == 0) {
+    const int64_t o[5] = {-line, -1, 0, 1, line};
+    co.n = 5;
+    for (int u = 0; u < 5; ++u) co.o[u] = o[u];
+  } else {
+    const int64_t o[7] = {-line, -ln, -1, 0, 1, ln, line};
+    co.n = 7;
+    for (int u = 0; u < 7; ++u) co.o[u] = o[u];
+  }
   // the padding value +0.0 is always in the (sorted) value list
   std::vector<double2> dict(S.ndict);
   MCG_HIP(hipMemcpyAsync(dict.data(), S.dict, dict.size() * sizeof(double2), hipMemcpyDeviceToHost, stream),
@@ -465,7 +760,7 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, uint8_t* dia4, double*
   const int64_t npairs = (S.n_rows + 63) / 64 * 32;
   if (npairs > 0)
     hipLaunchKernelGGL(k_sell_to_dia4, dim3((unsigned)std::min<int64_t>((npairs + 255) / 256, 65536)), dim3(256), 0,
-                       stream, S, nd, line, zero_vi, dia4, bad);
+                       stream, S, nd, co, zero_vi, dia4, bad);
   hipLaunchKernelGGL(k_dia_vals, dim3(1), dim3(64), 0, stream, S.dict, nv, nd, dvals);
   MCG_HIP(hipGetLastError(), "kernel launch failed(dia4)");
   unsigned h = 0;
@@ -495,7 +790,7 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     const int64_t n = tr.nt0 * 64;
 #define MCG_AF(CM, U)                                                                                        \
   hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, \
-                     (int32_t)(tr.strip * 64), partials, pstride, st, tol, first, check, k)
+                     (int32_t)(tr.strip * 64), 0, partials, pstride, st, tol, first, check, k)
     if (cm == 4) MCG_AF(4, 5);
     else if (cm == 3) { if (param == 4) MCG_AF(3, 4); else MCG_AF(3, 5); }
     else { if (param == 4) MCG_AF(2, 4); else MCG_AF(2, 5); }
@@ -526,6 +821,43 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
 #undef MCG_AQ
 #undef MCG_AP
 #undef MCG_A
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+
+void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
+                  int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
+                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc) {
+  if (tr.ntiles == 0 || grid == 0) return;
+  MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0 && ln % 64 == 0 &&
+                (int64_t)ln * ln == (int64_t)tr.strip * 64 && (kw == 4 || kw == 8 || kw == 16) && ln % kw == 0,
+            "3-D Ap-recomputing carry: one launch over the rank's whole planes, N a multiple of 64 and of the block");
+  MCG_CHECK(S.dia4 != nullptr && S.dvals != nullptr, "3-D Ap-recomputing carry: dia4 codes missing");
+  MCG_CHECK(v.ap_old != nullptr && v.ap_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
+            "3-D Ap-recomputing carry: vectors missing");
+  MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
+            "in-kernel reduction: bad control block");
+  if (final_mode) {
+    hipLaunchKernelGGL((k_ar_final<4, 7>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr.nt0 * 64,
+                       (int32_t)(tr.strip * 64), ln, partials, pstride, st, tol, first, check, k);
+    MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
+    return;
+  }
+  const bool pair = (k & 1) != 0;
+  const int qd = depth >= 3 ? 3 : 2;
+  const int g = gfull ? 1 : 0;
+#define MCG_A3(QD, PAIR, KW)                                                                                   \
+  hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW>), dim3(grid), dim3(64 * KW), 0, stream, S, v, own_off, tr, ln, \
+                     g, partials, pstride, st, tol, first, check, rc)
+#define MCG_A3K(QD, PAIR)                       \
+  do {                                          \
+    if (kw == 4) MCG_A3(QD, PAIR, 4);           \
+    else if (kw == 8) MCG_A3(QD, PAIR, 8);      \
+    else MCG_A3(QD, PAIR, 16);                  \
+  } while (0)
+  if (qd == 2) { if (pair) MCG_A3K(2, true); else MCG_A3K(2, false); }
+  else { if (pair) MCG_A3K(3, true); else MCG_A3K(3, false); }
+#undef MCG_A3K
+#undef MCG_A3
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 

@@ -514,11 +514,39 @@ void GpuCgSolver::setup() {
     }
     info_.carry = carry_all_ || carry_int_;
     // Ap recomputed instead of stored: the specialised 2-D pass over every owned line in one launch
-    // (with a split launch the boundary rows' generic pass would need the stored Ap)
-    ar_ = opt_.ap_recompute != 0 && carry_all_ && !carry_general_ && carry_lo2_ == 0 && c8_ && !split_ &&
-          info_.spmv_param <= 5 && tr_all_.b0 == 0 && tr_all_.strip > 0;
+    // (with a split launch the boundary rows' generic pass would need the stored Ap); 3-D: the plane
+    // carry with +-N through LDS, on SELL-64/dia4 only
+    const bool ar_any = opt_.ap_recompute != 0 && carry_all_ && !carry_general_ && c8_ && !split_ &&
+                        tr_all_.b0 == 0 && tr_all_.strip > 0;
+    const int kw = opt_.carry3_kw;
+    const bool ar2 = ar_any && carry_lo2_ == 0 && info_.spmv_param <= 5;
+    const bool ar3 = ar_any && carry_lo2_ > 0 && carry_lo2_ % 64 == 0 && info_.spmv_param <= 7 &&
+                     opt_.carry_dia != 0 && (kw == 4 || kw == 8 || kw == 16) && carry_lo2_ % kw == 0 &&
+                     (int64_t)carry_lo2_ * carry_lo2_ == gl;
+    MCG_CHECK(opt_.carry_dia != 1 || ar2 || ar3,
+              "carry_dia needs the Ap-recomputing line / plane carry (ap_recompute)");
+    if ((ar2 || ar3) && opt_.carry_dia != 0 && n > 0) {  // SELL-64/dia4 from the c8 codes (replaces c4 + metadata)
+      const int64_t ns = (n + 63) / 64;
+      const int nslot = ar3 ? 7 : 5;
+      dia4_.allocate(ns * 32 * nslot, "A", 256);
+      dvals_.allocate(16, "A");
+      const bool ok = kern::sell_to_dia4(sell_view(), (int)dict_offsets_.size(), (int64_t)tr_all_.strip * 64,
+                                         ar3 ? (int64_t)carry_lo2_ : 0, dia4_.get(), dvals_.get(), s0_);
+      MCG_CHECK(ok || opt_.carry_dia != 1, "carry_dia: the matrix is not a canonical 2-D 5-point / 3-D 7-point pattern");
+      if (ok) {
+        codes4_.release();
+      } else {
+        dia4_.release();
+        dvals_.release();
+      }
+    }
+    ar3_ = ar3 && dia4_.get() != nullptr;
+    ar_ = ar2 || ar3_;
     MCG_CHECK(opt_.ap_recompute != 1 || ar_,
-              "ap_recompute needs the specialised 2-D line-carry pass over all lines (c8, <= 5 entries per row)");
+              "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
+              "3-D: dia4, N a multiple of 64 and of carry3_kw)");
+    if (ar3_) g_all_ = ncu_ * 4 * 4 / kw;  // 4 waves per SIMD
+    info_.ar3_kw = ar3_ ? kw : 0;
     info_.carry_xchg = info_.carry && carry_lo2_ > 0 && opt_.carry_3d == 2 &&
                        kern::carry_block_exchange_ok(info_.spmv_param, carry_lo2_, gl / 64);
     if (!info_.carry || carry_general_ || carry_lo2_ != 0) codes4_.release();  // only the 2-D carry reads them
@@ -531,22 +559,6 @@ void GpuCgSolver::setup() {
   }
   info_.ap_recompute = ar_;
   info_.interleave = opt_.interleave == 1;
-  MCG_CHECK(opt_.carry_dia != 1 || ar_, "carry_dia needs the Ap-recomputing 2-D line carry (ap_recompute)");
-  if (ar_ && opt_.carry_dia != 0 && n > 0) {  // SELL-64/dia4 from the c8 codes (replaces c4 + slice metadata)
-    const int64_t ns = (n + 63) / 64;
-    dia4_.allocate(ns * 160, "A", 256);
-    dvals_.allocate(16, "A");
-    const bool ok = kern::sell_to_dia4(sell_view(), (int)dict_offsets_.size(), (int64_t)tr_all_.strip * 64,
-                                       dia4_.get(), dvals_.get(), s0_);
-    MCG_CHECK(ok || opt_.carry_dia != 1, "carry_dia: the matrix is not a canonical 2-D 5-point pattern");
-    if (ok) {
-      codes4_.release();
-      info_.codes4 = false;
-    } else {
-      dia4_.release();
-      dvals_.release();
-    }
-  }
   info_.dia4 = dia4_.get() != nullptr;
   if (ar_ && !info_.dia4 && n > 0) {
     const int64_t ns = (n + 63) / 64;
@@ -598,7 +610,11 @@ void GpuCgSolver::setup() {
     info_.bytes_per_iter_model = (double)matrix_bytes + 80.0 * n;
     info_.device_bytes = matrix_bytes + (size_t)(4 * n + L_.ext_len) * 8 + rp64_.bytes();
   }
-  if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
+  if (ar3_) {  // r rw, p rw 32; x 12; Ap of 2 of kw lines written + read, edge rows 0.5; dia4 codes 3.5
+    info_.bytes_per_iter_model = (double)dia4_.bytes() + (44.5 + 16.0 / info_.ar3_kw) * n;
+    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes();
+    for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
+  } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
     const double streamed = info_.dia4 ? (double)dia4_.bytes()
                                        : (codes4_.get() ? (double)codes4_.bytes() + 4.0 * (double)smeta_.size()
                                                         : (double)matrix_bytes);
@@ -649,9 +665,11 @@ void GpuCgSolver::allocate_vectors_() {
     r_.allocate(L_.ext_len, "r", 8, 2 * skew, cap);
     r1_.allocate(L_.ext_len, "r", 8, 3 * skew, cap);
     const int64_t ns = (n + 63) / 64;
-    ape_[0].allocate(2 * std::max<int64_t>(ns, 1), "Ap", 8);
-    ape_[1].allocate(2 * std::max<int64_t>(ns, 1), "Ap", 8);
-    if (use_halo_) {
+    if (!ar3_) {  // 3-D: the slices' edge rows go through the ext-layout Ap like the outer lines
+      ape_[0].allocate(2 * std::max<int64_t>(ns, 1), "Ap", 8);
+      ape_[1].allocate(2 * std::max<int64_t>(ns, 1), "Ap", 8);
+    }
+    if (use_halo_ || ar3_) {
       apx_[0].allocate(L_.ext_len, "Ap", 8);
       apx_[1].allocate(L_.ext_len, "Ap", 8);
     }
@@ -891,6 +909,12 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     v.ap_new = apx_[k & 1].get();
     v.ape_old = ape_[(k + 1) & 1].get();
     v.ape_new = ape_[k & 1].get();
+    if (ar3_) {
+      kern::cg_carry_ar3(opt_.carry_depth > 0 ? opt_.carry_depth : 2, info_.ar3_kw, S, v, L_.own_off, tr,
+                         carry_lo2_, use_halo_, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode,
+                         s0_, rc);
+      return;
+    }
     kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, opt_.carry_depth > 0 ? opt_.carry_depth : 3, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc);
     return;

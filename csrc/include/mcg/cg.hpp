@@ -89,6 +89,9 @@ struct CgOptions {
                              // -line, -1, 0, +1, +line; 4-bit value indices), so the pass neither decodes offsets
                              // nor selects operands per entry; -1 = auto (when every entry's offset is canonical
                              // and in ascending order, <= 16 distinct values), 0 = off (c4 codes), 1 = required
+  int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
+                             // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
+                             // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)
   int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
                              // right after pass k wrote it (side stream, next to the all-reduce) and run one
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's

@@ -265,7 +265,16 @@ void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipS
 // one of 0, +-1, +-line, a row's nonzero offsets are not strictly increasing in slot order (the
 // dia4 sum must add the same products in the same order as the slot-order sum), or there are more
 // than 16 distinct values.
-bool sell_to_dia4(const SellDev& S, int nd, int64_t line, uint8_t* dia4, double* dvals, hipStream_t stream);
+// ln = 0: the 2-D offsets (-line, -1, 0, +1, +line), 160 B per slice; ln > 0: the 3-D offsets
+// (-line, -ln, -1, 0, +1, +ln, +line), 224 B per slice
+bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* dia4, double* dvals,
+                  hipStream_t stream);
+// 3-D (7-pt) Ap-recomputing plane carry (SELL-64/dia4 with ln = N): blocks of kw (4 / 8 / 16) waves on
+// kw consecutive grid lines of one x slice; v.ap_old / ap_new = ext-layout Ap (outer lines, slice
+// edge rows, and with gfull the first / last plane for the ghosts); grid = blocks (any count)
+void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
+                  int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
+                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl());
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals)
 void cg_carry_ar(int cm,int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& slices, double* partials, int pstride, int grid, CgState* st, double tol,

@@ -66,6 +66,7 @@ struct SolverInfo {
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
+  int ar3_kw = 0;        // 3-D Ap-recomputing plane carry: waves (grid lines) per block; 0 = not in use
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
   double placement_gain = 1.0;  // slowest / fastest of the timed placements (the fastest is kept)
@@ -142,6 +143,7 @@ class GpuCgSolver {
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
   bool ar_ = false;             // CgOptions::ap_recompute in effect
+  bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool split_ = false;          // interior / boundary launches around an overlapped halo
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
   bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them

@@ -299,6 +299,42 @@ def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     assert a.true_residual_norm() == b.true_residual_norm()
 
 
+@pytest.mark.parametrize("n,kw", [(64, 4), (128, 4), (128, 8), (128, 16)])
+def test_ap_recompute_3d_matches_store_form(mcg, n, kw):
+    """3-D plane carry that recomputes Ap (SELL-64/dia4, +-N rows through LDS between the block's
+    kw waves, the outer lines' Ap stored): the same recurrence as the store-form plane carry.  With
+    kw = 4 the blocks, waves and rows are the store form's, so every bit agrees; other kw group the
+    dot-product partials differently (rounding only)."""
+    spec = mcg.make_problem("poisson3d", n=n, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=1, carry3_kw=kw, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=0, check_every=8)
+    assert a.info["ap_recompute"] and a.info["dia4"] and a.info["ar3_kw"] == kw
+    assert not b.info["ap_recompute"] and b.info["carry"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and abs(ra["iterations"] - rb["iterations"]) <= (0 if kw == 4 else 1)
+    if kw == 4:
+        assert ra["rnorm"] == rb["rnorm"]
+        np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+    else:
+        np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-9, atol=1e-12)
+    for its in (23, 24):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["iterations"] == its
+        if kw == 4:  # x is elementwise (same bits); ||r_m|| of the final pass sums rows in another grouping
+            assert abs(outs[0][0]["rnorm"] - outs[1][0]["rnorm"]) <= 1e-14 * outs[1][0]["rnorm"]
+            np.testing.assert_array_equal(outs[0][1], outs[1][1])
+        else:
+            assert abs(outs[0][0]["rnorm"] - outs[1][0]["rnorm"]) <= 1e-11 * outs[1][0]["rnorm"]
+            np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-10, atol=1e-13)
+    tr = a.true_residual_norm()
+    assert abs(tr - outs[0][0]["rnorm"]) <= 1e-8 * tr
+
+
 def test_ap_recompute_auto_and_refusal(mcg):
     """auto: on for the specialised 2-D carry; off where the carry is off (3-D generic) or the
     rows are not whole 64-row lines; required (=1) where it cannot apply: a clear error."""
