@@ -542,6 +542,13 @@ void GpuCgSolver::setup() {
     }
     ar3_ = ar3 && dia4_.get() != nullptr;
     ar_ = ar2 || ar3_;
+    // every rank takes the same pass form: it decides the vectors the halo carries ({r, Ap} pairs or
+    // r / Ap / p) and their widths (one all-reduce of a flag at setup, like pmat)
+    if (use_comm_ && world_ > 1 && !all_ranks_agree_(ar_) && ar_) {
+      ar_ = ar3_ = false;
+      dia4_.release();
+      dvals_.release();
+    }
     MCG_CHECK(opt_.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
               "3-D: dia4, N a multiple of 64 and of carry3_kw)");
