@@ -251,6 +251,28 @@ def recipes(a) -> dict:
             ("sim8_store", 200, bench("--problem poisson3d --grid 512 --sim-world 8 --sim-rank 3 --steps 400 "
                                       "--warmup 40 --set ap_recompute=0")),
         ],
+        "ar3pmc": [
+            ("valu", 120, prof("ar3pmc_valu", f"{PY} {ROOT}/bench.py --problem poisson3d --grid 512 --steps 8 --warmup 2 "
+                                              f"--phases 0 --no-verify",
+                               "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU "
+                               "SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS")),
+            ("bytes", 120, prof("ar3pmc_bytes", f"{PY} {ROOT}/bench.py --problem poisson3d --grid 512 --steps 8 "
+                                                f"--warmup 2 --phases 0 --no-verify",
+                                "TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum GRBM_GUI_ACTIVE")),
+            ("trace", 200, prof("ar3trace", f"{PY} {ROOT}/bench.py --problem poisson3d --grid 512 --steps 64 "
+                                            f"--warmup 8 --phases 0")),
+            ("sim8", 200, bench("--problem poisson3d --grid 512 --sim-world 8 --sim-rank 3 --steps 400 --warmup 40")),
+            ("qd3", 200, bench("--problem poisson3d --grid 512 --set carry_depth=3")),
+        ],
+        # knobs of the dia4 line carry on the headline grid
+        "diaknobs": [
+            ("nt", 200, bench("--set carry_nt=1")),
+            ("d2", 200, bench("--set carry_depth=2")),
+            ("d4", 200, bench("--set carry_depth=4")),
+            ("d5", 200, bench("--set carry_depth=5")),
+            ("base", 200, bench()),
+            ("nt3d", 200, bench("--problem poisson3d --grid 512 --set carry_nt=1")),
+        ],
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),
             ("r512", 600, f"{PY} bench/rehearse_ranks.py --problem poisson3d --n 512 --iters 20 --world 1 2 4 8 "

@@ -16,7 +16,7 @@ for d in sys.argv[1:]:
     for r in cur.execute("select * from counters_collection"):
         row = dict(zip(cols, r))
         name = str(row["kernel_name"])
-        if "k_cg_f1" not in name and "k_cg_carry_ar" not in name:
+        if "k_cg_f1" not in name and "k_cg_carry_ar" not in name:  # (k_cg_carry_ar3 included)
             continue
         k = re.search(r"(k_cg_(?:f1|carry_ar)\w*<[^>]*>)", name).group(1)
         agg[k][row["counter_name"]].append(row["value"])

@@ -195,8 +195,9 @@ void GpuCgSolver::setup() {
   const bool is_user = spec_.kind == ProblemKind::Csr;
   if (is_user) {
     user = build_local_csr(spec_, L_);
-    if (opt_.format == 1 && opt_.sell_sigma != 0 && n > 64) {
-      // SELL-C-sigma (int32 columns): the windows never mix interior and boundary slices
+    if (opt_.format == 1 && opt_.sell_sigma != 0 && n > 64 && (opt_.sell_sigma > 0 || stencil_line(spec_) == 0)) {
+      // SELL-C-sigma (int32 columns): the windows never mix interior and boundary slices (auto: not
+      // for a detected grid stencil, whose rows stay in grid order for the line / plane carry)
       const int64_t sig = opt_.sell_sigma > 1 ? (opt_.sell_sigma + 63) / 64 * 64 : 4096;
       std::vector<int64_t> cuts;
       if (use_halo_ && opt_.overlap && !L_.allgather) {
@@ -448,7 +449,7 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (opt_.xcd_map > 0) tr_all_.xcd = tr_int_.xcd = tr_bnd_.xcd = 8;
-  if (opt_.xcd_map < 0 && opt_.format == 1 && spec_.kind == ProblemKind::Poisson3D && win_doubles_ == 0 &&
+  if (opt_.xcd_map < 0 && opt_.format == 1 && stencil_plane(spec_) > 0 && win_doubles_ == 0 &&
       opt_.blocks_per_cu <= 0 && opt_.sell_slices != 2 && partition_granule(spec_) % 64 == 0) {
     // 3-D stencil, generic pass: XCD-aware sweep with one plane of slices per step.  Each XCD
     // walks a contiguous 1/8 of the slices with grid / 8 blocks x 4 waves = P slices (one plane)
@@ -471,7 +472,8 @@ void GpuCgSolver::setup() {
   if (opt_.format == 1 && opt_.sell_slices != 2 && win_doubles_ == 0) {
     // vertical-strip slice order: S = slices per grid line (2-D stencil, whole-slice lines)
     int64_t S = opt_.strip > 0 ? opt_.strip : 0;
-    if (opt_.strip < 0 && spec_.kind == ProblemKind::Poisson2D && spec_.N % 64 == 0) S = spec_.N / 64;
+    if (opt_.strip < 0 && stencil_plane(spec_) == 0 && stencil_line(spec_) > 0 && stencil_line(spec_) % 64 == 0)
+      S = stencil_line(spec_) / 64;
     auto apply = [&](TileRanges& t) {
       if (S > 0 && t.ntiles > 0 && t.nt0 == t.ntiles && t.ntiles % S == 0 && t.ntiles / S >= 2) t.strip = (int32_t)S;
     };
@@ -486,7 +488,7 @@ void GpuCgSolver::setup() {
     const bool ok = opt_.recurrence == 1 && opt_.format == 1 && (d16_ || c8_) && opt_.interleave == 1 &&
                     opt_.sell_slices != 2 && win_doubles_ == 0 && info_.max_row_len <= 8 &&
                     info_.spmv_param >= info_.max_row_len && info_.spmv_param >= 4 && gl > 1 && gl % 64 == 0 &&
-                    n % gl == 0 && L_.row_begin % gl == 0;
+                    n % gl == 0 && L_.row_begin % gl == 0 && !perm_.get();
     MCG_CHECK(opt_.carry != 1 || ok,
               "line-carry pass needs SELL d16/c8, interleaved pairs, rows <= param <= 8 and whole 64-row grid lines");
     if (ok && opt_.carry != 0) {
@@ -500,7 +502,7 @@ void GpuCgSolver::setup() {
       };
       // the specialised pass (no slow path) when every stored offset is carried: 0, +-1, +-one line
       // 3-D: the carried line is a plane (N^2 rows) and +-N is a second carried offset
-      carry_lo2_ = spec_.kind == ProblemKind::Poisson3D && opt_.carry_3d != 0 ? (int32_t)spec_.N : 0;
+      carry_lo2_ = stencil_plane(spec_) > 0 && opt_.carry_3d != 0 ? (int32_t)stencil_line(spec_) : 0;
       carry_general_ = !c8_;
       for (int64_t off : dict_offsets_)
         if (off != 0 && off != 1 && off != -1 && off != 64 * S && off != -64 * S &&

@@ -43,7 +43,47 @@ HostMatrix::HostMatrix(int64_t n, std::vector<int64_t> rowptr, std::vector<int64
   }
   view_.n = n;
   view_.bw = bw;
+  detect_stencil_();
   bind_();
+}
+
+// structured-grid stencil: the distinct column offsets are {0, +-1, +-L} (2-D, n a multiple of L)
+// or {0, +-1, +-L, +-L^2} (3-D, n a multiple of L^2), L >= 2 (CsrMatrix::line / plane)
+void HostMatrix::detect_stencil_() {
+  view_.line = view_.plane = 0;
+  const int64_t n = view_.n;
+  std::vector<int64_t> offs;
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t k = rowptr_[i]; k < rowptr_[i + 1]; ++k) {
+      const int64_t d = cols_[k] - i;
+      if (std::find(offs.begin(), offs.end(), d) == offs.end()) {
+        offs.push_back(d);
+        if (offs.size() > 7) return;
+      }
+    }
+  auto has = [&](int64_t d) { return std::find(offs.begin(), offs.end(), d) != offs.end(); };
+  int64_t far[2] = {0, 0};
+  int nf = 0;
+  for (int64_t d : offs) {
+    if (d == 0 || d == 1 || d == -1) continue;
+    if (d < 0) {
+      if (!has(-d)) return;  // the offsets of a symmetric stencil come in pairs
+      continue;
+    }
+    if (nf == 2) return;
+    far[nf++] = d;
+  }
+  if (!has(1) || !has(-1) || nf == 0) return;
+  if (nf == 1) {
+    const int64_t L = far[0];
+    if (L >= 2 && n % L == 0 && n / L >= 2) view_.line = L;
+    return;
+  }
+  const int64_t L = std::min(far[0], far[1]), P = std::max(far[0], far[1]);
+  if (L >= 2 && P == L * L && n % P == 0 && n / P >= 2) {
+    view_.line = L;
+    view_.plane = P;
+  }
 }
 
 void HostMatrix::bind_() {

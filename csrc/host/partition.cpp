@@ -59,7 +59,8 @@ RowPartition partition_rows(const ProblemSpec& s, int world, int halo_mode) {
     }
   }
   if (s.kind == ProblemKind::RandomSPD && world > 1 && n / 1024 >= world) return partition_randspd(s, world);
-  if (s.kind == ProblemKind::Csr && world > 1) {  // nnz + rows balanced
+  // nnz + rows balanced (a user matrix with a detected grid stencil is split at whole lines / planes below)
+  if (s.kind == ProblemKind::Csr && world > 1 && (partition_granule(s) <= 1 || n / partition_granule(s) < world)) {
     std::vector<int64_t> w(n + 1);
     for (int64_t i = 0; i <= n; ++i) w[i] = s.csr->rowptr[i] + i;
     return partition_by_weight(w, world);

@@ -35,6 +35,7 @@ class HostMatrix {
 
  private:
   void bind_();
+  void detect_stencil_();  // CsrMatrix::line / plane
   std::vector<int64_t> rowptr_, cols_;
   std::vector<double> vals_, b_;
   CsrMatrix view_;

@@ -51,6 +51,10 @@ struct CsrMatrix {
   const double* vals = nullptr;
   const double* b = nullptr;        // optional right-hand side (n); null: the spec's rhs kind
   int64_t bw = 0;                   // max |i - j| over the stored entries
+  // structured-grid stencil detected in the matrix (HostMatrix): every stored entry's column offset
+  // is 0, +-1, +-line (2-D) or also +-plane = line^2 (3-D), and the rows are whole lines / planes;
+  // 0 = none.  Lets a user matrix take the generated stencils' line / plane carry.
+  int64_t line = 0, plane = 0;
 };
 enum class RhsKind : int { Reference = 0, Random = 1, Ones = 2 };
 
@@ -105,7 +109,25 @@ MCG_HD inline int64_t partition_granule(const ProblemSpec& s) {
   switch (s.kind) {
     case ProblemKind::Poisson2D: return s.N;
     case ProblemKind::Poisson3D: return s.N * s.N;
+    case ProblemKind::Csr: return s.csr && s.csr->plane > 0 ? s.csr->plane : (s.csr && s.csr->line > 0 ? s.csr->line : 1);
     default: return 1;
+  }
+}
+// grid line length of a structured-grid stencil (generated, or detected in a user matrix); 0 = none
+MCG_HD inline int64_t stencil_line(const ProblemSpec& s) {
+  switch (s.kind) {
+    case ProblemKind::Poisson2D:
+    case ProblemKind::Poisson3D: return s.N;
+    case ProblemKind::Csr: return s.csr ? s.csr->line : 0;
+    default: return 0;
+  }
+}
+// plane length (line^2) of a 3-D stencil; 0 = not 3-D
+MCG_HD inline int64_t stencil_plane(const ProblemSpec& s) {
+  switch (s.kind) {
+    case ProblemKind::Poisson3D: return s.N * s.N;
+    case ProblemKind::Csr: return s.csr ? s.csr->plane : 0;
+    default: return 0;
   }
 }
 

@@ -127,3 +127,45 @@ def test_sell_sigma_local_ranks_keeps_interior_split(mcg, world):
         out = C.run_local_ranks(p.native(), o, world, 0, True)
         assert abs(out["ranks"][0]["iterations"] - cpu["iterations"]) <= 1
         np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-7, atol=1e-9)
+
+
+def _poisson(n, dim):  # the 5-/7-pt Dirichlet Laplacian on an n^dim grid, as SciPy builds it
+    T = sp.diags([-1.0, 2.0, -1.0], [-1, 0, 1], shape=(n, n))
+    I = sp.identity(n)
+    if dim == 2:
+        return (sp.kron(I, T) + sp.kron(T, I)).tocsr()
+    return (sp.kron(sp.kron(I, I), T) + sp.kron(sp.kron(I, T), I) + sp.kron(sp.kron(T, I), I)).tocsr()
+
+
+@pytest.mark.parametrize("dim,n", [(2, 128), (3, 64)])
+def test_user_stencil_matrix_takes_the_carry(mcg, dim, n):
+    """A 5- / 7-pt Poisson operator handed in as a user CSR: the grid structure is detected from
+    the column offsets (0, +-1, +-n and +-n^2), so the matrix takes the generated stencils' path
+    (Ap-recomputing line / plane carry on SELL-64/dia4) and solves bit for bit like the generated
+    problem (same entries in the same order, same counter-based random RHS)."""
+    p = mcg.csr_problem(_poisson(n, dim), rhs="random")
+    assert p.matrix.stencil_line == n and p.matrix.stencil_plane == (n * n if dim == 3 else 0)
+    g = mcg.make_problem("poisson2d" if dim == 2 else "poisson3d", n=n, rhs="random")
+    a = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8)
+    b = mcg.CGSolver(g, format="sellc8", recurrence=1, check_every=8)
+    for k in ("carry", "ap_recompute", "dia4"):
+        assert a.info[k] and b.info[k], k
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+
+
+def test_user_stencil_matrix_multirank_whole_lines(mcg):
+    """At P > 1 a detected stencil is split at whole grid lines (not nnz-balanced rows), so every
+    rank runs the line carry with ghost lines; P = 2 and 4 agree with P = 1."""
+    n = 128
+    p = mcg.csr_problem(_poisson(n, 2), rhs="random")
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
+    one = C.run_local_ranks(p.native(), o, 1, 60, True)
+    for world in (2, 4):
+        out = C.run_local_ranks(p.native(), o, world, 60, True)
+        assert all(q["carry"] and q["ap_recompute"] for q in out["ranks"])
+        r = one["ranks"][0]["rnorm"]
+        assert abs(out["ranks"][0]["rnorm"] - r) <= 1e-11 * r
+        np.testing.assert_allclose(out["x"], one["x"], rtol=1e-10, atol=1e-13)

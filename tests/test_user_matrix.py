@@ -172,3 +172,26 @@ def test_solve_helper_takes_a_matrix(mcg):
     for reorder in (None, "rcm"):
         r = mcg.solve(matrix=A, b=b, device="cpu", tol=1e-10, reorder=reorder)
         np.testing.assert_allclose(r["x"], sp.linalg.spsolve(A.tocsc(), b), rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_stencil_detection_and_line_partition(mcg, C, dim):
+    """A user matrix whose column offsets are {0, +-1, +-n} (2-D) or also +-n^2 (3-D) is recognised
+    as a grid stencil; a P-rank partition then cuts at whole lines / planes.  Other matrices keep
+    line = 0 and the nnz-balanced partition."""
+    n = 16
+    T = sp.diags([-1.0, 2.0, -1.0], [-1, 0, 1], shape=(n, n))
+    I = sp.identity(n)
+    A = (sp.kron(I, T) + sp.kron(T, I)) if dim == 2 else (
+        sp.kron(sp.kron(I, I), T) + sp.kron(sp.kron(I, T), I) + sp.kron(sp.kron(T, I), I))
+    p = mcg.csr_problem(A.tocsr())
+    g = n if dim == 2 else n * n
+    assert p.matrix.stencil_line == n and p.matrix.stencil_plane == (0 if dim == 2 else g)
+    for world in (2, 3, 5):
+        offs = C.partition_rows(p.native(), world, 0)
+        assert all(o % g == 0 for o in offs), offs
+    q = mcg.csr_problem(_spd())
+    assert q.matrix.stencil_line == 0 and q.matrix.stencil_plane == 0
+    # a matrix with the offsets but rows that are not whole lines: no stencil
+    B = sp.diags([-1.0, -1.0, 4.0, -1.0, -1.0], [-n, -1, 0, 1, n], shape=(n * n - 3, n * n - 3)).tocsr()
+    assert mcg.csr_problem(B).matrix.stencil_line == 0
