@@ -13,7 +13,7 @@
 //   --maxit M  --tol T  --rtol R (||r|| < R ||b||)  --check-every K  --fixed-iters K  --warmup W
 //   --nnz-per-row m (random-spd: density = (m - 1) / (2 band))
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
-//   --spmv-variant 0|1|2|3  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
+//   --spmv-variant 0|1|2|3|4  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
 //   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off  --window auto|on|off
 //   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
 //   --fused-reduce auto|on|off  --watchdog SECONDS

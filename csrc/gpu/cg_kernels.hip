@@ -112,6 +112,7 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
   if constexpr (ENG == 0) eng::csr_lds<IdxT, P>(A, tr, gather, epi);
   else if constexpr (ENG == 1) eng::csr_direct<IdxT, P, false>(A, tr, gather, epi);
   else if constexpr (ENG == 3) eng::csr_direct<IdxT, P, true>(A, tr, gather, epi);
+  else if constexpr (ENG == 4) eng::csr_adaptive<IdxT, P, 16>(A, tr, gather, epi);
   else eng::csr_vector<IdxT, P>(A, tr, gather, epi);
   block_partial<kBS>(acc, s_red, partials + blockIdx.x);
 }
@@ -372,6 +373,8 @@ void cg_spmv_fused(const CsrDev<IdxT>& A, const double* r_ext, const double* pol
     if (param <= 4) MCG_FUSED(1, 4); else if (param <= 6) MCG_FUSED(1, 6); else MCG_FUSED(1, 8);
   } else if (variant == 3) {
     if (param <= 4) MCG_FUSED(3, 4); else if (param <= 6) MCG_FUSED(3, 6); else MCG_FUSED(3, 8);
+  } else if (variant == 4) {
+    if (param <= 4) MCG_FUSED(4, 4); else if (param <= 6) MCG_FUSED(4, 6); else MCG_FUSED(4, 8);
   } else {
     if (param <= 4) MCG_FUSED(2, 4); else if (param <= 8) MCG_FUSED(2, 8); else MCG_FUSED(2, 16);
   }

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kBS) void k_split_spmv(CsrDev<IdxT> A, SellDev S, c
     s_apap = fma(sum, sum, s_apap);
     s_rr = fma(rk, rk, s_rr);
   };
-  if constexpr (FMT == 0) eng::csr_direct<IdxT, U, false>(A, tr, gather, epi);
+  if constexpr (FMT == 0) eng::csr_adaptive<IdxT, U, 16>(A, tr, gather, epi);
   else if constexpr (FMT == 5) eng::csr_vector<IdxT, U>(A, tr, gather, epi);
   else if constexpr (FMT == 1) eng::sell<U, false, 0>(S, tr, gather, epi);
   else if constexpr (FMT == 3) eng::sell<U, false, 1>(S, tr, gather, epi);

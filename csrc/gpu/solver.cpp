@@ -231,7 +231,9 @@ void GpuCgSolver::setup() {
   MCG_HIP(hipMemcpy(&nnz, rp64.get() + n, sizeof(int64_t), hipMemcpyDeviceToHost),
           "memcpy from device to host failed(A)");
   // engine choice: short rows -> thread-per-row engines, long rows -> CSR-vector
-  info_.spmv_variant = opt_.spmv_variant >= 0 ? opt_.spmv_variant : (info_.max_row_len > 16 ? 2 : 1);
+  // CSR engine: thread per row when every row is short; else row-length-adaptive per 256-row tile
+  // (eng::csr_adaptive: thread per row or 16 lanes per row, by one block vote per tile)
+  info_.spmv_variant = opt_.spmv_variant >= 0 ? opt_.spmv_variant : (info_.max_row_len > 16 ? 4 : 1);
   info_.spmv_param = opt_.spmv_param > 0 ? opt_.spmv_param
                                          : kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
   // SELL: one batch = the slice width when it is 4..8 (no clamped duplicate gathers)

@@ -17,6 +17,8 @@
 //   csr_vector  G lanes per row (CSR-vector), all G/passes of a 256-row tile
 //               batched, group reduction with xor-shuffles, LDS transpose so the
 //               epilogue is thread-per-row and fully coalesced.
+//   csr_adaptive per-tile choice (the tile is the row-length bin): thread per row
+//               when every row of the tile has <= G entries, else csr_vector's body.
 //   sell        one wave per 64-row SELL slice, entries column-major (every load
 //               is one coalesced 512-B / 256-B wave access), U per batch.
 #pragma once
@@ -255,6 +257,81 @@ __device__ __forceinline__ void csr_vector(const CsrDev<IdxT>& A, const TileRang
 #pragma unroll
     for (int p = 0; p < G; ++p) {
       double x = s[p];
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, G);
+      if (sub == 0) s_sum[p * RPP + grp] = x;
+    }
+    __syncthreads();
+    if (t < nr) epi(r0 + t, s_sum[t]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row-length-adaptive CSR (the tile is the bin): each 256-row tile reads its row pointers, and one
+// block vote (__syncthreads_or) sends it down the thread-per-row path when every row has <= G
+// entries, or the G-lanes-per-row path (csr_vector's tile body) when any row is longer.  A few long
+// rows then cost their own tiles a vector pass instead of pushing every row of the matrix onto it
+// (the old per-matrix choice by max_row_len), and short-row tiles keep csr_direct's batched loads.
+template <typename IdxT, int U, int G, class Gather, class Epi>
+__device__ __forceinline__ void csr_adaptive(const CsrDev<IdxT>& A, const TileRanges& tr, Gather&& gather,
+                                             Epi&& epi) {
+  static_assert(G == 4 || G == 8 || G == 16, "lanes per row");
+  constexpr int RPP = kBS / G;
+  __shared__ double s_sum[kBS];
+  const int t = threadIdx.x, sub = t & (G - 1), grp = t / G;
+  for (TileCursor cur = tile_cursor(tr, 0, 1); cur.t < cur.end; cur.t += cur.step) {
+    int64_t r0, r1;
+    tile_rows(tr, cur.t, r0, r1);
+    const int nr = (int)(r1 - r0);
+    int64_t rs = 0, re = 0;
+    if (t < nr) {
+      rs = (int64_t)A.rowptr[r0 + t];
+      re = (int64_t)A.rowptr[r0 + t + 1];
+    }
+    if (!__syncthreads_or(re - rs > G)) {  // short-row tile: thread per row (csr_direct)
+      double sum = 0.0;
+      for (int64_t j0 = rs; j0 < re; j0 += U) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = imin(j0 + u, re - 1);
+          c[u] = A.cols[j];
+          v[u] = A.vals[j];
+        }
+        double g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) g[u] = gather(c[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) sum = (j0 + u < re) ? fma(v[u], g[u], sum) : sum;
+      }
+      if (t < nr) epi(r0 + t, sum);
+      continue;
+    }
+    // long-row tile: G lanes per row, G passes of RPP rows (csr_vector's body)
+    int64_t qs[G], qe[G];
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      const int lr = p * RPP + grp;
+      const int64_t ii = r0 + (lr < nr ? lr : nr - 1);
+      qs[p] = (int64_t)A.rowptr[ii];
+      qe[p] = lr < nr ? (int64_t)A.rowptr[ii + 1] : qs[p];
+    }
+    double sp[G];
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      const int64_t j = qs[p] + sub;
+      const int64_t jj = qe[p] > qs[p] ? imin(j, qe[p] - 1) : 0;
+      const double g = gather(A.cols[jj]);
+      sp[p] = (j < qe[p]) ? A.vals[jj] * g : 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < G; ++p)
+      for (int64_t j = qs[p] + sub + G; j < qe[p]; j += G) sp[p] = fma(A.vals[j], gather(A.cols[j]), sp[p]);
+#pragma unroll
+    for (int p = 0; p < G; ++p) {
+      double x = sp[p];
 #pragma unroll
       for (int off = G / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, G);
       if (sub == 0) s_sum[p * RPP + grp] = x;

@@ -28,7 +28,8 @@ struct CgOptions {
   bool force_comm = false;   // run RCCL collectives even with one rank
   int format = 0;            // 0 = CSR, 1 = SELL-64
   int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
-  int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector; -1 = auto
+  int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector, 4 row-length adaptive per
+                             // tile (direct or 16 lanes per row); -1 = auto (1 when every row has <= 16 entries, else 4)
   int spmv_param = 0;        // batch U (engines 0/1, SELL) or lanes/row G (engine 2); 0 = auto
   int update_unroll = 1;     // double2 loads in flight per lane in the residual update
   int update_blocks_per_cu = 4;  // grid of the residual update / dot kernels (1024 blocks: best measured)

@@ -50,7 +50,7 @@ FLAGS = [
     ("--no-graph", None, "eager iterations (no hipGraph)"),
     ("--force-comm", None, "RCCL collectives also with one rank"),
     ("--blocks-per-cu", "0", "SpMV grid, blocks per CU (0 = auto)"),
-    ("--spmv-variant", "-1", "CSR engine: 0 LDS tiles, 1 direct, 2 CSR-vector, 3 direct nt; -1 auto"),
+    ("--spmv-variant", "-1", "CSR engine: 0 LDS tiles, 1 direct, 2 CSR-vector, 3 direct nt, 4 row-length adaptive; -1 auto"),
     ("--spmv-param", "0", "batch U / lanes per row G (0 = auto)"),
     ("--update-unroll", "1", "residual-update unroll (1, 2, 4)"),
     ("--nt-loads", "0", "non-temporal matrix loads (0 / 1)"),

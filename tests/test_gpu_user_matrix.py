@@ -169,3 +169,37 @@ def test_user_stencil_matrix_multirank_whole_lines(mcg):
         r = one["ranks"][0]["rnorm"]
         assert abs(out["ranks"][0]["rnorm"] - r) <= 1e-11 * r
         np.testing.assert_allclose(out["x"], one["x"], rtol=1e-10, atol=1e-13)
+
+
+def _hubs(n=6000, seed=7):  # short rows plus a few rows coupled to ~600 columns (hub rows)
+    A = _spd(n=n, density=0.0008, seed=seed).tolil()
+    rng = np.random.default_rng(seed)
+    for h in (5, 1000, 4321):
+        cols = rng.choice(n, 600, replace=False)
+        for c in cols:
+            if c != h:
+                A[h, c] = A[c, h] = -0.001
+    A = A.tocsr()
+    A = A + sp.diags(np.asarray(abs(A).sum(axis=1)).ravel() + 1.0)
+    return A.tocsr()
+
+
+@pytest.mark.parametrize("recurrence", [0, 1])
+def test_csr_row_length_adaptive_engine(mcg, recurrence):
+    """CSR with a few hub rows: the auto engine is the per-tile adaptive one (thread per row on
+    short-row tiles, 16 lanes per row on the tiles holding a hub); it matches the CPU oracle and the
+    all-CSR-vector / all-direct engines."""
+    A = _hubs()
+    b = np.random.default_rng(3).standard_normal(A.shape[0])
+    p = mcg.csr_problem(A, b=b)
+    C = mcg.native()
+    cpu = C.cpu_cg(p.native(), C.CgOptions(maxit=2000, tol=1e-8))
+    outs = {}
+    for v in (-1, 1, 2):
+        s = mcg.CGSolver(p, format="csr", recurrence=recurrence, tol=1e-8, spmv_variant=v)
+        if v == -1:
+            assert s.info["spmv_variant"] == 4
+        outs[v] = s.solve()
+        assert outs[v]["converged"] and abs(outs[v]["iterations"] - cpu["iterations"]) <= 2
+        np.testing.assert_allclose(outs[v]["x_local"], cpu["x"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(outs[-1]["x_local"], outs[2]["x_local"], rtol=1e-8, atol=1e-11)
