@@ -112,7 +112,7 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
   }
 }
 
-template <int CM, int U, int QD, bool PAIR>
+template <int CM, int U, int QD, bool PAIR, bool P3>
 __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
@@ -130,6 +130,13 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
   }
   __syncthreads();
   const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  // three-term form (P3): r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p's the pass reads anyway
+  // (p_{k-2} is the buffer p_k overwrites), so r is stored only where another wave or rank reads
+  // it: the slices' edge rows and every row of a run's first / last line (which include the
+  // rank's first / last line, the halo's source).  Pass 0 (r_{-1} = b in the full vector) runs the
+  // two-term kernel: with beta = 0 its r_0 equals the recovered value bit for bit
+  constexpr bool rfull = !P3;
+  const double nbp = P3 ? -st->b_prev : 0.0;
   const double* __restrict__ ro = v.r_old;
   const double* __restrict__ po = v.p_old;
   double* __restrict__ rn = v.r_new;
@@ -161,6 +168,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
 
+  // r = r_{k-1}, or (P3, a line of this run) p_{k-2}: see rof()
   struct Raw {
     double r, p;
   };
@@ -219,11 +227,15 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       const int64_t L = l0 + j;
       return L < 0 ? (int64_t)0 : (L >= nl ? nl - 1 : L);
     };
+    // P3: lines of this run take p_{k-2} (their r is recovered at use), others the stored r; the
+    // pointer is chosen before the load (wave-uniform), the recovery selected after it arrives
+    auto inrun = [&](int32_t j) { return !rfull && j >= 0 && j < n_run; };
     auto load_raw = [&](int32_t j, Raw& q) {
       const int32_t e = ebase(j) + lane;
-      q.r = ld_once(ro + e, ntl);
+      q.r = ld_once((inrun(j) ? (const double*)pn : ro) + e, ntl);
       q.p = ld_once(po + e, ntl);
     };
+    auto rof = [&](int32_t j, const Raw& q) { return inrun(j) ? fma(nbp, q.r, q.p) : q.r; };
     auto load_edge = [&](int32_t j, Edge& q) {
       const int32_t e = ebase(j);
       const int64_t s = oline(j) * SS + col;
@@ -242,7 +254,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
     auto load_xp = [&](int32_t j, XP& q) {
       if constexpr (PAIR) {
         const int32_t mm = j < n_run - 1 ? j : n_run - 1;
-        q.pkm2 = ld_once(pn + e0 + mm * LO + lane, ntl);
+        if constexpr (!P3) q.pkm2 = ld_once(pn + e0 + mm * LO + lane, ntl);  // P3: already read (o_pm2)
         q.xo = ld_once(x + i0 + mm * LO + lane, ntl);
       }
     };
@@ -281,15 +293,15 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
     double pr_pk = 0.0;
     if (owned(-1)) {
       const double t = stencil(cm1, rm1.p, edge_p(edm1), rm2.p, r0.p);
-      pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+      pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
     } else if (ghost(-1)) {
       const double t = apx_o[ebase(-1) + lane];
-      pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+      pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
     }
-    double o_pold = r0.p, o_rk, o_pk;
+    double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
     {
       const double t = stencil(c0, r0.p, edge_p(ed0), rm1.p, rq[0].p);
-      o_rk = fma(na, t, r0.r);
+      o_rk = fma(na, t, rof(0, r0));
       o_pk = fma(b, r0.p, o_rk);
     }
     double o_epk = edge_pk(ed0);
@@ -311,18 +323,26 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       double rk1 = 0.0, pk1 = 0.0;
       if (owned(m + 1)) {
         const double t = stencil(c1, rq[0].p, edge_p(ed1), o_pold, rq[1].p);
-        rk1 = fma(na, t, rq[0].r);
+        rk1 = fma(na, t, rof(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       } else if (ghost(m + 1)) {
         const double t = apx_o[ebase(m + 1) + lane];
-        rk1 = fma(na, t, rq[0].r);
+        rk1 = fma(na, t, rof(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       }
       // 3. Ap_k of line m, stores, partials
       const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1);
       const int32_t eb = e0 + m * LO;
-      st_stream(&(rn + eb)[lane], o_rk);
-      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, x0.pkm2, x0.xo)));
+      if constexpr (P3) {
+        // r_k only where another wave (edge rows, the run's outer lines) or rank reads it, and as
+        // the value the next pass recovers from the stored p's, fma(-b, p_{k-1}, p_k): every reader
+        // of a row's r_k -- owner, neighbouring wave, neighbouring rank -- uses the same bits
+        if (m == 0 || m == n_run - 1) st_stream(&(rn + eb)[lane], fma(-b, o_pold, o_pk));
+        else if (lane == 0 || lane == 63) rn[eb + lane] = fma(-b, o_pold, o_pk);
+      } else {
+        st_stream(&(rn + eb)[lane], o_rk);
+      }
+      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, P3 ? o_pm2 : x0.pkm2, x0.xo)));
       st_stream(&(pn + eb)[lane], o_pk);
       const int64_t s = (l0 + m) * SS + col;
       if (lane == 0 || lane == 63) en[2 * s + (lane == 63 ? 1 : 0)] = sum;
@@ -336,6 +356,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       o_pk = pk1;
       o_rk = rk1;
       o_pold = rq[0].p;
+      o_pm2 = rq[0].r;
       o_epk = edge_pk(ed1);
       ed1 = ed2;
 #pragma unroll
@@ -391,7 +412,7 @@ __device__ __forceinline__ void ar3_finish(double a0, double a1, double a2, doub
   if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
 }
 
-template <int QD, bool PAIR, int KW>
+template <int QD, bool PAIR, int KW, bool P3>
 __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                                   int32_t LN, int gfull,
                                                                   double* __restrict__ partials, int pstride,
@@ -409,6 +430,12 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
   if (threadIdx.x < 16) s_val[threadIdx.x] = S.dvals[threadIdx.x];
   __syncthreads();
   const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
+  // three-term form (P3, as in k_cg_carry_ar): r_{k-1} = p_{k-1} - b_prev p_{k-2} on the run's own
+  // planes; r stored (as that recovered value) only where another wave reads it: the block's outer
+  // lines, the slices' edge rows and the run's first / last plane (the halo's source at P > 1);
+  // pass 0 runs the two-term kernel (see k_cg_carry_ar)
+  constexpr bool rfull = !P3;
+  const double nbp = P3 ? -st->b_prev : 0.0;
   const double* __restrict__ ro = v.r_old;
   const double* __restrict__ po = v.p_old;
   double* __restrict__ rn = v.r_new;
@@ -475,11 +502,13 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       return L < 0 ? (int64_t)0 : (L >= nl ? nl - 1 : L);
     };
     auto clampr = [&](int32_t e) { return e < 0 ? 0 : (e >= ext32 ? ext32 - 1 : e); };
+    auto inrun = [&](int32_t j) { return !rfull && j >= 0 && j < n_run; };
     auto load_raw = [&](int32_t j, Raw& r) {
       const int32_t e = ebase(j) + lane;
-      r.r = ld_once(ro + e, ntl);
+      r.r = ld_once((inrun(j) ? (const double*)pn : ro) + e, ntl);
       r.p = ld_once(po + e, ntl);
     };
+    auto rof = [&](int32_t j, const Raw& q) { return inrun(j) ? fma(nbp, q.r, q.p) : q.r; };
     auto load_edge = [&](int32_t j, Edge& r) {
       const int32_t e = ebase(j);
       if (lane == 0 || lane == 63) {
@@ -500,7 +529,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     auto load_xp = [&](int32_t j, XP& r) {
       if constexpr (PAIR) {
         const int32_t mm = j < n_run - 1 ? j : n_run - 1;
-        r.pkm2 = ld_once(pn + e0 + mm * LO + lane, ntl);
+        if constexpr (!P3) r.pkm2 = ld_once(pn + e0 + mm * LO + lane, ntl);  // P3: already read (o_pm2)
         r.xo = ld_once(x + i0 + mm * LO + lane, ntl);
       }
     };
@@ -548,16 +577,16 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       double dn, up;
       nbr(1, 0, fm1.p, dn, up);
       const double t = stencil(cm1, rm1.p, edm1.p, rm2.p, r0.p, dn, up);
-      pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+      pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
     } else if (ghost(-1)) {
-      pr_pk = pk_of(rm1.r, apo[ebase(-1) + lane], rm1.p);
+      pr_pk = pk_of(rof(-1, rm1), apo[ebase(-1) + lane], rm1.p);
     }
-    double o_pold = r0.p, o_rk, o_pk;
+    double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
     {
       double dn, up;
       nbr(1, 1, f0.p, dn, up);
       const double t = stencil(c0, r0.p, ed0.p, rm1.p, rq[0].p, dn, up);
-      o_rk = fma(na, t, r0.r);
+      o_rk = fma(na, t, rof(0, r0));
       o_pk = fma(b, r0.p, o_rk);
     }
     double o_epk = edge_pk(ed0);
@@ -586,11 +615,11 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
         double dn, up;
         nbr(par, 0, fa.p, dn, up);
         const double t = stencil(c1, rq[0].p, ed1.p, o_pold, rq[1].p, dn, up);
-        rk1 = fma(na, t, rq[0].r);
+        rk1 = fma(na, t, rof(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       } else if (ghost(m + 1)) {
         const double t = apo[ebase(m + 1) + lane];
-        rk1 = fma(na, t, rq[0].r);
+        rk1 = fma(na, t, rof(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       }
       // 4. Ap_k of plane m, stores, partials
@@ -598,8 +627,13 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       nbr(par, 1, o_fpk, kdn, kup);
       const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1, kdn, kup);
       const int32_t eb = e0 + m * LO;
-      st_stream(&(rn + eb)[lane], o_rk);
-      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, x0.pkm2, x0.xo)));
+      if constexpr (P3) {  // r_k where another wave or rank reads it, as the value the next pass recovers
+        if (m == 0 || m == n_run - 1) st_stream(&(rn + eb)[lane], fma(-b, o_pold, o_pk));
+        else if (odn || oup || lane == 0 || lane == 63) rn[eb + lane] = fma(-b, o_pold, o_pk);
+      } else {
+        st_stream(&(rn + eb)[lane], o_rk);
+      }
+      if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, P3 ? o_pm2 : x0.pkm2, x0.xo)));
       st_stream(&(pn + eb)[lane], o_pk);
       if (odn || oup || lane == 0 || lane == 63 || (gfull && (l0 + m == 0 || l0 + m == nl - 1))) apw[eb + lane] = sum;
       s_pap = fma(o_pk, sum, s_pap);
@@ -611,6 +645,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       o_pk = pk1;
       o_rk = rk1;
       o_pold = rq[0].p;
+      o_pm2 = rq[0].r;
       o_epk = edge_pk(ed1);
       o_fpk = pk_of(fa.r, fa.a, fa.p);
       fa = fb;
@@ -631,7 +666,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
 template <int CM, int U>
 __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_t own, int64_t n, int32_t lo, int32_t ln,
                                                   double* __restrict__ partials, int pstride, CgState* st,
-                                                  double tol, int first, int check, int k) {
+                                                  double tol, int first, int check, int k, bool p3) {
   const int done = st->done;
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   const double a = sc.alpha, na = -a, ap = st->a_prev;
@@ -670,7 +705,9 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
         if (u < c.w) t = fma(val, v.p_old[e + off], t);
       }
     }
-    const double rk = fma(na, t, v.r_old[e]);
+    // three-term carry: r_{m-1} = p_{m-1} - b_prev p_{m-2} (p_new still holds p_{m-2})
+    const double ro = (p3 && !first) ? fma(-st->b_prev, v.p_new[e], v.p_old[e]) : v.r_old[e];
+    const double rk = fma(na, t, ro);
     v.r_new[e] = rk;
     v.x[i] = pair ? fma(a, v.p_old[e], fma(ap, v.p_new[e], v.x[i])) : fma(a, v.p_old[e], v.x[i]);
     s_rr = fma(rk, rk, s_rr);
@@ -772,7 +809,7 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* d
 
 void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol, int first,
-                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc) {
+                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
@@ -786,11 +823,13 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   MCG_CHECK((v.ap_old == nullptr) == (v.ap_new == nullptr), "Ap-recomputing carry: boundary Ap buffers");
   MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
             "in-kernel reduction: bad control block");
+  MCG_CHECK(!p3 || cm == 4, "three-term carry: SELL-64/dia4 only");
+  const bool p3k = p3 && !first;  // pass 0: the two-term kernel (r_{-1} = b stored in full)
   if (final_mode) {
     const int64_t n = tr.nt0 * 64;
 #define MCG_AF(CM, U)                                                                                        \
   hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, \
-                     (int32_t)(tr.strip * 64), 0, partials, pstride, st, tol, first, check, k)
+                     (int32_t)(tr.strip * 64), 0, partials, pstride, st, tol, first, check, k, p3)
     if (cm == 4) MCG_AF(4, 5);
     else if (cm == 3) { if (param == 4) MCG_AF(3, 4); else MCG_AF(3, 5); }
     else { if (param == 4) MCG_AF(2, 4); else MCG_AF(2, 5); }
@@ -800,13 +839,20 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   }
   const bool pair = (k & 1) != 0;
   const int qd = depth <= 2 ? 2 : (depth >= 5 ? 5 : depth);
-#define MCG_A(CM, U, QD, PAIR)                                                                                     \
-  hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, partials, \
-                     pstride, st, tol, first, check, rc)
-#define MCG_AP(CM, U, QD)                     \
-  do {                                        \
-    if (pair) MCG_A(CM, U, QD, true);         \
-    else MCG_A(CM, U, QD, false);             \
+#define MCG_A(CM, U, QD, PAIR, P3)                                                                      \
+  hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR, P3>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
+                     partials, pstride, st, tol, first, check, rc)
+#define MCG_AP(CM, U, QD)                                        \
+  do {                                                           \
+    if constexpr (CM == 4) {                                     \
+      if (p3k) {                                                 \
+        if (pair) MCG_A(CM, U, QD, true, true);                  \
+        else MCG_A(CM, U, QD, false, true);                      \
+        break;                                                   \
+      }                                                          \
+    }                                                            \
+    if (pair) MCG_A(CM, U, QD, true, false);                     \
+    else MCG_A(CM, U, QD, false, false);                         \
   } while (0)
 #define MCG_AQ(CM, U)                         \
   do {                                        \
@@ -826,7 +872,7 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
 
 void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
-                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc) {
+                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0 && ln % 64 == 0 &&
                 (int64_t)ln * ln == (int64_t)tr.strip * 64 && (kw == 4 || kw == 8 || kw == 16) && ln % kw == 0,
@@ -838,25 +884,31 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
             "in-kernel reduction: bad control block");
   if (final_mode) {
     hipLaunchKernelGGL((k_ar_final<4, 7>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr.nt0 * 64,
-                       (int32_t)(tr.strip * 64), ln, partials, pstride, st, tol, first, check, k);
+                       (int32_t)(tr.strip * 64), ln, partials, pstride, st, tol, first, check, k, p3);
     MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
     return;
   }
   const bool pair = (k & 1) != 0;
   const int qd = depth >= 3 ? 3 : 2;
   const int g = gfull ? 1 : 0;
-#define MCG_A3(QD, PAIR, KW)                                                                                   \
-  hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW>), dim3(grid), dim3(64 * KW), 0, stream, S, v, own_off, tr, ln, \
-                     g, partials, pstride, st, tol, first, check, rc)
+#define MCG_A3(QD, PAIR, KW, P3)                                                                              \
+  hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3>), dim3(grid), dim3(64 * KW), 0, stream, S, v, own_off, tr, \
+                     ln, g, partials, pstride, st, tol, first, check, rc)
+#define MCG_A3P(QD, PAIR, KW)                   \
+  do {                                          \
+    if (p3 && !first) MCG_A3(QD, PAIR, KW, true); \
+    else MCG_A3(QD, PAIR, KW, false);           \
+  } while (0)
 #define MCG_A3K(QD, PAIR)                       \
   do {                                          \
-    if (kw == 4) MCG_A3(QD, PAIR, 4);           \
-    else if (kw == 8) MCG_A3(QD, PAIR, 8);      \
-    else MCG_A3(QD, PAIR, 16);                  \
+    if (kw == 4) MCG_A3P(QD, PAIR, 4);          \
+    else if (kw == 8) MCG_A3P(QD, PAIR, 8);     \
+    else MCG_A3P(QD, PAIR, 16);                 \
   } while (0)
   if (qd == 2) { if (pair) MCG_A3K(2, true); else MCG_A3K(2, false); }
   else { if (pair) MCG_A3K(3, true); else MCG_A3K(3, false); }
 #undef MCG_A3K
+#undef MCG_A3P
 #undef MCG_A3
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }

@@ -92,10 +92,12 @@ __device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int 
   // alpha of the pass whose (global) sums are being replaced — the pass after next pairs it
   // into its x update; same division as f1_scalars so the bits agree
   st->a_prev = first ? 0.0 : st->red[3] / st->red[0];
+  st->b_prev = 0.0;
   if (!first) {  // the clamp in f1_scalars, re-evaluated on the same global sums: count when it fired
     const double a = st->red[3] / st->red[0];
     const double est = fma(a * a, st->red[2], fma(-2.0 * a, st->red[1], st->red[3]));
     if (!(est > 0.0)) st->clamps += 1;
+    st->b_prev = (est > 0.0 ? est : 0.0) / st->red[3];  // f1_scalars' beta, same operations: same bits
   }
   for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
   st->rr_new = tot[3];

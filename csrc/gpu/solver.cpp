@@ -571,6 +571,13 @@ void GpuCgSolver::setup() {
   info_.ap_recompute = ar_;
   info_.interleave = opt_.interleave == 1;
   info_.dia4 = dia4_.get() != nullptr;
+  // three-term form: the 2-D dia4 carry (the halo still carries r of the ghost lines: every rank
+  // stores r on its first / last line in either form, so ranks need not agree on it)
+  // auto: the 2-D carry only (the 3-D plane carry's three-term kernel needs more than the 128 VGPRs
+  // of its 16-wave blocks and spills; p3 = 1 forces it)
+  p3_ = ar_ && info_.dia4 && (opt_.p3 == 1 || (opt_.p3 < 0 && !ar3_));
+  MCG_CHECK(opt_.p3 != 1 || p3_, "p3 needs the Ap-recomputing line / plane carry on SELL-64/dia4");
+  info_.p3 = p3_;
   if (ar_ && !info_.dia4 && n > 0) {
     const int64_t ns = (n + 63) / 64;
     int64_t slots = 0;
@@ -622,14 +629,16 @@ void GpuCgSolver::setup() {
     info_.device_bytes = matrix_bytes + (size_t)(4 * n + L_.ext_len) * 8 + rp64_.bytes();
   }
   if (ar3_) {  // r rw, p rw 32; x 12; Ap of 2 of kw lines written + read, edge rows 0.5; dia4 codes 3.5
-    info_.bytes_per_iter_model = (double)dia4_.bytes() + (44.5 + 16.0 / info_.ar3_kw) * n;
+    // three-term form: p_{k-1}, p_{k-2} read + p_k written 24, x 8, r + Ap of the outer lines / edges
+    info_.bytes_per_iter_model = (double)dia4_.bytes() + ((p3_ ? 32.5 : 44.5) + (p3_ ? 24.0 : 16.0) / info_.ar3_kw) * n;
     info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
     const double streamed = info_.dia4 ? (double)dia4_.bytes()
                                        : (codes4_.get() ? (double)codes4_.bytes() + 4.0 * (double)smeta_.size()
                                                         : (double)matrix_bytes);
-    info_.bytes_per_iter_model = streamed + 44.25 * n;
+    // three-term form: p_{k-1}, p_{k-2} read, p_k written 24 B; x rw every second pass 8; edge r + Ap 0.5
+    info_.bytes_per_iter_model = streamed + (p3_ ? 32.5 : 44.25) * n;
     info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + codes4_.bytes() + smeta_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   }
@@ -923,11 +932,12 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     if (ar3_) {
       kern::cg_carry_ar3(opt_.carry_depth > 0 ? opt_.carry_depth : 2, info_.ar3_kw, S, v, L_.own_off, tr,
                          carry_lo2_, use_halo_, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode,
-                         s0_, rc);
+                         s0_, rc, p3_);
       return;
     }
     kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, opt_.carry_depth > 0 ? opt_.carry_depth : 3, S, v,
-                      L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc);
+                      L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
+                      p3_);
     return;
   }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {

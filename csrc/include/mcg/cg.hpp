@@ -90,6 +90,11 @@ struct CgOptions {
                              // -line, -1, 0, +1, +line; 4-bit value indices), so the pass neither decodes offsets
                              // nor selects operands per entry; -1 = auto (when every entry's offset is canonical
                              // and in ascending order, <= 16 distinct values), 0 = off (c4 codes), 1 = required
+  int p3 = -1;               // Ap-recomputing 2-D dia4 carry, three-term form: r_{k-1} = p_{k-1} - beta_{k-2} p_{k-2}
+                             // recovered from the two p buffers the pass reads anyway, so r is stored only at the
+                             // slices' edge rows and the runs' outer lines (24 instead of 32 B/row for r and p,
+                             // and the paired x update needs no extra p read); rounding differs from the
+                             // two-term form (not bitwise); -1 = auto (on with dia4), 0 = off, 1 = required
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
                              // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
                              // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)

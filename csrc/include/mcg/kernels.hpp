@@ -32,7 +32,9 @@ struct alignas(64) CgState {
   double rr0;     // b . b
   double rr_final;  // rr_new captured when the latch fires (later no-op all-reduces may clobber rr_new)
   double a_prev;    // single-reduction form: alpha of the pass before the last (paired x updates)
-  double pad0_[2];
+  double b_prev;    // ... and the beta that pass used (p_{k-1} = r_{k-1} + b_prev p_{k-2}: the three-term carry
+                    // recovers r_{k-1} from the two stored p's, cg_carry_ar.hip)
+  double pad0_[1];
   // single-reduction recurrence: {p.Ap, r.Ap, Ap.Ap, r.r} of the last fused pass
   // (one contiguous 32-B all-reduce slot)
   double red[4];
@@ -274,11 +276,15 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* d
 // edge rows, and with gfull the first / last plane for the ghosts); grid = blocks (any count)
 void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
-                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl());
-// cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals)
+                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
+                  bool p3 = false);
+// cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals).  p3 (dia4): three-term form --
+// r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p buffers, r stored only at the slices' edge rows
+// and the runs' first / last lines (v.r_old / r_new hold just those rows; pass 0 reads r_{-1} = b)
 void cg_carry_ar(int cm,int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& slices, double* partials, int pstride, int grid, CgState* st, double tol,
-                 int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl());
+                 int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
+                 bool p3 = false);
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,
                      bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,

@@ -66,6 +66,7 @@ struct SolverInfo {
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
+  bool p3 = false;       // ... in its three-term form (CgOptions::p3)
   int ar3_kw = 0;        // 3-D Ap-recomputing plane carry: waves (grid lines) per block; 0 = not in use
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
@@ -144,6 +145,7 @@ class GpuCgSolver {
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
   bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
+  bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)
   bool split_ = false;          // interior / boundary launches around an overlapped halo
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
   bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them

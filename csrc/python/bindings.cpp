@@ -218,6 +218,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("halo_ahead", &CgOptions::halo_ahead)
       .def_readwrite("ap_recompute", &CgOptions::ap_recompute)
       .def_readwrite("carry_dia", &CgOptions::carry_dia)
+      .def_readwrite("p3", &CgOptions::p3)
       .def_readwrite("carry3_kw", &CgOptions::carry3_kw)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
@@ -398,6 +399,7 @@ PYBIND11_MODULE(_C, m) {
         d["xcd_map"] = i.xcd_map;
         d["codes4"] = i.codes4;
         d["dia4"] = i.dia4;
+        d["p3"] = i.p3;
         d["ar3_kw"] = i.ar3_kw;
         d["carry_xchg"] = i.carry_xchg;
         d["placement_sets"] = i.placement_sets;

@@ -279,7 +279,7 @@ def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     c4 = 0 if codes == "c8" else 1
     dia = 1 if codes == "dia4" else 0
     a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=1, carry_dia=dia,
-                     check_every=8)
+                     p3=0, check_every=8)
     b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=0, check_every=8)
     assert a.info["ap_recompute"] and not a.info["interleave"]
     assert a.info["dia4"] == (codes == "dia4") and a.info["codes4"] == (codes == "c4")
@@ -299,6 +299,43 @@ def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     assert a.true_residual_norm() == b.true_residual_norm()
 
 
+@pytest.mark.parametrize("problem,n,kw", [("poisson2d", 128, 0), ("poisson2d", 256, 0), ("poisson2d", 512, 0),
+                                          ("poisson3d", 64, 4), ("poisson3d", 128, 16)])
+def test_three_term_carry_tracks_two_term(mcg, problem, n, kw):
+    """Three-term form of the dia4 line carry (r_{k-1} = p_{k-1} - beta p_{k-2} from the two stored p's,
+    r kept only at slice edges and run outer lines): the same CG iterates up to rounding -- same
+    iteration count (+-1), x and ||r|| to ~1e-9 -- against the two-term form, at convergence and at
+    fixed odd / even counts (final pass, paired x updates); the recurrence residual tracks ||b - A x||."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    k3 = dict(carry3_kw=kw) if kw else {}
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, p3=1, check_every=8, **k3)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, p3=0, check_every=8, **k3)
+    assert a.info["p3"] and a.info["dia4"] and a.info["ap_recompute"] and not b.info["p3"]
+    assert a.info["bytes_per_iter_model"] < b.info["bytes_per_iter_model"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["converged"] and abs(ra["iterations"] - rb["iterations"]) <= 1
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-7, atol=1e-9 * np.abs(rb["x_local"]).max())
+    for its in (23, 24, 101):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["iterations"] == its
+        assert abs(outs[0][0]["rnorm"] - outs[1][0]["rnorm"]) <= 1e-9 * outs[1][0]["rnorm"]
+        np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-9, atol=1e-12 * np.abs(outs[1][1]).max())
+        tr = a.true_residual_norm()
+        assert abs(tr - outs[0][0]["rnorm"]) <= 1e-9 * tr
+
+
+def test_three_term_carry_refusal(mcg):
+    """p3 = 1 where the 2-D dia4 carry does not run: a clear error; auto is on with dia4."""
+    assert mcg.CGSolver(mcg.make_problem("poisson2d", n=256), format="sellc8", recurrence=1).info["p3"]
+    with pytest.raises(Exception, match="p3"):
+        mcg.CGSolver(mcg.make_problem("poisson2d", n=256), format="sellc8", recurrence=1, carry_dia=0, p3=1)
+
+
 @pytest.mark.parametrize("n,kw", [(64, 4), (128, 4), (128, 8), (128, 16)])
 def test_ap_recompute_3d_matches_store_form(mcg, n, kw):
     """3-D plane carry that recomputes Ap (SELL-64/dia4, +-N rows through LDS between the block's
@@ -306,7 +343,7 @@ def test_ap_recompute_3d_matches_store_form(mcg, n, kw):
     kw = 4 the blocks, waves and rows are the store form's, so every bit agrees; other kw group the
     dot-product partials differently (rounding only)."""
     spec = mcg.make_problem("poisson3d", n=n, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=1, carry3_kw=kw, check_every=8)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=1, carry3_kw=kw, p3=0, check_every=8)
     b = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=0, check_every=8)
     assert a.info["ap_recompute"] and a.info["dia4"] and a.info["ar3_kw"] == kw
     assert not b.info["ap_recompute"] and b.info["carry"]
