@@ -145,6 +145,8 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
   const double* __restrict__ apx_o = v.ap_old;  // multi-rank: ghost lines' Ap_{k-1}
   double* __restrict__ apx_n = v.ap_new;        // multi-rank: first / last line's Ap_k for the neighbours
   double* __restrict__ en = v.ape_new;
+  const double* __restrict__ reo = v.re_old;  // P3: edge rows' r_{k-1}
+  double* __restrict__ ren = v.re_new;        // edge rows' r_k (P3; and pass 0 of a P3 run, two-term kernel)
   const int lane = threadIdx.x & 63;
   const int64_t SS = tr.strip;            // slices per line
   const int32_t LO = (int32_t)(SS * 64);  // one line
@@ -241,14 +243,16 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       const int64_t s = oline(j) * SS + col;
       if (lane == 0) {
         const int32_t row = e >= 1 ? e - 1 : 0;
-        q.r = ro[row];
+        const int64_t c = s >= 1 ? 2 * (s - 1) + 1 : 0;
+        q.r = P3 ? reo[c] : ro[row];
         q.p = po[row];
-        q.a = eo[s >= 1 ? 2 * (s - 1) + 1 : 0];
+        q.a = eo[c];
       } else if (lane == 63) {
         const int32_t row = e + 64 < ext32 ? e + 64 : ext32 - 1;
-        q.r = ro[row];
+        const int64_t c = s + 1 < nsl ? 2 * (s + 1) : 2 * nsl - 1;
+        q.r = P3 ? reo[c] : ro[row];
         q.p = po[row];
-        q.a = eo[s + 1 < nsl ? 2 * (s + 1) : 2 * nsl - 1];
+        q.a = eo[c];
       }
     };
     auto load_xp = [&](int32_t j, XP& q) {
@@ -333,18 +337,21 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       // 3. Ap_k of line m, stores, partials
       const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1);
       const int32_t eb = e0 + m * LO;
+      const int64_t s = (l0 + m) * SS + col;
       if constexpr (P3) {
-        // r_k only where another wave (edge rows, the run's outer lines) or rank reads it, and as
-        // the value the next pass recovers from the stored p's, fma(-b, p_{k-1}, p_k): every reader
-        // of a row's r_k -- owner, neighbouring wave, neighbouring rank -- uses the same bits
-        if (m == 0 || m == n_run - 1) st_stream(&(rn + eb)[lane], fma(-b, o_pold, o_pk));
-        else if (lane == 0 || lane == 63) rn[eb + lane] = fma(-b, o_pold, o_pk);
+        // r_k only where another wave (edge rows: compact, next to their Ap; the run's outer
+        // lines) or rank reads it, and as the value the next pass recovers from the stored p's,
+        // fma(-b, p_{k-1}, p_k): every reader of a row's r_k -- owner, neighbouring wave,
+        // neighbouring rank -- uses the same bits
+        const double rr = fma(-b, o_pold, o_pk);
+        if (m == 0 || m == n_run - 1) st_stream(&(rn + eb)[lane], rr);
+        if (lane == 0 || lane == 63) ren[2 * s + (lane == 63 ? 1 : 0)] = rr;
       } else {
         st_stream(&(rn + eb)[lane], o_rk);
+        if (ren != nullptr && (lane == 0 || lane == 63)) ren[2 * s + (lane == 63 ? 1 : 0)] = o_rk;
       }
       if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, P3 ? o_pm2 : x0.pkm2, x0.xo)));
       st_stream(&(pn + eb)[lane], o_pk);
-      const int64_t s = (l0 + m) * SS + col;
       if (lane == 0 || lane == 63) en[2 * s + (lane == 63 ? 1 : 0)] = sum;
       if (apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) apx_n[eb + lane] = sum;
       s_pap = fma(o_pk, sum, s_pap);

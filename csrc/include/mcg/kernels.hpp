@@ -225,6 +225,10 @@ struct F1Vectors {
   // ext-layout Ap of the rank's first / last line and of its ghost lines (multi-rank, else null)
   const double* ape_old = nullptr;
   double* ape_new = nullptr;
+  // ... its three-term form: r of the same edge rows, same compact layout (2 doubles per slice), so
+  // the neighbouring waves read 16 contiguous bytes per slice instead of two scattered sectors
+  const double* re_old = nullptr;
+  double* re_new = nullptr;
 };
 // In-kernel reduction of a fused pass's block partials (replaces the cg_reduce_f1 launch, so
 // one iteration is ONE kernel + the 32-B all-reduce).  Two-level last-arriver fan-in: each block

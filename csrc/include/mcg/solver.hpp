@@ -146,6 +146,7 @@ class GpuCgSolver {
   bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)
+  bool probing_ = false;        // placement probe running: passes take k's kernels, never first / check
   bool split_ = false;          // interior / boundary launches around an overlapped halo
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
   bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them
