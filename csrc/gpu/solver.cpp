@@ -949,7 +949,9 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
                          s0_, rc, p3_);
       return;
     }
-    kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, opt_.carry_depth > 0 ? opt_.carry_depth : 3, S, v,
+    const int depth = ((k & 1) == 0 && opt_.carry_depth_even > 0) ? opt_.carry_depth_even
+                                                                  : (opt_.carry_depth > 0 ? opt_.carry_depth : 3);
+    kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
                       p3_);
     return;
