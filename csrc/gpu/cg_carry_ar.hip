@@ -112,7 +112,7 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
   }
 }
 
-template <int CM, int U, int QD, bool PAIR, bool P3>
+template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1>
 __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
@@ -309,7 +309,9 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       o_pk = fma(b, r0.p, o_rk);
     }
     double o_epk = edge_pk(ed0);
-    for (int32_t m = 0; m < n_run; ++m) {
+    // one line step; the rotation at its end is register renaming once the driver below unrolls
+    // the steps by the rotation period (a rolled loop pays ~30 64-bit moves per step)
+    auto step = [&](int32_t m) {
       // 1. loads for later steps, in the order they are waited for: metadata of line m + 3, codes
       //    of line m + 2 (metadata from the previous step), edges of line m + 2, x / p_{k-2} of
       //    line m + 1, operands of line m + 1 + QD.  All vector loads: the in-order vmcnt lets
@@ -373,7 +375,18 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       c0 = c1;
       c1 = c2;
       mt2 = mt3;
+    };
+    // P3 even passes: unrolled by 3, the period of the codes / p_k chains (the odd pass, with x, then
+    // spills; it runs at the HBM rate rolled)
+    constexpr int kUn = (P3 && !PAIR) ? UN : 1;
+    int32_t m = 0;
+    if constexpr (kUn > 1) {
+      for (; m + kUn <= n_run; m += kUn) {
+#pragma unroll
+        for (int u = 0; u < kUn; ++u) step(m + u);
+      }
     }
+    for (; m < n_run; ++m) step(m);
   }
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
@@ -816,7 +829,7 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* d
 
 void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol, int first,
-                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3) {
+                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3, int unroll) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
@@ -846,14 +859,15 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   }
   const bool pair = (k & 1) != 0;
   const int qd = depth <= 2 ? 2 : (depth >= 5 ? 5 : depth);
-#define MCG_A(CM, U, QD, PAIR, P3)                                                                      \
-  hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR, P3>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
-                     partials, pstride, st, tol, first, check, rc)
+#define MCG_A(CM, U, QD, PAIR, P3, ...)                                                                 \
+  hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR, P3, ##__VA_ARGS__>), dim3(grid), dim3(kBS), 0, stream, S, v, \
+                     own_off, tr, partials, pstride, st, tol, first, check, rc)
 #define MCG_AP(CM, U, QD)                                        \
   do {                                                           \
     if constexpr (CM == 4) {                                     \
       if (p3k) {                                                 \
         if (pair) MCG_A(CM, U, QD, true, true);                  \
+        else if (unroll > 1) MCG_A(CM, U, QD, false, true, 3);   \
         else MCG_A(CM, U, QD, false, true);                      \
         break;                                                   \
       }                                                          \

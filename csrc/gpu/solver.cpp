@@ -953,7 +953,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
                                                                   : (opt_.carry_depth > 0 ? opt_.carry_depth : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
-                      p3_);
+                      p3_, opt_.carry_unroll);
     return;
   }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {

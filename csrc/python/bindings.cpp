@@ -220,6 +220,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry_dia", &CgOptions::carry_dia)
       .def_readwrite("p3", &CgOptions::p3)
       .def_readwrite("carry_depth_even", &CgOptions::carry_depth_even)
+      .def_readwrite("carry_unroll", &CgOptions::carry_unroll)
       .def_readwrite("carry3_kw", &CgOptions::carry3_kw)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
