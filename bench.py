@@ -245,7 +245,8 @@ def _run_rank(args, out_fd) -> int:
                 "format": ("sell64-dia4" if info.get("dia4") else "sell64-c4" if info.get("codes4")
                            else info["format"]),
                 "recurrence": info["recurrence"],
-                "pass": ("line-carry" if info.get("carry") else "split (materialized p)" if info.get("pmat")
+                "pass": (("line-carry, three-term (r from p_{k-1}, p_{k-2})" if info.get("p3") else "line-carry")
+                         if info.get("carry") else "split (materialized p)" if info.get("pmat")
                          else "windowed" if info.get("window") else "generic, xcd-aware" if info.get("xcd_map")
                          else "generic"),
                 "ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
