@@ -463,6 +463,13 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
   double* __restrict__ x = v.x;
   const double* __restrict__ apo = v.ap_old;  // Ap_{k-1}: outer lines, edge rows, ghost planes
   double* __restrict__ apw = v.ap_new;
+  // P3: the slices' edge rows' Ap and r in compact per-slice arrays (2 doubles per slice each, as
+  // k_cg_carry_ar), not scattered through the ext-layout vectors; pass 0 (two-term kernel) fills them
+  const double* __restrict__ eao = v.ape_old;
+  double* __restrict__ ean = v.ape_new;
+  const double* __restrict__ reo = v.re_old;
+  double* __restrict__ ren = v.re_new;
+  const int64_t nsl = tr.nt0;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t SS = tr.strip;            // slices per plane
@@ -533,9 +540,16 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       const int32_t e = ebase(j);
       if (lane == 0 || lane == 63) {
         const int32_t row = clampr(lane == 0 ? e - 1 : e + 64);
-        r.r = ro[row];
         r.p = po[row];
-        r.a = apo[row];
+        if constexpr (P3) {
+          const int64_t sj = oline(j) * SS + col;
+          const int64_t c = lane == 0 ? (sj >= 1 ? 2 * (sj - 1) + 1 : 0) : (sj + 1 < nsl ? 2 * (sj + 1) : 2 * nsl - 1);
+          r.r = reo[c];
+          r.a = eao[c];
+        } else {
+          r.r = ro[row];
+          r.a = apo[row];
+        }
       }
     };
     auto load_far = [&](int32_t j, Far& f) {
@@ -613,6 +627,11 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     double o_fpk = pk_of(f0.r, f0.a, f0.p);  // p_k of the outside row, plane 0
     for (int32_t m = 0; m < n_run; ++m) {
       const int par = m & 1;
+      if constexpr (P3) {  // r_k of plane m where another wave or rank reads it (stored early: short live range)
+        const int32_t eb = e0 + m * LO;
+        if (m == 0 || m == n_run - 1) st_stream(&(rn + eb)[lane], fma(-b, o_pold, o_pk));
+        else if (odn || oup) rn[eb + lane] = fma(-b, o_pold, o_pk);  // edge rows: compact (below)
+      }
       // 1. loads for later steps: codes / edges of plane m + 2, the outside row of m + 2, x / p_{k-2}
       //    of m + 1, operands of m + 1 + QD
       ArCodes<4, U> c2;
@@ -647,15 +666,16 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       nbr(par, 1, o_fpk, kdn, kup);
       const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1, kdn, kup);
       const int32_t eb = e0 + m * LO;
-      if constexpr (P3) {  // r_k where another wave or rank reads it, as the value the next pass recovers
-        if (m == 0 || m == n_run - 1) st_stream(&(rn + eb)[lane], fma(-b, o_pold, o_pk));
-        else if (odn || oup || lane == 0 || lane == 63) rn[eb + lane] = fma(-b, o_pold, o_pk);
-      } else {
-        st_stream(&(rn + eb)[lane], o_rk);
-      }
+      if constexpr (!P3) st_stream(&(rn + eb)[lane], o_rk);  // P3: stored at the step's start
       if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, P3 ? o_pm2 : x0.pkm2, x0.xo)));
       st_stream(&(pn + eb)[lane], o_pk);
-      if (odn || oup || lane == 0 || lane == 63 || (gfull && (l0 + m == 0 || l0 + m == nl - 1))) apw[eb + lane] = sum;
+      const bool edge_lane = lane == 0 || lane == 63;
+      if (odn || oup || (!P3 && edge_lane) || (gfull && (l0 + m == 0 || l0 + m == nl - 1))) apw[eb + lane] = sum;
+      if (edge_lane && (P3 || ean != nullptr)) {  // compact edge rows (P3, and pass 0 of a P3 run)
+        const int64_t c = 2 * ((l0 + m) * SS + col) + (lane == 63 ? 1 : 0);
+        ean[c] = sum;
+        ren[c] = P3 ? fma(-b, o_pold, o_pk) : o_rk;
+      }
       s_pap = fma(o_pk, sum, s_pap);
       s_rap = fma(o_rk, sum, s_rap);
       s_apap = fma(sum, sum, s_apap);

@@ -573,9 +573,9 @@ void GpuCgSolver::setup() {
   info_.dia4 = dia4_.get() != nullptr;
   // three-term form: the 2-D dia4 carry (the halo still carries r of the ghost lines: every rank
   // stores r on its first / last line in either form, so ranks need not agree on it)
-  // auto: the 2-D carry only (the 3-D plane carry's three-term kernel needs more than the 128 VGPRs
-  // of its 16-wave blocks and spills; p3 = 1 forces it)
-  p3_ = ar_ && info_.dia4 && (opt_.p3 == 1 || (opt_.p3 < 0 && !ar3_));
+  // auto: on for the 2-D line carry and the 3-D plane carry (whose three-term kernel spills a few
+  // registers at 16-wave blocks and is still 15 % faster: profiles/r2s6_p3_16384.md)
+  p3_ = ar_ && info_.dia4 && opt_.p3 != 0;
   MCG_CHECK(opt_.p3 != 1 || p3_, "p3 needs the Ap-recomputing line / plane carry on SELL-64/dia4");
   info_.p3 = p3_;
   if (ar_ && !info_.dia4 && n > 0) {
@@ -685,7 +685,7 @@ void GpuCgSolver::allocate_vectors_() {
     r_.allocate(L_.ext_len, "r", 8, 2 * skew, cap);
     r1_.allocate(L_.ext_len, "r", 8, 3 * skew, cap);
     const int64_t ns = (n + 63) / 64;
-    if (!ar3_) {  // 3-D: the slices' edge rows go through the ext-layout Ap like the outer lines
+    if (!ar3_ || p3_) {  // 3-D two-term: the slices' edge rows go through the ext-layout Ap like the outer lines
       // three-term form: the edge rows' r behind their Ap (F1Vectors::re_old / re_new)
       const int64_t per = p3_ ? 4 : 2;
       ape_[0].allocate(per * std::max<int64_t>(ns, 1), "Ap", 8);
@@ -938,7 +938,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     v.ap_new = apx_[k & 1].get();
     v.ape_old = ape_[(k + 1) & 1].get();
     v.ape_new = ape_[k & 1].get();
-    if (p3_ && !ar3_) {
+    if (p3_) {
       const int64_t ns2 = 2 * std::max<int64_t>((n + 63) / 64, 1);
       v.re_old = ape_[(k + 1) & 1].get() + ns2;
       v.re_new = ape_[k & 1].get() + ns2;
