@@ -113,7 +113,7 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
 }
 
 template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1>
-__global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+__global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
   __shared__ double2 s_dict[CM == 4 ? 1 : 256];
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
     };
     // P3 even passes: unrolled by 3, the period of the codes / p_k chains (the odd pass, with x, then
     // spills; it runs at the HBM rate rolled)
-    constexpr int kUn = (P3 && !PAIR) ? UN : 1;
+    constexpr int kUn = (P3 && !PAIR && UN != 5) ? UN : 1;  // UN == 5: rolled, 5 waves per SIMD
     int32_t m = 0;
     if constexpr (kUn > 1) {
       for (; m + kUn <= n_run; m += kUn) {
@@ -887,6 +887,7 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     if constexpr (CM == 4) {                                     \
       if (p3k) {                                                 \
         if (pair) MCG_A(CM, U, QD, true, true);                  \
+        else if (unroll == 5) MCG_A(CM, U, QD, false, true, 5);  \
         else if (unroll > 1) MCG_A(CM, U, QD, false, true, 3);   \
         else MCG_A(CM, U, QD, false, true);                      \
         break;                                                   \

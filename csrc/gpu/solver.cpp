@@ -495,11 +495,15 @@ void GpuCgSolver::setup() {
               "line-carry pass needs SELL d16/c8, interleaved pairs, rows <= param <= 8 and whole 64-row grid lines");
     if (ok && opt_.carry != 0) {
       const int64_t S = gl / 64;
-      const int g = ncu_ * std::max(1, opt_.carry_blocks_per_cu);
+      // auto grid: 8 blocks per CU (two rounds of resident blocks, so CUs that finish early take more
+      // jobs) when the launch has >= 4096 lines, else 4 (shorter runs would re-read their prologue
+      // lines too often): 16384^2 509-516 vs 500-508 it/s, 4096^2 7224 vs 7028, a P = 8 rank's 2048
+      // lines 3919 at 4 vs 3850 at 8 (profiles/r2s6_carry_grid.md)
       auto apply = [&](TileRanges& t, int& grid) {
         if (t.ntiles == 0 || t.nt0 != t.ntiles || t.b0 % S != 0 || t.nt0 % S != 0 || t.nt0 / S < 2) return false;
         t.strip = (int32_t)S;
-        grid = g;
+        const int bpc_c = opt_.carry_blocks_per_cu > 0 ? opt_.carry_blocks_per_cu : (t.nt0 / S >= 4096 ? 8 : 4);
+        grid = ncu_ * bpc_c;
         return true;
       };
       // the specialised pass (no slow path) when every stored offset is carried: 0, +-1, +-one line

@@ -50,7 +50,8 @@ struct CgOptions {
                              // per grid line / plane): line-carry pass — a wave walks down a column of slices and
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
-  int carry_blocks_per_cu = 4;  // grid of the line-carry pass (one job = a run of lines of one slice column)
+  int carry_blocks_per_cu = 0;  // grid of the line-carry pass (one job = a run of lines of one slice column);
+                                // 0 = auto (8 when the launch covers >= 4096 lines, else 4)
   int carry_nt = 0;             // line-carry pass: non-temporal loads of the operands each wave reads once (measured
                                 // slower: 281 vs 302 it/s 2-D, 480 vs 531 3-D; the +-1 edge rows are re-read from L2)
   int carry_c4 = 1;             // line-carry pass on a c8 matrix with <= 16 dictionary entries: 4-bit codes
