@@ -560,7 +560,9 @@ void GpuCgSolver::setup() {
     MCG_CHECK(opt_.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
               "3-D: dia4, N a multiple of 64 and of carry3_kw)");
-    if (ar3_) g_all_ = ncu_ * 4 * 4 / kw;  // 4 waves per SIMD
+    // 4 waves per SIMD (one round of resident blocks); carry_blocks_per_cu > 0: that many 4-wave
+    // block equivalents per CU
+    if (ar3_) g_all_ = std::max(1, ncu_ * (opt_.carry_blocks_per_cu > 0 ? opt_.carry_blocks_per_cu : 4) * 4 / kw);
     info_.ar3_kw = ar3_ ? kw : 0;
     info_.carry_xchg = info_.carry && carry_lo2_ > 0 && opt_.carry_3d == 2 &&
                        kern::carry_block_exchange_ok(info_.spmv_param, carry_lo2_, gl / 64);
