@@ -41,6 +41,10 @@ namespace {
 
 #include "f1_common.hpp"
 
+#ifndef MCG_EDGE_BRANCHLESS
+#define MCG_EDGE_BRANCHLESS 1
+#endif
+
 __device__ __forceinline__ double ld_once(const double* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
 
 // a slice's codes for one lane: c4 nibbles / c8 bytes packed into 32-bit registers (entry u at
@@ -241,6 +245,17 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
     auto load_edge = [&](int32_t j, Edge& q) {
       const int32_t e = ebase(j);
       const int64_t s = oline(j) * SS + col;
+      if constexpr (P3 && MCG_EDGE_BRANCHLESS) {
+        // every lane loads (lanes 1-62 at lane 0's addresses, the same cache lines): selects instead
+        // of exec-mask branches around the two edge lanes
+        const bool hi = lane == 63;
+        const int32_t row = hi ? (e + 64 < ext32 ? e + 64 : ext32 - 1) : (e >= 1 ? e - 1 : 0);
+        const int64_t c = hi ? (s + 1 < nsl ? 2 * (s + 1) : 2 * nsl - 1) : (s >= 1 ? 2 * (s - 1) + 1 : 0);
+        q.r = reo[c];
+        q.p = po[row];
+        q.a = eo[c];
+        return;
+      }
       if (lane == 0) {
         const int32_t row = e >= 1 ? e - 1 : 0;
         const int64_t c = s >= 1 ? 2 * (s - 1) + 1 : 0;
