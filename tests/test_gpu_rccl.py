@@ -77,6 +77,26 @@ def test_native_cli_threads_match_cpu(mcg, world, problem, mode):
 
 @needs2
 @pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("args", [["--problem", "poisson2d", "--n", "128"], ["--problem", "poisson3d", "--n", "64"]])
+@pytest.mark.parametrize("mode", [[], ["--no-graph"]])
+def test_native_cli_threads_carry_paths_match_cpu(mcg, world, args, mode):
+    """The default stencil path at P > 1 over real RCCL: dia4 line / plane carry in the three-term
+    form, halo ahead of the pass (r, Ap, p of the ghost lines), graphs with the collectives."""
+    x_cpu, rep_cpu = _cpu_x(mcg, args)
+    p = _run([mcg.cli_path(), "--gpus", str(world), "--print-x", "yes", "--report", "json", "--verify",
+              "--watchdog", "120"] + mode + args)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = p.stdout.splitlines()
+    rep = json.loads(lines[-2])
+    x = np.array([float(v) for v in lines[:-2]])
+    assert rep["ranks"] == world and rep["converged"]
+    assert abs(rep["iterations"] - rep_cpu["iterations"]) <= max(2, rep_cpu["iterations"] // 100)
+    assert rep["true_rnorm"] < 1e-6
+    np.testing.assert_allclose(x, x_cpu, atol=2e-6 * np.abs(x_cpu).max())
+
+
+@needs2
+@pytest.mark.parametrize("world", WORLDS)
 @pytest.mark.parametrize("problem", ["poisson2d", "randspd_wide"])
 def test_bench_launcher_processes(world, problem):
     """bench.py --gpus P starts P processes; all ranks agree and the true residual matches."""
