@@ -290,6 +290,10 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
     auto edge_pk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };  // p_k of the edge row
     // ghost line: Ap_{k-1} exchanged by the halo (multi-rank only)
     auto ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jmin && j <= jmax; };
+    // r_{k-1} of a ghost line (P > 1).  P3: recovered like an own line -- no wave writes the ghost
+    // rows, and the halo delivered p_{k-2} into p_new's ghost rows two iterations ago -- so the halo
+    // carries {Ap, p} and not r (one extra load, at a run's outer step only)
+    auto rghost = [&](int32_t j, const Raw& q) { return P3 && !first ? fma(nbp, pn[ebase(j) + lane], q.p) : q.r; };
 
     // prologue: p_k of lines -1 and 0, r_k of line 0; operands of lines 1 .. QD, codes of 0, 1
     Raw rm2, rm1, r0, rq[QD];
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
       pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
     } else if (ghost(-1)) {
       const double t = apx_o[ebase(-1) + lane];
-      pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
+      pr_pk = fma(b, rm1.p, fma(na, t, rghost(-1, rm1)));
     }
     double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
     {
@@ -348,7 +352,7 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
         pk1 = fma(b, rq[0].p, rk1);
       } else if (ghost(m + 1)) {
         const double t = apx_o[ebase(m + 1) + lane];
-        rk1 = fma(na, t, rof(m + 1, rq[0]));
+        rk1 = fma(na, t, rghost(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       }
       // 3. Ap_k of line m, stores, partials
@@ -586,6 +590,8 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       ar_load_dia<U>(S.dia4 + (oline(j) * SS + col) * (32 * U), lane, c);
     };
     auto ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jmin && j <= jmax; };
+    // ghost plane's r_{k-1}: P3 recovers it from the halo's p's (k_cg_carry_ar's rghost)
+    auto rghost = [&](int32_t j, const Raw& q) { return P3 && !first ? fma(nbp, pn[ebase(j) + lane], q.p) : q.r; };
     auto edge_pk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
     // neighbour waves' values through LDS (outer waves: `far` for the side outside the block)
     auto nbr = [&](int par, int which, double far, double& dn, double& up) {
@@ -628,7 +634,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       const double t = stencil(cm1, rm1.p, edm1.p, rm2.p, r0.p, dn, up);
       pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
     } else if (ghost(-1)) {
-      pr_pk = pk_of(rof(-1, rm1), apo[ebase(-1) + lane], rm1.p);
+      pr_pk = pk_of(rghost(-1, rm1), apo[ebase(-1) + lane], rm1.p);
     }
     double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
     {
@@ -673,7 +679,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
         pk1 = fma(b, rq[0].p, rk1);
       } else if (ghost(m + 1)) {
         const double t = apo[ebase(m + 1) + lane];
-        rk1 = fma(na, t, rof(m + 1, rq[0]));
+        rk1 = fma(na, t, rghost(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       }
       // 4. Ap_k of plane m, stores, partials

@@ -999,6 +999,12 @@ void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
     w = widths;
   }
   if (ar_) vecs[1] = apx_[(k + 1) & 1].get();  // Ap of the ghost lines: the owners' stored first / last line
+  if (p3_ && k > 0) {  // three-term form: a ghost line's r is recovered from its p_{k-1}, p_{k-2} (both
+                       // received); iteration 0 (two-term kernel) reads r_{-1} = b of the ghosts
+    vecs[0] = vecs[1];
+    vecs[1] = vecs[2];
+    nv = 2;
+  }
   comm_->halo_exchange(L_, vecs, nv, s, w);
 }
 
