@@ -657,12 +657,16 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       //    of m + 1, operands of m + 1 + QD
       ArCodes<4, U> c2;
       load_codes(m + 2, c2);
+      // P3: the edge and outside rows of plane m + 2 are loaded at the end of the step instead
+      // (one set live instead of two: the three-term kernel is at the 128-VGPR limit)
       Edge ed2{0.0, 0.0, 0.0};
-      load_edge(m + 2, ed2);
       Far fb{0.0, 0.0, 0.0};
-      load_far(m + 2, fb);
+      if constexpr (!P3) {
+        load_edge(m + 2, ed2);
+        load_far(m + 2, fb);
+      }
       XP x1{0.0, 0.0};
-      load_xp(m + 1, x1);
+      if constexpr (!P3) load_xp(m + 1, x1);  // P3: at the end of the step (below)
       Raw rnq;
       load_raw(m + 1 + QD, rnq);
       // 2. exchange: p_{k-1} of plane m + 1 and p_k of plane m with the neighbouring waves
@@ -709,12 +713,18 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       o_pm2 = rq[0].r;
       o_epk = edge_pk(ed1);
       o_fpk = pk_of(fa.r, fa.a, fa.p);
-      fa = fb;
-      ed1 = ed2;
+      if constexpr (P3) {
+        load_edge(m + 2, ed1);
+        load_far(m + 2, fa);
+        load_xp(m + 1, x0);
+      } else {
+        fa = fb;
+        ed1 = ed2;
+      }
 #pragma unroll
       for (int d = 0; d + 1 < QD; ++d) rq[d] = rq[d + 1];
       rq[QD - 1] = rnq;
-      x0 = x1;
+      if constexpr (!P3) x0 = x1;
       c0 = c1;
       c1 = c2;
     }
