@@ -582,6 +582,8 @@ void GpuCgSolver::setup() {
   // auto: on for the 2-D line carry and the 3-D plane carry (whose three-term kernel spills a few
   // registers at 16-wave blocks and is still 15 % faster: profiles/r2s6_p3_16384.md)
   p3_ = ar_ && info_.dia4 && opt_.p3 != 0;
+  // every rank takes the same form: it decides how many vectors the halo carries ({Ap, p} or {r, Ap, p})
+  if (use_comm_ && world_ > 1 && !all_ranks_agree_(p3_)) p3_ = false;
   MCG_CHECK(opt_.p3 != 1 || p3_, "p3 needs the Ap-recomputing line / plane carry on SELL-64/dia4");
   info_.p3 = p3_;
   if (ar_ && !info_.dia4 && n > 0) {
@@ -1372,10 +1374,11 @@ CgResult GpuCgSolver::solve(bool resume) {
 
 // ---- checkpoint / resume ----------------------------------------------------
 namespace {
-constexpr char kCkptMagic[8] = {'M', 'C', 'G', 'C', 'K', 'P', 'T', '1'};
+constexpr char kCkptMagic[8] = {'M', 'C', 'G', 'C', 'K', 'P', 'T', '2'};
 struct CkptHeader {
   char magic[8];
   int32_t rank, world, recurrence, format;
+  int32_t pass_form, pad_;  // bit 0: Ap recomputed, bit 1: three-term (the vectors hold different state)
   int64_t n_local, ext_len, row_begin, k;
   int64_t n_global;
   uint64_t seed;
@@ -1396,6 +1399,7 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
   h.world = world_;
   h.recurrence = opt_.recurrence;
   h.format = info_.format;
+  h.pass_form = (ar_ ? 1 : 0) | (p3_ ? 2 : 0);
   h.n_local = L_.n_local();
   h.ext_len = L_.ext_len;
   h.row_begin = L_.row_begin;
@@ -1426,6 +1430,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   CkptHeader h{};
   bool ok = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, 8) == 0;
   ok = ok && h.rank == rank_ && h.world == world_ && h.recurrence == opt_.recurrence && h.format == info_.format &&
+       h.pass_form == ((ar_ ? 1 : 0) | (p3_ ? 2 : 0)) &&
        h.n_local == L_.n_local() && h.ext_len == L_.ext_len && h.row_begin == L_.row_begin &&
        h.n_global == L_.n_global && h.seed == spec_.seed;
   if (!ok) {
