@@ -32,6 +32,28 @@ def test_checkpoint_resume_matches_uninterrupted(mcg, tmp_path, recurrence):
     np.testing.assert_array_equal(out["x_local"], full["x_local"])
 
 
+@pytest.mark.parametrize("p3", [0, 1])
+def test_checkpoint_resume_default_stencil_path(mcg, tmp_path, p3):
+    """The default stencil path (dia4 line carry, Ap recomputed; p3 = three-term form, whose r lives
+    only at edge rows / run outer lines and whose beta_{k-2} is in CgState): resume is bitwise equal
+    to the uninterrupted solve; a checkpoint of the other pass form is refused."""
+    spec = mcg.make_problem("poisson2d", n=256, rhs="random")
+    kw = dict(format="sellc8", recurrence=1, p3=p3, check_every=8)
+    full = mcg.CGSolver(spec, **kw).solve()
+    prefix = str(tmp_path / "ck")
+    a = mcg.CGSolver(spec, maxit=120, checkpoint_every=48, checkpoint_path=prefix, **kw)
+    assert a.info["p3"] == bool(p3) and a.info["ap_recompute"]
+    a.solve()
+    b = mcg.CGSolver(spec, **kw)
+    b.load_checkpoint(prefix)
+    out = b.solve(resume=True)
+    assert out["converged"] and out["iterations"] == full["iterations"] and out["rnorm"] == full["rnorm"]
+    np.testing.assert_array_equal(out["x_local"], full["x_local"])
+    other = mcg.CGSolver(spec, **dict(kw, p3=1 - p3))
+    with pytest.raises(Exception, match="does not match"):
+        other.load_checkpoint(prefix)
+
+
 def test_checkpoint_rejects_other_problem(mcg, tmp_path):
     prefix = str(tmp_path / "c")
     s = mcg.CGSolver(mcg.make_problem("poisson2d", n=64), maxit=5)
