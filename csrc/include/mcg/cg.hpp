@@ -62,7 +62,9 @@ struct CgOptions {
                                 // 301 it/s at 2; 3-D 1: the +-N rows, gathered one plane ahead, then meet the
                                 // neighbouring column's own prefetch in the L2: 534 vs 518 it/s at 2)
   int carry_unroll = 3;         // three-term 2-D carry, even passes: line steps unrolled by 3 (the period of the
-                                // codes / p_k rotations: renaming instead of 64-bit moves); 1 = rolled
+                                // codes / p_k rotations: renaming instead of 64-bit moves); 1 = rolled; 5 =
+                                // experiment: rolled at 5 waves per SIMD (96 VGPRs, spills; no gain,
+                                // profiles/r2s6_carry_grid.md)
   int carry_depth_even = 0;     // 2-D Ap-recomputing carry: prefetch depth of the even passes (no x update), 0 = as
                                 // carry_depth
   int placement_tries = 3;   // single-reduction form: time the pass on this many physical placements of the vector
