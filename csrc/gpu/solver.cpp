@@ -1576,6 +1576,7 @@ CgResult GpuCgSolver::result() {
   r.converged = st.converged != 0;
   r.breakdown = st.breakdown != 0;
   r.beta_clamps = st.clamps;
+  r.rr0_local = st.rr0;
   r.rnorm = std::sqrt(st.done ? st.rr_final : (opt_.recurrence == 1 ? st.red[3] : st.rr_new));
   r.setup_seconds = setup_seconds_;
   float ms = 0.f;

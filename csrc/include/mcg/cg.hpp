@@ -130,6 +130,7 @@ struct CgResult {
   bool breakdown = false;    // NaN/Inf in a reduction
   double rnorm = 0.0;        // final ||r||_2 (recurrence residual)
   int beta_clamps = 0;       // single-reduction form: passes whose expanded ||r_k||^2 estimate was clamped at 0
+  double rr0_local = 0.0;    // b.b over this rank's rows (||r_0||^2 summed over ranks)
   double setup_seconds = 0.0;
   double solve_seconds = 0.0;
   double iters_per_second() const { return solve_seconds > 0 ? iterations / solve_seconds : 0.0; }

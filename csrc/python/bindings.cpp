@@ -74,6 +74,7 @@ py::dict result_dict(const CgResult& r) {
   d["breakdown"] = r.breakdown;
   d["rnorm"] = r.rnorm;
   d["beta_clamps"] = r.beta_clamps;
+  d["rr0_local"] = r.rr0_local;
   d["setup_seconds"] = r.setup_seconds;
   d["solve_seconds"] = r.solve_seconds;
   d["iters_per_second"] = r.iters_per_second();
