@@ -79,7 +79,7 @@ def recipes(a) -> dict:
         "prof": [
             ("trace", 300, prof(f"prof{g}", f"{PY} {ROOT}/bench.py --grid {g} --steps 64 --warmup 8 --phases 0 "
                                             f"--force-comm")),
-            ("summary", 60, f"{PY} bench/trace_summary.py {OUT}/prof{g}/run_results.db --iters 48"),
+            ("summary", 60, f"{PY} bench/trace_summary.py {OUT}/prof{g}/run_results.db --pass k_cg_carry_ar --iters 48"),
         ],
         # counter passes (one group per run) of the headline pass
         "pmc": [
