@@ -313,6 +313,13 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
     uint32_t mt2 = load_meta(2);  // codes metadata one step ahead of the codes loads
     XP x0{0.0, 0.0};
     load_xp(0, x0);
+    // even three-term pass (E3): edge rows two lines ahead, so the operand, codes and edge streams
+    // are chains of 3 registers that the 3-step unroll renames -- no register whose load is in
+    // flight is moved at the end of a step (a move waits for its load, which drained every step's
+    // prefetches before the next step)
+    constexpr bool E3 = P3 && !PAIR && UN == 3 && QD == 2;
+    Edge ed2p;
+    if constexpr (E3) load_edge(2, ed2p);
     double pr_pk = 0.0;
     if (owned(-1)) {
       const double t = stencil(cm1, rm1.p, edge_p(edm1), rm2.p, r0.p);
@@ -338,8 +345,8 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
       const uint32_t mt3 = load_meta(m + 3);
       ArCodes<CM, U> c2;
       load_codes(mt2, c2);
-      Edge ed2;
-      load_edge(m + 2, ed2);
+      Edge ed2;  // edges of line m + 2 (E3: m + 3)
+      load_edge(m + (E3 ? 3 : 2), ed2);
       XP x1{0.0, 0.0};
       load_xp(m + 1, x1);
       Raw rnq;
@@ -386,7 +393,12 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
       o_pold = rq[0].p;
       o_pm2 = rq[0].r;
       o_epk = edge_pk(ed1);
-      ed1 = ed2;
+      if constexpr (E3) {
+        ed1 = ed2p;
+        ed2p = ed2;
+      } else {
+        ed1 = ed2;
+      }
 #pragma unroll
       for (int d = 0; d + 1 < QD; ++d) rq[d] = rq[d + 1];
       rq[QD - 1] = rnq;

@@ -957,8 +957,12 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
                          s0_, rc, p3_);
       return;
     }
-    const int depth = ((k & 1) == 0 && opt_.carry_depth_even > 0) ? opt_.carry_depth_even
-                                                                  : (opt_.carry_depth > 0 ? opt_.carry_depth : 3);
+    // three-term even passes: operands 2 lines ahead (chains of 3 registers, renamed by the 3-step unroll)
+    const int depth = ((k & 1) == 0 && opt_.carry_depth_even > 0)
+                          ? opt_.carry_depth_even
+                          : ((k & 1) == 0 && p3_ && opt_.carry_unroll == 3 && opt_.carry_depth <= 0)
+                                ? 2
+                                : (opt_.carry_depth > 0 ? opt_.carry_depth : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
                       p3_, opt_.carry_unroll);
