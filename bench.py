@@ -41,6 +41,22 @@ def aggregate(steps, ranks):
     return steps / dt, dt, ok
 
 
+def pass_label(info, problem):
+    """The pass the timed iterations run, as the solver chose it."""
+    if info.get("carry"):
+        kind = "plane-carry" if problem == "poisson3d" or info.get("ar3_kw") else "line-carry"
+        if info.get("p3"):
+            kind += ", three-term (r from p_{k-1}, p_{k-2})"
+        if info.get("ap_recompute"):
+            kind += ", Ap recomputed"
+        return kind
+    if info.get("pmat"):
+        return "split (materialized p)"
+    if info.get("window"):
+        return "windowed"
+    return "generic, xcd-aware" if info.get("xcd_map") else "generic"
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -52,7 +68,9 @@ def parse_args(argv=None):
     ap.add_argument("--band", type=int, default=4096, help="randspd: half bandwidth")
     ap.add_argument("--density", type=float, default=0.16, help="randspd: candidate-pair density")
     ap.add_argument("--spread", type=int, default=0,
-                    help="randspd: > 0 = candidate offsets over [1, spread] (unstructured; the all-gather path)")
+                    help="randspd: > 0 = candidate offsets over [1, spread] (wide multi-diagonal; the all-gather path)")
+    ap.add_argument("--scramble", type=int, default=0,
+                    help="randspd: 1 = P^T A P with a seeded random permutation P (genuinely irregular sparsity)")
     ap.add_argument("--format", default="sellc8", choices=["csr", "sell", "sell16", "sellc8"],
                     help="sparse storage: CSR, SELL-64, SELL-64/d16 (16-bit column offsets) or SELL-64/c8 "
                          "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
@@ -132,7 +150,7 @@ def _run_rank(args, out_fd) -> int:
 
     if args.problem == "randspd":
         spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, spread=args.spread,
-                                rhs="random")
+                                scramble=args.scramble, rhs="random")
     else:
         spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
     C = mcg.native()
@@ -222,7 +240,7 @@ def _run_rank(args, out_fd) -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             extra["phase_us_max"] = {k: round(float(v), 2) for k, v in zip(keys, t.tolist())}
     model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" + (f"_spread{args.spread}" if args.spread else "")
-             if args.problem == "randspd" else f"{args.problem}_N{args.grid}")
+             + ("_scrambled" if args.scramble else "") if args.problem == "randspd" else f"{args.problem}_N{args.grid}")
     if env.rank == 0:
         line = json.dumps({
             "metric": METRIC if headline else (
@@ -240,7 +258,8 @@ def _run_rank(args, out_fd) -> int:
             "dtype": "fp64",
             "data": "synthetic (on-device generated %s matrix, random RHS)" % {
                 "poisson2d": "5-pt Poisson", "poisson3d": "7-pt Poisson",
-                "randspd": "random SPD " + ("wide/unstructured" if args.spread else "banded")}[args.problem],
+                "randspd": "random SPD " + ("scrambled P^T A P (irregular)" if args.scramble else
+                                            "wide multi-diagonal" if args.spread else "banded")}[args.problem],
             "config": {
                 "model": model,
                 "problem": args.problem,
@@ -254,13 +273,10 @@ def _run_rank(args, out_fd) -> int:
                 "format": ("sell64-dia4" if info.get("dia4") else "sell64-c4" if info.get("codes4")
                            else info["format"]),
                 "recurrence": info["recurrence"],
-                "pass": (("line-carry, three-term (r from p_{k-1}, p_{k-2})" if info.get("p3") else "line-carry")
-                         if info.get("carry") else "split (materialized p)" if info.get("pmat")
-                         else "windowed" if info.get("window") else "generic, xcd-aware" if info.get("xcd_map")
-                         else "generic"),
-                "ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
-                if info.get("allgather") else ("window, exchanged ahead || all-reduce" if info.get("halo_ahead")
-                                               else "window"),
+                "pass": pass_label(info, args.problem),
+                **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
+                    if info.get("allgather") else ("window, exchanged ahead || all-reduce" if info.get("halo_ahead")
+                                                   else "window")} if (n_gpus > 1 or sim) else {}),
                 "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1,

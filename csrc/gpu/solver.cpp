@@ -178,6 +178,7 @@ void GpuCgSolver::setup() {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   const int64_t n = L_.n_local();
+  fingerprint_ = problem_fingerprint(spec_);
   info_.n_global = L_.n_global;
   info_.n_local = n;
   info_.ext_len = L_.ext_len;
@@ -250,7 +251,7 @@ void GpuCgSolver::setup() {
     slice_ptr_.allocate(ns + 1, "A");
     // SELL-64/aligned: the same decision on every rank (from the spec, not from this rank's rows),
     // since it implies the split pass and with it the ghost vectors exchanged
-    aligned_ = spec_.kind == ProblemKind::RandomSPD && spec_.spread > 0 && opt_.recurrence == 1 &&
+    aligned_ = spec_.kind == ProblemKind::RandomSPD && spec_.spread > 0 && !spec_.scramble && opt_.recurrence == 1 &&
                opt_.pmat != 0 && opt_.sell_aligned != 0 &&
                (opt_.sell_aligned == 1 || randspd_aligned_fill(spec_) <= 1.6);
     if (aligned_) kern::randspd_aligned_widths(spec_, L_.row_begin, n, slice_ptr_.get(), s0_);
@@ -827,6 +828,9 @@ void GpuCgSolver::reset() {
   MCG_CHECK(setup_done_, "solver not set up");
   const int64_t n = L_.n_local();
   hipStream_t s = s0_;
+  // a halo prefetched by the last iteration may still be sending / receiving rows of r, Ap and p
+  // on s1_: order the memsets below after it (no write of s0_ may race the side stream's RCCL)
+  join_halo_();
   MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
   for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1]})
     if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
@@ -865,7 +869,6 @@ void GpuCgSolver::reset() {
     }
     opt_.tol = tol;
   }
-  join_halo_();
   k_ = 0;
   finalized_ = false;
   halo_ready_for_ = -1;
@@ -1378,7 +1381,7 @@ CgResult GpuCgSolver::solve(bool resume) {
 
 // ---- checkpoint / resume ----------------------------------------------------
 namespace {
-constexpr char kCkptMagic[8] = {'M', 'C', 'G', 'C', 'K', 'P', 'T', '2'};
+constexpr char kCkptMagic[8] = {'M', 'C', 'G', 'C', 'K', 'P', 'T', '3'};
 struct CkptHeader {
   char magic[8];
   int32_t rank, world, recurrence, format;
@@ -1386,6 +1389,9 @@ struct CkptHeader {
   int64_t n_local, ext_len, row_begin, k;
   int64_t n_global;
   uint64_t seed;
+  int32_t kind, rhs;        // ProblemKind, RhsKind
+  int64_t nnz_local;
+  uint64_t fingerprint;     // problem_fingerprint(): the matrix (user CSR: rowptr / cols / vals) and b
 };
 }  // namespace
 
@@ -1410,6 +1416,10 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
   h.k = k_;
   h.n_global = L_.n_global;
   h.seed = spec_.seed;
+  h.kind = (int32_t)spec_.kind;
+  h.rhs = (int32_t)spec_.rhs;
+  h.nnz_local = info_.nnz_local;
+  h.fingerprint = fingerprint_;
   bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
   std::vector<char> host;
   auto dump = [&](const void* dev, size_t bytes) {
@@ -1428,6 +1438,9 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
 
 void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   MCG_CHECK(setup_done_, "solver not set up");
+  // nothing of an earlier solve may still run on either stream (a pending halo writes ghost rows)
+  synchronize();
+  join_halo_();
   const std::string path = prefix + ".rank" + std::to_string(rank_);
   std::FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) fail("checkpoint read failed", path);
@@ -1436,7 +1449,8 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   ok = ok && h.rank == rank_ && h.world == world_ && h.recurrence == opt_.recurrence && h.format == info_.format &&
        h.pass_form == ((ar_ ? 1 : 0) | (p3_ ? 2 : 0)) &&
        h.n_local == L_.n_local() && h.ext_len == L_.ext_len && h.row_begin == L_.row_begin &&
-       h.n_global == L_.n_global && h.seed == spec_.seed;
+       h.n_global == L_.n_global && h.seed == spec_.seed && h.kind == (int32_t)spec_.kind &&
+       h.rhs == (int32_t)spec_.rhs && h.nnz_local == info_.nnz_local && h.fingerprint == fingerprint_;
   if (!ok) {
     std::fclose(f);
     fail("checkpoint does not match this problem/layout", path);

@@ -200,23 +200,48 @@ HostMatrix* read_matrix_market(const std::string& path) {
 std::vector<double> read_vector(const std::string& path) {
   std::ifstream f(path);
   if (!f) fail("vector read failed", path);
+  // Matrix Market: only the dense `array` format (one value per line, column-major) is a vector;
+  // a `coordinate` file's lines are "i j v" and reading their first number would take the row
+  // indices as values, so it is refused.  Without a banner: one value per line.
   std::vector<double> v;
   std::string line;
-  bool header_done = false, mm = false;
+  bool header_done = false, mm = false, first = true;
+  int64_t want = -1;
   while (std::getline(f, line)) {
     if (line.empty()) continue;
-    if (line[0] == '%') {
-      if (lower(line).rfind("%%matrixmarket", 0) == 0) mm = true;
+    if (first && line[0] == '%') {
+      first = false;
+      const std::string l = lower(line);
+      if (l.rfind("%%matrixmarket", 0) == 0) {
+        mm = true;
+        std::istringstream ss(l);
+        std::string banner, object, fmt, field;
+        ss >> banner >> object >> fmt >> field;
+        if (object != "matrix" || fmt != "array")
+          fail("vector read failed", path + ": Matrix Market vector must be 'matrix array' (got '" + object + " " +
+                                         fmt + "')");
+        if (field == "complex") fail("vector read failed", path + ": complex vectors are not supported");
+      }
       continue;
     }
-    if (mm && !header_done) {  // "rows cols" of an array file
+    first = false;
+    if (line[0] == '%') continue;
+    std::istringstream ss(line);
+    if (mm && !header_done) {  // "rows cols" of an array file: a column vector
+      int64_t nr = 0, nc = 0;
+      if (!(ss >> nr >> nc) || nr < 0 || nc != 1)
+        fail("vector read failed", path + ": array size line must be 'rows 1'");
+      want = nr;
       header_done = true;
       continue;
     }
-    std::istringstream ss(line);
     double x;
     if (ss >> x) v.push_back(x);
   }
+  if (mm && !header_done) fail("vector read failed", path + ": missing size line");
+  if (want >= 0 && (int64_t)v.size() != want)
+    fail("vector read failed", path + ": " + std::to_string(v.size()) + " values, size line says " +
+                                   std::to_string(want));
   return v;
 }
 

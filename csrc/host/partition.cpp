@@ -32,8 +32,9 @@ RowPartition partition_randspd(const ProblemSpec& s, int world) {
     const int64_t r0 = g * R, r1 = std::min(n, r0 + R), mid = (r0 + r1) / 2;
     // pairs {i-d, i} use the density of i-d's region; pairs {i, i+d} that of i's (wide offsets:
     // the lower partners are spread over the whole matrix -> the mean density)
-    const double left = s.spread > 0 ? qmean * (double)W : qsum_rows(mid - W, mid);
-    const double right = q[g] * (double)std::min(W, n - 1 - mid);
+    // scrambled: a row is a random base row, every region has the mean length
+    const double left = (s.spread > 0 || s.scramble) ? qmean * (double)W : qsum_rows(mid - W, mid);
+    const double right = (s.scramble ? qmean : q[g]) * (double)std::min(W, n - 1 - mid);
     prefix[g + 1] = prefix[g] + (int64_t)((double)(r1 - r0) * (1.0 + left + right));
   }
   RowPartition pr = partition_by_weight(prefix, world);

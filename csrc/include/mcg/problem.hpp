@@ -22,7 +22,14 @@
 //              stratum of spread/W), so columns reach +-spread rows away — with
 //              spread ~ n the sparsity is unstructured at every scale (the all-gather
 //              ghost path), and each 64-row slice still reads 2W short runs of p.
-//   csr        a user matrix given as host CSR arrays (CsrMatrix view; Matrix
+//              Both are MULTI-DIAGONAL: every row draws from the same 2W offsets.
+//              scramble = 1: the symmetric permutation P^T A P of that matrix, with P a
+//              seeded bijection pi of [0, n) (Feistel network + cycle walking, O(1) per
+//              index both ways): row i is base row pi(i) with every column c mapped to
+//              pi^-1(c).  Still symmetric and strictly diagonally dominant (SPD), but
+//              genuinely irregular: no two rows share an offset set, row lengths vary
+//              with the base row's region, and every nonzero is a random column.
+//   csr       a user matrix given as host CSR arrays (CsrMatrix view; Matrix
 //              Market files, SciPy matrices) — the reference's own input form
 //              (cusparseCreateCsr over rowptr/col/val, CUDACG.cu:93-117,213-216).
 #pragma once
@@ -67,6 +74,7 @@ struct ProblemSpec {
   uint64_t seed = 1234;    // matrix + rhs seed
   RhsKind rhs = RhsKind::Reference;
   int64_t spread = 0;      // randspd: > 0 = wide candidate offsets over [1, spread] (see above)
+  int scramble = 0;        // randspd: 1 = P^T A P with a seeded random permutation P (irregular)
   const CsrMatrix* csr = nullptr;  // kind Csr: the matrix (host)
 };
 
@@ -78,6 +86,50 @@ MCG_HD inline uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 MCG_HD inline double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+
+// ---- seeded bijection pi of [0, n) (scrambled random SPD) ----
+// A 4-round balanced Feistel network on 2h-bit words (2^(2h) >= n, so the domain is < 4n) is a
+// bijection of [0, 2^(2h)); cycle walking (re-apply until the value is < n) restricts it to a
+// bijection of [0, n), and the inverse walks the inverse network the same way.  Both directions
+// cost O(1) hashes per index (expected < 4 walks), on the host and on the device.
+MCG_HD inline int perm_half_bits(int64_t n) {
+  const int bits = n > 1 ? 64 - __builtin_clzll((unsigned long long)(n - 1)) : 1;
+  return bits < 2 ? 1 : (bits + 1) / 2;
+}
+MCG_HD inline uint64_t feistel_key(uint64_t seed, int r) { return mix64(seed * 0xA24BAED4963EE407ull + (uint64_t)r); }
+MCG_HD inline uint64_t feistel(uint64_t x, int h, uint64_t seed, bool inverse) {
+  const uint64_t m = (1ull << h) - 1;
+  uint64_t L = x >> h, R = x & m;
+  if (!inverse) {
+    for (int r = 0; r < 4; ++r) {  // (L, R) -> (R, L ^ f_r(R))
+      const uint64_t t = L ^ (mix64(R ^ feistel_key(seed, r)) & m);
+      L = R;
+      R = t;
+    }
+  } else {
+    for (int r = 3; r >= 0; --r) {  // (L', R') -> (R' ^ f_r(L'), L')
+      const uint64_t t = R ^ (mix64(L ^ feistel_key(seed, r)) & m);
+      R = L;
+      L = t;
+    }
+  }
+  return (L << h) | R;
+}
+// pi(i): the base row behind scrambled row i
+MCG_HD inline int64_t scramble_fwd(const ProblemSpec& s, int64_t i) {
+  const int h = perm_half_bits(s.rows);
+  uint64_t x = (uint64_t)i;
+  do x = feistel(x, h, s.seed ^ 0x5C4A3B1Du, false); while (x >= (uint64_t)s.rows);
+  return (int64_t)x;
+}
+// pi^-1(c): the scrambled index of base row / column c
+MCG_HD inline int64_t scramble_inv(const ProblemSpec& s, int64_t c) {
+  const int h = perm_half_bits(s.rows);
+  uint64_t x = (uint64_t)c;
+  do x = feistel(x, h, s.seed ^ 0x5C4A3B1Du, true); while (x >= (uint64_t)s.rows);
+  return (int64_t)x;
+}
+MCG_HD inline bool scrambled(const ProblemSpec& s) { return s.kind == ProblemKind::RandomSPD && s.scramble != 0; }
 
 MCG_HD inline int64_t global_rows(const ProblemSpec& s) {
   switch (s.kind) {
@@ -97,7 +149,7 @@ MCG_HD inline int64_t bandwidth(const ProblemSpec& s) {
     case ProblemKind::Demo: return 2;
     case ProblemKind::Poisson2D: return s.N;
     case ProblemKind::Poisson3D: return s.N * s.N;
-    case ProblemKind::RandomSPD: return s.spread > 0 ? s.spread : s.band;
+    case ProblemKind::RandomSPD: return s.scramble ? (s.rows > 0 ? s.rows - 1 : 0) : (s.spread > 0 ? s.spread : s.band);
     case ProblemKind::Csr: return s.csr ? s.csr->bw : 0;
   }
   return 0;
@@ -156,7 +208,35 @@ MCG_HD inline int64_t randspd_offset(const ProblemSpec& s, int64_t t) {
   return t * step + 1 + (int64_t)(mix64(s.seed * 0xD1B54A32D192ED03ull + (uint64_t)t) % (uint64_t)step);
 }
 
-// Visit the entries of global row i in ascending column order: f(col, val).
+// randspd base matrix (not scrambled): row length and entries of row i in ascending column order
+MCG_HD inline int64_t randspd_row_length(const ProblemSpec& s, int64_t i) {
+  int64_t len = 1;
+  const int64_t n = s.rows, W = s.band;
+  for (int64_t t = 0; t < W; ++t) {
+    const int64_t d = randspd_offset(s, t);
+    if (i - d >= 0 && randspd_present(s, i - d, i)) ++len;
+    if (i + d < n && randspd_present(s, i, i + d)) ++len;
+  }
+  return len;
+}
+template <class F>
+MCG_HD inline void randspd_row(const ProblemSpec& s, int64_t i, F&& f, int64_t rowlen) {
+  const int64_t n = s.rows, W = s.band;
+  if (rowlen < 0) rowlen = randspd_row_length(s, i);
+  for (int64_t t = W - 1; t >= 0; --t) {
+    const int64_t d = randspd_offset(s, t);
+    if (d <= i && randspd_present(s, i - d, i)) f(i - d, -randspd_weight(s, i - d, i));
+  }
+  f(i, (double)rowlen);
+  for (int64_t t = 0; t < W; ++t) {
+    const int64_t d = randspd_offset(s, t);
+    if (i + d >= n) break;
+    if (randspd_present(s, i, i + d)) f(i + d, -randspd_weight(s, i, i + d));
+  }
+}
+
+// Visit the entries of global row i: f(col, val), in ascending column order except for the
+// scrambled random SPD (base-row order: the mapped columns are unordered).
 // For randspd the diagonal value depends on the row length, which the caller
 // passes in (from the count pass / rowptr); pass -1 to have it counted here.
 template <class F>
@@ -191,25 +271,10 @@ MCG_HD inline void for_each_entry(const ProblemSpec& s, int64_t i, F&& f, int64_
       return;
     }
     case ProblemKind::RandomSPD: {
-      const int64_t n = s.rows, W = s.band;
-      if (rowlen < 0) {
-        rowlen = 1;
-        for (int64_t t = 0; t < W; ++t) {
-          const int64_t d = randspd_offset(s, t);
-          if (i - d >= 0 && randspd_present(s, i - d, i)) ++rowlen;
-          if (i + d < n && randspd_present(s, i, i + d)) ++rowlen;
-        }
-      }
-      for (int64_t t = W - 1; t >= 0; --t) {
-        const int64_t d = randspd_offset(s, t);
-        if (d <= i && randspd_present(s, i - d, i)) f(i - d, -randspd_weight(s, i - d, i));
-      }
-      f(i, (double)rowlen);
-      for (int64_t t = 0; t < W; ++t) {
-        const int64_t d = randspd_offset(s, t);
-        if (i + d >= n) break;
-        if (randspd_present(s, i, i + d)) f(i + d, -randspd_weight(s, i, i + d));
-      }
+      if (s.scramble)  // row pi(i) of the base matrix, its columns through pi^-1
+        randspd_row(s, scramble_fwd(s, i), [&](int64_t c, double v) { f(scramble_inv(s, c), v); }, rowlen);
+      else
+        randspd_row(s, i, f, rowlen);
       return;
     }
     case ProblemKind::Csr: {
@@ -234,16 +299,7 @@ MCG_HD inline int64_t row_length(const ProblemSpec& s, int64_t i) {
       const int64_t ix = i % N, iy = (i / N) % N, iz = i / N2;
       return 1 + (iz > 0) + (iy > 0) + (ix > 0) + (ix < N - 1) + (iy < N - 1) + (iz < N - 1);
     }
-    case ProblemKind::RandomSPD: {
-      int64_t len = 1;
-      const int64_t n = s.rows, W = s.band;
-      for (int64_t t = 0; t < W; ++t) {
-        const int64_t d = randspd_offset(s, t);
-        if (i - d >= 0 && randspd_present(s, i - d, i)) ++len;
-        if (i + d < n && randspd_present(s, i, i + d)) ++len;
-      }
-      return len;
-    }
+    case ProblemKind::RandomSPD: return randspd_row_length(s, s.scramble ? scramble_fwd(s, i) : i);
     case ProblemKind::Csr: {
 #if !defined(__HIP_DEVICE_COMPILE__)
       return s.csr->rowptr[i + 1] - s.csr->rowptr[i];
@@ -283,6 +339,10 @@ inline int64_t closed_form_nnz(const ProblemSpec& s) {
 }
 
 std::string problem_name(const ProblemSpec& s);
+// 64-bit hash of everything that defines A and b: the family's parameters, and for a user matrix
+// (kind csr) its rowptr / cols / vals and b (O(nnz) on the host).  Checkpoints record it so a
+// resume against another matrix or right-hand side of the same size is refused.
+uint64_t problem_fingerprint(const ProblemSpec& s);
 ProblemKind parse_problem_kind(const std::string& name);
 RhsKind parse_rhs_kind(const std::string& name);
 

@@ -223,6 +223,7 @@ class GpuCgSolver {
   hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
   void drop_graphs_();
   double setup_seconds_ = 0.0;
+  uint64_t fingerprint_ = 0;  // problem_fingerprint(spec_), recorded in checkpoints
 };
 
 }  // namespace mcg

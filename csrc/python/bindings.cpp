@@ -27,7 +27,7 @@ using namespace mcg;
 namespace {
 
 ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64_t band, double density,
-                      uint64_t seed, const std::string& rhs, int64_t spread) {
+                      uint64_t seed, const std::string& rhs, int64_t spread, int scramble) {
   ProblemSpec s;
   s.kind = parse_problem_kind(problem);
   s.N = n;
@@ -37,6 +37,8 @@ ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64
   s.seed = seed;
   s.rhs = parse_rhs_kind(rhs);
   s.spread = spread;
+  s.scramble = scramble;
+  MCG_CHECK(scramble == 0 || s.kind == ProblemKind::RandomSPD, "scramble: random-SPD family only");
   if (s.kind == ProblemKind::Demo) s.N = 3;
   return s;
 }
@@ -132,7 +134,7 @@ PYBIND11_MODULE(_C, m) {
   py::class_<ProblemSpec>(m, "ProblemSpec")
       .def(py::init(&make_spec), py::arg("problem") = "demo", py::arg("n") = 3, py::arg("rows") = 0,
            py::arg("band") = 0, py::arg("density") = 0.5, py::arg("seed") = 1234, py::arg("rhs") = "reference",
-           py::arg("spread") = 0)
+           py::arg("spread") = 0, py::arg("scramble") = 0)
       .def_property_readonly("name", [](const ProblemSpec& s) { return problem_name(s); })
       .def_property_readonly("n_rows", [](const ProblemSpec& s) { return global_rows(s); })
       .def_property_readonly("bandwidth", [](const ProblemSpec& s) { return bandwidth(s); })
@@ -143,6 +145,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("density", &ProblemSpec::density)
       .def_readonly("seed", &ProblemSpec::seed)
       .def_readonly("spread", &ProblemSpec::spread)
+      .def_readonly("scramble", &ProblemSpec::scramble)
+      .def("perm", [](const ProblemSpec& s, int64_t i, bool inverse) {
+        MCG_CHECK(scrambled(s) && i >= 0 && i < s.rows, "perm: scrambled random SPD, 0 <= i < rows");
+        return inverse ? scramble_inv(s, i) : scramble_fwd(s, i);
+      }, py::arg("i"), py::arg("inverse") = false, "pi(i) (base row of scrambled row i) or pi^-1(i)")
       .def("row_length", [](const ProblemSpec& s, int64_t i) { return row_length(s, i); })
       .def("rhs_value", [](const ProblemSpec& s, int64_t i) { return rhs_value(s, i); })
       .def("row", [](const ProblemSpec& s, int64_t i) {

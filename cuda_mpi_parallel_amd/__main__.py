@@ -23,7 +23,7 @@ CHOICES = {"--problem": ["demo", "poisson2d", "poisson3d", "randspd", "csr", "ra
            "--rhs": ["reference", "random", "ones"], "--device": ["gpu", "cpu"],
            "--format": ["csr", "sell", "sell16", "sellc8"], "--print-x": ["auto", "yes", "no"],
            "--report": ["text", "json"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
-INTS = {"--n", "--rows", "--band", "--spread", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
+INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
         "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--spmv-param", "--update-unroll",
         "--nt-loads", "--xcd-map", "--sell-slices", "--checkpoint-every", "--inject-nan-at"}
 FLOATS = {"--density", "--nnz-per-row", "--tol", "--rtol", "--watchdog"}
@@ -71,7 +71,7 @@ def _spec(args):
     if problem in ("poisson2d", "poisson3d") and args.n is not None:
         kw["n"] = args.n
     if problem == "randspd":
-        for k in ("rows", "band", "density", "spread"):
+        for k in ("rows", "band", "density", "spread", "scramble"):
             v = getattr(args, k)
             if v is not None:
                 kw[k] = v

@@ -20,7 +20,8 @@ FLAGS = [
     ("--band", "8", "randspd: candidate offsets per side (half bandwidth when --spread 0)"),
     ("--density", "0.3", "randspd: mean candidate-pair density"),
     ("--nnz-per-row", "5", "randspd: mean nonzeros per row (sets --density)"),
-    ("--spread", "0", "randspd: > 0 = candidate offsets drawn over [1, spread] (wide / unstructured)"),
+    ("--spread", "0", "randspd: > 0 = candidate offsets drawn over [1, spread] (wide multi-diagonal)"),
+    ("--scramble", "0", "randspd: 1 = P^T A P with a seeded random permutation (genuinely irregular rows)"),
     ("--matrix", None, "FILE.mtx: a user matrix (problem csr), Matrix Market coordinate"),
     ("--rhs-file", None, "FILE: right-hand side of --matrix (Matrix Market array or one value per line)"),
     ("--rhs", "reference", "reference | random | ones"),

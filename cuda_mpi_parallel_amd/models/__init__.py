@@ -11,7 +11,8 @@ name           matrix                                       reference / config
 ``demo``       the reference's 3x3 indefinite system        CUDACG.cu:74-117,136-141
 ``poisson2d``  5-pt Dirichlet Laplacian, n = N^2            BASELINE.json configs 1-3
 ``poisson3d``  7-pt Dirichlet Laplacian, n = N^3            BASELINE.json config 4
-``randspd``    banded / wide (spread), irregular, strictly  BASELINE.json config 5
+``randspd``    banded / wide (spread) multi-diagonal, or    BASELINE.json config 5
+               scrambled (P^T A P, irregular); strictly
                diagonally dominant
 ``csr``        a user matrix: SciPy / NumPy CSR arrays or a  CUDACG.cu:93-117,213-216
                Matrix Market file (:func:`csr_problem`)       (the reference's input)
@@ -41,10 +42,11 @@ class ProblemSpec:
     seed: int = 1234
     rhs: str = "reference"  # reference | random | ones
     spread: int = 0       # randspd: > 0 = the band candidate offsets drawn over [1, spread] ("wide")
+    scramble: int = 0     # randspd: 1 = P^T A P with a seeded random permutation P (genuinely irregular)
 
     def native(self):
         return native().ProblemSpec(self.problem, self.n, self.rows, self.band, self.density, self.seed, self.rhs,
-                                    self.spread)
+                                    self.spread, self.scramble)
 
     @property
     def n_rows(self) -> int:

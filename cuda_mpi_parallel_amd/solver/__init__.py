@@ -105,8 +105,8 @@ class CGSolver:
 def solve(problem: str = "demo", device: str = "gpu", sim_ranks: int = 1, maxit: int = 2000, tol: float = 1e-7,
           **kw) -> Dict:
     """One-call solve.  ``solve()`` with no arguments is the reference's demo."""
-    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs", "spread", "nnz_per_row",
-                                      "matrix", "b", "reorder") if k in kw}
+    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs", "spread", "scramble",
+                                      "nnz_per_row", "matrix", "b", "reorder") if k in kw}
     if "matrix" in spec_kw:  # solve(matrix=A_or_path, b=...): a user matrix (kind csr)
         problem = "csr"
     spec = make_problem(problem, **spec_kw)

@@ -64,6 +64,29 @@ def test_checkpoint_rejects_other_problem(mcg, tmp_path):
         t.load_checkpoint(prefix)
 
 
+def test_checkpoint_rejects_perturbed_user_matrix_or_rhs(mcg, tmp_path):
+    """Checkpoint v3 records a fingerprint of the user matrix (rowptr / cols / vals) and of b: a
+    resume against a matrix of the same size and pattern with one value changed, or against the
+    same matrix with another right-hand side, is refused; the unchanged problem resumes."""
+    import scipy.sparse as sp
+
+    n = 400
+    T = sp.diags([-1.0, 2.5, -1.0], [-1, 0, 1], shape=(n, n)).tocsr()
+    b = np.linspace(0.0, 1.0, n)
+    prefix = str(tmp_path / "u")
+    kw = dict(format="sell16", recurrence=1, check_every=4)
+    a = mcg.CGSolver(mcg.csr_problem(T, b=b), maxit=8, **kw)
+    a.solve()
+    a.save_checkpoint(prefix)
+    mcg.CGSolver(mcg.csr_problem(T, b=b), **kw).load_checkpoint(prefix)  # same problem: accepted
+    T2 = T.copy()
+    T2.data[7] += 1e-3
+    with pytest.raises(Exception, match="does not match"):
+        mcg.CGSolver(mcg.csr_problem(T2, b=b), **kw).load_checkpoint(prefix)
+    with pytest.raises(Exception, match="does not match"):
+        mcg.CGSolver(mcg.csr_problem(T, b=b + 1.0), **kw).load_checkpoint(prefix)
+
+
 @pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "csr"), (1, "sell16")])
 def test_fault_injection_latches_breakdown(mcg, recurrence, fmt):
     spec = mcg.make_problem("poisson2d", n=64)

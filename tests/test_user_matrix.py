@@ -195,3 +195,22 @@ def test_stencil_detection_and_line_partition(mcg, C, dim):
     # a matrix with the offsets but rows that are not whole lines: no stencil
     B = sp.diags([-1.0, -1.0, 4.0, -1.0, -1.0], [-n, -1, 0, 1, n], shape=(n * n - 3, n * n - 3)).tocsr()
     assert mcg.csr_problem(B).matrix.stencil_line == 0
+
+
+def test_read_vector_formats(C, tmp_path):
+    """--rhs-file: a Matrix Market `array` vector (size line checked), plain one-value-per-line text,
+    and a clear refusal of a `coordinate` file (whose "i j v" lines would otherwise be read as b)."""
+    a = tmp_path / "a.mtx"
+    a.write_text("%%MatrixMarket matrix array real general\n% comment\n3 1\n3.5\n1.5\n2.0\n")
+    assert list(C.read_vector(str(a))) == [3.5, 1.5, 2.0]
+    t = tmp_path / "b.txt"
+    t.write_text("1\n2\n")
+    assert list(C.read_vector(str(t))) == [1.0, 2.0]
+    c = tmp_path / "c.mtx"
+    c.write_text("%%MatrixMarket matrix coordinate real general\n3 1 2\n1 1 3.5\n3 1 2.0\n")
+    with pytest.raises(Exception, match="array"):
+        C.read_vector(str(c))
+    s = tmp_path / "s.mtx"
+    s.write_text("%%MatrixMarket matrix array real general\n4 1\n1\n2\n3\n")
+    with pytest.raises(Exception, match="size line"):
+        C.read_vector(str(s))
