@@ -20,6 +20,15 @@ COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-function
 HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 CXXFLAGS  := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -pthread
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -pthread -ldl
+# One RCCL (and HIP runtime) for every entry point: the Python extension binds to the copies torch
+# ships (torch is imported first, the SONAMEs match), so the CLI is pointed at the same files
+# through in-tree links under build/rt searched before /opt/rocm/lib (DT_RPATH, transitive).
+TORCH_LIB := $(shell $(PYTHON) -c "import os, torch; print(os.path.dirname(torch.__file__) + '/lib')" 2>/dev/null)
+RT        := $(BUILD)/rt
+RT_LIBS   := librccl.so.1:librccl.so libamdhip64.so.7:libamdhip64.so libhsa-runtime64.so.1:libhsa-runtime64.so \
+             libroctx64.so.4:libroctx64.so librccl.so:librccl.so libamdhip64.so:libamdhip64.so \
+             libhsa-runtime64.so:libhsa-runtime64.so libroctx64.so:libroctx64.so
+CLI_LDLIBS:= -Wl,--disable-new-dtags -Wl,-rpath,'$$ORIGIN/../$(RT)' $(LDLIBS)
 
 HIP_SRC   := $(wildcard csrc/gpu/*.hip)
 HOST_SRC  := $(wildcard csrc/host/*.cpp)
@@ -47,9 +56,15 @@ $(BUILD)/python/bindings.o: csrc/python/bindings.cpp $(HEADERS)
 $(PYMOD): $(CORE_OBJ) $(BUILD)/python/bindings.o
 	$(CXX) -shared -o $@ $^ $(LDLIBS)
 
-$(CLI): $(CORE_OBJ) $(BUILD)/cli/main.o
+$(RT)/.stamp:
+	@mkdir -p $(RT)
+	@if [ -n "$(TORCH_LIB)" ]; then for m in $(RT_LIBS); do \
+	  so=$${m%%:*}; f=$${m##*:}; [ -e "$(TORCH_LIB)/$$f" ] && ln -sfn "$(TORCH_LIB)/$$f" "$(RT)/$$so"; done; true; fi
+	@touch $@
+
+$(CLI): $(CORE_OBJ) $(BUILD)/cli/main.o | $(RT)/.stamp
 	@mkdir -p bin
-	$(CXX) -o $@ $^ $(LDLIBS)
+	$(CXX) -o $@ $^ $(CLI_LDLIBS)
 
 $(TESTBIN): $(HOST_OBJ:$(BUILD)/gpu/%=) $(BUILD)/tests/test_host.o
 	$(CXX) -o $@ $(filter-out $(BUILD)/gpu/%,$(HOST_OBJ)) $(BUILD)/tests/test_host.o -pthread -ldl

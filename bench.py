@@ -85,6 +85,9 @@ def parse_args(argv=None):
     ap.add_argument("--phases", type=int, default=10,
                     help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
+    ap.add_argument("--comm", default="dual", choices=["dual", "single"],
+                    help="dual: reduce + halo RCCL communicators (halo on the side stream); single: one communicator, "
+                         "every collective in one stream order on the compute stream")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
     ap.add_argument("--sim-world", type=int, default=0,
@@ -94,6 +97,10 @@ def parse_args(argv=None):
     ap.add_argument("--watchdog", type=float, default=600.0,
                     help="seconds a host wait may go without progress before the run fails and RCCL is aborted "
                          "(a hung collective ends the job with a message instead of hanging; 0 = unbounded)")
+    ap.add_argument("--rehearse-ranks", action="store_true",
+                    help="multi-process rehearsal on ONE GPU: --gpus P ranks (spawned, or under torchrun) all on "
+                         "device 0 with collectives that move nothing (NullComm), but the real gloo rendezvous, "
+                         "barriers and all_gather_object aggregation of the P-rank bench")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank(s) as child processes even for --gpus 1 (the --gpus N > 1 launch route)")
     return ap.parse_args(argv)
@@ -107,7 +114,7 @@ def main(argv=None) -> int:
     # (a) --gpus N without torchrun: start the ranks and exit with their status.  Only the
     # parent decides; a child (WORLD_SIZE set) always runs as a rank.
     rc = launch.launch_or_none(args.gpus, [a for a in argv if a != "--spawn"], force_spawn=args.spawn,
-                               script=os.path.abspath(__file__))
+                               script=os.path.abspath(__file__), share_device=args.rehearse_ranks)
     if rc is not None:
         return rc
     return run_rank(args)
@@ -140,10 +147,14 @@ def _run_rank(args, out_fd) -> int:
     # no user-buffer registration while capturing RCCL calls into graphs (buffers are few and
     # small; registration would add an IPC-handle path the solver does not need)
     os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
-    pdist.set_device(env)
+    rehearse = args.rehearse_ranks and env.world > 1
+    if rehearse:  # every rank on device 0 (RCCL refuses two ranks on one GPU: collectives move nothing)
+        torch.cuda.set_device(0)
+    else:
+        pdist.set_device(env)
     if env.world > 1:
         pdist.init_process_group(env, backend="gloo")
-    comm = pdist.bootstrap_comm(env, force=args.force_comm)
+    comm = mcg.native().NullComm(env.rank, env.world) if rehearse else pdist.bootstrap_comm(env, force=args.force_comm, mode=args.comm)
     sim = args.sim_world > 1 and env.world == 1
     if sim:  # per-rank timing rehearsal (not a P-rank solve: see --sim-world)
         comm = mcg.native().NullComm(args.sim_rank, args.sim_world)
@@ -210,13 +221,13 @@ def _run_rank(args, out_fd) -> int:
         tr = solver.true_residual_norm()
         rr0 = torch.tensor([float(res.get("rr0_local", 0.0))], dtype=torch.float64)
         if env.world > 1 and not sim:
-            dist.all_reduce(rr0)
+            dist.all_reduce(rr0)  # gloo (host): every rank's b.b
         bnorm = math.sqrt(max(float(rr0.item()), 0.0))
         extra["true_rnorm"] = tr
         extra["true_gap_rel"] = abs(tr - res["rnorm"]) / max(tr, 1e-300)
         extra["true_rel_to_b"] = tr / max(bnorm, 1e-300)
         tracks = abs(tr - res["rnorm"]) <= 1e-8 * max(tr, 1e-300) + 1e-12
-        ok = ok and (sim or tracks or tr <= 1e-9 * bnorm)
+        ok = ok and (sim or rehearse or tracks or tr <= 1e-9 * bnorm)
     info = solver.info
     # whole-job result: the slowest rank's clock, every rank ok and latched at the same count
     mine = {"dt": dt, "ok": bool(ok), "iterations": int(res["iterations"])}
@@ -231,7 +242,7 @@ def _run_rank(args, out_fd) -> int:
         if env.world > 1:
             dist.all_reduce(t)
         nnz = int(t.item())
-    headline = args.problem == "poisson2d" and args.grid == 16384 and not sim
+    headline = args.problem == "poisson2d" and args.grid == 16384 and not sim and not rehearse
     if phases is not None:
         extra["phase_us"] = phases
         if env.world > 1:  # slowest rank per phase
@@ -245,7 +256,9 @@ def _run_rank(args, out_fd) -> int:
         line = json.dumps({
             "metric": METRIC if headline else (
                 "per-rank iterations/sec, timing rehearsal of rank %d of %d (collectives move nothing), %s"
-                % (args.sim_rank, args.sim_world, model) if sim else "CG iterations/sec (whole node), %s" % model),
+                % (args.sim_rank, args.sim_world, model) if sim else
+                "rehearsal: %d ranks on ONE GPU (collectives move nothing; rendezvous / barriers / aggregation real), %s"
+                % (env.world, model) if rehearse else "CG iterations/sec (whole node), %s" % model),
             "value": round(value, 4),
             "unit": "iterations/s",
             "n_gpus": n_gpus,
@@ -268,7 +281,8 @@ def _run_rank(args, out_fd) -> int:
                 "nnz": nnz,
                 "global_batch": 1,
                 "seq_len": spec.n_rows,
-                "parallelism": f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else f"rowpart{n_gpus}",
+                "parallelism": (f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else
+                                f"rehearse-rowpart{n_gpus}-one-gpu" if rehearse else f"rowpart{n_gpus}"),
                 # storage the timed pass streams: the 2-D line-carry pass reads 4-bit codes (c4)
                 "format": ("sell64-dia4" if info.get("dia4") else "sell64-c4" if info.get("codes4")
                            else info["format"]),
@@ -279,11 +293,13 @@ def _run_rank(args, out_fd) -> int:
                                                    else "window")} if (n_gpus > 1 or sim) else {}),
                 "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
-                "halo_overlap": (not args.no_overlap) and n_gpus > 1,
+                "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
+                "comm": args.comm,
                 "launch": route,
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
-                      "comm_world": comm.count if (comm is not None and not sim) else 1,
+                      "comm_world": comm.count if (comm is not None and not sim and not rehearse) else 1,
+                      "rccl": mcg.native().rccl_info(),
                       "graph_fallbacks": info.get("graph_fallbacks", 0),
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),

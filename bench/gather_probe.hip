@@ -72,6 +72,87 @@ __global__ __launch_bounds__(256) void k_seg(const double* __restrict__ p, uint3
   if (acc == 12345.678) *out = acc;
 }
 
+// bisection between k_seg (L2 hits) and k_tile (misses): F bit 0 = tile bounds from memory (tptr),
+// bit 1 = LDS accumulators (ds_add_f64), bit 2 = the tile is `per64 + 1` entries (a remainder pass),
+// bit 3 = pacing barrier per segment (the workgroups of group blockIdx % 8; counters 256 B apart,
+// gentle polling), bit 4 = packed (row, column) and value streamed from memory (NT loads) instead
+// of hashed in registers
+template <int F, int U = 4>
+__global__ __launch_bounds__(256) void k_tt(const double* __restrict__ p, const int64_t* __restrict__ tptr,
+                                            const uint32_t* __restrict__ idx, const double* __restrict__ vals,
+                                            uint32_t S, int G, int per64, double* __restrict__ y,
+                                            unsigned* __restrict__ arr, int D = 0) {
+  __shared__ double acc[4][1024];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  double* a = acc[wv];
+  double racc = 0.0;
+  if (F & 2)
+    for (int r = lane; r < 1024; r += 64) a[r] = 0.0;
+  const int64_t len = (int64_t)per64 + ((F & 4) ? 1 : 0);
+  for (int g = 0; g < G; ++g) {
+    int64_t lo, hi;
+    if (F & 1) {
+      lo = tptr[wave * G + g];
+      hi = tptr[wave * G + g + 1];
+    } else {
+      lo = (wave * G + g) * len;
+      hi = lo + len;
+    }
+    const double* pg = p + (size_t)g * S;
+    int64_t k = lo + lane;
+    for (; k + (U - 1) * 64 < hi; k += U * 64) {
+      double x[U], v[U];
+      uint32_t h[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (F & 16) {
+          h[u] = __builtin_nontemporal_load(&idx[k + u * 64]);
+          v[u] = __builtin_nontemporal_load(&vals[k + u * 64]);
+        } else {
+          h[u] = hash32((uint32_t)(k + u * 64) * 0x9E3779B9U);
+          v[u] = 0.5;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[u] = pg[(F & 16) ? (h[u] & 0x3FFFFFu) : (uint32_t)(((uint64_t)h[u] * S) >> 32)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (F & 2) atomicAdd(&a[(F & 16) ? (h[u] >> 22) : (h[u] & 1023)], v[u] * x[u]);
+        else racc = fma(v[u], x[u], racc);
+      }
+    }
+    for (; k < hi; k += 64) {
+      const uint32_t h = (F & 16) ? idx[k] : hash32((uint32_t)k * 0x9E3779B9U);
+      const double v = (F & 16) ? vals[k] : 0.5;
+      const double x = pg[(F & 16) ? (h & 0x3FFFFFu) : (uint32_t)(((uint64_t)h * S) >> 32)];
+      if (F & 2) atomicAdd(&a[(F & 16) ? (h >> 22) : (h & 1023)], v * x);
+      else racc = fma(v, x, racc);
+    }
+    if (F & 8) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const int grp = blockIdx.x & 7;
+        const unsigned nwg = (gridDim.x - grp + 7) / 8;
+        unsigned* c = arr + grp * 64;  // one 256-B block per group
+        __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = g + 1 > D ? (unsigned)(g + 1 - D) * nwg : 0u;
+        int spin = 0;
+        for (; spin < 20000; ++spin) {
+          if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+          __builtin_amdgcn_s_sleep(8);
+        }
+        if (spin == 20000) __hip_atomic_fetch_add(arr + 8 * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    }
+  }
+  if (F & 2)
+    for (int r = lane; r < 1024; r += 64) racc += a[r];
+  y[wave * 64 + lane] = racc;
+}
+
 // slices of 64 rows x w slots, column-major; grid-stride over slices
 template <int UNR>
 __global__ __launch_bounds__(256) void k_sell(const int32_t* __restrict__ cols, const double* __restrict__ vals,
@@ -105,7 +186,8 @@ __global__ __launch_bounds__(256) void k_sell(const int32_t* __restrict__ cols, 
 // S-double segment of p at about the same time (L2-resident); tile (block, g) is a flat list of
 // packed (row in block << 22 | column in segment) + value, spread over the 64 lanes.
 // V: 0 = as described; 1 = register accumulation instead of the LDS atomics (wrong sums: a cost
-// probe); 2 = packed indices from a hash instead of the stream; 3 = no gather (p[...] -> 1.0)
+// probe); 2 = packed indices from a hash instead of the stream; 3 = no gather (p[...] -> 1.0);
+// 4 = 2 and 1 (hash indices, register accumulation)
 // pacing: ngrp > 0 = after every segment the workgroup adds to its group's arrival counter (group =
 // blockIdx % ngrp, i.e. the XCD under round-robin dispatch) and waits (bounded spin, pacing only)
 // until every workgroup of the group has finished that segment
@@ -131,7 +213,7 @@ __global__ __launch_bounds__(256) void k_tile(const uint32_t* __restrict__ idx, 
         double v[UNR], x[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-          if constexpr (V == 2) {
+          if constexpr (V == 2 || V == 4) {
             const uint32_t h = hash32((uint32_t)(k + u * 64) * 0x9E3779B9U);
             q[u] = ((h & (B - 1)) << 22) | ((h >> 10) & (uint32_t)(S - 1));
             v[u] = 0.5;
@@ -144,7 +226,7 @@ __global__ __launch_bounds__(256) void k_tile(const uint32_t* __restrict__ idx, 
         for (int u = 0; u < UNR; ++u) x[u] = V == 3 ? 1.0 : pg[q[u] & 0x3FFFFFu];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-          if constexpr (V == 1) racc = fma(v[u], x[u], racc);
+          if constexpr (V == 1 || V == 4) racc = fma(v[u], x[u], racc);
           else atomicAdd(&a[q[u] >> 22], v[u] * x[u]);
         }
       }
@@ -196,7 +278,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int64_t sizes_all[] = {4, 16, 32, 64, 128, 192, 256, 384, 512, 800, 1600};
-  const bool skip_rand = only_tile || (argc >= 2 && std::string(argv[1]) == "tiles");
+  const bool skip_rand = only_tile || (argc >= 2 && std::string(argv[1]) != "all");
   std::vector<int64_t> sizes_mb(sizes_all, sizes_all + (skip_rand ? 0 : 11));
   // --- hash kernel: gathers only ---
   const int iters = 512;
@@ -244,13 +326,16 @@ int main(int argc, char** argv) {
     }
   }
   // --- segment sweep (gathers only) ---
-  if (argc >= 2 && std::string(argv[1]) == "seg") {
+  if (argc >= 2 && (std::string(argv[1]) == "seg" || std::string(argv[1]) == "seg1")) {
+    const bool one = std::string(argv[1]) == "seg1";
     printf("# kernel=seg: every thread sweeps segments of S doubles, `per` random gathers each\n");
     printf("S  G  per  UNR  wg_per_cu  ms  Ggathers_per_s\n");
     for (int S : {32768, 262144, 524288}) {
+      if (one && S != 262144) continue;
       const int G = (int)(100000000ll / S);
       for (int bpc : {4, 8}) {
         for (int unr : {4, 8}) {
+          if (one && (bpc != 4 || unr != 4)) continue;
           const int gr = ncu * bpc;
           const int per = (int)(2800000000ll / ((int64_t)gr * 256 * G)) / 8 * 8;
           auto launch = [&]() {
@@ -268,6 +353,62 @@ int main(int argc, char** argv) {
                  (double)gr * 256 * G * per / (ms * 1e-3) / 1e9);
         }
       }
+    }
+    return 0;
+  }
+  if (argc >= 2 && std::string(argv[1]) == "tt") {
+    printf("# kernel=tt: 4096 waves, segments of S doubles over 1e8 columns, ~1792 * S / 262144 entries per wave and segment\n");
+    printf("F  S  D  ms  Ggathers_per_s  arrivals  timeouts\n");
+    const int gr = ncu * 4;
+    const int64_t nw = (int64_t)gr * 4;
+    int64_t* tp = nullptr;
+    double* yy = nullptr;
+    CK(hipMalloc(&yy, nw * 64 * 8));
+    unsigned* arr = nullptr;
+    CK(hipMalloc(&arr, 16 * 64 * sizeof(unsigned)));
+    uint32_t* sidx = nullptr;
+    double* svals = nullptr;
+    const int64_t m_all = nw * 381 * (int64_t)(1792 + 1) + (1 << 20);
+    CK(hipMalloc(&sidx, m_all * 4));
+    CK(hipMalloc(&svals, m_all * 8));
+    hipLaunchKernelGGL(k_fill_d, dim3(4096), dim3(256), 0, 0, svals, m_all, 0.25);
+    struct Cfg { int F; uint32_t S; int D; };
+    std::vector<Cfg> cfgs = {{0, 262144, 0}, {26, 262144, 0}, {26, 262144, 1}, {26, 262144, 2}, {26, 131072, 0},
+                             {26, 131072, 1}, {26, 131072, 2}, {26, 131072, 3}, {26, 65536, 2}, {26, 65536, 4},
+                             {30, 131072, 2}, {18, 131072, 0}};
+    uint32_t filled_S = 0;
+    for (const Cfg& c : cfgs) {
+      const int F = c.F, D = c.D;
+      const uint32_t S = c.S;
+      const int G = (int)(100000000ll / S);
+      const int per64 = (int)(1792ll * S / 262144);
+      if (filled_S != S) {
+        hipLaunchKernelGGL(k_fill_tiles, dim3(4096), dim3(256), 0, 0, sidx, m_all, 1024, (int)S, 4242u);
+        filled_S = S;
+      }
+      const int64_t len = per64 + ((F & 4) ? 1 : 0);
+      std::vector<int64_t> h(nw * G + 1);
+      for (int64_t t = 0; t <= nw * G; ++t) h[t] = t * len;
+      CK(hipMalloc(&tp, h.size() * 8));
+      CK(hipMemcpy(tp, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+      auto launch = [&]() {
+        (void)hipMemsetAsync(arr, 0, 16 * 64 * sizeof(unsigned), 0);
+#define TT(f) case f: hipLaunchKernelGGL((k_tt<f, 4>), dim3(gr), dim3(256), 0, 0, p, tp, sidx, svals, S, G, per64, yy, arr, D); break
+        switch (F) { TT(0); TT(18); TT(26); TT(30); }
+#undef TT
+      };
+      launch();
+      CK(hipEventRecord(e0));
+      launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      unsigned hc[16 * 64];
+      CK(hipMemcpy(hc, arr, sizeof(hc), hipMemcpyDeviceToHost));
+      printf("F%d  %u  %d  %8.3f  %8.2f  %u  %u\n", F, S, D, ms, (double)nw * G * len / (ms * 1e-3) / 1e9, hc[0],
+             hc[8 * 64]);
+      CK(hipFree(tp));
     }
     return 0;
   }
@@ -313,6 +454,7 @@ int main(int argc, char** argv) {
           if (V == 1) hipLaunchKernelGGL((k_tile<1024, 4, 1>), dim3(ncu * 4), dim3(256), 0, 0, idx, vals, dtp, p, nb, G, S, y, arr, ngrp);
           if (V == 2) hipLaunchKernelGGL((k_tile<1024, 4, 2>), dim3(ncu * 4), dim3(256), 0, 0, idx, vals, dtp, p, nb, G, S, y, arr, ngrp);
           if (V == 3) hipLaunchKernelGGL((k_tile<1024, 4, 3>), dim3(ncu * 4), dim3(256), 0, 0, idx, vals, dtp, p, nb, G, S, y, arr, ngrp);
+          if (V == 4) hipLaunchKernelGGL((k_tile<1024, 4, 4>), dim3(ncu * 4), dim3(256), 0, 0, idx, vals, dtp, p, nb, G, S, y, arr, ngrp);
         };
         launch();
         CK(hipEventRecord(e0));

@@ -14,6 +14,7 @@
 //   --maxit M  --tol T  --rtol R (||r|| < R ||b||)  --check-every K  --fixed-iters K  --warmup W
 //   --nnz-per-row m (random-spd: density = (m - 1) / (2 band))
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
+//   --comm dual|single (two RCCL communicators, halo on a side stream | one, one stream order)
 //   --spmv-variant 0|1|2|3|4  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
 //   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off  --window auto|on|off
 //   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
@@ -63,6 +64,7 @@ struct Args {
   bool rhs_set = false;
   bool format_set = false, recurrence_set = false;
   std::string resume;  // checkpoint prefix to resume from
+  bool comm_single = false;  // --comm single: one RCCL communicator, collectives in one stream order
   std::string matrix, rhs_file;  // user matrix (Matrix Market) and its right-hand side
   std::shared_ptr<HostMatrix> mat;
 };
@@ -127,6 +129,11 @@ Args parse(int argc, char** argv) {
     else if (f == "--no-overlap") a.opt.overlap = false;
     else if (f == "--no-graph") a.opt.use_graph = false;
     else if (f == "--force-comm") a.opt.force_comm = true;
+    else if (f == "--comm") {
+      const std::string v = need(i);
+      if (v != "single" && v != "dual") usage_error("--comm " + v);
+      a.comm_single = v == "single";
+    }
     else if (f == "--blocks-per-cu") a.opt.blocks_per_cu = std::stoi(need(i));
     else if (f == "--spmv-variant") a.opt.spmv_variant = std::stoi(need(i));
     else if (f == "--spmv-param") a.opt.spmv_param = std::stoi(need(i));
@@ -245,7 +252,8 @@ void run_rank(const Args& a, int rank, int world, const std::string& id_red, con
     if (hipSetDevice(rank) != hipSuccess) fail("Device Set failed");  // CUDACG.cu:87-91
     std::unique_ptr<Comm> comm;
     if (world > 1 || a.opt.force_comm)
-      comm.reset(new Comm(rank, world, unique_id_from_bytes(id_red), unique_id_from_bytes(id_halo)));
+      comm.reset(a.comm_single ? new Comm(rank, world, unique_id_from_bytes(id_red))
+                               : new Comm(rank, world, unique_id_from_bytes(id_red), unique_id_from_bytes(id_halo)));
     if (comm) g_comms.add(comm.get());
     struct Unreg {
       Comm* c;
@@ -371,15 +379,17 @@ int main(int argc, char** argv) {
     std::printf("{\"problem\": \"%s\", \"n\": %lld, \"nnz_rank0\": %lld, \"ranks\": %d, \"device\": \"%s\", "
                 "\"format\": \"%s\", \"iterations\": %d, \"converged\": %s, \"breakdown\": %s, \"rnorm\": %.6e, "
                 "\"true_rnorm\": %.6e, \"setup_s\": %.6f, \"solve_s\": %.6f, \"it_per_s\": %.3f, "
-                "\"device_bytes_rank0\": %zu, \"device_bytes_per_rank\": %s}\n",
+                "\"device_bytes_rank0\": %zu, \"device_bytes_per_rank\": %s, \"rccl_version\": %d, "
+                "\"rccl_library\": \"%s\"}\n",
                 problem_name(a.spec).c_str(), (long long)n, (long long)info.nnz_local, world,
                 a.cpu ? "cpu" : "gpu",
                 a.cpu ? "csr"
-                      : info.format == 4 ? "sell64-aligned" : (info.format == 3 ? "sell64-c8"
+                      : info.format == 5 ? "tiles" : info.format == 4 ? "sell64-aligned" : (info.format == 3 ? "sell64-c8"
                                           : (info.format == 2 ? "sell64-d16" : (info.format == 1 ? "sell64" : "csr"))),
                 res.iterations,
                 res.converged ? "true" : "false", res.breakdown ? "true" : "false", res.rnorm, true_rnorm,
-                res.setup_seconds, res.solve_seconds, itps, info.device_bytes, per_rank.c_str());
+                res.setup_seconds, res.solve_seconds, itps, info.device_bytes, per_rank.c_str(), rccl_version(),
+                rccl_library().c_str());
   } else if (!want_x || n > 3) {
     std::fprintf(stderr,
                  "[mcg] problem=%s n=%lld ranks=%d iterations=%d converged=%d rnorm=%.3e solve=%.4fs "

@@ -1,0 +1,276 @@
+// L2-segment COO tiles: the SpMV of genuinely irregular matrices (BASELINE.json config 5 with the
+// scrambled random-SPD family, or a user CSR whose columns are scattered).
+//
+// Why: a gather of p[col] for a random column misses the XCD's 4 MiB L2, and those misses are
+// served at ~55 G requests/s whether p sits in the 256 MiB Infinity Cache or in HBM (the
+// reference's cuSPARSE CSR SpMV, CUDACG.cu:288, has the same access pattern).  Gathers that hit
+// the L2 run 4-5x faster (bench/gather_probe.hip, profiles/r3_gather_probe.md).  So the columns
+// are cut into segments of S = 2^seg_shift doubles (2 MiB), every wave owns kTileB = 1024 rows
+// (their running sums live in LDS), and ALL waves sweep the segments in the same order: while the
+// chip works on segment g, the XCDs' L2s hold p[g S, (g + 1) S) and the gathers hit.
+//
+// Storage (12 B per nonzero, like CSR): tile (b, g) = the nonzeros of row block b whose column is
+// in segment g, a flat list of (row in block << 22 | column in segment) and the value;
+// tptr[b * G + g] .. tptr[b * G + g + 1].  A wave spreads its tile over its 64 lanes and adds every
+// product into the row's LDS slot (ds_add_f64); the wave owns those slots, so the additions happen
+// in program order (deterministic).
+//
+// Pacing: waves left alone drift apart by a few segments within a sweep (a dependent load or a
+// ragged tile end is enough), the L2 then holds none of the segments in flight and the hit rate
+// falls from ~96 % to ~20 % (TCC counters, profiles/r3_gather_probe.md).  After each segment a
+// workgroup therefore adds to its group's arrival counter (group = blockIdx % 8, i.e. the XCD
+// under round-robin dispatch) and waits until the whole group has finished that segment.  The
+// wait is bounded (kPaceSpins polls): it paces, it never decides correctness, so a workgroup that
+// is not co-resident only costs time.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "mcg/check.hpp"
+#include "mcg/kernels.hpp"
+#include "spmv_engines.hpp"
+
+namespace mcg {
+namespace kern {
+namespace {
+
+#include "f1_common.hpp"
+
+constexpr int kTU = 8;                // entries per lane in flight (software-pipelined: the next batch's
+                                      // indices / values load while this batch gathers)
+constexpr int kPaceSpins = 4000;      // ~1 ms of polling at most per segment step
+constexpr uint32_t kColMask = (1u << 22) - 1;
+
+// `live` (LDS, per workgroup): cleared after the first wait that times out -- the group is not
+// co-resident (another kernel holds CUs, or several ranks share the GPU), so this workgroup stops
+// waiting for the rest of the launch instead of paying the cap at every segment
+__device__ __forceinline__ void pace_step(unsigned* pace, int step, int* live) {
+  __syncthreads();
+  if (threadIdx.x == 0 && pace != nullptr && *live) {
+    const int grp = blockIdx.x & 7;
+    const unsigned nwg = (gridDim.x - grp + 7) >> 3;
+    unsigned* c = pace + grp * 64;  // one 256-B block per group
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (unsigned)(step + 1) * nwg;
+    int spin = 0;
+    for (; spin < kPaceSpins; ++spin) {
+      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+    if (spin == kPaceSpins) *live = 0;
+  }
+  __syncthreads();
+}
+
+// MODE 0: the split pass's SpMV (Ap_k = A p_k + the 4 partials + in-kernel reduction, as
+// k_split_spmv); MODE 1: plain y = A x (true residual, ops)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
+                                               double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
+                                               int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
+  __shared__ double acc[4][kTileB];
+  __shared__ int live;
+  if constexpr (MODE == 0) {
+    const F1Scalars sc = f1_scalars(st, tol, first, check);
+    if (st->done || sc.conv) {  // uniform over the grid: every workgroup leaves, no pacing
+      f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+      return;
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t rounds = (T.nblocks + nwaves - 1) / nwaves;
+  const int G = T.G;
+  double* a = acc[wv];
+  double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
+  int step = 0;
+  if (threadIdx.x == 0) live = 1;
+  for (int64_t rd = 0; rd < rounds; ++rd) {
+    const int64_t b = wave + rd * nwaves;
+    const bool active = b < T.nblocks;
+    for (int rr = lane; rr < kTileB; rr += 64) a[rr] = 0.0;
+    for (int g = 0; g < G; ++g, ++step) {
+      if (active) {
+        const int64_t lo = T.tptr[b * G + g], hi = T.tptr[b * G + g + 1];
+        const double* __restrict__ pg = p + ((int64_t)g << T.seg_shift);
+        uint32_t q[kTU];
+        double v[kTU];
+        int64_t k = lo + lane;
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+          const int64_t e = k + u * 64;
+          q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
+          v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
+        }
+        for (; k < hi; k += kTU * 64) {
+          uint32_t qn[kTU];
+          double vn[kTU], x[kTU];
+#pragma unroll
+          for (int u = 0; u < kTU; ++u) {  // next batch in flight during this one's gathers
+            const int64_t e = k + (kTU + u) * 64;
+            qn[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
+            vn[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < kTU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
+#pragma unroll
+          for (int u = 0; u < kTU; ++u)
+            if (k + u * 64 < hi) atomicAdd(&a[q[u] >> 22], v[u] * x[u]);
+#pragma unroll
+          for (int u = 0; u < kTU; ++u) {
+            q[u] = qn[u];
+            v[u] = vn[u];
+          }
+        }
+      }
+      pace_step(T.pace, step, &live);
+    }
+    if (active) {
+      const int64_t r0 = b * kTileB;
+      for (int rr = lane; rr < kTileB; rr += 64) {
+        const int64_t i = r0 + rr;
+        if (i >= T.n_rows) break;
+        const double sum = a[rr];
+        if constexpr (MODE == 0) {
+          const double pk = p[own + i], rk = r[i];
+          st_stream(&Ap[i], sum);
+          s_pap = fma(pk, sum, s_pap);
+          s_rap = fma(rk, sum, s_rap);
+          s_apap = fma(sum, sum, s_apap);
+          s_rr = fma(rk, rk, s_rr);
+        } else {
+          Ap[i] = sum;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (MODE == 0) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+}
+
+// ---- setup: count / fill one row block per 64-thread workgroup (LDS counters per segment) ----
+struct GenSrc {  // a generated family (problem.hpp), global rows row_begin + i, ext columns
+  ProblemSpec s;
+  int64_t row_begin, col_lo, pad;
+  const int64_t* rp64;  // inclusive-scanned row lengths (the random-SPD diagonal = the row length)
+  template <class F>
+  __device__ void row(int64_t i, F&& f) const {
+    for_each_entry(s, row_begin + i, [&](int64_t c, double v) { f(c - col_lo + pad, v); }, rp64[i + 1] - rp64[i]);
+  }
+};
+struct CsrSrc {  // a user matrix's rows on the device (local CSR, ext columns)
+  const int64_t* rp;
+  const int32_t* cols;
+  const double* vals;
+  template <class F>
+  __device__ void row(int64_t i, F&& f) const {
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) f((int64_t)cols[k], vals[k]);
+  }
+};
+
+// FILL = false: tptr[b * G + g + 1] = entries of tile (b, g); FILL = true: write the tiles (tptr =
+// exclusive offsets).  Lanes take rows rr = lane, lane + 64, ... of the block in lockstep; within a
+// wave the LDS atomics return their old values in a fixed order, so the fill is deterministic.
+template <bool FILL, class Src>
+__global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, int seg_shift, int64_t* __restrict__ tptr,
+                                                    uint32_t* __restrict__ idx, double* __restrict__ vals) {
+  extern __shared__ int cnt[];
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  for (int g = lane; g < G; g += 64) cnt[g] = 0;
+  __syncthreads();
+  const uint32_t mask = (1u << seg_shift) - 1u;
+  for (int rr = lane; rr < kTileB; rr += 64) {
+    const int64_t i = b * kTileB + rr;
+    if (i >= n) break;
+    src.row(i, [&](int64_t ec, double v) {
+      const int g = (int)(ec >> seg_shift);
+      const int pos = atomicAdd(&cnt[g], 1);
+      if constexpr (FILL) {
+        const int64_t dst = tptr[b * G + g] + pos;
+        idx[dst] = ((uint32_t)rr << 22) | ((uint32_t)ec & mask);
+        vals[dst] = v;
+      }
+    });
+  }
+  __syncthreads();
+  if constexpr (!FILL)
+    for (int g = lane; g < G; g += 64) tptr[b * G + g + 1] = cnt[g];
+}
+
+}  // namespace
+
+TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
+  TilesGeometry t;
+  t.seg_shift = seg_shift;
+  t.nblocks = (n_rows + kTileB - 1) / kTileB;
+  t.G = (int)std::max<int64_t>(1, (ext_len + ((int64_t)1 << seg_shift) - 1) >> seg_shift);
+  return t;
+}
+
+int tiles_grid() {
+  static int cached = -1;
+  if (cached < 0) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_tiles<0>), 256, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    (void)hipGetLastError();
+    cached = std::min(per_cu, 4) * num_cus();  // every workgroup resident (pacing waits on them)
+  }
+  return cached;
+}
+
+namespace {
+template <class Src>
+void tiles_build_impl(const Src& src, int64_t n, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,
+                      bool fill, hipStream_t st) {
+  MCG_CHECK(geo.G <= kTileMaxSegments, "tiles: too many column segments for the LDS counters");
+  MCG_CHECK(geo.seg_shift <= 22, "tiles: segments are at most 2^22 columns");
+  if (geo.nblocks == 0) return;
+  const size_t lds = (size_t)geo.G * sizeof(int);
+  if (fill)
+    hipLaunchKernelGGL((k_tiles_build<true, Src>), dim3((unsigned)geo.nblocks), dim3(64), lds, st, src, n, geo.G,
+                       geo.seg_shift, tptr, idx, vals);
+  else
+    hipLaunchKernelGGL((k_tiles_build<false, Src>), dim3((unsigned)geo.nblocks), dim3(64), lds, st, src, n, geo.G,
+                       geo.seg_shift, tptr, idx, vals);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(tiles_build)");
+}
+}  // namespace
+
+void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
+                     const int64_t* rp64, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,
+                     bool fill, hipStream_t st) {
+  tiles_build_impl(GenSrc{s, row_begin, col_lo, pad, rp64}, n, geo, tptr, idx, vals, fill, st);
+}
+
+void tiles_build_csr(const int64_t* rp, const int32_t* cols, const double* cvals, int64_t n, const TilesGeometry& geo,
+                     int64_t* tptr, uint32_t* idx, double* vals, bool fill, hipStream_t st) {
+  tiles_build_impl(CsrSrc{rp, cols, cvals}, n, geo, tptr, idx, vals, fill, st);
+}
+
+void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r, double* Ap, int64_t own_off,
+                         double* partials, int pstride, int grid, CgState* st, double tol, int first, int check,
+                         hipStream_t stream, const RedCtl& rc) {
+  if (grid <= 0) return;
+  MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
+  if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
+  hipLaunchKernelGGL(k_tiles<0>, dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, pstride, st,
+                     tol, first, check, rc);
+  MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+}
+
+void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream) {
+  if (grid <= 0 || T.nblocks == 0) return;
+  if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
+  hipLaunchKernelGGL(k_tiles<1>, dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr,
+                     0.0, 0, 0, RedCtl());
+  MCG_HIP(hipGetLastError(), "compute mv failed(y)");
+}
+
+}  // namespace kern
+}  // namespace mcg

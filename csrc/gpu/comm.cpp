@@ -1,10 +1,25 @@
 #include "mcg/comm.hpp"
 
+#include <dlfcn.h>
+
 #include <cstring>
 
 #include "mcg/check.hpp"
 
 namespace mcg {
+
+int rccl_version() {
+  int v = 0;
+  if (ncclGetVersion(&v) != ncclSuccess) v = 0;
+  return v;
+}
+
+// the shared object that provides ncclGetVersion in this process: the one every RCCL call binds to
+std::string rccl_library() {
+  Dl_info info{};
+  if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) != 0 && info.dli_fname) return info.dli_fname;
+  return "?";
+}
 
 std::string unique_id_bytes() {
   ncclUniqueId id;
@@ -26,9 +41,15 @@ Comm::Comm(int rank, int world, const ncclUniqueId& reduce_id, const ncclUniqueI
   MCG_RCCL(ncclCommInitRank(&halo_, world, halo_id, rank), "RCCL communicator init failed(halo)");
 }
 
+Comm::Comm(int rank, int world, const ncclUniqueId& id) : rank_(rank), world_(world) {
+  MCG_CHECK(world >= 1 && rank >= 0 && rank < world, "invalid rank/world");
+  MCG_RCCL(ncclCommInitRank(&reduce_, world, id, rank), "RCCL communicator init failed(reduce)");
+  halo_ = reduce_;
+}
+
 Comm::~Comm() {
   if (aborted_) return;
-  if (halo_) (void)ncclCommDestroy(halo_);
+  if (halo_ && halo_ != reduce_) (void)ncclCommDestroy(halo_);
   if (reduce_) (void)ncclCommDestroy(reduce_);
 }
 
@@ -90,6 +111,7 @@ int Comm::count() const {
 
 void Comm::check_async() {
   for (ncclComm_t c : {reduce_, halo_}) {
+    if (c == nullptr) continue;
     ncclResult_t async = ncclSuccess;
     MCG_RCCL(ncclCommGetAsyncError(c, &async), "RCCL async error query failed");
     if (async != ncclSuccess) {
@@ -102,7 +124,7 @@ void Comm::check_async() {
 void Comm::abort() {
   if (aborted_) return;
   aborted_ = true;
-  if (halo_) (void)ncclCommAbort(halo_);
+  if (halo_ && halo_ != reduce_) (void)ncclCommAbort(halo_);
   if (reduce_) (void)ncclCommAbort(reduce_);
 }
 

@@ -101,6 +101,8 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   }
   use_comm_ = comm_ != nullptr && (world_ > 1 || opt_.force_comm);
   use_halo_ = use_comm_ && L_.has_halo();
+  // one communicator for halo and all-reduce: every collective in one stream order on s0_
+  if (use_comm_ && comm_->serialized()) opt_.overlap = false;
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
   MCG_CHECK(opt_.graph_iters >= 2 && opt_.graph_iters % 2 == 0, "graph_iters must be even and >= 2");
   if (opt_.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
@@ -194,9 +196,15 @@ void GpuCgSolver::setup() {
   DeviceBuffer<int64_t> rp64(n + 1, "A");
   HostCsr user;
   const bool is_user = spec_.kind == ProblemKind::Csr;
+  // ---- irregular sparsity: L2-segment COO tiles (the split pass's SpMV) ----
+  // auto: the scrambled random SPD, or a user matrix that is not a grid stencil on the all-gather
+  // layout (its columns are scattered over the whole vector); the same decision on every rank
+  // (the spec and the layout kind are global)
+  tiles_ = opt_.recurrence == 1 && opt_.pmat != 0 && opt_.tiles != 0 &&
+           (opt_.tiles == 1 || scrambled(spec_) || (is_user && L_.allgather && stencil_line(spec_) == 0));
   if (is_user) {
     user = build_local_csr(spec_, L_);
-    if (opt_.format == 1 && opt_.sell_sigma != 0 && n > 64 && (opt_.sell_sigma > 0 || stencil_line(spec_) == 0)) {
+    if (opt_.format == 1 && !tiles_ && opt_.sell_sigma != 0 && n > 64 && (opt_.sell_sigma > 0 || stencil_line(spec_) == 0)) {
       // SELL-C-sigma (int32 columns): the windows never mix interior and boundary slices (auto: not
       // for a detected grid stencil, whose rows stay in grid order for the line / plane carry)
       const int64_t sig = opt_.sell_sigma > 1 ? (opt_.sell_sigma + 63) / 64 * 64 : 4096;
@@ -245,7 +253,46 @@ void GpuCgSolver::setup() {
   info_.idx64 = nnz >= ((int64_t)1 << 31) - 64 || opt_.force_idx64;
 
   size_t matrix_bytes = 0;
-  if (opt_.format == 1) {
+  if (tiles_) {
+    tgeo_ = kern::tiles_geometry(n, L_.ext_len, std::max(10, std::min(22, opt_.tile_seg_log2)));
+    MCG_CHECK(tgeo_.G <= kern::kTileMaxSegments, "tiles: too many column segments (raise tile_seg_log2)");
+    tptr_.allocate(tgeo_.nblocks * tgeo_.G + 1, "A");
+    MCG_HIP(hipMemsetAsync(tptr_.get(), 0, tptr_.bytes(), s0_), "device memset failed(A)");
+    tidx_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
+    tvals_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
+    tpace_.allocate(kern::kTilePaceWords, "A");
+    DeviceBuffer<int32_t> tc;
+    DeviceBuffer<double> tv;
+    if (is_user && nnz) {  // this rank's rows on the device (temporary CSR, ext columns)
+      tc.allocate(nnz, "A");
+      tv.allocate(nnz, "A");
+      MCG_HIP(hipMemcpy(tc.get(), user.cols.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(A)");
+      MCG_HIP(hipMemcpy(tv.get(), user.vals.data(), nnz * sizeof(double), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(A)");
+    }
+    const int64_t ntp = tgeo_.nblocks * tgeo_.G;
+    for (int fill = 0; fill < 2; ++fill) {
+      if (is_user) kern::tiles_build_csr(rp64.get(), tc.get(), tv.get(), n, tgeo_, tptr_.get(), tidx_.get(), tvals_.get(), fill, s0_);
+      else kern::tiles_build_gen(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), tgeo_, tptr_.get(), tidx_.get(),
+                                 tvals_.get(), fill, s0_);
+      if (!fill && ntp > 0) {  // tile sizes -> offsets
+        DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ntp), "A");
+        kern::scan_inclusive_i64(tptr_.get() + 1, ntp, tmp.get(), s0_);
+        MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+      }
+    }
+    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
+    int64_t tot = 0;
+    MCG_HIP(hipMemcpy(&tot, tptr_.get() + ntp, sizeof(int64_t), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(A)");
+    MCG_CHECK(tot == nnz, "tiles: the fill does not match the row lengths");
+    d16_ = false;
+    c8_ = false;
+    info_.format = 5;
+    info_.sell_fill = 1.0;
+    matrix_bytes = (size_t)nnz * 12 + tptr_.bytes();
+  } else if (opt_.format == 1) {
     // ---- SELL-64, generated directly (no CSR intermediate: peak memory = the SELL arrays) ----
     const int64_t ns = (n + 63) / 64;
     slice_ptr_.allocate(ns + 1, "A");
@@ -360,11 +407,14 @@ void GpuCgSolver::setup() {
 
   // ---- iteration form for long / unstructured rows: the materialized-p split pass ----
   pmat_ = opt_.recurrence == 1 && opt_.pmat != 0 &&
-          (opt_.pmat == 1 || aligned_ || (win_doubles_ == 0 && !c8_ && (L_.allgather || nnz >= 32 * n)));
+          (opt_.pmat == 1 || aligned_ || tiles_ || (win_doubles_ == 0 && !c8_ && (L_.allgather || nnz >= 32 * n)));
   // the pass form decides which ghost vectors are exchanged ({r, Ap} + p, or p alone): every rank
   // must take the same one, whatever its own rows look like
   if (use_comm_ && world_ > 1) pmat_ = all_ranks_agree_(pmat_);
   MCG_CHECK(!aligned_ || pmat_, "aligned SELL needs the split pass");
+  MCG_CHECK(!tiles_ || pmat_, "tiles need the split pass on every rank");
+  info_.tiles = tiles_;
+  info_.tile_segments = tiles_ ? tgeo_.G : 0;
   if (pmat_) {
     opt_.interleave = 0;
     info_.interleave = false;
@@ -450,6 +500,12 @@ void GpuCgSolver::setup() {
     }
     g_int_ = grid_a(tr_int_);
     g_bnd_ = grid_a(tr_bnd_);
+  }
+  if (tiles_) {  // one launch over every row block: the resident workgroups (the pacing waits on each)
+    g_all_ = n > 0 ? kern::tiles_grid() : 0;
+    if (opt_.blocks_per_cu > 0) g_all_ = std::min(g_all_, ncu_ * opt_.blocks_per_cu);  // fewer waves: more rounds
+    g_int_ = 0;
+    g_bnd_ = g_all_;
   }
   if (opt_.xcd_map > 0) tr_all_.xcd = tr_int_.xcd = tr_bnd_.xcd = 8;
   if (opt_.xcd_map < 0 && opt_.format == 1 && stencil_plane(spec_) > 0 && win_doubles_ == 0 &&
@@ -1035,9 +1091,15 @@ void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red, int part
     rc.first = first;
   }
   const int64_t n = L_.n_local();
+  double* pp = partials_.get() + (which == 2 ? bnd_base_ : 0);
+  if (tiles_) {
+    MCG_CHECK(part == 0, "tiles: one SpMV launch per iteration");
+    kern::cg_split_spmv_tiles(tiles_view(), p_[0].get(), r_.get(), Ap_.get(), L_.own_off, pp, pstride_, grid, st_.get(),
+                              opt_.tol, first, check, s0_, rc);
+    return;
+  }
   const int fmt = opt_.format == 1 ? (aligned_ ? 6 : (c8_ ? 4 : (d16_ ? 3 : 1))) : (info_.spmv_variant == 2 ? 5 : 0);
   const SellDev S = sell_view();
-  double* pp = partials_.get() + (which == 2 ? bnd_base_ : 0);
   if (info_.idx64)
     kern::cg_split_spmv<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S,
                                  p_[0].get(), r_.get(), Ap_.get(), L_.own_off, tr, pp, pstride_, grid, st_.get(),
@@ -1625,7 +1687,9 @@ double GpuCgSolver::true_residual_norm() {
     double* v[1] = {xe.get()};
     comm_->halo_exchange(L_, v, 1, s);
   }
-  if (opt_.format == 1) {
+  if (tiles_) {
+    kern::spmv_tiles(tiles_view(), xe.get(), y.get(), g_all_, s);
+  } else if (opt_.format == 1) {
     kern::spmv_sell(sell_view(), xe.get(), y.get(), s);
   } else if (info_.idx64) {
     kern::spmv_csr<int64_t>(CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);

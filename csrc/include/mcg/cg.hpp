@@ -86,6 +86,11 @@ struct CgOptions {
   int ag_overlap = -1;       // SELL-64/aligned on an all-gather ghost layout: sum the own-block column slots while the
                              // all-gather of p is in flight, the rest after it (two SpMV halves); -1 = auto (on
                              // when the halo overlap is on), 0 = off
+  int tiles = -1;            // irregular sparsity: the split pass's SpMV on L2-segment COO tiles (cg_tiles.hip: rows
+                             // in blocks of 1024 owned by one wave, columns in segments of 2^tile_seg_log2, every
+                             // wave sweeping the segments together so the gathers of p hit the L2); -1 = auto (the
+                             // scrambled random SPD, or a non-stencil user matrix on the all-gather layout), 0 = off
+  int tile_seg_log2 = 18;    // tiles: column segment = 2^k doubles (18: 2 MiB of p, half an XCD's L2)
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

@@ -5,7 +5,9 @@
 // boundary-row halo exchange onto RCCL over xGMI.
 //
 //   Comm (RCCL)   two communicators so the halo (side stream) and the scalar
-//                 all-reduces (compute stream) can be in flight together:
+//                 all-reduces (compute stream) can be in flight together (or, single-
+//                 communicator mode, ONE communicator whose halo and all-reduce the solver
+//                 issues in one stream order on the compute stream: serialized()):
 //                 - reduce comm: ncclAllReduce(sum, f64) of the CG scalars, in place
 //                   on device memory (CgState) — no host round trip
 //                 - halo comm: ncclSend/ncclRecv inside ncclGroupStart/End straight
@@ -39,6 +41,8 @@
 namespace mcg {
 
 std::string unique_id_bytes();  // ncclGetUniqueId -> 128 raw bytes
+int rccl_version();             // ncclGetVersion of the RCCL this process runs (e.g. 22606 = 2.26.6)
+std::string rccl_library();     // path of the shared object that provides it
 ncclUniqueId unique_id_from_bytes(const std::string& b);
 
 class Communicator {
@@ -60,11 +64,16 @@ class Communicator {
   virtual bool moves_data() const { return true; }
   // tear down outstanding collectives after a fatal error (watchdog)
   virtual void abort() {}
+  // true: halo and all-reduce share one communicator, so the solver must issue them in one stream
+  // order (no side-stream halo; CgOptions::overlap is forced off)
+  virtual bool serialized() const { return false; }
 };
 
 class Comm final : public Communicator {
  public:
   Comm(int rank, int world, const ncclUniqueId& reduce_id, const ncclUniqueId& halo_id);
+  // single-communicator mode: halo and all-reduce on one communicator (serialized())
+  Comm(int rank, int world, const ncclUniqueId& id);
   ~Comm() override;
   Comm(const Comm&) = delete;
   Comm& operator=(const Comm&) = delete;
@@ -77,6 +86,7 @@ class Comm final : public Communicator {
   void check_async() override;
   // ranks in the communicator as RCCL sees them (ncclCommCount)
   int count() const;
+  bool serialized() const override { return halo_ == reduce_; }
   // one grouped point-to-point exchange on the halo communicator: send n doubles to `to`, receive
   // n doubles from `from` (either may be this rank: the loopback the 1-GPU tests capture in graphs)
   void sendrecv(const double* send, int to, double* recv, int from, size_t n, hipStream_t stream);

@@ -323,6 +323,41 @@ void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, 
                    double* Ap, int64_t own_off, const TileRanges& tr, double* partials, int pstride, int grid,
                    CgState* st, double tol, int first, int check, hipStream_t stream, const RedCtl& rc = RedCtl(),
                    int part = 0);
+// ---- L2-segment COO tiles (csrc/gpu/cg_tiles.hip): the irregular-sparsity SpMV ----
+// Row blocks of kTileB rows x column segments of 2^seg_shift doubles; tile (b, g) holds the block's
+// nonzeros in segment g as (row in block << 22 | column in segment) + value.  Every wave owns one
+// block at a time (sums in LDS) and all waves sweep the segments together (paced per segment), so
+// the gathers of p hit the L2.
+constexpr int kTileB = 1024;
+constexpr int kTileMaxSegments = 8192;  // LDS counters of the build kernels (32 KiB)
+constexpr int kTilePaceWords = 8 * 64;  // pacing counters: 8 groups, 256 B apart
+struct TilesGeometry {
+  int64_t nblocks = 0;
+  int G = 0;
+  int seg_shift = 18;
+};
+struct TilesDev {
+  const int64_t* tptr = nullptr;  // nblocks * G + 1
+  const uint32_t* idx = nullptr;
+  const double* vals = nullptr;
+  int64_t n_rows = 0, nblocks = 0;
+  int G = 0, seg_shift = 18;
+  unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
+};
+TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
+int tiles_grid();  // workgroups of the SpMV: the resident count (pacing waits on every workgroup)
+// count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0) then fill
+void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
+                     const int64_t* rp64, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,
+                     bool fill, hipStream_t st);
+void tiles_build_csr(const int64_t* rp, const int32_t* cols, const double* cvals, int64_t n, const TilesGeometry& geo,
+                     int64_t* tptr, uint32_t* idx, double* vals, bool fill, hipStream_t st);
+// the split pass's SpMV on tiles (same contract as cg_split_spmv part 0)
+void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r, double* Ap, int64_t own_off,
+                         double* partials, int pstride, int grid, CgState* st, double tol, int first, int check,
+                         hipStream_t stream, const RedCtl& rc = RedCtl());
+void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream);
+
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),

@@ -53,6 +53,8 @@ struct SolverInfo {
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool fused_reduce = false;  // the pass reduces its own block partials (one kernel per iteration)
   bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
+  bool tiles = false;         // ... its SpMV on L2-segment COO tiles (CgOptions::tiles)
+  int tile_segments = 0;      // column segments of the tiles (G)
   int sigma = 0;              // SELL-C-sigma window (rows) of a user matrix; 0 = slices in row order
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
@@ -174,6 +176,25 @@ class GpuCgSolver {
   bool ag_overlap_ = false;
   int ndict_ = 0;
   bool c8_ = false;
+  // L2-segment COO tiles (cg_tiles.hip): tile pointers, packed (row, column) indices, values, pacing
+  bool tiles_ = false;
+  kern::TilesGeometry tgeo_;
+  DeviceBuffer<int64_t> tptr_;
+  DeviceBuffer<uint32_t> tidx_;
+  DeviceBuffer<double> tvals_;
+  DeviceBuffer<unsigned> tpace_;
+  kern::TilesDev tiles_view() const {
+    kern::TilesDev t;
+    t.tptr = tptr_.get();
+    t.idx = tidx_.get();
+    t.vals = tvals_.get();
+    t.n_rows = L_.n_local();
+    t.nblocks = tgeo_.nblocks;
+    t.G = tgeo_.G;
+    t.seg_shift = tgeo_.seg_shift;
+    t.pace = tpace_.get();
+    return t;
+  }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
   int win_doubles_ = 0;         // 0 = windowed pass off
   bool pipe_ = false;           // software-pipelined stencil pass

@@ -218,6 +218,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("carry_nt", &CgOptions::carry_nt)
       .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("fused_reduce", &CgOptions::fused_reduce)
+      .def_readwrite("tiles", &CgOptions::tiles)
+      .def_readwrite("tile_seg_log2", &CgOptions::tile_seg_log2)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       .def_readwrite("pmat", &CgOptions::pmat)
       .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
@@ -305,6 +307,12 @@ PYBIND11_MODULE(_C, m) {
     return n;
   });
   m.def("unique_id", []() { return py::bytes(unique_id_bytes()); });
+  m.def("rccl_info", []() {
+    py::dict d;
+    d["version"] = rccl_version();
+    d["library"] = rccl_library();
+    return d;
+  }, "ncclGetVersion and the library that provides it (the same RCCL as bin/mcg-cg: tests/test_gpu_rccl.py)");
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
       .def(py::init([](int rank, int world, py::bytes id_red, py::bytes id_halo) {
@@ -313,6 +321,14 @@ PYBIND11_MODULE(_C, m) {
              return std::make_shared<Comm>(rank, world, unique_id_from_bytes(a), unique_id_from_bytes(b));
            }),
            py::arg("rank"), py::arg("world"), py::arg("reduce_id"), py::arg("halo_id"))
+      .def(py::init([](int rank, int world, py::bytes id) {
+             std::string a = id;
+             py::gil_scoped_release rel;
+             return std::make_shared<Comm>(rank, world, unique_id_from_bytes(a));
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("id"),
+           "single-communicator mode: halo and all-reduce on one communicator, issued in one stream order")
+      .def_property_readonly("serialized", &Comm::serialized)
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
       .def_property_readonly("count", &Comm::count)
@@ -387,7 +403,7 @@ PYBIND11_MODULE(_C, m) {
         d["halo_out"] = i.halo_out;
         d["interior_rows"] = i.interior_rows;
         d["idx64"] = i.idx64;
-        d["format"] = i.format == 4 ? "sell64-aligned"
+        d["format"] = i.format == 5 ? "tiles" : i.format == 4 ? "sell64-aligned"
                       : i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
         d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["interleave"] = i.interleave;
@@ -397,6 +413,8 @@ PYBIND11_MODULE(_C, m) {
         d["carry"] = i.carry;
         d["fused_reduce"] = i.fused_reduce;
         d["pmat"] = i.pmat;
+        d["tiles"] = i.tiles;
+        d["tile_segments"] = i.tile_segments;
         d["sigma"] = i.sigma;
         d["sell_fill"] = i.sell_fill;
         d["allgather"] = i.allgather;

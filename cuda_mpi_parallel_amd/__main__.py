@@ -22,7 +22,7 @@ SWITCHES = {"--no-overlap", "--no-graph", "--force-comm", "--verify"}
 CHOICES = {"--problem": ["demo", "poisson2d", "poisson3d", "randspd", "csr", "random-spd", "random"],
            "--rhs": ["reference", "random", "ones"], "--device": ["gpu", "cpu"],
            "--format": ["csr", "sell", "sell16", "sellc8"], "--print-x": ["auto", "yes", "no"],
-           "--report": ["text", "json"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
+           "--report": ["text", "json"], "--comm": ["dual", "single"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
 INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
         "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--spmv-param", "--update-unroll",
         "--nt-loads", "--xcd-map", "--sell-slices", "--checkpoint-every", "--inject-nan-at"}
@@ -33,7 +33,7 @@ DEFAULTS = {"--problem": "demo", "--seed": 1234, "--device": "gpu", "--gpus": No
             "--pmat": "auto", "--fused-reduce": "auto", "--halo-mode": "auto", "--blocks-per-cu": 0,
             "--spmv-variant": -1, "--spmv-param": 0, "--update-unroll": 1, "--nt-loads": 0, "--xcd-map": -1,
             "--sell-slices": 1, "--checkpoint": "", "--checkpoint-every": 0, "--resume": "", "--inject-nan-at": -1,
-            "--print-x": "auto", "--report": "text"}
+            "--print-x": "auto", "--report": "text", "--comm": "dual"}
 
 
 def _parser() -> argparse.ArgumentParser:
@@ -132,7 +132,7 @@ def _run(args) -> int:
         rank, world = 0, args.sim_ranks
     else:
         s = mcg.CGSolver(spec, maxit=maxit, tol=tol, check_every=args.check_every, overlap=not args.no_overlap,
-                         use_graph=not args.no_graph, force_comm=args.force_comm,
+                         use_graph=not args.no_graph, force_comm=args.force_comm, comm_mode=args.comm,
                          format=args.format or ("csr" if spec.problem == "demo" else "sellc8"),
                          blocks_per_cu=args.blocks_per_cu, spmv_variant=args.spmv_variant,
                          spmv_param=args.spmv_param, update_unroll=args.update_unroll, nt_loads=args.nt_loads,

@@ -43,20 +43,25 @@ def init_process_group(env: DistEnv, backend: str = "gloo") -> None:
         dist.init_process_group(backend=backend, rank=env.rank, world_size=env.world)
 
 
-def bootstrap_comm(env: DistEnv, force: bool = False):
-    """Create the native RCCL communicator pair for this rank (None for a single rank
-    unless ``force``).  Rank 0 draws the unique ids and broadcasts them over the
-    torch.distributed store-backed process group."""
+def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "dual"):
+    """Create the native RCCL communicator(s) for this rank (None for a single rank unless
+    ``force``).  Rank 0 draws the unique ids and broadcasts them over the torch.distributed
+    store-backed process group.  ``mode``: "dual" = a reduce and a halo communicator (halo on the
+    side stream, overlapped); "single" = one communicator, every collective in one stream order."""
     if env.world == 1 and not force:
         return None
+    if mode not in ("dual", "single"):
+        raise ValueError(f"comm mode must be dual or single, got {mode!r}")
     C = native()
+    nids = 2 if mode == "dual" else 1
     if env.world == 1:
-        return C.Comm(0, 1, C.unique_id(), C.unique_id())
-    if not dist.is_initialized():
-        raise RuntimeError("bootstrap_comm needs torch.distributed initialised (call init_process_group)")
-    ids = [C.unique_id(), C.unique_id()] if env.rank == 0 else [None, None]
-    dist.broadcast_object_list(ids, src=0)
-    return C.Comm(env.rank, env.world, ids[0], ids[1])
+        ids = [C.unique_id() for _ in range(nids)]
+    else:
+        if not dist.is_initialized():
+            raise RuntimeError("bootstrap_comm needs torch.distributed initialised (call init_process_group)")
+        ids = [C.unique_id() for _ in range(nids)] if env.rank == 0 else [None] * nids
+        dist.broadcast_object_list(ids, src=0)
+    return C.Comm(env.rank, env.world, *ids)
 
 
 def set_device(env: DistEnv) -> int:

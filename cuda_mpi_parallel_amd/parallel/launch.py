@@ -13,8 +13,12 @@ is loaded, counts devices without initialising HIP, and only forks/execs childre
 then SIGKILL after a grace period) so a rank stuck in a collective whose peer died
 cannot hang the job; the launcher exits with the first failing child's status.
 
-Only the standard library is used here (plus ``torch.cuda.device_count()`` for the
-device count, which does not initialise the GPU on this image).
+Only the standard library is used here: GPUs are counted the way the ROCm runtime enumerates
+them -- KFD topology nodes in sysfs (``/sys/class/kfd/kfd/topology/nodes/*/properties``) with a
+nonzero ``gfx_target_version`` whose render node ``/dev/dri/renderD<drm_render_minor>`` this
+process can open (a container sees the host's whole topology but only its own render nodes) --
+and the ``*_VISIBLE_DEVICES`` variables, so the parent cannot initialise HIP before it forks
+the ranks; ``torch.cuda.device_count()`` is only the fallback when there is no KFD topology.
 """
 from __future__ import annotations
 
@@ -34,6 +38,35 @@ def under_launcher() -> bool:
     return "WORLD_SIZE" in os.environ
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpu_count(root: str = KFD_NODES, dri: str = "/dev/dri") -> Optional[int]:
+    """GPUs this process can open: KFD topology nodes with a nonzero gfx_target_version whose
+    render node is accessible; None without a KFD topology."""
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        props = {}
+        try:
+            with open(os.path.join(root, node, "properties")) as f:
+                for line in f:
+                    k, _, v = line.strip().partition(" ")
+                    props[k] = v.strip()
+            if int(props.get("gfx_target_version", "0") or "0") == 0:
+                continue
+            minor = props.get("drm_render_minor")
+            if minor is not None and not os.access(os.path.join(dri, f"renderD{int(minor)}"), os.R_OK | os.W_OK):
+                continue
+            n += 1
+        except (OSError, ValueError):
+            continue
+    return n
+
+
 def visible_devices() -> int:
     """Number of GPUs this process may use (no HIP initialisation)."""
     for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
@@ -43,16 +76,18 @@ def visible_devices() -> int:
             break
     else:
         n_env = None
-    try:
-        import warnings
+    n = kfd_gpu_count()
+    if n is None:  # no KFD topology (not a ROCm host): ask torch, which does not initialise HIP either
+        try:
+            import warnings
 
-        import torch
+            import torch
 
-        with warnings.catch_warnings():  # torch warns when amdsmi finds no GPU (CPU hosts)
-            warnings.simplefilter("ignore")
-            n = int(torch.cuda.device_count())
-    except Exception:  # pragma: no cover - torch missing / broken
-        n = 0
+            with warnings.catch_warnings():  # torch warns when amdsmi finds no GPU (CPU hosts)
+                warnings.simplefilter("ignore")
+                n = int(torch.cuda.device_count())
+        except Exception:  # pragma: no cover - torch missing / broken
+            n = 0
     return n if n_env is None else min(n, n_env)
 
 
@@ -138,10 +173,14 @@ def spawn_ranks(world: int, argv: List[str], script: Optional[str] = None, modul
 
 
 def launch_or_none(gpus: Optional[int], argv: List[str], force_spawn: bool = False,
-                   script: Optional[str] = None, module: Optional[str] = None) -> Optional[int]:
+                   script: Optional[str] = None, module: Optional[str] = None,
+                   share_device: bool = False) -> Optional[int]:
     """Entry-point helper.  Returns None when this process should run as a rank itself
     (already under a launcher, or a single GPU without ``force_spawn``); otherwise checks
-    the device count, starts the ranks and returns the job's exit status."""
+    the device count, starts the ranks and returns the job's exit status.
+
+    ``share_device``: the ranks may outnumber the GPUs (a rehearsal whose ranks share device 0
+    and move no data between GPUs); the device-count check is skipped."""
     if under_launcher():
         world = int(os.environ["WORLD_SIZE"])
         if gpus is not None and gpus != world:
@@ -151,7 +190,7 @@ def launch_or_none(gpus: Optional[int], argv: List[str], force_spawn: bool = Fal
     n = 1 if gpus is None else gpus
     if n == 1 and not force_spawn:
         return None
-    have = visible_devices()
+    have = n if share_device else visible_devices()
     if n > have:
         print(f"launcher: --gpus {n} but {have} GPU(s) visible", file=sys.stderr)
         return 2

@@ -41,13 +41,14 @@ class CGSolver:
 
     def __init__(self, spec: ProblemSpec, maxit: int = 2000, tol: float = 1e-7, check_every: int = 32,
                  overlap: bool = True, use_graph: bool = True, format: str = "csr", force_comm: bool = False,
-                 blocks_per_cu: int = 0, env: Optional[_dist.DistEnv] = None, comm=None, **tuning):
+                 blocks_per_cu: int = 0, env: Optional[_dist.DistEnv] = None, comm=None, comm_mode: str = "dual",
+                 **tuning):
         self.spec = spec
         self.env = env or _dist.dist_env()
         _dist.set_device(self.env)
         if comm is None and (self.env.world > 1 or force_comm):
             _dist.init_process_group(self.env)
-            comm = _dist.bootstrap_comm(self.env, force=force_comm)
+            comm = _dist.bootstrap_comm(self.env, force=force_comm, mode=comm_mode)
         self.comm = comm
         self.opts = _opts(maxit, tol, check_every=check_every, overlap=overlap, use_graph=use_graph,
                           force_comm=force_comm, format=format, blocks_per_cu=blocks_per_cu, **tuning)

@@ -186,3 +186,90 @@ def test_null_comm_rank_share_takes_the_split_pass(mcg):
     s.reset()
     s.run_iterations(6)
     s.synchronize()
+
+
+# ---- scrambled random SPD (P^T A P: genuinely irregular) on L2-segment COO tiles ----
+SCR = dict(rows=60000, band=24, density=0.5, scramble=1)
+
+
+@pytest.mark.parametrize("seg", [18, 12])
+def test_tiles_scrambled_matches_cpu(mcg, seg):
+    """The scrambled family takes the tiles SpMV by default; seg = 12 cuts p into 15 segments of 4096
+    doubles (many tiles per row block); the solve matches the CPU oracle and ||b - A x||."""
+    spec = mcg.make_problem("randspd", **SCR)
+    cpu = _cpu(mcg, spec)
+    s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, check_every=8, tile_seg_log2=seg)
+    assert s.info["tiles"] and s.info["pmat"] and s.info["format"] == "tiles"
+    assert s.info["tile_segments"] == (1 if seg == 18 else 15)
+    out = s.solve()
+    assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 1
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    assert s.true_residual_norm() < 1e-6
+
+
+def test_tiles_same_recurrence_as_sell_split_and_deterministic(mcg):
+    """Tiles vs the SELL split pass: the same scalars and vectors up to the rounding of the row sums
+    (fixed iterations); two tile solvers built separately agree bit for bit (deterministic fill and
+    in-order LDS sums), and a graph solve equals an eager one."""
+    spec = mcg.make_problem("randspd", **SCR)
+    kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=40, tile_seg_log2=12)
+    a = mcg.CGSolver(spec, tiles=1, **kw).solve()
+    b = mcg.CGSolver(spec, tiles=0, pmat=1, **kw).solve()
+    assert a["iterations"] == b["iterations"] == 40
+    assert abs(a["rnorm"] - b["rnorm"]) <= 1e-10 * b["rnorm"]
+    np.testing.assert_allclose(a["x_local"], b["x_local"], rtol=1e-12, atol=1e-14 * np.abs(b["x_local"]).max())
+    c = mcg.CGSolver(spec, tiles=1, use_graph=False, **kw).solve()
+    assert c["rnorm"] == a["rnorm"]
+    np.testing.assert_array_equal(c["x_local"], a["x_local"])
+
+
+def test_tiles_several_rounds_of_row_blocks(mcg):
+    """More row blocks than waves (blocks_per_cu = 1: 1024 waves, 1.2 M rows = 1172 blocks): the
+    waves take a second round of blocks; the same row sums as the full grid (only the dot products'
+    block partials group differently)."""
+    spec = mcg.make_problem("randspd", rows=1200000, band=4, density=0.5, scramble=1)
+    kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=12, tile_seg_log2=16)
+    a = mcg.CGSolver(spec, blocks_per_cu=1, **kw)
+    b = mcg.CGSolver(spec, **kw)
+    assert a.info["tiles"] and a.info["grid_a"] < b.info["grid_a"]
+    ra, rb = a.solve(), b.solve()
+    assert abs(ra["rnorm"] - rb["rnorm"]) <= 1e-13 * rb["rnorm"]
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-13, atol=1e-15 * np.abs(rb["x_local"]).max())
+    assert abs(a.true_residual_norm() - ra["rnorm"]) <= 1e-9 * ra["rnorm"]
+
+
+def test_tiles_user_matrix_scattered(mcg):
+    """A user CSR with scattered columns (random sparsity, strictly diagonally dominant) on the tiles
+    SpMV (forced at P = 1; auto on the all-gather layout) matches the CPU reference solve."""
+    import scipy.sparse as sp
+
+    n = 20000
+    rng = np.random.default_rng(3)
+    B = sp.random(n, n, density=6.0 / n, random_state=4, format="csr")
+    B = B + B.T
+    A = B + sp.diags(np.asarray(abs(B).sum(axis=1)).ravel() + 1.0)
+    perm = rng.permutation(n)
+    A = A[perm][:, perm].tocsr()
+    b = rng.random(n)
+    prob = mcg.csr_problem(A, b=b)
+    s = mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tol=1e-10, tile_seg_log2=12)
+    assert s.info["tiles"]
+    out = s.solve()
+    cpu = _cpu(mcg, prob, tol=1e-10)
+    assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 1
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-8, atol=1e-10)
+
+
+def test_tiles_local_ranks_p8_agrees_with_p1(mcg):
+    """Config-5 rehearsal on the scrambled matrix: 8 LocalComm ranks (all-gather layout, tiles on
+    every rank) vs 1 rank over 12 fixed iterations agree to <= 1e-13."""
+    spec = mcg.make_problem("randspd", rows=80000, band=32, density=0.5, scramble=1)
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sell", recurrence=1)
+    o.tile_seg_log2 = 13
+    one = C.run_local_ranks(spec.native(), o, 1, 12, True)
+    eight = C.run_local_ranks(spec.native(), o, 8, 12, True)
+    r1, r8 = one["ranks"][0]["rnorm"], eight["ranks"][0]["rnorm"]
+    assert abs(r1 - r8) <= 1e-13 * r1
+    np.testing.assert_allclose(eight["x"], one["x"], rtol=1e-13, atol=1e-15 * np.abs(one["x"]).max())
+    assert all(abs(r["true_rnorm"] - r8) <= 1e-9 * r8 for r in eight["ranks"])

@@ -79,12 +79,15 @@ def test_native_cli_threads_match_cpu(mcg, world, problem, mode):
 @pytest.mark.parametrize("world", WORLDS)
 @pytest.mark.parametrize("args", [["--problem", "poisson2d", "--n", "128"], ["--problem", "poisson3d", "--n", "64"]])
 @pytest.mark.parametrize("mode", [[], ["--no-graph"]])
-def test_native_cli_threads_carry_paths_match_cpu(mcg, world, args, mode):
+@pytest.mark.parametrize("comm", ["dual", "single"])
+def test_native_cli_threads_carry_paths_match_cpu(mcg, world, args, mode, comm):
     """The default stencil path at P > 1 over real RCCL: dia4 line / plane carry in the three-term
-    form, halo ahead of the pass (r, Ap, p of the ghost lines), graphs with the collectives."""
+    form, halo ahead of the pass (r, Ap, p of the ghost lines), graphs with the collectives; with
+    two communicators (halo on the side stream) and with one (every collective on the compute
+    stream, in one order)."""
     x_cpu, rep_cpu = _cpu_x(mcg, args)
     p = _run([mcg.cli_path(), "--gpus", str(world), "--print-x", "yes", "--report", "json", "--verify",
-              "--watchdog", "120"] + mode + args)
+              "--watchdog", "120", "--comm", comm] + mode + args)
     assert p.returncode == 0, p.stdout + p.stderr
     lines = p.stdout.splitlines()
     rep = json.loads(lines[-2])
@@ -97,12 +100,15 @@ def test_native_cli_threads_carry_paths_match_cpu(mcg, world, args, mode):
 
 @needs2
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("problem", ["poisson2d", "randspd_wide"])
-def test_bench_launcher_processes(world, problem):
+@pytest.mark.parametrize("problem", ["poisson2d", "randspd_wide", "randspd_scrambled"])
+@pytest.mark.parametrize("comm", ["dual", "single"])
+def test_bench_launcher_processes(world, problem, comm):
     """bench.py --gpus P starts P processes; all ranks agree and the true residual matches."""
     extra = (["--grid", "512"] if problem == "poisson2d"
-             else ["--problem", "randspd", "--rows", "200000", "--band", "64", "--density", "0.5"])
-    p = _run([sys.executable, "bench.py", "--gpus", str(world), "--steps", "40", "--warmup", "5"] + extra)
+             else ["--problem", "randspd", "--rows", "200000", "--band", "64", "--density", "0.5"]
+             + (["--scramble", "1"] if problem == "randspd_scrambled" else []))
+    p = _run([sys.executable, "bench.py", "--gpus", str(world), "--steps", "40", "--warmup", "5", "--comm", comm]
+             + extra)
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == world and line["check"]["comm_world"] == world
@@ -159,6 +165,58 @@ def test_single_gpu_pool_skips_cleanly():
 def _one_rank_comm(mcg):
     C = mcg.native()
     return C.Comm(0, 1, C.unique_id(), C.unique_id())
+
+
+def test_cli_and_extension_share_one_rccl(mcg):
+    """Both entry points run the same RCCL: the native CLI (thread per GPU) links the copies torch
+    ships through build/rt, and the Python extension binds to them because torch is imported first.
+    Same ncclGetVersion, same shared object."""
+    info = mcg.native().rccl_info()
+    assert info["version"] >= 22600, info
+    p = _run([mcg.cli_path(), "--problem", "poisson2d", "--n", "32", "--force-comm", "--report", "json"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    rep = json.loads(p.stdout.splitlines()[-2])
+    assert rep["rccl_version"] == info["version"], (rep, info)
+    assert os.path.realpath(rep["rccl_library"]) == os.path.realpath(info["library"]), (rep, info)
+
+
+@pytest.mark.parametrize("route", ["spawn", "torchrun"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_multiprocess_rehearsal_on_one_gpu(route, world):
+    """The P-rank bench's host side on ONE GPU, every round: P processes (bench.py's own launcher,
+    or torchrun) on device 0 with collectives that move nothing, but the real gloo rendezvous,
+    barriers, all_gather_object aggregation and slowest-rank JSON line of the scaling runs."""
+    args = ["bench.py", "--gpus", str(world), "--rehearse-ranks", "--grid", "1024", "--steps", "10", "--warmup", "2",
+            "--phases", "0", "--watchdog", "60"]
+    if route == "spawn":
+        cmd = [sys.executable] + args
+    else:
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    p = _run(cmd, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["check"]["ok"] and line["steps"] == 10
+    assert line["config"]["launch"] == route and line["config"]["parallelism"] == f"rehearse-rowpart{world}-one-gpu"
+    assert line["check"]["device_iterations"] == 12 and line["check"]["rccl"]["version"] > 0
+
+
+@pytest.mark.parametrize("mode", ["dual", "single"])
+def test_one_rank_comm_modes_bitwise_equal_to_no_comm(mcg, mode):
+    """The 1-rank RCCL communicator in both modes (two communicators, or one with every collective
+    in one stream order) leaves the solve bitwise equal to the communicator-free one."""
+    spec = mcg.make_problem("poisson2d", n=128, rhs="random")
+    ref = mcg.CGSolver(spec, format="sellc8", recurrence=1).solve()
+    s = mcg.CGSolver(spec, format="sellc8", recurrence=1, force_comm=True, comm_mode=mode)
+    assert s.comm.serialized == (mode == "single")
+    out = s.solve()
+    assert out["iterations"] == ref["iterations"] and out["rnorm"] == ref["rnorm"]
+    np.testing.assert_array_equal(out["x_local"], ref["x_local"])
 
 
 @pytest.mark.parametrize("graph", [False, True])

@@ -101,3 +101,25 @@ def test_bench_aggregate_takes_slowest_rank():
     ranks[1]["iterations"] = 30
     ranks[0]["ok"] = False
     assert not bench.aggregate(100, ranks)[2]
+
+
+def test_kfd_gpu_count_from_a_fake_topology(tmp_path):
+    """The launcher counts GPUs without HIP: KFD topology nodes with a nonzero gfx_target_version
+    whose render node this process can open (a container sees the host's topology, not its cards)."""
+    from cuda_mpi_parallel_amd.parallel import launch
+
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    nodes.mkdir()
+    dri.mkdir()
+    specs = [(0, None), (90500, 128), (90500, 136), (90500, 144)]  # a CPU node and three GPUs
+    for i, (gfx, minor) in enumerate(specs):
+        d = nodes / str(i)
+        d.mkdir()
+        text = f"cpu_cores_count 8\ngfx_target_version {gfx}\n"
+        if minor is not None:
+            text += f"drm_render_minor {minor}\n"
+        (d / "properties").write_text(text)
+    for minor in (128, 144):  # only two of the three render nodes are in this "container"
+        (dri / f"renderD{minor}").write_text("")
+    assert launch.kfd_gpu_count(str(nodes), str(dri)) == 2
+    assert launch.kfd_gpu_count(str(tmp_path / "missing"), str(dri)) is None
