@@ -81,7 +81,7 @@ def parse_args(argv=None):
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="SpMV grid; 0 = auto")
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
-                    help="experiment: set a native CgOptions field (e.g. xcd_map=1, spmv_param=6)")
+                    help="experiment: set a native CgOptions field (e.g. tile_pace=2, placement_tries=1)")
     ap.add_argument("--phases", type=int, default=10,
                     help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
@@ -283,9 +283,8 @@ def _run_rank(args, out_fd) -> int:
                 "seq_len": spec.n_rows,
                 "parallelism": (f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else
                                 f"rehearse-rowpart{n_gpus}-one-gpu" if rehearse else f"rowpart{n_gpus}"),
-                # storage the timed pass streams: the 2-D line-carry pass reads 4-bit codes (c4)
-                "format": ("sell64-dia4" if info.get("dia4") else "sell64-c4" if info.get("codes4")
-                           else info["format"]),
+                # storage the timed pass streams (the carries read SELL-64/dia4 codes)
+                "format": "sell64-dia4" if info.get("dia4") else info["format"],
                 "recurrence": info["recurrence"],
                 "pass": pass_label(info, args.problem),
                 **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")

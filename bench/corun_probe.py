@@ -13,6 +13,13 @@ and a small elementwise torch kernel, timed on a high-priority stream
 If (b) takes about as long as (a), the collective overlaps the pass; if it takes about a pass
 (~3 ms), it waited for the pass to drain.
 
+Controls (r3): `spin_fat` = one 256-thread workgroup spinning 20 us with ~270
+VGPRs per wave live (RCCL's kernels' footprint) and no RCCL; `spin_thin` = the same with a few
+VGPRs.  If spin_fat waits like RCCL and spin_thin does not, the register file is the blocker; if
+spin_fat starts at once, something RCCL-specific is (its queue / the loopback path).  Run under
+`rocprofv3 --kernel-trace` the dispatches' queue ids and start / end stamps show which queue each
+kernel used and when it started relative to the pass (bench/corun_trace.py).
+
   python bench/corun_probe.py [--grid 16384] [--set carry_blocks_per_cu=3 ...]
 """
 from __future__ import annotations
@@ -58,6 +65,7 @@ def main() -> int:
     src = torch.rand(n, dtype=torch.float64, device="cuda")
     dst = torch.zeros_like(src)
     side = torch.cuda.Stream(priority=-1)
+    spin_out = torch.zeros(64, dtype=torch.float64, device="cuda")
 
     # the same send/recv captured into a graph on the side stream (how the halo runs at P > 1):
     # separates a host-side wait inside the RCCL call from a device-side wait for CUs
@@ -76,6 +84,8 @@ def main() -> int:
                 comm.sendrecv_ptr(src.data_ptr(), 0, dst.data_ptr(), 0, n, side.cuda_stream)
             elif kind == "rccl_graph":
                 g.replay()
+            elif kind in ("spin_fat", "spin_thin"):
+                C.kernels.spin(spin_out.data_ptr(), 20.0, kind == "spin_fat", 1, side.cuda_stream)
             else:
                 torch.add(src, 1.0, out=dst)
             host_us.setdefault(kind, []).append(round((time.perf_counter() - h0) * 1e6, 1))
@@ -89,7 +99,7 @@ def main() -> int:
     pass_ms = (time.perf_counter() - t0) * 1e3 / 16
 
     out = {"grid": a.grid, "pass_ms": round(pass_ms, 3), "info": {k: s.info[k] for k in ("carry", "format")}}
-    for kind in ("rccl", "rccl_graph", "torch_add"):
+    for kind in ("rccl", "rccl_graph", "torch_add", "spin_fat", "spin_thin"):
         alone, busy = [], []
         for _ in range(a.reps):
             torch.cuda.synchronize()

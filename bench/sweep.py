@@ -53,16 +53,12 @@ def main():
         for cs in args.cfg:
             c = parse_cfg(cs)
             o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, use_graph=bool(c["g"]), format=c["format"],
-                            blocks_per_cu=c["b"], spmv_variant=c["v"], spmv_param=c["p"], update_unroll=c["u"], nt_loads=c["n"], xcd_map=c["x"], sell_slices=c["s"], recurrence=c["r"])
-            o.update_blocks_per_cu = c.get("B", 0)
-            o.interleave = c["i"]
-            o.window = c["w"]
-            o.pipeline = c["P"]
-            o.strip = c["S"]
-            o.carry = c["c"]
-            o.carry_blocks_per_cu = c["k"]
-            o.carry_depth = c["d"]
-            o.carry_nt = c["T"]
+                            blocks_per_cu=c["b"], spmv_variant=c["v"], recurrence=c["r"])
+            # fields of earlier experiments (strip, carry_depth, carry_nt, ...) were removed in r3
+            for key, field in (("B", "update_blocks_per_cu"), ("i", "interleave"), ("w", "window"), ("P", "pipeline"),
+                               ("c", "carry")):
+                if key in c and hasattr(o, field):
+                    setattr(o, field, c[key])
             s = C.Solver(spec.native(), o, 0, 1, None)
             s.setup()
             s.reset()

@@ -15,8 +15,8 @@
 //   --nnz-per-row m (random-spd: density = (m - 1) / (2 band))
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
 //   --comm dual|single (two RCCL communicators, halo on a side stream | one, one stream order)
-//   --spmv-variant 0|1|2|3|4  --spmv-param U|G  --update-unroll 1|2|4  --nt-loads 0|1
-//   --xcd-map 0|1  --sell-slices 1|2  --recurrence two|single  --interleave auto|on|off  --window auto|on|off
+//   --spmv-variant 0|1|2|3|4
+//   --recurrence two|single  --interleave auto|on|off  --window auto|on|off
 //   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
 //   --fused-reduce auto|on|off  --watchdog SECONDS
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
@@ -136,11 +136,6 @@ Args parse(int argc, char** argv) {
     }
     else if (f == "--blocks-per-cu") a.opt.blocks_per_cu = std::stoi(need(i));
     else if (f == "--spmv-variant") a.opt.spmv_variant = std::stoi(need(i));
-    else if (f == "--spmv-param") a.opt.spmv_param = std::stoi(need(i));
-    else if (f == "--update-unroll") a.opt.update_unroll = std::stoi(need(i));
-    else if (f == "--nt-loads") a.opt.nt_loads = std::stoi(need(i));
-    else if (f == "--xcd-map") a.opt.xcd_map = std::stoi(need(i));
-    else if (f == "--sell-slices") a.opt.sell_slices = std::stoi(need(i));
     else if (f == "--checkpoint") a.opt.checkpoint_path = need(i);
     else if (f == "--checkpoint-every") a.opt.checkpoint_every = std::stoi(need(i));
     else if (f == "--resume") a.resume = need(i);

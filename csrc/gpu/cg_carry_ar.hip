@@ -63,17 +63,10 @@ __device__ __forceinline__ void ar_load_codes(const SellDev& S, int64_t base, in
   c.w = w;
 #pragma unroll
   for (int q = 0; q < (U * CB + 31) / 32; ++q) c.pk[q] = 0u;
-  if constexpr (CM == 2) {
-    const uint8_t* __restrict__ cp = S.codes + base;
+  static_assert(CM == 2, "per-entry codes: SELL-64/c8");
+  const uint8_t* __restrict__ cp = S.codes + base;
 #pragma unroll
-    for (int u = 0; u < U; ++u) c.pk[(u * CB) >> 5] |= (uint32_t)cp[64 * u + lane] << ((u * CB) & 31);
-  } else {
-    const uint8_t* __restrict__ cp = S.codes4 + (base >> 1);
-    const int sh = (lane & 1) * 4;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      c.pk[(u * CB) >> 5] |= (((uint32_t)cp[32 * u + (lane >> 1)] >> sh) & 15u) << ((u * CB) & 31);
-  }
+  for (int u = 0; u < U; ++u) c.pk[(u * CB) >> 5] |= (uint32_t)cp[64 * u + lane] << ((u * CB) & 31);
 }
 
 // SELL-64/dia4: the U value indices of slice row `lane` (slot u at bit 4 u); sp = the slice's 32 U bytes
@@ -117,7 +110,7 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
 }
 
 template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1>
-__global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+__global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
   __shared__ double2 s_dict[CM == 4 ? 1 : 256];
@@ -164,7 +157,7 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
   const int64_t runs = nw > SS ? nw / SS : 1;
   const int64_t chunk = (nl + runs - 1) / runs;
   const int32_t ext32 = (int32_t)v.ext_len;
-  const bool ntl = v.nt_loads != 0;
+  constexpr bool ntl = false;  // plain loads (non-temporal measured slower: 281 vs 302 it/s 2-D)
   const double* __restrict__ eo = v.ape_old;
   const uint32_t* __restrict__ meta = S.smeta;
   // a zero the compiler cannot see through: wave-uniform metadata loads stay vector loads (vmcnt,
@@ -409,7 +402,7 @@ __global__ __launch_bounds__(kBS, (P3 && !PAIR && UN == 5) ? 5 : 4) void k_cg_ca
     };
     // P3 even passes: unrolled by 3, the period of the codes / p_k chains (the odd pass, with x, then
     // spills; it runs at the HBM rate rolled)
-    constexpr int kUn = (P3 && !PAIR && UN != 5) ? UN : 1;  // UN == 5: rolled, 5 waves per SIMD
+    constexpr int kUn = (P3 && !PAIR) ? UN : 1;
     int32_t m = 0;
     if constexpr (kUn > 1) {
       for (; m + kUn <= n_run; m += kUn) {
@@ -513,7 +506,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
   const int64_t runs = nb > jpr ? nb / jpr : 1;
   const int64_t chunk = (nl + runs - 1) / runs;
   const int32_t ext32 = (int32_t)v.ext_len;
-  const bool ntl = v.nt_loads != 0;
+  constexpr bool ntl = false;  // plain loads (non-temporal measured slower: 281 vs 302 it/s 2-D)
   const bool odn = wv == 0, oup = wv == KW - 1;  // outer waves: the line below / above the block
   const int32_t fo = odn ? -LN : LN;
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
@@ -896,9 +889,8 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
-  MCG_CHECK((cm == 2 || cm == 3 || cm == 4) && param >= 4 && param <= 5 && S.dict != nullptr,
+  MCG_CHECK((cm == 2 || cm == 4) && param >= 4 && param <= 5 && S.dict != nullptr,
             "Ap-recomputing carry: SELL-64/c8, /c4 or /dia4 rows of at most 5 entries");
-  MCG_CHECK(cm != 3 || S.codes4 != nullptr, "Ap-recomputing carry: 4-bit codes missing");
   MCG_CHECK(cm != 4 || (S.dia4 != nullptr && S.dvals != nullptr), "Ap-recomputing carry: dia4 codes missing");
   MCG_CHECK(final_mode || cm == 4 || S.smeta != nullptr, "Ap-recomputing carry: slice metadata missing");
   MCG_CHECK(v.ape_old != nullptr && v.ape_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
@@ -914,14 +906,13 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, \
                      (int32_t)(tr.strip * 64), 0, partials, pstride, st, tol, first, check, k, p3)
     if (cm == 4) MCG_AF(4, 5);
-    else if (cm == 3) { if (param == 4) MCG_AF(3, 4); else MCG_AF(3, 5); }
     else { if (param == 4) MCG_AF(2, 4); else MCG_AF(2, 5); }
 #undef MCG_AF
     MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
     return;
   }
   const bool pair = (k & 1) != 0;
-  const int qd = depth <= 2 ? 2 : (depth >= 5 ? 5 : depth);
+  const int qd = depth <= 2 ? 2 : 3;  // operand prefetch depth in lines (solver: 2 or 3)
 #define MCG_A(CM, U, QD, PAIR, P3, ...)                                                                 \
   hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR, P3, ##__VA_ARGS__>), dim3(grid), dim3(kBS), 0, stream, S, v, \
                      own_off, tr, partials, pstride, st, tol, first, check, rc)
@@ -930,7 +921,6 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     if constexpr (CM == 4) {                                     \
       if (p3k) {                                                 \
         if (pair) MCG_A(CM, U, QD, true, true);                  \
-        else if (unroll == 5) MCG_A(CM, U, QD, false, true, 5);  \
         else if (unroll > 1) MCG_A(CM, U, QD, false, true, 3);   \
         else MCG_A(CM, U, QD, false, true);                      \
         break;                                                   \
@@ -942,12 +932,9 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
 #define MCG_AQ(CM, U)                         \
   do {                                        \
     if (qd == 2) MCG_AP(CM, U, 2);            \
-    else if (qd == 3) MCG_AP(CM, U, 3);       \
-    else if (qd == 4) MCG_AP(CM, U, 4);       \
-    else MCG_AP(CM, U, 5);                    \
+    else MCG_AP(CM, U, 3);                    \
   } while (0)
   if (cm == 4) MCG_AQ(4, 5);
-  else if (cm == 3) { if (param == 4) MCG_AQ(3, 4); else MCG_AQ(3, 5); }
   else { if (param == 4) MCG_AQ(2, 4); else MCG_AQ(2, 5); }
 #undef MCG_AQ
 #undef MCG_AP

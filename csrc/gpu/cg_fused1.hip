@@ -116,8 +116,7 @@ __global__ __launch_bounds__(kBS) void k_cg_f1(CsrDev<IdxT> A, SellDev S, F1Vect
   if constexpr (FMT == 0) eng::csr_adaptive<IdxT, U, 16>(A, tr, gather, epi);  // = csr_direct on short-row tiles
   else if constexpr (FMT == 1) eng::sell<U, false, 0>(S, tr, gather, epi);
   else if constexpr (FMT == 3) eng::sell<U, false, 1>(S, tr, gather, epi);
-  else if constexpr (FMT == 4) eng::sell<U, false, 2>(S, tr, gather, epi);
-  else eng::sell2<U, false>(S, tr, gather, epi);
+  else eng::sell<U, false, 2>(S, tr, gather, epi);
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
@@ -384,7 +383,7 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
   // are saddr + voffset forms and the per-step scalar work is a few adds.  Loads are never
   // conditional: line indices are clamped to lines that exist (values past the run are unused).
   const int32_t ext32 = (int32_t)v.ext_len;
-  const bool ntl = v.nt_loads != 0;
+  constexpr bool ntl = false;  // plain loads (non-temporal measured slower: 281 vs 302 it/s 2-D)
   for (int64_t job = M2 == 2 ? lb : gw; job < njobs; job += M2 == 2 ? nb : nw) {
     int64_t col, l0;
     if constexpr (M2 == 2) {
@@ -440,15 +439,6 @@ __global__ __launch_bounds__(kBS, M2 ? 4 : 1) void k_cg_f1_carry(SellDev S, F1Ve
         for (int q = 0; q < (U + 3) / 4; ++q) c.pk[q] = 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u) c.pk[u >> 2] |= (uint32_t)cp[64 * u + lane] << (8 * (u & 3));
-      } else if constexpr (CM == 3) {
-        // 4-bit codes (SellDev::codes4): lanes 2i, 2i+1 share a byte, 32 bytes per slice entry
-        const uint8_t* __restrict__ cp = S.codes4 + (base >> 1);
-        const int sh = (lane & 1) * 4;
-#pragma unroll
-        for (int q = 0; q < (U + 3) / 4; ++q) c.pk[q] = 0u;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          c.pk[u >> 2] |= (((uint32_t)cp[32 * u + (lane >> 1)] >> sh) & 15u) << (8 * (u & 3));
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -881,12 +871,11 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, bo
                      const RedCtl& rc) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0, "line-carry pass needs whole grid lines");
-  MCG_CHECK(v.ra_old != nullptr && cm >= 1 && cm <= 3 && param >= 4 && param <= 8,
-            "line-carry pass needs SELL-64 d16/c8/c4 with interleaved pairs");
-  MCG_CHECK(depth >= 1 && depth <= 3, "line-carry prefetch depth must be 1..3");
+  MCG_CHECK(v.ra_old != nullptr && cm >= 1 && cm <= 2 && param >= 4 && param <= 8,
+            "line-carry pass needs SELL-64 d16/c8 with interleaved pairs");
+  MCG_CHECK(depth == 1 || depth == 3, "line-carry prefetch depth must be 1 (3-D) or 3 (2-D)");
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
   MCG_CHECK(general || cm >= 2, "the specialised line-carry pass needs the c8 dictionary");
-  MCG_CHECK(cm != 3 || (!general && lo2 == 0 && S.codes4 != nullptr), "4-bit codes: specialised 2-D pass only");
   MCG_CHECK(lo2 == 0 || (cm == 2 && !general && lo2 > 1), "the +-LO2 carry needs the specialised c8 pass");
   MCG_CHECK(!block_exchange || carry_block_exchange_ok(param, lo2, tr.strip),
             "plane-carry block exchange needs +-LO2 whole slices, kWaves | grid lines per plane, 7-8 entries per row");
@@ -902,7 +891,6 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, bo
 #define MCG_CD(CM, U, GEN, M2)                         \
   do {                                                 \
     if (depth == 1) MCG_CP(CM, U, 1, GEN, M2);         \
-    else if (depth == 2) MCG_CP(CM, U, 2, GEN, M2);    \
     else MCG_CP(CM, U, 3, GEN, M2);                    \
   } while (0)
 #define MCG_CU(CM, GEN, M2)                       \
@@ -913,9 +901,7 @@ void cg_fused1_carry(int cm, int param, int depth, bool general, int32_t lo2, bo
     else if (param == 7) MCG_CD(CM, 7, GEN, M2);  \
     else MCG_CD(CM, 8, GEN, M2);                  \
   } while (0)
-  if (cm == 3) {
-    MCG_CU(3, false, 0);
-  } else if (cm == 2) {
+  if (cm == 2) {
     if (general) MCG_CU(2, true, 0);
     else if (lo2 > 0 && block_exchange) {
       if (param == 7) MCG_CD(2, 7, false, 2);
@@ -980,7 +966,6 @@ void cg_fused1(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, cons
   }
   if (fmt == 0) MCG_F1U(0, false);
   else if (fmt == 1) { if (ra) MCG_F1U(1, true); else MCG_F1U(1, false); }
-  else if (fmt == 2) MCG_F1U(2, false);
   else if (fmt == 3) { if (ra) MCG_F1U(3, true); else MCG_F1U(3, false); }
   else { if (ra) MCG_F1U(4, true); else MCG_F1U(4, false); }
 #undef MCG_F1U

@@ -118,8 +118,8 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused(CsrDev<IdxT> A, const dou
 }
 
 // K_A: fused SpMV (SELL-64: one wave per 64-row slice, column-major entries).
-// S = 2: two slices in flight per wave; CM: column mode of eng::sell (0 int32, 1 d16, 2 c8).
-template <int U, int S, int CM>
+// CM: column mode of eng::sell (0 int32, 1 d16, 2 c8).
+template <int U, int CM>
 __global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const double* __restrict__ r,
                                                             const double* __restrict__ pold,
                                                             double* __restrict__ pnew, double* __restrict__ x,
@@ -151,8 +151,7 @@ __global__ __launch_bounds__(kBS) void k_cg_spmv_fused_sell(SellDev A, const dou
     x[i] = fma(alpha, po, x[i]);
     acc = fma(pi, sum, acc);
   };
-  if constexpr (S == 2) eng::sell2<U, false>(A, sr, gather, epi);
-  else eng::sell<U, false, CM>(A, sr, gather, epi);
+  eng::sell<U, false, CM>(A, sr, gather, epi);
   block_partial<kBS>(acc, s_red, partials + blockIdx.x);
 }
 
@@ -396,16 +395,13 @@ void cg_spmv_fused_sell(const SellDev& A, const double* r_ext, const double* pol
 #define MCG_SELL(U)                                                                                     \
   do {                                                                                                  \
     if (flags & 8)                                                                                      \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, 2>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 2>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,          \
                          pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
     else if (flags & 4)                                                                                 \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, 1>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
-                         pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
-    else if (flags & 2)                                                                                 \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 2, 0>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,          \
                          pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
     else                                                                                                \
-      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 1, 0>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,       \
+      hipLaunchKernelGGL((k_cg_spmv_fused_sell<U, 0>), dim3(grid), dim3(kBS), 0, stream, A, r_ext,          \
                          pold_ext, pnew_ext, x, Ap, own_off, slices, partials, st, tol, first, final_mode); \
   } while (0)
   if (param <= 4) MCG_SELL(4);

@@ -45,14 +45,15 @@ constexpr uint32_t kColMask = (1u << 22) - 1;
 // `live` (LDS, per workgroup): cleared after the first wait that times out -- the group is not
 // co-resident (another kernel holds CUs, or several ranks share the GPU), so this workgroup stops
 // waiting for the rest of the launch instead of paying the cap at every segment
-__device__ __forceinline__ void pace_step(unsigned* pace, int step, int* live) {
+__device__ __forceinline__ void pace_step(unsigned* pace, int step, int* live, int slack8) {
   __syncthreads();
   if (threadIdx.x == 0 && pace != nullptr && *live) {
     const int grp = blockIdx.x & 7;
     const unsigned nwg = (gridDim.x - grp + 7) >> 3;
     unsigned* c = pace + grp * 64;  // one 256-B block per group
     __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = (unsigned)(step + 1) * nwg;
+    // every workgroup of the group has finished segment `step` (slack8 > 0: all but slack8 / 8 of them)
+    const unsigned target = (unsigned)(step + 1) * nwg - (unsigned)((nwg * (unsigned)slack8) >> 3);
     int spin = 0;
     for (; spin < kPaceSpins; ++spin) {
       if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
@@ -61,6 +62,16 @@ __device__ __forceinline__ void pace_step(unsigned* pace, int step, int* live) {
     if (spin == kPaceSpins) *live = 0;
   }
   __syncthreads();
+}
+
+// one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
+__device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
+#pragma unroll
+  for (int u = 0; u < kTU; ++u) {
+    const int64_t e = k + u * 64;
+    q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
+    v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
+  }
 }
 
 // MODE 0: the split pass's SpMV (Ap_k = A p_k + the 4 partials + in-kernel reduction, as
@@ -91,28 +102,23 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
     const int64_t b = wave + rd * nwaves;
     const bool active = b < T.nblocks;
     for (int rr = lane; rr < kTileB; rr += 64) a[rr] = 0.0;
+    // the block's tiles are contiguous: tile g = [tptr[b G + g], tptr[b G + g + 1])
+    int64_t lo = 0, hi = 0;
+    uint32_t q[kTU];
+    double v[kTU];
+    if (active) {
+      lo = T.tptr[b * G];
+      hi = T.tptr[b * G + 1];
+      tile_batch_load(T, lo + lane, hi, q, v);
+    }
     for (int g = 0; g < G; ++g, ++step) {
+      int64_t hi_next = hi;
       if (active) {
-        const int64_t lo = T.tptr[b * G + g], hi = T.tptr[b * G + g + 1];
         const double* __restrict__ pg = p + ((int64_t)g << T.seg_shift);
-        uint32_t q[kTU];
-        double v[kTU];
-        int64_t k = lo + lane;
-#pragma unroll
-        for (int u = 0; u < kTU; ++u) {
-          const int64_t e = k + u * 64;
-          q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
-          v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
-        }
-        for (; k < hi; k += kTU * 64) {
+        for (int64_t k = lo + lane; k < hi; k += kTU * 64) {
           uint32_t qn[kTU];
           double vn[kTU], x[kTU];
-#pragma unroll
-          for (int u = 0; u < kTU; ++u) {  // next batch in flight during this one's gathers
-            const int64_t e = k + (kTU + u) * 64;
-            qn[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
-            vn[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
-          }
+          tile_batch_load(T, k + kTU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
 #pragma unroll
           for (int u = 0; u < kTU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
 #pragma unroll
@@ -124,8 +130,15 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
             v[u] = vn[u];
           }
         }
+        // the next tile's first batch loads while the workgroup waits at the pacing step
+        if (g + 1 < G) {
+          hi_next = T.tptr[b * G + g + 2];
+          tile_batch_load(T, hi + lane, hi_next, q, v);
+        }
       }
-      pace_step(T.pace, step, &live);
+      pace_step(T.pace, step, &live, T.pace_slack8);
+      lo = hi;
+      hi = hi_next;
     }
     if (active) {
       const int64_t r0 = b * kTileB;

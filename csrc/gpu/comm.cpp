@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include "mcg/check.hpp"
+#include "mcg/kernels.hpp"
 
 namespace mcg {
 
@@ -101,6 +102,14 @@ void Comm::sendrecv(const double* send, int to, double* recv, int from, size_t n
 void Comm::allgather_inplace(double* buf, size_t block, hipStream_t stream) {
   MCG_RCCL(ncclAllGather(buf + (size_t)rank_ * block, buf, block, ncclFloat64, halo_, stream),
            "RCCL allgather failed");
+}
+
+void DelayComm::allreduce_sum(double*, size_t, hipStream_t stream) {
+  if (ar_us_ > 0) kern::spin(nullptr, ar_us_, false, 1, stream);
+}
+
+void DelayComm::halo_exchange(const LocalLayout& L, double* const*, int, hipStream_t stream, const int*) {
+  if (halo_us_ > 0 && L.has_halo()) kern::spin(nullptr, halo_us_, false, 1, stream);
 }
 
 int Comm::count() const {

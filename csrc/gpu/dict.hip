@@ -126,12 +126,6 @@ __global__ __launch_bounds__(kBlock) void k_sell_to_c8(SellDev S, const double2*
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_c8_to_c4(const uint8_t* __restrict__ c8, int64_t half,
-                                                      uint8_t* __restrict__ c4) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < half; i += stride)
-    c4[i] = (uint8_t)((c8[2 * i] & 15) | ((c8[2 * i + 1] & 15) << 4));
-}
 
 int dict_grid(int64_t n) {
   int64_t g = (n + kBlock - 1) / kBlock;
@@ -141,12 +135,6 @@ int dict_grid(int64_t n) {
 
 }  // namespace
 
-void sell_c8_to_c4(const uint8_t* codes, int64_t total, uint8_t* codes4, hipStream_t st) {
-  MCG_CHECK(total % 2 == 0, "c4 codes: odd entry count");
-  if (total <= 0) return;
-  hipLaunchKernelGGL(k_c8_to_c4, dim3(dict_grid(total / 2)), dim3(kBlock), 0, st, codes, total / 2, codes4);
-  MCG_HIP(hipGetLastError(), "kernel launch failed(c8_to_c4)");
-}
 
 bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st) {
   DictScratch* d = nullptr;

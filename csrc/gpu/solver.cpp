@@ -95,7 +95,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   // SELL, where its interleaved {r, Ap} gathers make it the faster pass (profiles/sweep_ra_*)
   if (opt_.recurrence < 0) opt_.recurrence = (world_ > 1 || opt_.format == 1) ? 1 : 0;
   {
-    const bool ra_ok = opt_.recurrence == 1 && opt_.format == 1 && opt_.sell_slices != 2;
+    const bool ra_ok = opt_.recurrence == 1 && opt_.format == 1;
     if (opt_.interleave < 0) opt_.interleave = ra_ok ? 1 : 0;
     MCG_CHECK(!opt_.interleave || ra_ok, "interleaved r/Ap layout needs the single-reduction recurrence on SELL");
   }
@@ -109,25 +109,8 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only (and not for
   // the split pass, whose ghosts come from its own update kernel; decided in setup())
   prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph && !L_.allgather;
-  // Compute stream, optionally on a CU-masked queue that keeps a few CUs free for the side stream's
-  // RCCL kernels.  Measured: the mask slows the pass by 20-33 % and the collective still waits for
-  // the pass (bench/corun_probe.py, profiles/r2_corun_probe.md), so it is off unless asked for.
-  const int all_cus = kern::num_cus();
-  info_.comm_cus = std::max(0, opt_.comm_cus);
-  MCG_CHECK(info_.comm_cus >= 0 && info_.comm_cus < all_cus / 2, "comm_cus must leave at least half the CUs");
-  ncu_ = all_cus - info_.comm_cus;
-  if (info_.comm_cus > 0) {
-    std::vector<uint32_t> mask((all_cus + 31) / 32, 0u);
-    for (int c = 0; c < all_cus; ++c) mask[c / 32] |= 1u << (c % 32);
-    const int w = info_.comm_cus, grp = all_cus / w;
-    for (int j = 0; j < w; ++j) {
-      const int c = opt_.cu_mask_pattern == 1 ? all_cus - 1 - j : j * grp + grp - 1;
-      mask[c / 32] &= ~(1u << (c % 32));
-    }
-    s0_ = Stream::with_cu_mask(mask);
-  } else {
-    s0_ = Stream(true, 0);
-  }
+  ncu_ = kern::num_cus();
+  s0_ = Stream(true, 0);
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);
   ev_h_ = Event(true);
@@ -243,12 +226,9 @@ void GpuCgSolver::setup() {
   // CSR engine: thread per row when every row is short; else row-length-adaptive per 256-row tile
   // (eng::csr_adaptive: thread per row or 16 lanes per row, by one block vote per tile)
   info_.spmv_variant = opt_.spmv_variant >= 0 ? opt_.spmv_variant : (info_.max_row_len > 16 ? 4 : 1);
-  info_.spmv_param = opt_.spmv_param > 0 ? opt_.spmv_param
-                                         : kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
+  info_.spmv_param = kern::spmv_param_for(info_.spmv_variant, info_.max_row_len);
   // SELL: one batch = the slice width when it is 4..8 (no clamped duplicate gathers)
-  if (opt_.format == 1 && opt_.spmv_param <= 0)
-    info_.spmv_param = (int)std::max<int64_t>(4, std::min<int64_t>(8, info_.max_row_len));
-  if (opt_.nt_loads && info_.spmv_variant == 1) info_.spmv_variant = 3;
+  if (opt_.format == 1) info_.spmv_param = (int)std::max<int64_t>(4, std::min<int64_t>(8, info_.max_row_len));
   info_.nnz_local = nnz;
   info_.idx64 = nnz >= ((int64_t)1 << 31) - 64 || opt_.force_idx64;
 
@@ -362,18 +342,12 @@ void GpuCgSolver::setup() {
         cols_.release();
         dcols_.release();
         vals_.release();
-        if (ndict_ <= 16 && opt_.carry != 0 && opt_.carry_c4 != 0 && opt_.recurrence == 1 && opt_.interleave != 0) {
-          // 4-bit codes for the line-carry pass (half the c8 stream; the generic passes keep c8)
-          codes4_.allocate(total / 2, "A", 256);
-          kern::sell_c8_to_c4(codes_.get(), total, codes4_.get(), s0_);
-          MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
-        }
         info_.format = 3;
         matrix_bytes = total + (ns + 1) * 8;
       }
     }
     info_.sell_fill = nnz > 0 ? (double)total / (double)nnz : 1.0;
-    if (!c8_ && !perm_.get() && !aligned_ && opt_.recurrence == 1 && opt_.window != 0 && opt_.sell_slices != 2 &&
+    if (!c8_ && !perm_.get() && !aligned_ && opt_.recurrence == 1 && opt_.window != 0 &&
         n > 0) {
       // windowed pass: per-chunk column windows of the generated matrix
       const int64_t nch = (n + kern::kWinRows - 1) / kern::kWinRows;
@@ -461,7 +435,7 @@ void GpuCgSolver::setup() {
   const int bpc = opt_.blocks_per_cu > 0 ? opt_.blocks_per_cu : (opt_.format == 1 ? 48 : 8);
   info_.window = win_doubles_;
   pipe_ = opt_.pipeline != 0 && opt_.format == 1 && (d16_ || c8_) && opt_.interleave == 1 &&
-          opt_.sell_slices != 2 && info_.max_row_len <= 8 && info_.spmv_param >= info_.max_row_len;
+          info_.max_row_len <= 8 && info_.spmv_param >= info_.max_row_len;
   MCG_CHECK(opt_.pipeline != 1 || pipe_, "pipelined pass needs SELL d16/c8, interleave and rows <= param <= 8");
   info_.pipeline = pipe_;
   auto grid_a = [&](const TileRanges& t) {
@@ -507,9 +481,8 @@ void GpuCgSolver::setup() {
     g_int_ = 0;
     g_bnd_ = g_all_;
   }
-  if (opt_.xcd_map > 0) tr_all_.xcd = tr_int_.xcd = tr_bnd_.xcd = 8;
-  if (opt_.xcd_map < 0 && opt_.format == 1 && stencil_plane(spec_) > 0 && win_doubles_ == 0 &&
-      opt_.blocks_per_cu <= 0 && opt_.sell_slices != 2 && partition_granule(spec_) % 64 == 0) {
+  if (opt_.format == 1 && stencil_plane(spec_) > 0 && win_doubles_ == 0 &&
+      opt_.blocks_per_cu <= 0 && partition_granule(spec_) % 64 == 0) {
     // 3-D stencil, generic pass: XCD-aware sweep with one plane of slices per step.  Each XCD
     // walks a contiguous 1/8 of the slices with grid / 8 blocks x 4 waves = P slices (one plane)
     // per grid-stride step, so a row's +-N^2 (previous / next plane) neighbours are the same
@@ -527,25 +500,12 @@ void GpuCgSolver::setup() {
     if (split_) apply(tr_int_, g_int_);
     info_.xcd_map = true;
   }
-  if (opt_.xcd_map > 0) info_.xcd_map = true;
-  if (opt_.format == 1 && opt_.sell_slices != 2 && win_doubles_ == 0) {
-    // vertical-strip slice order: S = slices per grid line (2-D stencil, whole-slice lines)
-    int64_t S = opt_.strip > 0 ? opt_.strip : 0;
-    if (opt_.strip < 0 && stencil_plane(spec_) == 0 && stencil_line(spec_) > 0 && stencil_line(spec_) % 64 == 0)
-      S = stencil_line(spec_) / 64;
-    auto apply = [&](TileRanges& t) {
-      if (S > 0 && t.ntiles > 0 && t.nt0 == t.ntiles && t.ntiles % S == 0 && t.ntiles / S >= 2) t.strip = (int32_t)S;
-    };
-    apply(tr_all_);
-    apply(tr_int_);
-    info_.strip = tr_all_.strip;
-  }
   {
     // line-carry pass: whole 64-row slices per grid line (2-D) / plane (3-D), the stencil path's
     // format and layout; applies to a launch whose slices are one range of whole lines
     const int64_t gl = partition_granule(spec_);
     const bool ok = opt_.recurrence == 1 && opt_.format == 1 && (d16_ || c8_) && opt_.interleave == 1 &&
-                    opt_.sell_slices != 2 && win_doubles_ == 0 && info_.max_row_len <= 8 &&
+                    win_doubles_ == 0 && info_.max_row_len <= 8 &&
                     info_.spmv_param >= info_.max_row_len && info_.spmv_param >= 4 && gl > 1 && gl % 64 == 0 &&
                     n % gl == 0 && L_.row_begin % gl == 0 && !perm_.get();
     MCG_CHECK(opt_.carry != 1 || ok,
@@ -559,13 +519,12 @@ void GpuCgSolver::setup() {
       auto apply = [&](TileRanges& t, int& grid) {
         if (t.ntiles == 0 || t.nt0 != t.ntiles || t.b0 % S != 0 || t.nt0 % S != 0 || t.nt0 / S < 2) return false;
         t.strip = (int32_t)S;
-        const int bpc_c = opt_.carry_blocks_per_cu > 0 ? opt_.carry_blocks_per_cu : (t.nt0 / S >= 4096 ? 8 : 4);
-        grid = ncu_ * bpc_c;
+        grid = ncu_ * (t.nt0 / S >= 4096 ? 8 : 4);
         return true;
       };
       // the specialised pass (no slow path) when every stored offset is carried: 0, +-1, +-one line
       // 3-D: the carried line is a plane (N^2 rows) and +-N is a second carried offset
-      carry_lo2_ = stencil_plane(spec_) > 0 && opt_.carry_3d != 0 ? (int32_t)stencil_line(spec_) : 0;
+      carry_lo2_ = stencil_plane(spec_) > 0 ? (int32_t)stencil_line(spec_) : 0;
       carry_general_ = !c8_;
       for (int64_t off : dict_offsets_)
         if (off != 0 && off != 1 && off != -1 && off != 64 * S && off != -64 * S &&
@@ -598,9 +557,7 @@ void GpuCgSolver::setup() {
       const bool ok = kern::sell_to_dia4(sell_view(), (int)dict_offsets_.size(), (int64_t)tr_all_.strip * 64,
                                          ar3 ? (int64_t)carry_lo2_ : 0, dia4_.get(), dvals_.get(), s0_);
       MCG_CHECK(ok || opt_.carry_dia != 1, "carry_dia: the matrix is not a canonical 2-D 5-point / 3-D 7-point pattern");
-      if (ok) {
-        codes4_.release();
-      } else {
+      if (!ok) {
         dia4_.release();
         dvals_.release();
       }
@@ -617,14 +574,11 @@ void GpuCgSolver::setup() {
     MCG_CHECK(opt_.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
               "3-D: dia4, N a multiple of 64 and of carry3_kw)");
-    // 4 waves per SIMD (one round of resident blocks); carry_blocks_per_cu > 0: that many 4-wave
-    // block equivalents per CU
-    if (ar3_) g_all_ = std::max(1, ncu_ * (opt_.carry_blocks_per_cu > 0 ? opt_.carry_blocks_per_cu : 4) * 4 / kw);
+    // 4 waves per SIMD (one round of resident blocks)
+    if (ar3_) g_all_ = std::max(1, ncu_ * 16 / kw);
     info_.ar3_kw = ar3_ ? kw : 0;
-    info_.carry_xchg = info_.carry && carry_lo2_ > 0 && opt_.carry_3d == 2 &&
+    info_.carry_xchg = info_.carry && carry_lo2_ > 0 &&
                        kern::carry_block_exchange_ok(info_.spmv_param, carry_lo2_, gl / 64);
-    if (!info_.carry || carry_general_ || carry_lo2_ != 0) codes4_.release();  // only the 2-D carry reads them
-    info_.codes4 = codes4_.get() != nullptr;
   }
   if (ar_) {  // r and p in the plain ext layout (no {r, Ap} pairs); the pipelined generic pass reads pairs
     opt_.interleave = 0;
@@ -653,7 +607,7 @@ void GpuCgSolver::setup() {
     kern::slice_meta(slice_ptr_.get(), ns, smeta_.get(), s0_);
   }
   allocate_vectors_();
-  g_b_ = kern::grid_for((n + 1) / 2, 256, opt_.update_blocks_per_cu > 0 ? opt_.update_blocks_per_cu : bpc);
+  g_b_ = kern::grid_for((n + 1) / 2, 256, 4);  // residual update / dot kernels: 1024 blocks (best measured)
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
   const bool split = split_;
@@ -699,12 +653,10 @@ void GpuCgSolver::setup() {
     info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
-    const double streamed = info_.dia4 ? (double)dia4_.bytes()
-                                       : (codes4_.get() ? (double)codes4_.bytes() + 4.0 * (double)smeta_.size()
-                                                        : (double)matrix_bytes);
+    const double streamed = info_.dia4 ? (double)dia4_.bytes() : (double)matrix_bytes;
     // three-term form: p_{k-1}, p_{k-2} read, p_k written 24 B; x rw every second pass 8; edge r + Ap 0.5
     info_.bytes_per_iter_model = streamed + (p3_ ? 32.5 : 44.25) * n;
-    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + codes4_.bytes() + smeta_.bytes();
+    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + smeta_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   }
   // vectors allocated with room for the placement probe's start offsets hold that headroom too
@@ -740,15 +692,12 @@ void GpuCgSolver::allocate_vectors_() {
     p_[0].allocate(L_.ext_len, "p", 8);
     return;
   }
-  // vec_skew: buffer i of the streams one pass reads / writes at the same row starts i * vec_skew
-  // 256-B blocks past its allocation.  With the placement probe, every vector gets room for
-  // leads up to kLeadCap (probe_placement_)
-  const size_t skew = (size_t)std::max(0, opt_.vec_skew) * 32;
+  // with the placement probe, every vector gets room for leads up to kLeadCap (probe_placement_)
   const size_t cap = opt_.placement_tries > 1 && opt_.placement_leads > 1 && opt_.recurrence == 1 ? kLeadCap : 0;
-  x_.allocate(n, "x", 8, 1 * skew, cap);
+  x_.allocate(n, "x", 8, 0, cap);
   if (ar_) {  // r, p by parity (ext layout); Ap only for slice edges (+ first / last / ghost lines at P > 1)
-    r_.allocate(L_.ext_len, "r", 8, 2 * skew, cap);
-    r1_.allocate(L_.ext_len, "r", 8, 3 * skew, cap);
+    r_.allocate(L_.ext_len, "r", 8, 0, cap);
+    r1_.allocate(L_.ext_len, "r", 8, 0, cap);
     const int64_t ns = (n + 63) / 64;
     if (!ar3_ || p3_) {  // 3-D two-term: the slices' edge rows go through the ext-layout Ap like the outer lines
       // three-term form: the edge rows' r behind their Ap (F1Vectors::re_old / re_new)
@@ -761,8 +710,8 @@ void GpuCgSolver::allocate_vectors_() {
       apx_[1].allocate(L_.ext_len, "Ap", 8);
     }
   } else if (opt_.interleave == 1) {  // single-reduction form, {r, Ap} pairs, double-buffered by parity
-    ra_[0].allocate(2 * L_.ext_len, "r", 8, 2 * skew, cap);
-    ra_[1].allocate(2 * L_.ext_len, "r", 8, 3 * skew, cap);
+    ra_[0].allocate(2 * L_.ext_len, "r", 8, 0, cap);
+    ra_[1].allocate(2 * L_.ext_len, "r", 8, 0, cap);
   } else if (opt_.recurrence == 1) {  // single-reduction form: r and Ap are gathered -> ext layout, double-buffered
     r_.allocate(L_.ext_len, "r", 8, 0, cap);
     Ap_.allocate(L_.ext_len, "Ap", 8, 0, cap);
@@ -772,8 +721,8 @@ void GpuCgSolver::allocate_vectors_() {
     r_.allocate(L_.ext_len, "r", 8);
     Ap_.allocate(n, "Ap", 8);
   }
-  p_[0].allocate(L_.ext_len, "p", 8, 4 * skew, cap);
-  p_[1].allocate(L_.ext_len, "p", 8, 5 * skew, cap);
+  p_[0].allocate(L_.ext_len, "p", 8, 0, cap);
+  p_[1].allocate(L_.ext_len, "p", 8, 0, cap);
 }
 
 // Physical placement of the vector streams.  The same stream kernel on the same sizes runs at
@@ -793,9 +742,7 @@ void GpuCgSolver::probe_placement_() {
   auto bufs = vectors_();
   size_t set_bytes = 0;
   for (auto* b : bufs) set_bytes += b->bytes();
-  // start-offset trials re-lead every buffer, which would discard a vec_skew experiment's offsets:
-  // with vec_skew only whole allocations are compared
-  const int leads = opt_.vec_skew > 0 ? 1 : std::max(1, opt_.placement_leads);
+  const int leads = std::max(1, opt_.placement_leads);
   // start offset (doubles) of buffer i in lead trial t: trial 0 all zero, then pseudo-random
   // multiples of 4 KiB (0..7) + 1 MiB (0..3)
   auto lead_of = [&](int t, size_t i) -> size_t {
@@ -944,7 +891,7 @@ void GpuCgSolver::enqueue_spmv_(int k, int which, int final_mode) {
     const SellDev A = sell_view();
     kern::cg_spmv_fused_sell(A, r_.get(), pold, pnew, x_.get(), Ap_.get(), L_.own_off, tr, part, grid, st_.get(),
                              opt_.tol, first, final_mode, info_.spmv_param,
-                             (opt_.nt_loads ? 1 : 0) | (opt_.sell_slices == 2 ? 2 : 0) | (d16_ ? 4 : 0) |
+                             (d16_ ? 4 : 0) |
                                  (c8_ ? 8 : 0),
                              s0_);
   } else if (info_.idx64) {
@@ -991,7 +938,6 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
                     x_.get()};
   v.p_fix = p_[1].get();
   v.ext_len = L_.ext_len;
-  v.nt_loads = opt_.carry_nt;
   if (opt_.interleave == 1) {
     v.ra_old = reinterpret_cast<const double2*>(ra_[(k + 1) & 1].get());
     v.ra_new = reinterpret_cast<double2*>(ra_[k & 1].get());
@@ -1011,25 +957,23 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
       v.re_new = ape_[k & 1].get() + ns2;
     }
     if (ar3_) {
-      kern::cg_carry_ar3(opt_.carry_depth > 0 ? opt_.carry_depth : 2, info_.ar3_kw, S, v, L_.own_off, tr,
+      kern::cg_carry_ar3(2, info_.ar3_kw, S, v, L_.own_off, tr,
                          carry_lo2_, use_halo_, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode,
                          s0_, rc, p3_);
       return;
     }
     // three-term even passes: operands 2 lines ahead (chains of 3 registers, renamed by the 3-step unroll)
-    const int depth = ((k & 1) == 0 && opt_.carry_depth_even > 0)
-                          ? opt_.carry_depth_even
-                          : ((k & 1) == 0 && p3_ && opt_.carry_unroll == 3 && opt_.carry_depth <= 0)
-                                ? 2
-                                : (opt_.carry_depth > 0 ? opt_.carry_depth : 3);
-    kern::cg_carry_ar(dia4_.get() ? 4 : (codes4_.get() ? 3 : 2), info_.spmv_param, depth, S, v,
+    // operand prefetch depth in lines: 3 (2-D: 318 vs 301 it/s at 2); the three-term even passes 2
+    // (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md)
+    const int depth = ((k & 1) == 0 && p3_) ? 2 : 3;
+    kern::cg_carry_ar(dia4_.get() ? 4 : 2, info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
-                      p3_, opt_.carry_unroll);
+                      p3_, 3);
     return;
   }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
-    kern::cg_fused1_carry(codes4_.get() && !carry_general_ && carry_lo2_ == 0 ? 3 : (c8_ ? 2 : 1), info_.spmv_param,
-                          opt_.carry_depth > 0 ? opt_.carry_depth : (carry_lo2_ > 0 ? 1 : 3), carry_general_,
+    kern::cg_fused1_carry(c8_ ? 2 : 1, info_.spmv_param,
+                          carry_lo2_ > 0 ? 1 : 3, carry_general_,
                           carry_lo2_, info_.carry_xchg, S, v, L_.own_off, tr, part, pstride_, grid, st_.get(),
                           opt_.tol, first, check, k, s0_, rc);
     return;
@@ -1039,7 +983,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
                         pstride_, grid, st_.get(), opt_.tol, first, check, k, s0_, rc);
     return;
   }
-  const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : (opt_.sell_slices == 2 ? 2 : 1))) : 0;
+  const int fmt = opt_.format == 1 ? (c8_ ? 4 : (d16_ ? 3 : 1)) : 0;
   if (info_.idx64)
     kern::cg_fused1<int64_t>(fmt, info_.spmv_param, CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, S, v,
                              L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, final_mode, k,
@@ -1231,7 +1175,7 @@ void GpuCgSolver::enqueue_iteration_(int k) {
   CgState* st = st_.get();
   kern::cg_reduce(partials_.get(), np, st, kReduceA, first, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(&st->pAp, 1, s0_);
-  kern::cg_update_r(r_.get() + L_.own_off, Ap_.get(), L_.n_local(), partials_.get(), g_b_, st, opt_.update_unroll,
+  kern::cg_update_r(r_.get() + L_.own_off, Ap_.get(), L_.n_local(), partials_.get(), g_b_, st, 1,
                     s0_);
   kern::cg_reduce(partials_.get(), g_b_, st, kReduceB, first, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(&st->rr_new, 1, s0_);

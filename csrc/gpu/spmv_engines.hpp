@@ -461,57 +461,6 @@ __device__ __forceinline__ void sell_aligned_part(const SellDev& A, const TileRa
   }
 }
 
-// SELL-64, two slices per wave iteration: two independent load -> gather chains
-// in flight per wave (memory-level parallelism without more waves).
-template <int U, bool NT, class Gather, class Epi>
-__device__ __forceinline__ void sell2(const SellDev& A, const TileRanges& sr, Gather&& gather, Epi&& epi) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w_in_blk = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  TileCursor cur = tile_cursor(sr, w_in_blk, kWaves);
-  for (; cur.t < cur.end; cur.t += 2 * cur.step) {
-    const int64_t ta = cur.t, tb = cur.t + cur.step;
-    const bool has_b = tb < cur.end;
-    const int64_t sa = ta < sr.nt0 ? sr.b0 + ta : sr.b1 + (ta - sr.nt0);
-    const int64_t sb = has_b ? (tb < sr.nt0 ? sr.b0 + tb : sr.b1 + (tb - sr.nt0)) : sa;
-    const int64_t base_a = A.slice_ptr[sa], base_b = A.slice_ptr[sb];
-    const int wa = (int)((A.slice_ptr[sa + 1] - base_a) >> 6);
-    const int wb = (int)((A.slice_ptr[sb + 1] - base_b) >> 6);
-    const int w = wa > wb ? wa : wb;
-    const int32_t* __restrict__ cpa = A.cols + base_a + lane;
-    const double* __restrict__ vpa = A.vals + base_a + lane;
-    const int32_t* __restrict__ cpb = A.cols + base_b + lane;
-    const double* __restrict__ vpb = A.vals + base_b + lane;
-    double suma = 0.0, sumb = 0.0;
-    for (int j0 = 0; j0 < w; j0 += U) {
-      int32_t ca[U], cb[U];
-      double va[U], vb[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int ja = (j0 + u < wa ? j0 + u : wa - 1) * 64;
-        const int jb = (j0 + u < wb ? j0 + u : wb - 1) * 64;
-        ca[u] = ld<NT>(cpa + ja);
-        va[u] = ld<NT>(vpa + ja);
-        cb[u] = ld<NT>(cpb + jb);
-        vb[u] = ld<NT>(vpb + jb);
-      }
-      double ga[U], gb[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        ga[u] = gather(ca[u]);
-        gb[u] = gather(cb[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        suma = (j0 + u < wa) ? fma(va[u], ga[u], suma) : suma;
-        sumb = (j0 + u < wb) ? fma(vb[u], gb[u], sumb) : sumb;
-      }
-    }
-    const int64_t ia = sa * 64 + lane, ib = sb * 64 + lane;
-    if (ia < A.n_rows) epi(A.perm ? (int64_t)A.perm[ia] : ia, suma);
-    if (has_b && ib < A.n_rows) epi(A.perm ? (int64_t)A.perm[ib] : ib, sumb);
-  }
-}
-
 }  // namespace eng
 }  // namespace kern
 }  // namespace mcg

@@ -30,18 +30,8 @@ struct CgOptions {
   int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
   int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector, 4 row-length adaptive per
                              // tile (direct or 16 lanes per row); -1 = auto (1 when every row has <= 16 entries, else 4)
-  int spmv_param = 0;        // batch U (engines 0/1, SELL) or lanes/row G (engine 2); 0 = auto
-  int update_unroll = 1;     // double2 loads in flight per lane in the residual update
-  int update_blocks_per_cu = 4;  // grid of the residual update / dot kernels (1024 blocks: best measured)
-  int nt_loads = 0;          // non-temporal loads for the matrix streams (direct CSR / SELL engines)
-  int xcd_map = -1;          // XCD-aware contiguous tile regions for the SpMV grid; -1 = auto (the 3-D stencil's
-                             // generic SELL pass, with a grid sweeping one plane of slices per step)
-  int sell_slices = 1;       // SELL engine: slices in flight per wave (1 or 2)
   int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
-  int strip = 0;             // SELL: visit slices in vertical strips of this many slices per grid line (each wave
-                             // walks down one column); -1 = 2-D stencil line width.  Off by default: measured
-                             // slower (241 vs 248 it/s at 16384^2, profiles/sweep_strip_order.log)
   int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
                              // With the XCD-aware 3-D sweep it is the faster pass (419 vs 383 it/s at 512^3,
@@ -50,27 +40,9 @@ struct CgOptions {
                              // per grid line / plane): line-carry pass — a wave walks down a column of slices and
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
-  int carry_blocks_per_cu = 0;  // grid of the line-carry pass (one job = a run of lines of one slice column);
-                                // 0 = auto (8 when the launch covers >= 4096 lines, else 4)
-  int carry_nt = 0;             // line-carry pass: non-temporal loads of the operands each wave reads once (measured
-                                // slower: 281 vs 302 it/s 2-D, 480 vs 531 3-D; the +-1 edge rows are re-read from L2)
-  int carry_c4 = 1;             // line-carry pass on a c8 matrix with <= 16 dictionary entries: 4-bit codes
-  int carry_3d = 2;             // line-carry pass on 3-D stencils: plane carry + the +-N rows gathered a plane ahead
-                                // (1); 2 = the block's waves on consecutive grid lines, inner +-N rows exchanged
-                                // through LDS (when N is a multiple of 64); 0 = off
-  int carry_depth = 0;          // line-carry pass: operand prefetch depth in lines (1..3); 0 = auto (2-D 3: 318 vs
-                                // 301 it/s at 2; 3-D 1: the +-N rows, gathered one plane ahead, then meet the
-                                // neighbouring column's own prefetch in the L2: 534 vs 518 it/s at 2)
-  int carry_unroll = 3;         // three-term 2-D carry, even passes: line steps unrolled by 3 (the period of the
-                                // codes / p_k rotations: renaming instead of 64-bit moves); 1 = rolled; 5 =
-                                // experiment: rolled at 5 waves per SIMD (96 VGPRs, spills; no gain,
-                                // profiles/r2s6_carry_grid.md)
-  int carry_depth_even = 0;     // 2-D Ap-recomputing carry: prefetch depth of the even passes (no x update), 0 = as
-                                // carry_depth
   int placement_tries = 3;   // single-reduction form: time the pass on this many physical placements of the vector
                              // set at setup and keep the fastest (1 = off; profiles/r1_placement_probe.md)
   int placement_leads = 8;   // ... times this many start offsets of the vectors inside their allocations
-  int vec_skew = 0;         // experiment: stagger the vector buffers' base addresses by i * vec_skew 256-B blocks
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int halo_mode = -1;        // ghosts: 0 = column-window ranges (p2p send/recv), 1 = all-gather of equal row blocks
@@ -91,6 +63,8 @@ struct CgOptions {
                              // wave sweeping the segments together so the gathers of p hit the L2); -1 = auto (the
                              // scrambled random SPD, or a non-stencil user matrix on the all-gather layout), 0 = off
   int tile_seg_log2 = 18;    // tiles: column segment = 2^k doubles (18: 2 MiB of p, half an XCD's L2)
+  int tile_pace = 1;         // tiles: 0 = unpaced, 1 = every workgroup of a group finishes a segment before
+                             // any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest)
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
@@ -115,11 +89,6 @@ struct CgOptions {
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's
                              // kernels cannot start next to a resident pass (profiles/r2_corun_probe.md), so
                              // the split never overlapped; -1 = auto (on when the halo overlap is on), 0 = off
-  int comm_cus = 0;          // experiment: CUs withheld from the compute stream (CU-masked queue) so RCCL's
-                             // halo / all-gather kernels on the side stream find room next to the resident
-                             // pass; measured slower and without effect (profiles/r2_corun_probe.md), 0 = off
-  int cu_mask_pattern = 0;   // which CUs comm_cus withholds: 0 = the last CU of each of comm_cus equal groups of
-                             // the mask bits, 1 = the last comm_cus bits
   int fail_graph_launch_at = -1;  // test hook: report the graph launch at this iteration as failed (nothing enqueued)
   int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")

@@ -119,6 +119,24 @@ class NullComm final : public Communicator {
   int rank_, world_;
 };
 
+// Latency rehearsal: like NullComm, but every all-reduce and halo exchange costs a fixed
+// device-side delay (a one-workgroup spin of `us` microseconds on the stream it is enqueued on),
+// so the time an iteration spends waiting for a collective can be priced on one GPU.
+class DelayComm final : public Communicator {
+ public:
+  DelayComm(int rank, int world, double allreduce_us, double halo_us)
+      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us) {}
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void allreduce_sum(double*, size_t, hipStream_t stream) override;
+  void halo_exchange(const LocalLayout& L, double* const*, int, hipStream_t stream, const int* = nullptr) override;
+  bool moves_data() const override { return false; }
+
+ private:
+  int rank_, world_;
+  double ar_us_, halo_us_;
+};
+
 // Shared state of P in-process ranks on one device.
 class LocalGroup {
  public:

@@ -95,10 +95,6 @@ struct SellDev {
   const uint8_t* codes = nullptr;
   const double2* dict = nullptr;
   int32_t ndict = 0;
-  // SELL-64/c4 (dictionaries of <= 16 entries, e.g. the 2-D 5-pt operator's 15): the same codes
-  // 4 bits each, lanes 2i / 2i+1 of a slice entry in one byte (byte offset = c8 offset / 2);
-  // read by the line-carry pass (half the matrix stream of c8)
-  const uint8_t* codes4 = nullptr;
   // SELL-C-sigma (user matrices): slot i of the slices holds local row perm[i] (rows sorted by
   // length inside windows, so a slice pads less); nullptr = identity.  int32 columns only.
   const int32_t* perm = nullptr;
@@ -166,8 +162,6 @@ void aligned_local_slots(const SellDev& S, int32_t* out, hipStream_t st);
 // it has too many distinct values / offsets.  dict[vi * nd + di] = {value_vi, bits(offset_di)}.
 bool sell_dict_build(const SellDev& S, std::vector<double2>& dict, int& nv, int& nd, hipStream_t st);
 void sell_to_c8(const SellDev& S, const double2* dict, int nv, int nd, uint8_t* codes, hipStream_t st);
-// c8 -> c4 (every code < 16): codes4[i / 2] = codes[i] | codes[i + 1] << 4 for even i
-void sell_c8_to_c4(const uint8_t* codes, int64_t total, uint8_t* codes4, hipStream_t st);
 
 // ---- CG kernels (csrc/gpu/cg_kernels.hip) ----
 // variant: 0 = LDS-staged tiles, 1 = direct thread-per-row, 2 = CSR-vector (G lanes/row),
@@ -219,7 +213,6 @@ struct F1Vectors {
   // the parity-1 p buffer, for the one-term catch-up when convergence latches after an even pass.
   const double* p_fix = nullptr;
   int64_t ext_len = 0;  // ext-layout length of r / Ap / p (bounds of the line-carry pass's edge loads)
-  int nt_loads = 0;     // line-carry pass: non-temporal loads of the once-read operands
   // Ap-recomputing carry (cg_carry_ar.hip): Ap of each slice's two edge rows (lanes 0 / 63),
   // 2 doubles per owned slice, iteration k-1 / k; r_old/new, p_old/new as above, ap_old/new the
   // ext-layout Ap of the rank's first / last line and of its ghost lines (multi-rank, else null)
@@ -343,6 +336,7 @@ struct TilesDev {
   int64_t n_rows = 0, nblocks = 0;
   int G = 0, seg_shift = 18;
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
+  int pace_slack8 = 0;       // a workgroup waits for all but pace_slack8 / 8 of its group (0: all)
 };
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
 int tiles_grid();  // workgroups of the SpMV: the resident count (pacing waits on every workgroup)
@@ -374,6 +368,11 @@ void axpy(double alpha, const double* x, double* y, int64_t n, hipStream_t strea
 void xpby(const double* x, double beta, double* y, int64_t n, hipStream_t stream);   // y = x + b y
 
 int grid_for(int64_t work_items, int block, int blocks_per_cu);
+
+// ---- probes (csrc/gpu/probe_kernels.hip) ----
+// `blocks` workgroups of 256 threads spinning for `microseconds` on the realtime clock; fat: ~270
+// VGPRs per wave live (RCCL's kernels' footprint), else a handful.  out: one double per block or null
+void spin(double* out, double microseconds, bool fat, int blocks, hipStream_t stream);
 
 }  // namespace kern
 }  // namespace mcg

@@ -49,7 +49,6 @@ struct SolverInfo {
   bool interleave = false;
   int window = 0;  // LDS window width (doubles) of the windowed pass; 0 = off
   bool pipeline = false;
-  int strip = 0;  // vertical-strip slice order (slices per grid line), 0 = natural order
   bool carry = false;  // line-carry pass (single GPU: every pass; multi-rank: the interior launch)
   bool fused_reduce = false;  // the pass reduces its own block partials (one kernel per iteration)
   bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
@@ -64,9 +63,7 @@ struct SolverInfo {
                               // the all-reduce; one full pass per iteration (CgOptions::halo_ahead)
   double ag_local_frac = 0.0; // own-block slots / all slots (the part of the SpMV that hides the all-gather)
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
-  int comm_cus = 0;           // CUs withheld from the compute stream for the side stream's RCCL kernels
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
-  bool codes4 = false;   // SELL-64/c4 codes for the line-carry pass
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
   int ar3_kw = 0;        // 3-D Ap-recomputing plane carry: waves (grid lines) per block; 0 = not in use
@@ -154,7 +151,7 @@ class GpuCgSolver {
   bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them
 
   Stream s0_, s1_;
-  int ncu_ = 0;  // CUs the compute stream may use (all, minus CgOptions::comm_cus)
+  int ncu_ = 0;  // CUs of the device
   Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2], ev_sync_[2];
   // matrix
   DeviceBuffer<int32_t> rp32_;
@@ -166,7 +163,6 @@ class GpuCgSolver {
   bool d16_ = false;
   DeviceBuffer<uint8_t> codes_;  // SELL-64/c8 dictionary codes
   DeviceBuffer<double2> dict_;
-  DeviceBuffer<uint8_t> codes4_;  // SELL-64/c4 copy of the codes (line-carry pass, <= 16 dictionary entries)
   DeviceBuffer<uint8_t> dia4_;    // SELL-64/dia4 copy (Ap-recomputing carry; 160 B per slice)
   DeviceBuffer<double> dvals_;    // ... its value table (16 doubles)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
@@ -192,7 +188,8 @@ class GpuCgSolver {
     t.nblocks = tgeo_.nblocks;
     t.G = tgeo_.G;
     t.seg_shift = tgeo_.seg_shift;
-    t.pace = tpace_.get();
+    t.pace = opt_.tile_pace > 0 ? tpace_.get() : nullptr;
+    t.pace_slack8 = opt_.tile_pace == 2 ? 1 : 0;
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
@@ -209,7 +206,6 @@ class GpuCgSolver {
     s.codes = codes_.get();
     s.dict = dict_.get();
     s.ndict = ndict_;
-    s.codes4 = codes4_.get();
     s.perm = perm_.get();
     s.soffs = soffs_.get();
     s.ext_len = L_.ext_len;

@@ -44,8 +44,7 @@ ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64
 }
 
 CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool use_graph, bool force_comm,
-                    const std::string& format, int blocks_per_cu, int spmv_variant, int spmv_param,
-                    int update_unroll, int nt_loads, int xcd_map, int sell_slices, int recurrence) {
+                    const std::string& format, int blocks_per_cu, int spmv_variant, int recurrence) {
   CgOptions o;
   o.maxit = maxit;
   o.tol = tol;
@@ -60,11 +59,6 @@ CgOptions make_opts(int maxit, double tol, int check_every, bool overlap, bool u
   else fail("unknown format: " + format);
   o.blocks_per_cu = blocks_per_cu;
   o.spmv_variant = spmv_variant;
-  o.spmv_param = spmv_param;
-  o.update_unroll = update_unroll;
-  o.nt_loads = nt_loads;
-  o.xcd_map = xcd_map;
-  o.sell_slices = sell_slices;
   o.recurrence = recurrence;
   return o;
 }
@@ -199,27 +193,18 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
            py::arg("format") = "csr", py::arg("blocks_per_cu") = 0, py::arg("spmv_variant") = -1,
-           py::arg("spmv_param") = 0, py::arg("update_unroll") = 1, py::arg("nt_loads") = 0,
-           py::arg("xcd_map") = -1, py::arg("sell_slices") = 1, py::arg("recurrence") = 0)
+           py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
-      .def_readwrite("comm_cus", &CgOptions::comm_cus)
-      .def_readwrite("cu_mask_pattern", &CgOptions::cu_mask_pattern)
       .def_readwrite("interleave", &CgOptions::interleave)
       .def_readwrite("window", &CgOptions::window)
       .def_readwrite("pipeline", &CgOptions::pipeline)
-      .def_readwrite("strip", &CgOptions::strip)
       .def_readwrite("carry", &CgOptions::carry)
-      .def_readwrite("vec_skew", &CgOptions::vec_skew)
       .def_readwrite("placement_tries", &CgOptions::placement_tries)
       .def_readwrite("placement_leads", &CgOptions::placement_leads)
-      .def_readwrite("carry_blocks_per_cu", &CgOptions::carry_blocks_per_cu)
-      .def_readwrite("carry_3d", &CgOptions::carry_3d)
-      .def_readwrite("carry_c4", &CgOptions::carry_c4)
-      .def_readwrite("carry_nt", &CgOptions::carry_nt)
-      .def_readwrite("carry_depth", &CgOptions::carry_depth)
       .def_readwrite("fused_reduce", &CgOptions::fused_reduce)
       .def_readwrite("tiles", &CgOptions::tiles)
       .def_readwrite("tile_seg_log2", &CgOptions::tile_seg_log2)
+      .def_readwrite("tile_pace", &CgOptions::tile_pace)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       .def_readwrite("pmat", &CgOptions::pmat)
       .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
@@ -229,21 +214,13 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ap_recompute", &CgOptions::ap_recompute)
       .def_readwrite("carry_dia", &CgOptions::carry_dia)
       .def_readwrite("p3", &CgOptions::p3)
-      .def_readwrite("carry_depth_even", &CgOptions::carry_depth_even)
-      .def_readwrite("carry_unroll", &CgOptions::carry_unroll)
       .def_readwrite("carry3_kw", &CgOptions::carry3_kw)
       .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       .def_readwrite("force_idx64", &CgOptions::force_idx64)
-      .def_readwrite("update_blocks_per_cu", &CgOptions::update_blocks_per_cu)
       .def_readwrite("inject_nan_at", &CgOptions::inject_nan_at)
-      .def_readwrite("sell_slices", &CgOptions::sell_slices)
-      .def_readwrite("nt_loads", &CgOptions::nt_loads)
-      .def_readwrite("xcd_map", &CgOptions::xcd_map)
       .def_readwrite("spmv_variant", &CgOptions::spmv_variant)
-      .def_readwrite("spmv_param", &CgOptions::spmv_param)
-      .def_readwrite("update_unroll", &CgOptions::update_unroll)
       .def_readwrite("maxit", &CgOptions::maxit)
       .def_readwrite("tol", &CgOptions::tol)
       .def_readwrite("rtol", &CgOptions::rtol)
@@ -350,6 +327,12 @@ PYBIND11_MODULE(_C, m) {
                                                   "(per-rank timing rehearsal on one GPU)")
       .def(py::init<int, int>(), py::arg("rank"), py::arg("world"));
 
+  py::class_<DelayComm, std::shared_ptr<DelayComm>>(m, "DelayComm",
+                                                    "one rank of a P-rank run whose all-reduce / halo cost a fixed "
+                                                    "device-side delay and move nothing (latency rehearsal)")
+      .def(py::init<int, int, double, double>(), py::arg("rank"), py::arg("world"), py::arg("allreduce_us"),
+           py::arg("halo_us") = 0.0);
+
   py::class_<GpuCgSolver>(m, "Solver")
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<Comm> comm) {
              return new GpuCgSolver(s, o, rank, world, comm.get());
@@ -357,6 +340,11 @@ PYBIND11_MODULE(_C, m) {
            py::arg("spec"), py::arg("opts"), py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("comm") = nullptr, py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<NullComm> comm) {
+             return new GpuCgSolver(s, o, rank, world, comm.get());
+           }),
+           py::arg("spec"), py::arg("opts"), py::arg("rank"), py::arg("world"), py::arg("comm"),
+           py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
+      .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<DelayComm> comm) {
              return new GpuCgSolver(s, o, rank, world, comm.get());
            }),
            py::arg("spec"), py::arg("opts"), py::arg("rank"), py::arg("world"), py::arg("comm"),
@@ -409,7 +397,6 @@ PYBIND11_MODULE(_C, m) {
         d["interleave"] = i.interleave;
         d["window"] = i.window;
         d["pipeline"] = i.pipeline;
-        d["strip"] = i.strip;
         d["carry"] = i.carry;
         d["fused_reduce"] = i.fused_reduce;
         d["pmat"] = i.pmat;
@@ -423,9 +410,7 @@ PYBIND11_MODULE(_C, m) {
         d["ap_recompute"] = i.ap_recompute;
         d["ag_local_frac"] = i.ag_local_frac;
         d["graph_fallbacks"] = i.graph_fallbacks;
-        d["comm_cus"] = i.comm_cus;
         d["xcd_map"] = i.xcd_map;
-        d["codes4"] = i.codes4;
         d["dia4"] = i.dia4;
         d["p3"] = i.p3;
         d["ar3_kw"] = i.ar3_kw;
@@ -571,5 +556,9 @@ PYBIND11_MODULE(_C, m) {
                             as_stream(stream));
   });
   k.def("grid_for", &kern::grid_for);
+  k.def("spin", [](uintptr_t out, double us, bool fat, int blocks, uintptr_t stream) {
+    kern::spin(reinterpret_cast<double*>(out), us, fat, blocks, as_stream(stream));
+  }, py::arg("out"), py::arg("microseconds"), py::arg("fat"), py::arg("blocks"), py::arg("stream"),
+     "probe: workgroups spinning on the realtime clock (fat: ~270 VGPRs per wave live)");
   k.attr("TILE_ROWS") = kTileRows;
 }

@@ -24,15 +24,13 @@ CHOICES = {"--problem": ["demo", "poisson2d", "poisson3d", "randspd", "csr", "ra
            "--format": ["csr", "sell", "sell16", "sellc8"], "--print-x": ["auto", "yes", "no"],
            "--report": ["text", "json"], "--comm": ["dual", "single"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
 INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
-        "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--spmv-param", "--update-unroll",
-        "--nt-loads", "--xcd-map", "--sell-slices", "--checkpoint-every", "--inject-nan-at"}
+        "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--checkpoint-every", "--inject-nan-at"}
 FLOATS = {"--density", "--nnz-per-row", "--tol", "--rtol", "--watchdog"}
 DEFAULTS = {"--problem": "demo", "--seed": 1234, "--device": "gpu", "--gpus": None, "--sim-ranks": 1,
             "--maxit": 2000, "--tol": 1e-7, "--rtol": 0.0, "--check-every": 32, "--fixed-iters": 0, "--warmup": 0,
             "--watchdog": 0.0, "--recurrence": "auto", "--interleave": "auto", "--window": "auto", "--carry": "auto",
             "--pmat": "auto", "--fused-reduce": "auto", "--halo-mode": "auto", "--blocks-per-cu": 0,
-            "--spmv-variant": -1, "--spmv-param": 0, "--update-unroll": 1, "--nt-loads": 0, "--xcd-map": -1,
-            "--sell-slices": 1, "--checkpoint": "", "--checkpoint-every": 0, "--resume": "", "--inject-nan-at": -1,
+            "--spmv-variant": -1, "--checkpoint": "", "--checkpoint-every": 0, "--resume": "", "--inject-nan-at": -1,
             "--print-x": "auto", "--report": "text", "--comm": "dual"}
 
 
@@ -135,8 +133,6 @@ def _run(args) -> int:
                          use_graph=not args.no_graph, force_comm=args.force_comm, comm_mode=args.comm,
                          format=args.format or ("csr" if spec.problem == "demo" else "sellc8"),
                          blocks_per_cu=args.blocks_per_cu, spmv_variant=args.spmv_variant,
-                         spmv_param=args.spmv_param, update_unroll=args.update_unroll, nt_loads=args.nt_loads,
-                         xcd_map=args.xcd_map, sell_slices=args.sell_slices,
                          recurrence=recurrence(args.recurrence) if spec.problem != "demo" or args.recurrence != "auto"
                          else 0,
                          interleave=tri(args.interleave), window=tri(args.window), carry=tri(args.carry),

@@ -53,11 +53,6 @@ FLAGS = [
     ("--comm", "dual", "dual: reduce + halo communicators (halo on a side stream) | single: one, one stream order"),
     ("--blocks-per-cu", "0", "SpMV grid, blocks per CU (0 = auto)"),
     ("--spmv-variant", "-1", "CSR engine: 0 LDS tiles, 1 direct, 2 CSR-vector, 3 direct nt, 4 row-length adaptive; -1 auto"),
-    ("--spmv-param", "0", "batch U / lanes per row G (0 = auto)"),
-    ("--update-unroll", "1", "residual-update unroll (1, 2, 4)"),
-    ("--nt-loads", "0", "non-temporal matrix loads (0 / 1)"),
-    ("--xcd-map", "-1", "XCD-aware tile regions (-1 auto, 0, 1)"),
-    ("--sell-slices", "1", "SELL slices per wave (1, 2)"),
     # aux subsystems
     ("--checkpoint", None, "PREFIX of per-rank checkpoint files"),
     ("--checkpoint-every", "0", "write a checkpoint every ~K iterations"),

@@ -24,9 +24,9 @@ from ..parallel import dist as _dist
 
 def _opts(maxit=2000, tol=1e-7, **kw):
     """Native CgOptions; keyword names as in csrc/include/mcg/cg.hpp (format, blocks_per_cu,
-    spmv_variant, spmv_param, update_unroll, nt_loads, xcd_map, sell_slices, recurrence, ...)."""
+    spmv_variant, recurrence, ...)."""
     ctor = {"check_every", "overlap", "use_graph", "force_comm", "format", "blocks_per_cu", "spmv_variant",
-            "spmv_param", "update_unroll", "nt_loads", "xcd_map", "sell_slices", "recurrence"}
+            "recurrence"}
     o = native().CgOptions(maxit=maxit, tol=tol, **{k: v for k, v in kw.items() if k in ctor})
     for k, v in kw.items():
         if k not in ctor:

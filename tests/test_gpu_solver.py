@@ -38,13 +38,13 @@ def test_matches_cpu_reference(mcg, fmt, graph, problem, kw):
     assert tr < 1e-6
 
 
-@pytest.mark.parametrize("fmt,slices", [("csr", 1), ("sell", 1), ("sell", 2), ("sell16", 1), ("sellc8", 1)])
+@pytest.mark.parametrize("fmt", ["csr", "sell", "sell16", "sellc8"])
 @pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=96)), ("poisson3d", dict(n=20)),
                                          ("randspd", dict(rows=20000, band=40, density=0.25))])
-def test_single_reduction_matches_cpu(mcg, fmt, slices, problem, kw):
+def test_single_reduction_matches_cpu(mcg, fmt, problem, kw):
     spec = mcg.make_problem(problem, **kw)
     cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions(maxit=2000, tol=1e-7))
-    s = mcg.CGSolver(spec, format=fmt, sell_slices=slices, recurrence=1, check_every=8)
+    s = mcg.CGSolver(spec, format=fmt, recurrence=1, check_every=8)
     out = s.solve()
     assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
     assert out["converged"] == cpu["converged"]
@@ -214,20 +214,19 @@ def test_line_carry_pass_matches_generic(mcg, fmt, problem, kw):
 
 @pytest.mark.parametrize("n", [64, 128])
 def test_plane_carry_block_exchange(mcg, n):
-    """3-D plane carry with the +-N rows of a block's inner waves exchanged through LDS (carry_3d=2)
-    vs every wave gathering them (carry_3d=1) vs the generic pass: the same p_k values in the same
-    fma order, dot-product partials blocked differently."""
+    """3-D store-form plane carry with the +-N rows of a block's inner waves exchanged through LDS vs
+    the generic pass: the same p_k values in the same fma order, dot-product partials blocked
+    differently.  (The variant where every wave gathers its +-N rows lost and was removed in r3.)"""
     spec = mcg.make_problem("poisson3d", n=n, rhs="random")
-    solvers = [mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=c, carry_3d=m, check_every=8)
-               for c, m in ((1, 2), (1, 1), (0, 1))]
-    assert [s.info["carry_xchg"] for s in solvers] == [True, False, False]
-    assert [s.info["carry"] for s in solvers] == [True, True, False]
+    solvers = [mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=c, ap_recompute=0, check_every=8)
+               for c in (1, 0)]
+    assert [s.info["carry_xchg"] for s in solvers] == [True, False]
+    assert [s.info["carry"] for s in solvers] == [True, False]
     res = [s.solve() for s in solvers]
     assert all(r["converged"] for r in res)
-    assert max(r["iterations"] for r in res) - min(r["iterations"] for r in res) <= 1
-    for r in res[1:]:
-        np.testing.assert_allclose(res[0]["x_local"], r["x_local"], rtol=1e-6,
-                                   atol=1e-6 * np.abs(r["x_local"]).max())
+    assert abs(res[0]["iterations"] - res[1]["iterations"]) <= 1
+    np.testing.assert_allclose(res[0]["x_local"], res[1]["x_local"], rtol=1e-6,
+                               atol=1e-6 * np.abs(res[1]["x_local"]).max())
     assert solvers[0].true_residual_norm() < 1e-6
     outs = []
     for s in solvers:
@@ -236,10 +235,9 @@ def test_plane_carry_block_exchange(mcg, n):
         s.finalize()
         outs.append(s.result())
     assert all(o["iterations"] == 24 for o in outs)
-    for o in outs[1:]:
-        assert abs(outs[0]["rnorm"] - o["rnorm"]) <= 1e-9 * o["rnorm"]
+    assert abs(outs[0]["rnorm"] - outs[1]["rnorm"]) <= 1e-9 * outs[1]["rnorm"]
     # run to run: bitwise
-    again = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_3d=2, check_every=8).solve()
+    again = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, ap_recompute=0, check_every=8).solve()
     np.testing.assert_array_equal(again["x_local"], res[0]["x_local"])
 
 
@@ -255,19 +253,7 @@ def test_line_carry_pass_reproducible_and_auto(mcg):
         mcg.CGSolver(odd, format="sellc8", recurrence=1, carry=1)
 
 
-def test_line_carry_c4_codes_match_c8(mcg):
-    """4-bit dictionary codes (<= 16 entries: the 2-D 5-pt operator's 15) read by the line-carry pass:
-    the same entries as c8, so the same bits."""
-    spec = mcg.make_problem("poisson2d", n=256, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=1, carry_dia=0, check_every=8)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=0, carry_dia=0, check_every=8)
-    assert a.info["codes4"] and not b.info["codes4"]
-    ra, rb = a.solve(), b.solve()
-    assert ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
-    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
-
-
-@pytest.mark.parametrize("codes", ["dia4", "c4", "c8"])
+@pytest.mark.parametrize("codes", ["dia4", "c8"])
 @pytest.mark.parametrize("n", [128, 256])
 def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     """The line-carry pass that recomputes Ap_{k-1} = A p_{k-1} (same entries, same fma order, same
@@ -276,13 +262,11 @@ def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     SELL-64/dia4 storage (slot = canonical offset, absent entries exact zeros) the row sums add the
     same products in the same order, so it is bitwise equal too."""
     spec = mcg.make_problem("poisson2d", n=n, rhs="random")
-    c4 = 0 if codes == "c8" else 1
     dia = 1 if codes == "dia4" else 0
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=1, carry_dia=dia,
-                     p3=0, check_every=8)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, carry_c4=c4, ap_recompute=0, check_every=8)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, ap_recompute=1, carry_dia=dia, p3=0, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, carry=1, ap_recompute=0, check_every=8)
     assert a.info["ap_recompute"] and not a.info["interleave"]
-    assert a.info["dia4"] == (codes == "dia4") and a.info["codes4"] == (codes == "c4")
+    assert a.info["dia4"] == (codes == "dia4")
     assert not b.info["ap_recompute"] and b.info["interleave"]
     ra, rb = a.solve(), b.solve()
     assert ra["converged"] and ra["iterations"] == rb["iterations"] and ra["rnorm"] == rb["rnorm"]
