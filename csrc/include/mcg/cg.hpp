@@ -62,9 +62,11 @@ struct CgOptions {
                              // in blocks of 1024 owned by one wave, columns in segments of 2^tile_seg_log2, every
                              // wave sweeping the segments together so the gathers of p hit the L2); -1 = auto (the
                              // scrambled random SPD, or a non-stencil user matrix on the all-gather layout), 0 = off
-  int tile_seg_log2 = 18;    // tiles: column segment = 2^k doubles (18: 2 MiB of p, half an XCD's L2)
-  int tile_pace = 1;         // tiles: 0 = unpaced, 1 = every workgroup of a group finishes a segment before
-                             // any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest)
+  int tile_seg_log2 = 19;    // tiles: column segment = 2^k doubles (19: 4 MiB of p = an XCD's L2; at a P = 8 rank's
+                             // share of the scrambled config 5: 17 / 18 / 19 / 20 / 21 -> 8.5 / 12.2 / 14.0 / 11.2
+                             // / 8.5 it/s, profiles/r3_config5_scrambled.md)
+  int tile_pace = 2;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
+                             // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest)
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
