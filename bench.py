@@ -43,6 +43,10 @@ def aggregate(steps, ranks):
 
 def pass_label(info, problem):
     """The pass the timed iterations run, as the solver chose it."""
+    if info.get("recurrence") == "pipelined":
+        rr = info.get("pipe_rr", 0)
+        return ("pipelined CG (Ghysels-Vanroose: all-reduce || SpMV)"
+                + (f", residual replacement every {rr}" if rr else ""))
     if info.get("carry"):
         kind = "plane-carry" if problem == "poisson3d" or info.get("ar3_kw") else "line-carry"
         if info.get("p3"):
@@ -54,7 +58,7 @@ def pass_label(info, problem):
         return "split (materialized p)"
     if info.get("window"):
         return "windowed"
-    return "generic, xcd-aware" if info.get("xcd_map") else "generic"
+    return "generic"
 
 
 def parse_args(argv=None):
@@ -74,7 +78,10 @@ def parse_args(argv=None):
     ap.add_argument("--format", default="sellc8", choices=["csr", "sell", "sell16", "sellc8"],
                     help="sparse storage: CSR, SELL-64, SELL-64/d16 (16-bit column offsets) or SELL-64/c8 "
                          "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
-    ap.add_argument("--recurrence", type=int, default=-1, help="0 two-reduction, 1 single-reduction, -1 auto")
+    ap.add_argument("--recurrence", type=int, default=-1,
+                    help="0 two-reduction, 1 single-reduction, 2 pipelined (Ghysels-Vanroose), -1 auto")
+    ap.add_argument("--pipe-rr", type=int, default=0,
+                    help="pipelined CG: residual replacement every K iterations (0 = off)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="(default since r2; kept for old command lines)")
     ap.add_argument("--no-overlap", action="store_true")
@@ -173,6 +180,7 @@ def _run_rank(args, out_fd) -> int:
                        use_graph=use_graph, force_comm=args.force_comm, format=args.format,
                        blocks_per_cu=args.blocks_per_cu, recurrence=args.recurrence)
     opts.watchdog_seconds = args.watchdog
+    opts.pipe_rr = args.pipe_rr
     for kv in args.set:
         k, v = kv.split("=", 1)
         if not hasattr(opts, k):

@@ -16,7 +16,7 @@
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
 //   --comm dual|single (two RCCL communicators, halo on a side stream | one, one stream order)
 //   --spmv-variant 0|1|2|3|4
-//   --recurrence two|single  --interleave auto|on|off  --window auto|on|off
+//   --recurrence two|single|pipelined  --pipe-rr K  --interleave auto|on|off  --window auto|on|off
 //   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
 //   --fused-reduce auto|on|off  --watchdog SECONDS
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
@@ -145,9 +145,11 @@ Args parse(int argc, char** argv) {
       if (v == "auto" || v == "-1") a.opt.recurrence = -1;
       else if (v == "single" || v == "fused1" || v == "1") a.opt.recurrence = 1;
       else if (v == "two" || v == "0") a.opt.recurrence = 0;
+      else if (v == "pipelined" || v == "2") a.opt.recurrence = 2;
       else usage_error("--recurrence " + v);
       a.recurrence_set = true;
     }
+    else if (f == "--pipe-rr") a.opt.pipe_rr = std::stoi(need(i));
     else if (f == "--window") a.opt.window = tri(need(i), "--window");
     else if (f == "--carry") a.opt.carry = tri(need(i), "--carry");
     else if (f == "--interleave") a.opt.interleave = tri(need(i), "--interleave");

@@ -105,11 +105,11 @@ void Comm::allgather_inplace(double* buf, size_t block, hipStream_t stream) {
 }
 
 void DelayComm::allreduce_sum(double*, size_t, hipStream_t stream) {
-  if (ar_us_ > 0) kern::spin(nullptr, ar_us_, false, 1, stream);
+  if (ar_us_ > 0) kern::spin(nullptr, ar_us_, fat_, 1, stream);
 }
 
 void DelayComm::halo_exchange(const LocalLayout& L, double* const*, int, hipStream_t stream, const int*) {
-  if (halo_us_ > 0 && L.has_halo()) kern::spin(nullptr, halo_us_, false, 1, stream);
+  if (halo_us_ > 0 && L.has_halo()) kern::spin(nullptr, halo_us_, fat_, 1, stream);
 }
 
 int Comm::count() const {

@@ -106,6 +106,9 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
   MCG_CHECK(opt_.graph_iters >= 2 && opt_.graph_iters % 2 == 0, "graph_iters must be even and >= 2");
   if (opt_.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
+  MCG_CHECK(opt_.recurrence >= -1 && opt_.recurrence <= 2, "recurrence must be -1 (auto), 0, 1 or 2 (pipelined)");
+  // pipelined CG: a residual replacement every pipe_rr iterations is an eager step (no capture)
+  if (opt_.recurrence == 2 && opt_.pipe_rr != 0) opt_.use_graph = false;
   // halo prefetch crosses iteration (and graph-launch) boundaries: eager runs only (and not for
   // the split pass, whose ghosts come from its own update kernel; decided in setup())
   prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph && !L_.allgather;
@@ -172,6 +175,8 @@ void GpuCgSolver::setup() {
   info_.interior_rows = L_.interior_end - L_.interior_begin;
   info_.format = d16_ ? 2 : opt_.format;
   info_.recurrence = opt_.recurrence;
+  info_.pipe_rr = opt_.recurrence == 2 ? opt_.pipe_rr : 0;
+  MCG_CHECK(opt_.recurrence == 2 || opt_.pipe_rr == 0, "pipe_rr needs the pipelined recurrence (2)");
   info_.interleave = opt_.interleave == 1;
 
   // ---- A: count -> scan -> fill (owned rows, ext-local columns) ----
@@ -183,7 +188,7 @@ void GpuCgSolver::setup() {
   // auto: the scrambled random SPD, or a user matrix that is not a grid stencil on the all-gather
   // layout (its columns are scattered over the whole vector); the same decision on every rank
   // (the spec and the layout kind are global)
-  tiles_ = opt_.recurrence == 1 && opt_.pmat != 0 && opt_.tiles != 0 &&
+  tiles_ = opt_.recurrence >= 1 && (opt_.pmat != 0 || opt_.recurrence == 2) && opt_.tiles != 0 &&
            (opt_.tiles == 1 || scrambled(spec_) || (is_user && L_.allgather && stencil_line(spec_) == 0));
   if (is_user) {
     user = build_local_csr(spec_, L_);
@@ -386,7 +391,7 @@ void GpuCgSolver::setup() {
   // must take the same one, whatever its own rows look like
   if (use_comm_ && world_ > 1) pmat_ = all_ranks_agree_(pmat_);
   MCG_CHECK(!aligned_ || pmat_, "aligned SELL needs the split pass");
-  MCG_CHECK(!tiles_ || pmat_, "tiles need the split pass on every rank");
+  MCG_CHECK(!tiles_ || pmat_ || opt_.recurrence == 2, "tiles need the split pass on every rank");
   info_.tiles = tiles_;
   info_.tile_segments = tiles_ ? tgeo_.G : 0;
   if (pmat_) {
@@ -400,6 +405,7 @@ void GpuCgSolver::setup() {
   if (halo_ahead_) prefetch_halo_ = false;
   info_.halo_ahead = halo_ahead_;
   split_ = use_halo_ && opt_.overlap && !halo_ahead_;
+  if (opt_.recurrence == 2) split_ = prefetch_halo_ = false;  // pipelined: the all-reduce is what overlaps
   // all-gather overlap: the own-block slots of each aligned slice are summed while p_k's all-gather
   // is in flight (aligned_ is decided from the spec and the layout is the same kind on every rank,
   // so every rank takes the same launches)
@@ -611,7 +617,7 @@ void GpuCgSolver::setup() {
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
   const bool split = split_;
-  fused_red_ = opt_.recurrence == 1 && opt_.fused_reduce != 0;
+  fused_red_ = (opt_.recurrence == 1 && opt_.fused_reduce != 0) || opt_.recurrence == 2;
   auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
   // the boundary launch's partials start on a reduction-group boundary: round the interior grid up
   // (the extra blocks find no work in the grid-stride loops and contribute zero partials)
@@ -619,14 +625,15 @@ void GpuCgSolver::setup() {
   bnd_base_ = split ? g_int_ : 0;
   const int np = std::max({g_all_, split ? g_int_ + g_bnd_ : 0, g_b_, 1});
   pstride_ = np + 64;
-  partials_.allocate((size_t)pstride_ * (opt_.recurrence == 1 ? 4 : 1), "partials");
+  partials_.allocate((size_t)pstride_ * (opt_.recurrence >= 1 ? 4 : 1), "partials");
   st_.allocate(1, "state");
   MCG_HIP(hipMemsetAsync(partials_.get(), 0, partials_.bytes(), s0_), "device memset failed");
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s0_), "device memset failed");
   if (fused_red_) {
     red_groups_all_ = groups(g_all_);
     red_groups_split_ = split ? groups(g_int_) + groups(g_bnd_) : 0;
-    red_l2s_ = std::max({red_groups_all_, red_groups_split_, 1});
+    red_groups_b_ = groups(g_b_);  // the pipelined update's grid
+    red_l2s_ = std::max({red_groups_all_, red_groups_split_, red_groups_b_, 1});
     red_cnt_.allocate(red_l2s_ + 1, "partials");
     red_l2_.allocate((size_t)4 * red_l2s_, "partials");
     MCG_HIP(hipMemsetAsync(red_cnt_.get(), 0, red_cnt_.bytes(), s0_), "device memset failed");
@@ -642,6 +649,8 @@ void GpuCgSolver::setup() {
   // single-reduction pass: gathers r, Ap, p (ideal 24), writes r, p, Ap 24; x rw 16 + p_{k-2} 8
   // every second pass (paired x updates) = 12 per pass
   if (opt_.recurrence == 1) info_.bytes_per_iter_model = (double)matrix_bytes + 60.0 * n;
+  // pipelined: S reads w (ideal gathers) and writes q (16 B), U reads 7 and writes 6 vectors (104 B)
+  if (opt_.recurrence == 2) info_.bytes_per_iter_model = (double)matrix_bytes + 120.0 * n;
   if (opt_.recurrence == 1) info_.device_bytes += (size_t)(3 * L_.ext_len - n) * 8;
   if (pmat_) {  // U: x rw, r rw, Ap r, p rw = 56 B; S: r, Ap 16 B + one pass over p (ideal gathers) 8 B
     info_.bytes_per_iter_model = (double)matrix_bytes + 80.0 * n;
@@ -680,11 +689,23 @@ bool GpuCgSolver::all_ranks_agree_(bool mine) {
 }
 
 std::vector<DeviceBuffer<double>*> GpuCgSolver::vectors_() {
-  return {&x_, &r_, &r1_, &Ap_, &Ap1_, &ra_[0], &ra_[1], &p_[0], &p_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1]};
+  return {&x_, &r_, &r1_, &Ap_, &Ap1_, &ra_[0], &ra_[1], &p_[0], &p_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1],
+          &w_, &z_, &q_};
 }
 
 void GpuCgSolver::allocate_vectors_() {
   const int64_t n = L_.n_local();
+  if (opt_.recurrence == 2) {  // pipelined: r, w, p, s gathered by SpMVs (ext); x, z, q owned
+    x_.allocate(n, "x", 8);
+    r_.allocate(L_.ext_len, "r", 8);
+    w_.allocate(L_.ext_len, "r", 8);
+    p_[0].allocate(L_.ext_len, "p", 8);
+    Ap_.allocate(L_.ext_len, "Ap", 8);  // s = A p
+    z_.allocate(n, "Ap", 8);
+    q_.allocate(n, "Ap", 8);
+    if (opt_.pipe_rr < 0) xe_.allocate(L_.ext_len, "x", 8);  // x in the ext layout for r = b - A x
+    return;
+  }
   if (pmat_) {  // split pass: r, Ap, x owned only; p once in the ext layout (the only gathered vector)
     x_.allocate(n, "x", 8);
     r_.allocate(n, "r", 8);
@@ -835,13 +856,27 @@ void GpuCgSolver::reset() {
   // on s1_: order the memsets below after it (no write of s0_ may race the side stream's RCCL)
   join_halo_();
   MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
-  for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1]})
+  for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1], &w_, &z_, &q_})
     if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
   MCG_HIP(hipMemsetAsync(p_[0].get(), 0, p_[0].bytes(), s), "device memset failed(p)");
   MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
   // r = b  (CUDACG.cu:248; x0 = 0 so r0 = b - A x0 = b, and p0 = r0 is formed by K_A at k = 0)
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s), "device memset failed");
-  if (pmat_) {
+  if (opt_.recurrence == 2) {
+    // pipelined: r_0 = b, w_0 = A r_0, {gamma_0, delta_0} all-reduced; p = s = z = 0
+    MCG_HIP(hipMemcpyAsync(r_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+            "vector copy failed(r)");
+    if (use_halo_) {
+      double* v[1] = {r_.get()};
+      comm_->halo_exchange(L_, v, 1, s);
+    }
+    spmv_plain_(r_.get(), w_.get() + L_.own_off, s);
+    kern::cg_pipe_dots(r_.get() + L_.own_off, w_.get() + L_.own_off, n, partials_.get(), pstride_, g_b_, st_.get(), 0, s);
+    if (use_comm_) {
+      comm_->allreduce_sum(st_.get()->red, 4, s);
+      comm_->allreduce_sum(&st_.get()->rr_new, 1, s);  // rr0 stays this rank's b.b (rr0_local)
+    }
+  } else if (pmat_) {
     // U_0 forms r_0 = b - 0 * Ap and p_0 = r_0 + 0 * p: r = b, Ap = 0, p = 0
     MCG_HIP(hipMemcpyAsync(r_.get(), b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
             "vector copy failed(r)");
@@ -858,9 +893,11 @@ void GpuCgSolver::reset() {
     MCG_HIP(hipMemcpyAsync(r_.get() + L_.own_off, b_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
             "vector copy failed(r)");
   }
-  kern::dot_partials(b_.get(), b_.get(), n, partials_.get(), g_b_, s);
-  kern::cg_reduce(partials_.get(), g_b_, st_.get(), kReduceInit, 1, opt_.tol, s);
-  if (use_comm_) comm_->allreduce_sum(&st_.get()->rr_new, 1, s);
+  if (opt_.recurrence != 2) {
+    kern::dot_partials(b_.get(), b_.get(), n, partials_.get(), g_b_, s);
+    kern::cg_reduce(partials_.get(), g_b_, st_.get(), kReduceInit, 1, opt_.tol, s);
+    if (use_comm_) comm_->allreduce_sum(&st_.get()->rr_new, 1, s);
+  }
   MCG_HIP(hipStreamSynchronize(s), "compute norm2 failed(r)");
   if (opt_.rtol > 0) {  // relative stopping: tol = rtol * ||b|| (kernels take tol by value: re-capture)
     double rr0 = 0.0;
@@ -1145,8 +1182,88 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
   if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
 }
 
+// y = A x over the owned rows (x in the ext layout, ghosts in place): the format's plain SpMV
+void GpuCgSolver::spmv_plain_(const double* x_ext, double* y, hipStream_t s) {
+  const int64_t n = L_.n_local();
+  if (tiles_) {
+    kern::spmv_tiles(tiles_view(), x_ext, y, g_all_, s);
+  } else if (opt_.format == 1) {
+    kern::spmv_sell(sell_view(), x_ext, y, s);
+  } else if (info_.idx64) {
+    kern::spmv_csr<int64_t>(CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, x_ext, y, s);
+  } else {
+    kern::spmv_csr<int32_t>(CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, x_ext, y, s);
+  }
+}
+
+// Pipelined CG iteration k (cg_pipe.hip): the all-reduce of {gamma_k, delta_k} (left local by the
+// previous update or by a residual replacement) runs on the side stream while S_k = A w_k runs on
+// the compute stream; the update U_k joins it.
+void GpuCgSolver::enqueue_iteration_pipe_(int k) {
+  trace::Range tr_("mcg.iteration.pipelined");
+  const int64_t n = L_.n_local();
+  CgState* st = st_.get();
+  bool ar_side = false;
+  if (use_comm_ && k > 0) {  // reset() left {gamma_0, delta_0} global
+    if (opt_.overlap && !comm_->serialized()) {
+      MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+      MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+      comm_->allreduce_sum(st->red, 4, s1_);
+      MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+      ar_side = true;
+    } else {
+      comm_->allreduce_sum(st->red, 4, s0_);
+    }
+  }
+  if (use_halo_) {  // ghosts of w_k for S_k
+    double* v[1] = {w_.get()};
+    comm_->halo_exchange(L_, v, 1, s0_);
+  }
+  spmv_plain_(w_.get(), q_.get(), s0_);  // S_k (|| the all-reduce)
+  if (ar_side) MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
+  kern::RedCtl rc;
+  rc.cnt = red_cnt_.get();
+  rc.lvl2 = red_l2_.get();
+  rc.l2s = red_l2s_;
+  rc.top = red_l2s_;
+  rc.base = 0;
+  rc.ngroups = red_groups_b_;
+  rc.check = k >= 1 ? 1 : 0;  // the reference never tests r_0
+  rc.first = k == 0 ? 1 : 0;
+  const int64_t o = L_.own_off;
+  kern::PipeVectors v{x_.get(), r_.get() + o, w_.get() + o, p_[0].get() + o, Ap_.get() + o, z_.get(), q_.get()};
+  kern::cg_pipe_update(v, n, partials_.get(), pstride_, g_b_, st, opt_.tol, s0_, rc);
+  const int rr = std::abs(opt_.pipe_rr);
+  if (rr > 0 && (k + 1) % rr == 0) {
+    // replacement of the auxiliary recurrences: w = A r, s = A p, z = A s (their drift removed; r
+    // stays the CG recurrence residual, as in the reference); pipe_rr < 0 also replaces r = b - A x
+    if (opt_.pipe_rr < 0) {
+      double* xv[1] = {xe_.get()};
+      MCG_HIP(hipMemcpyAsync(xe_.get() + o, x_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s0_),
+              "vector copy failed(x)");
+      if (use_halo_) comm_->halo_exchange(L_, xv, 1, s0_);
+      spmv_plain_(xe_.get(), q_.get(), s0_);
+      kern::sub_vec(b_.get(), q_.get(), r_.get() + o, n, s0_);
+    }
+    double* rv[1] = {r_.get()};
+    if (use_halo_) comm_->halo_exchange(L_, rv, 1, s0_);
+    spmv_plain_(r_.get(), w_.get() + o, s0_);
+    double* pv[1] = {p_[0].get()};
+    if (use_halo_) comm_->halo_exchange(L_, pv, 1, s0_);
+    spmv_plain_(p_[0].get(), Ap_.get() + o, s0_);
+    double* sv[1] = {Ap_.get()};
+    if (use_halo_) comm_->halo_exchange(L_, sv, 1, s0_);
+    spmv_plain_(Ap_.get(), z_.get(), s0_);
+    kern::cg_pipe_dots(r_.get() + o, w_.get() + o, n, partials_.get(), pstride_, g_b_, st, 1, s0_);
+  }
+}
+
 void GpuCgSolver::enqueue_iteration_(int k) {
   trace::Range tr_("mcg.iteration");
+  if (opt_.recurrence == 2) {
+    enqueue_iteration_pipe_(k);
+    return;
+  }
   if (opt_.recurrence == 1) {
     enqueue_iteration_f1_(k);
     return;
@@ -1286,7 +1403,8 @@ void GpuCgSolver::run_iterations(int count) {
 void GpuCgSolver::inject_fault_(int k) {
   static const double nan = std::numeric_limits<double>::quiet_NaN();
   if (L_.n_local() == 0 || rank_ != 0) return;
-  double* r = pmat_ ? r_.get()
+  double* r = opt_.recurrence == 2 ? r_.get() + L_.own_off
+              : pmat_ ? r_.get()
               : opt_.interleave == 1 ? ra_[(k + 1) & 1].get() + 2 * L_.own_off  // .x of the first owned pair
                                      : ((opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get()) + L_.own_off;
   MCG_HIP(hipMemcpyAsync(r, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
@@ -1297,6 +1415,11 @@ void GpuCgSolver::finalize() {
   finalized_ = true;  // the single-reduction catch-up of a pending x term must run once
   if (ar_ && use_halo_) ensure_ghosts_(k_);  // the final r_m recomputes Ap_{m-1} over the ghost lines too
   else join_halo_();
+  if (opt_.recurrence == 2) {  // gamma_m of the last update, all-reduced, decides the flag
+    if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
+    kern::cg_pipe_final(st_.get(), opt_.tol, s0_);
+    return;
+  }
   if (pmat_) {  // U in final mode: r_m, x_m and ||r_m||^2, then latch
     kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, L_.n_local(), st_.get(), opt_.tol,
                           0, k_ >= 2 ? 1 : 0, 1, partials_.get(), pstride_, g_b_, s0_);
@@ -1436,7 +1559,7 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
   };
   dump(st_.get(), sizeof(CgState));
   for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1], &ape_[0], &ape_[1],
-                                  &apx_[0], &apx_[1]})
+                                  &apx_[0], &apx_[1], &w_, &z_, &q_})
     dump(b->get(), b->bytes());
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) fail("checkpoint write failed", path);
@@ -1470,7 +1593,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   };
   load(st_.get(), sizeof(CgState));
   for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1], &ape_[0], &ape_[1],
-                                  &apx_[0], &apx_[1]})
+                                  &apx_[0], &apx_[1], &w_, &z_, &q_})
     load(b->get(), b->bytes());
   std::fclose(f);
   if (!ok) fail("checkpoint truncated", path);
@@ -1601,7 +1724,7 @@ CgResult GpuCgSolver::result() {
   r.breakdown = st.breakdown != 0;
   r.beta_clamps = st.clamps;
   r.rr0_local = st.rr0;
-  r.rnorm = std::sqrt(st.done ? st.rr_final : (opt_.recurrence == 1 ? st.red[3] : st.rr_new));
+  r.rnorm = std::sqrt(st.done ? st.rr_final : (opt_.recurrence >= 1 ? st.red[3] : st.rr_new));
   r.setup_seconds = setup_seconds_;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, ev_t0_, ev_t1_) == hipSuccess) r.solve_seconds = ms * 1e-3;
@@ -1631,15 +1754,7 @@ double GpuCgSolver::true_residual_norm() {
     double* v[1] = {xe.get()};
     comm_->halo_exchange(L_, v, 1, s);
   }
-  if (tiles_) {
-    kern::spmv_tiles(tiles_view(), xe.get(), y.get(), g_all_, s);
-  } else if (opt_.format == 1) {
-    kern::spmv_sell(sell_view(), xe.get(), y.get(), s);
-  } else if (info_.idx64) {
-    kern::spmv_csr<int64_t>(CsrDev<int64_t>{rp64_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
-  } else {
-    kern::spmv_csr<int32_t>(CsrDev<int32_t>{rp32_.get(), cols_.get(), vals_.get(), n}, xe.get(), y.get(), s);
-  }
+  spmv_plain_(xe.get(), y.get(), s);
   kern::xpby(b_.get(), -1.0, y.get(), n, s);  // y = b - A x
   kern::dot_partials(y.get(), y.get(), n, partials_.get(), g_b_, s);
   kern::sum_partials(partials_.get(), g_b_, out.get(), s);

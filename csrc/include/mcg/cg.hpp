@@ -30,7 +30,10 @@ struct CgOptions {
   int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
   int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector, 4 row-length adaptive per
                              // tile (direct or 16 lanes per row); -1 = auto (1 when every row has <= 16 entries, else 4)
-  int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass
+  int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass,
+                             // 2 = pipelined CG (Ghysels-Vanroose: the all-reduce overlaps the SpMV; cg_pipe.hip)
+  int pipe_rr = 0;           // pipelined CG: every |k| iterations recompute w = A r, s = A p, z = A s (their
+                             // recurrences drift); k < 0 also replaces r = b - A x (true residual); 0 = off
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
   int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.

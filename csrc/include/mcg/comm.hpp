@@ -121,11 +121,13 @@ class NullComm final : public Communicator {
 
 // Latency rehearsal: like NullComm, but every all-reduce and halo exchange costs a fixed
 // device-side delay (a one-workgroup spin of `us` microseconds on the stream it is enqueued on),
-// so the time an iteration spends waiting for a collective can be priced on one GPU.
+// so the time an iteration spends waiting for a collective can be priced on one GPU.  `fat` spins
+// with ~270 VGPRs per wave, RCCL's own kernel footprint (profiles/r3_corun_root_cause.md): such a
+// wave cannot be placed next to a resident pass, the thin one (6 VGPRs) can.
 class DelayComm final : public Communicator {
  public:
-  DelayComm(int rank, int world, double allreduce_us, double halo_us)
-      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us) {}
+  DelayComm(int rank, int world, double allreduce_us, double halo_us, bool fat = false)
+      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us), fat_(fat) {}
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   void allreduce_sum(double*, size_t, hipStream_t stream) override;
@@ -135,6 +137,7 @@ class DelayComm final : public Communicator {
  private:
   int rank_, world_;
   double ar_us_, halo_us_;
+  bool fat_;
 };
 
 // Shared state of P in-process ranks on one device.

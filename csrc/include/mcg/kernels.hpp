@@ -352,6 +352,22 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
                          hipStream_t stream, const RedCtl& rc = RedCtl());
 void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream);
 
+// ---- pipelined CG (csrc/gpu/cg_pipe.hip), recurrence = 2 ----
+// owned-row pointers: x, z, q owned vectors; r, w, p, s the owned parts of ext-layout vectors
+struct PipeVectors {
+  double *x, *r, *w, *p, *s, *z;
+  const double* q;
+};
+// U_i: the vector recurrences with alpha_i / beta_i from CgState (red = the all-reduced {gamma_i, delta_i}),
+// the latch on gamma_i (rc.check), and {gamma_{i+1}, delta_{i+1}} reduced in the kernel (rc over `grid`)
+void cg_pipe_update(const PipeVectors& v, int64_t n, double* partials, int pstride, int grid, CgState* st, double tol,
+                    hipStream_t stream, const RedCtl& rc);
+// local {r.r, w.r} -> CgState::red (mode 0: the initial state, mode 1: after a residual replacement)
+void cg_pipe_dots(const double* r, const double* w, int64_t n, double* partials, int pstride, int grid, CgState* st,
+                  int mode, hipStream_t stream);
+void cg_pipe_final(CgState* st, double tol, hipStream_t stream);  // latch after the last update
+void sub_vec(const double* b, const double* y, double* out, int64_t n, hipStream_t stream);  // out = b - y
+
 // out[i] = {a[i], 0} (seeds the interleaved {r, Ap} layout)
 void pack_pairs(const double* a, double2* out, int64_t n, hipStream_t stream);
 // modes: 0 = after a fused pass (conv check on the previous rr, sum 4 partials),

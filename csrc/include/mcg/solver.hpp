@@ -46,6 +46,7 @@ struct SolverInfo {
   int64_t max_row_len = 0;
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
+  int pipe_rr = 0;  // pipelined CG: residual-replacement period (0 = none)
   bool interleave = false;
   int window = 0;  // LDS window width (doubles) of the windowed pass; 0 = off
   bool pipeline = false;
@@ -118,6 +119,8 @@ class GpuCgSolver {
   void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
   void enqueue_iteration_split_(int k);                   // materialized-p split pass (pmat_)
+  void enqueue_iteration_pipe_(int k);                    // pipelined CG (recurrence 2)
+  void spmv_plain_(const double* x_ext, double* y, hipStream_t s);  // y = A x, the format's plain SpMV
   void enqueue_split_spmv_(int k, int which, bool fused_red, int part = 0);  // part: cg_split_spmv
   void capture_pair_(int kind);
   void join_halo_();            // s0_ waits for a halo in flight on s1_
@@ -218,6 +221,7 @@ class GpuCgSolver {
   // vectors
   DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
+  DeviceBuffer<double> w_, z_, q_, xe_;  // pipelined CG: w = A r (ext), z = A s, q = A w, x in the ext layout
   DeviceBuffer<double> ra_[2];     // interleaved {r, Ap} pairs by parity (2 * ext_len doubles each)
   DeviceBuffer<uint32_t> smeta_;  // Ap-recomputing carry: per-slice (first slot / 64 | width << 28)
   DeviceBuffer<double> ape_[2];    // Ap-recomputing carry: Ap of the slices' edge rows, by parity
@@ -226,7 +230,7 @@ class GpuCgSolver {
   int bnd_base_ = 0;               // first partial slot of the boundary launch (a multiple of kRedGroup)
   bool fused_red_ = false;         // in-kernel reduction of the fused pass (CgOptions::fused_reduce)
   bool pmat_ = false;              // materialized-p split pass (CgOptions::pmat)
-  int red_groups_all_ = 0, red_groups_split_ = 0, red_l2s_ = 0;
+  int red_groups_all_ = 0, red_groups_split_ = 0, red_groups_b_ = 0, red_l2s_ = 0;
   DeviceBuffer<unsigned> red_cnt_;  // group counters + top counter (zeroed at setup, reset by the kernels)
   DeviceBuffer<double> red_l2_;     // [4][red_l2s_] group sums
   DeviceBuffer<CgState> st_;

@@ -205,6 +205,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("tiles", &CgOptions::tiles)
       .def_readwrite("tile_seg_log2", &CgOptions::tile_seg_log2)
       .def_readwrite("tile_pace", &CgOptions::tile_pace)
+      .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       .def_readwrite("pmat", &CgOptions::pmat)
       .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
@@ -330,8 +331,8 @@ PYBIND11_MODULE(_C, m) {
   py::class_<DelayComm, std::shared_ptr<DelayComm>>(m, "DelayComm",
                                                     "one rank of a P-rank run whose all-reduce / halo cost a fixed "
                                                     "device-side delay and move nothing (latency rehearsal)")
-      .def(py::init<int, int, double, double>(), py::arg("rank"), py::arg("world"), py::arg("allreduce_us"),
-           py::arg("halo_us") = 0.0);
+      .def(py::init<int, int, double, double, bool>(), py::arg("rank"), py::arg("world"), py::arg("allreduce_us"),
+           py::arg("halo_us") = 0.0, py::arg("fat") = false);
 
   py::class_<GpuCgSolver>(m, "Solver")
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<Comm> comm) {
@@ -393,7 +394,8 @@ PYBIND11_MODULE(_C, m) {
         d["idx64"] = i.idx64;
         d["format"] = i.format == 5 ? "tiles" : i.format == 4 ? "sell64-aligned"
                       : i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
-        d["recurrence"] = i.recurrence == 1 ? "single-reduction" : "two-reduction";
+        d["recurrence"] = i.recurrence == 2 ? "pipelined" : i.recurrence == 1 ? "single-reduction" : "two-reduction";
+        d["pipe_rr"] = i.pipe_rr;
         d["interleave"] = i.interleave;
         d["window"] = i.window;
         d["pipeline"] = i.pipeline;

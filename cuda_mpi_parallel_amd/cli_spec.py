@@ -40,7 +40,8 @@ FLAGS = [
     ("--watchdog", "0", "> 0: fail (and abort RCCL) when a poll interval makes no progress for S seconds"),
     # solver form / kernels
     ("--format", "csr", "csr | sell | sell16 | sellc8"),
-    ("--recurrence", "auto", "auto | two | single"),
+    ("--recurrence", "auto", "auto | two | single | pipelined"),
+    ("--pipe-rr", "0", "pipelined CG: residual replacement every K iterations (0 = off)"),
     ("--interleave", "auto", TRI + ": {r, Ap} 16-B pairs (single-reduction SELL)"),
     ("--window", "auto", TRI + ": LDS column windows (long banded rows)"),
     ("--carry", "auto", TRI + ": line-carry stencil pass"),
@@ -85,4 +86,6 @@ def recurrence(v: str) -> int:
         return 1
     if v in ("two", "0"):
         return 0
-    raise ValueError(f"expected auto|two|single, got {v!r}")
+    if v in ("pipelined", "2"):
+        return 2
+    raise ValueError(f"expected auto|two|single|pipelined, got {v!r}")

@@ -1,0 +1,185 @@
+"""Pipelined CG (Ghysels-Vanroose, recurrence=2, csrc/gpu/cg_pipe.hip): the opt-in form whose one
+all-reduce per iteration overlaps the SpMV q = A w.
+
+Reference anchors: the reference's two blocking reductions per iteration (CUDACG.cu:304, :328) and
+its stop test ||r|| < tol after the x/r update (:333) -- the pipelined form keeps the stop rule and
+the iteration count (x_k after k SpMVs of the recurrence) and checks against the same CPU oracle
+(op-for-op CUDACG.cu:269-352).  Its extra recurrences (w = A r, s = A p, z = A s) drift in fp64, so
+`pipe_rr` recomputes them from x and p every k iterations (residual replacement).
+"""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("poisson2d", dict(n=128), dict(format="sellc8")),
+    ("poisson3d", dict(n=24), dict(format="sell16")),
+    ("poisson2d", dict(n=96), dict(format="csr")),
+    ("randspd", dict(rows=20000, band=40, density=0.4, scramble=1), dict(format="sell", tiles=1, tile_seg_log2=12)),
+]
+
+
+def _cpu(mcg, spec, **kw):
+    C = mcg.native()
+    return C.cpu_cg(spec.native(), C.CgOptions(**{"maxit": 2000, "tol": 1e-7, **kw}))
+
+
+@pytest.mark.parametrize("rr", [0, 25, -25])
+@pytest.mark.parametrize("problem,kw,skw", CASES)
+def test_pipelined_matches_cpu_oracle(mcg, problem, kw, skw, rr):
+    spec = mcg.make_problem(problem, **kw)
+    s = mcg.CGSolver(spec, recurrence=2, pipe_rr=rr, check_every=8, **skw)
+    assert s.info["recurrence"] == "pipelined" and s.info["pipe_rr"] == rr
+    if skw.get("tiles"):
+        assert s.info["tiles"]
+    out = s.solve()
+    cpu = _cpu(mcg, spec)
+    assert out["converged"] and cpu["converged"]
+    assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    tr = s.true_residual_norm()
+    assert tr < 1e-6
+    if rr:  # the replaced residual is the true one, up to the iterations since the last replacement
+        assert abs(tr - out["rnorm"]) <= 1e-3 * tr + 1e-9
+
+
+@pytest.mark.parametrize("problem,kw,skw", CASES[:2])
+def test_pipelined_bitwise_repeatable_and_graph_equals_eager(mcg, problem, kw, skw):
+    """Fixed-order in-kernel fan-in: the same bits however the blocks are scheduled, graph or eager."""
+    spec = mcg.make_problem(problem, **kw)
+    outs = []
+    for graph in (True, True, False):
+        outs.append(mcg.CGSolver(spec, recurrence=2, use_graph=graph, check_every=8, **skw).solve())
+    for o in outs[1:]:
+        assert o["iterations"] == outs[0]["iterations"] and o["rnorm"] == outs[0]["rnorm"]
+        np.testing.assert_array_equal(o["x_local"], outs[0]["x_local"])
+
+
+def test_pipelined_rccl_allreduce_on_side_stream(mcg):
+    """force_comm at one rank: the 32-B RCCL all-reduce runs on the side stream next to q = A w
+    (captured into the graphs) and gives the same bits as the communicator-free run."""
+    spec = mcg.make_problem("poisson2d", n=128)
+    plain = mcg.CGSolver(spec, recurrence=2, check_every=8).solve()
+    s = mcg.CGSolver(spec, recurrence=2, check_every=8, force_comm=True)
+    out = s.solve()
+    assert s.info["graph_fallbacks"] == 0
+    assert out["iterations"] == plain["iterations"] and out["rnorm"] == plain["rnorm"]
+    np.testing.assert_array_equal(out["x_local"], plain["x_local"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("problem,kw,fmt", [("poisson2d", dict(n=64), "sellc8"), ("poisson3d", dict(n=16), "csr"),
+                                            ("randspd", dict(rows=6000, band=30, density=0.3), "sell16")])
+def test_pipelined_local_ranks_match_cpu(mcg, world, problem, kw, fmt):
+    """P in-process ranks (LocalComm): halo of w and of the replacement vectors, the all-reduce on
+    the side stream, and the latch agreement."""
+    spec = mcg.make_problem(problem, **kw)
+    C = mcg.native()
+    cpu = _cpu(mcg, spec)
+    o = C.CgOptions(maxit=2000, tol=1e-7, format=fmt, recurrence=2, check_every=4)
+    o.pipe_rr = 20
+    out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    its = {r["iterations"] for r in out["ranks"]}
+    assert len(its) == 1, its
+    assert abs(its.pop() - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in out["ranks"])
+
+
+def test_pipelined_local_ranks_fixed_iterations_agree_with_single_rank(mcg):
+    spec = mcg.make_problem("poisson2d", n=256)
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sell16", recurrence=2)
+    o.pipe_rr = 16
+    one = C.run_local_ranks(spec.native(), o, 1, 40, True)
+    four = C.run_local_ranks(spec.native(), o, 4, 40, True)
+    r1, r4 = one["ranks"][0]["rnorm"], four["ranks"][0]["rnorm"]
+    assert abs(r1 - r4) <= 1e-9 * r1
+    np.testing.assert_allclose(four["x"], one["x"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.fixture(scope="module")
+def cpu_2000(mcg):
+    """CPU oracle at BASELINE config 1's size: 1024^2 5-pt Poisson, 2000 iterations, no stop."""
+    C = mcg.native()
+    spec = mcg.make_problem("poisson2d", n=1024, rhs="random")
+    return spec, C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=-1.0))
+
+
+@pytest.mark.parametrize("rr", [10, 25, 50])
+def test_2000_iterations_pipelined_track_cpu_oracle(mcg, cpu_2000, rr):
+    """The residual every 250th iteration against the reference recurrence over its full maxit
+    (<= 1e-8 relative), w, s, z recomputed every `rr` iterations.  Measured
+    (profiles/r3_pipelined_cg.md): worst gap 3e-11 / 8e-11 / 1.7e-9 at rr 10 / 25 / 50; without
+    replacement the drift of the extra recurrences reaches 4e-4 by iteration 2000, and replacing r
+    by b - A x too (rr < 0) follows the true residual rather than the reference's recurrence
+    (1e-7)."""
+    spec, cpu = cpu_2000
+    hist = np.asarray(cpu["rnorm_history"])
+    s = mcg.CGSolver(spec, recurrence=2, pipe_rr=rr, tol=-1.0, maxit=2000, format="sellc8")
+    s.reset()
+    worst = 0.0
+    for m in range(250, 2001, 250):
+        s.run(250)
+        s.synchronize()
+        out = s.result()
+        assert out["iterations"] == m
+        rel = abs(out["rnorm"] - hist[m - 1]) / hist[m - 1]
+        worst = max(worst, rel)
+        print(f"rr={rr} m={m} rel={rel:.3e}")
+    s.finalize()
+    x = s.x_local()
+    np.testing.assert_allclose(x, cpu["x"], rtol=1e-8, atol=1e-8 * np.abs(cpu["x"]).max())
+    tr = s.true_residual_norm()
+    print(f"pipelined rr={rr}: worst residual-history gap {worst:.3e}, true {tr:.3e} vs oracle {hist[-1]:.3e}")
+    assert worst <= 1e-8
+
+
+def _ms_per_iter(mcg, spec, recurrence, delay_us, fat=False, iters=320, fmt="sellc8"):
+    C = mcg.native()
+    o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, format=fmt, recurrence=recurrence)
+    comm = C.DelayComm(3, 8, delay_us, 0.0, fat)
+    s = C.Solver(spec.native(), o, 3, 8, comm)
+    s.setup()
+    s.reset()
+    s.run_iterations(64)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.run_iterations(iters)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    s.finalize()
+    res = s.result()
+    assert res["iterations"] == 64 + iters and not res["breakdown"]
+    return 1e3 * dt / iters
+
+
+def test_pipelined_hides_allreduce_latency_at_p8_share(mcg):
+    """Rank 3 of a P = 8 run of the 4096^2 Poisson problem on one GPU, each all-reduce a device-side
+    delay (DelayComm: a one-workgroup spin on the stream the collective would run on).  In the
+    single-reduction form every microsecond of delay is on the critical path; in the pipelined form
+    the delay runs on the side stream next to q = A w, so its iteration time grows by less (measured
+    +41 vs +24..30 us for a 40 us all-reduce, profiles/r3_pipelined_cg.md)."""
+    spec = mcg.make_problem("poisson2d", n=4096, rhs="random")
+    d = 40.0
+    t1_0, t1_d = _ms_per_iter(mcg, spec, 1, 0.0), _ms_per_iter(mcg, spec, 1, d)
+    t2_0, t2_d = _ms_per_iter(mcg, spec, 2, 0.0), _ms_per_iter(mcg, spec, 2, d)
+    g1, g2 = (t1_d - t1_0) * 1e3, (t2_d - t2_0) * 1e3
+    print(f"single-reduction {t1_0 * 1e3:.1f} -> {t1_d * 1e3:.1f} us (+{g1:.1f}); "
+          f"pipelined {t2_0 * 1e3:.1f} -> {t2_d * 1e3:.1f} us (+{g2:.1f}) for a {d:.0f} us all-reduce")
+    assert g1 >= 0.8 * d  # the single-reduction pass waits for every all-reduce
+    assert g2 < g1
+
+
+def test_pipelined_faster_under_latency_on_heavy_rows(mcg):
+    """Where the pipelined form pays: rank 3 of P = 8 on a 1e6-row random SPD matrix (~65 nonzeros
+    a row: the SpMV, not the 104 B/row update, dominates).  With a 40 us all-reduce it beats the
+    single-reduction form (measured 55 vs 73 us an iteration)."""
+    spec = mcg.make_problem("randspd", rows=1_000_000, band=64, density=0.5, rhs="random")
+    t1 = _ms_per_iter(mcg, spec, 1, 40.0, fmt="sell16")
+    t2 = _ms_per_iter(mcg, spec, 2, 40.0, fmt="sell16")
+    print(f"40 us all-reduce: single-reduction {t1 * 1e3:.1f} us, pipelined {t2 * 1e3:.1f} us an iteration")
+    assert t2 < 0.9 * t1
