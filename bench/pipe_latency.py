@@ -69,7 +69,8 @@ def main():
                                a.pipe_rr if rec == 2 else 0)
         print(json.dumps({"recurrence": info["recurrence"], "graph": g, "overlap": ov, "fat": fat, "delay_us": d,
                           "us_per_iter": round(us, 2), "graph_fallbacks": info.get("graph_fallbacks"),
-                          "pipe_rr": info.get("pipe_rr"), "format": info["format"], "carry": info.get("carry"), "pmat": info.get("pmat"),
+                          "pipe_rr": info.get("pipe_rr"), "ar_first": info.get("pipe_ar_first"),
+                          "t_spmv": round(info.get("pipe_spmv_us", 0), 1), "t_ar": round(info.get("pipe_allreduce_us", 0), 1), "format": info["format"], "carry": info.get("carry"), "pmat": info.get("pmat"),
                           "problem": a.problem}),
               flush=True)
 

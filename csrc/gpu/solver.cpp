@@ -671,8 +671,37 @@ void GpuCgSolver::setup() {
   // vectors allocated with room for the placement probe's start offsets hold that headroom too
   for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->lead_capacity() * sizeof(double);
   probe_placement_();
+  if (opt_.recurrence == 2) pick_pipe_order_();
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();
+}
+
+// Pipelined CG: which branch of the fork after U_{k-1} -- S_k or the all-reduce -- is enqueued first.
+// A graph runs a node's first-created child on the parent's queue and the others on helper queues,
+// and a dependency across queues costs 5-11 us here (rocprofv3 kernel trace, profiles/
+// r3_pipelined_cg.md), so the longer branch stays on the launch queue.  Both are timed once (3
+// launches after a warm-up; the all-reduce is collective, so every rank times it at this point of
+// setup).  The order changes scheduling only, never the arithmetic: ranks may decide differently.
+void GpuCgSolver::pick_pipe_order_() {
+  pipe_ar_first_ = false;
+  if (!(use_comm_ && opt_.overlap && !comm_->serialized())) return;
+  Event a(true, true), b(true, true);
+  auto time_us = [&](auto&& f) {
+    f();
+    MCG_HIP(hipEventRecord(a, s0_), "event record failed");
+    for (int i = 0; i < 3; ++i) f();
+    MCG_HIP(hipEventRecord(b, s0_), "event record failed");
+    MCG_HIP(hipEventSynchronize(b), "event synchronize failed");
+    float ms = 0.f;
+    MCG_HIP(hipEventElapsedTime(&ms, a, b), "event elapsed time failed");
+    return 1e3 * ms / 3.0;
+  };
+  const double t_s = time_us([&] { spmv_plain_(w_.get(), q_.get(), s0_); });
+  const double t_ar = time_us([&] { comm_->allreduce_sum(st_.get()->red, 4, s0_); });
+  pipe_ar_first_ = t_ar > t_s;
+  info_.pipe_ar_first = pipe_ar_first_;
+  info_.pipe_spmv_us = t_s;
+  info_.pipe_allreduce_us = t_ar;
 }
 
 // true iff `mine` is true on every rank (one all-reduce of a flag at setup; not in the loop)
@@ -1203,23 +1232,23 @@ void GpuCgSolver::enqueue_iteration_pipe_(int k) {
   trace::Range tr_("mcg.iteration.pipelined");
   const int64_t n = L_.n_local();
   CgState* st = st_.get();
-  bool ar_side = false;
-  if (use_comm_ && k > 0) {  // reset() left {gamma_0, delta_0} global
-    if (opt_.overlap && !comm_->serialized()) {
-      MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
-      MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
-      comm_->allreduce_sum(st->red, 4, s1_);
-      MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
-      ar_side = true;
-    } else {
-      comm_->allreduce_sum(st->red, 4, s0_);
-    }
-  }
+  // the all-reduce needs only U_{k-1}: forked after it onto the side stream, joined before U_k;
+  // the longer of the two branches is enqueued first (pick_pipe_order_)
+  const bool ar_side = use_comm_ && k > 0 && opt_.overlap && !comm_->serialized();
+  if (use_comm_ && k > 0 && !ar_side) comm_->allreduce_sum(st->red, 4, s0_);  // reset() left k = 0's global
+  if (ar_side) MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+  auto fork_ar = [&] {
+    MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+    comm_->allreduce_sum(st->red, 4, s1_);
+    MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+  };
+  if (ar_side && pipe_ar_first_) fork_ar();
   if (use_halo_) {  // ghosts of w_k for S_k
     double* v[1] = {w_.get()};
     comm_->halo_exchange(L_, v, 1, s0_);
   }
   spmv_plain_(w_.get(), q_.get(), s0_);  // S_k (|| the all-reduce)
+  if (ar_side && !pipe_ar_first_) fork_ar();
   if (ar_side) MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
   kern::RedCtl rc;
   rc.cnt = red_cnt_.get();

@@ -47,6 +47,8 @@ struct SolverInfo {
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
   int pipe_rr = 0;  // pipelined CG: residual-replacement period (0 = none)
+  bool pipe_ar_first = false;  // pipelined CG: the all-reduce branch is enqueued before S (it took longer)
+  double pipe_spmv_us = 0.0, pipe_allreduce_us = 0.0;  // the two branch times measured at setup
   bool interleave = false;
   int window = 0;  // LDS window width (doubles) of the windowed pass; 0 = off
   bool pipeline = false;
@@ -120,6 +122,7 @@ class GpuCgSolver {
   void enqueue_iteration_f1_(int k);
   void enqueue_iteration_split_(int k);                   // materialized-p split pass (pmat_)
   void enqueue_iteration_pipe_(int k);                    // pipelined CG (recurrence 2)
+  void pick_pipe_order_();                                // pipelined CG: which fork branch goes first
   void spmv_plain_(const double* x_ext, double* y, hipStream_t s);  // y = A x, the format's plain SpMV
   void enqueue_split_spmv_(int k, int which, bool fused_red, int part = 0);  // part: cg_split_spmv
   void capture_pair_(int kind);
@@ -221,6 +224,7 @@ class GpuCgSolver {
   // vectors
   DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
+  bool pipe_ar_first_ = false;
   DeviceBuffer<double> w_, z_, q_, xe_;  // pipelined CG: w = A r (ext), z = A s, q = A w, x in the ext layout
   DeviceBuffer<double> ra_[2];     // interleaved {r, Ap} pairs by parity (2 * ext_len doubles each)
   DeviceBuffer<uint32_t> smeta_;  // Ap-recomputing carry: per-slice (first slot / 64 | width << 28)

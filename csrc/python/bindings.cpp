@@ -396,6 +396,9 @@ PYBIND11_MODULE(_C, m) {
                       : i.format == 3 ? "sell64-c8" : (i.format == 2 ? "sell64-d16" : (i.format == 1 ? "sell64" : "csr"));
         d["recurrence"] = i.recurrence == 2 ? "pipelined" : i.recurrence == 1 ? "single-reduction" : "two-reduction";
         d["pipe_rr"] = i.pipe_rr;
+        d["pipe_ar_first"] = i.pipe_ar_first;
+        d["pipe_spmv_us"] = i.pipe_spmv_us;
+        d["pipe_allreduce_us"] = i.pipe_allreduce_us;
         d["interleave"] = i.interleave;
         d["window"] = i.window;
         d["pipeline"] = i.pipeline;
