@@ -103,8 +103,8 @@ Args parse(int argc, char** argv) {
       std::string v = need(i);
       a.opt.halo_mode = v == "window" ? 0 : (v == "allgather" ? 1 : tri(v, "--halo-mode"));
     }
-    else if (f == "--pmat") a.opt.pmat = tri(need(i), "--pmat");
-    else if (f == "--fused-reduce") a.opt.fused_reduce = tri(need(i), "--fused-reduce");
+    else if (f == "--pmat") a.opt.form.pmat = tri(need(i), "--pmat");
+    else if (f == "--fused-reduce") a.opt.form.fused_reduce = tri(need(i), "--fused-reduce");
     else if (f == "--rhs") { a.spec.rhs = parse_rhs_kind(need(i)); a.rhs_set = true; }
     else if (f == "--seed") a.spec.seed = std::stoull(need(i));
     else if (f == "--gpus") a.gpus = std::stoi(need(i));
@@ -139,7 +139,7 @@ Args parse(int argc, char** argv) {
     else if (f == "--checkpoint") a.opt.checkpoint_path = need(i);
     else if (f == "--checkpoint-every") a.opt.checkpoint_every = std::stoi(need(i));
     else if (f == "--resume") a.resume = need(i);
-    else if (f == "--inject-nan-at") a.opt.inject_nan_at = std::stoi(need(i));
+    else if (f == "--inject-nan-at") a.opt.hooks.inject_nan_at = std::stoi(need(i));
     else if (f == "--recurrence") {
       std::string v = need(i);
       if (v == "auto" || v == "-1") a.opt.recurrence = -1;
@@ -150,9 +150,9 @@ Args parse(int argc, char** argv) {
       a.recurrence_set = true;
     }
     else if (f == "--pipe-rr") a.opt.pipe_rr = std::stoi(need(i));
-    else if (f == "--window") a.opt.window = tri(need(i), "--window");
-    else if (f == "--carry") a.opt.carry = tri(need(i), "--carry");
-    else if (f == "--interleave") a.opt.interleave = tri(need(i), "--interleave");
+    else if (f == "--window") a.opt.form.window = tri(need(i), "--window");
+    else if (f == "--carry") a.opt.form.carry = tri(need(i), "--carry");
+    else if (f == "--interleave") a.opt.form.interleave = tri(need(i), "--interleave");
     else if (f == "--print-x") a.print_x = need(i);
     else if (f == "--report") a.report = need(i);
     else if (f == "--verify") a.verify = true;

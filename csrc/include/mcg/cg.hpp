@@ -16,24 +16,12 @@
 
 namespace mcg {
 
-struct CgOptions {
-  int maxit = 2000;          // CUDACG.cu:244
-  double tol = 1e-7;         // CUDACG.cu:245 (absolute ||r||_2)
-  double rtol = 0.0;         // > 0: stop on ||r||_2 < rtol * ||b||_2 instead (the "relative" of the comment at :238)
-  int check_every = 32;      // host polls the device convergence latch every k iterations
-  bool overlap = true;       // halo on a side stream, overlapped with the interior SpMV
-  bool use_graph = true;     // capture iteration pairs into a hipGraph
+// Pass-form overrides.  Every field's default is the dispatcher's automatic choice (the measured
+// fastest form for the matrix, rank layout and recurrence); setting one forces a form on or off for
+// tests, sweeps and A/B measurements.  None changes the arithmetic of CG, only how a pass is built.
+struct PassForm {
   int graph_iters = 32;      // iterations per graph launch (even, >= 2); the last < graph_iters run as pairs
                              // (32 vs 2: 4096^2 4700 -> 5025 it/s, profiles/r1_graph_iters.log)
-  bool force_comm = false;   // run RCCL collectives even with one rank
-  int format = 0;            // 0 = CSR, 1 = SELL-64
-  int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
-  int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector, 4 row-length adaptive per
-                             // tile (direct or 16 lanes per row); -1 = auto (1 when every row has <= 16 entries, else 4)
-  int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass,
-                             // 2 = pipelined CG (Ghysels-Vanroose: the all-reduce overlaps the SpMV; cg_pipe.hip)
-  int pipe_rr = 0;           // pipelined CG: every |k| iterations recompute w = A r, s = A p, z = A s (their
-                             // recurrences drift); k < 0 also replaces r = b - A x (true residual); 0 = off
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
   int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
@@ -48,8 +36,6 @@ struct CgOptions {
   int placement_leads = 8;   // ... times this many start offsets of the vectors inside their allocations
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
-  int halo_mode = -1;        // ghosts: 0 = column-window ranges (p2p send/recv), 1 = all-gather of equal row blocks
-                             // (unstructured sparsity), -1 = auto (partition_rows)
   int pmat = -1;             // single-reduction form: materialized-p split pass (update kernel + SpMV gathering the
                              // stored p only; cg_split.hip) — the irregular-sparsity path; -1 = auto (long rows
                              // without an LDS window, or the all-gather layout), 0 = off, 1 = on
@@ -94,13 +80,39 @@ struct CgOptions {
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's
                              // kernels cannot start next to a resident pass (profiles/r2_corun_probe.md), so
                              // the split never overlapped; -1 = auto (on when the halo overlap is on), 0 = off
+};
+
+// Test and fault-injection hooks (never set in production runs).
+struct TestHooks {
   int fail_graph_launch_at = -1;  // test hook: report the graph launch at this iteration as failed (nothing enqueued)
-  int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
-  std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   int force_idx64 = 0;       // test hook: int64 row pointers even when int32 would do
   int inject_nan_at = -1;    // fault-injection hook: poison r at this iteration (breakdown detection test)
+};
+
+struct CgOptions {
+  int maxit = 2000;          // CUDACG.cu:244
+  double tol = 1e-7;         // CUDACG.cu:245 (absolute ||r||_2)
+  double rtol = 0.0;         // > 0: stop on ||r||_2 < rtol * ||b||_2 instead (the "relative" of the comment at :238)
+  int check_every = 32;      // host polls the device convergence latch every k iterations
+  bool overlap = true;       // halo on a side stream, overlapped with the interior SpMV
+  bool use_graph = true;     // capture iteration pairs into a hipGraph
+  bool force_comm = false;   // run RCCL collectives even with one rank
+  int format = 0;            // 0 = CSR, 1 = SELL-64
+  int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
+  int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector, 4 row-length adaptive per
+                             // tile (direct or 16 lanes per row); -1 = auto (1 when every row has <= 16 entries, else 4)
+  int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass,
+                             // 2 = pipelined CG (Ghysels-Vanroose: the all-reduce overlaps the SpMV; cg_pipe.hip)
+  int pipe_rr = 0;           // pipelined CG: every |k| iterations recompute w = A r, s = A p, z = A s (their
+                             // recurrences drift); k < 0 also replaces r = b - A x (true residual); 0 = off
+  int halo_mode = -1;        // ghosts: 0 = column-window ranges (p2p send/recv), 1 = all-gather of equal row blocks
+                             // (unstructured sparsity), -1 = auto (partition_rows)
+  int checkpoint_every = 0;  // > 0: solve() writes a checkpoint every ~k iterations (at poll points)
+  std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   double watchdog_seconds = 0.0;  // > 0: solve() fails (and aborts the communicator) if one poll interval
                                   // makes no progress for this long (bounded host wait)
+  PassForm form;             // pass-form overrides (auto by default)
+  TestHooks hooks;           // test / fault-injection hooks
 };
 
 struct CgResult {

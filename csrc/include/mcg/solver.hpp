@@ -194,8 +194,8 @@ class GpuCgSolver {
     t.nblocks = tgeo_.nblocks;
     t.G = tgeo_.G;
     t.seg_shift = tgeo_.seg_shift;
-    t.pace = opt_.tile_pace > 0 ? tpace_.get() : nullptr;
-    t.pace_slack8 = opt_.tile_pace == 2 ? 1 : 0;
+    t.pace = opt_.form.tile_pace > 0 ? tpace_.get() : nullptr;
+    t.pace_slack8 = opt_.form.tile_pace == 2 ? 1 : 0;
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)

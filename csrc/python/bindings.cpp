@@ -189,38 +189,44 @@ PYBIND11_MODULE(_C, m) {
          "ProblemSpec of kind csr over this matrix (the spec keeps the matrix alive)");
   m.def("read_vector", &read_vector, "dense vector: Matrix Market array file or one value per line");
 
+  // the pass-form overrides and test hooks live in CgOptions::form / ::hooks (cg.hpp); Python sees
+  // them as flat attributes of CgOptions (opts.carry = 0), the C++ CLI as --carry / --pmat / ...
+#define MCG_FORM_PROP(n) \
+  .def_property(#n, [](const CgOptions& o) { return o.form.n; }, [](CgOptions& o, decltype(PassForm::n) v) { o.form.n = v; })
+#define MCG_HOOK_PROP(n) \
+  .def_property(#n, [](const CgOptions& o) { return o.hooks.n; }, [](CgOptions& o, decltype(TestHooks::n) v) { o.hooks.n = v; })
   py::class_<CgOptions>(m, "CgOptions")
       .def(py::init(&make_opts), py::arg("maxit") = 2000, py::arg("tol") = 1e-7, py::arg("check_every") = 32,
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("force_comm") = false,
            py::arg("format") = "csr", py::arg("blocks_per_cu") = 0, py::arg("spmv_variant") = -1,
            py::arg("recurrence") = 0)
       .def_readwrite("recurrence", &CgOptions::recurrence)
-      .def_readwrite("interleave", &CgOptions::interleave)
-      .def_readwrite("window", &CgOptions::window)
-      .def_readwrite("pipeline", &CgOptions::pipeline)
-      .def_readwrite("carry", &CgOptions::carry)
-      .def_readwrite("placement_tries", &CgOptions::placement_tries)
-      .def_readwrite("placement_leads", &CgOptions::placement_leads)
-      .def_readwrite("fused_reduce", &CgOptions::fused_reduce)
-      .def_readwrite("tiles", &CgOptions::tiles)
-      .def_readwrite("tile_seg_log2", &CgOptions::tile_seg_log2)
-      .def_readwrite("tile_pace", &CgOptions::tile_pace)
+      MCG_FORM_PROP(interleave)
+      MCG_FORM_PROP(window)
+      MCG_FORM_PROP(pipeline)
+      MCG_FORM_PROP(carry)
+      MCG_FORM_PROP(placement_tries)
+      MCG_FORM_PROP(placement_leads)
+      MCG_FORM_PROP(fused_reduce)
+      MCG_FORM_PROP(tiles)
+      MCG_FORM_PROP(tile_seg_log2)
+      MCG_FORM_PROP(tile_pace)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
-      .def_readwrite("pmat", &CgOptions::pmat)
-      .def_readwrite("sell_sigma", &CgOptions::sell_sigma)
-      .def_readwrite("sell_aligned", &CgOptions::sell_aligned)
-      .def_readwrite("ag_overlap", &CgOptions::ag_overlap)
-      .def_readwrite("halo_ahead", &CgOptions::halo_ahead)
-      .def_readwrite("ap_recompute", &CgOptions::ap_recompute)
-      .def_readwrite("carry_dia", &CgOptions::carry_dia)
-      .def_readwrite("p3", &CgOptions::p3)
-      .def_readwrite("carry3_kw", &CgOptions::carry3_kw)
-      .def_readwrite("fail_graph_launch_at", &CgOptions::fail_graph_launch_at)
+      MCG_FORM_PROP(pmat)
+      MCG_FORM_PROP(sell_sigma)
+      MCG_FORM_PROP(sell_aligned)
+      MCG_FORM_PROP(ag_overlap)
+      MCG_FORM_PROP(halo_ahead)
+      MCG_FORM_PROP(ap_recompute)
+      MCG_FORM_PROP(carry_dia)
+      MCG_FORM_PROP(p3)
+      MCG_FORM_PROP(carry3_kw)
+      MCG_HOOK_PROP(fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
-      .def_readwrite("force_idx64", &CgOptions::force_idx64)
-      .def_readwrite("inject_nan_at", &CgOptions::inject_nan_at)
+      MCG_HOOK_PROP(force_idx64)
+      MCG_HOOK_PROP(inject_nan_at)
       .def_readwrite("spmv_variant", &CgOptions::spmv_variant)
       .def_readwrite("maxit", &CgOptions::maxit)
       .def_readwrite("tol", &CgOptions::tol)
@@ -229,10 +235,12 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("check_every", &CgOptions::check_every)
       .def_readwrite("overlap", &CgOptions::overlap)
       .def_readwrite("use_graph", &CgOptions::use_graph)
-      .def_readwrite("graph_iters", &CgOptions::graph_iters)
+      MCG_FORM_PROP(graph_iters)
       .def_readwrite("force_comm", &CgOptions::force_comm)
       .def_readwrite("format", &CgOptions::format)
       .def_readwrite("blocks_per_cu", &CgOptions::blocks_per_cu);
+#undef MCG_FORM_PROP
+#undef MCG_HOOK_PROP
 
   // ---- partition / halo plan / host CSR ----
   m.def("partition_rows", [](const ProblemSpec& s, int world, int halo_mode) {
