@@ -85,39 +85,7 @@ __device__ __forceinline__ void pipe_bookkeep(CgState* st, const double* tot, in
 
 // the in-kernel two-level reduction of f1_common.hpp with the pipelined bookkeeping
 __device__ __noinline__ void pipe_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
-  if (threadIdx.x >= 64) return;
-  const int lane = threadIdx.x;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int g = (rc.base + (int)blockIdx.x) / kRedGroup;
-  const int g0 = g * kRedGroup - rc.base;
-  const int gsize = min(kRedGroup, (int)gridDim.x - g0);
-  unsigned old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __shfl(old, 0, 64);
-  if (old != (unsigned)(gsize - 1)) return;
-  if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double v[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) v[q] = eng::wave_sum(v[q]);
-  if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) st_wt(&rc.lvl2[q * rc.l2s + g], v[q]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[rc.top], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __shfl(old, 0, 64);
-  if (old != (unsigned)(rc.ngroups - 1)) return;
-  if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[rc.top], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double t[2] = {0.0, 0.0};
-  for (int j = lane; j < rc.ngroups; j += 64) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) t[q] += ld_wt(&rc.lvl2[q * rc.l2s + j]);
-  }
-#pragma unroll
-  for (int q = 0; q < 2; ++q) t[q] = eng::wave_sum(t[q]);
-  if (lane == 0) pipe_bookkeep(st, t, rc.check, rc.first, tol);
+  last_arriver_reduce<2>(out, pstride, rc, [&](const double* t) { pipe_bookkeep(st, t, rc.check, rc.first, tol); });
 }
 
 __global__ __launch_bounds__(kBS) void k_pipe_update(PipeVectors v, int64_t n, double* __restrict__ partials,

@@ -104,12 +104,20 @@ __device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int 
   st->iter += 1;
 }
 
-// In-kernel two-level last-arriver reduction (kernels.hpp RedCtl).  Runs in wave 0 after
-// block_partial4(wt = true): lanes 0-3 of that wave stored the block's partials write-through;
-// every hand-off is write-through stores -> s_waitcnt vmcnt(0) -> one relaxed agent-scope atomic
-// add, and the last arriver (told by the value its add returned) reads with write-through (sc1)
-// loads only (MI355X_MICROARCH.md, visibility: valid forms, first table row).
-__device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
+// In-kernel two-level last-arriver reduction (kernels.hpp RedCtl) of NV block sums, then
+// book(totals) in lane 0 of the grid's last arriver.  Runs in wave 0 after block_partial4(wt =
+// true): lanes 0..NV-1 of that wave stored the block's partials write-through.  Every hand-off is
+//   write-through (sc0 sc1) stores -> s_waitcnt vmcnt(0) -> one relaxed agent-scope atomic add,
+// and the last arriver (told by the value its add returned) reads with write-through (sc1) loads
+// only (MI355X_MICROARCH.md, visibility: valid forms, first table row): the stores have reached
+// the device-coherent level before the add is issued, and the loads cannot be served from a stale
+// L1/L2 line.  The ordering is pinned for the compiler as well: the waits are asm volatile with a
+// memory clobber (no store or load crosses them), and the winner's path starts with one more
+// compiler barrier, so no load of the hand-off can be hoisted above the atomic it depends on.  An
+// agent release fence on every block's add (buffer_wbl2, ~1.7 us a block) would order nothing the
+// write-through path has not ordered already.
+template <int NV, typename Book>
+__device__ __forceinline__ void last_arriver_reduce(const double* out, int pstride, const RedCtl& rc, Book&& book) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -120,29 +128,37 @@ __device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc,
   if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __shfl(old, 0, 64);
   if (old != (unsigned)(gsize - 1)) return;
+  asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double v[4];
+  double v[NV];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
+  for (int q = 0; q < NV; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = eng::wave_sum(v[q]);
+  for (int q = 0; q < NV; ++q) v[q] = eng::wave_sum(v[q]);
   if (lane == 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) st_wt(&rc.lvl2[q * rc.l2s + g], v[q]);
+    for (int q = 0; q < NV; ++q) st_wt(&rc.lvl2[q * rc.l2s + g], v[q]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[rc.top], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __shfl(old, 0, 64);
   if (old != (unsigned)(rc.ngroups - 1)) return;
+  asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[rc.top], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double t[4] = {0.0, 0.0, 0.0, 0.0};
+  double t[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) t[q] = 0.0;
   for (int j = lane; j < rc.ngroups; j += 64) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) t[q] += ld_wt(&rc.lvl2[q * rc.l2s + j]);
+    for (int q = 0; q < NV; ++q) t[q] += ld_wt(&rc.lvl2[q * rc.l2s + j]);
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) t[q] = eng::wave_sum(t[q]);
-  if (lane == 0) f1_bookkeep(st, t, rc.check, rc.first, tol);
+  for (int q = 0; q < NV; ++q) t[q] = eng::wave_sum(t[q]);
+  if (lane == 0) book(t);
+}
+
+__device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
+  last_arriver_reduce<4>(out, pstride, rc, [&](const double* t) { f1_bookkeep(st, t, rc.check, rc.first, tol); });
 }
 
 // end of a fused pass: block partials, then (rc on) the in-kernel reduction
