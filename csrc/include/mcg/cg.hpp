@@ -31,9 +31,11 @@ struct PassForm {
                              // per grid line / plane): line-carry pass — a wave walks down a column of slices and
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
-  int placement_tries = 3;   // single-reduction form: time the pass on this many physical placements of the vector
+  int placement_tries = 6;   // single-reduction form: time the pass on this many physical placements of the vector
                              // set at setup and keep the fastest (1 = off; profiles/r1_placement_probe.md)
-  int placement_leads = 8;   // ... times this many start offsets of the vectors inside their allocations
+  int placement_leads = 16;  // ... times this many start offsets of the vectors inside their allocations
+                             // (16384^2: 3 x 8 -> 503-517 it/s, 6 x 8 -> 516-525, 6 x 16 -> 524-525;
+                             // profiles/r3_placement_depth.txt)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int pmat = -1;             // single-reduction form: materialized-p split pass (update kernel + SpMV gathering the
