@@ -5,7 +5,8 @@
 // served at ~55 G requests/s whether p sits in the 256 MiB Infinity Cache or in HBM (the
 // reference's cuSPARSE CSR SpMV, CUDACG.cu:288, has the same access pattern).  Gathers that hit
 // the L2 run 4-5x faster (bench/gather_probe.hip, profiles/r3_gather_probe.md).  So the columns
-// are cut into segments of S = 2^seg_shift doubles (2 MiB), every wave owns kTileB = 1024 rows
+// are cut into segments of S = 2^seg_shift doubles (default 2^19 = 4 MiB, one XCD's L2; CgOptions
+// tile_seg_log2), every wave owns kTileB = 1024 rows
 // (their running sums live in LDS), and ALL waves sweep the segments in the same order: while the
 // chip works on segment g, the XCDs' L2s hold p[g S, (g + 1) S) and the gathers hit.
 //
@@ -19,7 +20,8 @@
 // ragged tile end is enough), the L2 then holds none of the segments in flight and the hit rate
 // falls from ~96 % to ~20 % (TCC counters, profiles/r3_gather_probe.md).  After each segment a
 // workgroup therefore adds to its group's arrival counter (group = blockIdx % 8, i.e. the XCD
-// under round-robin dispatch) and waits until the whole group has finished that segment.  The
+// under round-robin dispatch) and waits until the group has finished that segment (tile_pace 1:
+// every workgroup; 2, the default: all but 1/8 of them, so stragglers do not stall the rest).  The
 // wait is bounded (kPaceSpins polls): it paces, it never decides correctness, so a workgroup that
 // is not co-resident only costs time.
 #include <hip/hip_runtime.h>
