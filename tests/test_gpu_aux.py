@@ -14,18 +14,22 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("recurrence", [0, 1])
-def test_checkpoint_resume_matches_uninterrupted(mcg, tmp_path, recurrence):
+@pytest.mark.parametrize("recurrence,pipe_rr", [(0, 0), (1, 0), (2, 0), (2, 12)])
+def test_checkpoint_resume_matches_uninterrupted(mcg, tmp_path, recurrence, pipe_rr):
+    """Resume is bitwise equal to the uninterrupted solve for every recurrence (pipelined CG: the
+    w, s, z, q vectors, the local {gamma, delta} and the replacement schedule continue)."""
     spec = mcg.make_problem("poisson2d", n=128)
-    full = mcg.CGSolver(spec, recurrence=recurrence, format="sell16", check_every=8).solve()
+    kw = dict(recurrence=recurrence, format="sell16", check_every=8)
+    if recurrence == 2:
+        kw["pipe_rr"] = pipe_rr
+    full = mcg.CGSolver(spec, **kw).solve()
     # first leg: stop at maxit=40 with a checkpoint every 16 iterations
     prefix = str(tmp_path / "ckpt")
-    a = mcg.CGSolver(spec, recurrence=recurrence, format="sell16", check_every=8, maxit=40,
-                     checkpoint_every=16, checkpoint_path=prefix)
+    a = mcg.CGSolver(spec, maxit=40, checkpoint_every=16, checkpoint_path=prefix, **kw)
     a.solve()
     assert os.path.exists(prefix + ".rank0")
     # second leg: fresh solver (new process state), resume from the last checkpoint
-    b = mcg.CGSolver(spec, recurrence=recurrence, format="sell16", check_every=8)
+    b = mcg.CGSolver(spec, **kw)
     b.load_checkpoint(prefix)
     out = b.solve(resume=True)
     assert out["converged"] and out["iterations"] == full["iterations"]
@@ -87,7 +91,7 @@ def test_checkpoint_rejects_perturbed_user_matrix_or_rhs(mcg, tmp_path):
         mcg.CGSolver(mcg.csr_problem(T, b=b + 1.0), **kw).load_checkpoint(prefix)
 
 
-@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "csr"), (1, "sell16")])
+@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "csr"), (1, "sell16"), (2, "sell16")])
 def test_fault_injection_latches_breakdown(mcg, recurrence, fmt):
     spec = mcg.make_problem("poisson2d", n=64)
     out = mcg.CGSolver(spec, recurrence=recurrence, format=fmt, inject_nan_at=5, check_every=4).solve()
@@ -115,7 +119,7 @@ print(json.dumps({"it": out["iterations"], "x": out["x_local"].tolist()}))
 """
 
 
-@pytest.mark.parametrize("recurrence", [0, 1])
+@pytest.mark.parametrize("recurrence", [0, 1, 2])
 def test_serialised_launches_bitwise_identical(mcg, recurrence):
     """Race detection: AMD_SERIALIZE_KERNEL=3 (+ blocking launches) must not change one bit."""
     code = _RUN % (ROOT, recurrence)
