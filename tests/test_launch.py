@@ -103,6 +103,29 @@ def test_bench_aggregate_takes_slowest_rank():
     assert not bench.aggregate(100, ranks)[2]
 
 
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def test_bench_pass_labels():
+    """The JSON names the pass the solver chose: plane carry for 3-D, the
+    pipelined form with its replacement period, the split pass, the generic pass."""
+    bench = _bench_module()
+    carry3 = {"carry": True, "p3": True, "ap_recompute": True, "ar3_kw": 16}
+    assert bench.pass_label(carry3, "poisson3d").startswith("plane-carry, three-term")
+    assert bench.pass_label(dict(carry3, ar3_kw=0), "poisson2d").startswith("line-carry")
+    assert bench.pass_label({"recurrence": "pipelined", "pipe_rr": 25}, "poisson2d") == (
+        "pipelined CG (Ghysels-Vanroose: all-reduce || SpMV), residual replacement every 25")
+    assert bench.pass_label({"recurrence": "pipelined", "pipe_rr": 0}, "randspd").startswith("pipelined CG")
+    assert bench.pass_label({"pmat": True}, "randspd") == "split (materialized p)"
+    assert bench.pass_label({}, "randspd") == "generic"
+
+
 def test_kfd_gpu_count_from_a_fake_topology(tmp_path):
     """The launcher counts GPUs without HIP: KFD topology nodes with a nonzero gfx_target_version
     whose render node this process can open (a container sees the host's topology, not its cards)."""
