@@ -137,8 +137,14 @@ void GpuCgSolver::setup() {
   // auto: the scrambled random SPD, or a user matrix that is not a grid stencil on the all-gather
   // layout (its columns are scattered over the whole vector); the same decision on every rank
   // (the spec and the layout kind are global)
+  // tiles: the scrambled family, and non-stencil user matrices whose columns are scattered -- on the
+  // all-gather layout, or with >= 1/4 of the entries beyond kFarOffset of their row (a global
+  // property of the matrix, so every rank decides the same)
+  const bool scattered_user = is_user && stencil_line(spec_) == 0 && spec_.csr != nullptr &&
+                              (L_.allgather ||
+                               (spec_.csr->far > 0 && 4 * spec_.csr->far >= spec_.csr->rowptr[spec_.csr->n]));
   tiles_ = opt_.recurrence >= 1 && (opt_.form.pmat != 0 || opt_.recurrence == 2) && opt_.form.tiles != 0 &&
-           (opt_.form.tiles == 1 || scrambled(spec_) || (is_user && L_.allgather && stencil_line(spec_) == 0));
+           (opt_.form.tiles == 1 || scrambled(spec_) || scattered_user);
   if (is_user) {
     user = build_local_csr(spec_, L_);
     if (opt_.format == 1 && !tiles_ && opt_.form.sell_sigma != 0 && n > 64 && (opt_.form.sell_sigma > 0 || stencil_line(spec_) == 0)) {

@@ -21,14 +21,16 @@ HostMatrix::HostMatrix(int64_t n, std::vector<int64_t> rowptr, std::vector<int64
   MCG_CHECK((int64_t)cols_.size() == nnz && (int64_t)vals_.size() == nnz, "csr: cols / vals length != nnz");
   MCG_CHECK(b_.empty() || (int64_t)b_.size() == n, "csr: b length != n");
   MCG_CHECK(n < ((int64_t)1 << 31), "csr: more than 2^31 rows");
-  int64_t bw = 0;
+  int64_t bw = 0, far = 0;
   std::vector<std::pair<int64_t, double>> row;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t a = rowptr_[i], e = rowptr_[i + 1];
     bool sorted = true;
     for (int64_t k = a; k < e; ++k) {
       MCG_CHECK(cols_[k] >= 0 && cols_[k] < n, "csr: column index out of range");
-      bw = std::max(bw, cols_[k] > i ? cols_[k] - i : i - cols_[k]);
+      const int64_t d = cols_[k] > i ? cols_[k] - i : i - cols_[k];
+      bw = std::max(bw, d);
+      far += d > kFarOffset ? 1 : 0;
       if (k > a && cols_[k] < cols_[k - 1]) sorted = false;
     }
     if (!sorted) {  // the SpMV engines do not care; ascending order keeps the halo windows and tests simple
@@ -43,6 +45,7 @@ HostMatrix::HostMatrix(int64_t n, std::vector<int64_t> rowptr, std::vector<int64
   }
   view_.n = n;
   view_.bw = bw;
+  view_.far = far;
   detect_stencil_();
   bind_();
 }

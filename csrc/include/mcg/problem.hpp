@@ -48,6 +48,10 @@ namespace mcg {
 
 enum class ProblemKind : int { Demo = 0, Poisson2D = 1, Poisson3D = 2, RandomSPD = 3, Csr = 4 };
 
+// Column offset beyond which a gather leaves an L2-sized neighbourhood of the row (2^16 doubles =
+// 512 KiB of p): a user matrix with many such entries is "scattered" and takes the L2-segment tiles.
+constexpr int64_t kFarOffset = (int64_t)1 << 16;
+
 // Host CSR of a user matrix (global rows, 0-based, int64 row pointers and columns).  A view:
 // the arrays are owned by the caller (HostMatrix, a NumPy array, ...).  Only host code reads
 // it: a rank uploads its rows; the device generators never see this kind.
@@ -58,6 +62,7 @@ struct CsrMatrix {
   const double* vals = nullptr;
   const double* b = nullptr;        // optional right-hand side (n); null: the spec's rhs kind
   int64_t bw = 0;                   // max |i - j| over the stored entries
+  int64_t far = 0;                  // entries with |i - j| > kFarOffset: gathers no SELL slice keeps in the L2
   // structured-grid stencil detected in the matrix (HostMatrix): every stored entry's column offset
   // is 0, +-1, +-line (2-D) or also +-plane = line^2 (3-D), and the rows are whole lines / planes;
   // 0 = none.  Lets a user matrix take the generated stencils' line / plane carry.

@@ -179,6 +179,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("n", &HostMatrix::n)
       .def_property_readonly("nnz", &HostMatrix::nnz)
       .def_property_readonly("bandwidth", [](const HostMatrix& a) { return a.view().bw; })
+      .def_property_readonly("far_entries", [](const HostMatrix& a) { return a.view().far; })
       .def_property_readonly("stencil_line", [](const HostMatrix& a) { return a.view().line; })
       .def_property_readonly("stencil_plane", [](const HostMatrix& a) { return a.view().plane; })
       .def_property_readonly("has_rhs", [](const HostMatrix& a) { return !a.rhs().empty(); })

@@ -261,6 +261,34 @@ def test_tiles_user_matrix_scattered(mcg):
     np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-8, atol=1e-10)
 
 
+def test_tiles_auto_for_scattered_user_matrix_at_one_rank(mcg):
+    """P = 1, no all-gather layout: a user CSR with >= 1/4 of its entries beyond 2^16 columns of
+    their row (HostMatrix.far_entries) takes the tiles by itself; a banded one keeps SELL.  The two
+    SpMVs agree over 30 fixed iterations."""
+    import scipy.sparse as sp
+
+    n = 200000
+    rng = np.random.default_rng(5)
+    B = sp.random(n, n, density=8.0 / n, random_state=6, format="csr")
+    B = B + B.T
+    A = (B + sp.diags(np.asarray(abs(B).sum(axis=1)).ravel() + 1.0)).tocsr()
+    b = rng.random(n)
+    prob = mcg.csr_problem(A, b=b)
+    assert 4 * prob.matrix.far_entries >= A.nnz
+    kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=30)
+    t = mcg.CGSolver(prob, **kw)
+    assert t.info["tiles"]
+    plain = mcg.CGSolver(prob, tiles=0, **kw)
+    assert not plain.info["tiles"]
+    rt, rp = t.solve(), plain.solve()
+    assert rt["iterations"] == rp["iterations"] == 30
+    assert abs(rt["rnorm"] - rp["rnorm"]) <= 1e-10 * rp["rnorm"]
+    T = sp.diags([-1.0, 2.5, -1.0], [-1, 0, 1], shape=(n, n)).tocsr()
+    banded = mcg.csr_problem(T, b=b)
+    assert banded.matrix.far_entries == 0
+    assert not mcg.CGSolver(banded, **kw).info["tiles"]
+
+
 def test_tiles_local_ranks_p8_agrees_with_p1(mcg):
     """Config-5 rehearsal on the scrambled matrix: 8 LocalComm ranks (all-gather layout, tiles on
     every rank) vs 1 rank over 12 fixed iterations agree to <= 1e-13."""
