@@ -246,7 +246,8 @@ def test_tiles_user_matrix_scattered(mcg):
 
     n = 20000
     rng = np.random.default_rng(3)
-    B = sp.random(n, n, density=6.0 / n, random_state=4, format="csr")
+    rows = np.repeat(np.arange(n), 6)  # 6 random entries a row (sp.random would enumerate n^2 candidates)
+    B = sp.csr_matrix((rng.random(6 * n), (rows, rng.integers(0, n, 6 * n))), shape=(n, n))
     B = B + B.T
     A = B + sp.diags(np.asarray(abs(B).sum(axis=1)).ravel() + 1.0)
     perm = rng.permutation(n)
@@ -269,7 +270,9 @@ def test_tiles_auto_for_scattered_user_matrix_at_one_rank(mcg):
 
     n = 200000
     rng = np.random.default_rng(5)
-    B = sp.random(n, n, density=8.0 / n, random_state=6, format="csr")
+    # 8 random entries a row, built from index draws (sp.random would enumerate n^2 candidates)
+    rows = np.repeat(np.arange(n), 8)
+    B = sp.csr_matrix((rng.random(8 * n), (rows, rng.integers(0, n, 8 * n))), shape=(n, n))
     B = B + B.T
     A = (B + sp.diags(np.asarray(abs(B).sum(axis=1)).ravel() + 1.0)).tocsr()
     b = rng.random(n)
