@@ -92,9 +92,11 @@ def parse_args(argv=None):
     ap.add_argument("--phases", type=int, default=10,
                     help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
-    ap.add_argument("--comm", default="dual", choices=["dual", "single"],
-                    help="dual: reduce + halo RCCL communicators (halo on the side stream); single: one communicator, "
-                         "every collective in one stream order on the compute stream")
+    ap.add_argument("--comm", default="single", choices=["dual", "single"],
+                    help="single (default): one RCCL communicator, every collective in one stream order on the "
+                         "compute stream; dual: reduce + halo communicators, the halo on the side stream next to the "
+                         "all-reduce (profiles/r3_priced_shares.md: 1-6 %% slower at P = 8 shares, two "
+                         "communicators in flight at once)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
     ap.add_argument("--sim-world", type=int, default=0,

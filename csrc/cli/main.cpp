@@ -14,7 +14,7 @@
 //   --maxit M  --tol T  --rtol R (||r|| < R ||b||)  --check-every K  --fixed-iters K  --warmup W
 //   --nnz-per-row m (random-spd: density = (m - 1) / (2 band))
 //   --format csr|sell|sell16|sellc8  --no-overlap  --no-graph  --force-comm  --blocks-per-cu B
-//   --comm dual|single (two RCCL communicators, halo on a side stream | one, one stream order)
+//   --comm single|dual (one RCCL communicator, one stream order (default) | two, halo on a side stream)
 //   --spmv-variant 0|1|2|3|4
 //   --recurrence two|single|pipelined  --pipe-rr K  --interleave auto|on|off  --window auto|on|off
 //   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
@@ -64,7 +64,7 @@ struct Args {
   bool rhs_set = false;
   bool format_set = false, recurrence_set = false;
   std::string resume;  // checkpoint prefix to resume from
-  bool comm_single = false;  // --comm single: one RCCL communicator, collectives in one stream order
+  bool comm_single = true;  // --comm single (default): one RCCL communicator, collectives in one stream order
   std::string matrix, rhs_file;  // user matrix (Matrix Market) and its right-hand side
   std::shared_ptr<HostMatrix> mat;
 };

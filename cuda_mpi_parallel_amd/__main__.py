@@ -32,7 +32,7 @@ DEFAULTS = {"--problem": "demo", "--seed": 1234, "--device": "gpu", "--gpus": No
             "--watchdog": 0.0, "--recurrence": "auto", "--interleave": "auto", "--window": "auto", "--carry": "auto",
             "--pmat": "auto", "--fused-reduce": "auto", "--halo-mode": "auto", "--blocks-per-cu": 0,
             "--spmv-variant": -1, "--checkpoint": "", "--checkpoint-every": 0, "--resume": "", "--inject-nan-at": -1,
-            "--print-x": "auto", "--report": "text", "--comm": "dual", "--pipe-rr": 0}
+            "--print-x": "auto", "--report": "text", "--comm": "single", "--pipe-rr": 0}
 
 
 def _parser() -> argparse.ArgumentParser:

@@ -51,7 +51,7 @@ FLAGS = [
     ("--no-overlap", None, "halo on the compute stream (no interior / boundary split)"),
     ("--no-graph", None, "eager iterations (no hipGraph)"),
     ("--force-comm", None, "RCCL collectives also with one rank"),
-    ("--comm", "dual", "dual: reduce + halo communicators (halo on a side stream) | single: one, one stream order"),
+    ("--comm", "single", "single (default): one communicator, one stream order | dual: reduce + halo communicators (halo on a side stream)"),
     ("--blocks-per-cu", "0", "SpMV grid, blocks per CU (0 = auto)"),
     ("--spmv-variant", "-1", "CSR engine: 0 LDS tiles, 1 direct, 2 CSR-vector, 3 direct nt, 4 row-length adaptive; -1 auto"),
     # aux subsystems

@@ -43,7 +43,7 @@ def init_process_group(env: DistEnv, backend: str = "gloo") -> None:
         dist.init_process_group(backend=backend, rank=env.rank, world_size=env.world)
 
 
-def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "dual"):
+def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "single"):
     """Create the native RCCL communicator(s) for this rank (None for a single rank unless
     ``force``).  Rank 0 draws the unique ids and broadcasts them over the torch.distributed
     store-backed process group.  ``mode``: "dual" = a reduce and a halo communicator (halo on the

@@ -41,7 +41,7 @@ class CGSolver:
 
     def __init__(self, spec: ProblemSpec, maxit: int = 2000, tol: float = 1e-7, check_every: int = 32,
                  overlap: bool = True, use_graph: bool = True, format: str = "csr", force_comm: bool = False,
-                 blocks_per_cu: int = 0, env: Optional[_dist.DistEnv] = None, comm=None, comm_mode: str = "dual",
+                 blocks_per_cu: int = 0, env: Optional[_dist.DistEnv] = None, comm=None, comm_mode: str = "single",
                  **tuning):
         self.spec = spec
         self.env = env or _dist.dist_env()
