@@ -201,3 +201,27 @@ def test_null_comm_halo_ahead_graph_equals_eager(mcg, problem, n):
     assert infos[0]["halo_ahead"] and infos[0]["graph_fallbacks"] == 0
     assert infos[0]["iterations"] == infos[1]["iterations"] == 75
     np.testing.assert_array_equal(xs[0], xs[1])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=512)), ("poisson3d", dict(n=64))])
+def test_local_ranks_default_serial_order_matches_single_rank(mcg, world, problem, kw):
+    """The P > 1 default since r3 (`--comm single`: the collectives in one stream order, overlap
+    off): the Ap-recomputing dia4 three-term carry over each rank's whole grid, the {Ap, p} halo
+    before the pass.  Vs the CPU oracle, and vs P = 1 over 40 fixed iterations (<= 1e-12)."""
+    spec = mcg.make_problem(problem, rhs="random", **kw)
+    C = mcg.native()
+    o = _opts(mcg, format="sellc8", recurrence=-1, check_every=4, overlap=False)
+    out = C.run_local_ranks(spec.native(), o, world, 0, True)
+    assert all(r["carry"] and r["ap_recompute"] for r in out["ranks"])
+    its = {r["iterations"] for r in out["ranks"]}
+    assert len(its) == 1, its
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=1e-7))
+    assert abs(its.pop() - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+    o = _opts(mcg, format="sellc8", recurrence=-1, tol=-1.0, maxit=1 << 30, overlap=False)
+    one = C.run_local_ranks(spec.native(), o, 1, 40, True)
+    many = C.run_local_ranks(spec.native(), o, world, 40, True)
+    r1, rp = one["ranks"][0]["rnorm"], many["ranks"][0]["rnorm"]
+    assert abs(r1 - rp) <= 1e-12 * r1
+    np.testing.assert_allclose(many["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
