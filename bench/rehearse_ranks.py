@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--band", type=int, default=100, help="randspd candidate offsets per side")
     ap.add_argument("--density", type=float, default=1.0)
     ap.add_argument("--spread", type=int, default=-1, help="randspd spread (-1 = rows: unstructured)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="collectives in one stream order (what --comm single runs at P > 1)")
     ap.add_argument("--phases", type=int, default=0,
                     help="> 0: per-rank phase timing (interior || halo, boundary wait) over that many iterations")
     args = ap.parse_args()
@@ -40,7 +42,8 @@ def main():
         spec = mcg.make_problem(args.problem, n=args.grid or args.n)
     ref = None
     for w in args.world:
-        o = C.CgOptions(maxit=1 << 30, tol=-1.0, format="sellc8", recurrence=1, check_every=1 << 30)
+        o = C.CgOptions(maxit=1 << 30, tol=-1.0, format="sellc8", recurrence=1, check_every=1 << 30,
+                        overlap=not args.no_overlap)
         out = C.run_local_ranks(spec.native(), o, w, args.iters, True, args.phases)
         r = out["ranks"]
         rn = r[0]["rnorm"]
@@ -48,7 +51,7 @@ def main():
         ok = all(x["iterations"] == args.iters + args.phases for x in r) and abs(tr - rn) <= 1e-6 * max(tr, 1e-300)
         if ref is None:
             ref = rn
-        line = {"world": w, "iterations": r[0]["iterations"], "rnorm": rn, "true_rnorm": tr,
+        line = {"world": w, "overlap": not args.no_overlap, "iterations": r[0]["iterations"], "rnorm": rn, "true_rnorm": tr,
                 "rel_vs_first": abs(rn - ref) / ref, "ok": ok}
         if args.phases:  # worst rank per phase (the ranks share one GPU: relative sizes, not speed)
             keys = sorted(r[0]["phases"])
