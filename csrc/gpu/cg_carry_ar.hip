@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "mcg/check.hpp"
@@ -99,6 +100,41 @@ __device__ __forceinline__ double lane_dn(double v) {  // wave_shr:1
   const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
   return __hiloint2double(hi, lo);
+}
+
+// lane + 1 / lane - 1 with lane 63 / lane 0 (no source lane) keeping `edge`: the DPP move's old
+// value is the select (a stencil's row just across the slice edge), so no compare or cndmask
+__device__ __forceinline__ double lane_up_or(double v, double edge) {  // wave_shl:1
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_dn_or(double v, double edge) {  // wave_shr:1
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// a wave-uniform value in scalar registers (the compiler cannot prove a loaded value uniform)
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double uni_d(double v) {
+  return __longlong_as_double((long long)uni_u64((uint64_t)__double_as_longlong(v)));
+}
+// global-memory accesses at a kernel-wide base plus a 32-bit byte offset (global_load / store's
+// saddr + voffset form: the base stays in scalar registers, one 32-bit add per address)
+typedef __attribute__((address_space(1))) double g_double;
+typedef __attribute__((address_space(1))) char g_char;
+__device__ __forceinline__ double g_ld(const double* base, uint32_t bo) {
+  return *(const g_double*)((const g_char*)(const g_double*)base + bo);
+}
+__device__ __forceinline__ void g_st(double* base, uint32_t bo, double v) { *(g_double*)((g_char*)(g_double*)base + bo) = v; }
+__device__ __forceinline__ void g_st_nt(double* base, uint32_t bo, double v) {
+  if constexpr (MCG_NT_STORES) __builtin_nontemporal_store(v, (g_double*)((g_char*)(g_double*)base + bo));
+  else *(g_double*)((g_char*)(g_double*)base + bo) = v;
 }
 
 // per-slice metadata for the carry's codes loads: first slot / 64 (28 bits) | width << 28
@@ -216,6 +252,214 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
     const int32_t e0 = (int32_t)(own + sl0 * 64);
     const int32_t i0 = (int32_t)(sl0 * 64);
     const int32_t n_run = (int32_t)(l1 - l0);
+    if constexpr (CM == 4 && P3) {
+      // Lean run.  A run whose lines l0 - 1 .. l1 carry uniform value patterns in this slice column
+      // (SellDev::dpat: every row the same value index per slot; one pattern B for the inner lines,
+      // the grid's first / last line may have their own, A / C) runs the loop below instead of
+      // step(): the values in scalar registers, no codes streamed or decoded, every access a
+      // kernel-wide global base plus a 32-bit byte offset, the slice-edge select folded into the
+      // lane shift.  It computes what step() computes, in the same fma order (bitwise equal): same
+      // loads (p_{k-2} for lines of the run, the stored r_{k-1} beyond it, lines clamped to the
+      // rank's), same stores (r in full on the run's first / last line, compact edge rows), same
+      // partials.  A slice at the start / end of a grid line (lane 0 / 63 without its -1 / +1
+      // entry: dpat bits 28 / 29) multiplies that lane's edge operand, set to 0, by the slot's
+      // value instead of the operand by 0 -- the same sum, as a row sum is never -0.  Every
+      // stream is a chain of LD registers (operands LD lines ahead, edges LD, x LD - 1) that the
+      // LD-step unroll rotates by renaming: no move of a register whose load is in flight.  With
+      // ghost lines (P > 1) only runs clear of the rank's outer lines take it.
+      constexpr int LD = QD + 1;
+      const bool ghosts = apx_o != nullptr || apx_n != nullptr;
+      bool go = S.dpat != nullptr && n_run >= 3 && nl >= 4 && v.ext_len < ((int64_t)1 << 29) &&
+                (!ghosts || (l0 >= 2 && l1 + LD + 1 <= nl));
+      uint32_t WA = 0, WB = 0, WC = 0;
+      if (go) {
+        const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;  // inner lines of l0 - 1 .. l1
+        const uint64_t wb = uni_u64(S.dpat[ia * SS + col]);
+        WB = (uint32_t)wb;
+        go = (WB >> 31) != 0u && (int64_t)(wb >> 32) >= ib - ia + 1;
+        if (l0 <= 1) {
+          WA = (uint32_t)uni_u64(S.dpat[col]);
+          go = go && (WA >> 31) != 0u && ((WA ^ WB) & (3u << 28)) == 0u;
+        }
+        if (l1 >= nl - 1) {
+          WC = (uint32_t)uni_u64(S.dpat[(nl - 1) * SS + col]);
+          go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
+        }
+      }
+      if (go) {
+        struct VSet {
+          double v[5];
+        };
+        auto vals = [&](uint32_t P) {
+          VSet V;
+#pragma unroll
+          for (int u = 0; u < 5; ++u) V.v[u] = uni_d(s_val[(P >> (4 * u)) & 15u]);
+          return V;
+        };
+        const bool z0 = (WB >> 28) & 1u, z63 = (WB >> 29) & 1u;
+        auto lean = [&](auto zlc) __attribute__((always_inline)) {
+          constexpr bool ZL = decltype(zlc)::value;
+          const VSet VB = vals(WB);
+          const bool hi = lane == 63, edge_lane = lane == 0 || lane == 63;
+          const bool zl = (lane == 0 && z0) || (hi && z63);  // lanes whose edge entry is absent
+          const uint32_t l8 = (uint32_t)lane << 3;
+          const uint32_t LOB = (uint32_t)LO << 3;                         // one line of the vectors
+          const uint32_t SB = (uint32_t)(2 * SS) << 3;                    // one line of the edge arrays
+          const uint32_t ob0 = (uint32_t)e0 << 3;                         // line 0 (ext layout)
+          const uint32_t xb0 = (uint32_t)i0 << 3;                         // line 0 of x
+          const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;  // edge arrays: 2 s - 1 of line 0
+          // lane 0: entry 2 s - 1 and row e - 1, lane 63: 2 s + 2 and row e + 64; a lane without
+          // its edge entry reads its own slice's (in range at the rank's first / last slice)
+          const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
+          const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
+          const int32_t jlo = -(int32_t)l0, jhi = (int32_t)(nl - 1 - l0);  // the rank's lines
+          auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
+          auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
+          auto raw_at = [&](int32_t j) {
+            Raw q;
+            const uint32_t o = line_ofs(jc(j)) + l8;
+            q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
+            q.p = g_ld(po, o);
+            return q;
+          };
+          auto edge_at = [&](int32_t j) {
+            Edge q;
+            const int32_t k = jc(j);
+            const uint32_t c = cb0 + (uint32_t)k * SB + oc;
+            q.r = g_ld(reo, c);
+            q.a = g_ld(eo, c);
+            q.p = g_ld(po, line_ofs(k) - 8u + op);
+            return q;
+          };
+          auto raw_un = [&](int32_t j) {  // a line of the run or below it, inside the rank
+            Raw q;
+            const uint32_t o = line_ofs(j) + l8;
+            q.r = g_ld(j < n_run ? (const double*)pn : ro, o);
+            q.p = g_ld(po, o);
+            return q;
+          };
+          auto edge_un = [&](int32_t j) {
+            Edge q;
+            const uint32_t c = cb0 + (uint32_t)j * SB + oc;
+            q.r = g_ld(reo, c);
+            q.a = g_ld(eo, c);
+            q.p = g_ld(po, line_ofs(j) - 8u + op);
+            return q;
+          };
+          auto x_at = [&](int32_t j) {
+            if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+            else return 0.0;
+          };
+          auto ez = [&](double e) {
+            if constexpr (ZL) return zl ? 0.0 : e;
+            else return e;
+          };
+          auto stencil_u = [&](const VSet& V, double mid, double edge, double dnl, double upl) {
+            const double upv = lane_up_or(mid, edge);
+            const double dnv = lane_dn_or(mid, edge);
+            double sum = fma(V.v[0], dnl, 0.0);
+            sum = fma(V.v[1], dnv, sum);
+            sum = fma(V.v[2], mid, sum);
+            sum = fma(V.v[3], upv, sum);
+            return fma(V.v[4], upl, sum);
+          };
+          auto epk = [&](const Edge& q) { return ez(fma(b, q.p, fma(na, q.a, q.r))); };
+          // prologue (step()'s): lines -2 .. LD - 1
+          const Raw rm2 = raw_at(-2), rm1 = raw_at(-1), r0 = raw_at(0);
+          Raw q[LD - 1];  // lines m + 1 .. m + LD - 1
+#pragma unroll
+          for (int d = 0; d < LD - 1; ++d) q[d] = raw_at(1 + d);
+          const Edge edm1 = edge_at(-1), ed0 = edge_at(0);
+          Edge e[LD - 1];  // lines m + 1 .. m + LD - 1
+#pragma unroll
+          for (int d = 0; d < LD - 1; ++d) e[d] = edge_at(1 + d);
+          double xs[LD - 1];  // lines m .. m + LD - 2
+#pragma unroll
+          for (int d = 0; d < LD - 1; ++d) xs[d] = x_at(d);
+          double pr_pk = 0.0;  // p_k of line -1 (none above the rank's first line: no ghosts here)
+          if (l0 >= 1) {
+            const VSet Vm = l0 == 1 ? vals(WA) : VB;
+            pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p), rm1.r));
+          }
+          double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
+          {
+            const VSet V0 = l0 == 0 ? vals(WA) : VB;
+            o_rk = fma(na, stencil_u(V0, r0.p, ez(ed0.p), rm1.p, q[0].p), fma(nbp, r0.r, r0.p));
+            o_pk = fma(b, r0.p, o_rk);
+          }
+          double o_epk = epk(ed0);
+          // step m: Ap_{k-1} of line m + 1 (values Vt; none past the rank's last line) and Ap_k of line m (Vs)
+          auto lstep = [&](auto clc, int32_t m, const VSet& Vs, const VSet& Vt, bool next) __attribute__((always_inline)) {
+            // CL: loads that may reach past the rank's last line (clamped); the main loop's never do
+            constexpr bool CL = decltype(clc)::value;
+            const Raw qn = CL ? raw_at(m + LD) : raw_un(m + LD);
+            const Edge en2 = CL ? edge_at(m + LD) : edge_un(m + LD);
+            const double xn = x_at(m + LD - 1);
+            double rk1 = 0.0, pk1 = 0.0;
+            if (next) {
+              const double t = stencil_u(Vt, q[0].p, ez(e[0].p), o_pold, q[1].p);
+              rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
+              pk1 = fma(b, q[0].p, rk1);
+            }
+            const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1);
+            const uint32_t ob = line_ofs(m);
+            const double rr = fma(-b, o_pold, o_pk);
+            if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+            if (edge_lane) {
+              const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
+              g_st(ren, sb, rr);
+              g_st(en, sb, sum);
+            }
+            if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+            g_st_nt(pn, ob + l8, o_pk);
+            s_pap = fma(o_pk, sum, s_pap);
+            s_rap = fma(o_rk, sum, s_rap);
+            s_apap = fma(sum, sum, s_apap);
+            s_rr = fma(o_rk, o_rk, s_rr);
+            pr_pk = o_pk;
+            o_pk = pk1;
+            o_rk = rk1;
+            o_pold = q[0].p;
+            o_pm2 = q[0].r;
+            o_epk = epk(e[0]);
+#pragma unroll
+            for (int d = 0; d + 1 < LD - 1; ++d) {
+              q[d] = q[d + 1];
+              e[d] = e[d + 1];
+              xs[d] = xs[d + 1];
+            }
+            q[LD - 2] = qn;
+            e[LD - 2] = en2;
+            xs[LD - 2] = xn;
+          };
+          // main loop: steps whose lines m, m + 1 are inner lines and whose loads (line m + LD) stay
+          // inside the rank, [m_lo, m_hi]; then the clamped tail
+          const std::true_type clamped;
+          const std::false_type unclamped;
+          const int32_t m_lo = l0 == 0 ? 1 : 0;
+          const int32_t m_hi = min(n_run - 1, (int32_t)(nl - 1 - LD - l0));
+          int32_t m = 0;
+          if (m_lo == 1) lstep(clamped, 0, vals(WA), VB, true);
+          m = m_lo;
+          for (; m + LD - 1 <= m_hi; m += LD) {
+#pragma unroll
+            for (int u = 0; u < LD; ++u) lstep(unclamped, m + u, VB, VB, true);
+          }
+          for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, true);
+          if (m < n_run) {  // near the rank's last line: clamped loads, its values C
+            const VSet VC = vals(WC);
+            for (; m < n_run; ++m) {
+              const bool lastl = l0 + m == nl - 1;
+              const bool nextc = l0 + m + 1 == nl - 1;
+              lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl);
+            }
+          }
+        };
+        if (z0 || z63) lean(std::true_type{});
+        else lean(std::false_type{});
+        continue;
+      }
+    }
     // lines j (relative to l0) inside the ext vectors: [jmin, jmax]; loads clamp to them (values
     // of lines that do not exist are never multiplied: the matrix has no entry for them)
     const int32_t jmax = (ext32 - 64 - e0) / LO;
@@ -835,7 +1079,87 @@ __global__ void k_dia_vals(const double2* __restrict__ dict, int nv, int nd, dou
   if (a < 16) dvals[a] = a < nv ? dict[a * nd].x : 0.0;
 }
 
+// SellDev::dpat, pass 1: a slice's pattern word -- bit 31 and the slot indices (4 bits per slot,
+// bits 0..27) when each slot holds one value index for all 64 rows, else 0.  One exception is
+// allowed per slice edge: lane 0's entry in the -1 slot (sm) and lane 63's in the +1 slot (sp)
+// may be absent (the zero value index zv) while the other 63 lanes hold the slot's index -- a
+// slice that starts / ends a grid line -- flagged in bit 28 / 29
+__global__ __launch_bounds__(256) void k_dia_pattern(const uint8_t* __restrict__ dia, int64_t ns, int nslot, int sm,
+                                                     int sp, int zv, uint64_t* __restrict__ dpat) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* sp_ = dia + s * 32 * nslot;
+    uint32_t w = 1u << 31;
+    for (int u = 0; u < nslot && w != 0u; ++u) {
+      const uint8_t* b = sp_ + 32 * u;
+      const uint32_t maj = (uint32_t)(b[0] >> 4);  // lane 1
+      bool same = true;
+      for (int i = 1; i < 31; ++i) same = same && b[i] == (uint8_t)(maj | (maj << 4));
+      const uint32_t l0 = b[0] & 15u, l63 = (uint32_t)(b[31] >> 4), l62 = b[31] & 15u;
+      same = same && l62 == maj;
+      if (l0 != maj) {
+        if (u == sm && l0 == (uint32_t)zv) w |= 1u << 28;
+        else same = false;
+      }
+      if (l63 != maj) {
+        if (u == sp && l63 == (uint32_t)zv) w |= 1u << 29;
+        else same = false;
+      }
+      w = same ? (w | (maj << (4 * u))) : 0u;
+    }
+    dpat[s] = w;
+  }
+}
+
+// pass 2: one thread per slice column walks its lines upwards and counts, per slice, the lines
+// from it down the column that carry the same uniform pattern; also counts the uniform slices
+__global__ __launch_bounds__(256) void k_dia_runs(uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
+                                                  unsigned long long* __restrict__ nuni) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= ss) return;
+  uint64_t len = 0;
+  uint32_t prev = 0;
+  unsigned long long cnt = 0;
+  for (int64_t l = nl - 1; l >= 0; --l) {
+    const int64_t s = l * ss + col;
+    const uint32_t w = (uint32_t)dpat[s];
+    len = (w >> 31) ? (w == prev ? len + 1 : 1) : 0;
+    cnt += (w >> 31);
+    prev = w;
+    dpat[s] = (len << 32) | w;
+  }
+  atomicAdd(nuni, cnt);
+}
+
 }  // namespace
+
+int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64_t ss, int nslot, uint64_t* dpat,
+                     hipStream_t stream) {
+  MCG_CHECK(dia4 != nullptr && dvals != nullptr && dpat != nullptr && ss > 0 && ns % ss == 0 &&
+                (nslot == 5 || nslot == 7),
+            "dia4 patterns: whole lines of slices");
+  if (ns <= 0) return 0;
+  // the value index of +0.0 (absent entries; sell_to_dia4 guarantees one)
+  double hv[16];
+  MCG_HIP(hipMemcpyAsync(hv, dvals, sizeof(hv), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed(A)");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(A)");
+  int zv = -1;
+  for (int a = 0; a < 16 && zv < 0; ++a)
+    if (hv[a] == 0.0 && !std::signbit(hv[a])) zv = a;
+  MCG_CHECK(zv >= 0, "dia4 patterns: no zero value");
+  const int sm = nslot == 5 ? 1 : 2, sp = nslot == 5 ? 3 : 4;  // slots of the -1 / +1 offsets
+  unsigned long long* cnt = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned long long), stream), "device malloc failed(dia4)");
+  MCG_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), stream), "device memset failed");
+  hipLaunchKernelGGL(k_dia_pattern, dim3(grid_for(ns, 256, 4)), dim3(256), 0, stream, dia4, ns, nslot, sm, sp, zv,
+                     dpat);
+  hipLaunchKernelGGL(k_dia_runs, dim3((unsigned)((ss + 255) / 256)), dim3(256), 0, stream, dpat, ss, ns / ss, cnt);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(dia4 patterns)");
+  unsigned long long h = 0;
+  MCG_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(dia4 patterns)");
+  (void)hipFreeAsync(cnt, stream);
+  return (int64_t)h;
+}
 
 void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipStream_t stream) {
   if (n_slices <= 0) return;

@@ -521,6 +521,10 @@ void GpuCgSolver::setup() {
       if (!ok) {
         dia4_.release();
         dvals_.release();
+      } else if (opt_.form.dia_uniform != 0) {
+        dpat_.allocate(ns, "A");
+        const int64_t nu = kern::dia_patterns(dia4_.get(), dvals_.get(), ns, tr_all_.strip, nslot, dpat_.get(), s0_);
+        info_.dia_uniform = ns > 0 ? (double)nu / (double)ns : 0.0;
       }
     }
     ar3_ = ar3 && dia4_.get() != nullptr;
@@ -531,6 +535,8 @@ void GpuCgSolver::setup() {
       ar_ = ar3_ = false;
       dia4_.release();
       dvals_.release();
+      dpat_.release();
+      info_.dia_uniform = 0.0;
     }
     MCG_CHECK(opt_.form.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
@@ -617,7 +623,9 @@ void GpuCgSolver::setup() {
     info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
-    const double streamed = info_.dia4 ? (double)dia4_.bytes() : (double)matrix_bytes;
+    // dia4 codes; the three-term pass streams none over its lean runs (uniform slices)
+    const double streamed = info_.dia4 ? (double)dia4_.bytes() * (p3_ ? 1.0 - info_.dia_uniform : 1.0)
+                                       : (double)matrix_bytes;
     // three-term form: p_{k-1}, p_{k-2} read, p_k written 24 B; x rw every second pass 8; edge r + Ap 0.5
     info_.bytes_per_iter_model = streamed + (p3_ ? 32.5 : 44.25) * n;
     info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + smeta_.bytes();

@@ -74,6 +74,9 @@ struct PassForm {
                              // slices' edge rows and the runs' outer lines (24 instead of 32 B/row for r and p,
                              // and the paired x update needs no extra p read); rounding differs from the
                              // two-term form (not bitwise); -1 = auto (on with dia4), 0 = off, 1 = required
+  int dia_uniform = -1;      // dia4 carry: slices whose 64 rows share one value-index pattern take a lean loop with the
+                             // values in scalar registers and no codes streamed (the 2-D three-term pass over runs
+                             // of such lines; bitwise the same sums); -1 = auto (on), 0 = off
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
                              // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
                              // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)

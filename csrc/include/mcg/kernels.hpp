@@ -107,6 +107,13 @@ struct SellDev {
   // column offset is the slot's, so the pass needs no per-entry offset decode or operand select.
   const uint8_t* dia4 = nullptr;
   const double* dvals = nullptr;
+  // SELL-64/dia4 slice patterns (dia_patterns): per slice, bit 31 set when all 64 rows hold the
+  // same value index in every slot (the indices packed 4 bits per slot in bits 0..27; bit 28 / 29:
+  // except lane 0's -1 / lane 63's +1 entry, absent: a slice at the start / end of a grid line),
+  // and in the high word the number of consecutive lines, from this slice's line down the same slice column,
+  // whose slices carry that same uniform pattern.  The line carry streams no codes over such runs
+  // (the values sit in scalar registers); nullptr = every slice through the codes.
+  const uint64_t* dpat = nullptr;
   // SELL-64/aligned (long rows whose slices share their column offsets, e.g. the wide random-SPD
   // family): entry j of EVERY lane of slice s is the row's own column + soffs[slice_ptr[s] / 64 + j]
   // (one wave-uniform offset per slot, clamped to [0, ext_len); absent entries hold 0.0), so a
@@ -268,6 +275,10 @@ void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipS
 // (-line, -ln, -1, 0, +1, +ln, +line), 224 B per slice
 bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* dia4, double* dvals,
                   hipStream_t stream);
+// SellDev::dpat from a dia4 copy (and its value table) of ns = ss * lines slices (ss slices per line,
+// nslot 5 or 7); returns the number of uniform slices (synchronises the stream)
+int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64_t ss, int nslot, uint64_t* dpat,
+                     hipStream_t stream);
 // 3-D (7-pt) Ap-recomputing plane carry (SELL-64/dia4 with ln = N): blocks of kw (4 / 8 / 16) waves on
 // kw consecutive grid lines of one x slice; v.ap_old / ap_new = ext-layout Ap (outer lines, slice
 // edge rows, and with gfull the first / last plane for the ghosts); grid = blocks (any count)

@@ -69,6 +69,7 @@ struct SolverInfo {
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
+  double dia_uniform = 0.0;  // dia4 slices whose 64 rows share one value pattern (no codes streamed; PassForm::dia_uniform)
   int ar3_kw = 0;        // 3-D Ap-recomputing plane carry: waves (grid lines) per block; 0 = not in use
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
@@ -171,6 +172,7 @@ class GpuCgSolver {
   DeviceBuffer<double2> dict_;
   DeviceBuffer<uint8_t> dia4_;    // SELL-64/dia4 copy (Ap-recomputing carry; 160 B per slice)
   DeviceBuffer<double> dvals_;    // ... its value table (16 doubles)
+  DeviceBuffer<uint64_t> dpat_;   // ... its uniform-slice patterns and run lengths (SellDev::dpat)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
   DeviceBuffer<int32_t> soffs_;   // SELL-64/aligned per-slot column offsets
   bool aligned_ = false;
@@ -219,6 +221,7 @@ class GpuCgSolver {
     s.smeta = smeta_.get();
     s.dia4 = dia4_.get();
     s.dvals = dvals_.get();
+    s.dpat = dpat_.get();
     return s;
   }
   // vectors

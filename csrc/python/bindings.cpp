@@ -222,6 +222,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(ap_recompute)
       MCG_FORM_PROP(carry_dia)
       MCG_FORM_PROP(p3)
+      MCG_FORM_PROP(dia_uniform)
       MCG_FORM_PROP(carry3_kw)
       MCG_HOOK_PROP(fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
@@ -427,6 +428,7 @@ PYBIND11_MODULE(_C, m) {
         d["xcd_map"] = i.xcd_map;
         d["dia4"] = i.dia4;
         d["p3"] = i.p3;
+        d["dia_uniform"] = i.dia_uniform;
         d["ar3_kw"] = i.ar3_kw;
         d["carry_xchg"] = i.carry_xchg;
         d["placement_sets"] = i.placement_sets;

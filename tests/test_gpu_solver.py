@@ -417,3 +417,27 @@ def test_long_graph_bitwise_equal_pairs(mcg, fmt, rec):
     assert a.result()["iterations"] == b.result()["iterations"] == 32
     assert a.result()["rnorm"] == b.result()["rnorm"]
     assert np.array_equal(a.x_local(), b.x_local())
+
+
+@pytest.mark.parametrize("n", [1024, 2048])
+def test_dia_uniform_lean_runs_bitwise(mcg, n):
+    """Lean runs of the three-term 2-D dia4 carry (runs whose slices all carry one uniform value
+    pattern: values in scalar registers, no codes streamed) compute exactly what the generic step
+    computes: x and ||r|| bit for bit against dia_uniform = 0, at odd and even iteration counts
+    (paired x update) and at convergence.  At these sizes the auto grid gives runs of 4 / 16 lines,
+    so most runs are lean (l0 >= 2, l1 <= lines - 4)."""
+    spec = mcg.make_problem("poisson2d", n=n, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, dia_uniform=0)
+    assert a.info["p3"] and a.info["dia4"] and b.info["p3"]
+    assert a.info["dia_uniform"] > 0.9 and b.info["dia_uniform"] == 0.0
+    assert a.info["bytes_per_iter_model"] < b.info["bytes_per_iter_model"]
+    for its in (37, 38):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
+        assert np.array_equal(outs[0][1], outs[1][1])
