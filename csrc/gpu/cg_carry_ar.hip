@@ -265,12 +265,13 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       // entry: dpat bits 28 / 29) multiplies that lane's edge operand, set to 0, by the slot's
       // value instead of the operand by 0 -- the same sum, as a row sum is never -0.  Every
       // stream is a chain of LD registers (operands LD lines ahead, edges LD, x LD - 1) that the
-      // LD-step unroll rotates by renaming: no move of a register whose load is in flight.  With
-      // ghost lines (P > 1) only runs clear of the rank's outer lines take it.
+      // LD-step unroll rotates by renaming: no move of a register whose load is in flight.  Ghost
+      // lines (P > 1) as in step(): their Ap_{k-1} exchanged (apx), r recovered from the halo's
+      // p's; the rank's first / last line stores its Ap_k for the neighbours.
       constexpr int LD = QD + 1;
-      const bool ghosts = apx_o != nullptr || apx_n != nullptr;
-      bool go = S.dpat != nullptr && n_run >= 3 && nl >= 4 && v.ext_len < ((int64_t)1 << 29) &&
-                (!ghosts || (l0 >= 2 && l1 + LD + 1 <= nl));
+      // a slice column at a grid line's start / end must have the absent edge entry (no load
+      // outside the ext vectors at the rank's first / last slice)
+      bool go = S.dpat != nullptr && n_run >= 3 && nl >= 4 && v.ext_len < ((int64_t)1 << 29);
       uint32_t WA = 0, WB = 0, WC = 0;
       if (go) {
         const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;  // inner lines of l0 - 1 .. l1
@@ -285,6 +286,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
           WC = (uint32_t)uni_u64(S.dpat[(nl - 1) * SS + col]);
           go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
         }
+        go = go && (col != 0 || ((WB >> 28) & 1u)) && (col != SS - 1 || ((WB >> 29) & 1u));
       }
       if (go) {
         struct VSet {
@@ -312,8 +314,11 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
           // its edge entry reads its own slice's (in range at the rank's first / last slice)
           const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
           const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
-          const int32_t jlo = -(int32_t)l0, jhi = (int32_t)(nl - 1 - l0);  // the rank's lines
+          // lines of the ext vectors (ghosts included; step()'s ebase) and of the rank (oline)
+          const int32_t jlo = -(e0 / LO), jhi = (ext32 - 64 - e0) / LO;
+          const int32_t rlo = -(int32_t)l0, rhi = (int32_t)(nl - 1 - l0);
           auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
+          auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
           auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
           auto raw_at = [&](int32_t j) {
             Raw q;
@@ -324,13 +329,15 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
           };
           auto edge_at = [&](int32_t j) {
             Edge q;
-            const int32_t k = jc(j);
-            const uint32_t c = cb0 + (uint32_t)k * SB + oc;
+            const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
             q.r = g_ld(reo, c);
             q.a = g_ld(eo, c);
-            q.p = g_ld(po, line_ofs(k) - 8u + op);
+            q.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
             return q;
           };
+          // a ghost line's r_{k-1} (step()'s rghost): from the halo's p_{k-2} in p_new's ghost rows
+          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), q.p); };
+          auto is_ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
           auto raw_un = [&](int32_t j) {  // a line of the run or below it, inside the rank
             Raw q;
             const uint32_t o = line_ofs(j) + l8;
@@ -376,10 +383,12 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
           double xs[LD - 1];  // lines m .. m + LD - 2
 #pragma unroll
           for (int d = 0; d < LD - 1; ++d) xs[d] = x_at(d);
-          double pr_pk = 0.0;  // p_k of line -1 (none above the rank's first line: no ghosts here)
+          double pr_pk = 0.0;  // p_k of line -1: owned, a ghost, or none
           if (l0 >= 1) {
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
             pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p), rm1.r));
+          } else if (is_ghost(-1)) {
+            pr_pk = fma(b, rm1.p, fma(na, g_ld(apx_o, line_ofs(-1) + l8), rghost(-1, rm1)));
           }
           double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
           {
@@ -388,17 +397,21 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
             o_pk = fma(b, r0.p, o_rk);
           }
           double o_epk = epk(ed0);
-          // step m: Ap_{k-1} of line m + 1 (values Vt; none past the rank's last line) and Ap_k of line m (Vs)
-          auto lstep = [&](auto clc, int32_t m, const VSet& Vs, const VSet& Vt, bool next) __attribute__((always_inline)) {
+          // step m: Ap_{k-1} of line m + 1 (next: 1 owned, values Vt; 2 a ghost line; 0 none) and
+          // Ap_k of line m (values Vs)
+          auto lstep = [&](auto clc, int32_t m, const VSet& Vs, const VSet& Vt, int next) __attribute__((always_inline)) {
             // CL: loads that may reach past the rank's last line (clamped); the main loop's never do
             constexpr bool CL = decltype(clc)::value;
             const Raw qn = CL ? raw_at(m + LD) : raw_un(m + LD);
             const Edge en2 = CL ? edge_at(m + LD) : edge_un(m + LD);
             const double xn = x_at(m + LD - 1);
             double rk1 = 0.0, pk1 = 0.0;
-            if (next) {
+            if (next == 1) {
               const double t = stencil_u(Vt, q[0].p, ez(e[0].p), o_pold, q[1].p);
               rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
+              pk1 = fma(b, q[0].p, rk1);
+            } else if (CL && next == 2) {
+              rk1 = fma(na, g_ld(apx_o, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
               pk1 = fma(b, q[0].p, rk1);
             }
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1);
@@ -412,6 +425,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
             }
             if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
             g_st_nt(pn, ob + l8, o_pk);
+            if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apx_n, ob + l8, sum);
             s_pap = fma(o_pk, sum, s_pap);
             s_rap = fma(o_rk, sum, s_rap);
             s_apap = fma(sum, sum, s_apap);
@@ -439,19 +453,19 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
           const int32_t m_lo = l0 == 0 ? 1 : 0;
           const int32_t m_hi = min(n_run - 1, (int32_t)(nl - 1 - LD - l0));
           int32_t m = 0;
-          if (m_lo == 1) lstep(clamped, 0, vals(WA), VB, true);
+          if (m_lo == 1) lstep(clamped, 0, vals(WA), VB, 1);
           m = m_lo;
           for (; m + LD - 1 <= m_hi; m += LD) {
 #pragma unroll
-            for (int u = 0; u < LD; ++u) lstep(unclamped, m + u, VB, VB, true);
+            for (int u = 0; u < LD; ++u) lstep(unclamped, m + u, VB, VB, 1);
           }
-          for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, true);
+          for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, 1);
           if (m < n_run) {  // near the rank's last line: clamped loads, its values C
             const VSet VC = vals(WC);
             for (; m < n_run; ++m) {
               const bool lastl = l0 + m == nl - 1;
               const bool nextc = l0 + m + 1 == nl - 1;
-              lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl);
+              lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
         };
@@ -778,6 +792,13 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     return sum;
   };
   auto pk_of = [&](double r, double a_, double p) { return fma(b, p, fma(na, a_, r)); };
+  // neighbour waves' values through LDS (outer waves: `far` for the side outside the block)
+  auto nbr = [&](int par, int which, double far, double& dn, double& up) {
+    const double* sx = &s_x[par][which][0][lane];
+    const double vd = sx[(odn ? wv : wv - 1) * 64], vu = sx[(oup ? wv : wv + 1) * 64];
+    dn = odn ? far : vd;
+    up = oup ? far : vu;
+  };
   for (int64_t job = lb; job < jpr * runs; job += nb) {
     const int64_t run = job / jpr, q = job % jpr;
     const int64_t col = ((q / G) * KW + wv) * G + q % G;  // slice of grid line y = yg KW + wv, x slice q % G
@@ -788,6 +809,257 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     const int32_t e0 = (int32_t)(own + sl0 * 64);
     const int32_t i0 = (int32_t)(sl0 * 64);
     const int32_t n_run = (int32_t)(l1 - l0);
+    if constexpr (P3) {
+      // Lean run (the 2-D kernel's, per wave, with the +-N rows through LDS as in the step below):
+      // the seven values in scalar registers, no codes streamed, global base + 32-bit byte offset
+      // accesses; bitwise what the generic step computes.  Block-uniform: the waves exchange rows
+      // every step, so the block takes it only when every wave's run qualifies (one barrier,
+      // which is also the barrier after the previous job's last LDS reads).  A wave on the grid's
+      // first / last y line has no far row (its -N / +N slot is absent): it reads its own row,
+      // which the absent slot's 0 multiplies as it would the clamped one.
+      // Streams: operands RD = 3 planes ahead (the stencil of plane m + 1 needs plane m + 2), edge /
+      // far rows and x ED = 2 ahead (their values are short-lived; 128 VGPRs); the 6-step unroll
+      // renames both chain lengths
+      constexpr int LD = 3, ED = 2, UNR = 6;
+      uint32_t WA = 0, WB = 0, WC = 0;
+      bool go = false, zany = false;
+      if (S.dpat != nullptr) {
+        go = n_run >= 3 && nl >= 4 && v.ext_len < ((int64_t)1 << 29);
+        if (go) {
+          const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;
+          const uint64_t wb = uni_u64(S.dpat[ia * SS + col]);
+          WB = (uint32_t)wb;
+          go = (WB >> 31) != 0u && (int64_t)(wb >> 32) >= ib - ia + 1;
+          if (l0 <= 1) {
+            WA = (uint32_t)uni_u64(S.dpat[col]);
+            go = go && (WA >> 31) != 0u && ((WA ^ WB) & (3u << 28)) == 0u;
+          }
+          if (l1 >= nl - 1) {
+            WC = (uint32_t)uni_u64(S.dpat[(nl - 1) * SS + col]);
+            go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
+          }
+          go = go && (col != 0 || ((WB >> 28) & 1u)) && (col != SS - 1 || ((WB >> 29) & 1u));
+        }
+        go = __syncthreads_and(go) != 0;
+        zany = go && __syncthreads_or(((WB >> 28) & 3u) != 0u) != 0;
+      }
+      if (go) {
+        struct VSet {
+          double v[7];
+        };
+        auto vals = [&](uint32_t P) {
+          VSet V;
+#pragma unroll
+          for (int u = 0; u < 7; ++u) V.v[u] = uni_d(s_val[(P >> (4 * u)) & 15u]);
+          return V;
+        };
+        const bool z0 = (WB >> 28) & 1u, z63 = (WB >> 29) & 1u;
+        const int64_t yl = (q / G) * KW + wv;  // the wave's grid line
+        const bool fnone = (odn && yl == 0) || (oup && yl == LN - 1);
+        auto lean = [&](auto zlc) __attribute__((always_inline)) {
+          constexpr bool ZL = decltype(zlc)::value;
+          const VSet VB = vals(WB);
+          const bool hi = lane == 63, edge_lane = lane == 0 || lane == 63;
+          const bool zl = (lane == 0 && z0) || (hi && z63);
+          const bool outer = odn || oup;
+          const uint32_t l8 = (uint32_t)lane << 3;
+          const uint32_t LOB = (uint32_t)LO << 3;                         // one plane of the vectors
+          const uint32_t SB = (uint32_t)(2 * SS) << 3;                    // one plane of the edge arrays
+          const uint32_t ob0 = (uint32_t)e0 << 3;                         // plane 0 (ext layout)
+          const uint32_t xb0 = (uint32_t)i0 << 3;                         // plane 0 of x
+          const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;  // edge arrays: 2 s - 1 of plane 0
+          const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
+          const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
+          const uint32_t fob = fnone ? 0u : (uint32_t)fo << 3;  // the far row, bytes from the wave's own
+          // planes of the ext vectors (ghosts included; the generic ebase) and of the rank (oline)
+          const int32_t jlo = -(e0 / LO), jhi = (ext32 - 64 - e0) / LO;
+          const int32_t rlo = -(int32_t)l0, rhi = (int32_t)(nl - 1 - l0);
+          auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
+          auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
+          auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
+          auto raw_ld = [&](int32_t j, int32_t k) {  // plane j's source, plane k's address
+            Raw r;
+            const uint32_t o = line_ofs(k) + l8;
+            r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
+            r.p = g_ld(po, o);
+            return r;
+          };
+          auto edge_ld = [&](int32_t j) {  // plane j (clamped: compact index to the rank, row to ext)
+            Edge r;
+            const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
+            r.r = g_ld(reo, c);
+            r.a = g_ld(eao, c);
+            r.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
+            return r;
+          };
+          auto edge_un = [&](int32_t j) {
+            Edge r;
+            const uint32_t c = cb0 + (uint32_t)j * SB + oc;
+            r.r = g_ld(reo, c);
+            r.a = g_ld(eao, c);
+            r.p = g_ld(po, line_ofs(j) - 8u + op);
+            return r;
+          };
+          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), q.p); };
+          auto is_ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
+          auto far_ld = [&](int32_t k) {
+            Far f{0.0, 0.0, 0.0};
+            if (outer) {
+              const uint32_t o = line_ofs(k) + l8 + fob;
+              f.r = g_ld(ro, o);
+              f.p = g_ld(po, o);
+              f.a = g_ld(apo, o);
+            }
+            return f;
+          };
+          auto x_at = [&](int32_t j) {
+            if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+            else return 0.0;
+          };
+          auto ez = [&](double e) {
+            if constexpr (ZL) return zl ? 0.0 : e;
+            else return e;
+          };
+          auto stencil_u = [&](const VSet& V, double mid, double edge, double dnl, double upl, double dnn, double upn) {
+            const double upv = lane_up_or(mid, edge);
+            const double dnv = lane_dn_or(mid, edge);
+            double sum = fma(V.v[0], dnl, 0.0);
+            sum = fma(V.v[1], dnn, sum);
+            sum = fma(V.v[2], dnv, sum);
+            sum = fma(V.v[3], mid, sum);
+            sum = fma(V.v[4], upv, sum);
+            sum = fma(V.v[5], upn, sum);
+            return fma(V.v[6], upl, sum);
+          };
+          auto epk = [&](const Edge& e) { return ez(pk_of(e.r, e.a, e.p)); };
+          // prologue (the generic one's): planes -2 .. LD - 1
+          const Raw rm2 = raw_ld(-2, jc(-2)), rm1 = raw_ld(-1, jc(-1)), r0 = raw_ld(0, 0);
+          Raw qv[LD - 1];  // planes m + 1 .. m + LD - 1
+#pragma unroll
+          for (int d = 0; d < LD - 1; ++d) qv[d] = raw_ld(1 + d, jc(1 + d));
+          const Edge edm1 = edge_ld(-1), ed0 = edge_ld(0);
+          Edge ev[ED - 1];  // planes m + 1 .. m + ED - 1
+#pragma unroll
+          for (int d = 0; d < ED - 1; ++d) ev[d] = edge_ld(1 + d);
+          const Far fm1 = far_ld(jc(-1)), f0 = far_ld(0);
+          Far fv[ED - 1];
+#pragma unroll
+          for (int d = 0; d < ED - 1; ++d) fv[d] = far_ld(jc(1 + d));
+          double xs[ED - 1];  // planes m .. m + ED - 2
+#pragma unroll
+          for (int d = 0; d < ED - 1; ++d) xs[d] = x_at(d);
+          s_x[1][0][wv][lane] = rm1.p;
+          s_x[1][1][wv][lane] = r0.p;
+          __syncthreads();
+          double pr_pk = 0.0;
+          if (l0 >= 1) {
+            double dn, up;
+            nbr(1, 0, fm1.p, dn, up);
+            const VSet Vm = l0 == 1 ? vals(WA) : VB;
+            const double t = stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p, dn, up);
+            pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+          } else if (is_ghost(-1)) {
+            pr_pk = pk_of(rghost(-1, rm1), g_ld(apo, line_ofs(-1) + l8), rm1.p);
+          }
+          double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
+          {
+            double dn, up;
+            nbr(1, 1, f0.p, dn, up);
+            const VSet V0 = l0 == 0 ? vals(WA) : VB;
+            const double t = stencil_u(V0, r0.p, ez(ed0.p), rm1.p, qv[0].p, dn, up);
+            o_rk = fma(na, t, fma(nbp, r0.r, r0.p));
+            o_pk = fma(b, r0.p, o_rk);
+          }
+          double o_epk = epk(ed0);
+          double o_fpk = pk_of(f0.r, f0.a, f0.p);
+          // next: 1 plane m + 1 owned (values Vt), 2 a ghost plane, 0 none
+          auto lstep = [&](auto clc, int32_t m, const VSet& Vs, const VSet& Vt, int next) __attribute__((always_inline)) {
+            constexpr bool CL = decltype(clc)::value;
+            const int par = m & 1;
+            const uint32_t ob = line_ofs(m);
+            const double rr = fma(-b, o_pold, o_pk);
+            if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+            else if (outer) g_st(rn, ob + l8, rr);
+            const int32_t kn = CL ? jc(m + LD) : m + LD;
+            const Raw qn = raw_ld(m + LD, kn);
+            const Edge en2 = CL ? edge_ld(m + ED) : edge_un(m + ED);
+            const Far fn = far_ld(CL ? jc(m + ED) : m + ED);
+            const double xn = x_at(m + ED - 1);
+            s_x[par][0][wv][lane] = qv[0].p;
+            s_x[par][1][wv][lane] = o_pk;
+            __syncthreads();
+            double rk1 = 0.0, pk1 = 0.0;
+            if (next == 1) {
+              double dn, up;
+              nbr(par, 0, fv[0].p, dn, up);
+              const double t = stencil_u(Vt, qv[0].p, ez(ev[0].p), o_pold, qv[1].p, dn, up);
+              rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
+              pk1 = fma(b, qv[0].p, rk1);
+            } else if (CL && next == 2) {
+              rk1 = fma(na, g_ld(apo, line_ofs(m + 1) + l8), rghost(m + 1, qv[0]));
+              pk1 = fma(b, qv[0].p, rk1);
+            }
+            double kdn, kup;
+            nbr(par, 1, o_fpk, kdn, kup);
+            const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1, kdn, kup);
+            if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+            g_st_nt(pn, ob + l8, o_pk);
+            if (outer || (CL && gfull && (l0 + m == 0 || l0 + m == nl - 1))) g_st(apw, ob + l8, sum);
+            if (edge_lane) {
+              const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
+              g_st(ean, sb, sum);
+              g_st(ren, sb, rr);
+            }
+            s_pap = fma(o_pk, sum, s_pap);
+            s_rap = fma(o_rk, sum, s_rap);
+            s_apap = fma(sum, sum, s_apap);
+            s_rr = fma(o_rk, o_rk, s_rr);
+            pr_pk = o_pk;
+            o_pk = pk1;
+            o_rk = rk1;
+            o_pold = qv[0].p;
+            o_pm2 = qv[0].r;
+            o_epk = epk(ev[0]);
+            o_fpk = pk_of(fv[0].r, fv[0].a, fv[0].p);
+#pragma unroll
+            for (int d = 0; d + 1 < LD - 1; ++d) qv[d] = qv[d + 1];
+#pragma unroll
+            for (int d = 0; d + 1 < ED - 1; ++d) {
+              ev[d] = ev[d + 1];
+              fv[d] = fv[d + 1];
+              xs[d] = xs[d + 1];
+            }
+            qv[LD - 2] = qn;
+            ev[ED - 2] = en2;
+            fv[ED - 2] = fn;
+            xs[ED - 2] = xn;
+          };
+          const std::true_type clamped;
+          const std::false_type unclamped;
+          const int32_t m_lo = l0 == 0 ? 1 : 0;
+          const int32_t m_hi = min(n_run - 1, (int32_t)(nl - 1 - LD - l0));
+          int32_t m = 0;
+          if (m_lo == 1) lstep(clamped, 0, vals(WA), VB, 1);
+          m = m_lo;
+          for (; m + UNR - 1 <= m_hi; m += UNR) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) lstep(unclamped, m + u, VB, VB, 1);
+          }
+          for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, 1);
+          if (m < n_run) {
+            const VSet VC = vals(WC);
+            for (; m < n_run; ++m) {
+              const bool lastl = l0 + m == nl - 1;
+              const bool nextc = l0 + m + 1 == nl - 1;
+              lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
+            }
+          }
+        };
+        if (zany) lean(std::true_type{});
+        else lean(std::false_type{});
+        continue;
+      }
+    }
     const int32_t jmax = (ext32 - 64 - e0) / LO;
     const int32_t jmin = -(e0 / LO);
     auto ebase = [&](int32_t j) { return e0 + (j < jmin ? jmin : (j > jmax ? jmax : j)) * LO; };
@@ -842,13 +1114,6 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     // ghost plane's r_{k-1}: P3 recovers it from the halo's p's (k_cg_carry_ar's rghost)
     auto rghost = [&](int32_t j, const Raw& q) { return P3 && !first ? fma(nbp, pn[ebase(j) + lane], q.p) : q.r; };
     auto edge_pk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
-    // neighbour waves' values through LDS (outer waves: `far` for the side outside the block)
-    auto nbr = [&](int par, int which, double far, double& dn, double& up) {
-      const double* sx = &s_x[par][which][0][lane];
-      const double vd = sx[(odn ? wv : wv - 1) * 64], vu = sx[(oup ? wv : wv + 1) * 64];
-      dn = odn ? far : vd;
-      up = oup ? far : vu;
-    };
 
     __syncthreads();  // the previous job's last step has read its LDS slots
     // prologue: planes -2 .. QD, edges / codes of -1 .. 1, the outside rows of -1 .. 1

@@ -225,3 +225,19 @@ def test_local_ranks_default_serial_order_matches_single_rank(mcg, world, proble
     r1, rp = one["ranks"][0]["rnorm"], many["ranks"][0]["rnorm"]
     assert abs(r1 - rp) <= 1e-12 * r1
     np.testing.assert_allclose(many["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
+
+
+@pytest.mark.parametrize("problem,n,world", [("poisson2d", 2048, 2), ("poisson2d", 2048, 4), ("poisson3d", 128, 2)])
+def test_local_ranks_lean_runs_bitwise(mcg, problem, n, world):
+    """With ghost lines (P > 1) the lean runs of the three-term dia4 carry take the runs clear of the
+    rank's outer lines; every rank's x and the iteration count are bit for bit those of
+    dia_uniform = 0 (the generic step for every run)."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    C = mcg.native()
+    outs = []
+    for du in (-1, 0):
+        o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8)
+        o.dia_uniform = du
+        outs.append(C.run_local_ranks(spec.native(), o, world, 30, True))
+    assert [r["rnorm"] for r in outs[0]["ranks"]] == [r["rnorm"] for r in outs[1]["ranks"]]
+    np.testing.assert_array_equal(outs[0]["x"], outs[1]["x"])

@@ -441,3 +441,24 @@ def test_dia_uniform_lean_runs_bitwise(mcg, n):
             outs.append((s.result(), s._s.x_local()))
         assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
         assert np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,kw", [(128, 16), (128, 8), (128, 4), (256, 16)])
+def test_dia_uniform_lean_runs_bitwise_3d(mcg, n, kw):
+    """Lean runs of the 3-D three-term plane carry (per wave: the seven values in scalar registers,
+    no codes streamed; the block takes them when every wave's run qualifies): x and ||r|| bit for
+    bit against dia_uniform = 0.  Runs of 8 / 4 planes at n = 128, 64 at n = 256, including the
+    grid's first / last planes and the x / y boundary slices."""
+    spec = mcg.make_problem("poisson3d", n=n, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, carry3_kw=kw)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, carry3_kw=kw, dia_uniform=0)
+    assert a.info["p3"] and a.info["ar3_kw"] == kw and a.info["dia_uniform"] > 0.99
+    for its in (21, 22):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
+        assert np.array_equal(outs[0][1], outs[1][1])
