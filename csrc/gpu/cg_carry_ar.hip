@@ -42,6 +42,12 @@ namespace {
 
 #include "f1_common.hpp"
 
+// experiment: the even lean pass also streams x (reads it and writes it back unchanged), to tell a
+// per-step cost from a bytes-per-step one (profiles/r3/lean)
+#ifndef MCG_LEAN_XDUMMY
+#define MCG_LEAN_XDUMMY 0
+#endif
+
 #ifndef MCG_EDGE_BRANCHLESS
 #define MCG_EDGE_BRANCHLESS 1
 #endif
@@ -137,6 +143,32 @@ __device__ __forceinline__ void g_st_nt(double* base, uint32_t bo, double v) {
   else *(g_double*)((g_char*)(g_double*)base + bo) = v;
 }
 
+// Lean-run eligibility of one slice column's run [l0, l1) of a rank's nl lines (ss slices per
+// line): lines l0 - 1 .. l1 carry uniform patterns (one, B, for the inner lines; the rank's first
+// / last line their own, A / C, with B's slice-edge bits), and a column at a grid line's start /
+// end has the absent edge entry.  UNI: the caller is a wave (one run; values made wave-uniform).
+template <bool UNI>
+__device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat, int64_t l0, int64_t l1, int64_t nl,
+                                              int64_t ss, int64_t col, int64_t ext_len, uint32_t& WA, uint32_t& WB,
+                                              uint32_t& WC) {
+  auto ld = [&](int64_t i) { return UNI ? uni_u64(dpat[i]) : dpat[i]; };
+  WA = WB = WC = 0u;
+  if (dpat == nullptr || l1 - l0 < 3 || nl < 4 || ext_len >= ((int64_t)1 << 29)) return false;  // 32-bit byte offsets
+  const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;  // inner lines of l0 - 1 .. l1
+  const uint64_t wb = ld(ia * ss + col);
+  WB = (uint32_t)wb;
+  bool go = (WB >> 31) != 0u && (int64_t)(wb >> 32) >= ib - ia + 1;
+  if (l0 <= 1) {
+    WA = (uint32_t)ld(col);
+    go = go && (WA >> 31) != 0u && ((WA ^ WB) & (3u << 28)) == 0u;
+  }
+  if (l1 >= nl - 1) {
+    WC = (uint32_t)ld((nl - 1) * ss + col);
+    go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
+  }
+  return go && (col != 0 || ((WB >> 28) & 1u)) && (col != ss - 1 || ((WB >> 29) & 1u));
+}
+
 // per-slice metadata for the carry's codes loads: first slot / 64 (28 bits) | width << 28
 __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, uint32_t* __restrict__ meta) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
@@ -145,8 +177,9 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
   }
 }
 
-template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1>
-__global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
+// LEAN > 0: lean-only kernel (every run checked at setup) for at least LEAN waves per SIMD
+template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0>
+__global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
   __shared__ double2 s_dict[CM == 4 ? 1 : 256];
@@ -268,27 +301,12 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       // LD-step unroll rotates by renaming: no move of a register whose load is in flight.  Ghost
       // lines (P > 1) as in step(): their Ap_{k-1} exchanged (apx), r recovered from the halo's
       // p's; the rank's first / last line stores its Ap_k for the neighbours.
+      // LEAN: the setup checked every run of the launch (carry_lean_check), so the kernel has no
+      // generic step at all (its registers and scalar values are not in the way)
       constexpr int LD = QD + 1;
-      // a slice column at a grid line's start / end must have the absent edge entry (no load
-      // outside the ext vectors at the rank's first / last slice)
-      bool go = S.dpat != nullptr && n_run >= 3 && nl >= 4 && v.ext_len < ((int64_t)1 << 29);
-      uint32_t WA = 0, WB = 0, WC = 0;
-      if (go) {
-        const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;  // inner lines of l0 - 1 .. l1
-        const uint64_t wb = uni_u64(S.dpat[ia * SS + col]);
-        WB = (uint32_t)wb;
-        go = (WB >> 31) != 0u && (int64_t)(wb >> 32) >= ib - ia + 1;
-        if (l0 <= 1) {
-          WA = (uint32_t)uni_u64(S.dpat[col]);
-          go = go && (WA >> 31) != 0u && ((WA ^ WB) & (3u << 28)) == 0u;
-        }
-        if (l1 >= nl - 1) {
-          WC = (uint32_t)uni_u64(S.dpat[(nl - 1) * SS + col]);
-          go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
-        }
-        go = go && (col != 0 || ((WB >> 28) & 1u)) && (col != SS - 1 || ((WB >> 29) & 1u));
-      }
-      if (go) {
+      uint32_t WA, WB, WC;
+      const bool go = lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
+      if (LEAN > 0 || go) {
         struct VSet {
           double v[5];
         };
@@ -354,7 +372,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
             return q;
           };
           auto x_at = [&](int32_t j) {
-            if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+            if constexpr (PAIR || MCG_LEAN_XDUMMY) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
             else return 0.0;
           };
           auto ez = [&](double e) {
@@ -424,6 +442,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
               g_st(en, sb, sum);
             }
             if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+            else if constexpr (MCG_LEAN_XDUMMY) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, xs[0]);  // experiment
             g_st_nt(pn, ob + l8, o_pk);
             if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apx_n, ob + l8, sum);
             s_pap = fma(o_pk, sum, s_pap);
@@ -474,6 +493,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
         continue;
       }
     }
+    if constexpr (LEAN == 0) {
     // lines j (relative to l0) inside the ext vectors: [jmin, jmax]; loads clamp to them (values
     // of lines that do not exist are never multiplied: the matrix has no entry for them)
     const int32_t jmax = (ext32 - 64 - e0) / LO;
@@ -669,6 +689,7 @@ __global__ __launch_bounds__(kBS, 4) void k_cg_carry_ar(SellDev S, F1Vectors v, 
       }
     }
     for (; m < n_run; ++m) step(m);
+    }  // !LEAN
   }
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
@@ -714,7 +735,7 @@ __device__ __forceinline__ void ar3_finish(double a0, double a1, double a2, doub
   if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
 }
 
-template <int QD, bool PAIR, int KW, bool P3>
+template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false>
 __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                                   int32_t LN, int gfull,
                                                                   double* __restrict__ partials, int pstride,
@@ -824,24 +845,14 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       uint32_t WA = 0, WB = 0, WC = 0;
       bool go = false, zany = false;
       if (S.dpat != nullptr) {
-        go = n_run >= 3 && nl >= 4 && v.ext_len < ((int64_t)1 << 29);
-        if (go) {
-          const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;
-          const uint64_t wb = uni_u64(S.dpat[ia * SS + col]);
-          WB = (uint32_t)wb;
-          go = (WB >> 31) != 0u && (int64_t)(wb >> 32) >= ib - ia + 1;
-          if (l0 <= 1) {
-            WA = (uint32_t)uni_u64(S.dpat[col]);
-            go = go && (WA >> 31) != 0u && ((WA ^ WB) & (3u << 28)) == 0u;
-          }
-          if (l1 >= nl - 1) {
-            WC = (uint32_t)uni_u64(S.dpat[(nl - 1) * SS + col]);
-            go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
-          }
-          go = go && (col != 0 || ((WB >> 28) & 1u)) && (col != SS - 1 || ((WB >> 29) & 1u));
+        go = lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
+        if constexpr (LEAN) {  // every run checked at setup; the barrier after the last job's LDS reads
+          go = true;
+          zany = __syncthreads_or(((WB >> 28) & 3u) != 0u) != 0;
+        } else {
+          go = __syncthreads_and(go) != 0;
+          zany = go && __syncthreads_or(((WB >> 28) & 3u) != 0u) != 0;
         }
-        go = __syncthreads_and(go) != 0;
-        zany = go && __syncthreads_or(((WB >> 28) & 3u) != 0u) != 0;
       }
       if (go) {
         struct VSet {
@@ -1060,6 +1071,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
         continue;
       }
     }
+    if constexpr (!LEAN) {
     const int32_t jmax = (ext32 - 64 - e0) / LO;
     const int32_t jmin = -(e0 / LO);
     auto ebase = [&](int32_t j) { return e0 + (j < jmin ? jmin : (j > jmax ? jmax : j)) * LO; };
@@ -1242,6 +1254,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       c0 = c1;
       c1 = c2;
     }
+    }  // !LEAN
   }
   ar3_finish<KW>(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
@@ -1395,7 +1408,61 @@ __global__ __launch_bounds__(256) void k_dia_runs(uint64_t* __restrict__ dpat, i
   atomicAdd(nuni, cnt);
 }
 
+// carry_lean_failures: one thread per (job, wave) of the launch's job decomposition (k_cg_carry_ar:
+// kw = 0, one wave per job; k_cg_carry_ar3: kw waves per job, their slice columns)
+__global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
+                                                    int64_t ext_len, int64_t grid, int kw, int64_t ln,
+                                                    unsigned long long* __restrict__ fails) {
+  const int64_t waves = kw > 0 ? kw : 1;
+  int64_t jobs, runs;
+  if (kw == 0) {
+    const int64_t nw = grid * kWaves;
+    runs = nw > ss ? nw / ss : 1;
+    jobs = ss * runs;
+  } else {
+    const int64_t jpr = (ln / kw) * (ln / 64);
+    runs = grid > jpr ? grid / jpr : 1;
+    jobs = jpr * runs;
+  }
+  const int64_t chunk = (nl + runs - 1) / runs;
+  unsigned long long f = 0;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < jobs * waves; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t job = t / waves, wv = t % waves;
+    int64_t col, l0;
+    if (kw == 0) {
+      col = job % ss;
+      l0 = (job / ss) * chunk;
+    } else {
+      const int64_t jpr = (ln / kw) * (ln / 64), G = ln / 64, q = job % jpr;
+      col = ((q / G) * kw + wv) * G + q % G;
+      l0 = (job / jpr) * chunk;
+    }
+    const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
+    if (l0 >= l1) continue;
+    uint32_t a, b, c;
+    if (!lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c)) ++f;
+  }
+  if (f) atomicAdd(fails, f);
+}
+
 }  // namespace
+
+int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
+                            int32_t ln, hipStream_t stream) {
+  MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && (kw == 0 || (ln % 64 == 0 && ln % kw == 0)),
+            "lean check: bad launch geometry");
+  unsigned long long* f = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&f), sizeof(unsigned long long), stream), "device malloc failed(lean)");
+  MCG_HIP(hipMemsetAsync(f, 0, sizeof(unsigned long long), stream), "device memset failed");
+  hipLaunchKernelGGL(k_lean_check, dim3(64), dim3(256), 0, stream, dpat, ss, nl, ext_len, (int64_t)grid, kw,
+                     (int64_t)ln, f);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(lean check)");
+  unsigned long long h = 0;
+  MCG_HIP(hipMemcpyAsync(&h, f, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(lean check)");
+  (void)hipFreeAsync(f, stream);
+  return (int64_t)h;
+}
 
 int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64_t ss, int nslot, uint64_t* dpat,
                      hipStream_t stream) {
@@ -1474,7 +1541,8 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* d
 
 void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol, int first,
-                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3, int unroll) {
+                 int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3, int unroll,
+                 int lean) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
@@ -1501,6 +1569,23 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     return;
   }
   const bool pair = (k & 1) != 0;
+  if (cm == 4 && p3k && lean > 0 && S.dpat != nullptr) {  // lean-only kernels: depth 2 / 3, 4 / 6 / 8 waves per SIMD
+#define MCG_LW(QD, PAIR, W) \
+  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
+                     partials, pstride, st, tol, first, check, rc)
+#define MCG_LWQ(QD, PAIR)                 \
+  do {                                    \
+    if (lean >= 8) MCG_LW(QD, PAIR, 8);   \
+    else if (lean >= 6) MCG_LW(QD, PAIR, 6); \
+    else MCG_LW(QD, PAIR, 4);             \
+  } while (0)
+    if (depth >= 3) { if (pair) MCG_LWQ(3, true); else MCG_LWQ(3, false); }
+    else { if (pair) MCG_LWQ(2, true); else MCG_LWQ(2, false); }
+#undef MCG_LWQ
+#undef MCG_LW
+    MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+    return;
+  }
   const int qd = depth <= 2 ? 2 : 3;  // operand prefetch depth in lines (solver: 2 or 3)
 #define MCG_A(CM, U, QD, PAIR, P3, ...)                                                                 \
   hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR, P3, ##__VA_ARGS__>), dim3(grid), dim3(kBS), 0, stream, S, v, \
@@ -1533,7 +1618,8 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
 
 void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
-                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3) {
+                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3,
+                  bool lean) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0 && ln % 64 == 0 &&
                 (int64_t)ln * ln == (int64_t)tr.strip * 64 && (kw == 4 || kw == 8 || kw == 16) && ln % kw == 0,
@@ -1552,13 +1638,14 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
   const bool pair = (k & 1) != 0;
   const int qd = depth >= 3 ? 3 : 2;
   const int g = gfull ? 1 : 0;
-#define MCG_A3(QD, PAIR, KW, P3)                                                                              \
-  hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3>), dim3(grid), dim3(64 * KW), 0, stream, S, v, own_off, tr, \
-                     ln, g, partials, pstride, st, tol, first, check, rc)
-#define MCG_A3P(QD, PAIR, KW)                   \
-  do {                                          \
-    if (p3 && !first) MCG_A3(QD, PAIR, KW, true); \
-    else MCG_A3(QD, PAIR, KW, false);           \
+#define MCG_A3(QD, PAIR, KW, P3, ...)                                                                         \
+  hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, stream, S, v, \
+                     own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
+#define MCG_A3P(QD, PAIR, KW)                                         \
+  do {                                                                \
+    if (p3 && !first && lean && S.dpat != nullptr) MCG_A3(QD, PAIR, KW, true, true); \
+    else if (p3 && !first) MCG_A3(QD, PAIR, KW, true);                \
+    else MCG_A3(QD, PAIR, KW, false);                                 \
   } while (0)
 #define MCG_A3K(QD, PAIR)                       \
   do {                                          \

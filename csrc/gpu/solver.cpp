@@ -219,18 +219,22 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
       v.re_new = ape_[k & 1].get() + ns2;
     }
     if (ar3_) {
-      kern::cg_carry_ar3(2, info_.ar3_kw, S, v, L_.own_off, tr,
+      // lean runs in the 3-D passes that gain from them (lean3_: bit 0 even, bit 1 odd passes)
+      SellDev S3 = S;
+      if (!((lean3_ >> (k & 1)) & 1)) S3.dpat = nullptr;
+      kern::cg_carry_ar3(2, info_.ar3_kw, S3, v, L_.own_off, tr,
                          carry_lo2_, use_halo_, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode,
-                         s0_, rc, p3_);
+                         s0_, rc, p3_, false);
       return;
     }
     // three-term even passes: operands 2 lines ahead (chains of 3 registers, renamed by the 3-step unroll)
     // operand prefetch depth in lines: 3 (2-D: 318 vs 301 it/s at 2); the three-term even passes 2
     // (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md)
-    const int depth = ((k & 1) == 0 && p3_) ? 2 : 3;
+    int depth = ((k & 1) == 0 && p3_) ? 2 : 3;
+    if (lean_only_ && lean_depth_ > 0) depth = lean_depth_;
     kern::cg_carry_ar(dia4_.get() ? 4 : 2, info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
-                      p3_, 3);
+                      p3_, 3, lean_only_ ? lean_waves_ : 0);
     return;
   }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {

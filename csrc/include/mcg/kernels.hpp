@@ -285,14 +285,19 @@ int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64
 void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
                   int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
-                  bool p3 = false);
+                  bool p3 = false, bool lean = false);
+// Runs of a line (kw = 0, 2-D) / plane (kw = waves per block, 3-D, ln = N) carry launch of `grid`
+// blocks over ss * nl slices that do not qualify for the lean step (SellDev::dpat); 0 lets the
+// three-term passes launch their lean-only kernels (`lean`).  Synchronises the stream.
+int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
+                            int32_t ln, hipStream_t stream);
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals).  p3 (dia4): three-term form --
 // r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p buffers, r stored only at the slices' edge rows
 // and the runs' first / last lines (v.r_old / r_new hold just those rows; pass 0 reads r_{-1} = b)
 void cg_carry_ar(int cm,int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& slices, double* partials, int pstride, int grid, CgState* st, double tol,
                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
-                 bool p3 = false, int unroll = 1);
+                 bool p3 = false, int unroll = 1, int lean = 0);  // lean: > 0 lean-only kernels, waves per SIMD
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,
                      bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,

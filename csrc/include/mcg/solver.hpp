@@ -70,6 +70,7 @@ struct SolverInfo {
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
   double dia_uniform = 0.0;  // dia4 slices whose 64 rows share one value pattern (no codes streamed; PassForm::dia_uniform)
+  bool lean_only = false;    // every run of the three-term carry takes the lean step (lean-only kernels)
   int ar3_kw = 0;        // 3-D Ap-recomputing plane carry: waves (grid lines) per block; 0 = not in use
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
@@ -152,6 +153,10 @@ class GpuCgSolver {
   bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)
+  bool lean_only_ = false;      // ... every run lean (carry_lean_failures == 0)
+  int lean_depth_ = 0;          // experiment: operand prefetch depth of the 2-D lean-only passes (MCG_LEAN_DEPTH)
+  int lean_waves_ = 0;          // ... the waves per SIMD their kernels are built for
+  int lean3_ = 3;               // 3-D plane carry: lean runs in even (bit 0) / odd (bit 1) passes
   bool probing_ = false;        // placement probe running: passes take k's kernels, never first / check
   bool split_ = false;          // interior / boundary launches around an overlapped halo
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_

@@ -429,6 +429,7 @@ PYBIND11_MODULE(_C, m) {
         d["dia4"] = i.dia4;
         d["p3"] = i.p3;
         d["dia_uniform"] = i.dia_uniform;
+        d["lean_only"] = i.lean_only;
         d["ar3_kw"] = i.ar3_kw;
         d["carry_xchg"] = i.carry_xchg;
         d["placement_sets"] = i.placement_sets;
