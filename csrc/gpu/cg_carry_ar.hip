@@ -295,18 +295,18 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       // loads (p_{k-2} for lines of the run, the stored r_{k-1} beyond it, lines clamped to the
       // rank's), same stores (r in full on the run's first / last line, compact edge rows), same
       // partials.  A slice at the start / end of a grid line (lane 0 / 63 without its -1 / +1
-      // entry: dpat bits 28 / 29) multiplies that lane's edge operand, set to 0, by the slot's
-      // value instead of the operand by 0 -- the same sum, as a row sum is never -0.  Every
+      // entry: dpat bits 28 / 29) gives that lane the absent entry's value, +0.0, as its -1 / +1
+      // coefficient: per-lane coefficients for those two slots (the same fma).  Every
       // stream is a chain of LD registers (operands LD lines ahead, edges LD, x LD - 1) that the
       // LD-step unroll rotates by renaming: no move of a register whose load is in flight.  Ghost
       // lines (P > 1) as in step(): their Ap_{k-1} exchanged (apx), r recovered from the halo's
       // p's; the rank's first / last line stores its Ap_k for the neighbours.
-      // LEAN: the setup checked every run of the launch (carry_lean_check), so the kernel has no
-      // generic step at all (its registers and scalar values are not in the way)
+      // LEAN > 0 kernels only: the setup checked every run of the launch (carry_lean_failures), and
+      // the kernel has no generic step at all (one kernel with both measured slower for each)
       constexpr int LD = QD + 1;
       uint32_t WA, WB, WC;
-      const bool go = lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
-      if (LEAN > 0 || go) {
+      (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
+      if constexpr (LEAN > 0) {
         struct VSet {
           double v[5];
         };
@@ -317,11 +317,10 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           return V;
         };
         const bool z0 = (WB >> 28) & 1u, z63 = (WB >> 29) & 1u;
-        auto lean = [&](auto zlc) __attribute__((always_inline)) {
-          constexpr bool ZL = decltype(zlc)::value;
+        {
           const VSet VB = vals(WB);
           const bool hi = lane == 63, edge_lane = lane == 0 || lane == 63;
-          const bool zl = (lane == 0 && z0) || (hi && z63);  // lanes whose edge entry is absent
+          const bool zlo = lane == 0 && z0, zhi = hi && z63;  // lanes whose -1 / +1 entry is absent
           const uint32_t l8 = (uint32_t)lane << 3;
           const uint32_t LOB = (uint32_t)LO << 3;                         // one line of the vectors
           const uint32_t SB = (uint32_t)(2 * SS) << 3;                    // one line of the edge arrays
@@ -375,20 +374,18 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             if constexpr (PAIR || MCG_LEAN_XDUMMY) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
             else return 0.0;
           };
-          auto ez = [&](double e) {
-            if constexpr (ZL) return zl ? 0.0 : e;
-            else return e;
-          };
+          auto ez = [&](double e) { return e; };
           auto stencil_u = [&](const VSet& V, double mid, double edge, double dnl, double upl) {
             const double upv = lane_up_or(mid, edge);
             const double dnv = lane_dn_or(mid, edge);
+            const double cm = zlo ? 0.0 : V.v[1], cp = zhi ? 0.0 : V.v[3];  // loop-invariant
             double sum = fma(V.v[0], dnl, 0.0);
-            sum = fma(V.v[1], dnv, sum);
+            sum = fma(cm, dnv, sum);
             sum = fma(V.v[2], mid, sum);
-            sum = fma(V.v[3], upv, sum);
+            sum = fma(cp, upv, sum);
             return fma(V.v[4], upl, sum);
           };
-          auto epk = [&](const Edge& q) { return ez(fma(b, q.p, fma(na, q.a, q.r))); };
+          auto epk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };
           // prologue (step()'s): lines -2 .. LD - 1
           const Raw rm2 = raw_at(-2), rm1 = raw_at(-1), r0 = raw_at(0);
           Raw q[LD - 1];  // lines m + 1 .. m + LD - 1
@@ -487,9 +484,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
-        };
-        if (z0 || z63) lean(std::true_type{});
-        else lean(std::false_type{});
+        }
         continue;
       }
     }
@@ -843,18 +838,11 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       // renames both chain lengths
       constexpr int LD = 3, ED = 2, UNR = 6;
       uint32_t WA = 0, WB = 0, WC = 0;
-      bool go = false, zany = false;
-      if (S.dpat != nullptr) {
-        go = lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
-        if constexpr (LEAN) {  // every run checked at setup; the barrier after the last job's LDS reads
-          go = true;
-          zany = __syncthreads_or(((WB >> 28) & 3u) != 0u) != 0;
-        } else {
-          go = __syncthreads_and(go) != 0;
-          zany = go && __syncthreads_or(((WB >> 28) & 3u) != 0u) != 0;
-        }
+      if constexpr (LEAN) {  // every run checked at setup (carry_lean_failures)
+        (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
+        __syncthreads();  // the previous job's last step has read its LDS slots
       }
-      if (go) {
+      if constexpr (LEAN) {
         struct VSet {
           double v[7];
         };
@@ -867,11 +855,10 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
         const bool z0 = (WB >> 28) & 1u, z63 = (WB >> 29) & 1u;
         const int64_t yl = (q / G) * KW + wv;  // the wave's grid line
         const bool fnone = (odn && yl == 0) || (oup && yl == LN - 1);
-        auto lean = [&](auto zlc) __attribute__((always_inline)) {
-          constexpr bool ZL = decltype(zlc)::value;
+        {
           const VSet VB = vals(WB);
           const bool hi = lane == 63, edge_lane = lane == 0 || lane == 63;
-          const bool zl = (lane == 0 && z0) || (hi && z63);
+          const bool zlo = lane == 0 && z0, zhi = hi && z63;  // lanes whose -1 / +1 entry is absent
           const bool outer = odn || oup;
           const uint32_t l8 = (uint32_t)lane << 3;
           const uint32_t LOB = (uint32_t)LO << 3;                         // one plane of the vectors
@@ -927,22 +914,20 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
             if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
             else return 0.0;
           };
-          auto ez = [&](double e) {
-            if constexpr (ZL) return zl ? 0.0 : e;
-            else return e;
-          };
+          auto ez = [&](double e) { return e; };
           auto stencil_u = [&](const VSet& V, double mid, double edge, double dnl, double upl, double dnn, double upn) {
             const double upv = lane_up_or(mid, edge);
             const double dnv = lane_dn_or(mid, edge);
+            const double cm = zlo ? 0.0 : V.v[2], cp = zhi ? 0.0 : V.v[4];  // loop-invariant
             double sum = fma(V.v[0], dnl, 0.0);
             sum = fma(V.v[1], dnn, sum);
-            sum = fma(V.v[2], dnv, sum);
+            sum = fma(cm, dnv, sum);
             sum = fma(V.v[3], mid, sum);
-            sum = fma(V.v[4], upv, sum);
+            sum = fma(cp, upv, sum);
             sum = fma(V.v[5], upn, sum);
             return fma(V.v[6], upl, sum);
           };
-          auto epk = [&](const Edge& e) { return ez(pk_of(e.r, e.a, e.p)); };
+          auto epk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
           // prologue (the generic one's): planes -2 .. LD - 1
           const Raw rm2 = raw_ld(-2, jc(-2)), rm1 = raw_ld(-1, jc(-1)), r0 = raw_ld(0, 0);
           Raw qv[LD - 1];  // planes m + 1 .. m + LD - 1
@@ -1065,9 +1050,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
               lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
-        };
-        if (zany) lean(std::true_type{});
-        else lean(std::false_type{});
+        }
         continue;
       }
     }

@@ -219,12 +219,9 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
       v.re_new = ape_[k & 1].get() + ns2;
     }
     if (ar3_) {
-      // lean runs in the 3-D passes that gain from them (lean3_: bit 0 even, bit 1 odd passes)
-      SellDev S3 = S;
-      if (!((lean3_ >> (k & 1)) & 1)) S3.dpat = nullptr;
-      kern::cg_carry_ar3(2, info_.ar3_kw, S3, v, L_.own_off, tr,
+      kern::cg_carry_ar3(2, info_.ar3_kw, S, v, L_.own_off, tr,
                          carry_lo2_, use_halo_, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode,
-                         s0_, rc, p3_, false);
+                         s0_, rc, p3_, lean_only_ && ((lean3_ >> (k & 1)) & 1));
       return;
     }
     // three-term even passes: operands 2 lines ahead (chains of 3 registers, renamed by the 3-step unroll)

@@ -565,10 +565,10 @@ void GpuCgSolver::setup() {
   if (use_comm_ && world_ > 1 && !all_ranks_agree_(p3_)) p3_ = false;
   MCG_CHECK(opt_.form.p3 != 1 || p3_, "p3 needs the Ap-recomputing line / plane carry on SELL-64/dia4");
   info_.p3 = p3_;
-  // lean-only three-term passes (2-D): every run of the launch takes the lean step, so the kernels
-  // without the generic step run (cg_carry_ar.hip, LEAN = waves per SIMD they are built for); the
-  // 3-D lean-only kernels spill (726 vs 927 it/s at 512^3, profiles/r3/lean), so 3-D keeps the lean
-  // step inside the generic kernel
+  // lean-only three-term passes: every run of the launch takes the lean step, so the kernels
+  // without the generic step run (cg_carry_ar.hip: LEAN = waves per SIMD the 2-D kernels are built
+  // for; 3-D: LEAN); otherwise the generic kernels (no lean code: one kernel holding both measured
+  // slower for each, profiles/r3/lean)
   lean_only_ = false;
   lean_waves_ = 0;
   auto env_int = [](const char* k, int d) {
@@ -577,11 +577,13 @@ void GpuCgSolver::setup() {
   };
   lean_depth_ = env_int("MCG_LEAN_DEPTH", 0);  // experiments (profiles/r3/lean)
   lean3_ = env_int("MCG_LEAN3", 3);
-  if (p3_ && !ar3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0 && env_int("MCG_LEAN_ONLY", 1) != 0) {
-    const int lw = env_int("MCG_LEAN_WAVES", 4), rounds = env_int("MCG_LEAN_ROUNDS", 0);
+  if (p3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0 && env_int("MCG_LEAN_ONLY", 1) != 0) {
+    // 2-D: 16 blocks per CU (4 rounds of resident blocks): 585.8 vs 581 it/s at 8 (profiles/r3/lean)
+    const int lw = env_int("MCG_LEAN_WAVES", 4), rounds = ar3_ ? 0 : env_int("MCG_LEAN_ROUNDS", 4);
     const int g = rounds > 0 ? ncu_ * lw * rounds : g_all_;
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
-    if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, 0, 0, s0_) == 0) {
+    if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, ar3_ ? info_.ar3_kw : 0,
+                                  ar3_ ? carry_lo2_ : 0, s0_) == 0) {
       lean_only_ = true;
       lean_waves_ = lw;
       g_all_ = g;
