@@ -53,6 +53,8 @@ def pass_label(info, problem):
             kind += ", three-term (r from p_{k-1}, p_{k-2})"
         if info.get("ap_recompute"):
             kind += ", Ap recomputed"
+        if info.get("lean_only"):
+            kind += ", lean runs (values in scalar registers, no codes streamed)"
         return kind
     if info.get("pmat"):
         return "split (materialized p)"
@@ -293,8 +295,10 @@ def _run_rank(args, out_fd) -> int:
                 "seq_len": spec.n_rows,
                 "parallelism": (f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else
                                 f"rehearse-rowpart{n_gpus}-one-gpu" if rehearse else f"rowpart{n_gpus}"),
-                # storage the timed pass streams (the carries read SELL-64/dia4 codes)
-                "format": "sell64-dia4" if info.get("dia4") else info["format"],
+                # storage the timed pass streams (the carries read SELL-64/dia4 codes; their lean runs
+                # only the per-slice pattern words of uniform slices)
+                "format": (("sell64-dia4, uniform-slice patterns" if info.get("lean_only") else "sell64-dia4")
+                           if info.get("dia4") else info["format"]),
                 "recurrence": info["recurrence"],
                 "pass": pass_label(info, args.problem),
                 **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
@@ -313,6 +317,7 @@ def _run_rank(args, out_fd) -> int:
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
                       "placement_lead_trial": info.get("placement_lead_trial"),
+                      "dia_uniform": round(info.get("dia_uniform", 0.0), 4), "lean_only": info.get("lean_only", False),
                       **({"ag_local_frac": round(info["ag_local_frac"], 4)} if info.get("ag_overlap") else {}),
                       "model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
                       "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3),

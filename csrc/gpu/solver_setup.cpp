@@ -580,8 +580,12 @@ void GpuCgSolver::setup() {
   if (p3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0 && env_int("MCG_LEAN_ONLY", 1) != 0) {
     // 2-D: 16 blocks per CU (4 rounds of resident blocks): 585.8 vs 581 it/s at 8 (profiles/r3/lean)
     const int lw = env_int("MCG_LEAN_WAVES", 4), rounds = ar3_ ? 0 : env_int("MCG_LEAN_ROUNDS", 4);
-    const int g = rounds > 0 ? ncu_ * lw * rounds : g_all_;
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
+    // the larger grid only where its runs stay long (>= 64 lines; shorter ones re-read their
+    // prologue lines too often)
+    const int64_t gw = (int64_t)ncu_ * lw * rounds * 4;  // waves (256-thread blocks)
+    const bool big = rounds > 0 && nlines / std::max<int64_t>(1, gw / tr_all_.strip) >= 64;
+    const int g = big ? ncu_ * lw * rounds : g_all_;
     if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, ar3_ ? info_.ar3_kw : 0,
                                   ar3_ ? carry_lo2_ : 0, s0_) == 0) {
       lean_only_ = true;
