@@ -20,9 +20,10 @@ __device__ __forceinline__ double add(double a, double b) { return a + 0.5 * b; 
 __device__ __forceinline__ d2v add(d2v a, d2v b) { return a + 0.5 * b; }
 
 // D-line chains rotated by renaming under a D-step unroll
-template <int W, int D>
+// NT: non-temporal stores; OUTC: write a third buffer instead of overwriting pb (in place, as the pass)
+template <int W, int D, bool NT = true, bool OUTC = false, bool NOST = false>
 __global__ __launch_bounds__(256) void k_walk(const double* __restrict__ pa, double* __restrict__ pb, int64_t lines,
-                                              int64_t line_len, int64_t runs) {
+                                              int64_t line_len, int64_t runs, double* __restrict__ pc) {
   typedef typename Vec<W>::T T;
   const int lane = threadIdx.x & 63;
   const int64_t cols = line_len / (64 * W);
@@ -34,7 +35,8 @@ __global__ __launch_bounds__(256) void k_walk(const double* __restrict__ pa, dou
     if (l1 - l0 <= D) continue;
     const T* a = reinterpret_cast<const T*>(pa + l0 * line_len + col * 64 * W) + lane;
     const T* b = reinterpret_cast<const T*>(pb + l0 * line_len + col * 64 * W) + lane;
-    T* o = reinterpret_cast<T*>(pb + l0 * line_len + col * 64 * W) + lane;
+    T* o = reinterpret_cast<T*>((OUTC ? pc : pb) + l0 * line_len + col * 64 * W) + lane;
+    T acc = T{};
     const int64_t ls = line_len / W;  // one line, in T
     T qa[D], qb[D];
 #pragma unroll
@@ -48,46 +50,56 @@ __global__ __launch_bounds__(256) void k_walk(const double* __restrict__ pa, dou
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const T na = a[(m + u + D) * ls], nb = b[(m + u + D) * ls];
-        __builtin_nontemporal_store(add(qa[u], qb[u]), &o[(m + u) * ls]);
+        if constexpr (NOST) acc = add(acc, add(qa[u], qb[u]));
+        else if constexpr (NT) __builtin_nontemporal_store(add(qa[u], qb[u]), &o[(m + u) * ls]);
+        else o[(m + u) * ls] = add(qa[u], qb[u]);
         qa[u] = na;
         qb[u] = nb;
       }
+    }
+    if constexpr (NOST) {
+      if (lines < 0) o[0] = acc;  // keeps the loads
     }
   }
 }
 
 int main() {
   const int64_t line_len = 16384, lines = 16384, n = line_len * lines;
-  double *a, *b;
+  double *a, *b, *c;
   CK(hipMalloc(&a, n * 8));
   CK(hipMalloc(&b, n * 8 + 4096));
+  CK(hipMalloc(&c, n * 8 + 4096));
   CK(hipMemset(a, 0, n * 8));
   CK(hipMemset(b, 0, n * 8));
+  CK(hipMemset(c, 0, n * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   int ncu = 0;
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
-  auto run = [&](const char* name, auto kern, int bpc, int64_t cols) {
+  auto run = [&](const char* name, auto kern, int bpc, int64_t cols, double streams = 3.0) {
     const int grid = ncu * bpc;
     const int64_t nw = (int64_t)grid * 4, runs = nw > cols ? nw / cols : 1;
-    for (int it = 0; it < 2; ++it) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, a, b, lines, line_len, runs);
+    for (int it = 0; it < 2; ++it) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, a, b, lines, line_len, runs, c);
     hipEventRecord(e0);
     const int reps = 10;
-    for (int it = 0; it < reps; ++it) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, a, b, lines, line_len, runs);
+    for (int it = 0; it < reps; ++it) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, a, b, lines, line_len, runs, c);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     ms /= reps;
-    printf("%-28s blocks/CU %2d  %.3f ms  %.2f TB/s\n", name, bpc, ms, 3.0 * n * 8 / (ms * 1e-3) / 1e12);
+    printf("%-34s blocks/CU %2d  %.3f ms  %.2f TB/s\n", name, bpc, ms, streams * n * 8 / (ms * 1e-3) / 1e12);
     fflush(stdout);
   };
   for (int bpc : {8, 16}) {
-    run("W=1 (8-B lanes) D=3", k_walk<1, 3>, bpc, line_len / 64);
-    run("W=1 (8-B lanes) D=4", k_walk<1, 4>, bpc, line_len / 64);
-    run("W=2 (16-B lanes) D=3", k_walk<2, 3>, bpc, line_len / 128);
-    run("W=2 (16-B lanes) D=4", k_walk<2, 4>, bpc, line_len / 128);
+    run("W=1 D=3 in place, nt", k_walk<1, 3>, bpc, line_len / 64);
+    run("W=1 D=3 in place, plain stores", k_walk<1, 3, false>, bpc, line_len / 64);
+    run("W=1 D=3 third buffer, nt", k_walk<1, 3, true, true>, bpc, line_len / 64);
+    run("W=1 D=3 third buffer, plain", k_walk<1, 3, false, true>, bpc, line_len / 64);
+    run("W=1 D=3 reads only (2R)", k_walk<1, 3, true, false, true>, bpc, line_len / 64, 2.0);
+    run("W=2 D=3 in place, nt", k_walk<2, 3>, bpc, line_len / 128);
+    run("W=2 D=3 third buffer, nt", k_walk<2, 3, true, true>, bpc, line_len / 128);
   }
   return 0;
 }
