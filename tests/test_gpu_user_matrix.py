@@ -203,3 +203,42 @@ def test_csr_row_length_adaptive_engine(mcg, recurrence):
         assert outs[v]["converged"] and abs(outs[v]["iterations"] - cpu["iterations"]) <= 2
         np.testing.assert_allclose(outs[v]["x_local"], cpu["x"], rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(outs[-1]["x_local"], outs[2]["x_local"], rtol=1e-8, atol=1e-11)
+
+
+@pytest.mark.parametrize("kind", ["shift", "spot", "lines"])
+def test_lean_runs_on_user_stencils(mcg, kind):
+    """Lean runs on user stencil matrices (the dia4 three-term carry): a diagonal shifted everywhere
+    keeps every slice uniform (one pattern, lean-only kernels); one changed row leaves one slice
+    non-uniform, and a shift on every 7th grid line changes the pattern down every slice column --
+    in both the setup check finds runs that do not qualify and the generic kernels run.  Every
+    case is bit for bit the solve with dia_uniform = 0."""
+    n = 1024
+    A = _poisson(n, 2).tolil()
+    d = A.diagonal()
+    if kind == "shift":
+        d = d + 0.5
+    elif kind == "spot":
+        d[n * 300 + 500] += 0.5
+    else:
+        d = d + 0.25 * (((np.arange(n * n) // n) % 7) == 3)
+    A.setdiag(d)
+    p = mcg.csr_problem(A.tocsr(), rhs="random")
+    a = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8)
+    b = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, dia_uniform=0)
+    assert a.info["dia4"] and a.info["p3"] and b.info["p3"]
+    if kind == "shift":
+        assert a.info["dia_uniform"] == 1.0 and a.info["lean_only"]
+    elif kind == "spot":
+        assert a.info["dia_uniform"] < 1.0 and not a.info["lean_only"]
+    else:
+        assert a.info["dia_uniform"] == 1.0 and not a.info["lean_only"]
+    outs = []
+    for s in (a, b):
+        s.reset()
+        s.run(41)
+        s.finalize()
+        outs.append((s.result(), s._s.x_local()))
+    assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
+    assert np.array_equal(outs[0][1], outs[1][1])
+    tr = a.true_residual_norm()
+    assert abs(tr - outs[0][0]["rnorm"]) <= 1e-8 * tr
