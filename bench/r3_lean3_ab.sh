@@ -1,5 +1,7 @@
 #!/bin/bash
 # r3: 3-D lean runs per pass parity (MCG_LEAN3: bit 0 even, bit 1 odd passes), 512^3, interleaved
+# (historical: the MCG_LEAN_* setup knobs these runs set were removed once the defaults were chosen;
+#  the results are in profiles/r3/lean/)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3l3}

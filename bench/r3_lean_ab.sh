@@ -1,5 +1,7 @@
 #!/bin/bash
 # r3 lean-run A/B on one box: lean-only kernels vs lean inside the generic kernel, operand prefetch
+# (historical: the MCG_LEAN_* setup knobs these runs set were removed once the defaults were chosen;
+#  the results are in profiles/r3/lean/)
 # depth of the lean-only 2-D passes (MCG_LEAN_DEPTH), 2-D and 3-D.  One JSON line per run.
 set -o pipefail
 cd $GRAFT_REPO_ROOT

@@ -1,5 +1,7 @@
 #!/bin/bash
 # r3: lean-only kernels vs the generic ones, 2-D grid / waves and 3-D per-parity, one box, interleaved
+# (historical: the MCG_LEAN_* setup knobs these runs set were removed once the defaults were chosen;
+#  the results are in profiles/r3/lean/)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3ab2}

@@ -42,12 +42,6 @@ namespace {
 
 #include "f1_common.hpp"
 
-// experiment: the even lean pass also streams x (reads it and writes it back unchanged), to tell a
-// per-step cost from a bytes-per-step one (profiles/r3/lean)
-#ifndef MCG_LEAN_XDUMMY
-#define MCG_LEAN_XDUMMY 0
-#endif
-
 #ifndef MCG_EDGE_BRANCHLESS
 #define MCG_EDGE_BRANCHLESS 1
 #endif
@@ -371,7 +365,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             return q;
           };
           auto x_at = [&](int32_t j) {
-            if constexpr (PAIR || MCG_LEAN_XDUMMY) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+            if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
             else return 0.0;
           };
           auto ez = [&](double e) { return e; };
@@ -439,7 +433,6 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               g_st(en, sb, sum);
             }
             if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-            else if constexpr (MCG_LEAN_XDUMMY) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, xs[0]);  // experiment
             g_st_nt(pn, ob + l8, o_pk);
             if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apx_n, ob + l8, sum);
             s_pap = fma(o_pk, sum, s_pap);
@@ -1525,7 +1518,7 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* d
 void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& tr, double* partials, int pstride, int grid, CgState* st, double tol, int first,
                  int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3, int unroll,
-                 int lean) {
+                 bool lean) {
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
@@ -1552,19 +1545,12 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     return;
   }
   const bool pair = (k & 1) != 0;
-  if (cm == 4 && p3k && lean > 0 && S.dpat != nullptr) {  // lean-only kernels: depth 2 / 3, 4 / 6 / 8 waves per SIMD
-#define MCG_LW(QD, PAIR, W) \
-  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
+  if (cm == 4 && p3k && lean && S.dpat != nullptr) {  // lean-only kernels (4 waves per SIMD)
+#define MCG_LW(QD, PAIR) \
+  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
                      partials, pstride, st, tol, first, check, rc)
-#define MCG_LWQ(QD, PAIR)                 \
-  do {                                    \
-    if (lean >= 8) MCG_LW(QD, PAIR, 8);   \
-    else if (lean >= 6) MCG_LW(QD, PAIR, 6); \
-    else MCG_LW(QD, PAIR, 4);             \
-  } while (0)
-    if (depth >= 3) { if (pair) MCG_LWQ(3, true); else MCG_LWQ(3, false); }
-    else { if (pair) MCG_LWQ(2, true); else MCG_LWQ(2, false); }
-#undef MCG_LWQ
+    if (depth >= 3) { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
+    else { if (pair) MCG_LW(2, true); else MCG_LW(2, false); }
 #undef MCG_LW
     MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
     return;

@@ -221,17 +221,16 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     if (ar3_) {
       kern::cg_carry_ar3(2, info_.ar3_kw, S, v, L_.own_off, tr,
                          carry_lo2_, use_halo_, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode,
-                         s0_, rc, p3_, lean_only_ && ((lean3_ >> (k & 1)) & 1));
+                         s0_, rc, p3_, lean_only_);
       return;
     }
     // three-term even passes: operands 2 lines ahead (chains of 3 registers, renamed by the 3-step unroll)
     // operand prefetch depth in lines: 3 (2-D: 318 vs 301 it/s at 2); the three-term even passes 2
     // (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md)
-    int depth = ((k & 1) == 0 && p3_) ? 2 : 3;
-    if (lean_only_ && lean_depth_ > 0) depth = lean_depth_;
+    const int depth = ((k & 1) == 0 && p3_) ? 2 : 3;
     kern::cg_carry_ar(dia4_.get() ? 4 : 2, info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
-                      p3_, 3, lean_only_ ? lean_waves_ : 0);
+                      p3_, 3, lean_only_);
     return;
   }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {

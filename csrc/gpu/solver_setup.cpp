@@ -4,7 +4,6 @@
 #include "mcg/solver.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -570,26 +569,25 @@ void GpuCgSolver::setup() {
   // for; 3-D: LEAN); otherwise the generic kernels (no lean code: one kernel holding both measured
   // slower for each, profiles/r3/lean)
   lean_only_ = false;
-  lean_waves_ = 0;
-  auto env_int = [](const char* k, int d) {
-    const char* e = std::getenv(k);
-    return e != nullptr ? std::atoi(e) : d;
-  };
-  lean_depth_ = env_int("MCG_LEAN_DEPTH", 0);  // experiments (profiles/r3/lean)
-  lean3_ = env_int("MCG_LEAN3", 3);
-  if (p3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0 && env_int("MCG_LEAN_ONLY", 1) != 0) {
-    // 2-D: 16 blocks per CU (4 rounds of resident blocks): 585.8 vs 581 it/s at 8 (profiles/r3/lean)
-    const int lw = env_int("MCG_LEAN_WAVES", 4), rounds = ar3_ ? 0 : env_int("MCG_LEAN_ROUNDS", 4);
+  if (p3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0) {
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
-    // the larger grid only where its runs stay long (>= 64 lines; shorter ones re-read their
-    // prologue lines too often)
-    const int64_t gw = (int64_t)ncu_ * lw * rounds * 4;  // waves (256-thread blocks)
-    const bool big = rounds > 0 && nlines / std::max<int64_t>(1, gw / tr_all_.strip) >= 64;
-    const int g = big ? ncu_ * lw * rounds : g_all_;
+    int g = g_all_;
+    if (!ar3_) {
+      // 2-D: the largest grid of 16 / 8 / 4 blocks per CU whose runs keep >= 64 lines (shorter runs
+      // re-read their prologue lines too often): 16384^2 16 per CU, 585.8 vs 581 it/s at 8; 4096^2
+      // 4 per CU, 8592-8655 vs 7911-8484 at 8; a P = 8 share of 16384^2 8 per CU, within noise of 4
+      // (profiles/r3/lean)
+      for (int bpc : {16, 8, 4}) {
+        const int64_t waves = (int64_t)ncu_ * bpc * 4;  // 256-thread blocks
+        if (nlines / std::max<int64_t>(1, waves / tr_all_.strip) >= 64) {
+          g = ncu_ * bpc;
+          break;
+        }
+      }
+    }
     if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, ar3_ ? info_.ar3_kw : 0,
                                   ar3_ ? carry_lo2_ : 0, s0_) == 0) {
       lean_only_ = true;
-      lean_waves_ = lw;
       g_all_ = g;
     }
   }

@@ -297,7 +297,7 @@ int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_
 void cg_carry_ar(int cm,int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
                  const TileRanges& slices, double* partials, int pstride, int grid, CgState* st, double tol,
                  int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
-                 bool p3 = false, int unroll = 1, int lean = 0);  // lean: > 0 lean-only kernels, waves per SIMD
+                 bool p3 = false, int unroll = 1, bool lean = false);  // lean: the lean-only kernels
 void cg_fused1_carry(int cm /* 1 SELL-64/d16, 2 SELL-64/c8, 3 SELL-64/c4 */, int param, int depth /* operand prefetch, lines */,
                      bool general /* false: every dictionary offset is 0, +-1, +-one line or +-lo2 (no slow path) */,
                      int32_t lo2 /* > 0: a second carried offset, gathered one line ahead (3-D: N); 0 = none */,

@@ -154,9 +154,6 @@ class GpuCgSolver {
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)
   bool lean_only_ = false;      // ... every run lean (carry_lean_failures == 0)
-  int lean_depth_ = 0;          // experiment: operand prefetch depth of the 2-D lean-only passes (MCG_LEAN_DEPTH)
-  int lean_waves_ = 0;          // ... the waves per SIMD their kernels are built for
-  int lean3_ = 3;               // 3-D plane carry: lean runs in even (bit 0) / odd (bit 1) passes
   bool probing_ = false;        // placement probe running: passes take k's kernels, never first / check
   bool split_ = false;          // interior / boundary launches around an overlapped halo
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
