@@ -52,7 +52,8 @@ def main():
         if ref is None:
             ref = rn
         line = {"world": w, "overlap": not args.no_overlap, "iterations": r[0]["iterations"], "rnorm": rn, "true_rnorm": tr,
-                "rel_vs_first": abs(rn - ref) / ref, "ok": ok}
+                "rel_vs_first": abs(rn - ref) / ref, "ok": ok,
+                "lean_only": all(x.get("lean_only", False) for x in r)}
         if args.phases:  # worst rank per phase (the ranks share one GPU: relative sizes, not speed)
             keys = sorted(r[0]["phases"])
             line["phase_us_max"] = {k: round(max(x["phases"][k] for x in r), 2) for k in keys}

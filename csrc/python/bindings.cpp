@@ -462,6 +462,7 @@ PYBIND11_MODULE(_C, m) {
       d["true_rnorm"] = rr.true_rnorm;
       d["carry"] = rr.carry;
       d["ap_recompute"] = rr.ap_recompute;
+      d["lean_only"] = rr.lean_only;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;
       py::dict ph;

@@ -124,6 +124,10 @@ def test_bench_pass_labels():
     assert bench.pass_label({"recurrence": "pipelined", "pipe_rr": 0}, "randspd").startswith("pipelined CG")
     assert bench.pass_label({"pmat": True}, "randspd") == "split (materialized p)"
     assert bench.pass_label({}, "randspd") == "generic"
+    # the lean-only kernels (uniform slice patterns) are named; the generic three-term ones are not
+    assert bench.pass_label(dict(carry3, lean_only=True), "poisson3d").endswith(
+        "lean runs (values in scalar registers, no codes streamed)")
+    assert "lean" not in bench.pass_label(dict(carry3, lean_only=False), "poisson3d")
 
 
 def test_kfd_gpu_count_from_a_fake_topology(tmp_path):
