@@ -17,10 +17,13 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def us_per_iter(C, spec, recurrence, delay, fat, graph, overlap, world, rank, iters, fmt, pipe_rr=0, halo_us=0.0):
+def us_per_iter(C, spec, recurrence, delay, fat, graph, overlap, world, rank, iters, fmt, pipe_rr=0, halo_us=0.0,
+                reserve_cus=0, halo_ahead=-1):
     o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=overlap, use_graph=graph, format=fmt,
                     recurrence=recurrence)
     o.pipe_rr = pipe_rr
+    o.reserve_cus = reserve_cus
+    o.halo_ahead = halo_ahead
     comm = C.DelayComm(rank, world, delay, halo_us, fat)
     s = C.Solver(spec.native(), o, rank, world, comm)
     s.setup()
@@ -55,6 +58,8 @@ def main():
     ap.add_argument("--format", default="sellc8")
     ap.add_argument("--pipe-rr", type=int, default=0)
     ap.add_argument("--halo-us", type=float, default=0.0, help="device-side delay of each halo exchange")
+    ap.add_argument("--reserve-cus", default="0", help="CgOptions.reserve_cus values (CU-masked compute stream)")
+    ap.add_argument("--halo-ahead", default="-1", help="PassForm.halo_ahead values (0: interior || halo split)")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime initialised as in the other tools)
 
@@ -64,15 +69,17 @@ def main():
     spec = (mcg.make_problem("randspd", rows=a.rows, band=a.band, density=a.density, rhs="random")
             if a.problem == "randspd" else mcg.make_problem(a.problem, n=a.grid, rhs="random"))
     ints = lambda s: [int(v) for v in s.split(",")]  # noqa: E731
-    for rec, g, ov, fat, d in itertools.product(ints(a.recurrences), ints(a.graphs), ints(a.overlaps), ints(a.fat),
-                                                [float(v) for v in a.delays.split(",")]):
+    for rec, g, ov, fat, d, rc, ha in itertools.product(ints(a.recurrences), ints(a.graphs), ints(a.overlaps),
+                                                        ints(a.fat), [float(v) for v in a.delays.split(",")],
+                                                        ints(a.reserve_cus), ints(a.halo_ahead)):
         us, info = us_per_iter(C, spec, rec, d, bool(fat), bool(g), bool(ov), a.world, a.rank, a.iters, a.format,
-                               a.pipe_rr if rec == 2 else 0, a.halo_us)
+                               a.pipe_rr if rec == 2 else 0, a.halo_us, rc, ha)
         print(json.dumps({"recurrence": info["recurrence"], "graph": g, "overlap": ov, "fat": fat, "delay_us": d,
                           "us_per_iter": round(us, 2), "graph_fallbacks": info.get("graph_fallbacks"),
                           "pipe_rr": info.get("pipe_rr"), "ar_first": info.get("pipe_ar_first"),
                           "t_spmv": round(info.get("pipe_spmv_us", 0), 1), "t_ar": round(info.get("pipe_allreduce_us", 0), 1), "format": info["format"], "carry": info.get("carry"), "pmat": info.get("pmat"),
                           "problem": a.problem, "world": a.world, "rank": a.rank, "halo_us": a.halo_us,
+                          "reserve_cus": rc, "halo_ahead": ha, "halo_ahead_on": info.get("halo_ahead"),
                           "grid": a.grid}),
               flush=True)
 

@@ -53,7 +53,19 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   // the split pass, whose ghosts come from its own update kernel; decided in setup())
   prefetch_halo_ = use_halo_ && opt_.overlap && !opt_.use_graph && !L_.allgather;
   ncu_ = kern::num_cus();
-  s0_ = Stream(true, 0);
+  MCG_CHECK(opt_.reserve_cus >= 0 && opt_.reserve_cus <= ncu_ / 4, "reserve_cus must leave >= 3/4 of the CUs");
+  if (opt_.reserve_cus > 0) {
+    // withhold the top reserve_cus bits of the mask.  Bit i is CU slot i / 32 of shader engine (i / 8) % 4
+    // of XCD i % 8 (__smid of a masked grid, profiles/r3_cumask_probe.md), so 32 withholds one CU per
+    // shader engine: the dispatcher spreads a grid's blocks evenly over the XCDs and their SEs, and any
+    // other count leaves some SE with fewer CUs for the same share of blocks
+    std::vector<uint32_t> mask((ncu_ + 31) / 32, 0u);
+    for (int i = 0; i < ncu_ - opt_.reserve_cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    s0_ = Stream::with_cu_mask(mask);
+    ncu_ -= opt_.reserve_cus;
+  } else {
+    s0_ = Stream(true, 0);
+  }
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
   ev_r_ = Event(true);
   ev_h_ = Event(true);

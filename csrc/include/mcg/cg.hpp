@@ -116,6 +116,10 @@ struct CgOptions {
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   double watchdog_seconds = 0.0;  // > 0: solve() fails (and aborts the communicator) if one poll interval
                                   // makes no progress for this long (bounded host wait)
+  int reserve_cus = 0;       // CUs withheld from the compute stream (a CU-masked queue, the mask's top bits; 32 = one
+                             // per shader engine) so a collective's ~270-VGPR kernels find a free CU beside the
+                             // resident pass (profiles/r3_cumask_probe.md); the pass grids are sized for the CUs
+                             // left.  0 = off
   PassForm form;             // pass-form overrides (auto by default)
   TestHooks hooks;           // test / fault-injection hooks
 };

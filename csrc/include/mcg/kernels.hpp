@@ -404,7 +404,9 @@ int grid_for(int64_t work_items, int block, int blocks_per_cu);
 // ---- probes (csrc/gpu/probe_kernels.hip) ----
 // `blocks` workgroups of 256 threads spinning for `microseconds` on the realtime clock; fat: ~270
 // VGPRs per wave live (RCCL's kernels' footprint), else a handful.  out: one double per block or null
-void spin(double* out, double microseconds, bool fat, int blocks, hipStream_t stream);
+void spin(double* out, double microseconds, bool fat, int blocks, hipStream_t stream, int* where = nullptr);
+// the same with ~120 VGPRs per wave (4 blocks of 256 per CU fill a CU's register file)
+void hog(double* out, double microseconds, int blocks, hipStream_t stream, int* where = nullptr);
 
 }  // namespace kern
 }  // namespace mcg

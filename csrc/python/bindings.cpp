@@ -235,6 +235,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("rtol", &CgOptions::rtol)
       .def_readwrite("watchdog_seconds", &CgOptions::watchdog_seconds)
       .def_readwrite("check_every", &CgOptions::check_every)
+      .def_readwrite("reserve_cus", &CgOptions::reserve_cus)
       .def_readwrite("overlap", &CgOptions::overlap)
       .def_readwrite("use_graph", &CgOptions::use_graph)
       MCG_FORM_PROP(graph_iters)
@@ -574,9 +575,20 @@ PYBIND11_MODULE(_C, m) {
                             as_stream(stream));
   });
   k.def("grid_for", &kern::grid_for);
-  k.def("spin", [](uintptr_t out, double us, bool fat, int blocks, uintptr_t stream) {
-    kern::spin(reinterpret_cast<double*>(out), us, fat, blocks, as_stream(stream));
+  k.def("spin", [](uintptr_t out, double us, bool fat, int blocks, uintptr_t stream, uintptr_t where) {
+    kern::spin(reinterpret_cast<double*>(out), us, fat, blocks, as_stream(stream), reinterpret_cast<int*>(where));
   }, py::arg("out"), py::arg("microseconds"), py::arg("fat"), py::arg("blocks"), py::arg("stream"),
-     "probe: workgroups spinning on the realtime clock (fat: ~270 VGPRs per wave live)");
+     py::arg("where") = 0,
+     "probe: workgroups spinning on the realtime clock (fat: ~270 VGPRs per wave live); where: __smid per block");
+  k.def("hog", [](uintptr_t out, double us, int blocks, uintptr_t stream, uintptr_t where) {
+    kern::hog(reinterpret_cast<double*>(out), us, blocks, as_stream(stream), reinterpret_cast<int*>(where));
+  }, py::arg("out"), py::arg("microseconds"), py::arg("blocks"), py::arg("stream"), py::arg("where") = 0,
+     "probe: spinning workgroups of ~120 VGPRs per wave (a stand-in for the resident pass)");
+  k.def("cu_mask_stream", [](const std::vector<uint32_t>& mask) {
+    hipStream_t st = nullptr;
+    MCG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "stream create failed");
+    return reinterpret_cast<uintptr_t>(st);
+  }, "probe: a raw stream restricted to the CUs set in mask (32 per word); free with stream_destroy");
+  k.def("stream_destroy", [](uintptr_t st) { MCG_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(st)), "stream destroy failed"); });
   k.attr("TILE_ROWS") = kTileRows;
 }
