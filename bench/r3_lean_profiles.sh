@@ -25,6 +25,7 @@ for step in "$@"; do
     dram2d) run_dram dram_16384 k_cg_carry_ar --steps 8 --warmup 2 || exit 1 ;;
     dram3d) run_dram dram_512 k_cg_carry_ar3 --problem poisson3d --grid 512 --steps 8 --warmup 2 || exit 1 ;;
     sq2d) (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY -d $O/sq_16384 -o p --output-format csv -- python3 $R/bench.py --phases 0 --steps 8 --warmup 2 > /dev/null 2> $O/sq_16384.err) && python3 $R/bench/pmc_csv.py $O/sq_16384 k_cg_carry_ar > $O/sq_16384.txt || exit 1 ;;
+    sq3d) (cd /tmp && TMPDIR=/tmp timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU -d $O/sq_512 -o p --output-format csv -- python3 $R/bench.py --phases 0 --problem poisson3d --grid 512 --steps 8 --warmup 2 > /dev/null 2> $O/sq_512.err) && python3 $R/bench/pmc_csv.py $O/sq_512 k_cg_carry_ar3 > $O/sq_512.txt || exit 1 ;;
     suite) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 1 ;;
     b4096) timeout -k 10 200 python bench.py --grid 4096 --steps 2000 --warmup 100 > $O/bench_4096.json 2>> $O/bench.err || exit 1 ;;
     b3d) timeout -k 10 200 python bench.py --problem poisson3d --grid 512 > $O/bench_512.json 2>> $O/bench.err || exit 1 ;;
