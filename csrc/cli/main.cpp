@@ -18,7 +18,7 @@
 //   --spmv-variant 0|1|2|3|4
 //   --recurrence two|single|pipelined  --pipe-rr K  --interleave auto|on|off  --window auto|on|off
 //   --carry auto|on|off (line-carry stencil pass)  --halo-mode auto|window|allgather  --pmat auto|on|off
-//   --fused-reduce auto|on|off  --watchdog SECONDS
+//   --fused-reduce auto|on|off  --watchdog SECONDS  --reserve-cus K
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
 //   --print-x auto|yes|no  --report text|json  --verify
 // Multi-GPU runs use one host thread per GPU inside this process (no MPI in
@@ -114,6 +114,7 @@ Args parse(int argc, char** argv) {
     else if (f == "--tol") a.opt.tol = std::stod(need(i));
     else if (f == "--rtol") a.opt.rtol = std::stod(need(i));
     else if (f == "--watchdog") a.opt.watchdog_seconds = std::stod(need(i));
+    else if (f == "--reserve-cus") a.opt.reserve_cus = std::stoi(need(i));
     else if (f == "--nnz-per-row") a.nnz_per_row = std::stod(need(i));
     else if (f == "--check-every") a.opt.check_every = std::stoi(need(i));
     else if (f == "--fixed-iters") a.fixed_iters = std::stoi(need(i));

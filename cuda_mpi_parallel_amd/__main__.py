@@ -25,14 +25,15 @@ CHOICES = {"--problem": ["demo", "poisson2d", "poisson3d", "randspd", "csr", "ra
            "--report": ["text", "json"], "--comm": ["dual", "single"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
 INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
         "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--checkpoint-every", "--inject-nan-at",
-        "--pipe-rr"}
+        "--pipe-rr", "--reserve-cus"}
 FLOATS = {"--density", "--nnz-per-row", "--tol", "--rtol", "--watchdog"}
 DEFAULTS = {"--problem": "demo", "--seed": 1234, "--device": "gpu", "--gpus": None, "--sim-ranks": 1,
             "--maxit": 2000, "--tol": 1e-7, "--rtol": 0.0, "--check-every": 32, "--fixed-iters": 0, "--warmup": 0,
             "--watchdog": 0.0, "--recurrence": "auto", "--interleave": "auto", "--window": "auto", "--carry": "auto",
             "--pmat": "auto", "--fused-reduce": "auto", "--halo-mode": "auto", "--blocks-per-cu": 0,
             "--spmv-variant": -1, "--checkpoint": "", "--checkpoint-every": 0, "--resume": "", "--inject-nan-at": -1,
-            "--print-x": "auto", "--report": "text", "--comm": "single", "--pipe-rr": 0}
+            "--print-x": "auto", "--report": "text", "--comm": "single", "--pipe-rr": 0,
+            "--reserve-cus": 0}
 
 
 def _parser() -> argparse.ArgumentParser:
@@ -139,7 +140,8 @@ def _run(args) -> int:
                          interleave=tri(args.interleave), window=tri(args.window), carry=tri(args.carry),
                          pmat=tri(args.pmat), fused_reduce=tri(args.fused_reduce), halo_mode=_halo(args.halo_mode),
                          rtol=args.rtol, pipe_rr=args.pipe_rr, checkpoint_every=args.checkpoint_every, checkpoint_path=args.checkpoint,
-                         inject_nan_at=args.inject_nan_at, watchdog_seconds=args.watchdog)
+                         inject_nan_at=args.inject_nan_at, watchdog_seconds=args.watchdog,
+                         reserve_cus=args.reserve_cus)
         if fixed:
             import torch.distributed as dist
 

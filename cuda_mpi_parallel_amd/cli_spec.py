@@ -53,6 +53,7 @@ FLAGS = [
     ("--force-comm", None, "RCCL collectives also with one rank"),
     ("--comm", "single", "single (default): one communicator, one stream order | dual: reduce + halo communicators (halo on a side stream)"),
     ("--blocks-per-cu", "0", "SpMV grid, blocks per CU (0 = auto)"),
+    ("--reserve-cus", "0", "CUs withheld from the compute stream (32 = one per shader engine) so collectives start beside the pass"),
     ("--spmv-variant", "-1", "CSR engine: 0 LDS tiles, 1 direct, 2 CSR-vector, 3 direct nt, 4 row-length adaptive; -1 auto"),
     # aux subsystems
     ("--checkpoint", None, "PREFIX of per-rank checkpoint files"),

@@ -54,3 +54,15 @@ def test_masked_hog_leaves_one_cu_per_engine(mcg):
     finally:
         torch.cuda.synchronize()
         K.stream_destroy(st)
+
+
+def test_cli_reserve_cus(mcg):
+    """The native CLI takes --reserve-cus (shared flag table) and solves on the masked stream."""
+    import json
+    import subprocess
+
+    p = subprocess.run([mcg.cli_path(), "--problem", "poisson2d", "--n", "128", "--format", "sellc8",
+                        "--reserve-cus", "32", "--report", "json"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    rep = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rep["converged"]
