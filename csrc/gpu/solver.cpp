@@ -61,7 +61,8 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
     // other count leaves some SE with fewer CUs for the same share of blocks
     std::vector<uint32_t> mask((ncu_ + 31) / 32, 0u);
     for (int i = 0; i < ncu_ - opt_.reserve_cus; ++i) mask[i / 32] |= 1u << (i % 32);
-    s0_ = Stream::with_cu_mask(mask);
+    s0_ = Stream::with_cu_mask(mask);  // (a blocking stream: the CU-mask create takes no flags, so it
+                                       // also orders against the legacy null stream -- ordering only)
     ncu_ -= opt_.reserve_cus;
   } else {
     s0_ = Stream(true, 0);
