@@ -309,6 +309,7 @@ def _run_rank(args, out_fd) -> int:
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
                 "comm": args.comm,
                 "launch": route,
+                **({"reserve_cus": opts.reserve_cus} if opts.reserve_cus else {}),
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
                       "comm_world": comm.count if (comm is not None and not sim and not rehearse) else 1,
