@@ -77,6 +77,8 @@ def parse_args(argv=None):
                     help="randspd: > 0 = candidate offsets over [1, spread] (wide multi-diagonal; the all-gather path)")
     ap.add_argument("--scramble", type=int, default=0,
                     help="randspd: 1 = P^T A P with a seeded random permutation P (genuinely irregular sparsity)")
+    ap.add_argument("--coef", type=int, default=0,
+                    help="poisson2d/3d: 1 = variable coefficients (seeded random conductivity field; not the headline)")
     ap.add_argument("--format", default="sellc8", choices=["csr", "sell", "sell16", "sellc8"],
                     help="sparse storage: CSR, SELL-64, SELL-64/d16 (16-bit column offsets) or SELL-64/c8 "
                          "(one-byte (value, offset) dictionary codes; default, falls back to d16)")
@@ -174,7 +176,7 @@ def _run_rank(args, out_fd) -> int:
         spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, spread=args.spread,
                                 scramble=args.scramble, rhs="random")
     else:
-        spec = mcg.make_problem(args.problem, n=args.grid, rhs="random")
+        spec = mcg.make_problem(args.problem, n=args.grid, rhs="random", coef=args.coef)
     C = mcg.native()
     # hipGraph replay of 32-iteration blocks at every N: at N > 1 the RCCL all-reduce and the halo
     # send/recv (forked onto the side stream and joined by events) are captured with the kernels,
@@ -254,7 +256,7 @@ def _run_rank(args, out_fd) -> int:
         if env.world > 1:
             dist.all_reduce(t)
         nnz = int(t.item())
-    headline = args.problem == "poisson2d" and args.grid == 16384 and not sim and not rehearse
+    headline = args.problem == "poisson2d" and args.grid == 16384 and not sim and not rehearse and not args.coef
     if phases is not None:
         extra["phase_us"] = phases
         if env.world > 1:  # slowest rank per phase
@@ -263,7 +265,8 @@ def _run_rank(args, out_fd) -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             extra["phase_us_max"] = {k: round(float(v), 2) for k, v in zip(keys, t.tolist())}
     model = (f"randspd_rows{args.rows}_band{args.band}_q{args.density}" + (f"_spread{args.spread}" if args.spread else "")
-             + ("_scrambled" if args.scramble else "") if args.problem == "randspd" else f"{args.problem}_N{args.grid}")
+             + ("_scrambled" if args.scramble else "") if args.problem == "randspd" else
+             f"{args.problem}_N{args.grid}" + ("_varcoef" if args.coef else ""))
     if env.rank == 0:
         line = json.dumps({
             "metric": METRIC if headline else (
@@ -282,7 +285,8 @@ def _run_rank(args, out_fd) -> int:
             "vs_baseline": round(value / BASELINE_IT_PER_S, 4) if headline else None,
             "dtype": "fp64",
             "data": "synthetic (on-device generated %s matrix, random RHS)" % {
-                "poisson2d": "5-pt Poisson", "poisson3d": "7-pt Poisson",
+                "poisson2d": "5-pt Poisson" + (" (variable coefficients)" if args.coef else ""),
+                "poisson3d": "7-pt Poisson" + (" (variable coefficients)" if args.coef else ""),
                 "randspd": "random SPD " + ("scrambled P^T A P (irregular)" if args.scramble else
                                             "wide multi-diagonal" if args.spread else "banded")}[args.problem],
             "config": {

@@ -36,11 +36,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=16384)
+    ap.add_argument("--problem", default="poisson2d")
     ap.add_argument("--iters", type=int, default=8, help="solver iterations queued ahead of each probe")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--doubles", type=int, default=3 * 16384, help="message size (doubles)")
     ap.add_argument("--graph", type=int, default=1, help="solver iterations as hipGraphs (1) or eager (0)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="extra CgOptions")
+    ap.add_argument("--copy-kib", type=int, action="append", default=[],
+                    help="r4: also time two side-stream hipMemcpyAsync copies of this many KiB each, with the "
+                         "copy engine (hipMemcpyDeviceToDeviceNoCU) and with the default (blit-kernel) path")
+    ap.add_argument("--kinds", default="rccl,rccl_graph,torch_add,spin_fat,spin_thin")
     a = ap.parse_args()
 
     import torch
@@ -49,7 +54,7 @@ def main() -> int:
 
     torch.cuda.set_device(0)
     C = mcg.native()
-    spec = mcg.make_problem("poisson2d", n=a.grid)
+    spec = mcg.make_problem(a.problem, n=a.grid)
     o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
     o.use_graph = bool(a.graph)
     for kv in a.set:
@@ -66,6 +71,10 @@ def main() -> int:
     dst = torch.zeros_like(src)
     side = torch.cuda.Stream(priority=-1)
     spin_out = torch.zeros(64, dtype=torch.float64, device="cuda")
+    # two ghost-sized copies (lo / hi halo) per probe: the CU-free transport candidate
+    cmax = max(a.copy_kib or [0]) * 1024
+    csrc = torch.rand(max(1, 2 * cmax // 8), dtype=torch.float64, device="cuda")
+    cdst = torch.zeros_like(csrc)
 
     # the same send/recv captured into a graph on the side stream (how the halo runs at P > 1):
     # separates a host-side wait inside the RCCL call from a device-side wait for CUs
@@ -84,6 +93,12 @@ def main() -> int:
                 comm.sendrecv_ptr(src.data_ptr(), 0, dst.data_ptr(), 0, n, side.cuda_stream)
             elif kind == "rccl_graph":
                 g.replay()
+            elif kind.startswith("copy_"):
+                _, eng, kib = kind.split("_")
+                nb = int(kib) * 1024
+                k = 1024 if eng == "nocu" else 3
+                for h in range(2):
+                    C.kernels.memcpy_async(cdst.data_ptr() + h * nb, csrc.data_ptr() + h * nb, nb, k, side.cuda_stream)
             elif kind in ("spin_fat", "spin_thin"):
                 C.kernels.spin(spin_out.data_ptr(), 20.0, kind == "spin_fat", 1, side.cuda_stream)
             else:
@@ -98,8 +113,11 @@ def main() -> int:
     s.synchronize()
     pass_ms = (time.perf_counter() - t0) * 1e3 / 16
 
-    out = {"grid": a.grid, "pass_ms": round(pass_ms, 3), "info": {k: s.info[k] for k in ("carry", "format")}}
-    for kind in ("rccl", "rccl_graph", "torch_add", "spin_fat", "spin_thin"):
+    out = {"problem": a.problem, "grid": a.grid, "pass_ms": round(pass_ms, 3), "info": {k: s.info[k] for k in ("carry", "format")}}
+    kinds = [k for k in a.kinds.split(",") if k]
+    for kib in a.copy_kib:
+        kinds += [f"copy_nocu_{kib}", f"copy_blit_{kib}"]
+    for kind in kinds:
         alone, busy = [], []
         for _ in range(a.reps):
             torch.cuda.synchronize()

@@ -25,6 +25,9 @@ OUT = os.path.join(ROOT, "gpurun_out")
 PY = sys.executable
 PYTEST = f"{PY} -u -m pytest -x -q --timeout 300 --timeout-method thread"
 PROF = "rocprofv3"
+# BASELINE config 5, genuinely irregular: a P = 8 rank's share (12.5 M rows, 8.33 G nnz, ~101 GB) of the
+# scrambled random SPD (P^T A P), alone on one GPU with collectives that move nothing
+C5SCR = "--problem randspd --rows 100000000 --band 410 --density 1.0 --scramble 1 --sim-world 8 --sim-rank 3"
 
 
 def bench(extra: str = "") -> str:
@@ -272,6 +275,28 @@ def recipes(a) -> dict:
             ("d5", 200, bench("--set carry_depth=5")),
             ("base", 200, bench()),
             ("nt3d", 200, bench("--problem poisson3d --grid 512 --set carry_nt=1")),
+        ],
+        # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
+        "vc": [
+            ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),
+            ("b16384", 300, bench("--coef 1 --steps 100 --warmup 10 --phases 0")),
+            ("b16384_generic", 300, bench("--coef 1 --steps 50 --warmup 5 --phases 0 --set carry_vc=0")),
+            ("b4096", 300, bench("--coef 1 --grid 4096 --steps 1000 --warmup 100 --phases 0")),
+        ],
+        # r4: tile pacing mechanism (counter polls vs step flags, lag) at the scrambled config-5 P = 8 share
+        "c5pace": [
+            (f"{tag}", 400, bench(f"{C5SCR} --steps 6 --warmup 2 --phases 0 --no-verify " +
+                                  " ".join(f"--set {kv}" for kv in sets)))
+            for tag, sets in (("p2", ["tile_pace=2"]), ("p4", ["tile_pace=4"]), ("p3", ["tile_pace=3"]),
+                              ("p4_s18_lag1", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_lag=1"]),
+                              ("p4_s18", ["tile_pace=4", "tile_seg_log2=18"]),
+                              ("p2_again", ["tile_pace=2"]))
+        ],
+        # r4: can a copy-engine (hipMemcpyDeviceToDeviceNoCU) halo run beside the resident pass?
+        "copyprobe": [
+            ("p2d", 240, f"{PY} bench/corun_probe.py --reps 4 --kinds rccl,spin_thin --copy-kib 128 --copy-kib 2048"),
+            ("p3d", 240, f"{PY} bench/corun_probe.py --reps 4 --problem poisson3d --grid 512 --kinds rccl "
+                         f"--copy-kib 2048"),
         ],
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 20 --world 1 2 4 8 --phases 10"),

@@ -9,6 +9,7 @@
 // Flags (all additive):
 //   --problem demo|poisson2d|poisson3d|randspd|csr   --n N   --rows R --band W --density q --spread S
 //   --scramble 0|1 (random-spd: P^T A P, a seeded random symmetric permutation)
+//   --coef 0|1 (poisson2d/3d: 1 = variable coefficients from a seeded random conductivity field)
 //   --matrix FILE.mtx (a user matrix, problem csr)  --rhs-file FILE (its b: Matrix Market array / one per line)
 //   --rhs reference|random|ones  --seed S  --gpus P  --device gpu|cpu  --sim-ranks P (cpu)
 //   --maxit M  --tol T  --rtol R (||r|| < R ||b||)  --check-every K  --fixed-iters K  --warmup W
@@ -97,6 +98,7 @@ Args parse(int argc, char** argv) {
     else if (f == "--density") a.spec.density = std::stod(need(i));
     else if (f == "--spread") a.spec.spread = std::stoll(need(i));
     else if (f == "--scramble") a.spec.scramble = std::stoi(need(i));
+    else if (f == "--coef") a.spec.coef = std::stoi(need(i));
     else if (f == "--matrix") a.matrix = need(i);
     else if (f == "--rhs-file") a.rhs_file = need(i);
     else if (f == "--halo-mode") {

@@ -46,6 +46,9 @@ namespace {
 #define MCG_EDGE_BRANCHLESS 1
 #endif
 
+// waves per SIMD the diav lean-only kernels are built for (their coefficient chains need the VGPRs)
+constexpr int kLeanV = 3;
+
 __device__ __forceinline__ double ld_once(const double* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
 
 // a slice's codes for one lane: c4 nibbles / c8 bytes packed into 32-bit registers (entry u at
@@ -55,6 +58,14 @@ struct ArCodes {
   static constexpr int CB = CM >= 3 ? 4 : 8;
   uint32_t pk[(U * CB + 31) / 32];
   int w;
+};
+
+// SELL-64/diav (variable coefficients): the row's five coefficients in column order (north, west,
+// diagonal, east, south), loaded per line instead of decoded
+template <int U>
+struct ArCodes<5, U> {
+  double k[5];
+  int w = 5;
 };
 
 // codes of slice row `lane` from its first slot `base` (slots, multiple of 64) and width w
@@ -176,7 +187,7 @@ template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
-  __shared__ double2 s_dict[CM == 4 ? 1 : 256];
+  __shared__ double2 s_dict[CM >= 4 ? 1 : 256];
   __shared__ double s_val[16];  // dia4 values
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   if (st->done || sc.conv) {
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   }
   if constexpr (CM == 4) {
     if (threadIdx.x < 16) s_val[threadIdx.x] = S.dvals[threadIdx.x];
-  } else {
+  } else if constexpr (CM != 5) {
     for (int q = threadIdx.x; q < S.ndict; q += kBS) s_dict[q] = S.dict[q];
   }
   __syncthreads();
@@ -250,26 +261,33 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     const double upv = lane == 63 ? edge : sh_up;
     const double dnv = lane == 0 ? edge : sh_dn;
     double sum = 0.0;
-    if constexpr (CM == 4) {  // slot u = the u-th canonical offset: ascending columns, no selects
+    if constexpr (CM == 5) {  // the row's own coefficients, canonical column order
+      const double g[5] = {dnl, dnv, mid, upv, upl};
+#pragma unroll
+      for (int u = 0; u < 5; ++u) sum = fma(c.k[u], g[u], sum);
+      return sum;
+    }
+    else if constexpr (CM == 4) {  // slot u = the u-th canonical offset: ascending columns, no selects
       const double g[5] = {dnl, dnv, mid, upv, upl};
 #pragma unroll
       for (int u = 0; u < 5; ++u) sum = fma(s_val[(c.pk[0] >> (4 * u)) & 15u], g[u], sum);
       return sum;
-    }
+    } else {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      double val;
-      const int32_t off = ar_entry<CM, U>(s_dict, c, u, val);
-      double t = off == LO ? upl : dnl;
-      asm volatile("" : "+v"(t));
-      t = off == -1 ? dnv : t;
-      asm volatile("" : "+v"(t));
-      t = off == 1 ? upv : t;
-      asm volatile("" : "+v"(t));
-      const double g = off == 0 ? mid : t;
-      sum = (u < c.w) ? fma(val, g, sum) : sum;
+      for (int u = 0; u < U; ++u) {
+        double val;
+        const int32_t off = ar_entry<CM, U>(s_dict, c, u, val);
+        double t = off == LO ? upl : dnl;
+        asm volatile("" : "+v"(t));
+        t = off == -1 ? dnv : t;
+        asm volatile("" : "+v"(t));
+        t = off == 1 ? upv : t;
+        asm volatile("" : "+v"(t));
+        const double g = off == 0 ? mid : t;
+        sum = (u < c.w) ? fma(val, g, sum) : sum;
+      }
+      return sum;
     }
-    return sum;
   };
   for (int64_t job = gw; job < SS * runs; job += nw) {
     const int64_t col = job % SS, l0 = (job / SS) * chunk;
@@ -481,6 +499,198 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         continue;
       }
     }
+    if constexpr (CM == 5 && P3 && LEAN > 0) {
+      // Lean run with variable coefficients (SELL-64/diav): the CM == 4 lean loop above with the
+      // five values of a line streamed instead of held in scalar registers.  Per line the row's own
+      // d, e, s and the east value of the row before the slice (lane 0's west coefficient) are
+      // loaded LD lines ahead with the operands; the west column is e shifted one lane (DPP), the
+      // north column the previous line's s (carried).  Every run of >= 3 lines qualifies (the setup
+      // checks the launch's runs); same sums in the same fma order as step() with CM == 5.
+      constexpr int LD = QD + 1;
+      struct VSet {
+        double v[5];
+      };
+      struct CRaw {
+        double d, e, s, ee;
+      };
+      const bool z0 = col == 0, z63 = col == SS - 1;  // slices at a grid line's start / end
+      const bool hi = lane == 63, edge_lane = lane == 0 || lane == 63;
+      const uint32_t l8 = (uint32_t)lane << 3;
+      const uint32_t LOB = (uint32_t)LO << 3;
+      const uint32_t SB = (uint32_t)(2 * SS) << 3;
+      const uint32_t ob0 = (uint32_t)e0 << 3;
+      const uint32_t xb0 = (uint32_t)i0 << 3;
+      const uint32_t kb0 = xb0 + LOB;  // the coefficient arrays: one line in front
+      const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;
+      const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
+      const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
+      const int32_t jlo = -(e0 / LO), jhi = (ext32 - 64 - e0) / LO;
+      const int32_t rlo = -(int32_t)l0, rhi = (int32_t)(nl - 1 - l0);
+      auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
+      auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
+      auto kc = [&](int32_t j) { return j < rlo - 1 ? rlo - 1 : (j > rhi ? rhi : j); };
+      auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
+      auto raw_at = [&](int32_t j) {
+        Raw q;
+        const uint32_t o = line_ofs(jc(j)) + l8;
+        q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
+        q.p = g_ld(po, o);
+        return q;
+      };
+      auto edge_at = [&](int32_t j) {
+        Edge q;
+        const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
+        q.r = g_ld(reo, c);
+        q.a = g_ld(eo, c);
+        q.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
+        return q;
+      };
+      auto coef_ofs = [&](int32_t j) { return kb0 + (uint32_t)j * LOB; };
+      // o >= one line inside the loop; the prologue's front line may start at offset 0 (its ee is
+      // never used there)
+      auto coef_ld = [&](uint32_t o) {
+        CRaw c;
+        c.d = g_ld(S.cvd, o + l8);
+        c.e = g_ld(S.cve, o + l8);
+        c.s = g_ld(S.cvs, o + l8);
+        c.ee = g_ld(S.cve, o >= 8u ? o - 8u : o);
+        return c;
+      };
+      auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), q.p); };
+      auto is_ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
+      auto raw_un = [&](int32_t j) {
+        Raw q;
+        const uint32_t o = line_ofs(j) + l8;
+        q.r = g_ld(j < n_run ? (const double*)pn : ro, o);
+        q.p = g_ld(po, o);
+        return q;
+      };
+      auto edge_un = [&](int32_t j) {
+        Edge q;
+        const uint32_t c = cb0 + (uint32_t)j * SB + oc;
+        q.r = g_ld(reo, c);
+        q.a = g_ld(eo, c);
+        q.p = g_ld(po, line_ofs(j) - 8u + op);
+        return q;
+      };
+      auto x_at = [&](int32_t j) {
+        if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+        else return 0.0;
+      };
+      auto mkv = [&](const CRaw& c, double s_up) {
+        VSet V;
+        V.v[0] = s_up;
+        V.v[1] = lane_dn_or(c.e, c.ee);
+        V.v[2] = c.d;
+        V.v[3] = c.e;
+        V.v[4] = c.s;
+        return V;
+      };
+      auto stencil_v = [&](const VSet& V, double mid, double edge, double dnl, double upl) {
+        const double upv = lane_up_or(mid, edge);
+        const double dnv = lane_dn_or(mid, edge);
+        double sum = fma(V.v[0], dnl, 0.0);
+        sum = fma(V.v[1], dnv, sum);
+        sum = fma(V.v[2], mid, sum);
+        sum = fma(V.v[3], upv, sum);
+        return fma(V.v[4], upl, sum);
+      };
+      auto epk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };
+      const Raw rm2 = raw_at(-2), rm1 = raw_at(-1), r0 = raw_at(0);
+      Raw q[LD - 1];
+#pragma unroll
+      for (int d = 0; d < LD - 1; ++d) q[d] = raw_at(1 + d);
+      const Edge edm1 = edge_at(-1), ed0 = edge_at(0);
+      Edge e[LD - 1];
+#pragma unroll
+      for (int d = 0; d < LD - 1; ++d) e[d] = edge_at(1 + d);
+      double xs[LD - 1];
+#pragma unroll
+      for (int d = 0; d < LD - 1; ++d) xs[d] = x_at(d);
+      const CRaw cm2 = coef_ld(coef_ofs(kc(-2))), cm1 = coef_ld(coef_ofs(kc(-1))), c0 = coef_ld(coef_ofs(0));
+      CRaw cq[LD - 1];  // coefficients of lines m + 1 .. m + LD - 1
+#pragma unroll
+      for (int d = 0; d < LD - 1; ++d) cq[d] = coef_ld(coef_ofs(kc(1 + d)));
+      double pr_pk = 0.0;
+      if (l0 >= 1) {
+        pr_pk = fma(b, rm1.p, fma(na, stencil_v(mkv(cm1, cm2.s), rm1.p, edm1.p, rm2.p, r0.p), rm1.r));
+      } else if (is_ghost(-1)) {
+        pr_pk = fma(b, rm1.p, fma(na, g_ld(apx_o, line_ofs(-1) + l8), rghost(-1, rm1)));
+      }
+      VSet Vs = mkv(c0, cm1.s);  // line m
+      double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
+      o_rk = fma(na, stencil_v(Vs, r0.p, ed0.p, rm1.p, q[0].p), fma(nbp, r0.r, r0.p));
+      o_pk = fma(b, r0.p, o_rk);
+      double o_epk = epk(ed0);
+      auto lstep = [&](auto clc, int32_t m, int next) __attribute__((always_inline)) {
+        constexpr bool CL = decltype(clc)::value;
+        const Raw qn = CL ? raw_at(m + LD) : raw_un(m + LD);
+        const Edge en2 = CL ? edge_at(m + LD) : edge_un(m + LD);
+        const double xn = x_at(m + LD - 1);
+        const CRaw cn = coef_ld(coef_ofs(CL ? kc(m + LD) : m + LD));
+        const VSet Vt = mkv(cq[0], Vs.v[4]);  // line m + 1
+        double rk1 = 0.0, pk1 = 0.0;
+        if (next == 1) {
+          const double t = stencil_v(Vt, q[0].p, e[0].p, o_pold, q[1].p);
+          rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
+          pk1 = fma(b, q[0].p, rk1);
+        } else if (CL && next == 2) {
+          rk1 = fma(na, g_ld(apx_o, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
+          pk1 = fma(b, q[0].p, rk1);
+        }
+        const double sum = stencil_v(Vs, o_pk, o_epk, pr_pk, pk1);
+        const uint32_t ob = line_ofs(m);
+        const double rr = fma(-b, o_pold, o_pk);
+        if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+        if (edge_lane) {
+          const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);
+          g_st(ren, sb, rr);
+          g_st(en, sb, sum);
+        }
+        if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+        g_st_nt(pn, ob + l8, o_pk);
+        if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apx_n, ob + l8, sum);
+        s_pap = fma(o_pk, sum, s_pap);
+        s_rap = fma(o_rk, sum, s_rap);
+        s_apap = fma(sum, sum, s_apap);
+        s_rr = fma(o_rk, o_rk, s_rr);
+        pr_pk = o_pk;
+        o_pk = pk1;
+        o_rk = rk1;
+        o_pold = q[0].p;
+        o_pm2 = q[0].r;
+        o_epk = epk(e[0]);
+        Vs = Vt;
+#pragma unroll
+        for (int d = 0; d + 1 < LD - 1; ++d) {
+          q[d] = q[d + 1];
+          e[d] = e[d + 1];
+          xs[d] = xs[d + 1];
+          cq[d] = cq[d + 1];
+        }
+        q[LD - 2] = qn;
+        e[LD - 2] = en2;
+        xs[LD - 2] = xn;
+        cq[LD - 2] = cn;
+      };
+      const std::true_type clamped;
+      const std::false_type unclamped;
+      const int32_t m_lo = l0 == 0 ? 1 : 0;  // the rank's first line stores its Ap_k (clamped step)
+      const int32_t m_hi = min(n_run - 1, (int32_t)(nl - 1 - LD - l0));
+      int32_t m = 0;
+      if (m_lo == 1) lstep(clamped, 0, 1);
+      m = m_lo;
+      for (; m + LD - 1 <= m_hi; m += LD) {
+#pragma unroll
+        for (int u = 0; u < LD; ++u) lstep(unclamped, m + u, 1);
+      }
+      for (; m <= m_hi; ++m) lstep(unclamped, m, 1);
+      for (; m < n_run; ++m) {
+        const bool lastl = l0 + m == nl - 1;
+        lstep(clamped, m, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
+      }
+      continue;
+    }
     if constexpr (LEAN == 0) {
     // lines j (relative to l0) inside the ext vectors: [jmin, jmax]; loads clamp to them (values
     // of lines that do not exist are never multiplied: the matrix has no entry for them)
@@ -538,11 +748,18 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     };
     // dia4: the "metadata" is the slice index (fixed 160 B per slice, nothing to load)
     auto load_meta = [&](int32_t j) {
-      if constexpr (CM == 4) return (uint32_t)(oline(j) * SS + col);
+      if constexpr (CM >= 4) return (uint32_t)(oline(j) * SS + col);
       else return meta[oline(j) * SS + col + vz];
     };
     auto load_codes = [&](uint32_t mt, ArCodes<CM, U>& c) {
-      if constexpr (CM == 4) ar_load_dia<U>(S.dia4 + (int64_t)mt * 160, lane, c);
+      if constexpr (CM == 5) {  // diav: own d, e, s; north = s one line up, west = e of the row before
+        const int64_t f = (int64_t)mt * 64 + LO;
+        c.k[0] = S.cvs[f - LO + lane];
+        c.k[2] = S.cvd[f + lane];
+        c.k[3] = S.cve[f + lane];
+        c.k[4] = S.cvs[f + lane];
+        c.k[1] = lane_dn_or(c.k[3], S.cve[f - 1]);
+      } else if constexpr (CM == 4) ar_load_dia<U>(S.dia4 + (int64_t)mt * 160, lane, c);
       else ar_load_codes<CM, U>(S, (int64_t)(mt & 0x0fffffffu) << 6, (int)(mt >> 28), lane, c);
     };
     auto edge_p = [&](const Edge& q) { return q.p; };
@@ -1258,7 +1475,18 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
     const int64_t e = own + i;
     ArCodes<CM, U> c;
     double t = 0.0;
-    if constexpr (CM == 4) {  // absent entries: value 0 times a clamped (finite) operand
+    if constexpr (CM == 5) {  // diav: west / north from the partners' east / south (symmetric)
+      const int64_t f = i + lo;
+      const double kk[5] = {S.cvs[f - lo], S.cve[f - 1], S.cvd[f], S.cve[f], S.cvs[f]};
+      const int64_t o5[5] = {-(int64_t)lo, -1, 0, 1, (int64_t)lo};
+#pragma unroll
+      for (int u = 0; u < 5; ++u) {
+        int64_t q = e + o5[u];
+        q = q < 0 ? 0 : (q >= v.ext_len ? v.ext_len - 1 : q);
+        t = fma(kk[u], v.p_old[q], t);
+      }
+      (void)c;
+    } else if constexpr (CM == 4) {  // absent entries: value 0 times a clamped (finite) operand
       ar_load_dia<U>(S.dia4 + (i >> 6) * (32 * U), (int)(i & 63), c);
       const int64_t o5[5] = {-(int64_t)lo, -1, 0, 1, (int64_t)lo};
       const int64_t o7[7] = {-(int64_t)lo, -(int64_t)ln, -1, 0, 1, (int64_t)ln, (int64_t)lo};
@@ -1331,6 +1559,55 @@ __global__ __launch_bounds__(256) void k_sell_to_dia4(SellDev S, int nd, DiaOffs
 __global__ void k_dia_vals(const double2* __restrict__ dict, int nv, int nd, double* __restrict__ dvals) {
   const int a = threadIdx.x;
   if (a < 16) dvals[a] = a < nv ? dict[a * nd].x : 0.0;
+}
+
+// SELL-64 -> /diav, one thread per local row.  CHECK = 0: the row's entries in slot order must sit at
+// offsets -line, -1, 0, +1, +line, strictly increasing (else `bad`); d, e, s stored (absent: +0.0), a
+// first-line row's north value into the front line of cvs.  CHECK = 1 (after the fill): the west /
+// north values must equal the partners' east / south (the kernels take them from there).
+// CM: 0 int32 ext columns, 1 d16 offsets, 2 c8 codes
+template <int CM, bool CHECK>
+__global__ __launch_bounds__(256) void k_sell_to_diav(SellDev S, int64_t line, double* __restrict__ cvd,
+                                                      double* __restrict__ cve, double* __restrict__ cvs,
+                                                      unsigned* __restrict__ bad) {
+  const int64_t n = S.n_rows;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sl = i >> 6, lane = i & 63;
+    const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
+    const int64_t rowcol = S.own_off + i;
+    double v5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    int prev = -1;
+    for (int64_t j = 0; j < w; ++j) {
+      const int64_t k = base + 64 * j + lane;
+      int64_t off;
+      double val;
+      if constexpr (CM == 2) {
+        const double2 q = S.dict[S.codes[k]];
+        val = q.x;
+        off = (int64_t)__double_as_longlong(q.y);
+      } else {
+        val = S.vals[k];
+        off = (CM == 1 ? rowcol + (int64_t)S.dcols[k] : (int64_t)S.cols[k]) - rowcol;
+      }
+      if (val == 0.0) continue;  // SELL padding (and explicit zeros: they add nothing)
+      const int cls = off == -line ? 0 : (off == -1 ? 1 : (off == 0 ? 2 : (off == 1 ? 3 : (off == line ? 4 : -1))));
+      if (cls <= prev) {
+        atomicOr(bad, 1u);
+        return;
+      }
+      prev = cls;
+      v5[cls] = val;
+    }
+    if constexpr (!CHECK) {
+      cvd[line + i] = v5[2];
+      cve[line + i] = v5[3];
+      cvs[line + i] = v5[4];
+      if (i < line) cvs[i] = v5[0];
+    } else {
+      // a row at a grid line's start has no west entry, and the row before it (a line's end) no east one
+      if (!(v5[1] == cve[line + i - 1]) || (i >= line && !(v5[0] == cvs[i]))) atomicOr(bad, 2u);
+    }
+  }
 }
 
 // SellDev::dpat, pass 1: a slice's pattern word -- bit 31 and the slot indices (4 bits per slot,
@@ -1469,6 +1746,35 @@ int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64
   return (int64_t)h;
 }
 
+bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream) {
+  const int64_t n = S.n_rows;
+  MCG_CHECK(cv != nullptr && line >= 64 && line % 64 == 0 && n % line == 0, "diav: whole 64-row grid lines");
+  if (line > INT32_MAX / 2) return false;
+  MCG_HIP(hipMemsetAsync(cv, 0, (size_t)3 * (n + line) * sizeof(double), stream), "device memset failed(diav)");
+  unsigned* bad = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&bad), sizeof(unsigned), stream), "device malloc failed(diav)");
+  MCG_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), stream), "device memset failed");
+  double *cd = cv, *ce = cv + (n + line), *cs = cv + 2 * (n + line);
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 8192);
+#define MCG_DV(CM)                                                                                             \
+  do {                                                                                                         \
+    hipLaunchKernelGGL((k_sell_to_diav<CM, false>), dim3(g), dim3(256), 0, stream, S, line, cd, ce, cs, bad); \
+    hipLaunchKernelGGL((k_sell_to_diav<CM, true>), dim3(g), dim3(256), 0, stream, S, line, cd, ce, cs, bad);  \
+  } while (0)
+  if (n > 0) {
+    if (S.codes != nullptr) MCG_DV(2);
+    else if (S.dcols != nullptr) MCG_DV(1);
+    else MCG_DV(0);
+  }
+#undef MCG_DV
+  MCG_HIP(hipGetLastError(), "kernel launch failed(diav)");
+  unsigned h = 0;
+  MCG_HIP(hipMemcpyAsync(&h, bad, sizeof(unsigned), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(diav)");
+  (void)hipFreeAsync(bad, stream);
+  return h == 0;
+}
+
 void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipStream_t stream) {
   if (n_slices <= 0) return;
   hipLaunchKernelGGL(k_slice_meta, dim3(grid_for(n_slices, 256, 4)), dim3(256), 0, stream, slice_ptr, n_slices, meta);
@@ -1522,16 +1828,18 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
-  MCG_CHECK((cm == 2 || cm == 4) && param >= 4 && param <= 5 && S.dict != nullptr,
-            "Ap-recomputing carry: SELL-64/c8, /c4 or /dia4 rows of at most 5 entries");
+  MCG_CHECK((cm == 2 || cm == 4 || cm == 5) && param >= 4 && param <= 5 && (cm == 5 || S.dict != nullptr),
+            "Ap-recomputing carry: SELL-64/c8, /c4, /dia4 or /diav rows of at most 5 entries");
   MCG_CHECK(cm != 4 || (S.dia4 != nullptr && S.dvals != nullptr), "Ap-recomputing carry: dia4 codes missing");
-  MCG_CHECK(final_mode || cm == 4 || S.smeta != nullptr, "Ap-recomputing carry: slice metadata missing");
+  MCG_CHECK(cm != 5 || (S.cvd != nullptr && S.cve != nullptr && S.cvs != nullptr),
+            "Ap-recomputing carry: diav coefficients missing");
+  MCG_CHECK(final_mode || cm >= 4 || S.smeta != nullptr, "Ap-recomputing carry: slice metadata missing");
   MCG_CHECK(v.ape_old != nullptr && v.ape_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
             "Ap-recomputing carry: vectors missing");
   MCG_CHECK((v.ap_old == nullptr) == (v.ap_new == nullptr), "Ap-recomputing carry: boundary Ap buffers");
   MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
             "in-kernel reduction: bad control block");
-  MCG_CHECK(!p3 || cm == 4, "three-term carry: SELL-64/dia4 only");
+  MCG_CHECK(!p3 || cm >= 4, "three-term carry: SELL-64/dia4 or /diav only");
   const bool p3k = p3 && !first;  // pass 0: the two-term kernel (r_{-1} = b stored in full)
   if (final_mode) {
     const int64_t n = tr.nt0 * 64;
@@ -1539,6 +1847,7 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   hipLaunchKernelGGL((k_ar_final<CM, U>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, n, \
                      (int32_t)(tr.strip * 64), 0, partials, pstride, st, tol, first, check, k, p3)
     if (cm == 4) MCG_AF(4, 5);
+    else if (cm == 5) MCG_AF(5, 5);
     else { if (param == 4) MCG_AF(2, 4); else MCG_AF(2, 5); }
 #undef MCG_AF
     MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
@@ -1555,13 +1864,23 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
     return;
   }
+  if (cm == 5 && p3k && lean) {  // diav lean-only kernels: the streamed coefficients need more VGPRs
+#define MCG_LV(QD, PAIR) \
+  hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
+                     tr, partials, pstride, st, tol, first, check, rc)
+    if (depth >= 3) { if (pair) MCG_LV(3, true); else MCG_LV(3, false); }
+    else { if (pair) MCG_LV(2, true); else MCG_LV(2, false); }
+#undef MCG_LV
+    MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+    return;
+  }
   const int qd = depth <= 2 ? 2 : 3;  // operand prefetch depth in lines (solver: 2 or 3)
 #define MCG_A(CM, U, QD, PAIR, P3, ...)                                                                 \
   hipLaunchKernelGGL((k_cg_carry_ar<CM, U, QD, PAIR, P3, ##__VA_ARGS__>), dim3(grid), dim3(kBS), 0, stream, S, v, \
                      own_off, tr, partials, pstride, st, tol, first, check, rc)
 #define MCG_AP(CM, U, QD)                                        \
   do {                                                           \
-    if constexpr (CM == 4) {                                     \
+    if constexpr (CM >= 4) {                                     \
       if (p3k) {                                                 \
         if (pair) MCG_A(CM, U, QD, true, true);                  \
         else if (unroll > 1) MCG_A(CM, U, QD, false, true, 3);   \
@@ -1578,6 +1897,7 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     else MCG_AP(CM, U, 3);                    \
   } while (0)
   if (cm == 4) MCG_AQ(4, 5);
+  else if (cm == 5) MCG_AQ(5, 5);
   else { if (param == 4) MCG_AQ(2, 4); else MCG_AQ(2, 5); }
 #undef MCG_AQ
 #undef MCG_AP

@@ -46,20 +46,42 @@ constexpr uint32_t kColMask = (1u << 22) - 1;
 
 // `live` (LDS, per workgroup): cleared after the first wait that times out -- the group is not
 // co-resident (another kernel holds CUs, or several ranks share the GPU), so this workgroup stops
-// waiting for the rest of the launch instead of paying the cap at every segment
-__device__ __forceinline__ void pace_step(unsigned* pace, int step, int* live, int slack8) {
+// waiting for the rest of the launch instead of paying the cap at every segment.
+//
+// Two ways to wait (TilesDev::pace_flag).  Counter polls: every waiter polls the group's arrival
+// counter.  Its line lives at the memory side (an atomic drops it from the L2), so ~128 pollers per
+// group keep one word busy and the arrivals queue behind the polls.  Step flags: the arrival whose
+// add completes step s (the counter's return value says so: the counter passes every integer once)
+// raises the group's step flag to s + 1 in 8 replicas on lines of their own; the waiters poll one
+// replica each with `sc1` loads, which the XCD's L2 serves until the flag changes.
+__device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live) {
   __syncthreads();
-  if (threadIdx.x == 0 && pace != nullptr && *live) {
+  if (threadIdx.x == 0 && T.pace != nullptr && *live) {
     const int grp = blockIdx.x & 7;
     const unsigned nwg = (gridDim.x - grp + 7) >> 3;
-    unsigned* c = pace + grp * 64;  // one 256-B block per group
-    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every workgroup of the group has finished segment `step` (slack8 > 0: all but slack8 / 8 of them)
-    const unsigned target = (unsigned)(step + 1) * nwg - (unsigned)((nwg * (unsigned)slack8) >> 3);
+    const unsigned slack = (nwg * (unsigned)T.pace_slack8) >> 3;
+    unsigned* c = T.pace + grp * 64;  // one 256-B block per group
+    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // wait until the group finished segment step - lag (slack > 0: all but slack of its workgroups)
+    const int need = step + 1 - T.pace_lag;
     int spin = 0;
-    for (; spin < kPaceSpins; ++spin) {
-      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      __builtin_amdgcn_s_sleep(8);
+    if (T.pace_flag) {
+      unsigned* f = T.pace + kTilePaceCnt + grp * 8 * 64;
+      const unsigned done = old + 1 + slack;
+      if (done % nwg == 0)
+        for (int r = 0; r < 8; ++r) __hip_atomic_fetch_max(f + r * 64, done / nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned* fr = f + ((blockIdx.x >> 3) & 7) * 64;
+      if (need > 0)
+        for (; spin < kPaceSpins; ++spin) {
+          if (__hip_atomic_load(fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)need) break;
+          __builtin_amdgcn_s_sleep(8);
+        }
+    } else if (need > 0) {
+      const unsigned target = (unsigned)need * nwg - slack;
+      for (; spin < kPaceSpins; ++spin) {
+        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
     }
     if (spin == kPaceSpins) *live = 0;
   }
@@ -138,7 +160,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
           tile_batch_load(T, hi + lane, hi_next, q, v);
         }
       }
-      pace_step(T.pace, step, &live, T.pace_slack8);
+      pace_step(T, step, &live);
       lo = hi;
       hi = hi_next;
     }
@@ -225,18 +247,14 @@ TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
   return t;
 }
 
-int tiles_grid() {
-  static int cached = -1;
-  if (cached < 0) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_tiles<0>), 256, 0) !=
-            hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    (void)hipGetLastError();
-    cached = std::min(per_cu, 4) * num_cus();  // every workgroup resident (pacing waits on them)
-  }
-  return cached;
+int tiles_grid(int ncu) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_tiles<0>), 256, 0) !=
+          hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  (void)hipGetLastError();
+  return std::min(per_cu, 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
 }
 
 namespace {

@@ -56,7 +56,7 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
   h.kind = (int32_t)spec_.kind;
   h.rhs = (int32_t)spec_.rhs;
   h.nnz_local = info_.nnz_local;
-  h.fingerprint = fingerprint_;
+  h.fingerprint = fingerprint();
   bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
   std::vector<char> host;
   auto dump = [&](const void* dev, size_t bytes) {
@@ -87,7 +87,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
        h.pass_form == ((ar_ ? 1 : 0) | (p3_ ? 2 : 0)) &&
        h.n_local == L_.n_local() && h.ext_len == L_.ext_len && h.row_begin == L_.row_begin &&
        h.n_global == L_.n_global && h.seed == spec_.seed && h.kind == (int32_t)spec_.kind &&
-       h.rhs == (int32_t)spec_.rhs && h.nnz_local == info_.nnz_local && h.fingerprint == fingerprint_;
+       h.rhs == (int32_t)spec_.rhs && h.nnz_local == info_.nnz_local && h.fingerprint == fingerprint();
   if (!ok) {
     std::fclose(f);
     fail("checkpoint does not match this problem/layout", path);

@@ -115,7 +115,6 @@ void GpuCgSolver::setup() {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   const int64_t n = L_.n_local();
-  fingerprint_ = problem_fingerprint(spec_);
   info_.n_global = L_.n_global;
   info_.n_local = n;
   info_.ext_len = L_.ext_len;
@@ -437,7 +436,7 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (tiles_) {  // one launch over every row block: the resident workgroups (the pacing waits on each)
-    g_all_ = n > 0 ? kern::tiles_grid() : 0;
+    g_all_ = n > 0 ? kern::tiles_grid(ncu_) : 0;
     if (opt_.blocks_per_cu > 0) g_all_ = std::min(g_all_, ncu_ * opt_.blocks_per_cu);  // fewer waves: more rounds
     g_int_ = 0;
     g_bnd_ = g_all_;
@@ -492,6 +491,23 @@ void GpuCgSolver::setup() {
             (carry_lo2_ == 0 || (off != carry_lo2_ && off != -carry_lo2_)))
           carry_general_ = true;
       if (carry_general_) carry_lo2_ = 0;
+      // variable-coefficient 2-D 5-point stencil (no c8 dictionary: > 256 (value, offset) pairs):
+      // SELL-64/diav, the per-row values streamed by the Ap-recomputing line carry
+      if (!c8_ && carry_lo2_ == 0 && stencil_plane(spec_) == 0 && stencil_line(spec_) == gl &&
+          info_.max_row_len <= 5 && opt_.form.carry_vc != 0 && opt_.form.ap_recompute != 0 && !split_ && n > 0 &&
+          (n + gl) < ((int64_t)1 << 29)) {
+        cv_len_ = n + gl;
+        cv_.allocate(3 * cv_len_, "A", 64);
+        if (kern::sell_to_diav(sell_view(), gl, cv_.get(), s0_)) {
+          diav_ = true;
+          carry_general_ = false;
+        } else {
+          cv_.release();
+          cv_len_ = 0;
+        }
+      }
+      MCG_CHECK(opt_.form.carry_vc != 1 || diav_,
+                "carry_vc: needs a symmetric 2-D 5-point stencil without a c8 dictionary, ap_recompute on");
       // auto: only the specialised pass (2-D stencils); with the slow path (3-D's +-N gathers) it
       // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log)
       if (opt_.form.carry == 1 || !carry_general_) carry_all_ = apply(tr_all_, g_all_);
@@ -501,7 +517,7 @@ void GpuCgSolver::setup() {
     // Ap recomputed instead of stored: the specialised 2-D pass over every owned line in one launch
     // (with a split launch the boundary rows' generic pass would need the stored Ap); 3-D: the plane
     // carry with +-N through LDS, on SELL-64/dia4 only
-    const bool ar_any = opt_.form.ap_recompute != 0 && carry_all_ && !carry_general_ && c8_ && !split_ &&
+    const bool ar_any = opt_.form.ap_recompute != 0 && carry_all_ && !carry_general_ && (c8_ || diav_) && !split_ &&
                         tr_all_.b0 == 0 && tr_all_.strip > 0;
     const int kw = opt_.form.carry3_kw;
     const bool ar2 = ar_any && carry_lo2_ == 0 && info_.spmv_param <= 5;
@@ -510,7 +526,7 @@ void GpuCgSolver::setup() {
                      (int64_t)carry_lo2_ * carry_lo2_ == gl;
     MCG_CHECK(opt_.form.carry_dia != 1 || ar2 || ar3,
               "carry_dia needs the Ap-recomputing line / plane carry (ap_recompute)");
-    if ((ar2 || ar3) && opt_.form.carry_dia != 0 && n > 0) {  // SELL-64/dia4 from the c8 codes (replaces c4 + metadata)
+    if ((ar2 || ar3) && opt_.form.carry_dia != 0 && n > 0 && c8_) {  // SELL-64/dia4 from the c8 codes (replaces c4 + metadata)
       const int64_t ns = (n + 63) / 64;
       const int nslot = ar3 ? 7 : 5;
       dia4_.allocate(ns * 32 * nslot, "A", 256);
@@ -536,6 +552,8 @@ void GpuCgSolver::setup() {
       dia4_.release();
       dvals_.release();
       dpat_.release();
+      cv_.release();
+      diav_ = false;
       info_.dia_uniform = 0.0;
     }
     MCG_CHECK(opt_.form.ap_recompute != 1 || ar_,
@@ -559,7 +577,8 @@ void GpuCgSolver::setup() {
   // stores r on its first / last line in either form, so ranks need not agree on it)
   // auto: on for the 2-D line carry and the 3-D plane carry (whose three-term kernel spills a few
   // registers at 16-wave blocks and is still 15 % faster: profiles/r2s6_p3_16384.md)
-  p3_ = ar_ && info_.dia4 && opt_.form.p3 != 0;
+  info_.diav = diav_;
+  p3_ = ar_ && (info_.dia4 || diav_) && opt_.form.p3 != 0;
   // every rank takes the same form: it decides how many vectors the halo carries ({Ap, p} or {r, Ap, p})
   if (use_comm_ && world_ > 1 && !all_ranks_agree_(p3_)) p3_ = false;
   MCG_CHECK(opt_.form.p3 != 1 || p3_, "p3 needs the Ap-recomputing line / plane carry on SELL-64/dia4");
@@ -591,8 +610,31 @@ void GpuCgSolver::setup() {
       g_all_ = g;
     }
   }
+  if (p3_ && diav_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
+    // diav: every run of >= 3 lines streams its coefficients in the lean loop (the same grids as the
+    // dia4 2-D passes); checked here on the host from the launch's job decomposition
+    const int64_t ss = tr_all_.strip, nlines = (n + 63) / 64 / ss;
+    int g = g_all_;
+    for (int bpc : {16, 8, 4}) {
+      const int64_t waves = (int64_t)ncu_ * bpc * 4;
+      if (nlines / std::max<int64_t>(1, waves / ss) >= 64) {
+        g = ncu_ * bpc;
+        break;
+      }
+    }
+    const int64_t nw = (int64_t)g * 4, runs = nw > ss ? nw / ss : 1, chunk = (nlines + runs - 1) / runs;
+    bool all = nlines >= 4 && L_.ext_len < ((int64_t)1 << 29);
+    for (int64_t r = 0; r < runs && all; ++r) {
+      const int64_t l0 = r * chunk, l1 = std::min(nlines, l0 + chunk);
+      if (l0 < nlines && l1 - l0 < 3) all = false;
+    }
+    if (all) {
+      lean_only_ = true;
+      g_all_ = g;
+    }
+  }
   info_.lean_only = lean_only_;
-  if (ar_ && !info_.dia4 && n > 0) {
+  if (ar_ && !info_.dia4 && !diav_ && n > 0) {
     const int64_t ns = (n + 63) / 64;
     int64_t slots = 0;
     MCG_HIP(hipMemcpy(&slots, slice_ptr_.get() + ns, sizeof(int64_t), hipMemcpyDeviceToHost),
@@ -653,10 +695,10 @@ void GpuCgSolver::setup() {
   } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
     // dia4 codes; the three-term pass streams none over its lean runs (uniform slices)
     const double streamed = info_.dia4 ? (double)dia4_.bytes() * (p3_ ? 1.0 - info_.dia_uniform : 1.0)
-                                       : (double)matrix_bytes;
+                                       : (diav_ ? 24.0 * n : (double)matrix_bytes);
     // three-term form: p_{k-1}, p_{k-2} read, p_k written 24 B; x rw every second pass 8; edge r + Ap 0.5
     info_.bytes_per_iter_model = streamed + (p3_ ? 32.5 : 44.25) * n;
-    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + smeta_.bytes();
+    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + smeta_.bytes() + cv_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   }
   // vectors allocated with room for the placement probe's start offsets hold that headroom too
@@ -672,7 +714,9 @@ void GpuCgSolver::setup() {
 // and a dependency across queues costs 5-11 us here (rocprofv3 kernel trace, profiles/
 // r3_pipelined_cg.md), so the longer branch stays on the launch queue.  Both are timed once (3
 // launches after a warm-up; the all-reduce is collective, so every rank times it at this point of
-// setup).  The order changes scheduling only, never the arithmetic: ranks may decide differently.
+// setup, on a scratch buffer).  The order changes scheduling only, never the arithmetic, but every
+// rank takes the same one (one all-reduce of the flag), so the halo and reduce communicators' kernels
+// are enqueued in the same order everywhere.
 void GpuCgSolver::pick_pipe_order_() {
   pipe_ar_first_ = false;
   if (!(use_comm_ && opt_.overlap && !comm_->serialized())) return;
@@ -688,8 +732,11 @@ void GpuCgSolver::pick_pipe_order_() {
     return 1e3 * ms / 3.0;
   };
   const double t_s = time_us([&] { spmv_plain_(w_.get(), q_.get(), s0_); });
-  const double t_ar = time_us([&] { comm_->allreduce_sum(st_.get()->red, 4, s0_); });
-  pipe_ar_first_ = t_ar > t_s;
+  DeviceBuffer<double> scratch(4, "state");
+  MCG_HIP(hipMemsetAsync(scratch.get(), 0, scratch.bytes(), s0_), "device memset failed");
+  const double t_ar = time_us([&] { comm_->allreduce_sum(scratch.get(), 4, s0_); });
+  MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
+  pipe_ar_first_ = all_ranks_agree_(t_ar > t_s);
   info_.pipe_ar_first = pipe_ar_first_;
   info_.pipe_spmv_us = t_s;
   info_.pipe_allreduce_us = t_ar;

@@ -9,8 +9,8 @@ namespace mcg {
 std::string problem_name(const ProblemSpec& s) {
   switch (s.kind) {
     case ProblemKind::Demo: return "demo";
-    case ProblemKind::Poisson2D: return "poisson2d";
-    case ProblemKind::Poisson3D: return "poisson3d";
+    case ProblemKind::Poisson2D: return s.coef ? "poisson2d-varcoef" : "poisson2d";
+    case ProblemKind::Poisson3D: return s.coef ? "poisson3d-varcoef" : "poisson3d";
     case ProblemKind::RandomSPD: return s.scramble ? "randspd-scrambled" : "randspd";
     case ProblemKind::Csr: return "csr";
   }
@@ -54,6 +54,7 @@ uint64_t problem_fingerprint(const ProblemSpec& s) {
   f.add_d(s.density);
   f.add((uint64_t)s.spread);
   f.add((uint64_t)s.scramble);
+  if (s.coef) f.add(0xC0EF0000ull + (uint64_t)s.coef);  // (absent for coef 0: older checkpoints stay valid)
   return f.h;
 }
 

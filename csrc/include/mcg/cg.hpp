@@ -57,7 +57,9 @@ struct PassForm {
                              // share of the scrambled config 5: 17 / 18 / 19 / 20 / 21 -> 8.5 / 12.2 / 14.0 / 11.2
                              // / 8.5 it/s, profiles/r3_config5_scrambled.md)
   int tile_pace = 2;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
-                             // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest)
+                             // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest);
+                             // 3 / 4 = as 1 / 2, the waiters polling a step flag instead of the arrival counter
+  int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
@@ -74,6 +76,9 @@ struct PassForm {
                              // slices' edge rows and the runs' outer lines (24 instead of 32 B/row for r and p,
                              // and the paired x update needs no extra p read); rounding differs from the
                              // two-term form (not bitwise); -1 = auto (on with dia4), 0 = off, 1 = required
+  int carry_vc = -1;         // variable-coefficient 2-D 5-point stencils (no c8 dictionary): the Ap-recomputing line
+                             // carry on SELL-64/diav, streaming each row's d, e, s (a symmetric matrix's west / north
+                             // values are its partners' east / south); -1 = auto, 0 = off (generic d16 pass), 1 = required
   int dia_uniform = -1;      // dia4 carry: slices whose 64 rows share one value-index pattern take a lean loop with the
                              // values in scalar registers and no codes streamed (the 2-D three-term pass over runs
                              // of such lines; bitwise the same sums); -1 = auto (on), 0 = off

@@ -114,6 +114,15 @@ struct SellDev {
   // whose slices carry that same uniform pattern.  The line carry streams no codes over such runs
   // (the values sit in scalar registers); nullptr = every slice through the codes.
   const uint64_t* dpat = nullptr;
+  // SELL-64/diav (variable-coefficient 2-D 5-point stencils, sell_to_diav): the row's own values in
+  // three arrays of local rows shifted by one grid line (index line + i): cvd = a_ii, cve = a_{i,i+1},
+  // cvs = a_{i,i+line}; the extra line in front holds zeros and, in cvs, the rank's line 0 north
+  // coefficients (a_{i,i-line} of its first line).  A symmetric matrix's other two coefficients of
+  // row i are its partners': west a_{i,i-1} = cve[i - 1], north a_{i,i-line} = cvs[i - line] (checked
+  // bitwise at setup).  24 B per row streamed instead of one shared value table.
+  const double* cvd = nullptr;
+  const double* cve = nullptr;
+  const double* cvs = nullptr;
   // SELL-64/aligned (long rows whose slices share their column offsets, e.g. the wide random-SPD
   // family): entry j of EVERY lane of slice s is the row's own column + soffs[slice_ptr[s] / 64 + j]
   // (one wave-uniform offset per slot, clamped to [0, ext_len); absent entries hold 0.0), so a
@@ -275,6 +284,11 @@ void slice_meta(const int64_t* slice_ptr, int64_t n_slices, uint32_t* meta, hipS
 // (-line, -ln, -1, 0, +1, +ln, +line), 224 B per slice
 bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* dia4, double* dvals,
                   hipStream_t stream);
+// SELL-64 (d16 / int32 columns / c8) of a 2-D 5-point stencil (line = grid line, every local row
+// in whole lines) -> SELL-64/diav: cv = 3 * (n + line) doubles (cvd | cve | cvs, SellDev).  False
+// when an entry sits at another offset, a row's offsets are not strictly increasing, or the matrix
+// is not bitwise symmetric inside the rank (west / north entries = their partners' east / south).
+bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream);
 // SellDev::dpat from a dia4 copy (and its value table) of ns = ss * lines slices (ss slices per line,
 // nslot 5 or 7); returns the number of uniform slices (synchronises the stream)
 int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64_t ss, int nslot, uint64_t* dpat,
@@ -291,7 +305,8 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
 // three-term passes launch their lean-only kernels (`lean`).  Synchronises the stream.
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
                             int32_t ln, hipStream_t stream);
-// cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals).  p3 (dia4): three-term form --
+// cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals), 5 SELL-64/diav (S.cvd / cve / cvs,
+// variable coefficients; lean runs stream them: every run of >= 3 lines).  p3 (dia4): three-term form --
 // r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p buffers, r stored only at the slices' edge rows
 // and the runs' first / last lines (v.r_old / r_new hold just those rows; pass 0 reads r_{-1} = b)
 void cg_carry_ar(int cm,int param, int depth, const SellDev& S, const F1Vectors& v, int64_t own_off,
@@ -339,7 +354,8 @@ void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, 
 // the gathers of p hit the L2.
 constexpr int kTileB = 1024;
 constexpr int kTileMaxSegments = 8192;  // LDS counters of the build kernels (32 KiB)
-constexpr int kTilePaceWords = 8 * 64;  // pacing counters: 8 groups, 256 B apart
+constexpr int kTilePaceCnt = 8 * 64;     // pacing arrival counters: 8 groups, 256 B apart
+constexpr int kTilePaceWords = kTilePaceCnt + 8 * 8 * 64;  // + per group 8 replicas of its step flag, 256 B apart
 struct TilesGeometry {
   int64_t nblocks = 0;
   int G = 0;
@@ -353,9 +369,12 @@ struct TilesDev {
   int G = 0, seg_shift = 18;
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
   int pace_slack8 = 0;       // a workgroup waits for all but pace_slack8 / 8 of its group (0: all)
+  int pace_flag = 0;         // 1: the arrival that completes a step publishes it in a step flag and the waiters
+                             // poll the flag (an L2-resident line) instead of the hot arrival counter
+  int pace_lag = 0;          // a workgroup may start segment s + pace_lag before its group finished segment s
 };
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
-int tiles_grid();  // workgroups of the SpMV: the resident count (pacing waits on every workgroup)
+int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
 // count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0) then fill
 void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
                      const int64_t* rp64, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,

@@ -12,6 +12,12 @@
 //              nnz = 5N^2 - 4N  (BASELINE.json configs 1-3).
 //   poisson3d  7-point Dirichlet Laplacian on an N^3 grid (6 / -1),
 //              nnz = 7N^3 - 6N^2 (BASELINE.json config 4).
+//              coef = 1 (both): heterogeneous diffusion -div(c grad u) with a seeded random
+//              conductivity field: cell i has c_i in [0.1, 10) (0.1 + 9.9 u^3), the face between
+//              neighbours i < j has k = 2 c_i c_j / (c_i + c_j) (harmonic mean) and a_ij = a_ji = -k, a
+//              boundary face (Dirichlet) has k = c_i, and a_ii = the sum of the cell's face k's, so
+//              the matrix is symmetric and diagonally dominant (strictly on the boundary rows): SPD,
+//              with (almost) every off-diagonal value distinct.  coef = 0: every k = 1 (4 / -1, 6 / -1).
 //   randspd    symmetric, strictly diagonally dominant (hence SPD) banded matrix
 //              with irregular row lengths: pair {a<b}, 0<b-a<=W, is present iff a
 //              counter-based hash of the pair passes a density that varies per
@@ -80,6 +86,7 @@ struct ProblemSpec {
   RhsKind rhs = RhsKind::Reference;
   int64_t spread = 0;      // randspd: > 0 = wide candidate offsets over [1, spread] (see above)
   int scramble = 0;        // randspd: 1 = P^T A P with a seeded random permutation P (irregular)
+  int coef = 0;            // poisson2d/3d: 0 = constant coefficients, 1 = random conductivity field
   const CsrMatrix* csr = nullptr;  // kind Csr: the matrix (host)
 };
 
@@ -188,6 +195,25 @@ MCG_HD inline int64_t stencil_plane(const ProblemSpec& s) {
   }
 }
 
+// poisson2d/3d coefficients (coef = 1): cell conductivity, and the conductivity of the face between
+// cells a < b (or a boundary face of cell a: b = -1).  Only correctly rounded operations, written so
+// that no compiler can contract them differently on the host and the device: every rank, the CPU
+// path and the host CSR see the same bits, and k(a, b) is computed from the ordered pair, so a_ij
+// and a_ji are the same double.
+MCG_HD inline double cell_cond(const ProblemSpec& s, int64_t i) {
+  const double u = u01(mix64((s.seed * 0x3C6EF372FE94F82Bull) ^ mix64((uint64_t)i + 0xC0EFull)));
+  const double u3 = (u * u) * u;
+  return fma(9.9, u3, 0.1);
+}
+MCG_HD inline double face_cond(const ProblemSpec& s, int64_t a, int64_t b) {
+  if (s.coef == 0) return 1.0;
+  const double ca = cell_cond(s, a);
+  if (b < 0) return ca;
+  const double cb = cell_cond(s, b);
+  const double num = (2.0 * ca) * cb;
+  return num / (ca + cb);
+}
+
 // randspd pair presence / weight.  a < b required.
 MCG_HD inline double randspd_density(const ProblemSpec& s, int64_t a) {
   // per-1024-row region density factor in [0.25, 1.75] -> irregular row lengths
@@ -256,23 +282,52 @@ MCG_HD inline void for_each_entry(const ProblemSpec& s, int64_t i, F&& f, int64_
     }
     case ProblemKind::Poisson2D: {
       const int64_t N = s.N, ix = i % N, iy = i / N;
-      if (iy > 0) f(i - N, -1.0);
-      if (ix > 0) f(i - 1, -1.0);
-      f(i, 4.0);
-      if (ix < N - 1) f(i + 1, -1.0);
-      if (iy < N - 1) f(i + N, -1.0);
+      if (s.coef == 0) {
+        if (iy > 0) f(i - N, -1.0);
+        if (ix > 0) f(i - 1, -1.0);
+        f(i, 4.0);
+        if (ix < N - 1) f(i + 1, -1.0);
+        if (iy < N - 1) f(i + N, -1.0);
+        return;
+      }
+      // faces in column order (north, west, east, south); a missing neighbour is a boundary face
+      const double kn = face_cond(s, iy > 0 ? i - N : i, iy > 0 ? i : -1);
+      const double kw = face_cond(s, ix > 0 ? i - 1 : i, ix > 0 ? i : -1);
+      const double ke = face_cond(s, i, ix < N - 1 ? i + 1 : -1);
+      const double ks = face_cond(s, i, iy < N - 1 ? i + N : -1);
+      if (iy > 0) f(i - N, -kn);
+      if (ix > 0) f(i - 1, -kw);
+      f(i, ((kn + kw) + ke) + ks);
+      if (ix < N - 1) f(i + 1, -ke);
+      if (iy < N - 1) f(i + N, -ks);
       return;
     }
     case ProblemKind::Poisson3D: {
       const int64_t N = s.N, N2 = N * N;
       const int64_t ix = i % N, iy = (i / N) % N, iz = i / N2;
-      if (iz > 0) f(i - N2, -1.0);
-      if (iy > 0) f(i - N, -1.0);
-      if (ix > 0) f(i - 1, -1.0);
-      f(i, 6.0);
-      if (ix < N - 1) f(i + 1, -1.0);
-      if (iy < N - 1) f(i + N, -1.0);
-      if (iz < N - 1) f(i + N2, -1.0);
+      if (s.coef == 0) {
+        if (iz > 0) f(i - N2, -1.0);
+        if (iy > 0) f(i - N, -1.0);
+        if (ix > 0) f(i - 1, -1.0);
+        f(i, 6.0);
+        if (ix < N - 1) f(i + 1, -1.0);
+        if (iy < N - 1) f(i + N, -1.0);
+        if (iz < N - 1) f(i + N2, -1.0);
+        return;
+      }
+      const double kb = face_cond(s, iz > 0 ? i - N2 : i, iz > 0 ? i : -1);
+      const double kn = face_cond(s, iy > 0 ? i - N : i, iy > 0 ? i : -1);
+      const double kw = face_cond(s, ix > 0 ? i - 1 : i, ix > 0 ? i : -1);
+      const double ke = face_cond(s, i, ix < N - 1 ? i + 1 : -1);
+      const double ks = face_cond(s, i, iy < N - 1 ? i + N : -1);
+      const double kt = face_cond(s, i, iz < N - 1 ? i + N2 : -1);
+      if (iz > 0) f(i - N2, -kb);
+      if (iy > 0) f(i - N, -kn);
+      if (ix > 0) f(i - 1, -kw);
+      f(i, ((((kb + kn) + kw) + ke) + ks) + kt);
+      if (ix < N - 1) f(i + 1, -ke);
+      if (iy < N - 1) f(i + N, -ks);
+      if (iz < N - 1) f(i + N2, -kt);
       return;
     }
     case ProblemKind::RandomSPD: {

@@ -68,6 +68,7 @@ struct SolverInfo {
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
+  bool diav = false;     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
   double dia_uniform = 0.0;  // dia4 slices whose 64 rows share one value pattern (no codes streamed; PassForm::dia_uniform)
   bool lean_only = false;    // every run of the three-term carry takes the lean step (lean-only kernels)
@@ -173,6 +174,9 @@ class GpuCgSolver {
   DeviceBuffer<uint8_t> codes_;  // SELL-64/c8 dictionary codes
   DeviceBuffer<double2> dict_;
   DeviceBuffer<uint8_t> dia4_;    // SELL-64/dia4 copy (Ap-recomputing carry; 160 B per slice)
+  DeviceBuffer<double> cv_;       // SELL-64/diav: cvd | cve | cvs, (n + line) doubles each (kernels.hpp SellDev)
+  int64_t cv_len_ = 0;
+  bool diav_ = false;
   DeviceBuffer<double> dvals_;    // ... its value table (16 doubles)
   DeviceBuffer<uint64_t> dpat_;   // ... its uniform-slice patterns and run lengths (SellDev::dpat)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
@@ -199,7 +203,9 @@ class GpuCgSolver {
     t.G = tgeo_.G;
     t.seg_shift = tgeo_.seg_shift;
     t.pace = opt_.form.tile_pace > 0 ? tpace_.get() : nullptr;
-    t.pace_slack8 = opt_.form.tile_pace == 2 ? 1 : 0;
+    t.pace_slack8 = (opt_.form.tile_pace == 2 || opt_.form.tile_pace == 4) ? 1 : 0;
+    t.pace_flag = opt_.form.tile_pace >= 3 ? 1 : 0;
+    t.pace_lag = std::max(0, opt_.form.tile_pace_lag);
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
@@ -224,6 +230,11 @@ class GpuCgSolver {
     s.dia4 = dia4_.get();
     s.dvals = dvals_.get();
     s.dpat = dpat_.get();
+    if (cv_.get() != nullptr) {
+      s.cvd = cv_.get();
+      s.cve = cv_.get() + cv_len_;
+      s.cvs = cv_.get() + 2 * cv_len_;
+    }
     return s;
   }
   // vectors
@@ -253,7 +264,15 @@ class GpuCgSolver {
   hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
   void drop_graphs_();
   double setup_seconds_ = 0.0;
-  uint64_t fingerprint_ = 0;  // problem_fingerprint(spec_), recorded in checkpoints
+  uint64_t fingerprint_ = 0;  // problem_fingerprint(spec_), recorded in checkpoints (computed on first use:
+  bool fingerprint_done_ = false;  // O(nnz) on the host for a user matrix, so never at setup)
+  uint64_t fingerprint() {
+    if (!fingerprint_done_) {
+      fingerprint_ = problem_fingerprint(spec_);
+      fingerprint_done_ = true;
+    }
+    return fingerprint_;
+  }
 };
 
 }  // namespace mcg

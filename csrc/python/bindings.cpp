@@ -27,7 +27,7 @@ using namespace mcg;
 namespace {
 
 ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64_t band, double density,
-                      uint64_t seed, const std::string& rhs, int64_t spread, int scramble) {
+                      uint64_t seed, const std::string& rhs, int64_t spread, int scramble, int coef) {
   ProblemSpec s;
   s.kind = parse_problem_kind(problem);
   s.N = n;
@@ -39,6 +39,9 @@ ProblemSpec make_spec(const std::string& problem, int64_t n, int64_t rows, int64
   s.spread = spread;
   s.scramble = scramble;
   MCG_CHECK(scramble == 0 || s.kind == ProblemKind::RandomSPD, "scramble: random-SPD family only");
+  s.coef = coef;
+  MCG_CHECK(coef == 0 || ((coef == 1) && (s.kind == ProblemKind::Poisson2D || s.kind == ProblemKind::Poisson3D)),
+            "coef: 0 (constant) or 1 (random conductivity field), Poisson families only");
   if (s.kind == ProblemKind::Demo) s.N = 3;
   return s;
 }
@@ -128,7 +131,7 @@ PYBIND11_MODULE(_C, m) {
   py::class_<ProblemSpec>(m, "ProblemSpec")
       .def(py::init(&make_spec), py::arg("problem") = "demo", py::arg("n") = 3, py::arg("rows") = 0,
            py::arg("band") = 0, py::arg("density") = 0.5, py::arg("seed") = 1234, py::arg("rhs") = "reference",
-           py::arg("spread") = 0, py::arg("scramble") = 0)
+           py::arg("spread") = 0, py::arg("scramble") = 0, py::arg("coef") = 0)
       .def_property_readonly("name", [](const ProblemSpec& s) { return problem_name(s); })
       .def_property_readonly("n_rows", [](const ProblemSpec& s) { return global_rows(s); })
       .def_property_readonly("bandwidth", [](const ProblemSpec& s) { return bandwidth(s); })
@@ -140,6 +143,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("seed", &ProblemSpec::seed)
       .def_readonly("spread", &ProblemSpec::spread)
       .def_readonly("scramble", &ProblemSpec::scramble)
+      .def_readonly("coef", &ProblemSpec::coef)
       .def("perm", [](const ProblemSpec& s, int64_t i, bool inverse) {
         MCG_CHECK(scrambled(s) && i >= 0 && i < s.rows, "perm: scrambled random SPD, 0 <= i < rows");
         return inverse ? scramble_inv(s, i) : scramble_fwd(s, i);
@@ -212,6 +216,8 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(tiles)
       MCG_FORM_PROP(tile_seg_log2)
       MCG_FORM_PROP(tile_pace)
+      MCG_FORM_PROP(carry_vc)
+      MCG_FORM_PROP(tile_pace_lag)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       MCG_FORM_PROP(pmat)
@@ -428,6 +434,7 @@ PYBIND11_MODULE(_C, m) {
         d["graph_fallbacks"] = i.graph_fallbacks;
         d["xcd_map"] = i.xcd_map;
         d["dia4"] = i.dia4;
+        d["diav"] = i.diav;
         d["p3"] = i.p3;
         d["dia_uniform"] = i.dia_uniform;
         d["lean_only"] = i.lean_only;
@@ -589,6 +596,11 @@ PYBIND11_MODULE(_C, m) {
     MCG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "stream create failed");
     return reinterpret_cast<uintptr_t>(st);
   }, "probe: a raw stream restricted to the CUs set in mask (32 per word); free with stream_destroy");
+  k.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t bytes, int kind, uintptr_t stream) {
+    MCG_HIP(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes,
+                           static_cast<hipMemcpyKind>(kind), as_stream(stream)), "memcpy async failed");
+  }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("kind"), py::arg("stream"),
+     "probe: hipMemcpyAsync of kind (3 = device to device, 1024 = device to device without compute units)");
   k.def("stream_destroy", [](uintptr_t st) { MCG_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(st)), "stream destroy failed"); });
   k.attr("TILE_ROWS") = kTileRows;
 }

@@ -23,7 +23,7 @@ CHOICES = {"--problem": ["demo", "poisson2d", "poisson3d", "randspd", "csr", "ra
            "--rhs": ["reference", "random", "ones"], "--device": ["gpu", "cpu"],
            "--format": ["csr", "sell", "sell16", "sellc8"], "--print-x": ["auto", "yes", "no"],
            "--report": ["text", "json"], "--comm": ["dual", "single"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
-INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
+INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--coef", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
         "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--checkpoint-every", "--inject-nan-at",
         "--pipe-rr", "--reserve-cus"}
 FLOATS = {"--density", "--nnz-per-row", "--tol", "--rtol", "--watchdog"}
@@ -70,6 +70,8 @@ def _spec(args):
     problem = {"random-spd": "randspd", "random": "randspd"}.get(args.problem, args.problem)
     if problem in ("poisson2d", "poisson3d") and args.n is not None:
         kw["n"] = args.n
+    if problem in ("poisson2d", "poisson3d") and args.coef:
+        kw["coef"] = args.coef
     if problem == "randspd":
         for k in ("rows", "band", "density", "spread", "scramble"):
             v = getattr(args, k)

@@ -22,6 +22,7 @@ FLAGS = [
     ("--nnz-per-row", "5", "randspd: mean nonzeros per row (sets --density)"),
     ("--spread", "0", "randspd: > 0 = candidate offsets drawn over [1, spread] (wide multi-diagonal)"),
     ("--scramble", "0", "randspd: 1 = P^T A P with a seeded random permutation (genuinely irregular rows)"),
+    ("--coef", "0", "poisson2d/3d: 1 = variable coefficients (seeded random conductivity field)"),
     ("--matrix", None, "FILE.mtx: a user matrix (problem csr), Matrix Market coordinate"),
     ("--rhs-file", None, "FILE: right-hand side of --matrix (Matrix Market array or one value per line)"),
     ("--rhs", "reference", "reference | random | ones"),

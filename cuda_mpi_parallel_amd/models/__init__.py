@@ -11,6 +11,8 @@ name           matrix                                       reference / config
 ``demo``       the reference's 3x3 indefinite system        CUDACG.cu:74-117,136-141
 ``poisson2d``  5-pt Dirichlet Laplacian, n = N^2            BASELINE.json configs 1-3
 ``poisson3d``  7-pt Dirichlet Laplacian, n = N^3            BASELINE.json config 4
+               (both: ``coef=1`` = heterogeneous diffusion,  CUDACG.cu:93-117 (arbitrary
+               a seeded random conductivity field)           stencil values)
 ``randspd``    banded / wide (spread) multi-diagonal, or    BASELINE.json config 5
                scrambled (P^T A P, irregular); strictly
                diagonally dominant
@@ -43,10 +45,11 @@ class ProblemSpec:
     rhs: str = "reference"  # reference | random | ones
     spread: int = 0       # randspd: > 0 = the band candidate offsets drawn over [1, spread] ("wide")
     scramble: int = 0     # randspd: 1 = P^T A P with a seeded random permutation P (genuinely irregular)
+    coef: int = 0         # poisson2d/3d: 1 = variable coefficients (random conductivity field, symmetric)
 
     def native(self):
         return native().ProblemSpec(self.problem, self.n, self.rows, self.band, self.density, self.seed, self.rhs,
-                                    self.spread, self.scramble)
+                                    self.spread, self.scramble, self.coef)
 
     @property
     def n_rows(self) -> int:

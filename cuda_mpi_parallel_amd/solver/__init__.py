@@ -37,12 +37,22 @@ def _opts(maxit=2000, tol=1e-7, **kw):
 
 
 class CGSolver:
-    """Distributed GPU CG for one rank (one process per GPU, or a single GPU)."""
+    """Distributed GPU CG for one rank (one process per GPU, or a single GPU).
+
+    ``format="auto"`` (default) picks what both CLIs pick: the reference's CSR and two-reduction
+    order for the built-in demo, SELL-64/c8 (falling back to /dia4, /diav, /d16, tiles as the matrix
+    allows) with the auto recurrence (single-reduction pass) for every other problem, so
+    ``solve("poisson2d")`` runs the Ap-recomputing line carry."""
 
     def __init__(self, spec: ProblemSpec, maxit: int = 2000, tol: float = 1e-7, check_every: int = 32,
-                 overlap: bool = True, use_graph: bool = True, format: str = "csr", force_comm: bool = False,
+                 overlap: bool = True, use_graph: bool = True, format: str = "auto", force_comm: bool = False,
                  blocks_per_cu: int = 0, env: Optional[_dist.DistEnv] = None, comm=None, comm_mode: str = "single",
                  **tuning):
+        if format == "auto":
+            demo = getattr(spec, "problem", "") == "demo"
+            format = "csr" if demo else "sellc8"
+            if not demo:
+                tuning.setdefault("recurrence", -1)
         self.spec = spec
         self.env = env or _dist.dist_env()
         _dist.set_device(self.env)
@@ -106,7 +116,7 @@ class CGSolver:
 def solve(problem: str = "demo", device: str = "gpu", sim_ranks: int = 1, maxit: int = 2000, tol: float = 1e-7,
           **kw) -> Dict:
     """One-call solve.  ``solve()`` with no arguments is the reference's demo."""
-    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs", "spread", "scramble",
+    spec_kw = {k: kw.pop(k) for k in ("n", "rows", "band", "density", "seed", "rhs", "spread", "scramble", "coef",
                                       "nnz_per_row", "matrix", "b", "reorder") if k in kw}
     if "matrix" in spec_kw:  # solve(matrix=A_or_path, b=...): a user matrix (kind csr)
         problem = "csr"

@@ -147,10 +147,22 @@ def test_fixed_iterations_counter(mcg):
 def test_maxit_exhaustion_matches_cpu(mcg):
     spec = mcg.make_problem("poisson2d", n=200)
     cpu = mcg.native().cpu_cg(spec.native(), mcg.native().CgOptions(maxit=50, tol=1e-7))
-    out = mcg.CGSolver(spec, maxit=50).solve()
+    out = mcg.CGSolver(spec, maxit=50, format="csr", recurrence=0).solve()
     assert out["iterations"] == 50 and not out["converged"]
     np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-9, atol=1e-12)
     assert abs(out["rnorm"] - cpu["rnorm"]) <= 1e-8 * cpu["rnorm"]
+
+
+def test_library_default_is_the_cli_fast_path(mcg):
+    """CGSolver / solve() pick what the CLIs pick: the lean three-term line carry
+    for a generated 2-D stencil, the reference's CSR two-reduction order for the demo."""
+    s = mcg.CGSolver(mcg.make_problem("poisson2d", n=1024))
+    i = s.info
+    assert i["carry"] and i["ap_recompute"] and i["dia4"] and i["p3"] and i["lean_only"], i
+    out = mcg.solve("poisson2d", n=1024, tol=1e-6)
+    assert out["converged"]
+    d = mcg.CGSolver(mcg.make_problem("demo"))
+    assert d.info["recurrence"] == "two-reduction"
 
 
 def test_force_comm_single_rank(mcg):

@@ -1,0 +1,132 @@
+"""Variable-coefficient stencils on the line carry (SELL-64/diav).
+
+The reference's SpMV takes arbitrary values (CUDACG.cu:93-117, :288).  A 5-point operator whose
+values differ row to row (heterogeneous diffusion: ``poisson2d --coef 1``) has no small value
+table, so it cannot take the dia4 / c8 carries; SELL-64/diav streams each row's d, e, s through
+the same Ap-recomputing three-term line carry (west / north values from the symmetric partners).
+These tests pin it against the CPU oracle (op for op CUDACG.cu:269-352), the generic d16 pass, its
+own generic step, graph replays and multi-rank runs.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _vc(mcg, n=256, **kw):
+    return mcg.make_problem("poisson2d", n=n, coef=1, rhs="random", **kw)
+
+
+def test_varcoef_takes_the_diav_lean_carry(mcg):
+    s = mcg.CGSolver(_vc(mcg, 1024), format="sellc8", recurrence=-1, tol=1e-6)
+    i = s.info
+    assert i["diav"] and not i["dia4"], i
+    assert i["carry"] and i["ap_recompute"] and i["p3"] and i["lean_only"], i
+    assert i["recurrence"] == "single-reduction" and i["fused_reduce"], i
+
+
+def test_varcoef_matches_cpu_oracle(mcg):
+    spec = _vc(mcg, 256)
+    C = mcg.native()
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=4000, tol=1e-8))
+    s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, tol=1e-8, maxit=4000)
+    assert s.info["diav"] and s.info["lean_only"]
+    out = s.solve()
+    assert out["converged"] and cpu["converged"]
+    assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 200)
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-7 * np.abs(cpu["x"]).max())
+    assert s.true_residual_norm() < 1e-6
+
+
+def test_varcoef_fixed_iterations_match_generic_d16_pass(mcg):
+    """40 fixed iterations: diav carry vs the generic single-reduction pass on d16 (carry_vc = 0)."""
+    spec = _vc(mcg, 384)
+    res = []
+    for vc in (-1, 0):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=40, carry_vc=vc)
+        assert s.info["diav"] == (vc != 0)
+        out = s.solve()
+        res.append((out["rnorm"], out["x_local"], s.true_residual_norm()))
+    (ra, xa, ta), (rb, xb, tb) = res
+    assert abs(ra - rb) <= 1e-10 * rb
+    np.testing.assert_allclose(xa, xb, rtol=1e-10, atol=1e-12 * np.abs(xb).max())
+    assert abs(ta - ra) <= 1e-8 * ta  # the recurrence tracks ||b - A x||
+
+
+def test_varcoef_lean_equals_generic_step_bitwise(mcg):
+    """The diav lean loop computes what step() computes, in the same fma order."""
+    spec = _vc(mcg, 512)
+    outs = []
+    for du in (-1, 0):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=37, dia_uniform=du)
+        assert s.info["diav"] and s.info["lean_only"] == (du != 0)
+        outs.append(s.solve())
+    assert outs[0]["rnorm"] == outs[1]["rnorm"]
+    np.testing.assert_array_equal(outs[0]["x_local"], outs[1]["x_local"])
+
+
+def test_varcoef_two_term_form_close(mcg):
+    """p3 = 0: the two-term diav carry (r stored in full), same iterates up to rounding."""
+    spec = _vc(mcg, 256)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=60).solve()
+    s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=60, p3=0)
+    assert s.info["diav"] and not s.info["p3"]
+    b = s.solve()
+    assert abs(a["rnorm"] - b["rnorm"]) <= 1e-9 * b["rnorm"]
+    np.testing.assert_allclose(a["x_local"], b["x_local"], rtol=1e-9, atol=1e-12 * np.abs(b["x_local"]).max())
+
+
+def test_varcoef_bitwise_repeatable_and_graph_equals_eager(mcg):
+    spec = _vc(mcg, 320)
+    outs = [mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=1e-7, use_graph=g).solve()
+            for g in (True, True, False)]
+    for o in outs[1:]:
+        assert o["iterations"] == outs[0]["iterations"] and o["rnorm"] == outs[0]["rnorm"]
+        np.testing.assert_array_equal(o["x_local"], outs[0]["x_local"])
+
+
+def test_varcoef_2000_iterations_track_cpu_oracle(mcg):
+    """BASELINE config 1's size with variable coefficients: residual every 500th iteration within
+    1e-9 of the CPU oracle over the reference's maxit (CUDACG.cu:244)."""
+    spec = _vc(mcg, 1024)
+    C = mcg.native()
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=-1.0))
+    hist = np.asarray(cpu["rnorm_history"])
+    worst = 0.0
+    for m in (500, 1000, 1500, 2000):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, tol=-1.0, maxit=m)
+        assert s.info["diav"] and s.info["lean_only"]
+        out = s.solve()
+        rel = abs(out["rnorm"] - hist[m - 1]) / hist[m - 1]
+        worst = max(worst, rel)
+        assert rel <= 1e-9, (m, out["rnorm"], hist[m - 1])
+    np.testing.assert_allclose(s.x_local(), cpu["x"], rtol=1e-9, atol=1e-9 * np.abs(cpu["x"]).max())
+    print(f"varcoef: worst residual-history gap {worst:.3e}")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_varcoef_local_ranks_agree_with_single_rank(mcg, world):
+    """P ranks (LocalComm) on the diav carry: ghost lines' north coefficients from the rank's own rows."""
+    spec = _vc(mcg, 512)
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8)
+    one = C.run_local_ranks(spec.native(), o, 1, 40, True)
+    many = C.run_local_ranks(spec.native(), o, world, 40, True)
+    assert all(r["ap_recompute"] for r in many["ranks"])
+    r1, rp = one["ranks"][0]["rnorm"], many["ranks"][0]["rnorm"]
+    assert abs(r1 - rp) <= 1e-12 * r1
+    np.testing.assert_allclose(many["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
+
+
+def test_varcoef_user_matrix_takes_diav(mcg):
+    """The same operator given as a SciPy CSR (the reference's input form) takes the diav carry and
+    solves bit for bit like the generated problem."""
+    spec = _vc(mcg, 256)
+    u = mcg.csr_problem(mcg.models.to_scipy(spec), rhs="random")
+    assert u.matrix.stencil_line == 256 and u.matrix.stencil_plane == 0
+    su = mcg.CGSolver(u, format="sellc8", recurrence=1, tol=1e-8)
+    sg = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=1e-8)
+    assert su.info["diav"] and sg.info["diav"]
+    ou, og = su.solve(), sg.solve()
+    assert ou["iterations"] == og["iterations"]
+    np.testing.assert_array_equal(ou["x_local"], og["x_local"])
