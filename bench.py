@@ -103,6 +103,10 @@ def parse_args(argv=None):
                          "communicators in flight at once)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
+    ap.add_argument("--delay-comm", default="",
+                    help="with --sim-world: AR_US,HALO_US -- every all-reduce / halo (or all-gather) exchange of the "
+                         "rehearsed rank costs a device-side delay of that many microseconds (DelayComm) instead "
+                         "of nothing (NullComm): the collectives priced at an assumed latency / volume")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="timing rehearsal: run rank --sim-rank of a P-rank job alone on this GPU (its rows, "
                          "ghost layout, interior/boundary launches, graphs) with collectives that move nothing")
@@ -170,7 +174,11 @@ def _run_rank(args, out_fd) -> int:
     comm = mcg.native().NullComm(env.rank, env.world) if rehearse else pdist.bootstrap_comm(env, force=args.force_comm, mode=args.comm)
     sim = args.sim_world > 1 and env.world == 1
     if sim:  # per-rank timing rehearsal (not a P-rank solve: see --sim-world)
-        comm = mcg.native().NullComm(args.sim_rank, args.sim_world)
+        if args.delay_comm:
+            ar_us, halo_us = (float(v) for v in args.delay_comm.split(","))
+            comm = mcg.native().DelayComm(args.sim_rank, args.sim_world, ar_us, halo_us, False)
+        else:
+            comm = mcg.native().NullComm(args.sim_rank, args.sim_world)
 
     if args.problem == "randspd":
         spec = mcg.make_problem("randspd", rows=args.rows, band=args.band, density=args.density, spread=args.spread,
@@ -297,7 +305,8 @@ def _run_rank(args, out_fd) -> int:
                 "nnz": nnz,
                 "global_batch": 1,
                 "seq_len": spec.n_rows,
-                "parallelism": (f"sim-rank{args.sim_rank}-of-{args.sim_world}" if sim else
+                "parallelism": (f"sim-rank{args.sim_rank}-of-{args.sim_world}"
+                                + (f"-delaycomm{args.delay_comm.replace(',', '-')}us" if args.delay_comm else "") if sim else
                                 f"rehearse-rowpart{n_gpus}-one-gpu" if rehearse else f"rowpart{n_gpus}"),
                 # storage the timed pass streams (the carries read SELL-64/dia4 codes; their lean runs
                 # only the per-slice pattern words of uniform slices)

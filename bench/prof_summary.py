@@ -7,6 +7,8 @@
 import argparse
 import collections
 import csv
+import glob
+import os
 import re
 
 
@@ -22,6 +24,9 @@ def main():
     ap.add_argument("--title", default="rocprofv3 summary")
     a = ap.parse_args()
     print(f"# {a.title}\n")
+    if a.stats and os.path.isdir(a.stats):  # a rocprofv3 output directory: its kernel-stats CSV
+        found = glob.glob(os.path.join(a.stats, "**", "*kernel_stats.csv"), recursive=True)
+        a.stats = found[0] if found else None
     if a.stats:
         rows = list(csv.DictReader(open(a.stats)))
         print("| kernel | calls | avg µs | total ms | % |")

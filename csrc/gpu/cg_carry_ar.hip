@@ -155,10 +155,16 @@ __device__ __forceinline__ void g_st_nt(double* base, uint32_t bo, double v) {
 template <bool UNI>
 __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat, int64_t l0, int64_t l1, int64_t nl,
                                               int64_t ss, int64_t col, int64_t ext_len, uint32_t& WA, uint32_t& WB,
-                                              uint32_t& WC) {
+                                              uint32_t& WC, int big = 0) {
   auto ld = [&](int64_t i) { return UNI ? uni_u64(dpat[i]) : dpat[i]; };
   WA = WB = WC = 0u;
-  if (dpat == nullptr || l1 - l0 < 3 || nl < 4 || ext_len >= ((int64_t)1 << 29)) return false;  // 32-bit byte offsets
+  // 32-bit byte offsets: from kernel-wide bases (ext_len < 2^29), or past that (BIG kernels) from
+  // per-run bases (big = 1, the 2-D loop: lines -3 .. the run's end + 4 inside 4 GiB) or bases moved
+  // along the run (big = 2, the 3-D loop)
+  if (dpat == nullptr || l1 - l0 < 3 || nl < 4) return false;
+  if (ext_len >= ((int64_t)1 << 29) &&
+      (big == 0 || ext_len >= ((int64_t)1 << 31) || (big == 1 && (l1 - l0 + 8) * ss * 512 >= ((int64_t)1 << 32))))
+    return false;
   const int64_t ia = l0 - 1 > 1 ? l0 - 1 : 1, ib = l1 < nl - 2 ? l1 : nl - 2;  // inner lines of l0 - 1 .. l1
   const uint64_t wb = ld(ia * ss + col);
   WB = (uint32_t)wb;
@@ -183,7 +189,9 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
 }
 
 // LEAN > 0: lean-only kernel (every run checked at setup) for at least LEAN waves per SIMD
-template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0>
+// BIG (lean kernels): the rank's vectors exceed 2^29 doubles, so each run re-bases its global pointers
+// (64-bit, scalar registers) at its own first lines and keeps 32-bit byte offsets inside the run
+template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
@@ -317,7 +325,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       // the kernel has no generic step at all (one kernel with both measured slower for each)
       constexpr int LD = QD + 1;
       uint32_t WA, WB, WC;
-      (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
+      (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC, BIG ? 1 : 0);
       if constexpr (LEAN > 0) {
         struct VSet {
           double v[5];
@@ -336,8 +344,18 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           const uint32_t l8 = (uint32_t)lane << 3;
           const uint32_t LOB = (uint32_t)LO << 3;                         // one line of the vectors
           const uint32_t SB = (uint32_t)(2 * SS) << 3;                    // one line of the edge arrays
-          const uint32_t ob0 = (uint32_t)e0 << 3;                         // line 0 (ext layout)
-          const uint32_t xb0 = (uint32_t)i0 << 3;                         // line 0 of x
+          // BIG: byte offsets from per-run bases (ext index e0 - 3 lines, x index i0)
+          const int64_t rb = BIG ? (int64_t)e0 - 3 * (int64_t)LO : 0;
+          const int64_t xr = BIG ? (int64_t)i0 : 0;
+          const double* __restrict__ po_ = po + rb;
+          const double* __restrict__ ro_ = ro + rb;
+          double* __restrict__ pn_ = pn + rb;
+          double* __restrict__ rn_ = rn + rb;
+          double* __restrict__ x_ = x + xr;
+          const double* __restrict__ apo_ = apx_o + rb;
+          double* __restrict__ apn_ = apx_n + rb;
+          const uint32_t ob0 = BIG ? 3u * ((uint32_t)LO << 3) : (uint32_t)e0 << 3;  // line 0 (ext layout)
+          const uint32_t xb0 = BIG ? 0u : (uint32_t)i0 << 3;                         // line 0 of x
           const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;  // edge arrays: 2 s - 1 of line 0
           // lane 0: entry 2 s - 1 and row e - 1, lane 63: 2 s + 2 and row e + 64; a lane without
           // its edge entry reads its own slice's (in range at the rank's first / last slice)
@@ -352,8 +370,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           auto raw_at = [&](int32_t j) {
             Raw q;
             const uint32_t o = line_ofs(jc(j)) + l8;
-            q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
-            q.p = g_ld(po, o);
+            q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
+            q.p = g_ld(po_, o);
             return q;
           };
           auto edge_at = [&](int32_t j) {
@@ -361,17 +379,17 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
             q.r = g_ld(reo, c);
             q.a = g_ld(eo, c);
-            q.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
+            q.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
             return q;
           };
           // a ghost line's r_{k-1} (step()'s rghost): from the halo's p_{k-2} in p_new's ghost rows
-          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), q.p); };
+          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn_, line_ofs(j) + l8), q.p); };
           auto is_ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
           auto raw_un = [&](int32_t j) {  // a line of the run or below it, inside the rank
             Raw q;
             const uint32_t o = line_ofs(j) + l8;
-            q.r = g_ld(j < n_run ? (const double*)pn : ro, o);
-            q.p = g_ld(po, o);
+            q.r = g_ld(j < n_run ? (const double*)pn_ : ro_, o);
+            q.p = g_ld(po_, o);
             return q;
           };
           auto edge_un = [&](int32_t j) {
@@ -379,11 +397,11 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const uint32_t c = cb0 + (uint32_t)j * SB + oc;
             q.r = g_ld(reo, c);
             q.a = g_ld(eo, c);
-            q.p = g_ld(po, line_ofs(j) - 8u + op);
+            q.p = g_ld(po_, line_ofs(j) - 8u + op);
             return q;
           };
           auto x_at = [&](int32_t j) {
-            if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+            if constexpr (PAIR) return g_ld(x_, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
             else return 0.0;
           };
           auto ez = [&](double e) { return e; };
@@ -415,7 +433,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
             pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p), rm1.r));
           } else if (is_ghost(-1)) {
-            pr_pk = fma(b, rm1.p, fma(na, g_ld(apx_o, line_ofs(-1) + l8), rghost(-1, rm1)));
+            pr_pk = fma(b, rm1.p, fma(na, g_ld(apo_, line_ofs(-1) + l8), rghost(-1, rm1)));
           }
           double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
           {
@@ -438,21 +456,21 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
               pk1 = fma(b, q[0].p, rk1);
             } else if (CL && next == 2) {
-              rk1 = fma(na, g_ld(apx_o, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
+              rk1 = fma(na, g_ld(apo_, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
               pk1 = fma(b, q[0].p, rk1);
             }
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1);
             const uint32_t ob = line_ofs(m);
             const double rr = fma(-b, o_pold, o_pk);
-            if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+            if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
             if (edge_lane) {
               const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
               g_st(ren, sb, rr);
               g_st(en, sb, sum);
             }
-            if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-            g_st_nt(pn, ob + l8, o_pk);
-            if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apx_n, ob + l8, sum);
+            if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+            g_st_nt(pn_, ob + l8, o_pk);
+            if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apn_, ob + l8, sum);
             s_pap = fma(o_pk, sum, s_pap);
             s_rap = fma(o_rk, sum, s_rap);
             s_apap = fma(sum, sum, s_apap);
@@ -518,9 +536,23 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       const uint32_t l8 = (uint32_t)lane << 3;
       const uint32_t LOB = (uint32_t)LO << 3;
       const uint32_t SB = (uint32_t)(2 * SS) << 3;
-      const uint32_t ob0 = (uint32_t)e0 << 3;
-      const uint32_t xb0 = (uint32_t)i0 << 3;
-      const uint32_t kb0 = xb0 + LOB;  // the coefficient arrays: one line in front
+      const int64_t rb = BIG ? (int64_t)e0 - 3 * (int64_t)LO : 0;  // BIG: per-run bases (see the CM == 4 loop)
+      const int64_t xr = BIG ? (int64_t)i0 : 0;
+      const double* __restrict__ po_ = po + rb;
+      const double* __restrict__ ro_ = ro + rb;
+      double* __restrict__ pn_ = pn + rb;
+      double* __restrict__ rn_ = rn + rb;
+      double* __restrict__ x_ = x + xr;
+      const double* __restrict__ apo_ = apx_o + rb;
+      double* __restrict__ apn_ = apx_n + rb;
+      const int64_t kr = BIG ? (int64_t)i0 - 2 * (int64_t)LO : 0;  // lines -2 .. of the run: offsets >= 0
+      const double* __restrict__ cvd_ = S.cvd + kr;
+      const double* __restrict__ cve_ = S.cve + kr;
+      const double* __restrict__ cvs_ = S.cvs + kr;
+      const uint32_t ob0 = BIG ? 3u * LOB : (uint32_t)e0 << 3;
+      const uint32_t xb0 = BIG ? 0u : (uint32_t)i0 << 3;
+      // the coefficient arrays have one line in front: line j of the run at kb0 + j LOB
+      const uint32_t kb0 = BIG ? 3u * LOB : ((uint32_t)i0 << 3) + LOB;
       const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;
       const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
       const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
@@ -533,8 +565,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       auto raw_at = [&](int32_t j) {
         Raw q;
         const uint32_t o = line_ofs(jc(j)) + l8;
-        q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
-        q.p = g_ld(po, o);
+        q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
+        q.p = g_ld(po_, o);
         return q;
       };
       auto edge_at = [&](int32_t j) {
@@ -542,7 +574,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
         q.r = g_ld(reo, c);
         q.a = g_ld(eo, c);
-        q.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
+        q.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
         return q;
       };
       auto coef_ofs = [&](int32_t j) { return kb0 + (uint32_t)j * LOB; };
@@ -550,19 +582,19 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       // never used there)
       auto coef_ld = [&](uint32_t o) {
         CRaw c;
-        c.d = g_ld(S.cvd, o + l8);
-        c.e = g_ld(S.cve, o + l8);
-        c.s = g_ld(S.cvs, o + l8);
-        c.ee = g_ld(S.cve, o >= 8u ? o - 8u : o);
+        c.d = g_ld(cvd_, o + l8);
+        c.e = g_ld(cve_, o + l8);
+        c.s = g_ld(cvs_, o + l8);
+        c.ee = g_ld(cve_, o >= 8u ? o - 8u : o);
         return c;
       };
-      auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), q.p); };
+      auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn_, line_ofs(j) + l8), q.p); };
       auto is_ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
       auto raw_un = [&](int32_t j) {
         Raw q;
         const uint32_t o = line_ofs(j) + l8;
-        q.r = g_ld(j < n_run ? (const double*)pn : ro, o);
-        q.p = g_ld(po, o);
+        q.r = g_ld(j < n_run ? (const double*)pn_ : ro_, o);
+        q.p = g_ld(po_, o);
         return q;
       };
       auto edge_un = [&](int32_t j) {
@@ -570,11 +602,11 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         const uint32_t c = cb0 + (uint32_t)j * SB + oc;
         q.r = g_ld(reo, c);
         q.a = g_ld(eo, c);
-        q.p = g_ld(po, line_ofs(j) - 8u + op);
+        q.p = g_ld(po_, line_ofs(j) - 8u + op);
         return q;
       };
       auto x_at = [&](int32_t j) {
-        if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+        if constexpr (PAIR) return g_ld(x_, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
         else return 0.0;
       };
       auto mkv = [&](const CRaw& c, double s_up) {
@@ -615,7 +647,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       if (l0 >= 1) {
         pr_pk = fma(b, rm1.p, fma(na, stencil_v(mkv(cm1, cm2.s), rm1.p, edm1.p, rm2.p, r0.p), rm1.r));
       } else if (is_ghost(-1)) {
-        pr_pk = fma(b, rm1.p, fma(na, g_ld(apx_o, line_ofs(-1) + l8), rghost(-1, rm1)));
+        pr_pk = fma(b, rm1.p, fma(na, g_ld(apo_, line_ofs(-1) + l8), rghost(-1, rm1)));
       }
       VSet Vs = mkv(c0, cm1.s);  // line m
       double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
@@ -635,21 +667,21 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
           pk1 = fma(b, q[0].p, rk1);
         } else if (CL && next == 2) {
-          rk1 = fma(na, g_ld(apx_o, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
+          rk1 = fma(na, g_ld(apo_, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
           pk1 = fma(b, q[0].p, rk1);
         }
         const double sum = stencil_v(Vs, o_pk, o_epk, pr_pk, pk1);
         const uint32_t ob = line_ofs(m);
         const double rr = fma(-b, o_pold, o_pk);
-        if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+        if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
         if (edge_lane) {
           const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);
           g_st(ren, sb, rr);
           g_st(en, sb, sum);
         }
-        if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-        g_st_nt(pn, ob + l8, o_pk);
-        if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apx_n, ob + l8, sum);
+        if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+        g_st_nt(pn_, ob + l8, o_pk);
+        if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apn_, ob + l8, sum);
         s_pap = fma(o_pk, sum, s_pap);
         s_rap = fma(o_rk, sum, s_rap);
         s_apap = fma(sum, sum, s_apap);
@@ -940,7 +972,9 @@ __device__ __forceinline__ void ar3_finish(double a0, double a1, double a2, doub
   if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
 }
 
-template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false>
+// BIG (lean kernels): past 2^29 doubles a run's planes (N^2 rows each) do not fit 32-bit byte offsets
+// from kernel-wide bases, so the lean loop re-bases its ext / x pointers every unrolled step group
+template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false, bool BIG = false>
 __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                                   int32_t LN, int gfull,
                                                                   double* __restrict__ partials, int pstride,
@@ -1049,7 +1083,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       constexpr int LD = 3, ED = 2, UNR = 6;
       uint32_t WA = 0, WB = 0, WC = 0;
       if constexpr (LEAN) {  // every run checked at setup (carry_lean_failures)
-        (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC);
+        (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC, BIG ? 2 : 0);
         __syncthreads();  // the previous job's last step has read its LDS slots
       }
       if constexpr (LEAN) {
@@ -1073,8 +1107,27 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
           const uint32_t l8 = (uint32_t)lane << 3;
           const uint32_t LOB = (uint32_t)LO << 3;                         // one plane of the vectors
           const uint32_t SB = (uint32_t)(2 * SS) << 3;                    // one plane of the edge arrays
-          const uint32_t ob0 = (uint32_t)e0 << 3;                         // plane 0 (ext layout)
-          const uint32_t xb0 = (uint32_t)i0 << 3;                         // plane 0 of x
+          // BIG: pointers re-based at plane mb (ext: plane mb - 3, x: plane mb) by rebase(); the
+          // 32-bit offsets are then (j - mb) planes from there.  !BIG: mb = 0, kernel-wide bases
+          int32_t mb = 0;
+          const double *po_ = po, *ro_ = ro, *apo_ = apo;
+          double *pn_ = pn, *rn_ = rn, *x_ = x, *apw_ = apw;
+          auto rebase = [&](int32_t m) {
+            if constexpr (BIG) {
+              mb = m;
+              const int64_t eb = (int64_t)e0 + (int64_t)(m - 3) * LO, xb = (int64_t)i0 + (int64_t)m * LO;
+              po_ = po + eb;
+              ro_ = ro + eb;
+              apo_ = apo + eb;
+              pn_ = pn + eb;
+              rn_ = rn + eb;
+              apw_ = apw + eb;
+              x_ = x + xb;
+            }
+          };
+          rebase(0);
+          const uint32_t ob0 = BIG ? 3u * ((uint32_t)LO << 3) : (uint32_t)e0 << 3;  // plane 0 (ext layout)
+          const uint32_t xb0 = BIG ? 0u : (uint32_t)i0 << 3;                         // plane 0 of x
           const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;  // edge arrays: 2 s - 1 of plane 0
           const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
           const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
@@ -1084,12 +1137,12 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
           const int32_t rlo = -(int32_t)l0, rhi = (int32_t)(nl - 1 - l0);
           auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
           auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
-          auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
+          auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)(j - mb) * LOB; };
           auto raw_ld = [&](int32_t j, int32_t k) {  // plane j's source, plane k's address
             Raw r;
             const uint32_t o = line_ofs(k) + l8;
-            r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
-            r.p = g_ld(po, o);
+            r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
+            r.p = g_ld(po_, o);
             return r;
           };
           auto edge_ld = [&](int32_t j) {  // plane j (clamped: compact index to the rank, row to ext)
@@ -1097,7 +1150,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
             const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
             r.r = g_ld(reo, c);
             r.a = g_ld(eao, c);
-            r.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
+            r.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
             return r;
           };
           auto edge_un = [&](int32_t j) {
@@ -1105,23 +1158,23 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
             const uint32_t c = cb0 + (uint32_t)j * SB + oc;
             r.r = g_ld(reo, c);
             r.a = g_ld(eao, c);
-            r.p = g_ld(po, line_ofs(j) - 8u + op);
+            r.p = g_ld(po_, line_ofs(j) - 8u + op);
             return r;
           };
-          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), q.p); };
+          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn_, line_ofs(j) + l8), q.p); };
           auto is_ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
           auto far_ld = [&](int32_t k) {
             Far f{0.0, 0.0, 0.0};
             if (outer) {
               const uint32_t o = line_ofs(k) + l8 + fob;
-              f.r = g_ld(ro, o);
-              f.p = g_ld(po, o);
-              f.a = g_ld(apo, o);
+              f.r = g_ld(ro_, o);
+              f.p = g_ld(po_, o);
+              f.a = g_ld(apo_, o);
             }
             return f;
           };
           auto x_at = [&](int32_t j) {
-            if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+            if constexpr (PAIR) return g_ld(x_, xb0 + (uint32_t)((j < n_run - 1 ? j : n_run - 1) - mb) * LOB + l8);
             else return 0.0;
           };
           auto ez = [&](double e) { return e; };
@@ -1165,7 +1218,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
             const double t = stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p, dn, up);
             pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
           } else if (is_ghost(-1)) {
-            pr_pk = pk_of(rghost(-1, rm1), g_ld(apo, line_ofs(-1) + l8), rm1.p);
+            pr_pk = pk_of(rghost(-1, rm1), g_ld(apo_, line_ofs(-1) + l8), rm1.p);
           }
           double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
           {
@@ -1184,8 +1237,8 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
             const int par = m & 1;
             const uint32_t ob = line_ofs(m);
             const double rr = fma(-b, o_pold, o_pk);
-            if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
-            else if (outer) g_st(rn, ob + l8, rr);
+            if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
+            else if (outer) g_st(rn_, ob + l8, rr);
             const int32_t kn = CL ? jc(m + LD) : m + LD;
             const Raw qn = raw_ld(m + LD, kn);
             const Edge en2 = CL ? edge_ld(m + ED) : edge_un(m + ED);
@@ -1202,15 +1255,15 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
               rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
               pk1 = fma(b, qv[0].p, rk1);
             } else if (CL && next == 2) {
-              rk1 = fma(na, g_ld(apo, line_ofs(m + 1) + l8), rghost(m + 1, qv[0]));
+              rk1 = fma(na, g_ld(apo_, line_ofs(m + 1) + l8), rghost(m + 1, qv[0]));
               pk1 = fma(b, qv[0].p, rk1);
             }
             double kdn, kup;
             nbr(par, 1, o_fpk, kdn, kup);
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1, kdn, kup);
-            if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-            g_st_nt(pn, ob + l8, o_pk);
-            if (outer || (CL && gfull && (l0 + m == 0 || l0 + m == nl - 1))) g_st(apw, ob + l8, sum);
+            if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)(m - mb) * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+            g_st_nt(pn_, ob + l8, o_pk);
+            if (outer || (CL && gfull && (l0 + m == 0 || l0 + m == nl - 1))) g_st(apw_, ob + l8, sum);
             if (edge_lane) {
               const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
               g_st(ean, sb, sum);
@@ -1248,9 +1301,11 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
           if (m_lo == 1) lstep(clamped, 0, vals(WA), VB, 1);
           m = m_lo;
           for (; m + UNR - 1 <= m_hi; m += UNR) {
+            rebase(m);
 #pragma unroll
             for (int u = 0; u < UNR; ++u) lstep(unclamped, m + u, VB, VB, 1);
           }
+          rebase(m);
           for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, 1);
           if (m < n_run) {
             const VSet VC = vals(WC);
@@ -1693,7 +1748,8 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
     const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
     if (l0 >= l1) continue;
     uint32_t a, b, c;
-    if (!lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c)) ++f;
+    // past 2^29 the BIG kernels re-base: per run (2-D), along the run (3-D)
+    if (!lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c, kw == 0 ? 1 : 2)) ++f;
   }
   if (f) atomicAdd(fails, f);
 }
@@ -1854,10 +1910,18 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     return;
   }
   const bool pair = (k & 1) != 0;
+  const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: per-run 64-bit bases
+  MCG_CHECK(v.ext_len < ((int64_t)1 << 31), "Ap-recomputing carry: a rank's vectors must stay below 2^31 rows");
   if (cm == 4 && p3k && lean && S.dpat != nullptr) {  // lean-only kernels (4 waves per SIMD)
-#define MCG_LW(QD, PAIR) \
-  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
-                     partials, pstride, st, tol, first, check, rc)
+#define MCG_LW(QD, PAIR)                                                                                       \
+  do {                                                                                                         \
+    if (big)                                                                                                   \
+      hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4, true>), dim3(grid), dim3(kBS), 0, stream, S, v, \
+                         own_off, tr, partials, pstride, st, tol, first, check, rc);                           \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
+                         tr, partials, pstride, st, tol, first, check, rc);                                    \
+  } while (0)
     if (depth >= 3) { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
     else { if (pair) MCG_LW(2, true); else MCG_LW(2, false); }
 #undef MCG_LW
@@ -1865,9 +1929,15 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     return;
   }
   if (cm == 5 && p3k && lean) {  // diav lean-only kernels: the streamed coefficients need more VGPRs
-#define MCG_LV(QD, PAIR) \
-  hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
-                     tr, partials, pstride, st, tol, first, check, rc)
+#define MCG_LV(QD, PAIR)                                                                                        \
+  do {                                                                                                          \
+    if (big)                                                                                                    \
+      hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV, true>), dim3(grid), dim3(kBS), 0, stream, S, \
+                         v, own_off, tr, partials, pstride, st, tol, first, check, rc);                         \
+    else                                                                                                        \
+      hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV>), dim3(grid), dim3(kBS), 0, stream, S, v, \
+                         own_off, tr, partials, pstride, st, tol, first, check, rc);                            \
+  } while (0)
     if (depth >= 3) { if (pair) MCG_LV(3, true); else MCG_LV(3, false); }
     else { if (pair) MCG_LV(2, true); else MCG_LV(2, false); }
 #undef MCG_LV
@@ -1927,12 +1997,14 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
   const bool pair = (k & 1) != 0;
   const int qd = depth >= 3 ? 3 : 2;
   const int g = gfull ? 1 : 0;
+  const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: bases moved along the run
 #define MCG_A3(QD, PAIR, KW, P3, ...)                                                                         \
   hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, stream, S, v, \
                      own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
 #define MCG_A3P(QD, PAIR, KW)                                         \
   do {                                                                \
-    if (p3 && !first && lean && S.dpat != nullptr) MCG_A3(QD, PAIR, KW, true, true); \
+    if (p3 && !first && lean && S.dpat != nullptr && big) MCG_A3(QD, PAIR, KW, true, true, true); \
+    else if (p3 && !first && lean && S.dpat != nullptr) MCG_A3(QD, PAIR, KW, true, true); \
     else if (p3 && !first) MCG_A3(QD, PAIR, KW, true);                \
     else MCG_A3(QD, PAIR, KW, false);                                 \
   } while (0)

@@ -65,6 +65,7 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
     // wait until the group finished segment step - lag (slack > 0: all but slack of its workgroups)
     const int need = step + 1 - T.pace_lag;
     int spin = 0;
+    const int cap = kPaceSpins * 8 / T.pace_sleep;  // ~1 ms whatever the poll interval
     if (T.pace_flag) {
       unsigned* f = T.pace + kTilePaceCnt + grp * 8 * 64;
       const unsigned done = old + 1 + slack;
@@ -72,18 +73,18 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
         for (int r = 0; r < 8; ++r) __hip_atomic_fetch_max(f + r * 64, done / nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned* fr = f + ((blockIdx.x >> 3) & 7) * 64;
       if (need > 0)
-        for (; spin < kPaceSpins; ++spin) {
+        for (; spin < cap; ++spin) {
           if (__hip_atomic_load(fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)need) break;
-          __builtin_amdgcn_s_sleep(8);
+          for (int z = 0; z < T.pace_sleep; ++z) __builtin_amdgcn_s_sleep(1);
         }
     } else if (need > 0) {
       const unsigned target = (unsigned)need * nwg - slack;
-      for (; spin < kPaceSpins; ++spin) {
+      for (; spin < cap; ++spin) {
         if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
         __builtin_amdgcn_s_sleep(8);
       }
     }
-    if (spin == kPaceSpins) *live = 0;
+    if (spin == cap) *live = 0;
   }
   __syncthreads();
 }

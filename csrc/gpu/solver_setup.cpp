@@ -495,7 +495,7 @@ void GpuCgSolver::setup() {
       // SELL-64/diav, the per-row values streamed by the Ap-recomputing line carry
       if (!c8_ && carry_lo2_ == 0 && stencil_plane(spec_) == 0 && stencil_line(spec_) == gl &&
           info_.max_row_len <= 5 && opt_.form.carry_vc != 0 && opt_.form.ap_recompute != 0 && !split_ && n > 0 &&
-          (n + gl) < ((int64_t)1 << 29)) {
+          (n + gl) < ((int64_t)1 << 31)) {
         cv_len_ = n + gl;
         cv_.allocate(3 * cv_len_, "A", 64);
         if (kern::sell_to_diav(sell_view(), gl, cv_.get(), s0_)) {
@@ -614,21 +614,26 @@ void GpuCgSolver::setup() {
     // diav: every run of >= 3 lines streams its coefficients in the lean loop (the same grids as the
     // dia4 2-D passes); checked here on the host from the launch's job decomposition
     const int64_t ss = tr_all_.strip, nlines = (n + 63) / 64 / ss;
-    int g = g_all_;
-    for (int bpc : {16, 8, 4}) {
-      const int64_t waves = (int64_t)ncu_ * bpc * 4;
-      if (nlines / std::max<int64_t>(1, waves / ss) >= 64) {
+    // every run of the launch must be >= 3 lines (within 4 GiB of byte offsets past 2^29 rows)
+    auto all_lean = [&](int g) {
+      const int64_t nw = (int64_t)g * 4, runs = nw > ss ? nw / ss : 1, chunk = (nlines + runs - 1) / runs;
+      bool all = nlines >= 4 && L_.ext_len < ((int64_t)1 << 31) && (chunk + 8) * ss * 512 < ((int64_t)1 << 32);
+      for (int64_t r = 0; r < runs && all; ++r) {
+        const int64_t l0 = r * chunk, l1 = std::min(nlines, l0 + chunk);
+        if (l0 < nlines && l1 - l0 < 3) all = false;
+      }
+      return all;
+    };
+    // the dia4 2-D grids (runs of >= 64 lines), else the largest smaller grid whose runs all qualify
+    int g = 0;
+    for (int bpc : {16, 8, 4})
+      if (nlines / std::max<int64_t>(1, (int64_t)ncu_ * bpc * 4 / ss) >= 64) {
         g = ncu_ * bpc;
         break;
       }
-    }
-    const int64_t nw = (int64_t)g * 4, runs = nw > ss ? nw / ss : 1, chunk = (nlines + runs - 1) / runs;
-    bool all = nlines >= 4 && L_.ext_len < ((int64_t)1 << 29);
-    for (int64_t r = 0; r < runs && all; ++r) {
-      const int64_t l0 = r * chunk, l1 = std::min(nlines, l0 + chunk);
-      if (l0 < nlines && l1 - l0 < 3) all = false;
-    }
-    if (all) {
+    if (g == 0) g = g_all_;
+    for (int gg = g; gg >= 1 && !all_lean(gg); gg /= 2) g = gg / 2;
+    if (g >= 1 && all_lean(g)) {
       lean_only_ = true;
       g_all_ = g;
     }

@@ -60,6 +60,8 @@ struct PassForm {
                              // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest);
                              // 3 / 4 = as 1 / 2, the waiters polling a step flag instead of the arrival counter
   int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
+  int tile_pace_slack = 1;   // tiles, tile_pace 2 / 4: a workgroup waits for all but this many eighths of its group
+  int tile_pace_sleep = 8;   // tiles: s_sleep units (64 clocks each) between two polls of a waiting workgroup
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

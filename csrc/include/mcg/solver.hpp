@@ -203,9 +203,10 @@ class GpuCgSolver {
     t.G = tgeo_.G;
     t.seg_shift = tgeo_.seg_shift;
     t.pace = opt_.form.tile_pace > 0 ? tpace_.get() : nullptr;
-    t.pace_slack8 = (opt_.form.tile_pace == 2 || opt_.form.tile_pace == 4) ? 1 : 0;
+    t.pace_slack8 = (opt_.form.tile_pace == 2 || opt_.form.tile_pace == 4) ? std::max(0, std::min(7, opt_.form.tile_pace_slack)) : 0;
     t.pace_flag = opt_.form.tile_pace >= 3 ? 1 : 0;
     t.pace_lag = std::max(0, opt_.form.tile_pace_lag);
+    t.pace_sleep = std::max(1, std::min(64, opt_.form.tile_pace_sleep));
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)

@@ -218,6 +218,8 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(tile_pace)
       MCG_FORM_PROP(carry_vc)
       MCG_FORM_PROP(tile_pace_lag)
+      MCG_FORM_PROP(tile_pace_slack)
+      MCG_FORM_PROP(tile_pace_sleep)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       MCG_FORM_PROP(pmat)
