@@ -139,6 +139,15 @@ def recipes(a) -> dict:
                             ("s18_lag1", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_lag=1"]),
                             ("s18_again", ["tile_pace=4", "tile_seg_log2=18"]))
         ],
+        # r4: next-segment L2 prefetch during the pacing wait
+        "c5pf": [
+            (tag, 400, bench(f"{c5} --steps 6 --warmup 2 {sets(kv)}"))
+            for tag, kv in (("s18_pf", ["tile_pace=4", "tile_seg_log2=18", "tile_prefetch=1"]),
+                            ("s18", ["tile_pace=4", "tile_seg_log2=18"]),
+                            ("s19_pf", ["tile_pace=4", "tile_seg_log2=19", "tile_prefetch=1"]),
+                            ("s17_pf", ["tile_pace=4", "tile_seg_log2=17", "tile_prefetch=1"]),
+                            ("s18_pf_again", ["tile_pace=4", "tile_seg_log2=18", "tile_prefetch=1"]))
+        ],
         # config 5 at ~200 GB per GPU and with the all-gather priced (DelayComm)
         "c5big": [
             ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2 "
@@ -203,6 +212,12 @@ def recipes(a) -> dict:
                                               f"--set carry3_kw={kw}")) for rep in (1, 2) for kw in (16, 8, 4)],
         "placement": [(f"t{t}_{rep}", 150, bench(f"--phases 0 --set placement_tries={t}"))
                       for rep in (1, 2) for t in (1, 3, 6)],
+        # r4: 4096^2 (BASELINE config 2) lean-pass geometry: prefetch depth x blocks per CU
+        "p4096": [
+            (f"d{d}_b{b}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify "
+                                      f"--set lean_depth={d} --set lean_bpc={b}"))
+            for d in (3, 4, 6) for b in (2, 4, 8)
+        ] + [("auto_again", 200, bench("--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify"))],
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),

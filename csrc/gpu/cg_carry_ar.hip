@@ -1922,8 +1922,15 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
       hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
                          tr, partials, pstride, st, tol, first, check, rc);                                    \
   } while (0)
-    if (depth >= 3) { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
+#define MCG_LWD(QD, PAIR, W)                                                                                   \
+  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
+                     partials, pstride, st, tol, first, check, rc)
+    // deeper prefetch (lean_depth 4 / 6: fewer waves per SIMD, more lines in flight per wave; small grids)
+    if (depth >= 6 && !big) { if (pair) MCG_LWD(6, true, 2); else MCG_LWD(6, false, 2); }
+    else if (depth == 4 && !big) { if (pair) MCG_LWD(4, true, 3); else MCG_LWD(4, false, 3); }
+    else if (depth >= 3) { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
     else { if (pair) MCG_LW(2, true); else MCG_LW(2, false); }
+#undef MCG_LWD
 #undef MCG_LW
     MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
     return;

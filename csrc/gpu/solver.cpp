@@ -241,7 +241,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     // passes 2 (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md);
     // the lean ones 3 as well (4096^2 8191-8225 vs 8064-8084 it/s, 16384^2 586.4 vs 584.9,
     // profiles/r3/lean/README.md)
-    const int depth = ((k & 1) == 0 && p3_ && !lean_only_) ? 2 : 3;
+    const int depth = ((k & 1) == 0 && p3_ && !lean_only_) ? 2 : (lean_only_ && opt_.form.lean_depth > 0 ? opt_.form.lean_depth : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
                       p3_, 3, lean_only_);

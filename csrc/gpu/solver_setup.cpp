@@ -30,6 +30,46 @@ double randspd_aligned_fill(const ProblemSpec& s) {
   return (double)(s.band + 1) / (1.0 + (double)s.band * qm);
 }
 
+// SELL-64/aligned for a user matrix (per-slice offset unions): a slice's slots are the sorted union
+// of its 64 rows' column offsets (ext column - the row's own ext column), each row's value at its
+// offset's slot and 0.0 elsewhere, so every slot's 64 gathers are one contiguous run of p.  The
+// entries keep their order (ascending offset = ascending column), so the row sums are CSR's.
+// Returns the total slots (64 per slot of every slice); fills the arrays when `fill`.
+int64_t aligned_unions(const HostCsr& A, int64_t own_off, bool fill, std::vector<int64_t>* slice_ptr,
+                       std::vector<int32_t>* soffs, std::vector<double>* vals) {
+  const int64_t n = A.n_rows, ns = (n + 63) / 64;
+  int64_t total = 0;
+  std::vector<int32_t> u;
+  if (fill) {
+    slice_ptr->assign(ns + 1, 0);
+    soffs->clear();
+    vals->clear();
+  }
+  for (int64_t sl = 0; sl < ns; ++sl) {
+    u.clear();
+    const int64_t r0 = sl * 64, r1 = std::min(n, r0 + 64);
+    for (int64_t i = r0; i < r1; ++i)
+      for (int64_t k = A.rowptr[i]; k < A.rowptr[i + 1]; ++k) u.push_back((int32_t)(A.cols[k] - (own_off + i)));
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    const int64_t w = (int64_t)u.size();
+    if (fill) {
+      const int64_t base = (int64_t)vals->size();
+      soffs->insert(soffs->end(), u.begin(), u.end());
+      vals->resize(base + 64 * w, 0.0);
+      for (int64_t i = r0; i < r1; ++i)
+        for (int64_t k = A.rowptr[i]; k < A.rowptr[i + 1]; ++k) {
+          const int32_t off = (int32_t)(A.cols[k] - (own_off + i));
+          const int64_t j = std::lower_bound(u.begin(), u.end(), off) - u.begin();
+          (*vals)[base + 64 * j + (i - r0)] += A.vals[k];  // duplicates were summed on input already
+        }
+      (*slice_ptr)[sl + 1] = base + 64 * w;
+    }
+    total += 64 * w;
+  }
+  return total;
+}
+
 // stored SELL-64 slots of rows taken in the order `order` (slice = 64 consecutive slots)
 int64_t sell_slots(const HostCsr& A, const std::vector<int32_t>* order) {
   const int64_t n = A.n_rows;
@@ -146,7 +186,33 @@ void GpuCgSolver::setup() {
            (opt_.form.tiles == 1 || scrambled(spec_) || scattered_user);
   if (is_user) {
     user = build_local_csr(spec_, L_);
-    if (opt_.format == 1 && !tiles_ && opt_.form.sell_sigma != 0 && n > 64 && (opt_.form.sell_sigma > 0 || stencil_line(spec_) == 0)) {
+    // a banded user matrix whose slices share few offsets: SELL-64/aligned with per-slice offset
+    // unions (the generated wide random SPD's layout), when the unions cost <= 1.6 slots per
+    // nonzero; the same decision on every rank (it implies the split pass and its ghost vectors)
+    if (opt_.format == 1 && !tiles_ && stencil_line(spec_) == 0 && opt_.recurrence == 1 && opt_.form.pmat != 0 &&
+        opt_.form.sell_aligned != 0) {
+      const int64_t slots = n > 0 ? aligned_unions(user, L_.own_off, false, nullptr, nullptr, nullptr) : 0;
+      const int64_t unnz = user.nnz();
+      // a matrix with a one-byte (value, offset) dictionary streams 1 B per entry on c8 (sellc8): keep it
+      bool small_dict = false;
+      if (c8_) {
+        std::vector<std::pair<double, int32_t>> seen;
+        small_dict = true;
+        for (int64_t i = 0; i < n && small_dict; ++i)
+          for (int64_t k = user.rowptr[i]; k < user.rowptr[i + 1] && small_dict; ++k) {
+            const std::pair<double, int32_t> e(user.vals[k], (int32_t)(user.cols[k] - (L_.own_off + i)));
+            if (std::find(seen.begin(), seen.end(), e) == seen.end()) {
+              seen.push_back(e);
+              small_dict = seen.size() <= 256;
+            }
+          }
+      }
+      user_aligned_ = opt_.form.sell_aligned == 1 ||
+                      (!small_dict && unnz > 0 && (double)slots <= 1.6 * (double)unnz);
+      if (use_comm_ && world_ > 1) user_aligned_ = all_ranks_agree_(user_aligned_);
+      info_.aligned_fill = unnz > 0 ? (double)slots / (double)unnz : 0.0;
+    }
+    if (opt_.format == 1 && !tiles_ && !user_aligned_ && opt_.form.sell_sigma != 0 && n > 64 && (opt_.form.sell_sigma > 0 || stencil_line(spec_) == 0)) {
       // SELL-C-sigma (int32 columns): the windows never mix interior and boundary slices (auto: not
       // for a detected grid stencil, whose rows stay in grid order for the line / plane carry)
       const int64_t sig = opt_.form.sell_sigma > 1 ? (opt_.form.sell_sigma + 63) / 64 * 64 : 4096;
@@ -237,12 +303,23 @@ void GpuCgSolver::setup() {
     slice_ptr_.allocate(ns + 1, "A");
     // SELL-64/aligned: the same decision on every rank (from the spec, not from this rank's rows),
     // since it implies the split pass and with it the ghost vectors exchanged
-    aligned_ = spec_.kind == ProblemKind::RandomSPD && spec_.spread > 0 && !spec_.scramble && opt_.recurrence == 1 &&
-               opt_.form.pmat != 0 && opt_.form.sell_aligned != 0 &&
-               (opt_.form.sell_aligned == 1 || randspd_aligned_fill(spec_) <= 1.6);
-    if (aligned_) kern::randspd_aligned_widths(spec_, L_.row_begin, n, slice_ptr_.get(), s0_);
-    else kern::sell_slice_widths(rp64.get(), n, slice_ptr_.get(), s0_);
-    {
+    aligned_ = (spec_.kind == ProblemKind::RandomSPD && spec_.spread > 0 && !spec_.scramble && opt_.recurrence == 1 &&
+                opt_.form.pmat != 0 && opt_.form.sell_aligned != 0 &&
+                (opt_.form.sell_aligned == 1 || randspd_aligned_fill(spec_) <= 1.6)) ||
+               user_aligned_;
+    std::vector<int64_t> h_sp;
+    std::vector<int32_t> h_so;
+    std::vector<double> h_sv;
+    if (user_aligned_) {  // per-slice offset unions, built on the host from the user's rows
+      aligned_unions(user, L_.own_off, true, &h_sp, &h_so, &h_sv);
+      MCG_HIP(hipMemcpy(slice_ptr_.get(), h_sp.data(), (ns + 1) * sizeof(int64_t), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(A)");
+    } else if (aligned_) {
+      kern::randspd_aligned_widths(spec_, L_.row_begin, n, slice_ptr_.get(), s0_);
+    } else {
+      kern::sell_slice_widths(rp64.get(), n, slice_ptr_.get(), s0_);
+    }
+    if (!user_aligned_) {  // widths -> slot offsets (the host-built unions come scanned)
       DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ns), "A");
       kern::scan_inclusive_i64(slice_ptr_.get() + 1, ns, tmp.get(), s0_);
       MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
@@ -258,7 +335,14 @@ void GpuCgSolver::setup() {
     } else if (d16_) dcols_.allocate(total, "A", 16);
     else cols_.allocate(total, "A", 8);
     vals_.allocate(total, "A", 8);
-    if (aligned_) {
+    if (user_aligned_) {
+      if (!h_so.empty()) {
+        MCG_HIP(hipMemcpy(soffs_.get(), h_so.data(), h_so.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(A)");
+        MCG_HIP(hipMemcpy(vals_.get(), h_sv.data(), h_sv.size() * sizeof(double), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(A)");
+      }
+    } else if (aligned_) {
       kern::randspd_fill_aligned(spec_, L_.row_begin, n, rp64.get(), slice_ptr_.get(), soffs_.get(), vals_.get(),
                                  s0_);
       MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
@@ -603,6 +687,7 @@ void GpuCgSolver::setup() {
           break;
         }
       }
+      if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
     }
     if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, ar3_ ? info_.ar3_kw : 0,
                                   ar3_ ? carry_lo2_ : 0, s0_) == 0) {
@@ -632,6 +717,7 @@ void GpuCgSolver::setup() {
         break;
       }
     if (g == 0) g = g_all_;
+    if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
     for (int gg = g; gg >= 1 && !all_lean(gg); gg /= 2) g = gg / 2;
     if (g >= 1 && all_lean(g)) {
       lean_only_ = true;

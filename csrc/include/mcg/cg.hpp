@@ -61,6 +61,7 @@ struct PassForm {
                              // 3 / 4 = as 1 / 2, the waiters polling a step flag instead of the arrival counter
   int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
   int tile_pace_slack = 1;   // tiles, tile_pace 2 / 4: a workgroup waits for all but this many eighths of its group
+  int tile_prefetch = 0;     // tiles: each workgroup touches its share of the next segment before the pacing wait
   int tile_pace_sleep = 8;   // tiles: s_sleep units (64 clocks each) between two polls of a waiting workgroup
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
@@ -84,6 +85,10 @@ struct PassForm {
   int dia_uniform = -1;      // dia4 carry: slices whose 64 rows share one value-index pattern take a lean loop with the
                              // values in scalar registers and no codes streamed (the 2-D three-term pass over runs
                              // of such lines; bitwise the same sums); -1 = auto (on), 0 = off
+  int lean_depth = 0;        // 2-D lean-only passes: operand prefetch depth in lines (0 = auto: 3; 4 and 6 build with
+                             // 3 / 2 waves per SIMD for the registers)
+  int lean_bpc = 0;          // 2-D lean-only passes: blocks per CU of the grid (0 = auto: the largest of 16 / 8 / 4
+                             // whose runs keep >= 64 lines)
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
                              // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
                              // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)

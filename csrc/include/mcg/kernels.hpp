@@ -373,6 +373,8 @@ struct TilesDev {
                              // poll the flag (an L2-resident line) instead of the hot arrival counter
   int pace_lag = 0;          // a workgroup may start segment s + pace_lag before its group finished segment s
   int pace_sleep = 8;        // s_sleep units (64 clocks) between two polls
+  int prefetch = 0;          // 1: touch the next segment's lines before the pacing wait (kernel comment)
+  int64_t ext_len = 0;       // length of p (the last segment may be short)
 };
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
 int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)

@@ -68,7 +68,8 @@ struct SolverInfo {
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
-  bool diav = false;     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
+  bool diav = false;
+  double aligned_fill = 0.0;  // user matrices: SELL-64/aligned slots per nonzero of the per-slice offset unions     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
   double dia_uniform = 0.0;  // dia4 slices whose 64 rows share one value pattern (no codes streamed; PassForm::dia_uniform)
   bool lean_only = false;    // every run of the three-term carry takes the lean step (lean-only kernels)
@@ -182,6 +183,7 @@ class GpuCgSolver {
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
   DeviceBuffer<int32_t> soffs_;   // SELL-64/aligned per-slot column offsets
   bool aligned_ = false;
+  bool user_aligned_ = false;  // SELL-64/aligned from a user matrix's per-slice offset unions (host-built)
   DeviceBuffer<int32_t> lslots_;  // SELL-64/aligned + all-gather: per slice the own-block slot run {a, b}
   bool ag_overlap_ = false;
   int ndict_ = 0;
@@ -207,6 +209,8 @@ class GpuCgSolver {
     t.pace_flag = opt_.form.tile_pace >= 3 ? 1 : 0;
     t.pace_lag = std::max(0, opt_.form.tile_pace_lag);
     t.pace_sleep = std::max(1, std::min(64, opt_.form.tile_pace_sleep));
+    t.prefetch = opt_.form.tile_prefetch > 0 ? 1 : 0;
+    t.ext_len = L_.ext_len;
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)

@@ -217,9 +217,12 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(tile_seg_log2)
       MCG_FORM_PROP(tile_pace)
       MCG_FORM_PROP(carry_vc)
+      MCG_FORM_PROP(lean_depth)
+      MCG_FORM_PROP(lean_bpc)
       MCG_FORM_PROP(tile_pace_lag)
       MCG_FORM_PROP(tile_pace_slack)
       MCG_FORM_PROP(tile_pace_sleep)
+      MCG_FORM_PROP(tile_prefetch)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       MCG_FORM_PROP(pmat)
@@ -437,6 +440,7 @@ PYBIND11_MODULE(_C, m) {
         d["xcd_map"] = i.xcd_map;
         d["dia4"] = i.dia4;
         d["diav"] = i.diav;
+        d["aligned_fill"] = i.aligned_fill;
         d["p3"] = i.p3;
         d["dia_uniform"] = i.dia_uniform;
         d["lean_only"] = i.lean_only;

