@@ -104,9 +104,10 @@ def parse_args(argv=None):
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
     ap.add_argument("--delay-comm", default="",
-                    help="with --sim-world: AR_US,HALO_US -- every all-reduce / halo (or all-gather) exchange of the "
-                         "rehearsed rank costs a device-side delay of that many microseconds (DelayComm) instead "
-                         "of nothing (NullComm): the collectives priced at an assumed latency / volume")
+                    help="with --sim-world: AR_US,HALO_US[,copy] -- every all-reduce / halo (or all-gather) exchange "
+                         "of the rehearsed rank costs a device-side delay of that many microseconds (DelayComm) "
+                         "instead of nothing (NullComm); 'copy': the halo is real copy-engine traffic of the "
+                         "layout's message sizes (a CU-free transport's timing)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="timing rehearsal: run rank --sim-rank of a P-rank job alone on this GPU (its rows, "
                          "ghost layout, interior/boundary launches, graphs) with collectives that move nothing")
@@ -175,8 +176,9 @@ def _run_rank(args, out_fd) -> int:
     sim = args.sim_world > 1 and env.world == 1
     if sim:  # per-rank timing rehearsal (not a P-rank solve: see --sim-world)
         if args.delay_comm:
-            ar_us, halo_us = (float(v) for v in args.delay_comm.split(","))
-            comm = mcg.native().DelayComm(args.sim_rank, args.sim_world, ar_us, halo_us, False)
+            f = args.delay_comm.split(",")
+            comm = mcg.native().DelayComm(args.sim_rank, args.sim_world, float(f[0]), float(f[1]), False,
+                                          len(f) > 2 and f[2] == "copy")
         else:
             comm = mcg.native().NullComm(args.sim_rank, args.sim_world)
 

@@ -139,6 +139,11 @@ def recipes(a) -> dict:
                             ("s18_lag1", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_lag=1"]),
                             ("s18_again", ["tile_pace=4", "tile_seg_log2=18"]))
         ],
+        # r4: the pacing beside other kernels (fat = RCCL's register footprint) and the collision test
+        "pacecorun": [
+            ("probe", 400, f"{PY} -u bench/pace_corun.py --set tile_pace=4 --set tile_seg_log2=18"),
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'colliding or tiles'"),
+        ],
         # r4: next-segment L2 prefetch during the pacing wait
         "c5pf": [
             (tag, 400, bench(f"{c5} --steps 6 --warmup 2 {sets(kv)}"))
@@ -218,6 +223,18 @@ def recipes(a) -> dict:
                                       f"--set lean_depth={d} --set lean_bpc={b}"))
             for d in (3, 4, 6) for b in (2, 4, 8)
         ] + [("auto_again", 200, bench("--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify"))],
+        # r4: CU-free halo (copy engines) hidden behind the interior band of the pass (halo_hide), at
+        # P = 8 shares with a 10 us all-reduce; the halo as copy-engine traffic or as an RCCL-like spin
+        "hide": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_multirank.py -k 'halo_hide'"),
+        ] + [
+            (f"{g}_{tag}", 200, bench(f"{'--grid ' + str(g) if g != 512 else '--problem poisson3d --grid 512'} "
+                                      f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 "
+                                      f"--comm dual --delay-comm {dc} {hh}"))
+            for g in (16384, 4096)
+            for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
+                                ("spin20_ahead", "10,20", ""), ("null", "0,0", ""))
+        ],
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),

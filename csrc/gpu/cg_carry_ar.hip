@@ -180,6 +180,35 @@ __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat,
   return go && (col != 0 || ((WB >> 28) & 1u)) && (col != ss - 1 || ((WB >> 29) & 1u));
 }
 
+// The 2-D carry's job decomposition: job -> (slice column, run of lines [l0, l1)) for a launch of nw
+// waves over nl lines of ss slices (TileRanges::band: the whole rank, the interior band, or the
+// band_h lines at each end).  Returns the number of jobs.
+__host__ __device__ __forceinline__ int64_t carry_jobs(int64_t nw, int64_t ss, int64_t nl, int band, int64_t h,
+                                                       int64_t& runs, int64_t& chunk) {
+  if (band == 2) {
+    runs = 2;
+    chunk = h;
+    return 2 * ss;
+  }
+  const int64_t lines = band == 1 ? nl - 2 * h : nl;
+  runs = nw > ss ? nw / ss : 1;
+  chunk = (lines + runs - 1) / runs;
+  return ss * runs;
+}
+__host__ __device__ __forceinline__ void carry_run(int64_t job, int64_t ss, int64_t nl, int band, int64_t h,
+                                                   int64_t chunk, int64_t& col, int64_t& l0, int64_t& l1) {
+  col = job % ss;
+  const int64_t r = job / ss;
+  if (band == 2) {
+    l0 = r == 0 ? 0 : nl - h;
+    l1 = l0 + h;
+    return;
+  }
+  const int64_t lo = band == 1 ? h : 0, hi = band == 1 ? nl - h : nl;
+  l0 = lo + r * chunk;
+  l1 = l0 + chunk < hi ? l0 + chunk : hi;
+}
+
 // per-slice metadata for the carry's codes loads: first slot / 64 (28 bits) | width << 28
 __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, uint32_t* __restrict__ meta) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
@@ -236,8 +265,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   const int64_t nw = nb * kWaves;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t gw = lb * kWaves + wv;
-  const int64_t runs = nw > SS ? nw / SS : 1;
-  const int64_t chunk = (nl + runs - 1) / runs;
+  int64_t runs, chunk;
+  const int64_t njobs = carry_jobs(nw, SS, nl, tr.band, tr.band_h, runs, chunk);
   const int32_t ext32 = (int32_t)v.ext_len;
   constexpr bool ntl = false;  // plain loads (non-temporal measured slower: 281 vs 302 it/s 2-D)
   const double* __restrict__ eo = v.ape_old;
@@ -297,9 +326,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       return sum;
     }
   };
-  for (int64_t job = gw; job < SS * runs; job += nw) {
-    const int64_t col = job % SS, l0 = (job / SS) * chunk;
-    const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
+  for (int64_t job = gw; job < njobs; job += nw) {
+    int64_t col, l0, l1;
+    carry_run(job, SS, nl, tr.band, tr.band_h, chunk, col, l0, l1);
     if (l0 >= l1) continue;
     const int64_t sl0 = l0 * SS + col;
     const int32_t e0 = (int32_t)(own + sl0 * 64);
@@ -1720,32 +1749,30 @@ __global__ __launch_bounds__(256) void k_dia_runs(uint64_t* __restrict__ dpat, i
 // kw = 0, one wave per job; k_cg_carry_ar3: kw waves per job, their slice columns)
 __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
                                                     int64_t ext_len, int64_t grid, int kw, int64_t ln,
+                                                    int band, int64_t band_h,
                                                     unsigned long long* __restrict__ fails) {
   const int64_t waves = kw > 0 ? kw : 1;
-  int64_t jobs, runs;
+  int64_t jobs, runs, chunk;
   if (kw == 0) {
-    const int64_t nw = grid * kWaves;
-    runs = nw > ss ? nw / ss : 1;
-    jobs = ss * runs;
+    jobs = carry_jobs(grid * kWaves, ss, nl, band, band_h, runs, chunk);
   } else {
     const int64_t jpr = (ln / kw) * (ln / 64);
     runs = grid > jpr ? grid / jpr : 1;
     jobs = jpr * runs;
+    chunk = (nl + runs - 1) / runs;
   }
-  const int64_t chunk = (nl + runs - 1) / runs;
   unsigned long long f = 0;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < jobs * waves; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t job = t / waves, wv = t % waves;
-    int64_t col, l0;
+    int64_t col, l0, l1;
     if (kw == 0) {
-      col = job % ss;
-      l0 = (job / ss) * chunk;
+      carry_run(job, ss, nl, band, band_h, chunk, col, l0, l1);
     } else {
       const int64_t jpr = (ln / kw) * (ln / 64), G = ln / 64, q = job % jpr;
       col = ((q / G) * kw + wv) * G + q % G;
       l0 = (job / jpr) * chunk;
+      l1 = l0 + chunk < nl ? l0 + chunk : nl;
     }
-    const int64_t l1 = l0 + chunk < nl ? l0 + chunk : nl;
     if (l0 >= l1) continue;
     uint32_t a, b, c;
     // past 2^29 the BIG kernels re-base: per run (2-D), along the run (3-D)
@@ -1757,14 +1784,14 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
 }  // namespace
 
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream) {
+                            int32_t ln, hipStream_t stream, int band, int band_h) {
   MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && (kw == 0 || (ln % 64 == 0 && ln % kw == 0)),
             "lean check: bad launch geometry");
   unsigned long long* f = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&f), sizeof(unsigned long long), stream), "device malloc failed(lean)");
   MCG_HIP(hipMemsetAsync(f, 0, sizeof(unsigned long long), stream), "device memset failed");
   hipLaunchKernelGGL(k_lean_check, dim3(64), dim3(256), 0, stream, dpat, ss, nl, ext_len, (int64_t)grid, kw,
-                     (int64_t)ln, f);
+                     (int64_t)ln, band, (int64_t)band_h, f);
   MCG_HIP(hipGetLastError(), "kernel launch failed(lean check)");
   unsigned long long h = 0;
   MCG_HIP(hipMemcpyAsync(&h, f, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
@@ -1884,6 +1911,8 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
+  MCG_CHECK(tr.band == 0 || (!final_mode && lean && tr.band_h >= 3 && 2 * tr.band_h + 3 <= tr.nt0 / tr.strip),
+            "Ap-recomputing carry: a line band needs the lean kernels and >= 3 lines per band");
   MCG_CHECK((cm == 2 || cm == 4 || cm == 5) && param >= 4 && param <= 5 && (cm == 5 || S.dict != nullptr),
             "Ap-recomputing carry: SELL-64/c8, /c4, /dia4 or /diav rows of at most 5 entries");
   MCG_CHECK(cm != 4 || (S.dia4 != nullptr && S.dvals != nullptr), "Ap-recomputing carry: dia4 codes missing");
@@ -1987,6 +2016,7 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
                   int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3,
                   bool lean) {
   if (tr.ntiles == 0 || grid == 0) return;
+  MCG_CHECK(tr.band == 0, "3-D plane carry: no line bands");
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0 && ln % 64 == 0 &&
                 (int64_t)ln * ln == (int64_t)tr.strip * 64 && (kw == 4 || kw == 8 || kw == 16) && ln % kw == 0,
             "3-D Ap-recomputing carry: one launch over the rank's whole planes, N a multiple of 64 and of the block");

@@ -13,8 +13,12 @@
 // Storage (12 B per nonzero, like CSR): tile (b, g) = the nonzeros of row block b whose column is
 // in segment g, a flat list of (row in block << 22 | column in segment) and the value;
 // tptr[b * G + g] .. tptr[b * G + g + 1].  A wave spreads its tile over its 64 lanes and adds every
-// product into the row's LDS slot (ds_add_f64); the wave owns those slots, so the additions happen
-// in program order (deterministic).
+// product into the row's LDS slot (ds_add_f64); the wave owns those slots, so no other wave's adds
+// interleave with its own, batch after batch in program order.  Inside ONE batch two lanes can hold
+// entries of the same row; the order in which one ds_add_f64 applies same-address lanes is a
+// hardware behaviour, not an architectural guarantee.  It is observed fixed on MI355X (repeated
+// solves, graph and eager, bit for bit: tests/test_gpu_irregular.py, a tile built to collide), so
+// the results are run-to-run bitwise on this hardware, not by construction.
 //
 // Pacing: waves left alone drift apart by a few segments within a sweep (a dependent load or a
 // ragged tile end is enough), the L2 then holds none of the segments in flight and the hit rate
@@ -233,8 +237,8 @@ struct CsrSrc {  // a user matrix's rows on the device (local CSR, ext columns)
 };
 
 // FILL = false: tptr[b * G + g + 1] = entries of tile (b, g); FILL = true: write the tiles (tptr =
-// exclusive offsets).  Lanes take rows rr = lane, lane + 64, ... of the block in lockstep; within a
-// wave the LDS atomics return their old values in a fixed order, so the fill is deterministic.
+// exclusive offsets).  Lanes take rows rr = lane, lane + 64, ... of the block in lockstep; the order
+// of one LDS atomic's same-address lanes (observed fixed, as above) orders a batch's appends.
 template <bool FILL, class Src>
 __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, int seg_shift, int64_t* __restrict__ tptr,
                                                     uint32_t* __restrict__ idx, double* __restrict__ vals) {

@@ -108,8 +108,20 @@ void DelayComm::allreduce_sum(double*, size_t, hipStream_t stream) {
   if (ar_us_ > 0) kern::spin(nullptr, ar_us_, fat_, 1, stream);
 }
 
-void DelayComm::halo_exchange(const LocalLayout& L, double* const*, int, hipStream_t stream, const int*) {
-  if (halo_us_ > 0 && L.has_halo()) kern::spin(nullptr, halo_us_, fat_, 1, stream);
+void DelayComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                              const int* widths) {
+  if (!L.has_halo()) return;
+  if (copy_) {  // the messages' bytes through the copy engines (source: the rank's own first rows)
+    for (int v = 0; v < nvec; ++v) {
+      const int64_t w = widths ? widths[v] : 1;
+      for (const HaloRange& h : L.recvs)
+        MCG_HIP(hipMemcpyAsync(ext_vecs[v] + w * L.ext_index(h.gbegin), ext_vecs[v] + w * L.own_off,
+                               w * h.count * sizeof(double), hipMemcpyDeviceToDeviceNoCU, stream),
+                "halo copy failed");
+    }
+    return;
+  }
+  if (halo_us_ > 0) kern::spin(nullptr, halo_us_, fat_, 1, stream);
 }
 
 int Comm::count() const {

@@ -7,7 +7,8 @@
 //     barrier
 //     wait every ev_copy[p][q]; sum staging[p][0..P) in rank order -> buf; record ev_done[p][rank]
 //   halo: record ev_pre[rank]; publish (vecs, layout); barrier
-//     for every recv range: wait ev_pre[peer]; D2D copy from the peer's owned block
+//     for every recv range: wait ev_pre[peer]; D2D copy from the peer's owned block on the copy
+//     engines (hipMemcpyDeviceToDeviceNoCU: the CU-free transport a real peer copy would use)
 //     record ev_post[rank]; barrier; wait every ev_post[q] (no rank overwrites a
 //     source block before every reader has copied it — RCCL send semantics)
 // A rank re-records an event only after the next barrier, by which time every
@@ -112,7 +113,7 @@ void LocalComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
       const int64_t w = widths ? widths[v] : 1;
       MCG_HIP(hipMemcpyAsync(ext_vecs[v] + w * L.ext_index(h.gbegin),
                              g.halo_vecs_[h.peer][v] + w * Lp.ext_index(h.gbegin), w * h.count * sizeof(double),
-                             hipMemcpyDeviceToDevice, stream),
+                             hipMemcpyDeviceToDeviceNoCU, stream),
               "local halo copy failed");
     }
   }

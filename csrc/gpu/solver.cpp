@@ -219,7 +219,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
   }
   const SellDev S = sell_view();
   if (ar_) {
-    MCG_CHECK(which == 0, "Ap-recomputing carry: one launch per iteration");
+    MCG_CHECK(which == 0 || hide_, "Ap-recomputing carry: one launch per iteration (halo_hide: two bands)");
     v.ra_old = nullptr;
     v.ra_new = nullptr;
     v.ap_old = apx_[(k + 1) & 1].get();
@@ -378,7 +378,22 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
   trace::Range tr_("mcg.iteration.single_reduction");
   int np = g_all_;
   const bool fr = fused_red_;
-  if (halo_ahead_) {
+  if (hide_) {
+    // halo_hide: the interior band reads no ghost line, so it runs while this iteration's ghosts land
+    // (copy engines: no CU is taken from the pass); then the lines at both ends of the rank, whose
+    // last arriver finishes the reduction; then the next iteration's ghosts -- this pass's outputs,
+    // final now -- on the side stream next to the all-reduce and the next interior band
+    enqueue_f1_(k, 1, 0, fr);
+    ensure_ghosts_(k);
+    enqueue_f1_(k, 2, 0, fr);
+    np = g_int_ + g_bnd_;
+    MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
+    MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
+    enqueue_halo_f1_(k + 1, s1_);
+    MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
+    ghosts_for_ = k + 1;
+    halo_pending_ = true;
+  } else if (halo_ahead_) {
     ensure_ghosts_(k);
     enqueue_f1_(k, 0, 0, fr);  // every owned row in one pass (the line-carry pass at P > 1 too)
     // the next iteration's ghosts are this pass's outputs, final now: exchange them on the side

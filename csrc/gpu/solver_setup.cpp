@@ -725,6 +725,41 @@ void GpuCgSolver::setup() {
     }
   }
   info_.lean_only = lean_only_;
+  // halo_hide: the lean 2-D pass split into the interior band (reads no ghost line; it runs while a
+  // copy-engine halo lands) and the kHideLines lines at each end of the rank (after the halo)
+  if (opt_.form.halo_hide == 1 && halo_ahead_ && comm_->halo_cu_free() && lean_only_ && ar_ && !ar3_ && p3_ &&
+      n > 0 && tr_all_.strip > 0) {
+    constexpr int kHideLines = 4;
+    const int64_t ss = tr_all_.strip, nlines = (n + 63) / 64 / ss;
+    TileRanges ti = tr_all_, tb = tr_all_;
+    ti.band = 1;
+    tb.band = 2;
+    ti.band_h = tb.band_h = kHideLines;
+    // band 1 on the full grid (rounded to whole reduction groups, as the split launches are below: the
+    // job decomposition depends on the grid), band 2 one wave per (end, slice column)
+    const int gi = (g_all_ + kern::kRedGroup - 1) / kern::kRedGroup * kern::kRedGroup;
+    const int gb = (int)((2 * ss + 3) / 4);
+    bool ok = nlines >= 2 * kHideLines + 3;
+    if (ok && dpat_.get() != nullptr)
+      ok = kern::carry_lean_failures(dpat_.get(), ss, nlines, L_.ext_len, gi, 0, 0, s0_, 1, kHideLines) == 0 &&
+           kern::carry_lean_failures(dpat_.get(), ss, nlines, L_.ext_len, gb, 0, 0, s0_, 2, kHideLines) == 0;
+    if (ok && diav_) {  // every interior-band run >= 3 lines
+      const int64_t nw = (int64_t)gi * 4, runs = nw > ss ? nw / ss : 1, lines = nlines - 2 * kHideLines;
+      const int64_t chunk = (lines + runs - 1) / runs;
+      for (int64_t r = 0; r < runs && ok; ++r) {
+        const int64_t a = r * chunk, b = std::min(lines, a + chunk);
+        if (a < lines && b - a < 3) ok = false;
+      }
+    }
+    if (ok) {
+      hide_ = true;
+      tr_int_ = ti;
+      tr_bnd_ = tb;
+      g_int_ = gi;
+      g_bnd_ = gb;
+    }
+  }
+  info_.halo_hide = hide_;
   if (ar_ && !info_.dia4 && !diav_ && n > 0) {
     const int64_t ns = (n + 63) / 64;
     int64_t slots = 0;
@@ -738,7 +773,7 @@ void GpuCgSolver::setup() {
   g_b_ = kern::grid_for((n + 1) / 2, 256, 4);  // residual update / dot kernels: 1024 blocks (best measured)
   info_.grid_a = g_all_;
   info_.grid_b = g_b_;
-  const bool split = split_;
+  const bool split = split_ || hide_;
   fused_red_ = (opt_.recurrence == 1 && opt_.form.fused_reduce != 0) || opt_.recurrence == 2;
   auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
   // the boundary launch's partials start on a reduction-group boundary: round the interior grid up

@@ -92,6 +92,10 @@ struct PassForm {
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
                              // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
                              // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)
+  int halo_hide = 0;         // 2-D lean line carry at P > 1 with a CU-free halo (Communicator::halo_cu_free: copy
+                             // engines): the pass runs as the interior band (no ghost read) while the ghosts
+                             // arrive, then the band_h = 4 lines at each end of the rank; the halo of the next
+                             // iteration is issued on the side stream right after that second launch. 1 = on
   int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
                              // right after pass k wrote it (side stream, next to the all-reduce) and run one
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's

@@ -67,6 +67,9 @@ class Communicator {
   // true: halo and all-reduce share one communicator, so the solver must issue them in one stream
   // order (no side-stream halo; CgOptions::overlap is forced off)
   virtual bool serialized() const { return false; }
+  // true: the halo moves its bytes with copy engines (no compute units), so it can run while a pass
+  // holds every CU (CgOptions::form.halo_hide splits the pass around it)
+  virtual bool halo_cu_free() const { return false; }
 };
 
 class Comm final : public Communicator {
@@ -126,18 +129,22 @@ class NullComm final : public Communicator {
 // wave cannot be placed next to a resident pass, the thin one (6 VGPRs) can.
 class DelayComm final : public Communicator {
  public:
-  DelayComm(int rank, int world, double allreduce_us, double halo_us, bool fat = false)
-      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us), fat_(fat) {}
+  // copy_halo: the halo is real copy-engine traffic of the layout's message sizes (each receive range
+  // copied from this rank's own rows with hipMemcpyDeviceToDeviceNoCU: a timing stand-in for the
+  // peer-to-peer copies, the ghosts get wrong values) instead of a spin
+  DelayComm(int rank, int world, double allreduce_us, double halo_us, bool fat = false, bool copy_halo = false)
+      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us), fat_(fat), copy_(copy_halo) {}
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   void allreduce_sum(double*, size_t, hipStream_t stream) override;
   void halo_exchange(const LocalLayout& L, double* const*, int, hipStream_t stream, const int* = nullptr) override;
   bool moves_data() const override { return false; }
+  bool halo_cu_free() const override { return copy_; }
 
  private:
   int rank_, world_;
   double ar_us_, halo_us_;
-  bool fat_;
+  bool fat_, copy_;
 };
 
 // Shared state of P in-process ranks on one device.
@@ -174,6 +181,7 @@ class LocalComm final : public Communicator {
   void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
                      const int* widths = nullptr) override;
   bool graph_capturable() const override { return false; }
+  bool halo_cu_free() const override { return true; }  // hipMemcpyDeviceToDeviceNoCU (SDMA engines)
 
  private:
   std::shared_ptr<LocalGroup> group_;

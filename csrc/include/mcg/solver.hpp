@@ -68,6 +68,7 @@ struct SolverInfo {
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
+  bool halo_hide = false;  // PassForm::halo_hide: the pass split around a copy-engine halo
   bool diav = false;
   double aligned_fill = 0.0;  // user matrices: SELL-64/aligned slots per nonzero of the per-slice offset unions     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
@@ -152,6 +153,7 @@ class GpuCgSolver {
   bool prefetch_halo_ = false;  // single-reduction form: next iteration's halo right after the boundary pass
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
+  bool hide_ = false;           // PassForm::halo_hide in effect: interior band || copy-engine halo, then the ends
   bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)

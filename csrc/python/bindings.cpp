@@ -219,6 +219,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(carry_vc)
       MCG_FORM_PROP(lean_depth)
       MCG_FORM_PROP(lean_bpc)
+      MCG_FORM_PROP(halo_hide)
       MCG_FORM_PROP(tile_pace_lag)
       MCG_FORM_PROP(tile_pace_slack)
       MCG_FORM_PROP(tile_pace_sleep)
@@ -353,8 +354,9 @@ PYBIND11_MODULE(_C, m) {
   py::class_<DelayComm, std::shared_ptr<DelayComm>>(m, "DelayComm",
                                                     "one rank of a P-rank run whose all-reduce / halo cost a fixed "
                                                     "device-side delay and move nothing (latency rehearsal)")
-      .def(py::init<int, int, double, double, bool>(), py::arg("rank"), py::arg("world"), py::arg("allreduce_us"),
-           py::arg("halo_us") = 0.0, py::arg("fat") = false);
+      .def(py::init<int, int, double, double, bool, bool>(), py::arg("rank"), py::arg("world"), py::arg("allreduce_us"),
+           py::arg("halo_us") = 0.0, py::arg("fat") = false, py::arg("copy_halo") = false,
+           "copy_halo: the halo as copy-engine (NoCU) copies of the layout's message sizes instead of a spin");
 
   py::class_<GpuCgSolver>(m, "Solver")
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<Comm> comm) {
@@ -440,6 +442,7 @@ PYBIND11_MODULE(_C, m) {
         d["xcd_map"] = i.xcd_map;
         d["dia4"] = i.dia4;
         d["diav"] = i.diav;
+        d["halo_hide"] = i.halo_hide;
         d["aligned_fill"] = i.aligned_fill;
         d["p3"] = i.p3;
         d["dia_uniform"] = i.dia_uniform;
@@ -477,6 +480,7 @@ PYBIND11_MODULE(_C, m) {
       d["carry"] = rr.carry;
       d["ap_recompute"] = rr.ap_recompute;
       d["lean_only"] = rr.lean_only;
+      d["halo_hide"] = rr.halo_hide;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;
       py::dict ph;

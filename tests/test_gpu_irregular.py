@@ -305,3 +305,31 @@ def test_tiles_local_ranks_p8_agrees_with_p1(mcg):
     assert abs(r1 - r8) <= 1e-13 * r1
     np.testing.assert_allclose(eight["x"], one["x"], rtol=1e-13, atol=1e-15 * np.abs(one["x"]).max())
     assert all(abs(r["true_rnorm"] - r8) <= 1e-9 * r8 for r in eight["ranks"])
+
+
+def test_tiles_row_colliding_batches_run_to_run_bitwise(mcg):
+    """lanes of one ds_add_f64 batch may target the same row's LDS sum.  Ten dense
+    rows with 300 entries each inside one 4096-column segment force it (every 64-entry batch of their
+    tile holds at most 10 distinct rows).  The order of same-address lanes inside one LDS atomic is a
+    hardware behaviour, not an architectural guarantee; on MI355X it is observed fixed: repeated
+    solves, graph and eager, are bit for bit equal (cg_tiles.hip documents exactly this)."""
+    import scipy.sparse as sp
+
+    n = 20000
+    rng = np.random.default_rng(11)
+    rows = [np.repeat(np.arange(n), 4), np.repeat(np.arange(10), 300)]
+    cols = [rng.integers(0, n, 4 * n), rng.integers(0, 4096, 3000)]
+    B = sp.csr_matrix((rng.random(4 * n + 3000), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    B = B + B.T
+    A = (B + sp.diags(np.asarray(abs(B).sum(axis=1)).ravel() + 1.0)).tocsr()
+    assert A[:10, :4096].getnnz(axis=1).min() > 64
+    prob = mcg.csr_problem(A, b=rng.random(n))
+    outs = []
+    for graph in (True, True, False):
+        s = mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tol=-1.0, maxit=25, tile_seg_log2=12,
+                         use_graph=graph)
+        assert s.info["tiles"]
+        outs.append(s.solve())
+    for o in outs[1:]:
+        assert o["rnorm"] == outs[0]["rnorm"]
+        np.testing.assert_array_equal(o["x_local"], outs[0]["x_local"])
