@@ -103,6 +103,10 @@ def parse_args(argv=None):
                          "communicators in flight at once)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
+    ap.add_argument("--halo-transport", default="rccl", choices=["rccl", "sdma"],
+                    help="sdma: the halo on copy engines (PeerHaloComm: the neighbours' buffers mapped through IPC, "
+                         "flags by stream memory operations; all-reduce on RCCL) -- CU-free, so halo_hide can "
+                         "run the interior band beside it")
     ap.add_argument("--delay-comm", default="",
                     help="with --sim-world: AR_US,HALO_US[,copy] -- every all-reduce / halo (or all-gather) exchange "
                          "of the rehearsed rank costs a device-side delay of that many microseconds (DelayComm) "
@@ -203,9 +207,15 @@ def _run_rank(args, out_fd) -> int:
             raise SystemExit(f"bench.py: unknown option {k!r}")
         setattr(opts, k, type(getattr(opts, k))(v))
     t_setup = time.perf_counter()
+    sdma = args.halo_transport == "sdma" and comm is not None and not sim
+    base_comm = comm  # RCCL's (or the rehearsal's) communicator: the count, the all-reduce
+    if sdma:
+        comm = pdist.peer_halo(comm, env)
     solver = (C.Solver(spec.native(), opts, args.sim_rank, args.sim_world, comm) if sim
               else C.Solver(spec.native(), opts, env.rank, env.world, comm))
     solver.setup()
+    if sdma:
+        pdist.attach_peer_halo(comm, env)
     solver.reset()
     setup_s = time.perf_counter() - t_setup
 
@@ -323,11 +333,13 @@ def _run_rank(args, out_fd) -> int:
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
                 "comm": args.comm,
+                **({"halo_transport": "sdma (copy engines, IPC)", "halo_hide": bool(info.get("halo_hide"))}
+                   if sdma else {}),
                 "launch": route,
                 **({"reserve_cus": opts.reserve_cus} if opts.reserve_cus else {}),
             },
             "check": {"device_iterations": res["iterations"], "rnorm": res["rnorm"], "ok": ok,
-                      "comm_world": comm.count if (comm is not None and not sim and not rehearse) else 1,
+                      "comm_world": base_comm.count if (comm is not None and not sim and not rehearse) else 1,
                       "rccl": mcg.native().rccl_info(),
                       "graph_fallbacks": info.get("graph_fallbacks", 0),
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),

@@ -140,6 +140,9 @@ def recipes(a) -> dict:
                             ("s18_again", ["tile_pace=4", "tile_seg_log2=18"]))
         ],
         # r4: the pacing beside other kernels (fat = RCCL's register footprint) and the collision test
+        "useraligned": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'aligned'"),
+        ],
         "pacecorun": [
             ("probe", 400, f"{PY} -u bench/pace_corun.py --set tile_pace=4 --set tile_seg_log2=18"),
             ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'colliding or tiles'"),
@@ -223,6 +226,21 @@ def recipes(a) -> dict:
                                       f"--set lean_depth={d} --set lean_bpc={b}"))
             for d in (3, 4, 6) for b in (2, 4, 8)
         ] + [("auto_again", 200, bench("--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify"))],
+        # r4: stream memory operations (write / wait value) around a NoCU copy, eager and captured
+        "streamop": [
+            ("probe", 60, f"{PY} -c 'import torch, json, cuda_mpi_parallel_amd as m; torch.cuda.init(); "
+                          f"print(json.dumps(dict(m.native().kernels.streamop_probe())))'"),
+        ],
+        # r4: the copy-engine halo across processes (PeerHaloComm, IPC-mapped buffers), P ranks on one GPU
+        "peer": [
+            ("check2", 180, f"{PY} -u bench/peer_halo_check.py --world 2"),
+            ("check4", 180, f"{PY} -u bench/peer_halo_check.py --world 4 --n 512 --rounds 6"),
+        ] + [
+            (f"bench{w}_{t}", 300, f"{PY} -m torch.distributed.run --nnodes=1 --nproc-per-node {w} "
+                                   f"--master-addr 127.0.0.1 --master-port {29600 + w} bench.py --gpus {w} "
+                                   f"--rehearse-ranks --steps 200 --warmup 20 --phases 0 --halo-transport {t}")
+            for w in (2, 4) for t in ("rccl", "sdma")
+        ],
         # r4: CU-free halo (copy engines) hidden behind the interior band of the pass (halo_hide), at
         # P = 8 shares with a 10 us all-reduce; the halo as copy-engine traffic or as an RCCL-like spin
         "hide": [

@@ -1,0 +1,192 @@
+// PeerHaloComm: the CU-free halo transport (comm.hpp).  Ghost rows are pulled from the owners'
+// buffers with copy engines (hipMemcpyDeviceToDeviceNoCU), ordered by flags written and waited on
+// with stream memory operations; the all-reduce is delegated to the wrapped communicator.
+//
+// The reference has no communication at all (CUDACG.cu is one process on device 0, :87); this is
+// the north star's halo (the SpMV reads neighbours' p, CUDACG.cu:288), moved off the
+// compute units so it can run beside the resident pass (CgOptions::form.halo_hide).
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "mcg/check.hpp"
+#include "mcg/comm.hpp"
+#include "mcg/partition.hpp"
+
+namespace mcg {
+
+namespace {
+constexpr uint64_t kBlobMagic = 0x4D4347504852ull;  // "MCGPHR"
+struct Entry {  // one mapped allocation: this process's pointer, its IPC handle, the offset inside it
+  uint64_t ptr;
+  hipIpcMemHandle_t handle;
+  int64_t offset;
+};
+void put(std::string& s, const void* p, size_t n) { s.append(reinterpret_cast<const char*>(p), n); }
+template <class T>
+T get(const std::string& s, size_t& at) {
+  MCG_CHECK(at + sizeof(T) <= s.size(), "peer halo: truncated handle blob");
+  T v;
+  std::memcpy(&v, s.data() + at, sizeof(T));
+  at += sizeof(T);
+  return v;
+}
+Entry make_entry(void* p) {
+  Entry e{};
+  e.ptr = reinterpret_cast<uint64_t>(p);
+  void* base = nullptr;
+  size_t size = 0;
+  MCG_HIP(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t*>(&base), &size, p), "peer halo: address range failed");
+  e.offset = static_cast<char*>(p) - static_cast<char*>(base);
+  MCG_HIP(hipIpcGetMemHandle(&e.handle, base), "peer halo: IPC handle failed");
+  return e;
+}
+}  // namespace
+
+PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int world)
+    : inner_(std::move(inner)), rank_(rank), world_(world) {
+  MCG_CHECK(inner_ != nullptr && world >= 1 && rank >= 0 && rank < world, "peer halo: invalid rank / world");
+  MCG_HIP(hipMalloc(&flags_, 2 * world * sizeof(uint64_t)), "device malloc failed(peer halo flags)");
+  MCG_HIP(hipMemset(flags_, 0, 2 * world * sizeof(uint64_t)), "device memset failed");
+  peer_bufs_.assign(world, {});
+  peer_flags_.assign(world, nullptr);
+  peer_own_off_.assign(world, 0);
+  peer_row_begin_.assign(world, 0);
+}
+
+PeerHaloComm::~PeerHaloComm() {
+  for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+  if (flags_) (void)hipFree(flags_);
+}
+
+void PeerHaloComm::register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) {
+  bufs_ = bufs;
+  own_off_ = own_off;
+  row_begin_ = row_begin;
+  attached_ = false;
+}
+
+std::string PeerHaloComm::local_handles() const {
+  std::string s;
+  const uint64_t magic = kBlobMagic;
+  const int64_t pid = (int64_t)getpid(), nb = (int64_t)bufs_.size();
+  int dev = 0;
+  MCG_HIP(hipGetDevice(&dev), "get device failed");
+  const int64_t d64 = dev;
+  put(s, &magic, 8);
+  put(s, &pid, 8);
+  put(s, &d64, 8);
+  put(s, &nb, 8);
+  put(s, &own_off_, 8);
+  put(s, &row_begin_, 8);
+  const Entry f = make_entry(flags_);
+  put(s, &f, sizeof(Entry));
+  for (double* b : bufs_) {
+    MCG_CHECK(b != nullptr, "peer halo: null halo buffer");
+    const Entry e = make_entry(b);
+    put(s, &e, sizeof(Entry));
+  }
+  return s;
+}
+
+void PeerHaloComm::attach(const std::vector<std::string>& all) {
+  MCG_CHECK((int)all.size() == world_, "peer halo: one handle blob per rank");
+  const int64_t me = (int64_t)getpid();
+  int dev = 0;
+  MCG_HIP(hipGetDevice(&dev), "get device failed");
+  auto map = [&](const Entry& e, int64_t pid, int64_t pdev) -> void* {
+    if (pid == me) {  // the same process (threads, or one rank): plain pointers, peer access if needed
+      if (pdev != dev) {
+        const hipError_t r = hipDeviceEnablePeerAccess((int)pdev, 0);
+        if (r != hipSuccess && r != hipErrorPeerAccessAlreadyEnabled) MCG_HIP(r, "peer halo: peer access failed");
+        (void)hipGetLastError();
+      }
+      return reinterpret_cast<void*>(e.ptr);
+    }
+    void* base = nullptr;
+    MCG_HIP(hipIpcOpenMemHandle(&base, e.handle, hipIpcMemLazyEnablePeerAccess), "peer halo: IPC open failed");
+    opened_.push_back(base);
+    return static_cast<char*>(base) + e.offset;
+  };
+  for (int q = 0; q < world_; ++q) {
+    if (q == rank_) {
+      peer_flags_[q] = flags_;
+      peer_bufs_[q] = bufs_;
+      peer_own_off_[q] = own_off_;
+      peer_row_begin_[q] = row_begin_;
+      continue;
+    }
+    size_t at = 0;
+    const std::string& s = all[q];
+    MCG_CHECK(get<uint64_t>(s, at) == kBlobMagic, "peer halo: bad handle blob");
+    const int64_t pid = get<int64_t>(s, at), pdev = get<int64_t>(s, at), nb = get<int64_t>(s, at);
+    peer_own_off_[q] = get<int64_t>(s, at);
+    peer_row_begin_[q] = get<int64_t>(s, at);
+    MCG_CHECK(nb == (int64_t)bufs_.size(), "peer halo: ranks registered different buffer lists");
+    peer_flags_[q] = static_cast<uint64_t*>(map(get<Entry>(s, at), pid, pdev));
+    peer_bufs_[q].resize(nb);
+    for (int64_t i = 0; i < nb; ++i) peer_bufs_[q][i] = static_cast<double*>(map(get<Entry>(s, at), pid, pdev));
+  }
+  attached_ = true;
+}
+
+std::vector<uintptr_t> PeerHaloComm::peer_buffers(int q) const {
+  std::vector<uintptr_t> v;
+  for (double* p : peer_bufs_.at(q)) v.push_back(reinterpret_cast<uintptr_t>(p));
+  return v;
+}
+
+void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                                 const int* widths) {
+  if (!L.has_halo()) return;
+  for (int k = 0; k < nvec; ++k)  // a vector outside the iteration's set (true residual's temporary x)
+    if (std::find(bufs_.begin(), bufs_.end(), ext_vecs[k]) == bufs_.end()) {
+      inner_->halo_exchange(L, ext_vecs, nvec, stream, widths);
+      return;
+    }
+  MCG_CHECK(attached_, "peer halo: attach() the peers' handles before the first exchange");
+  MCG_CHECK(!L.allgather, "peer halo: window halos only (the all-gather layout stays on RCCL)");
+  ++seq_;
+  const uint64_t v = 1 + (uint64_t)(seq_ % 2), vprev = 1 + (uint64_t)((seq_ - 1) % 2);
+  std::vector<int> readers, sources;
+  for (const HaloRange& h : L.sends)
+    if (std::find(readers.begin(), readers.end(), h.peer) == readers.end()) readers.push_back(h.peer);
+  for (const HaloRange& h : L.recvs)
+    if (std::find(sources.begin(), sources.end(), h.peer) == sources.end()) sources.push_back(h.peer);
+  // my rows of this exchange are final (the call follows the pass on this stream): tell my readers,
+  // once each has copied my rows of the previous exchange (which this exchange's pass overwrote a
+  // buffer parity later: the wait protects the one after)
+  for (int q : readers) {
+    if (seq_ > 1)
+      MCG_HIP(hipStreamWaitValue64(stream, flags_ + world_ + q, vprev, hipStreamWaitValueEq, ~0ull),
+              "peer halo: wait failed");
+    MCG_HIP(hipStreamWriteValue64(stream, peer_flags_[q] + rank_, v, 0), "peer halo: flag write failed");
+  }
+  // pull: the owner's rows for my ghost ranges, per vector, once the owner's rows are final
+  std::vector<int> idx(nvec);
+  for (int k = 0; k < nvec; ++k) {
+    auto it = std::find(bufs_.begin(), bufs_.end(), ext_vecs[k]);
+    MCG_CHECK(it != bufs_.end(), "peer halo: vector not registered");
+    idx[k] = (int)(it - bufs_.begin());
+  }
+  for (int q : sources) {
+    MCG_HIP(hipStreamWaitValue64(stream, flags_ + q, v, hipStreamWaitValueEq, ~0ull), "peer halo: wait failed");
+    // the owner's ext index of global row g: its own block starts at own_off(q) with row_begin(q);
+    // ghost ranges come from its owned rows, located through the owner's registered layout numbers
+    for (const HaloRange& h : L.recvs) {
+      if (h.peer != q) continue;
+      for (int k = 0; k < nvec; ++k) {
+        const int64_t w = widths ? widths[k] : 1;
+        const int64_t src_row = peer_own_off_.at(q) + (h.gbegin - peer_row_begin_.at(q));
+        MCG_HIP(hipMemcpyAsync(ext_vecs[k] + w * L.ext_index(h.gbegin), peer_bufs_[q][idx[k]] + w * src_row,
+                               w * h.count * sizeof(double), hipMemcpyDeviceToDeviceNoCU, stream),
+                "peer halo: copy failed");
+      }
+    }
+    MCG_HIP(hipStreamWriteValue64(stream, peer_flags_[q] + world_ + rank_, v, 0), "peer halo: flag write failed");
+  }
+}
+
+}  // namespace mcg

@@ -830,6 +830,14 @@ void GpuCgSolver::setup() {
   // vectors allocated with room for the placement probe's start offsets hold that headroom too
   for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->lead_capacity() * sizeof(double);
   probe_placement_();
+  // the vectors a halo may carry, final now (after the placement probe): for a transport that maps
+  // its peers' buffers (PeerHaloComm); the same list, in the same order, on every rank
+  {
+    std::vector<double*> hb;
+    for (DeviceBuffer<double>* b : {&r_, &r1_, &Ap_, &Ap1_, &p_[0], &p_[1], &ra_[0], &ra_[1], &apx_[0], &apx_[1], &w_, &xe_})
+      if (b->get() != nullptr) hb.push_back(b->get());
+    comm_->register_halo_buffers(hb, L_.own_off, L_.row_begin);
+  }
   if (opt_.recurrence == 2) pick_pipe_order_();
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();

@@ -70,6 +70,11 @@ class Communicator {
   // true: the halo moves its bytes with copy engines (no compute units), so it can run while a pass
   // holds every CU (CgOptions::form.halo_hide splits the pass around it)
   virtual bool halo_cu_free() const { return false; }
+  // the solver's halo-exchanged vectors (every rank registers the same list in the same order, once
+  // its buffers are final): a transport that maps its peers' memory needs them
+  // (own_off / row_begin: where this rank's owned rows start in those ext vectors, and their first
+  // global row)
+  virtual void register_halo_buffers(const std::vector<double*>&, int64_t /*own_off*/, int64_t /*row_begin*/) {}
 };
 
 class Comm final : public Communicator {
@@ -145,6 +150,59 @@ class DelayComm final : public Communicator {
   int rank_, world_;
   double ar_us_, halo_us_;
   bool fat_, copy_;
+};
+
+// CU-free halo between the GPUs of one node (or processes / threads sharing one GPU): every rank
+// maps its peers' halo buffers (IPC memory handles, exchanged out of band: attach()) and PULLS its
+// ghost rows from the owners' rows with hipMemcpyAsync(..., hipMemcpyDeviceToDeviceNoCU) -- copy
+// engines, no compute unit, so the copies run next to a pass that holds every CU
+// (profiles/r4/corun: 2 x 128 KiB in 27-30 us beside the 16384^2 pass, RCCL 744 us).  Ordering
+// without a host round trip: per peer two 64-bit flags in the RECEIVER's / OWNER's memory, written
+// by stream memory operations (hipStreamWriteValue64) and waited on by the CP (hipStreamWaitValue64):
+//   exchange s (value v(s) = 1 + s % 2, sense reversal; every rank makes the same calls):
+//     for each rank q reading from me: wait done[q] == v(s - 1) (q copied my previous rows), then
+//       write v(s) into q's ready[me] (my rows of this exchange are final: the call follows my pass)
+//     for each rank q I read from: wait ready[q] == v(s), pull the ranges, write v(s) into q's done[me]
+// The all-reduce goes to `inner` (RCCL, or NullComm in a one-GPU rehearsal).
+class PeerHaloComm final : public Communicator {
+ public:
+  PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int world);
+  ~PeerHaloComm() override;
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void allreduce_sum(double* buf, size_t count, hipStream_t stream) override { inner_->allreduce_sum(buf, count, stream); }
+  void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
+                     const int* widths = nullptr) override;
+  void check_async() override { inner_->check_async(); }
+  bool graph_capturable() const override { return inner_->graph_capturable() && capturable_; }
+  bool moves_data() const override { return inner_->moves_data(); }
+  void abort() override { inner_->abort(); }
+  bool serialized() const override { return false; }  // the halo never enters the inner communicator
+  bool halo_cu_free() const override { return true; }
+  void register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) override;
+  // this rank's IPC handles (flags + registered buffers) as bytes, for an out-of-band all-gather
+  std::string local_handles() const;
+  // every rank's local_handles(), in rank order: map the peers' buffers (same process: plain pointers)
+  void attach(const std::vector<std::string>& all);
+  bool attached() const { return attached_; }
+  void set_capturable(bool c) { capturable_ = c; }
+  // test hook: the registered buffer list (device pointers) of rank q as mapped here
+  std::vector<uintptr_t> peer_buffers(int q) const;
+
+ private:
+  std::shared_ptr<Communicator> inner_;
+  int rank_, world_;
+  std::vector<double*> bufs_;
+  uint64_t* flags_ = nullptr;  // [0, world): ready[q] (written by q), [world, 2 world): done[q]
+  std::vector<std::vector<double*>> peer_bufs_;  // [q][i]
+  std::vector<uint64_t*> peer_flags_;            // [q]
+  int64_t own_off_ = 0, row_begin_ = 0;
+  std::vector<int64_t> peer_own_off_, peer_row_begin_;
+  std::vector<void*> opened_;                    // IPC mappings to close
+  long seq_ = 0;
+  // eager by default: a captured exchange replays the flag values of its capture, which keeps the
+  // 1/2 alternation only if every graph holds an even number of exchanges (set_capturable asserts that)
+  bool attached_ = false, capturable_ = false;
 };
 
 // Shared state of P in-process ranks on one device.

@@ -358,6 +358,38 @@ PYBIND11_MODULE(_C, m) {
            py::arg("halo_us") = 0.0, py::arg("fat") = false, py::arg("copy_halo") = false,
            "copy_halo: the halo as copy-engine (NoCU) copies of the layout's message sizes instead of a spin");
 
+  py::class_<PeerHaloComm, std::shared_ptr<PeerHaloComm>>(
+      m, "PeerHaloComm",
+      "the halo on copy engines (IPC-mapped peer buffers, flags by stream memory operations); the all-reduce "
+      "goes to the wrapped communicator")
+      .def(py::init([](std::shared_ptr<Comm> c, int rank, int world) { return std::make_shared<PeerHaloComm>(c, rank, world); }),
+           py::arg("inner"), py::arg("rank"), py::arg("world"))
+      .def(py::init([](std::shared_ptr<NullComm> c, int rank, int world) { return std::make_shared<PeerHaloComm>(c, rank, world); }),
+           py::arg("inner"), py::arg("rank"), py::arg("world"))
+      .def(py::init([](std::shared_ptr<DelayComm> c, int rank, int world) { return std::make_shared<PeerHaloComm>(c, rank, world); }),
+           py::arg("inner"), py::arg("rank"), py::arg("world"))
+      .def("local_handles", [](const PeerHaloComm& c) { return py::bytes(c.local_handles()); })
+      .def("attach", [](PeerHaloComm& c, const std::vector<py::bytes>& all) {
+        std::vector<std::string> v;
+        for (const py::bytes& b : all) v.push_back(std::string(b));
+        c.attach(v);
+      })
+      .def_property_readonly("attached", &PeerHaloComm::attached)
+      .def("set_capturable", &PeerHaloComm::set_capturable)
+      .def("peer_buffers", &PeerHaloComm::peer_buffers)
+      .def("register_halo_buffers", [](PeerHaloComm& c, const std::vector<uintptr_t>& bufs, int64_t own_off, int64_t row_begin) {
+        std::vector<double*> v;
+        for (uintptr_t b : bufs) v.push_back(reinterpret_cast<double*>(b));
+        c.register_halo_buffers(v, own_off, row_begin);
+      })
+      .def("halo_exchange_ptrs", [](PeerHaloComm& c, const ProblemSpec& s, const std::vector<uintptr_t>& vecs,
+                                    uintptr_t stream) {
+        const LocalLayout L = make_layout(s, partition_rows(s, c.world()), c.rank());
+        std::vector<double*> v;
+        for (uintptr_t b : vecs) v.push_back(reinterpret_cast<double*>(b));
+        c.halo_exchange(L, v.data(), (int)v.size(), as_stream(stream));
+      }, "test hook: one halo exchange of ext-layout vectors laid out for (spec, world, rank)");
+
   py::class_<GpuCgSolver>(m, "Solver")
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<Comm> comm) {
              return new GpuCgSolver(s, o, rank, world, comm.get());
@@ -370,6 +402,11 @@ PYBIND11_MODULE(_C, m) {
            py::arg("spec"), py::arg("opts"), py::arg("rank"), py::arg("world"), py::arg("comm"),
            py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
       .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<DelayComm> comm) {
+             return new GpuCgSolver(s, o, rank, world, comm.get());
+           }),
+           py::arg("spec"), py::arg("opts"), py::arg("rank"), py::arg("world"), py::arg("comm"),
+           py::keep_alive<1, 6>(), py::keep_alive<1, 2>())
+      .def(py::init([](const ProblemSpec& s, const CgOptions& o, int rank, int world, std::shared_ptr<PeerHaloComm> comm) {
              return new GpuCgSolver(s, o, rank, world, comm.get());
            }),
            py::arg("spec"), py::arg("opts"), py::arg("rank"), py::arg("world"), py::arg("comm"),
@@ -606,6 +643,60 @@ PYBIND11_MODULE(_C, m) {
     MCG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "stream create failed");
     return reinterpret_cast<uintptr_t>(st);
   }, "probe: a raw stream restricted to the CUs set in mask (32 per word); free with stream_destroy");
+  k.def("streamop_probe", []() {
+    // probe (r4): do stream memory operations (hipStreamWriteValue64 / hipStreamWaitValue64, the
+    // copy-engine halo's flags) work, order a NoCU copy, and survive stream capture?
+    py::dict d;
+    uint64_t* flag = nullptr;
+    double *a = nullptr, *b = nullptr;
+    MCG_HIP(hipMalloc(&flag, 64), "probe malloc failed");
+    MCG_HIP(hipMalloc(&a, 1 << 20), "probe malloc failed");
+    MCG_HIP(hipMalloc(&b, 1 << 20), "probe malloc failed");
+    MCG_HIP(hipMemset(flag, 0, 64), "probe memset failed");
+    MCG_HIP(hipMemset(a, 0x3f, 1 << 20), "probe memset failed");
+    MCG_HIP(hipMemset(b, 0, 1 << 20), "probe memset failed");
+    hipStream_t s1, s2;
+    MCG_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "stream create failed");
+    MCG_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "stream create failed");
+    // s1: wait flag >= 1, then copy a -> b; s2: write flag = 1 after a spin
+    d["wait"] = (int)hipStreamWaitValue64(s1, flag, 1, hipStreamWaitValueGte, ~0ull);
+    d["copy"] = (int)hipMemcpyAsync(b, a, 1 << 20, hipMemcpyDeviceToDeviceNoCU, s1);
+    kern::spin(nullptr, 200.0, false, 1, s2, nullptr);
+    d["write"] = (int)hipStreamWriteValue64(s2, flag, 1, 0);
+    d["sync"] = (int)hipDeviceSynchronize();
+    double h = 0;
+    (void)hipMemcpy(&h, b + 1000, 8, hipMemcpyDeviceToHost);
+    d["copied_ok"] = h != 0.0;
+    // capture: the same ops inside a graph
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    d["cap_begin"] = (int)hipStreamBeginCapture(s1, hipStreamCaptureModeThreadLocal);
+    d["cap_wait"] = (int)hipStreamWaitValue64(s1, flag, 2, hipStreamWaitValueGte, ~0ull);
+    d["cap_copy"] = (int)hipMemcpyAsync(a, b, 1 << 20, hipMemcpyDeviceToDeviceNoCU, s1);
+    d["cap_write"] = (int)hipStreamWriteValue64(s1, flag, 3, 0);
+    d["cap_end"] = (int)hipStreamEndCapture(s1, &g);
+    if (g) {
+      d["cap_inst"] = (int)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+      (void)hipStreamWriteValue64(s2, flag, 2, 0);
+      if (ge) {
+        d["cap_launch"] = (int)hipGraphLaunch(ge, s1);
+        d["cap_sync"] = (int)hipStreamSynchronize(s1);
+        uint64_t fv = 0;
+        (void)hipMemcpy(&fv, flag, 8, hipMemcpyDeviceToHost);
+        d["cap_flag_after"] = (unsigned long long)fv;
+        (void)hipGraphExecDestroy(ge);
+      }
+      (void)hipGraphDestroy(g);
+    }
+    (void)hipGetLastError();
+    (void)hipDeviceSynchronize();
+    (void)hipStreamDestroy(s1);
+    (void)hipStreamDestroy(s2);
+    (void)hipFree(flag);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return d;
+  }, "probe: stream memory operations (write / wait value) with a NoCU copy, eager and captured");
   k.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t bytes, int kind, uintptr_t stream) {
     MCG_HIP(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes,
                            static_cast<hipMemcpyKind>(kind), as_stream(stream)), "memcpy async failed");

@@ -64,6 +64,27 @@ def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "single"):
     return C.Comm(env.rank, env.world, *ids)
 
 
+def peer_halo(inner, env: DistEnv):
+    """Wrap a communicator so that the halo moves on copy engines (native ``PeerHaloComm``: the
+    ghost rows are pulled from the neighbours' buffers, mapped through IPC handles; the all-reduce
+    stays on ``inner``).  Call :func:`attach_peer_halo` after the solver's ``setup()``."""
+    return native().PeerHaloComm(inner, env.rank, env.world)
+
+
+def attach_peer_halo(comm, env: DistEnv) -> None:
+    """Exchange every rank's IPC handles (registered by the solver's setup) over torch.distributed
+    and map the peers' halo buffers.  Collective: every rank calls it once, after ``setup()``."""
+    mine = comm.local_handles()
+    if env.world == 1:
+        comm.attach([mine])
+        return
+    if not dist.is_initialized():
+        raise RuntimeError("attach_peer_halo needs torch.distributed initialised")
+    allb = [None] * env.world
+    dist.all_gather_object(allb, mine)
+    comm.attach(allb)
+
+
 def set_device(env: DistEnv) -> int:
     """Bind this process to its GPU (LOCAL_RANK) — like the reference's cudaSetDevice(0)."""
     n = torch.cuda.device_count()
