@@ -228,7 +228,7 @@ def recipes(a) -> dict:
         ] + [("auto_again", 200, bench("--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify"))],
         # r4: stream memory operations (write / wait value) around a NoCU copy, eager and captured
         "streamop": [
-            ("probe", 60, f"{PY} -c 'import torch, json, cuda_mpi_parallel_amd as m; torch.cuda.init(); "
+            ("probe", 240, f"{PY} -c 'import torch, json, cuda_mpi_parallel_amd as m; torch.cuda.init(); "
                           f"print(json.dumps(dict(m.native().kernels.streamop_probe())))'"),
         ],
         # r4: the copy-engine halo across processes (PeerHaloComm, IPC-mapped buffers), P ranks on one GPU
@@ -259,7 +259,13 @@ def recipes(a) -> dict:
             ("b16384", 300, bench("--coef 1 --steps 100 --warmup 10 --phases 0")),
             ("b16384_generic", 300, bench("--coef 1 --steps 50 --warmup 5 --phases 0 --set carry_vc=0")),
             ("b4096", 300, bench("--coef 1 --grid 4096 --steps 1000 --warmup 100 --phases 0")),
-        ] + counters("vc_dram", "k_cg_carry_ar", "--coef 1 --steps 8 --warmup 2"),
+            ("b512", 300, bench("--coef 1 --problem poisson3d --grid 512 --steps 60 --warmup 6 --phases 0")),
+            ("b512_kw4", 300, bench("--coef 1 --problem poisson3d --grid 512 --steps 60 --warmup 6 --phases 0 "
+                                    "--set carry3_kw=4")),
+            ("b512_generic", 300, bench("--coef 1 --problem poisson3d --grid 512 --steps 30 --warmup 3 --phases 0 "
+                                        "--set carry_vc=0")),
+        ] + counters("vc_dram", "k_cg_carry_ar", "--coef 1 --steps 8 --warmup 2")
+          + counters("vc3_dram", "k_cg_carry_ar3", "--coef 1 --problem poisson3d --grid 512 --steps 8 --warmup 2"),
         # r4: ranks past 2^29 rows on the lean carries (BIG kernels)
         "large": [
             ("pytest", 900, f"{PY} -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_large.py"),

@@ -67,6 +67,12 @@ struct ArCodes<5, U> {
   double k[5];
   int w = 5;
 };
+// 3-D (CM 6): down, south, west, diagonal, east, north, up
+template <int U>
+struct ArCodes<6, U> {
+  double k[7];
+  int w = 7;
+};
 
 // codes of slice row `lane` from its first slot `base` (slots, multiple of 64) and width w
 template <int CM, int U>
@@ -535,11 +541,11 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           }
           for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, 1);
           if (m < n_run) {  // near the rank's last line: clamped loads, its values C
-            const VSet VC = vals(WC);
+            const VSet VL = vals(WC);
             for (; m < n_run; ++m) {
               const bool lastl = l0 + m == nl - 1;
               const bool nextc = l0 + m + 1 == nl - 1;
-              lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
+              lstep(clamped, m, lastl ? VL : VB, nextc ? VL : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
         }
@@ -1003,14 +1009,18 @@ __device__ __forceinline__ void ar3_finish(double a0, double a1, double a2, doub
 
 // BIG (lean kernels): past 2^29 doubles a run's planes (N^2 rows each) do not fit 32-bit byte offsets
 // from kernel-wide bases, so the lean loop re-bases its ext / x pointers every unrolled step group
-template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false, bool BIG = false>
-__global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
-                                                                  int32_t LN, int gfull,
-                                                                  double* __restrict__ partials, int pstride,
-                                                                  CgState* st, double tol, int first, int check,
-                                                                  RedCtl rc) {
+// VC: SELL-64/diav 3-D (variable coefficients, S.cvd / cve / cvs / cvt) instead of dia4 codes; the
+// lean loop carries the streamed values per lane, so these kernels run 2 waves per SIMD (256 VGPRs)
+template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false, bool BIG = false, bool VC = false>
+__global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own,
+                                                                          TileRanges tr, int32_t LN, int gfull,
+                                                                          double* __restrict__ partials, int pstride,
+                                                                          CgState* st, double tol, int first,
+                                                                          int check, RedCtl rc) {
   static_assert(KW >= 2 && QD >= 2, "3-D carry: >= 2 waves per block, operands >= 2 planes ahead");
+  static_assert(!(VC && BIG), "3-D diav: 32-bit byte offsets (ranks below 2^29 rows)");
   constexpr int U = 7;
+  using Co = ArCodes<VC ? 6 : 4, U>;
   __shared__ double s_val[16];
   __shared__ double s_x[2][2][KW][64];  // [step parity][p_{k-1}(m+1), p_k(m)][wave][lane]
   const F1Scalars sc = f1_scalars(st, tol, first, check);
@@ -1018,7 +1028,9 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     ar3_finish<KW>(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
     return;
   }
-  if (threadIdx.x < 16) s_val[threadIdx.x] = S.dvals[threadIdx.x];
+  if constexpr (!VC) {
+    if (threadIdx.x < 16) s_val[threadIdx.x] = S.dvals[threadIdx.x];
+  }
   __syncthreads();
   const double a = sc.alpha, b = sc.beta, na = -a, ap = st->a_prev;
   // three-term form (P3, as in k_cg_carry_ar): r_{k-1} = p_{k-1} - b_prev p_{k-2} on the run's own
@@ -1069,7 +1081,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
   struct Far {  // the outside line's row (outer waves): r, p, Ap of iteration k-1
     double r, p, a;
   };
-  auto stencil = [&](const ArCodes<4, U>& c, double mid, double edge, double dnl, double upl, double dnn, double upn) {
+  auto stencil = [&](const Co& c, double mid, double edge, double dnl, double upl, double dnn, double upn) {
     const double sh_up = lane_up(mid);
     const double sh_dn = lane_dn(mid);
     const double upv = lane == 63 ? edge : sh_up;
@@ -1077,7 +1089,10 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     const double g[7] = {dnl, dnn, dnv, mid, upv, upn, upl};
     double sum = 0.0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) sum = fma(s_val[(c.pk[0] >> (4 * u)) & 15u], g[u], sum);
+    for (int u = 0; u < U; ++u) {
+      if constexpr (VC) sum = fma(c.k[u], g[u], sum);
+      else sum = fma(s_val[(c.pk[0] >> (4 * u)) & 15u], g[u], sum);
+    }
     return sum;
   };
   auto pk_of = [&](double r, double a_, double p) { return fma(b, p, fma(na, a_, r)); };
@@ -1111,11 +1126,249 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       // renames both chain lengths
       constexpr int LD = 3, ED = 2, UNR = 6;
       uint32_t WA = 0, WB = 0, WC = 0;
-      if constexpr (LEAN) {  // every run checked at setup (carry_lean_failures)
+      if constexpr (LEAN && !VC) {  // every run checked at setup (carry_lean_failures)
         (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC, BIG ? 2 : 0);
         __syncthreads();  // the previous job's last step has read its LDS slots
       }
-      if constexpr (LEAN) {
+      if constexpr (LEAN && VC) {
+        // Variable coefficients (SELL-64/diav 3-D): the loop below with the seven values of a plane
+        // per lane instead of in scalar registers.  Streamed from HBM: the row's own d, e, s, t (32 B;
+        // the arrays have one plane in front).  Re-read from cache: south s[i - N] (the neighbouring
+        // wave's line of the same plane, loaded there this step) and lane 0's west e[i - 1].  Carried:
+        // west = e one lane down (DPP), down = the previous plane's t.  A value of 0 (absent entry:
+        // grid edges) multiplies the same clamped, finite operand as the generic step; every run of
+        // >= 3 planes qualifies (setup).  Coefficients 2 planes ahead.
+        struct VSet {
+          double v[7];
+        };
+        struct CRaw {
+          double d, e, s, t, ss, ee;
+        };
+        __syncthreads();  // the previous job's last step has read its LDS slots
+        const int64_t yl = (q / G) * KW + wv;  // the wave's grid line
+        const bool fnone = (odn && yl == 0) || (oup && yl == LN - 1);
+        const bool z0 = q % G == 0, z63 = q % G == G - 1;  // slices at a grid line's start / end
+        const bool hi = lane == 63, edge_lane = lane == 0 || lane == 63;
+        const bool outer = odn || oup;
+        const uint32_t l8 = (uint32_t)lane << 3;
+        const uint32_t LOB = (uint32_t)LO << 3;
+        const uint32_t SB = (uint32_t)(2 * SS) << 3;
+        const uint32_t NB = (uint32_t)LN << 3;  // one grid line of rows
+        const uint32_t ob0 = (uint32_t)e0 << 3, xb0 = (uint32_t)i0 << 3;
+        const uint32_t kb0 = ((uint32_t)i0 << 3) + LOB;
+        const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;
+        const uint32_t oc = hi ? (z63 ? 16u : 24u) : (z0 ? 8u : 0u);
+        const uint32_t op = hi ? (z63 ? 512u : 520u) : (z0 ? 8u : 0u);
+        const uint32_t fob = fnone ? 0u : (uint32_t)fo << 3;
+        const int32_t jlo = -(e0 / LO), jhi = (ext32 - 64 - e0) / LO;
+        const int32_t rlo = -(int32_t)l0, rhi = (int32_t)(nl - 1 - l0);
+        auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
+        auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
+        auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
+        auto raw_ld = [&](int32_t j, int32_t k) {
+          Raw r;
+          const uint32_t o = line_ofs(k) + l8;
+          r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
+          r.p = g_ld(po, o);
+          return r;
+        };
+        auto edge_ld = [&](int32_t j) {
+          Edge r;
+          const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
+          r.r = g_ld(reo, c);
+          r.a = g_ld(eao, c);
+          r.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
+          return r;
+        };
+        auto edge_un = [&](int32_t j) {
+          Edge r;
+          const uint32_t c = cb0 + (uint32_t)j * SB + oc;
+          r.r = g_ld(reo, c);
+          r.a = g_ld(eao, c);
+          r.p = g_ld(po, line_ofs(j) - 8u + op);
+          return r;
+        };
+        auto rghost = [&](int32_t j, const Raw& qq) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), qq.p); };
+        auto is_ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
+        auto far_ld = [&](int32_t k) {
+          Far f{0.0, 0.0, 0.0};
+          if (outer) {
+            const uint32_t o = line_ofs(k) + l8 + fob;
+            f.r = g_ld(ro, o);
+            f.p = g_ld(po, o);
+            f.a = g_ld(apo, o);
+          }
+          return f;
+        };
+        auto x_at = [&](int32_t j) {
+          if constexpr (PAIR) return g_ld(x, xb0 + (uint32_t)(j < n_run - 1 ? j : n_run - 1) * LOB + l8);
+          else return 0.0;
+        };
+        // plane j's values (j >= rlo - 1: the front plane, whose t alone is read; its south / west
+        // loads take plane rlo's addresses instead, which stay inside the arrays)
+        auto coef_ld = [&](int32_t j, int32_t jo) {
+          CRaw c;
+          const uint32_t o = kb0 + (uint32_t)j * LOB + l8, oo = kb0 + (uint32_t)jo * LOB;
+          c.d = g_ld(S.cvd, o);
+          c.e = g_ld(S.cve, o);
+          c.s = g_ld(S.cvs, o);
+          c.t = g_ld(S.cvt, o);
+          c.ss = g_ld(S.cvs, oo + l8 - NB);
+          c.ee = g_ld(S.cve, oo - 8u);
+          return c;
+        };
+        auto coef_at = [&](int32_t j) {
+          const int32_t k = j < rlo - 1 ? rlo - 1 : (j > rhi ? rhi : j);
+          return coef_ld(k, k < rlo ? rlo : k);
+        };
+        auto coef_un = [&](int32_t j) { return coef_ld(j, j); };
+        auto mkv = [&](const CRaw& c, double t_dn) {
+          VSet V;
+          V.v[0] = t_dn;
+          V.v[1] = c.ss;
+          V.v[2] = lane_dn_or(c.e, c.ee);
+          V.v[3] = c.d;
+          V.v[4] = c.e;
+          V.v[5] = c.s;
+          V.v[6] = c.t;
+          return V;
+        };
+        auto stencil_v = [&](const VSet& V, double mid, double edge, double dnl, double upl, double dnn, double upn) {
+          const double upv = lane_up_or(mid, edge);
+          const double dnv = lane_dn_or(mid, edge);
+          double sum = fma(V.v[0], dnl, 0.0);
+          sum = fma(V.v[1], dnn, sum);
+          sum = fma(V.v[2], dnv, sum);
+          sum = fma(V.v[3], mid, sum);
+          sum = fma(V.v[4], upv, sum);
+          sum = fma(V.v[5], upn, sum);
+          return fma(V.v[6], upl, sum);
+        };
+        auto epk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
+        const Raw rm2 = raw_ld(-2, jc(-2)), rm1 = raw_ld(-1, jc(-1)), r0 = raw_ld(0, 0);
+        Raw qv[LD - 1];
+#pragma unroll
+        for (int d = 0; d < LD - 1; ++d) qv[d] = raw_ld(1 + d, jc(1 + d));
+        const Edge edm1 = edge_ld(-1), ed0 = edge_ld(0);
+        Edge ev[ED - 1];
+#pragma unroll
+        for (int d = 0; d < ED - 1; ++d) ev[d] = edge_ld(1 + d);
+        const Far fm1 = far_ld(jc(-1)), f0 = far_ld(0);
+        Far fv[ED - 1];
+#pragma unroll
+        for (int d = 0; d < ED - 1; ++d) fv[d] = far_ld(jc(1 + d));
+        double xs[ED - 1];
+#pragma unroll
+        for (int d = 0; d < ED - 1; ++d) xs[d] = x_at(d);
+        const CRaw cm2 = coef_at(-2), cm1 = coef_at(-1), c0 = coef_at(0);
+        CRaw cq = coef_at(1);  // plane m + 1
+        s_x[1][0][wv][lane] = rm1.p;
+        s_x[1][1][wv][lane] = r0.p;
+        __syncthreads();
+        double pr_pk = 0.0;
+        if (l0 >= 1) {
+          double dn, up;
+          nbr(1, 0, fm1.p, dn, up);
+          const double t = stencil_v(mkv(cm1, cm2.t), rm1.p, edm1.p, rm2.p, r0.p, dn, up);
+          pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+        } else if (is_ghost(-1)) {
+          pr_pk = pk_of(rghost(-1, rm1), g_ld(apo, line_ofs(-1) + l8), rm1.p);
+        }
+        VSet Vs = mkv(c0, cm1.t);  // plane m
+        double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
+        {
+          double dn, up;
+          nbr(1, 1, f0.p, dn, up);
+          const double t = stencil_v(Vs, r0.p, ed0.p, rm1.p, qv[0].p, dn, up);
+          o_rk = fma(na, t, fma(nbp, r0.r, r0.p));
+          o_pk = fma(b, r0.p, o_rk);
+        }
+        double o_epk = epk(ed0);
+        double o_fpk = pk_of(f0.r, f0.a, f0.p);
+        // next: 1 plane m + 1 owned, 2 a ghost plane, 0 none
+        auto lstep = [&](auto clc, int32_t m, int next) __attribute__((always_inline)) {
+          constexpr bool CL = decltype(clc)::value;
+          const int par = m & 1;
+          const uint32_t ob = line_ofs(m);
+          const double rr = fma(-b, o_pold, o_pk);
+          if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+          else if (outer) g_st(rn, ob + l8, rr);
+          const Raw qn = raw_ld(m + LD, CL ? jc(m + LD) : m + LD);
+          const Edge en2 = CL ? edge_ld(m + ED) : edge_un(m + ED);
+          const Far fn = far_ld(CL ? jc(m + ED) : m + ED);
+          const double xn = x_at(m + ED - 1);
+          const CRaw cn = CL ? coef_at(m + 2) : coef_un(m + 2);
+          s_x[par][0][wv][lane] = qv[0].p;
+          s_x[par][1][wv][lane] = o_pk;
+          __syncthreads();
+          const VSet Vt = mkv(cq, Vs.v[6]);  // plane m + 1 (down: plane m's up values)
+          double rk1 = 0.0, pk1 = 0.0;
+          if (next == 1) {
+            double dn, up;
+            nbr(par, 0, fv[0].p, dn, up);
+            const double t = stencil_v(Vt, qv[0].p, ev[0].p, o_pold, qv[1].p, dn, up);
+            rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
+            pk1 = fma(b, qv[0].p, rk1);
+          } else if (CL && next == 2) {
+            rk1 = fma(na, g_ld(apo, line_ofs(m + 1) + l8), rghost(m + 1, qv[0]));
+            pk1 = fma(b, qv[0].p, rk1);
+          }
+          double kdn, kup;
+          nbr(par, 1, o_fpk, kdn, kup);
+          const double sum = stencil_v(Vs, o_pk, o_epk, pr_pk, pk1, kdn, kup);
+          if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
+          g_st_nt(pn, ob + l8, o_pk);
+          if (outer || (CL && gfull && (l0 + m == 0 || l0 + m == nl - 1))) g_st(apw, ob + l8, sum);
+          if (edge_lane) {
+            const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);
+            g_st(ean, sb, sum);
+            g_st(ren, sb, rr);
+          }
+          s_pap = fma(o_pk, sum, s_pap);
+          s_rap = fma(o_rk, sum, s_rap);
+          s_apap = fma(sum, sum, s_apap);
+          s_rr = fma(o_rk, o_rk, s_rr);
+          pr_pk = o_pk;
+          o_pk = pk1;
+          o_rk = rk1;
+          o_pold = qv[0].p;
+          o_pm2 = qv[0].r;
+          o_epk = epk(ev[0]);
+          o_fpk = pk_of(fv[0].r, fv[0].a, fv[0].p);
+          Vs = Vt;
+          cq = cn;
+#pragma unroll
+          for (int d = 0; d + 1 < LD - 1; ++d) qv[d] = qv[d + 1];
+#pragma unroll
+          for (int d = 0; d + 1 < ED - 1; ++d) {
+            ev[d] = ev[d + 1];
+            fv[d] = fv[d + 1];
+            xs[d] = xs[d + 1];
+          }
+          qv[LD - 2] = qn;
+          ev[ED - 2] = en2;
+          fv[ED - 2] = fn;
+          xs[ED - 2] = xn;
+        };
+        const std::true_type clamped;
+        const std::false_type unclamped;
+        const int32_t m_lo = l0 == 0 ? 1 : 0;
+        const int32_t m_hi = min(n_run - 1, (int32_t)(nl - 1 - LD - l0));
+        int32_t m = 0;
+        if (m_lo == 1) lstep(clamped, 0, 1);
+        m = m_lo;
+        for (; m + UNR - 1 <= m_hi; m += UNR) {
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) lstep(unclamped, m + u, 1);
+        }
+        for (; m <= m_hi; ++m) lstep(unclamped, m, 1);
+        for (; m < n_run; ++m) {
+          const bool lastl = l0 + m == nl - 1;
+          lstep(clamped, m, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
+        }
+        continue;
+      }
+      if constexpr (LEAN && !VC) {
         struct VSet {
           double v[7];
         };
@@ -1337,11 +1590,11 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
           rebase(m);
           for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, 1);
           if (m < n_run) {
-            const VSet VC = vals(WC);
+            const VSet VL = vals(WC);
             for (; m < n_run; ++m) {
               const bool lastl = l0 + m == nl - 1;
               const bool nextc = l0 + m + 1 == nl - 1;
-              lstep(clamped, m, lastl ? VC : VB, nextc ? VC : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
+              lstep(clamped, m, lastl ? VL : VB, nextc ? VL : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
         }
@@ -1396,8 +1649,19 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
         r.xo = ld_once(x + i0 + mm * LO + lane, ntl);
       }
     };
-    auto load_codes = [&](int32_t j, ArCodes<4, U>& c) {
-      ar_load_dia<U>(S.dia4 + (oline(j) * SS + col) * (32 * U), lane, c);
+    auto load_codes = [&](int32_t j, Co& c) {
+      if constexpr (VC) {  // diav: the row's own values, south / west / down from the partners
+        const int64_t f = (oline(j) * SS + col) * 64 + lane + LO;
+        c.k[0] = S.cvt[f - LO];
+        c.k[1] = S.cvs[f - LN];
+        c.k[2] = S.cve[f - 1];
+        c.k[3] = S.cvd[f];
+        c.k[4] = S.cve[f];
+        c.k[5] = S.cvs[f];
+        c.k[6] = S.cvt[f];
+      } else {
+        ar_load_dia<U>(S.dia4 + (oline(j) * SS + col) * (32 * U), lane, c);
+      }
     };
     auto ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jmin && j <= jmax; };
     // ghost plane's r_{k-1}: P3 recovers it from the halo's p's (k_cg_carry_ar's rghost)
@@ -1416,7 +1680,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
     load_edge(-1, edm1);
     load_edge(0, ed0);
     load_edge(1, ed1);
-    ArCodes<4, U> cm1, c0, c1;
+    Co cm1, c0, c1;
     load_codes(-1, cm1);
     load_codes(0, c0);
     load_codes(1, c1);
@@ -1458,7 +1722,7 @@ __global__ __launch_bounds__(64 * KW, 4) void k_cg_carry_ar3(SellDev S, F1Vector
       }
       // 1. loads for later steps: codes / edges of plane m + 2, the outside row of m + 2, x / p_{k-2}
       //    of m + 1, operands of m + 1 + QD
-      ArCodes<4, U> c2;
+      Co c2;
       load_codes(m + 2, c2);
       // P3: the edge and outside rows of plane m + 2 are loaded at the end of the step instead
       // (one set live instead of two: the three-term kernel is at the 128-VGPR limit)
@@ -1570,6 +1834,17 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
         t = fma(kk[u], v.p_old[q], t);
       }
       (void)c;
+    } else if constexpr (CM == 6) {  // 3-D diav (lo = plane, ln = N): south / down from the partners too
+      const int64_t f = i + lo;
+      const double kk[7] = {S.cvt[f - lo], S.cvs[f - ln], S.cve[f - 1], S.cvd[f], S.cve[f], S.cvs[f], S.cvt[f]};
+      const int64_t o7[7] = {-(int64_t)lo, -(int64_t)ln, -1, 0, 1, (int64_t)ln, (int64_t)lo};
+#pragma unroll
+      for (int u = 0; u < 7; ++u) {
+        int64_t q = e + o7[u];
+        q = q < 0 ? 0 : (q >= v.ext_len ? v.ext_len - 1 : q);
+        t = fma(kk[u], v.p_old[q], t);
+      }
+      (void)c;
     } else if constexpr (CM == 4) {  // absent entries: value 0 times a clamped (finite) operand
       ar_load_dia<U>(S.dia4 + (i >> 6) * (32 * U), (int)(i & 63), c);
       const int64_t o5[5] = {-(int64_t)lo, -1, 0, 1, (int64_t)lo};
@@ -1650,16 +1925,19 @@ __global__ void k_dia_vals(const double2* __restrict__ dict, int nv, int nd, dou
 // first-line row's north value into the front line of cvs.  CHECK = 1 (after the fill): the west /
 // north values must equal the partners' east / south (the kernels take them from there).
 // CM: 0 int32 ext columns, 1 d16 offsets, 2 c8 codes
+// plane > 0 (3-D): seven classes (-plane, -line, -1, 0, +1, +line, +plane), arrays shifted by one
+// plane, the front plane of cvt holding the plane-0 down values; check: down = cvt[i - plane] too.
 template <int CM, bool CHECK>
-__global__ __launch_bounds__(256) void k_sell_to_diav(SellDev S, int64_t line, double* __restrict__ cvd,
+__global__ __launch_bounds__(256) void k_sell_to_diav(SellDev S, int64_t line, int64_t plane, double* __restrict__ cvd,
                                                       double* __restrict__ cve, double* __restrict__ cvs,
-                                                      unsigned* __restrict__ bad) {
+                                                      double* __restrict__ cvt, unsigned* __restrict__ bad) {
   const int64_t n = S.n_rows;
+  const int64_t fr = plane > 0 ? plane : line;  // rows in front of each array
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t sl = i >> 6, lane = i & 63;
     const int64_t base = S.slice_ptr[sl], w = (S.slice_ptr[sl + 1] - base) >> 6;
     const int64_t rowcol = S.own_off + i;
-    double v5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    double v7[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     int prev = -1;
     for (int64_t j = 0; j < w; ++j) {
       const int64_t k = base + 64 * j + lane;
@@ -1674,22 +1952,33 @@ __global__ __launch_bounds__(256) void k_sell_to_diav(SellDev S, int64_t line, d
         off = (CM == 1 ? rowcol + (int64_t)S.dcols[k] : (int64_t)S.cols[k]) - rowcol;
       }
       if (val == 0.0) continue;  // SELL padding (and explicit zeros: they add nothing)
-      const int cls = off == -line ? 0 : (off == -1 ? 1 : (off == 0 ? 2 : (off == 1 ? 3 : (off == line ? 4 : -1))));
+      const int cls = off == -line ? 1 : (off == -1 ? 2 : (off == 0 ? 3 : (off == 1 ? 4 : (off == line ? 5 :
+                      (plane > 0 && off == -plane ? 0 : (plane > 0 && off == plane ? 6 : -1))))));
       if (cls <= prev) {
         atomicOr(bad, 1u);
         return;
       }
       prev = cls;
-      v5[cls] = val;
+      v7[cls] = val;
     }
     if constexpr (!CHECK) {
-      cvd[line + i] = v5[2];
-      cve[line + i] = v5[3];
-      cvs[line + i] = v5[4];
-      if (i < line) cvs[i] = v5[0];
+      cvd[fr + i] = v7[3];
+      cve[fr + i] = v7[4];
+      cvs[fr + i] = v7[5];
+      if (plane > 0) {
+        cvt[fr + i] = v7[6];
+        if (i < plane) cvt[i] = v7[0];
+      } else if (i < line) {
+        cvs[i] = v7[1];
+      }
     } else {
-      // a row at a grid line's start has no west entry, and the row before it (a line's end) no east one
-      if (!(v5[1] == cve[line + i - 1]) || (i >= line && !(v5[0] == cvs[i]))) atomicOr(bad, 2u);
+      // a row at a grid line's start has no west entry, and the row before it (a line's end) no east
+      // one; 3-D: a line's row at y = 0 has no south entry, and its partner (y = N - 1 of the plane
+      // before, or the front's zeros) no north one
+      bool ok = v7[2] == cve[fr + i - 1];
+      if (plane > 0) ok = ok && v7[1] == cvs[fr + i - line] && (i < plane || v7[0] == cvt[i]);
+      else ok = ok && (i < line || v7[1] == cvs[i]);
+      if (!ok) atomicOr(bad, 2u);
     }
   }
 }
@@ -1829,20 +2118,25 @@ int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64
   return (int64_t)h;
 }
 
-bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream) {
+bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream, int64_t plane) {
   const int64_t n = S.n_rows;
-  MCG_CHECK(cv != nullptr && line >= 64 && line % 64 == 0 && n % line == 0, "diav: whole 64-row grid lines");
+  const int64_t fr = plane > 0 ? plane : line;
+  MCG_CHECK(cv != nullptr && line >= 64 && line % 64 == 0 && n % fr == 0 && (plane == 0 || plane == line * line),
+            "diav: whole 64-row grid lines (3-D: whole planes)");
   if (line > INT32_MAX / 2) return false;
-  MCG_HIP(hipMemsetAsync(cv, 0, (size_t)3 * (n + line) * sizeof(double), stream), "device memset failed(diav)");
+  const int na = plane > 0 ? 4 : 3;
+  MCG_HIP(hipMemsetAsync(cv, 0, (size_t)na * (n + fr) * sizeof(double), stream), "device memset failed(diav)");
   unsigned* bad = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&bad), sizeof(unsigned), stream), "device malloc failed(diav)");
   MCG_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), stream), "device memset failed");
-  double *cd = cv, *ce = cv + (n + line), *cs = cv + 2 * (n + line);
+  double *cd = cv, *ce = cv + (n + fr), *cs = cv + 2 * (n + fr), *ct = plane > 0 ? cv + 3 * (n + fr) : nullptr;
   const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 8192);
 #define MCG_DV(CM)                                                                                             \
   do {                                                                                                         \
-    hipLaunchKernelGGL((k_sell_to_diav<CM, false>), dim3(g), dim3(256), 0, stream, S, line, cd, ce, cs, bad); \
-    hipLaunchKernelGGL((k_sell_to_diav<CM, true>), dim3(g), dim3(256), 0, stream, S, line, cd, ce, cs, bad);  \
+    hipLaunchKernelGGL((k_sell_to_diav<CM, false>), dim3(g), dim3(256), 0, stream, S, line, plane, cd, ce, cs, ct, \
+                       bad);                                                                                   \
+    hipLaunchKernelGGL((k_sell_to_diav<CM, true>), dim3(g), dim3(256), 0, stream, S, line, plane, cd, ce, cs, ct, \
+                       bad);                                                                                   \
   } while (0)
   if (n > 0) {
     if (S.codes != nullptr) MCG_DV(2);
@@ -2020,20 +2314,51 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0 && ln % 64 == 0 &&
                 (int64_t)ln * ln == (int64_t)tr.strip * 64 && (kw == 4 || kw == 8 || kw == 16) && ln % kw == 0,
             "3-D Ap-recomputing carry: one launch over the rank's whole planes, N a multiple of 64 and of the block");
-  MCG_CHECK(S.dia4 != nullptr && S.dvals != nullptr, "3-D Ap-recomputing carry: dia4 codes missing");
+  const bool vc = S.cvt != nullptr;  // SELL-64/diav 3-D
+  MCG_CHECK(vc || (S.dia4 != nullptr && S.dvals != nullptr), "3-D Ap-recomputing carry: dia4 codes missing");
+  MCG_CHECK(!vc || (S.cvd && S.cve && S.cvs && (kw == 4 || kw == 8) && v.ext_len < ((int64_t)1 << 29) &&
+                    (tr.nt0 * 64 + tr.strip * 64) < ((int64_t)1 << 29)),
+            "3-D diav carry: 4 / 8 waves per block, ranks below 2^29 rows");
   MCG_CHECK(v.ap_old != nullptr && v.ap_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
             "3-D Ap-recomputing carry: vectors missing");
   MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
             "in-kernel reduction: bad control block");
   if (final_mode) {
-    hipLaunchKernelGGL((k_ar_final<4, 7>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr.nt0 * 64,
-                       (int32_t)(tr.strip * 64), ln, partials, pstride, st, tol, first, check, k, p3);
+    if (vc)
+      hipLaunchKernelGGL((k_ar_final<6, 7>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr.nt0 * 64,
+                         (int32_t)(tr.strip * 64), ln, partials, pstride, st, tol, first, check, k, p3);
+    else
+      hipLaunchKernelGGL((k_ar_final<4, 7>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr.nt0 * 64,
+                         (int32_t)(tr.strip * 64), ln, partials, pstride, st, tol, first, check, k, p3);
     MCG_HIP(hipGetLastError(), "compute axpy failed(r)");
     return;
   }
   const bool pair = (k & 1) != 0;
   const int qd = depth >= 3 ? 3 : 2;
   const int g = gfull ? 1 : 0;
+  if (vc) {
+#define MCG_A3V(PAIR, KW, P3, LEAN)                                                                            \
+  hipLaunchKernelGGL((k_cg_carry_ar3<2, PAIR, KW, P3, LEAN, false, true>), dim3(grid), dim3(64 * KW), 0, stream, \
+                     S, v, own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
+#define MCG_A3VK(PAIR, P3, LEAN)                     \
+  do {                                               \
+    if (kw == 4) MCG_A3V(PAIR, 4, P3, LEAN);         \
+    else MCG_A3V(PAIR, 8, P3, LEAN);                 \
+  } while (0)
+#define MCG_A3VP(PAIR)                                          \
+  do {                                                          \
+    if (p3 && !first && lean) MCG_A3VK(PAIR, true, true);       \
+    else if (p3 && !first) MCG_A3VK(PAIR, true, false);         \
+    else MCG_A3VK(PAIR, false, false);                          \
+  } while (0)
+    if (pair) MCG_A3VP(true);
+    else MCG_A3VP(false);
+#undef MCG_A3VP
+#undef MCG_A3VK
+#undef MCG_A3V
+    MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
+    return;
+  }
   const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: bases moved along the run
 #define MCG_A3(QD, PAIR, KW, P3, ...)                                                                         \
   hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, stream, S, v, \

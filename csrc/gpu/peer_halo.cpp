@@ -49,7 +49,13 @@ PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int wo
     : inner_(std::move(inner)), rank_(rank), world_(world) {
   MCG_CHECK(inner_ != nullptr && world >= 1 && rank >= 0 && rank < world, "peer halo: invalid rank / world");
   MCG_HIP(hipMalloc(&flags_, 2 * world * sizeof(uint64_t)), "device malloc failed(peer halo flags)");
-  MCG_HIP(hipMemset(flags_, 0, 2 * world * sizeof(uint64_t)), "device memset failed");
+  // ready[q] = 0 (no exchange yet: never a value an exchange waits for); done[q] = 1, the value
+  // exchange 1 waits for ("exchange 0 copied"), so every exchange waits, the first one included, and
+  // a graph that captures the first exchange replays correctly as a later one
+  std::vector<uint64_t> init(2 * world, 0);
+  for (int q = 0; q < world; ++q) init[world + q] = 1;
+  MCG_HIP(hipMemcpy(flags_, init.data(), init.size() * sizeof(uint64_t), hipMemcpyHostToDevice),
+          "memcpy from host to device failed(peer halo flags)");
   peer_bufs_.assign(world, {});
   peer_flags_.assign(world, nullptr);
   peer_own_off_.assign(world, 0);
@@ -132,6 +138,16 @@ void PeerHaloComm::attach(const std::vector<std::string>& all) {
   attached_ = true;
 }
 
+void PeerHaloComm::on_captured(bool kept) {
+  const long n = cap_n_;
+  cap_n_ = 0;
+  if (!kept) {  // the capture was abandoned: its exchanges never run, the sequence resumes before them
+    seq_ -= n;
+    return;
+  }
+  MCG_CHECK(n % 2 == 0, "peer halo: a graph must hold an even number of exchanges (its flag values replay)");
+}
+
 std::vector<uintptr_t> PeerHaloComm::peer_buffers(int q) const {
   std::vector<uintptr_t> v;
   for (double* p : peer_bufs_.at(q)) v.push_back(reinterpret_cast<uintptr_t>(p));
@@ -148,6 +164,9 @@ void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, 
     }
   MCG_CHECK(attached_, "peer halo: attach() the peers' handles before the first exchange");
   MCG_CHECK(!L.allgather, "peer halo: window halos only (the all-gather layout stays on RCCL)");
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  MCG_HIP(hipStreamIsCapturing(stream, &cs), "peer halo: capture query failed");
+  if (cs == hipStreamCaptureStatusActive) ++cap_n_;
   ++seq_;
   const uint64_t v = 1 + (uint64_t)(seq_ % 2), vprev = 1 + (uint64_t)((seq_ - 1) % 2);
   std::vector<int> readers, sources;
@@ -159,9 +178,8 @@ void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, 
   // once each has copied my rows of the previous exchange (which this exchange's pass overwrote a
   // buffer parity later: the wait protects the one after)
   for (int q : readers) {
-    if (seq_ > 1)
-      MCG_HIP(hipStreamWaitValue64(stream, flags_ + world_ + q, vprev, hipStreamWaitValueEq, ~0ull),
-              "peer halo: wait failed");
+    MCG_HIP(hipStreamWaitValue64(stream, flags_ + world_ + q, vprev, hipStreamWaitValueEq, ~0ull),
+            "peer halo: wait failed");
     MCG_HIP(hipStreamWriteValue64(stream, peer_flags_[q] + rank_, v, 0), "peer halo: flag write failed");
   }
   // pull: the owner's rows for my ghost ranges, per vector, once the owner's rows are final

@@ -591,13 +591,16 @@ void GpuCgSolver::capture_pair_(int kind) {
     hipGraph_t g = nullptr;
     (void)hipStreamEndCapture(s, &g);
     if (g) (void)hipGraphDestroy(g);
+    if (comm_ != nullptr) comm_->on_captured(false);
     ghosts_for_ = -1;
     halo_pending_ = false;
     throw;
   }
   ghosts_for_ = halo_ahead_ ? k_ : -1;  // nothing captured has run yet
   halo_pending_ = false;
-  MCG_HIP(hipStreamEndCapture(s, &graph_[kind]), "graph capture failed");
+  const hipError_t ec = hipStreamEndCapture(s, &graph_[kind]);
+  if (comm_ != nullptr) comm_->on_captured(ec == hipSuccess);
+  MCG_HIP(ec, "graph capture failed");
   MCG_HIP(hipGraphInstantiate(&graph_exec_[kind], graph_[kind], nullptr, nullptr, 0), "graph instantiate failed");
 }
 

@@ -590,8 +590,27 @@ void GpuCgSolver::setup() {
           cv_len_ = 0;
         }
       }
+      // 3-D 7-point with variable coefficients: SELL-64/diav 3-D (four arrays, one plane in front) on
+      // the plane carry's three-term lean loop (32-bit byte offsets: ranks below 2^29 rows)
+      const int64_t ln3 = stencil_line(spec_);
+      const int kwv = opt_.form.carry3_kw == 4 ? 4 : 8;
+      if (!c8_ && !diav_ && stencil_plane(spec_) > 0 && ln3 >= 64 && ln3 % 64 == 0 && ln3 % kwv == 0 &&
+          ln3 * ln3 == gl && info_.max_row_len <= 7 && opt_.form.carry_vc != 0 && opt_.form.ap_recompute != 0 &&
+          opt_.form.p3 != 0 && !split_ && n > 0 && L_.ext_len < ((int64_t)1 << 29) && n + gl < ((int64_t)1 << 29)) {
+        cv_len_ = n + gl;
+        cv_.allocate(4 * cv_len_, "A", 64);
+        if (kern::sell_to_diav(sell_view(), ln3, cv_.get(), s0_, gl)) {
+          diav_ = diav3_ = true;
+          carry_general_ = false;
+          carry_lo2_ = (int32_t)ln3;
+        } else {
+          cv_.release();
+          cv_len_ = 0;
+        }
+      }
       MCG_CHECK(opt_.form.carry_vc != 1 || diav_,
-                "carry_vc: needs a symmetric 2-D 5-point stencil without a c8 dictionary, ap_recompute on");
+                "carry_vc: needs a symmetric 2-D 5-point / 3-D 7-point stencil without a c8 dictionary, ap_recompute "
+                "on (3-D: p3 on, N a multiple of 64, ranks below 2^29 rows)");
       // auto: only the specialised pass (2-D stencils); with the slow path (3-D's +-N gathers) it
       // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log)
       if (opt_.form.carry == 1 || !carry_general_) carry_all_ = apply(tr_all_, g_all_);
@@ -603,11 +622,12 @@ void GpuCgSolver::setup() {
     // carry with +-N through LDS, on SELL-64/dia4 only
     const bool ar_any = opt_.form.ap_recompute != 0 && carry_all_ && !carry_general_ && (c8_ || diav_) && !split_ &&
                         tr_all_.b0 == 0 && tr_all_.strip > 0;
-    const int kw = opt_.form.carry3_kw;
+    // 3-D diav: blocks of 8 (or 4) waves, 2 per SIMD (the streamed values need the registers)
+    const int kw = diav3_ ? (opt_.form.carry3_kw == 4 ? 4 : 8) : opt_.form.carry3_kw;
     const bool ar2 = ar_any && carry_lo2_ == 0 && info_.spmv_param <= 5;
     const bool ar3 = ar_any && carry_lo2_ > 0 && carry_lo2_ % 64 == 0 && info_.spmv_param <= 7 &&
-                     opt_.form.carry_dia != 0 && (kw == 4 || kw == 8 || kw == 16) && carry_lo2_ % kw == 0 &&
-                     (int64_t)carry_lo2_ * carry_lo2_ == gl;
+                     (opt_.form.carry_dia != 0 || diav3_) && (kw == 4 || kw == 8 || kw == 16) &&
+                     carry_lo2_ % kw == 0 && (int64_t)carry_lo2_ * carry_lo2_ == gl;
     MCG_CHECK(opt_.form.carry_dia != 1 || ar2 || ar3,
               "carry_dia needs the Ap-recomputing line / plane carry (ap_recompute)");
     if ((ar2 || ar3) && opt_.form.carry_dia != 0 && n > 0 && c8_) {  // SELL-64/dia4 from the c8 codes (replaces c4 + metadata)
@@ -627,7 +647,7 @@ void GpuCgSolver::setup() {
         info_.dia_uniform = ns > 0 ? (double)nu / (double)ns : 0.0;
       }
     }
-    ar3_ = ar3 && dia4_.get() != nullptr;
+    ar3_ = ar3 && (dia4_.get() != nullptr || diav3_);
     ar_ = ar2 || ar3_;
     // every rank takes the same pass form: it decides the vectors the halo carries ({r, Ap} pairs or
     // r / Ap / p) and their widths (one all-reduce of a flag at setup, like pmat)
@@ -637,14 +657,18 @@ void GpuCgSolver::setup() {
       dvals_.release();
       dpat_.release();
       cv_.release();
-      diav_ = false;
+      if (diav3_) {  // back to the d16 pass with the general carry (the 3-D stencil without the dictionary)
+        carry_general_ = true;
+        carry_lo2_ = 0;
+      }
+      diav_ = diav3_ = false;
       info_.dia_uniform = 0.0;
     }
     MCG_CHECK(opt_.form.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
               "3-D: dia4, N a multiple of 64 and of carry3_kw)");
     // 4 waves per SIMD (one round of resident blocks)
-    if (ar3_) g_all_ = std::max(1, ncu_ * 16 / kw);
+    if (ar3_) g_all_ = std::max(1, ncu_ * (diav3_ ? 8 : 16) / kw);
     info_.ar3_kw = ar3_ ? kw : 0;
     info_.carry_xchg = info_.carry && carry_lo2_ > 0 &&
                        kern::carry_block_exchange_ok(info_.spmv_param, carry_lo2_, gl / 64);
@@ -695,7 +719,23 @@ void GpuCgSolver::setup() {
       g_all_ = g;
     }
   }
-  if (p3_ && diav_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
+  if (p3_ && diav3_ && ar3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
+    // 3-D diav: every run of the launch's job decomposition (k_cg_carry_ar3) >= 3 planes
+    // (small grids: fewer blocks until the runs hold >= 8 planes, so the 3-plane prologues stay a
+    // small share of each run)
+    const int64_t ss = tr_all_.strip, nl = (n + 63) / 64 / ss, G = carry_lo2_ / 64;
+    const int64_t jpr = (carry_lo2_ / info_.ar3_kw) * G;
+    auto runs_of = [&](int64_t nb) { return nb > jpr ? nb / jpr : (int64_t)1; };
+    while (g_all_ > jpr && (nl + runs_of(g_all_) - 1) / runs_of(g_all_) < 8) g_all_ = std::max<int64_t>(jpr, g_all_ / 2);
+    const int64_t runs = runs_of(g_all_), chunk = (nl + runs - 1) / runs;
+    bool all = nl >= 4;
+    for (int64_t r = 0; r < runs && all; ++r) {
+      const int64_t l0 = r * chunk, l1 = std::min(nl, l0 + chunk);
+      if (l0 < nl && l1 - l0 < 3) all = false;
+    }
+    lean_only_ = all;
+  }
+  if (p3_ && diav_ && !diav3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
     // diav: every run of >= 3 lines streams its coefficients in the lean loop (the same grids as the
     // dia4 2-D passes); checked here on the host from the launch's job decomposition
     const int64_t ss = tr_all_.strip, nlines = (n + 63) / 64 / ss;
@@ -727,7 +767,7 @@ void GpuCgSolver::setup() {
   info_.lean_only = lean_only_;
   // halo_hide: the lean 2-D pass split into the interior band (reads no ghost line; it runs while a
   // copy-engine halo lands) and the kHideLines lines at each end of the rank (after the halo)
-  if (opt_.form.halo_hide == 1 && halo_ahead_ && comm_->halo_cu_free() && lean_only_ && ar_ && !ar3_ && p3_ &&
+  if (opt_.form.halo_hide == 1 && halo_ahead_ && comm_ != nullptr && comm_->halo_cu_free() && lean_only_ && ar_ && !ar3_ && p3_ &&
       n > 0 && tr_all_.strip > 0) {
     constexpr int kHideLines = 4;
     const int64_t ss = tr_all_.strip, nlines = (n + 63) / 64 / ss;
@@ -821,7 +861,7 @@ void GpuCgSolver::setup() {
   } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
     // dia4 codes; the three-term pass streams none over its lean runs (uniform slices)
     const double streamed = info_.dia4 ? (double)dia4_.bytes() * (p3_ ? 1.0 - info_.dia_uniform : 1.0)
-                                       : (diav_ ? 24.0 * n : (double)matrix_bytes);
+                                       : (diav_ ? (diav3_ ? 32.0 : 24.0) * n : (double)matrix_bytes);
     // three-term form: p_{k-1}, p_{k-2} read, p_k written 24 B; x rw every second pass 8; edge r + Ap 0.5
     info_.bytes_per_iter_model = streamed + (p3_ ? 32.5 : 44.25) * n;
     info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + smeta_.bytes() + cv_.bytes();
@@ -832,7 +872,7 @@ void GpuCgSolver::setup() {
   probe_placement_();
   // the vectors a halo may carry, final now (after the placement probe): for a transport that maps
   // its peers' buffers (PeerHaloComm); the same list, in the same order, on every rank
-  {
+  if (comm_ != nullptr) {
     std::vector<double*> hb;
     for (DeviceBuffer<double>* b : {&r_, &r1_, &Ap_, &Ap1_, &p_[0], &p_[1], &ra_[0], &ra_[1], &apx_[0], &apx_[1], &w_, &xe_})
       if (b->get() != nullptr) hb.push_back(b->get());

@@ -75,6 +75,10 @@ class Communicator {
   // (own_off / row_begin: where this rank's owned rows start in those ext vectors, and their first
   // global row)
   virtual void register_halo_buffers(const std::vector<double*>&, int64_t /*own_off*/, int64_t /*row_begin*/) {}
+  // a graph capture holding this communicator's operations has ended (the solver calls it after
+  // hipStreamEndCapture; kept = false: the capture failed and its graph is dropped): a transport whose
+  // captured operations replay fixed values checks / rewinds its sequence here
+  virtual void on_captured(bool /*kept*/) {}
 };
 
 class Comm final : public Communicator {
@@ -180,6 +184,7 @@ class PeerHaloComm final : public Communicator {
   bool serialized() const override { return false; }  // the halo never enters the inner communicator
   bool halo_cu_free() const override { return true; }
   void register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) override;
+  void on_captured(bool kept) override;
   // this rank's IPC handles (flags + registered buffers) as bytes, for an out-of-band all-gather
   std::string local_handles() const;
   // every rank's local_handles(), in rank order: map the peers' buffers (same process: plain pointers)
@@ -200,9 +205,12 @@ class PeerHaloComm final : public Communicator {
   std::vector<int64_t> peer_own_off_, peer_row_begin_;
   std::vector<void*> opened_;                    // IPC mappings to close
   long seq_ = 0;
-  // eager by default: a captured exchange replays the flag values of its capture, which keeps the
-  // 1/2 alternation only if every graph holds an even number of exchanges (set_capturable asserts that)
-  bool attached_ = false, capturable_ = false;
+  long cap_n_ = 0;  // exchanges recorded by the capture in progress
+  // A captured exchange replays the flag values of its capture, which continues the 1/2 alternation
+  // only if every graph holds an even number of exchanges (the solver's graphs hold an even number
+  // of iterations, one exchange each; on_captured() checks it).  Measured: stream write / wait value
+  // and NoCU copies capture and replay (bench/gpu_run.py streamop)
+  bool attached_ = false, capturable_ = true;
 };
 
 // Shared state of P in-process ranks on one device.

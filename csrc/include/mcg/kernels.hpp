@@ -124,9 +124,13 @@ struct SellDev {
   // coefficients (a_{i,i-line} of its first line).  A symmetric matrix's other two coefficients of
   // row i are its partners': west a_{i,i-1} = cve[i - 1], north a_{i,i-line} = cvs[i - line] (checked
   // bitwise at setup).  24 B per row streamed instead of one shared value table.
+  // 3-D 7-point (sell_to_diav with plane > 0): four arrays shifted by one PLANE (index plane + i),
+  // cvt = a_{i,i+plane} as well, the front plane of cvt holding the rank's plane 0 down coefficients
+  // (a_{i,i-plane}); south a_{i,i-N} = cvs[i - N], down a_{i,i-plane} = cvt[i - plane].  32 B per row.
   const double* cvd = nullptr;
   const double* cve = nullptr;
   const double* cvs = nullptr;
+  const double* cvt = nullptr;
   // SELL-64/aligned (long rows whose slices share their column offsets, e.g. the wide random-SPD
   // family): entry j of EVERY lane of slice s is the row's own column + soffs[slice_ptr[s] / 64 + j]
   // (one wave-uniform offset per slot, clamped to [0, ext_len); absent entries hold 0.0), so a
@@ -292,14 +296,18 @@ bool sell_to_dia4(const SellDev& S, int nd, int64_t line, int64_t ln, uint8_t* d
 // in whole lines) -> SELL-64/diav: cv = 3 * (n + line) doubles (cvd | cve | cvs, SellDev).  False
 // when an entry sits at another offset, a row's offsets are not strictly increasing, or the matrix
 // is not bitwise symmetric inside the rank (west / north entries = their partners' east / south).
-bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream);
+// plane > 0: a 3-D 7-point stencil (line = N, plane = N^2, every local row in whole planes): cv =
+// 4 * (n + plane) doubles (cvd | cve | cvs | cvt)
+bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream, int64_t plane = 0);
 // SellDev::dpat from a dia4 copy (and its value table) of ns = ss * lines slices (ss slices per line,
 // nslot 5 or 7); returns the number of uniform slices (synchronises the stream)
 int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64_t ss, int nslot, uint64_t* dpat,
                      hipStream_t stream);
 // 3-D (7-pt) Ap-recomputing plane carry (SELL-64/dia4 with ln = N): blocks of kw (4 / 8 / 16) waves on
 // kw consecutive grid lines of one x slice; v.ap_old / ap_new = ext-layout Ap (outer lines, slice
-// edge rows, and with gfull the first / last plane for the ghosts); grid = blocks (any count)
+// edge rows, and with gfull the first / last plane for the ghosts); grid = blocks (any count).
+// With S.cvt set (SELL-64/diav 3-D, variable coefficients) the per-row values are streamed instead
+// (kw 4 / 8, 2 waves per SIMD: the lean loop's coefficient chain needs up to 256 VGPRs)
 void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
                   int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),

@@ -178,8 +178,9 @@ class GpuCgSolver {
   DeviceBuffer<double2> dict_;
   DeviceBuffer<uint8_t> dia4_;    // SELL-64/dia4 copy (Ap-recomputing carry; 160 B per slice)
   DeviceBuffer<double> cv_;       // SELL-64/diav: cvd | cve | cvs, (n + line) doubles each (kernels.hpp SellDev)
-  int64_t cv_len_ = 0;
+  int64_t cv_len_ = 0;            // ... 3-D (diav3_): | cvt, (n + plane) doubles each
   bool diav_ = false;
+  bool diav3_ = false;
   DeviceBuffer<double> dvals_;    // ... its value table (16 doubles)
   DeviceBuffer<uint64_t> dpat_;   // ... its uniform-slice patterns and run lengths (SellDev::dpat)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
@@ -241,6 +242,7 @@ class GpuCgSolver {
       s.cvd = cv_.get();
       s.cve = cv_.get() + cv_len_;
       s.cvs = cv_.get() + 2 * cv_len_;
+      if (diav3_) s.cvt = cv_.get() + 3 * cv_len_;
     }
     return s;
   }

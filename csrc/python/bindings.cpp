@@ -7,8 +7,10 @@
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <chrono>
 #include <cstring>
 #include <pybind11/stl.h>
+#include <thread>
 
 #include <memory>
 
@@ -658,11 +660,23 @@ PYBIND11_MODULE(_C, m) {
     hipStream_t s1, s2;
     MCG_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "stream create failed");
     MCG_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "stream create failed");
-    // s1: wait flag >= 1, then copy a -> b; s2: write flag = 1 after a spin
+    // a stream that never drains must not hang the probe: poll it for up to 5 s, then release the
+    // wait from the host (a plain copy into the flag) and report it
+    auto drain = [&](hipStream_t s, uint64_t release, const char* key) {
+      const auto t0 = std::chrono::steady_clock::now();
+      hipError_t q;
+      while ((q = hipStreamQuery(s)) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      d[key] = q == hipErrorNotReady ? -1 : (int)q;
+      if (q == hipErrorNotReady) (void)hipMemcpy(flag, &release, 8, hipMemcpyHostToDevice);
+    };
+    // s2: write flag = 1; s1: wait flag >= 1, then copy a -> b
+    d["write"] = (int)hipStreamWriteValue64(s2, flag, 1, 0);
+    d["write_done"] = (int)hipStreamSynchronize(s2);
     d["wait"] = (int)hipStreamWaitValue64(s1, flag, 1, hipStreamWaitValueGte, ~0ull);
     d["copy"] = (int)hipMemcpyAsync(b, a, 1 << 20, hipMemcpyDeviceToDeviceNoCU, s1);
-    kern::spin(nullptr, 200.0, false, 1, s2, nullptr);
-    d["write"] = (int)hipStreamWriteValue64(s2, flag, 1, 0);
+    drain(s1, 1, "wait_drained");
     d["sync"] = (int)hipDeviceSynchronize();
     double h = 0;
     (void)hipMemcpy(&h, b + 1000, 8, hipMemcpyDeviceToHost);
@@ -678,8 +692,10 @@ PYBIND11_MODULE(_C, m) {
     if (g) {
       d["cap_inst"] = (int)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
       (void)hipStreamWriteValue64(s2, flag, 2, 0);
+      (void)hipStreamSynchronize(s2);
       if (ge) {
         d["cap_launch"] = (int)hipGraphLaunch(ge, s1);
+        drain(s1, 3, "cap_drained");
         d["cap_sync"] = (int)hipStreamSynchronize(s1);
         uint64_t fv = 0;
         (void)hipMemcpy(&fv, flag, 8, hipMemcpyDeviceToHost);

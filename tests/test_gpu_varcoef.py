@@ -125,6 +125,82 @@ def test_varcoef_local_ranks_agree_with_single_rank(mcg, world):
     np.testing.assert_allclose(many["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
 
 
+def _vc3(mcg, n=64, **kw):
+    return mcg.make_problem("poisson3d", n=n, coef=1, rhs="random", **kw)
+
+
+def test_varcoef3d_takes_the_diav_plane_carry(mcg):
+    """3-D 7-point, variable coefficients: SELL-64/diav 3-D on the three-term plane carry."""
+    s = mcg.CGSolver(_vc3(mcg, 128), format="sellc8", recurrence=-1, tol=1e-6)
+    i = s.info
+    assert i["diav"] and not i["dia4"], i
+    assert i["ap_recompute"] and i["p3"] and i["lean_only"] and i["ar3_kw"] == 8, i
+
+
+def test_varcoef3d_matches_cpu_oracle(mcg):
+    spec = _vc3(mcg, 64)
+    C = mcg.native()
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=4000, tol=1e-8))
+    s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, tol=1e-8, maxit=4000)
+    assert s.info["diav"] and s.info["lean_only"]
+    out = s.solve()
+    assert out["converged"] and cpu["converged"]
+    assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 200)
+    np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-6, atol=1e-7 * np.abs(cpu["x"]).max())
+    assert s.true_residual_norm() < 1e-6
+
+
+def test_varcoef3d_fixed_iterations_match_generic_d16_pass(mcg):
+    """40 fixed iterations: the 3-D diav plane carry vs the generic single-reduction d16 pass."""
+    spec = _vc3(mcg, 128)
+    res = []
+    for vc in (-1, 0):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=40, carry_vc=vc)
+        assert s.info["diav"] == (vc != 0)
+        out = s.solve()
+        res.append((out["rnorm"], out["x_local"], s.true_residual_norm()))
+    (ra, xa, ta), (rb, xb, tb) = res
+    assert abs(ra - rb) <= 1e-9 * rb
+    assert np.linalg.norm(xa - xb) <= 1e-9 * np.linalg.norm(xb)
+    assert abs(ta - ra) <= 1e-8 * ta
+
+
+def test_varcoef3d_lean_matches_generic_step(mcg):
+    """The 3-D diav lean loop vs the generic three-term plane step (dia_uniform = 0), same grid."""
+    spec = _vc3(mcg, 128)
+    outs = []
+    for du in (-1, 0):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=37, dia_uniform=du)
+        assert s.info["diav"] and s.info["p3"] and s.info["lean_only"] == (du != 0)
+        outs.append(s.solve())
+    assert abs(outs[0]["rnorm"] - outs[1]["rnorm"]) <= 1e-11 * outs[1]["rnorm"]
+    np.testing.assert_allclose(outs[0]["x_local"], outs[1]["x_local"], rtol=1e-9,
+                               atol=1e-12 * np.abs(outs[1]["x_local"]).max())
+
+
+def test_varcoef3d_bitwise_repeatable_and_graph_equals_eager(mcg):
+    spec = _vc3(mcg, 96 + 32)
+    outs = [mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=1e-7, use_graph=g).solve()
+            for g in (True, True, False)]
+    for o in outs[1:]:
+        assert o["iterations"] == outs[0]["iterations"] and o["rnorm"] == outs[0]["rnorm"]
+        np.testing.assert_array_equal(o["x_local"], outs[0]["x_local"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_varcoef3d_local_ranks_agree_with_single_rank(mcg, world):
+    """P ranks (LocalComm) on the 3-D diav carry: the ghost planes' down values from the rank's own rows."""
+    spec = _vc3(mcg, 128)
+    C = mcg.native()
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8)
+    one = C.run_local_ranks(spec.native(), o, 1, 40, True)
+    many = C.run_local_ranks(spec.native(), o, world, 40, True)
+    assert all(r["ap_recompute"] for r in many["ranks"])
+    r1, rp = one["ranks"][0]["rnorm"], many["ranks"][0]["rnorm"]
+    assert abs(r1 - rp) <= 1e-11 * r1
+    assert np.linalg.norm(many["x"] - one["x"]) <= 1e-11 * np.linalg.norm(one["x"])
+
+
 def test_varcoef_user_matrix_takes_diav(mcg):
     """The same operator given as a SciPy CSR (the reference's input form) takes the diav carry and
     solves bit for bit like the generated problem."""
