@@ -1062,7 +1062,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
   const int64_t jpr = (LN / KW) * G;      // jobs (y group, x slice) per run of planes
   const int64_t nb = gridDim.x, blk = blockIdx.x;
   const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;  // XCD-aware (k_cg_f1_carry)
-  const int64_t runs = nb > jpr ? nb / jpr : 1;
+  const int64_t runs = tr.runs3 > 0 ? tr.runs3 : (nb > jpr ? nb / jpr : 1);
   const int64_t chunk = (nl + runs - 1) / runs;
   const int32_t ext32 = (int32_t)v.ext_len;
   constexpr bool ntl = false;  // plain loads (non-temporal measured slower: 281 vs 302 it/s 2-D)
@@ -2038,7 +2038,7 @@ __global__ __launch_bounds__(256) void k_dia_runs(uint64_t* __restrict__ dpat, i
 // kw = 0, one wave per job; k_cg_carry_ar3: kw waves per job, their slice columns)
 __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
                                                     int64_t ext_len, int64_t grid, int kw, int64_t ln,
-                                                    int band, int64_t band_h,
+                                                    int band, int64_t band_h, int runs3,
                                                     unsigned long long* __restrict__ fails) {
   const int64_t waves = kw > 0 ? kw : 1;
   int64_t jobs, runs, chunk;
@@ -2046,7 +2046,7 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
     jobs = carry_jobs(grid * kWaves, ss, nl, band, band_h, runs, chunk);
   } else {
     const int64_t jpr = (ln / kw) * (ln / 64);
-    runs = grid > jpr ? grid / jpr : 1;
+    runs = runs3 > 0 ? runs3 : (grid > jpr ? grid / jpr : 1);
     jobs = jpr * runs;
     chunk = (nl + runs - 1) / runs;
   }
@@ -2072,15 +2072,29 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
 
 }  // namespace
 
+int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl) {
+  if (nb <= 0 || jpr <= 0 || nl <= 0) return 1;
+  int32_t best = 1;
+  int64_t best_cost = INT64_MAX;
+  for (int64_t r = 1; r <= 64 && (r == 1 || nl / r >= 4); ++r) {
+    const int64_t rounds = (jpr * r + nb - 1) / nb, cost = rounds * ((nl + r - 1) / r + 3);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = (int32_t)r;
+    }
+  }
+  return best;
+}
+
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream, int band, int band_h) {
+                            int32_t ln, hipStream_t stream, int band, int band_h, int runs3) {
   MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && (kw == 0 || (ln % 64 == 0 && ln % kw == 0)),
             "lean check: bad launch geometry");
   unsigned long long* f = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&f), sizeof(unsigned long long), stream), "device malloc failed(lean)");
   MCG_HIP(hipMemsetAsync(f, 0, sizeof(unsigned long long), stream), "device memset failed");
   hipLaunchKernelGGL(k_lean_check, dim3(64), dim3(256), 0, stream, dpat, ss, nl, ext_len, (int64_t)grid, kw,
-                     (int64_t)ln, band, (int64_t)band_h, f);
+                     (int64_t)ln, band, (int64_t)band_h, runs3, f);
   MCG_HIP(hipGetLastError(), "kernel launch failed(lean check)");
   unsigned long long h = 0;
   MCG_HIP(hipMemcpyAsync(&h, f, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");

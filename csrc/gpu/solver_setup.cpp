@@ -667,9 +667,17 @@ void GpuCgSolver::setup() {
     MCG_CHECK(opt_.form.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
               "3-D: dia4, N a multiple of 64 and of carry3_kw)");
-    // 4 waves per SIMD (one round of resident blocks)
-    if (ar3_) g_all_ = std::max(1, ncu_ * (diav3_ ? 8 : 16) / kw);
+    // 4 waves per SIMD (one round of resident blocks; diav 3-D: 2).  Runs of planes per job column:
+    // as many as make the jobs fill whole rounds of those blocks (a launch of 224 blocks over 256
+    // jobs ran a second round for 32 of them: the 44 % that reserve_cus = 32 cost at 512^3,
+    // profiles/r3_cumask_probe.md; 7 runs of 73 planes fill 8 rounds exactly)
+    if (ar3_) {
+      g_all_ = std::max(1, ncu_ * (diav3_ ? 8 : 16) / kw);
+      const int64_t jpr = (int64_t)(carry_lo2_ / kw) * (carry_lo2_ / 64);
+      tr_all_.runs3 = kern::carry3_runs(g_all_, jpr, n / gl);
+    }
     info_.ar3_kw = ar3_ ? kw : 0;
+    info_.ar3_runs = ar3_ ? tr_all_.runs3 : 0;
     info_.carry_xchg = info_.carry && carry_lo2_ > 0 &&
                        kern::carry_block_exchange_ok(info_.spmv_param, carry_lo2_, gl / 64);
   }
@@ -714,20 +722,15 @@ void GpuCgSolver::setup() {
       if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
     }
     if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, ar3_ ? info_.ar3_kw : 0,
-                                  ar3_ ? carry_lo2_ : 0, s0_) == 0) {
+                                  ar3_ ? carry_lo2_ : 0, s0_, 0, 0, ar3_ ? tr_all_.runs3 : 0) == 0) {
       lean_only_ = true;
       g_all_ = g;
     }
   }
   if (p3_ && diav3_ && ar3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
-    // 3-D diav: every run of the launch's job decomposition (k_cg_carry_ar3) >= 3 planes
-    // (small grids: fewer blocks until the runs hold >= 8 planes, so the 3-plane prologues stay a
-    // small share of each run)
-    const int64_t ss = tr_all_.strip, nl = (n + 63) / 64 / ss, G = carry_lo2_ / 64;
-    const int64_t jpr = (carry_lo2_ / info_.ar3_kw) * G;
-    auto runs_of = [&](int64_t nb) { return nb > jpr ? nb / jpr : (int64_t)1; };
-    while (g_all_ > jpr && (nl + runs_of(g_all_) - 1) / runs_of(g_all_) < 8) g_all_ = std::max<int64_t>(jpr, g_all_ / 2);
-    const int64_t runs = runs_of(g_all_), chunk = (nl + runs - 1) / runs;
+    // 3-D diav: every run of the launch's job decomposition (k_cg_carry_ar3, tr_all_.runs3) >= 3 planes
+    const int64_t ss = tr_all_.strip, nl = (n + 63) / 64 / ss;
+    const int64_t runs = std::max<int32_t>(1, tr_all_.runs3), chunk = (nl + runs - 1) / runs;
     bool all = nl >= 4;
     for (int64_t r = 0; r < runs && all; ++r) {
       const int64_t l0 = r * chunk, l1 = std::min(nl, l0 + chunk);
@@ -855,8 +858,10 @@ void GpuCgSolver::setup() {
   }
   if (ar3_) {  // r rw, p rw 32; x 12; Ap of 2 of kw lines written + read, edge rows 0.5; dia4 codes 3.5
     // three-term form: p_{k-1}, p_{k-2} read + p_k written 24, x 8, r + Ap of the outer lines / edges
-    info_.bytes_per_iter_model = (double)dia4_.bytes() + ((p3_ ? 32.5 : 44.5) + (p3_ ? 24.0 : 16.0) / info_.ar3_kw) * n;
-    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes();
+    // (diav 3-D: the four per-row value arrays, 32 B, instead of the codes)
+    const double streamed = diav3_ ? 32.0 * n : (double)dia4_.bytes();
+    info_.bytes_per_iter_model = streamed + ((p3_ ? 32.5 : 44.5) + (p3_ ? 24.0 : 16.0) / info_.ar3_kw) * n;
+    info_.device_bytes = matrix_bytes + rp64_.bytes() + b_.bytes() + dia4_.bytes() + cv_.bytes();
     for (DeviceBuffer<double>* v : vectors_()) info_.device_bytes += v->bytes();
   } else if (ar_) {  // r rw, p rw 32 B; x rw 16 + p_{k-2} 8 every second pass = 12; edge Ap 0.25; + the codes it streams
     // dia4 codes; the three-term pass streams none over its lean runs (uniform slices)

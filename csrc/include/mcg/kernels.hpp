@@ -66,6 +66,9 @@ struct TileRanges {
   // (no ghost line is read), band 2 = the runs of the band_h lines at each end of the rank (the
   // ghost-adjacent lines, after the halo lands); 0 = every line in one launch
   int32_t band = 0, band_h = 0;
+  // 3-D plane carry: runs of planes per job column (> 0: chosen at setup by carry3_runs, so the
+  // jobs fill whole rounds of the launch's blocks); 0 = blocks / jobs-per-run (at least 1)
+  int32_t runs3 = 0;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);
@@ -315,8 +318,11 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
 // Runs of a line (kw = 0, 2-D) / plane (kw = waves per block, 3-D, ln = N) carry launch of `grid`
 // blocks over ss * nl slices that do not qualify for the lean step (SellDev::dpat); 0 lets the
 // three-term passes launch their lean-only kernels (`lean`).  Synchronises the stream.
+// The 3-D plane carry's run count (TileRanges::runs3) for `nb` blocks, `jpr` jobs per run and nl
+// planes: the R whose job rounds x (planes per run + the 3-plane prologue) is least (ties: fewer runs)
+int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl);
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream, int band = 0, int band_h = 0);
+                            int32_t ln, hipStream_t stream, int band = 0, int band_h = 0, int runs3 = 0);
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals), 5 SELL-64/diav (S.cvd / cve / cvs,
 // variable coefficients; lean runs stream them: every run of >= 3 lines).  p3 (dia4): three-term form --
 // r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p buffers, r stored only at the slices' edge rows

@@ -75,6 +75,7 @@ struct SolverInfo {
   double dia_uniform = 0.0;  // dia4 slices whose 64 rows share one value pattern (no codes streamed; PassForm::dia_uniform)
   bool lean_only = false;    // every run of the three-term carry takes the lean step (lean-only kernels)
   int ar3_kw = 0;        // 3-D Ap-recomputing plane carry: waves (grid lines) per block; 0 = not in use
+  int ar3_runs = 0;      // ... runs of planes per job column (kern::carry3_runs)
   bool carry_xchg = false;  // 3-D plane carry: the +-N rows of a block's inner waves exchanged through LDS
   int placement_sets = 1;       // vector placements timed at setup (CgOptions::placement_tries)
   double placement_gain = 1.0;  // slowest / fastest of the timed placements (the fastest is kept)

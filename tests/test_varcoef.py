@@ -62,3 +62,18 @@ def test_varcoef_cpu_oracle_converges_and_names(mcg):
     assert mcg.make_problem("poisson3d", n=4, coef=1).native().name == "poisson3d-varcoef"
     with pytest.raises(Exception):
         mcg.make_problem("randspd", rows=100, band=4, coef=1).native()
+
+
+def test_plane_carry_run_count_fills_rounds(mcg):
+    """kern::carry3_runs (the 3-D plane carry's runs per job column, setup's choice): 512^3 with all
+    256 CUs keeps one run (one job per block); 224 CUs (reserve_cus = 32) take 7 runs, whose 1792
+    jobs fill 8 rounds exactly instead of 256 jobs running a second round for 32 blocks; a grid
+    with fewer jobs than blocks splits its planes (384^3: 144 jobs per run)."""
+    k = mcg.native().kernels
+    assert k.carry3_runs(256, 256, 512) == 1
+    assert k.carry3_runs(224, 256, 512) == 7
+    assert k.carry3_runs(256, 64, 256) == 4  # the old rule (blocks / jobs) where it already fit
+    r = k.carry3_runs(256, 144, 384)
+    rounds = -(-144 * r // 256)
+    assert r > 1 and rounds * (-(-384 // r) + 3) < 384 + 3
+    assert k.carry3_runs(256, 8, 64) <= 16  # runs keep >= 4 planes
