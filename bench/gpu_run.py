@@ -202,6 +202,17 @@ def recipes(a) -> dict:
                                  f"--graphs 1 --overlaps 1 --fat 1 --delays 10 --halo-us 30 --iters 640 "
                                  f"--reserve-cus 0,32 --halo-ahead 0,1") for gg in (16384, 4096)
         ],
+        # r4: the 3-D plane carry's runs per job column (carry3_runs) with CUs withheld, and a
+        # non-power-of-two grid whose jobs do not fill the blocks
+        "runs3": [
+            (f"p{g}_rc{rc}", 300, bench(f"--problem poisson3d --grid {g} --steps 64 --warmup 8 --phases 0 "
+                                        f"--set reserve_cus={rc}"))
+            for g in (512, 384) for rc in (0, 32)
+        ] + [
+            (f"p{g}_rc{rc}_r3rule", 300, bench(f"--problem poisson3d --grid {g} --steps 64 --warmup 8 --phases 0 "
+                                               f"--set reserve_cus={rc} --set carry3_runs=0"))
+            for g, rc in ((512, 32), (384, 0))
+        ],
         # the distributed path at headline sizes as P in-process ranks on one GPU (r3_rehearse_lean.sh)
         "rehearse": [
             ("r16384", 600, f"{PY} bench/rehearse_ranks.py --n 16384 --iters 40 --world 1 2 4 8 --no-overlap"),

@@ -674,7 +674,7 @@ void GpuCgSolver::setup() {
     if (ar3_) {
       g_all_ = std::max(1, ncu_ * (diav3_ ? 8 : 16) / kw);
       const int64_t jpr = (int64_t)(carry_lo2_ / kw) * (carry_lo2_ / 64);
-      tr_all_.runs3 = kern::carry3_runs(g_all_, jpr, n / gl);
+      tr_all_.runs3 = opt_.form.carry3_runs < 0 ? kern::carry3_runs(g_all_, jpr, n / gl) : opt_.form.carry3_runs;
     }
     info_.ar3_kw = ar3_ ? kw : 0;
     info_.ar3_runs = ar3_ ? tr_all_.runs3 : 0;
@@ -730,7 +730,9 @@ void GpuCgSolver::setup() {
   if (p3_ && diav3_ && ar3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
     // 3-D diav: every run of the launch's job decomposition (k_cg_carry_ar3, tr_all_.runs3) >= 3 planes
     const int64_t ss = tr_all_.strip, nl = (n + 63) / 64 / ss;
-    const int64_t runs = std::max<int32_t>(1, tr_all_.runs3), chunk = (nl + runs - 1) / runs;
+    const int64_t jpr = (int64_t)(carry_lo2_ / info_.ar3_kw) * (carry_lo2_ / 64);
+    const int64_t runs = tr_all_.runs3 > 0 ? tr_all_.runs3 : (g_all_ > jpr ? g_all_ / jpr : 1);
+    const int64_t chunk = (nl + runs - 1) / runs;
     bool all = nl >= 4;
     for (int64_t r = 0; r < runs && all; ++r) {
       const int64_t l0 = r * chunk, l1 = std::min(nl, l0 + chunk);

@@ -53,12 +53,13 @@ struct PassForm {
                              // in blocks of 1024 owned by one wave, columns in segments of 2^tile_seg_log2, every
                              // wave sweeping the segments together so the gathers of p hit the L2); -1 = auto (the
                              // scrambled random SPD, or a non-stencil user matrix on the all-gather layout), 0 = off
-  int tile_seg_log2 = 19;    // tiles: column segment = 2^k doubles (19: 4 MiB of p = an XCD's L2; at a P = 8 rank's
-                             // share of the scrambled config 5: 17 / 18 / 19 / 20 / 21 -> 8.5 / 12.2 / 14.0 / 11.2
-                             // / 8.5 it/s, profiles/r3_config5_scrambled.md)
-  int tile_pace = 2;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
+  int tile_seg_log2 = 18;    // tiles: column segment = 2^k doubles (18: 2 MiB of p, half an XCD's L2; at a P = 8
+                             // rank's share of the scrambled config 5 with step-flag pacing: 17 / 18 / 19 -> 18.5 /
+                             // 19.3-19.5 / 17.5 it/s, profiles/r4/c5; r3's counter pacing peaked at 19: 14.0)
+  int tile_pace = 4;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
                              // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest);
-                             // 3 / 4 = as 1 / 2, the waiters polling a step flag instead of the arrival counter
+                             // 3 / 4 = as 1 / 2, the waiters polling a step flag (8 replicas) instead of the arrival
+                             // counter, whose line every arrival writes (4: 17.5 vs 14.3 it/s for 2 at 2^19)
   int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
   int tile_pace_slack = 1;   // tiles, tile_pace 2 / 4: a workgroup waits for all but this many eighths of its group
   int tile_prefetch = 0;     // tiles: each workgroup touches its share of the next segment before the pacing wait
@@ -92,6 +93,8 @@ struct PassForm {
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
                              // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
                              // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)
+  int carry3_runs = -1;      // 3-D plane carry: runs of planes per job column (-1 auto: kern::carry3_runs, whole
+                             // rounds of blocks; 0 = blocks / jobs per run, the r3 rule; > 0 fixed)
   int halo_hide = 0;         // 2-D lean line carry at P > 1 with a CU-free halo (Communicator::halo_cu_free: copy
                              // engines): the pass runs as the interior band (no ghost read) while the ghosts
                              // arrive, then the band_h = 4 lines at each end of the rank; the halo of the next

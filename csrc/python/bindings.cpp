@@ -238,6 +238,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(p3)
       MCG_FORM_PROP(dia_uniform)
       MCG_FORM_PROP(carry3_kw)
+      MCG_FORM_PROP(carry3_runs)
       MCG_HOOK_PROP(fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)

@@ -192,16 +192,16 @@ def test_null_comm_rank_share_takes_the_split_pass(mcg):
 SCR = dict(rows=60000, band=24, density=0.5, scramble=1)
 
 
-@pytest.mark.parametrize("seg,pace", [(19, 2), (12, 1), (12, 0)])
+@pytest.mark.parametrize("seg,pace", [(19, 2), (18, 4), (12, 1), (12, 0), (12, 3), (12, 4)])
 def test_tiles_scrambled_matches_cpu(mcg, seg, pace):
     """The scrambled family takes the tiles SpMV by default; seg = 12 cuts p into 15 segments of 4096
-    doubles (many tiles per row block), strictly paced or unpaced; the solve matches the CPU oracle
-    and ||b - A x||."""
+    doubles (many tiles per row block), strictly paced, step-flag paced (3 / 4, the default 4) or
+    unpaced; the solve matches the CPU oracle and ||b - A x||."""
     spec = mcg.make_problem("randspd", **SCR)
     cpu = _cpu(mcg, spec)
     s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, check_every=8, tile_seg_log2=seg, tile_pace=pace)
     assert s.info["tiles"] and s.info["pmat"] and s.info["format"] == "tiles"
-    assert s.info["tile_segments"] == (1 if seg == 19 else 15)
+    assert s.info["tile_segments"] == (1 if seg >= 18 else 15)
     out = s.solve()
     assert out["converged"] and abs(out["iterations"] - cpu["iterations"]) <= 1
     np.testing.assert_allclose(out["x_local"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
