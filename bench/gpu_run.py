@@ -156,6 +156,18 @@ def recipes(a) -> dict:
                             ("s17_pf", ["tile_pace=4", "tile_seg_log2=17", "tile_prefetch=1"]),
                             ("s18_pf_again", ["tile_pace=4", "tile_seg_log2=18", "tile_prefetch=1"]))
         ],
+        # r4: tiles with fp32-exact values (8 B / entry) vs fp64 storage, the 101 GB share and the ~200 GB one
+        "c5v32": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'tiles'"),
+            ("v32", 400, bench(f"{c5} --steps 6 --warmup 2")),
+            ("v64", 400, bench(f"{c5} --steps 6 --warmup 2 --set tile_vals32=0")),
+            ("v32_priced", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330")),
+            ("v32_again", 400, bench(f"{c5} --steps 6 --warmup 2")),
+        ] + counters("v32_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
+          + counters("v32_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"),
+        "c5v32big": [
+            ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2")),
+        ],
         # config 5 at ~200 GB per GPU and with the all-gather priced (DelayComm)
         "c5big": [
             ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2 "

@@ -10,8 +10,9 @@
 // (their running sums live in LDS), and ALL waves sweep the segments in the same order: while the
 // chip works on segment g, the XCDs' L2s hold p[g S, (g + 1) S) and the gathers hit.
 //
-// Storage (12 B per nonzero, like CSR): tile (b, g) = the nonzeros of row block b whose column is
-// in segment g, a flat list of (row in block << 22 | column in segment) and the value;
+// Storage (12 B per nonzero, like CSR; 8 B when every value is exactly an fp32, tile_vals32): tile
+// (b, g) = the nonzeros of row block b whose column is in segment g, a flat list of (row in block <<
+// 22 | column in segment) and the value;
 // tptr[b * G + g] .. tptr[b * G + g + 1].  A wave spreads its tile over its 64 lanes and adds every
 // product into the row's LDS slot (ds_add_f64); the wave owns those slots, so no other wave's adds
 // interleave with its own, batch after batch in program order.  Inside ONE batch two lanes can hold
@@ -106,19 +107,22 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
   __syncthreads();
 }
 
-// one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
+// one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once).  V32: the values
+// are stored as fp32 (exact, checked at build time) and widened here; everything after is fp64
+template <bool V32>
 __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
 #pragma unroll
   for (int u = 0; u < kTU; ++u) {
     const int64_t e = k + u * 64;
     q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
-    v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
+    if constexpr (V32) v[u] = e < hi ? (double)__builtin_nontemporal_load(&T.vals32[e]) : 0.0;
+    else v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
   }
 }
 
 // MODE 0: the split pass's SpMV (Ap_k = A p_k + the 4 partials + in-kernel reduction, as
 // k_split_spmv); MODE 1: plain y = A x (true residual, ops)
-template <int MODE>
+template <int MODE, bool V32>
 __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
     if (active) {
       lo = T.tptr[b * G];
       hi = T.tptr[b * G + 1];
-      tile_batch_load(T, lo + lane, hi, q, v);
+      tile_batch_load<V32>(T, lo + lane, hi, q, v);
     }
     for (int g = 0; g < G; ++g, ++step) {
       int64_t hi_next = hi;
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
         for (int64_t k = lo + lane; k < hi; k += kTU * 64) {
           uint32_t qn[kTU];
           double vn[kTU], x[kTU];
-          tile_batch_load(T, k + kTU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
+          tile_batch_load<V32>(T, k + kTU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
 #pragma unroll
           for (int u = 0; u < kTU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
 #pragma unroll
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
         // the next tile's first batch loads while the workgroup waits at the pacing step
         if (g + 1 < G) {
           hi_next = T.tptr[b * G + g + 2];
-          tile_batch_load(T, hi + lane, hi_next, q, v);
+          tile_batch_load<V32>(T, hi + lane, hi_next, q, v);
         }
       }
       const double* nxt = nullptr;  // the segment the group starts next (prefetched while it waits)
@@ -236,18 +240,22 @@ struct CsrSrc {  // a user matrix's rows on the device (local CSR, ext columns)
   }
 };
 
-// FILL = false: tptr[b * G + g + 1] = entries of tile (b, g); FILL = true: write the tiles (tptr =
-// exclusive offsets).  Lanes take rows rr = lane, lane + 64, ... of the block in lockstep; the order
-// of one LDS atomic's same-address lanes (observed fixed, as above) orders a batch's appends.
-template <bool FILL, class Src>
+// FILL = false: tptr[b * G + g + 1] = entries of tile (b, g), and *inexact += the entries whose value
+// does not survive fp64 -> fp32 -> fp64 (the fp32 value storage is taken only when none does);
+// FILL = true: write the tiles (tptr = exclusive offsets; values as V).  Lanes take rows rr = lane,
+// lane + 64, ... of the block in lockstep; the order of one LDS atomic's same-address lanes
+// (observed fixed, as above) orders a batch's appends.
+template <bool FILL, class V, class Src>
 __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, int seg_shift, int64_t* __restrict__ tptr,
-                                                    uint32_t* __restrict__ idx, double* __restrict__ vals) {
+                                                    uint32_t* __restrict__ idx, V* __restrict__ vals,
+                                                    unsigned long long* __restrict__ inexact) {
   extern __shared__ int cnt[];
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
   for (int g = lane; g < G; g += 64) cnt[g] = 0;
   __syncthreads();
   const uint32_t mask = (1u << seg_shift) - 1u;
+  unsigned bad = 0;
   for (int rr = lane; rr < kTileB; rr += 64) {
     const int64_t i = b * kTileB + rr;
     if (i >= n) break;
@@ -257,13 +265,17 @@ __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, i
       if constexpr (FILL) {
         const int64_t dst = tptr[b * G + g] + pos;
         idx[dst] = ((uint32_t)rr << 22) | ((uint32_t)ec & mask);
-        vals[dst] = v;
+        vals[dst] = (V)v;
+      } else {
+        bad += (double)(float)v != v;  // NaN counts as inexact too
       }
     });
   }
   __syncthreads();
-  if constexpr (!FILL)
+  if constexpr (!FILL) {
     for (int g = lane; g < G; g += 64) tptr[b * G + g + 1] = cnt[g];
+    if (inexact != nullptr && bad) atomicAdd(inexact, (unsigned long long)bad);
+  }
 }
 
 }  // namespace
@@ -278,7 +290,7 @@ TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
 
 int tiles_grid(int ncu) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_tiles<0>), 256, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_tiles<0, false>), 256, 0) !=
           hipSuccess ||
       per_cu < 1)
     per_cu = 1;
@@ -288,31 +300,34 @@ int tiles_grid(int ncu) {
 
 namespace {
 template <class Src>
-void tiles_build_impl(const Src& src, int64_t n, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,
-                      bool fill, hipStream_t st) {
+void tiles_build_impl(const Src& src, int64_t n, const TilesGeometry& geo, const TilesOut& o, bool fill, hipStream_t st) {
   MCG_CHECK(geo.G <= kTileMaxSegments, "tiles: too many column segments for the LDS counters");
   MCG_CHECK(geo.seg_shift <= 22, "tiles: segments are at most 2^22 columns");
+  MCG_CHECK(!fill || (o.vals != nullptr) != (o.vals32 != nullptr), "tiles: fill needs exactly one value array");
   if (geo.nblocks == 0) return;
   const size_t lds = (size_t)geo.G * sizeof(int);
-  if (fill)
-    hipLaunchKernelGGL((k_tiles_build<true, Src>), dim3((unsigned)geo.nblocks), dim3(64), lds, st, src, n, geo.G,
-                       geo.seg_shift, tptr, idx, vals);
+  const dim3 grid((unsigned)geo.nblocks);
+  if (!fill)
+    hipLaunchKernelGGL((k_tiles_build<false, double, Src>), grid, dim3(64), lds, st, src, n, geo.G, geo.seg_shift,
+                       o.tptr, o.idx, nullptr, o.inexact);
+  else if (o.vals32 != nullptr)
+    hipLaunchKernelGGL((k_tiles_build<true, float, Src>), grid, dim3(64), lds, st, src, n, geo.G, geo.seg_shift,
+                       o.tptr, o.idx, o.vals32, nullptr);
   else
-    hipLaunchKernelGGL((k_tiles_build<false, Src>), dim3((unsigned)geo.nblocks), dim3(64), lds, st, src, n, geo.G,
-                       geo.seg_shift, tptr, idx, vals);
+    hipLaunchKernelGGL((k_tiles_build<true, double, Src>), grid, dim3(64), lds, st, src, n, geo.G, geo.seg_shift,
+                       o.tptr, o.idx, o.vals, nullptr);
   MCG_HIP(hipGetLastError(), "kernel launch failed(tiles_build)");
 }
 }  // namespace
 
 void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
-                     const int64_t* rp64, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,
-                     bool fill, hipStream_t st) {
-  tiles_build_impl(GenSrc{s, row_begin, col_lo, pad, rp64}, n, geo, tptr, idx, vals, fill, st);
+                     const int64_t* rp64, const TilesGeometry& geo, const TilesOut& out, bool fill, hipStream_t st) {
+  tiles_build_impl(GenSrc{s, row_begin, col_lo, pad, rp64}, n, geo, out, fill, st);
 }
 
 void tiles_build_csr(const int64_t* rp, const int32_t* cols, const double* cvals, int64_t n, const TilesGeometry& geo,
-                     int64_t* tptr, uint32_t* idx, double* vals, bool fill, hipStream_t st) {
-  tiles_build_impl(CsrSrc{rp, cols, cvals}, n, geo, tptr, idx, vals, fill, st);
+                     const TilesOut& out, bool fill, hipStream_t st) {
+  tiles_build_impl(CsrSrc{rp, cols, cvals}, n, geo, out, fill, st);
 }
 
 void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r, double* Ap, int64_t own_off,
@@ -321,16 +336,24 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   if (grid <= 0) return;
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-  hipLaunchKernelGGL(k_tiles<0>, dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, pstride, st,
-                     tol, first, check, rc);
+  if (T.vals32 != nullptr)
+    hipLaunchKernelGGL((k_tiles<0, true>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, pstride,
+                       st, tol, first, check, rc);
+  else
+    hipLaunchKernelGGL((k_tiles<0, false>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, pstride,
+                       st, tol, first, check, rc);
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 
 void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream) {
   if (grid <= 0 || T.nblocks == 0) return;
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-  hipLaunchKernelGGL(k_tiles<1>, dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr,
-                     0.0, 0, 0, RedCtl());
+  if (T.vals32 != nullptr)
+    hipLaunchKernelGGL((k_tiles<1, true>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr,
+                       0.0, 0, 0, RedCtl());
+  else
+    hipLaunchKernelGGL((k_tiles<1, false>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr,
+                       0.0, 0, 0, RedCtl());
   MCG_HIP(hipGetLastError(), "compute mv failed(y)");
 }
 

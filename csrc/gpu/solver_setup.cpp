@@ -264,7 +264,6 @@ void GpuCgSolver::setup() {
     tptr_.allocate(tgeo_.nblocks * tgeo_.G + 1, "A");
     MCG_HIP(hipMemsetAsync(tptr_.get(), 0, tptr_.bytes(), s0_), "device memset failed(A)");
     tidx_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
-    tvals_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
     tpace_.allocate(kern::kTilePaceWords, "A");
     DeviceBuffer<int32_t> tc;
     DeviceBuffer<double> tv;
@@ -277,17 +276,35 @@ void GpuCgSolver::setup() {
               "memcpy from host to device failed(A)");
     }
     const int64_t ntp = tgeo_.nblocks * tgeo_.G;
+    DeviceBuffer<unsigned long long> inexact(1, "A");
+    MCG_HIP(hipMemsetAsync(inexact.get(), 0, sizeof(unsigned long long), s0_), "device memset failed(A)");
+    kern::TilesOut to;
+    to.tptr = tptr_.get();
+    to.idx = tidx_.get();
+    to.inexact = inexact.get();
     for (int fill = 0; fill < 2; ++fill) {
-      if (is_user) kern::tiles_build_csr(rp64.get(), tc.get(), tv.get(), n, tgeo_, tptr_.get(), tidx_.get(), tvals_.get(), fill, s0_);
-      else kern::tiles_build_gen(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), tgeo_, tptr_.get(), tidx_.get(),
-                                 tvals_.get(), fill, s0_);
+      if (fill) {
+        // values as fp32 when every value of every rank round-trips exactly (the same matrix bits; the
+        // products and sums stay fp64): 8 instead of 12 B per entry streamed
+        unsigned long long bad = 0;
+        MCG_HIP(hipMemcpy(&bad, inexact.get(), sizeof(bad), hipMemcpyDeviceToHost), "memcpy from device to host failed(A)");
+        bool v32 = opt_.form.tile_vals32 == 1 || (opt_.form.tile_vals32 < 0 && bad == 0);
+        MCG_CHECK(opt_.form.tile_vals32 != 1 || bad == 0, "tiles: tile_vals32=1 needs every value exactly representable in fp32");
+        if (opt_.form.tile_vals32 < 0 && use_comm_ && world_ > 1) v32 = all_ranks_agree_(v32);
+        if (v32) tvals32_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
+        else tvals_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
+        to.vals = v32 ? nullptr : tvals_.get();
+        to.vals32 = v32 ? tvals32_.get() : nullptr;
+        info_.tile_vals32 = v32;
+      }
+      if (is_user) kern::tiles_build_csr(rp64.get(), tc.get(), tv.get(), n, tgeo_, to, fill, s0_);
+      else kern::tiles_build_gen(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), tgeo_, to, fill, s0_);
       if (!fill && ntp > 0) {  // tile sizes -> offsets
         DeviceBuffer<int64_t> tmp(kern::scan_tmp_elems(ntp), "A");
         kern::scan_inclusive_i64(tptr_.get() + 1, ntp, tmp.get(), s0_);
-        MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
       }
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
     }
-    MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(A)");
     int64_t tot = 0;
     MCG_HIP(hipMemcpy(&tot, tptr_.get() + ntp, sizeof(int64_t), hipMemcpyDeviceToHost),
             "memcpy from device to host failed(A)");
@@ -296,7 +313,7 @@ void GpuCgSolver::setup() {
     c8_ = false;
     info_.format = 5;
     info_.sell_fill = 1.0;
-    matrix_bytes = (size_t)nnz * 12 + tptr_.bytes();
+    matrix_bytes = (size_t)nnz * (info_.tile_vals32 ? 8 : 12) + tptr_.bytes();
   } else if (opt_.format == 1) {
     // ---- SELL-64, generated directly (no CSR intermediate: peak memory = the SELL arrays) ----
     const int64_t ns = (n + 63) / 64;

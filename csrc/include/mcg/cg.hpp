@@ -63,6 +63,10 @@ struct PassForm {
   int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
   int tile_pace_slack = 1;   // tiles, tile_pace 2 / 4: a workgroup waits for all but this many eighths of its group
   int tile_prefetch = 0;     // tiles: each workgroup touches its share of the next segment before the pacing wait
+  int tile_vals32 = -1;      // tiles: values stored as fp32 (8 instead of 12 B per entry streamed) when every value
+                             // round-trips fp64 -> fp32 -> fp64 exactly, checked while the tiles are counted: the
+                             // same matrix, products and sums in fp64; -1 = auto (when exact on every rank), 0 = off,
+                             // 1 = required (an inexact value is an error)
   int tile_pace_sleep = 8;   // tiles: s_sleep units (64 clocks each) between two polls of a waiting workgroup
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an

@@ -382,7 +382,9 @@ struct TilesGeometry {
 struct TilesDev {
   const int64_t* tptr = nullptr;  // nblocks * G + 1
   const uint32_t* idx = nullptr;
-  const double* vals = nullptr;
+  const double* vals = nullptr;    // fp64 values, or
+  const float* vals32 = nullptr;   // values stored as fp32 (every value round-trips fp64 -> fp32 -> fp64 exactly,
+                                   // checked at build time; products and sums stay fp64): 8 instead of 12 B/entry
   int64_t n_rows = 0, nblocks = 0;
   int G = 0, seg_shift = 18;
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
@@ -396,12 +398,19 @@ struct TilesDev {
 };
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
 int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
-// count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0) then fill
+// count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0; *inexact += the
+// entries whose value is not exactly an fp32) then fill (into vals, or vals32 when vals is null)
+struct TilesOut {
+  int64_t* tptr = nullptr;
+  uint32_t* idx = nullptr;
+  double* vals = nullptr;
+  float* vals32 = nullptr;
+  unsigned long long* inexact = nullptr;  // count pass
+};
 void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
-                     const int64_t* rp64, const TilesGeometry& geo, int64_t* tptr, uint32_t* idx, double* vals,
-                     bool fill, hipStream_t st);
+                     const int64_t* rp64, const TilesGeometry& geo, const TilesOut& out, bool fill, hipStream_t st);
 void tiles_build_csr(const int64_t* rp, const int32_t* cols, const double* cvals, int64_t n, const TilesGeometry& geo,
-                     int64_t* tptr, uint32_t* idx, double* vals, bool fill, hipStream_t st);
+                     const TilesOut& out, bool fill, hipStream_t st);
 // the split pass's SpMV on tiles (same contract as cg_split_spmv part 0)
 void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r, double* Ap, int64_t own_off,
                          double* partials, int pstride, int grid, CgState* st, double tol, int first, int check,

@@ -57,6 +57,7 @@ struct SolverInfo {
   bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
   bool tiles = false;         // ... its SpMV on L2-segment COO tiles (CgOptions::tiles)
   int tile_segments = 0;      // column segments of the tiles (G)
+  bool tile_vals32 = false;   // ... the tiles' values stored as fp32 (every value exact; CgOptions::tile_vals32)
   int sigma = 0;              // SELL-C-sigma window (rows) of a user matrix; 0 = slices in row order
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
@@ -198,12 +199,14 @@ class GpuCgSolver {
   DeviceBuffer<int64_t> tptr_;
   DeviceBuffer<uint32_t> tidx_;
   DeviceBuffer<double> tvals_;
+  DeviceBuffer<float> tvals32_;  // the values as fp32 when every one is exact (tile_vals32)
   DeviceBuffer<unsigned> tpace_;
   kern::TilesDev tiles_view() const {
     kern::TilesDev t;
     t.tptr = tptr_.get();
     t.idx = tidx_.get();
     t.vals = tvals_.get();
+    t.vals32 = tvals32_.get();
     t.n_rows = L_.n_local();
     t.nblocks = tgeo_.nblocks;
     t.G = tgeo_.G;

@@ -225,6 +225,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(tile_pace_lag)
       MCG_FORM_PROP(tile_pace_slack)
       MCG_FORM_PROP(tile_pace_sleep)
+      MCG_FORM_PROP(tile_vals32)
       MCG_FORM_PROP(tile_prefetch)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
@@ -471,6 +472,7 @@ PYBIND11_MODULE(_C, m) {
         d["pmat"] = i.pmat;
         d["tiles"] = i.tiles;
         d["tile_segments"] = i.tile_segments;
+        d["tile_vals32"] = i.tile_vals32;
         d["sigma"] = i.sigma;
         d["sell_fill"] = i.sell_fill;
         d["allgather"] = i.allgather;

@@ -333,3 +333,32 @@ def test_tiles_row_colliding_batches_run_to_run_bitwise(mcg):
     for o in outs[1:]:
         assert o["rnorm"] == outs[0]["rnorm"]
         np.testing.assert_array_equal(o["x_local"], outs[0]["x_local"])
+
+
+def test_tiles_fp32_exact_values_bitwise_and_auto(mcg):
+    """tile_vals32: the scrambled family's values (1 - k / 2^20 and integer diagonals) are all exact
+    fp32, so the tiles store them in 4 bytes by default (8 instead of 12 B per entry); the solve is
+    bit for bit the fp64-storage solve (the same matrix, products and sums in fp64).  A user matrix
+    with a value that is not an fp32 keeps fp64 storage, and requiring fp32 for it is an error."""
+    import scipy.sparse as sp
+
+    spec = mcg.make_problem("randspd", **SCR)
+    kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=30, tile_seg_log2=12)
+    a = mcg.CGSolver(spec, tiles=1, **kw)
+    b = mcg.CGSolver(spec, tiles=1, tile_vals32=0, **kw)
+    assert a.info["tile_vals32"] and not b.info["tile_vals32"]
+    ra, rb = a.solve(), b.solve()
+    assert ra["rnorm"] == rb["rnorm"]
+    np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
+    assert a.true_residual_norm() == b.true_residual_norm()
+
+    n = 5000
+    T = sp.diags([-1.0, 2.5, -1.0], [-7, 0, 7], shape=(n, n)).tolil()
+    T[3, 10] = T[10, 3] = -0.1  # not an fp32
+    T[3, 3] = T[10, 10] = 2.6
+    prob = mcg.csr_problem(T.tocsr(), b=np.ones(n))
+    u = mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tol=1e-10, tile_seg_log2=12)
+    assert u.info["tiles"] and not u.info["tile_vals32"]
+    assert u.solve()["converged"]
+    with pytest.raises(Exception, match="tile_vals32"):
+        mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tile_seg_log2=12, tile_vals32=1)
