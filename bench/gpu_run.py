@@ -249,6 +249,20 @@ def recipes(a) -> dict:
                                       f"--set lean_depth={d} --set lean_bpc={b}"))
             for d in (3, 4, 6) for b in (2, 4, 8)
         ] + [("auto_again", 200, bench("--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify"))],
+        # r4: packed slice edges (lean_depth 13: depth 3 at 5 waves / SIMD, 14: depth 4 at 4) at 4096^2
+        # and 16384^2 against the default lean kernels, interleaved
+        "edge": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'packed_edges'"),
+        ] + [
+            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify {kv}"))
+            for rep in (1, 2)
+            for tag, kv in (("auto", ""), ("e13", "--set lean_depth=13 --set lean_bpc=5"),
+                            ("e14", "--set lean_depth=14 --set lean_bpc=4"), ("d3b5", "--set lean_bpc=5"))
+        ] + [
+            (f"g16384_{tag}", 200, bench(f"--phases 0 --no-verify {kv}"))
+            for tag, kv in (("auto", ""), ("e13", "--set lean_depth=13 --set lean_bpc=5"),
+                            ("e14", "--set lean_depth=14"))
+        ] + stats("edge_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=13 --set lean_bpc=5"),
         # r4: stream memory operations (write / wait value) around a NoCU copy, eager and captured
         "streamop": [
             ("probe", 240, f"{PY} -c 'import torch, json, cuda_mpi_parallel_amd as m; torch.cuda.init(); "

@@ -226,7 +226,12 @@ __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, 
 // LEAN > 0: lean-only kernel (every run checked at setup) for at least LEAN waves per SIMD
 // BIG (lean kernels): the rank's vectors exceed 2^29 doubles, so each run re-bases its global pointers
 // (64-bit, scalar registers) at its own first lines and keeps 32-bit byte offsets inside the run
-template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false>
+// EP (lean dia4 kernels): packed edges -- the three values a slice-edge lane needs per line (its
+// neighbour row's r_{k-1}, Ap_{k-1}, p_{k-1}) arrive in ONE load per line, lanes 0 / 15 / 7 fetching
+// lane 0's and lanes 63 / 48 / 56 lane 63's, and move to lanes 0 / 63 by row_mirror /
+// row_half_mirror DPP (one move serves both ends).  A line in flight then holds 2 instead of 6
+// VGPRs of edges, which buys a wave per SIMD (LEAN 5) or a line of prefetch depth
+template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
@@ -409,12 +414,33 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             q.p = g_ld(po_, o);
             return q;
           };
+          // EP: lane roles (kernel comment) -- r: lanes 0 / 63, Ap: 15 / 48, p: 7 / 56; the other lanes
+          // repeat lane 0's r load (the same address: no extra traffic).  Per lane a 64-bit base (reo,
+          // eo or po_) and the byte offset of line 0 plus a per-line stride (SB, or LOB for p)
+          const int erole = !EP ? 0 : (lane == 15 || lane == 48) ? 1 : (lane == 7 || lane == 56) ? 2 : 0;
+          const bool eright = lane >= 32;
+          const bool erz = eright ? z63 : z0;
+          const uint32_t eoc = eright ? (erz ? 16u : 24u) : (erz ? 8u : 0u);
+          const uint32_t eop = eright ? (erz ? 512u : 520u) : (erz ? 8u : 0u);
+          const bool erole_ok = erole != 0 || lane == 0 || lane == 63;
+          const char* ebase = (const char*)(erole == 1 ? eo : erole == 2 ? po_ : reo);
+          const uint32_t eoff0 = erole == 2 ? ob0 - 8u + eop : cb0 + (erole_ok ? eoc : oc);
+          const uint32_t estr = erole == 2 ? LOB : SB;
+          auto edge_pk_ld = [&](int32_t jr, int32_t jp) {  // jr: line of the edge arrays, jp: line of po
+            const uint32_t o = eoff0 + (uint32_t)(erole == 2 ? jp : jr) * estr;
+            return *(const g_double*)((const g_char*)(const g_double*)ebase + o);
+          };
           auto edge_at = [&](int32_t j) {
             Edge q;
-            const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
-            q.r = g_ld(reo, c);
-            q.a = g_ld(eo, c);
-            q.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
+            if constexpr (EP) {
+              q.r = edge_pk_ld(rc_(j), jc(j));
+              q.a = q.p = 0.0;
+            } else {
+              const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
+              q.r = g_ld(reo, c);
+              q.a = g_ld(eo, c);
+              q.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
+            }
             return q;
           };
           // a ghost line's r_{k-1} (step()'s rghost): from the halo's p_{k-2} in p_new's ghost rows
@@ -429,10 +455,15 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           };
           auto edge_un = [&](int32_t j) {
             Edge q;
-            const uint32_t c = cb0 + (uint32_t)j * SB + oc;
-            q.r = g_ld(reo, c);
-            q.a = g_ld(eo, c);
-            q.p = g_ld(po_, line_ofs(j) - 8u + op);
+            if constexpr (EP) {
+              q.r = edge_pk_ld(j, j);
+              q.a = q.p = 0.0;
+            } else {
+              const uint32_t c = cb0 + (uint32_t)j * SB + oc;
+              q.r = g_ld(reo, c);
+              q.a = g_ld(eo, c);
+              q.p = g_ld(po_, line_ofs(j) - 8u + op);
+            }
             return q;
           };
           auto x_at = [&](int32_t j) {
@@ -440,6 +471,17 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             else return 0.0;
           };
           auto ez = [&](double e) { return e; };
+          // an edge's p_{k-1} / p_k in lanes 0 and 63 (EP: gathered from the role lanes by DPP)
+          auto e_p = [&](const Edge& q) {
+            if constexpr (EP) {
+              const double v = q.r;
+              const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x141, 0xf, 0xf, false);  // row_half_mirror
+              const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x141, 0xf, 0xf, false);
+              return __hiloint2double(hi, lo);
+            } else {
+              return q.p;
+            }
+          };
           auto stencil_u = [&](const VSet& V, double mid, double edge, double dnl, double upl) {
             const double upv = lane_up_or(mid, edge);
             const double dnv = lane_dn_or(mid, edge);
@@ -450,7 +492,16 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             sum = fma(cp, upv, sum);
             return fma(V.v[4], upl, sum);
           };
-          auto epk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };
+          auto epk = [&](const Edge& q) {
+            if constexpr (EP) {
+              const double v = q.r;
+              const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x140, 0xf, 0xf, false);  // row_mirror
+              const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x140, 0xf, 0xf, false);
+              return fma(b, e_p(q), fma(na, __hiloint2double(hi, lo), v));
+            } else {
+              return fma(b, q.p, fma(na, q.a, q.r));
+            }
+          };
           // prologue (step()'s): lines -2 .. LD - 1
           const Raw rm2 = raw_at(-2), rm1 = raw_at(-1), r0 = raw_at(0);
           Raw q[LD - 1];  // lines m + 1 .. m + LD - 1
@@ -466,14 +517,14 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           double pr_pk = 0.0;  // p_k of line -1: owned, a ghost, or none
           if (l0 >= 1) {
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
-            pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p), rm1.r));
+            pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(e_p(edm1)), rm2.p, r0.p), rm1.r));
           } else if (is_ghost(-1)) {
             pr_pk = fma(b, rm1.p, fma(na, g_ld(apo_, line_ofs(-1) + l8), rghost(-1, rm1)));
           }
           double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
           {
             const VSet V0 = l0 == 0 ? vals(WA) : VB;
-            o_rk = fma(na, stencil_u(V0, r0.p, ez(ed0.p), rm1.p, q[0].p), fma(nbp, r0.r, r0.p));
+            o_rk = fma(na, stencil_u(V0, r0.p, ez(e_p(ed0)), rm1.p, q[0].p), fma(nbp, r0.r, r0.p));
             o_pk = fma(b, r0.p, o_rk);
           }
           double o_epk = epk(ed0);
@@ -487,7 +538,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const double xn = x_at(m + LD - 1);
             double rk1 = 0.0, pk1 = 0.0;
             if (next == 1) {
-              const double t = stencil_u(Vt, q[0].p, ez(e[0].p), o_pold, q[1].p);
+              const double t = stencil_u(Vt, q[0].p, ez(e_p(e[0])), o_pold, q[1].p);
               rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
               pk1 = fma(b, q[0].p, rk1);
             } else if (CL && next == 2) {
@@ -2262,11 +2313,18 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
 #define MCG_LWD(QD, PAIR, W)                                                                                   \
   hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
                      partials, pstride, st, tol, first, check, rc)
+#define MCG_LWE(QD, PAIR, W)                                                                                   \
+  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true>), dim3(grid), dim3(kBS), 0, stream, S, v, \
+                     own_off, tr, partials, pstride, st, tol, first, check, rc)
+    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4)
+    if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
+    else if (depth == 14 && !big) { if (pair) MCG_LWE(4, true, 4); else MCG_LWE(4, false, 4); }
     // deeper prefetch (lean_depth 4 / 6: fewer waves per SIMD, more lines in flight per wave; small grids)
-    if (depth >= 6 && !big) { if (pair) MCG_LWD(6, true, 2); else MCG_LWD(6, false, 2); }
+    else if (depth >= 6 && depth < 13 && !big) { if (pair) MCG_LWD(6, true, 2); else MCG_LWD(6, false, 2); }
     else if (depth == 4 && !big) { if (pair) MCG_LWD(4, true, 3); else MCG_LWD(4, false, 3); }
     else if (depth >= 3) { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
     else { if (pair) MCG_LW(2, true); else MCG_LW(2, false); }
+#undef MCG_LWE
 #undef MCG_LWD
 #undef MCG_LW
     MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");

@@ -474,3 +474,25 @@ def test_dia_uniform_lean_runs_bitwise_3d(mcg, n, kw):
             outs.append((s.result(), s._s.x_local()))
         assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
         assert np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,depth,bpc", [(1024, 13, 5), (2048, 13, 5), (2048, 14, 4), (1024, 14, 4)])
+def test_lean_packed_edges_bitwise(mcg, n, depth, bpc):
+    """Packed edges (lean_depth 13: prefetch depth 3 at 5 waves per SIMD; 14: depth 4 at 4): a
+    slice-edge lane's three neighbour values arrive in one load per line and move to lanes 0 / 63 by
+    DPP mirrors.  The same arithmetic in the same order, so x and ||r|| are bit for bit those of the
+    default lean kernels on the same grid (lean_bpc fixes the job decomposition for both)."""
+    spec = mcg.make_problem("poisson2d", n=n, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=bpc)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=bpc, lean_depth=depth)
+    assert a.info["lean_only"] and b.info["lean_only"] and a.info["grid_a"] == b.info["grid_a"]
+    for its in (37, 38):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
+        assert np.array_equal(outs[0][1], outs[1][1])
+    assert b.solve()["converged"]
