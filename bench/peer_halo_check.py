@@ -7,6 +7,8 @@ mismatch.  The reference has no multi-process code (CUDACG.cu:87, one device); t
 north star's halo on the copy engines.
 
     python bench/peer_halo_check.py --world 2 [--n 256 --rounds 4]
+    python bench/peer_halo_check.py --world 4 --problem scrambled   # the all-gather layout (every peer's
+                                                                     # block, one copy stream per peer)
 """
 from __future__ import annotations
 
@@ -28,8 +30,12 @@ def rank_main(rank: int, a, port: int, q) -> None:
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=a.world)
     C = mcg.native()
-    spec = mcg.make_problem("poisson2d", n=a.n).native()
+    if a.problem == "scrambled":  # unstructured: the all-gather ghost layout
+        spec = mcg.make_problem("randspd", rows=a.rows, band=16, density=0.5, scramble=1).native()
+    else:
+        spec = mcg.make_problem("poisson2d", n=a.n).native()
     L = C.make_layout(spec, a.world, rank, -1)
+    assert L["allgather"] == (a.problem == "scrambled"), L["allgather"]
     ext, own, rb, nloc = L["ext_len"], L["own_off"], L["row_begin"], L["row_end"] - L["row_begin"]
     vecs = [torch.zeros(ext, dtype=torch.float64, device="cuda") for _ in range(2)]
     comm = C.PeerHaloComm(C.NullComm(rank, a.world), rank, a.world)
@@ -54,7 +60,7 @@ def rank_main(rank: int, a, port: int, q) -> None:
                 want = 1e6 * (rnd + 1) + 1e5 * k + torch.arange(gbegin, gbegin + count, dtype=torch.float64)
                 bad += int((got != want).sum())
         dist.barrier()
-    q.put((rank, bad, len(L["recvs"])))
+    q.put((rank, bad, len(L["recvs"]), bool(L["allgather"])))
     dist.destroy_process_group()
 
 
@@ -62,6 +68,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--problem", choices=["poisson2d", "scrambled"], default="poisson2d")
+    ap.add_argument("--rows", type=int, default=200000, help="scrambled: global rows")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--port", type=int, default=29531)
     ap.add_argument("--timeout", type=float, default=120.0)
@@ -80,9 +88,10 @@ def main() -> int:
             p.kill()
             p.join()
     res = sorted(q.get(timeout=5) for _ in procs) if all(p.exitcode == 0 for p in procs) else []
-    ok = bool(res) and all(b == 0 for _, b, _ in res) and all(p.exitcode == 0 for p in procs)
-    print(json.dumps({"world": a.world, "n": a.n, "rounds": a.rounds, "ok": ok,
-                      "ranks": [{"rank": r, "mismatches": b, "recv_ranges": nr} for r, b, nr in res],
+    ok = bool(res) and all(b == 0 for _, b, _, _ in res) and all(p.exitcode == 0 for p in procs)
+    print(json.dumps({"world": a.world, "problem": a.problem, "n": a.n, "rounds": a.rounds, "ok": ok,
+                      "ranks": [{"rank": r, "mismatches": b, "recv_ranges": nr, "allgather": ag}
+                                for r, b, nr, ag in res],
                       "exitcodes": [p.exitcode for p in procs]}), flush=True)
     return 0 if ok else 1
 

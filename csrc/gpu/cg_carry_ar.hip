@@ -511,9 +511,11 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           Edge e[LD - 1];  // lines m + 1 .. m + LD - 1
 #pragma unroll
           for (int d = 0; d < LD - 1; ++d) e[d] = edge_at(1 + d);
-          double xs[LD - 1];  // lines m .. m + LD - 2
+          // x chain: lines m .. m + XD - 1 (EP: one line shorter, 2 VGPRs for the 5-wave kernels)
+          constexpr int XD = EP ? LD - 2 : LD - 1;
+          double xs[XD];
 #pragma unroll
-          for (int d = 0; d < LD - 1; ++d) xs[d] = x_at(d);
+          for (int d = 0; d < XD; ++d) xs[d] = x_at(d);
           double pr_pk = 0.0;  // p_k of line -1: owned, a ghost, or none
           if (l0 >= 1) {
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             constexpr bool CL = decltype(clc)::value;
             const Raw qn = CL ? raw_at(m + LD) : raw_un(m + LD);
             const Edge en2 = CL ? edge_at(m + LD) : edge_un(m + LD);
-            const double xn = x_at(m + LD - 1);
+            const double xn = x_at(m + XD);
             double rk1 = 0.0, pk1 = 0.0;
             if (next == 1) {
               const double t = stencil_u(Vt, q[0].p, ez(e_p(e[0])), o_pold, q[1].p);
@@ -571,11 +573,12 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             for (int d = 0; d + 1 < LD - 1; ++d) {
               q[d] = q[d + 1];
               e[d] = e[d + 1];
-              xs[d] = xs[d + 1];
             }
+#pragma unroll
+            for (int d = 0; d + 1 < XD; ++d) xs[d] = xs[d + 1];
             q[LD - 2] = qn;
             e[LD - 2] = en2;
-            xs[LD - 2] = xn;
+            xs[XD - 1] = xn;
           };
           // main loop: steps whose lines m, m + 1 are inner lines and whose loads (line m + LD) stay
           // inside the rank, [m_lo, m_hi]; then the clamped tail

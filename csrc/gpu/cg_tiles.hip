@@ -121,8 +121,12 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 }
 
 // MODE 0: the split pass's SpMV (Ap_k = A p_k + the 4 partials + in-kernel reduction, as
-// k_split_spmv); MODE 1: plain y = A x (true residual, ops)
-template <int MODE, bool V32>
+// k_split_spmv); MODE 1: plain y = A x (true residual, ops).
+// PART (MODE 0, all-gather overlap): 0 = every segment; 1 = only the segments [g_lo, g_hi) inside
+// this rank's own block of p (they are final before the all-gather of p_k lands), the partial row
+// sums stored in Ap, no partials; 2 = the other segments, added to those sums, then the epilogue
+// (as k_split_spmv_aligned_part's halves)
+template <int MODE, bool V32, int PART = 0>
 __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
   if constexpr (MODE == 0) {
     const F1Scalars sc = f1_scalars(st, tol, first, check);
     if (st->done || sc.conv) {  // uniform over the grid: every workgroup leaves, no pacing
-      f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+      if constexpr (PART != 1) f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
       return;
     }
   }
@@ -140,6 +144,10 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
   const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
   const int64_t rounds = (T.nblocks + nwaves - 1) / nwaves;
   const int G = T.G;
+  // the segments this launch sweeps, in order: seg(0 .. ns - 1)
+  const int glo = PART == 0 ? 0 : T.g_lo, ghi = PART == 0 ? 0 : T.g_hi;
+  const int ns = PART == 0 ? G : (PART == 1 ? ghi - glo : G - (ghi - glo));
+  auto seg = [&](int i) { return PART == 0 ? i : (PART == 1 ? glo + i : (i < glo ? i : i - glo + ghi)); };
   double* a = acc[wv];
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
   double pf = 0.0;  // prefetch sink
@@ -149,17 +157,19 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
     const int64_t b = wave + rd * nwaves;
     const bool active = b < T.nblocks;
     for (int rr = lane; rr < kTileB; rr += 64) a[rr] = 0.0;
-    // the block's tiles are contiguous: tile g = [tptr[b G + g], tptr[b G + g + 1])
+    // tile g of block b = [tptr[b G + g], tptr[b G + g + 1])
     int64_t lo = 0, hi = 0;
     uint32_t q[kTU];
     double v[kTU];
-    if (active) {
-      lo = T.tptr[b * G];
-      hi = T.tptr[b * G + 1];
+    if (active && ns > 0) {
+      const int g0 = seg(0);
+      lo = T.tptr[b * G + g0];
+      hi = T.tptr[b * G + g0 + 1];
       tile_batch_load<V32>(T, lo + lane, hi, q, v);
     }
-    for (int g = 0; g < G; ++g, ++step) {
-      int64_t hi_next = hi;
+    for (int i = 0; i < ns; ++i, ++step) {
+      const int g = seg(i);
+      int64_t lo_next = hi, hi_next = hi;
       if (active) {
         const double* __restrict__ pg = p + ((int64_t)g << T.seg_shift);
         for (int64_t k = lo + lane; k < hi; k += kTU * 64) {
@@ -178,21 +188,23 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
           }
         }
         // the next tile's first batch loads while the workgroup waits at the pacing step
-        if (g + 1 < G) {
-          hi_next = T.tptr[b * G + g + 2];
-          tile_batch_load<V32>(T, hi + lane, hi_next, q, v);
+        if (i + 1 < ns) {
+          const int gn = seg(i + 1);
+          lo_next = T.tptr[b * G + gn];
+          hi_next = T.tptr[b * G + gn + 1];
+          tile_batch_load<V32>(T, lo_next + lane, hi_next, q, v);
         }
       }
       const double* nxt = nullptr;  // the segment the group starts next (prefetched while it waits)
       int64_t nlen = 0;
-      if (T.prefetch && (g + 1 < G || rd + 1 < rounds)) {
-        const int gn = g + 1 < G ? g + 1 : 0;
+      if (T.prefetch && (i + 1 < ns || rd + 1 < rounds)) {
+        const int gn = seg(i + 1 < ns ? i + 1 : 0);
         const int64_t s0 = (int64_t)gn << T.seg_shift;
         nxt = p + s0;
         nlen = ((int64_t)1 << T.seg_shift) < T.ext_len - s0 ? ((int64_t)1 << T.seg_shift) : T.ext_len - s0;
       }
       pace_step(T, step, &live, nxt, nlen, pf);
-      lo = hi;
+      lo = lo_next;
       hi = hi_next;
     }
     if (active) {
@@ -200,8 +212,10 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
       for (int rr = lane; rr < kTileB; rr += 64) {
         const int64_t i = r0 + rr;
         if (i >= T.n_rows) break;
-        const double sum = a[rr];
-        if constexpr (MODE == 0) {
+        if constexpr (MODE == 0 && PART == 1) {
+          Ap[i] = a[rr];  // the own-segment part of the row sum; part 2 adds the rest
+        } else if constexpr (MODE == 0) {
+          const double sum = PART == 2 ? Ap[i] + a[rr] : a[rr];
           const double pk = p[own + i], rk = r[i];
           st_stream(&Ap[i], sum);
           s_pap = fma(pk, sum, s_pap);
@@ -209,7 +223,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
           s_apap = fma(sum, sum, s_apap);
           s_rr = fma(rk, rk, s_rr);
         } else {
-          Ap[i] = sum;
+          Ap[i] = a[rr];
         }
       }
     }
@@ -217,7 +231,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
   }
   // keep the prefetch loads (a bit pattern no sum of finite values produces)
   if (__double_as_longlong(pf) == (long long)0x7FF4DEAD0000BEEFll) Ap[0] = pf;
-  if constexpr (MODE == 0) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+  if constexpr (MODE == 0 && PART != 1) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
 // ---- setup: count / fill one row block per 64-thread workgroup (LDS counters per segment) ----
@@ -332,16 +346,20 @@ void tiles_build_csr(const int64_t* rp, const int32_t* cols, const double* cvals
 
 void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r, double* Ap, int64_t own_off,
                          double* partials, int pstride, int grid, CgState* st, double tol, int first, int check,
-                         hipStream_t stream, const RedCtl& rc) {
+                         hipStream_t stream, const RedCtl& rc, int part) {
   if (grid <= 0) return;
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
+  MCG_CHECK(part == 0 || (T.g_lo >= 0 && T.g_lo <= T.g_hi && T.g_hi <= T.G), "tiles: bad own-segment range");
+  MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-  if (T.vals32 != nullptr)
-    hipLaunchKernelGGL((k_tiles<0, true>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, pstride,
-                       st, tol, first, check, rc);
-  else
-    hipLaunchKernelGGL((k_tiles<0, false>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, pstride,
-                       st, tol, first, check, rc);
+#define MCG_TL(V32, PART)                                                                                             \
+  hipLaunchKernelGGL((k_tiles<0, V32, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
+                     pstride, st, tol, first, check, rc)
+  const bool v32 = T.vals32 != nullptr;
+  if (part == 1) { if (v32) MCG_TL(true, 1); else MCG_TL(false, 1); }
+  else if (part == 2) { if (v32) MCG_TL(true, 2); else MCG_TL(false, 2); }
+  else { if (v32) MCG_TL(true, 0); else MCG_TL(false, 0); }
+#undef MCG_TL
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 

@@ -312,10 +312,9 @@ void GpuCgSolver::enqueue_split_spmv_(int k, int which, bool fused_red, int part
   }
   const int64_t n = L_.n_local();
   double* pp = partials_.get() + (which == 2 ? bnd_base_ : 0);
-  if (tiles_) {
-    MCG_CHECK(part == 0, "tiles: one SpMV launch per iteration");
+  if (tiles_) {  // part 1 / 2: the own-block segments while p_k's all-gather is in flight / the rest
     kern::cg_split_spmv_tiles(tiles_view(), p_[0].get(), r_.get(), Ap_.get(), L_.own_off, pp, pstride_, grid, st_.get(),
-                              opt_.tol, first, check, s0_, rc);
+                              opt_.tol, first, check, s0_, rc, part);
     return;
   }
   const int fmt = opt_.format == 1 ? (aligned_ ? 6 : (c8_ ? 4 : (d16_ ? 3 : 1))) : (info_.spmv_variant == 2 ? 5 : 0);
@@ -350,7 +349,8 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
     enqueue_split_spmv_(k, 2, fr);
     np = g_int_ + g_bnd_;
   } else if (ag_overlap_) {
-    // all-gather of p_k on the side stream || the own-block slots of every row; then the rest
+    // all-gather of p_k on the side stream || the own-block slots of every row (tiles: the segments
+    // inside the own block); then the rest
     MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
     MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
     comm_->halo_exchange(L_, pv, 1, s1_);

@@ -464,8 +464,20 @@ void GpuCgSolver::setup() {
   // all-gather overlap: the own-block slots of each aligned slice are summed while p_k's all-gather
   // is in flight (aligned_ is decided from the spec and the layout is the same kind on every rank,
   // so every rank takes the same launches)
-  ag_overlap_ = aligned_ && pmat_ && use_halo_ && L_.allgather && opt_.overlap && opt_.form.ag_overlap != 0 && n > 0;
-  if (ag_overlap_) {
+  ag_overlap_ = (aligned_ || tiles_) && pmat_ && use_halo_ && L_.allgather && opt_.overlap && opt_.form.ag_overlap != 0 &&
+                n > 0;
+  if (ag_overlap_ && tiles_) {
+    // the segments wholly inside the own block [own_off, own_off + n) of p: final before the all-gather
+    const int64_t S = (int64_t)1 << tgeo_.seg_shift;
+    tg_lo_ = (int)std::min<int64_t>(tgeo_.G, (L_.own_off + S - 1) / S);
+    tg_hi_ = (int)std::max<int64_t>(tg_lo_, std::min<int64_t>(tgeo_.G, (L_.own_off + n) / S));
+    std::vector<int64_t> tp(tgeo_.nblocks * tgeo_.G + 1);
+    MCG_HIP(hipMemcpy(tp.data(), tptr_.get(), tp.size() * sizeof(int64_t), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(A)");
+    int64_t loc = 0;
+    for (int64_t b = 0; b < tgeo_.nblocks; ++b) loc += tp[b * tgeo_.G + tg_hi_] - tp[b * tgeo_.G + tg_lo_];
+    info_.ag_local_frac = tp.back() > 0 ? (double)loc / (double)tp.back() : 0.0;
+  } else if (ag_overlap_) {
     const int64_t ns = (n + 63) / 64;
     lslots_.allocate(2 * ns, "A");
     kern::aligned_local_slots(sell_view(), lslots_.get(), s0_);

@@ -46,7 +46,8 @@ struct PassForm {
                              // the padded SELL slots by >= 10 %), 0 = off
   int sell_aligned = -1;     // wide random SPD: SELL-64/aligned (one column offset per slot shared by the slice's
                              // rows, values only; contiguous gathers); -1 = auto (expected fill <= 1.6), 0 = off
-  int ag_overlap = -1;       // SELL-64/aligned on an all-gather ghost layout: sum the own-block column slots while the
+  int ag_overlap = -1;       // SELL-64/aligned or tiles on an all-gather ghost layout: sum the own-block column slots
+                             // (tiles: the column segments inside the own block) while the
                              // all-gather of p is in flight, the rest after it (two SpMV halves); -1 = auto (on
                              // when the halo overlap is on), 0 = off
   int tiles = -1;            // irregular sparsity: the split pass's SpMV on L2-segment COO tiles (cg_tiles.hip: rows

@@ -167,6 +167,8 @@ class DelayComm final : public Communicator {
 //     for each rank q reading from me: wait done[q] == v(s - 1) (q copied my previous rows), then
 //       write v(s) into q's ready[me] (my rows of this exchange are final: the call follows my pass)
 //     for each rank q I read from: wait ready[q] == v(s), pull the ranges, write v(s) into q's done[me]
+// The all-gather ghost layout (unstructured sparsity) takes the same path: every peer's block is a
+// receive range, pulled on a stream of its own (several copy engines at once).
 // The all-reduce goes to `inner` (RCCL, or NullComm in a one-GPU rehearsal).
 class PeerHaloComm final : public Communicator {
  public:
@@ -204,6 +206,9 @@ class PeerHaloComm final : public Communicator {
   int64_t own_off_ = 0, row_begin_ = 0;
   std::vector<int64_t> peer_own_off_, peer_row_begin_;
   std::vector<void*> opened_;                    // IPC mappings to close
+  std::vector<hipStream_t> ag_streams_;          // all-gather layout: one copy stream per source peer
+  std::vector<hipEvent_t> ag_ev_;
+  hipEvent_t fork_ev_ = nullptr;
   long seq_ = 0;
   long cap_n_ = 0;  // exchanges recorded by the capture in progress
   // A captured exchange replays the flag values of its capture, which continues the 1/2 alternation

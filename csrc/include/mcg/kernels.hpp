@@ -395,6 +395,7 @@ struct TilesDev {
   int pace_sleep = 8;        // s_sleep units (64 clocks) between two polls
   int prefetch = 0;          // 1: touch the next segment's lines before the pacing wait (kernel comment)
   int64_t ext_len = 0;       // length of p (the last segment may be short)
+  int g_lo = 0, g_hi = 0;    // the segments inside this rank's own block of p (all-gather overlap, part 1 / 2)
 };
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
 int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
@@ -412,9 +413,10 @@ void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t
 void tiles_build_csr(const int64_t* rp, const int32_t* cols, const double* cvals, int64_t n, const TilesGeometry& geo,
                      const TilesOut& out, bool fill, hipStream_t st);
 // the split pass's SpMV on tiles (same contract as cg_split_spmv part 0)
+// part: 0 = every segment; 1 / 2 = the own-block segments [g_lo, g_hi) / the others (all-gather overlap)
 void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r, double* Ap, int64_t own_off,
                          double* partials, int pstride, int grid, CgState* st, double tol, int first, int check,
-                         hipStream_t stream, const RedCtl& rc = RedCtl());
+                         hipStream_t stream, const RedCtl& rc = RedCtl(), int part = 0);
 void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream);
 
 // ---- pipelined CG (csrc/gpu/cg_pipe.hip), recurrence = 2 ----

@@ -201,6 +201,7 @@ class GpuCgSolver {
   DeviceBuffer<double> tvals_;
   DeviceBuffer<float> tvals32_;  // the values as fp32 when every one is exact (tile_vals32)
   DeviceBuffer<unsigned> tpace_;
+  int tg_lo_ = 0, tg_hi_ = 0;  // the tile segments inside the own block of p (all-gather overlap)
   kern::TilesDev tiles_view() const {
     kern::TilesDev t;
     t.tptr = tptr_.get();
@@ -218,6 +219,8 @@ class GpuCgSolver {
     t.pace_sleep = std::max(1, std::min(64, opt_.form.tile_pace_sleep));
     t.prefetch = opt_.form.tile_prefetch > 0 ? 1 : 0;
     t.ext_len = L_.ext_len;
+    t.g_lo = tg_lo_;
+    t.g_hi = tg_hi_;
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)

@@ -362,3 +362,30 @@ def test_tiles_fp32_exact_values_bitwise_and_auto(mcg):
     assert u.solve()["converged"]
     with pytest.raises(Exception, match="tile_vals32"):
         mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tile_seg_log2=12, tile_vals32=1)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_tiles_all_gather_overlap_halves_match(mcg, world):
+    """Tiles on the all-gather layout (scrambled family): the column segments inside a rank's own
+    block of p are swept while the all-gather of p_k is in flight (part 1, partial row sums stored in
+    Ap), the other segments after it (part 2).  Against the one-launch sweep: same iterations, x to
+    rounding (the two halves add a row's products in another order), the CPU oracle, and ~1/P of
+    the entries in the own segments."""
+    spec = mcg.make_problem("randspd", rows=80000, band=32, density=0.5, scramble=1)
+    C = mcg.native()
+    cpu = _cpu(mcg, spec)
+    outs = []
+    for ag in (1, 0):
+        o = C.CgOptions(format="sell", recurrence=1, check_every=4)
+        o.tile_seg_log2 = 10
+        o.ag_overlap = ag
+        outs.append(C.run_local_ranks(spec.native(), o, world, 0, True))
+    on, off = outs
+    assert all(r["ag_overlap"] for r in on["ranks"]) and not any(r["ag_overlap"] for r in off["ranks"])
+    frac = np.mean([r["ag_local_frac"] for r in on["ranks"]])
+    assert 0.5 / world < frac < 1.5 / world
+    assert len({r["iterations"] for r in on["ranks"]}) == 1
+    assert abs(on["ranks"][0]["iterations"] - off["ranks"][0]["iterations"]) <= 1
+    np.testing.assert_allclose(on["x"], off["x"], rtol=1e-10, atol=1e-12 * np.abs(off["x"]).max())
+    np.testing.assert_allclose(on["x"], cpu["x"], rtol=1e-8, atol=1e-10 * np.abs(cpu["x"]).max())
+    assert all(r["true_rnorm"] < 1e-6 for r in on["ranks"])

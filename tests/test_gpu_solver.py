@@ -495,4 +495,3 @@ def test_lean_packed_edges_bitwise(mcg, n, depth, bpc):
             outs.append((s.result(), s._s.x_local()))
         assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
         assert np.array_equal(outs[0][1], outs[1][1])
-    assert b.solve()["converged"]
