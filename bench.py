@@ -108,10 +108,11 @@ def parse_args(argv=None):
                          "flags by stream memory operations; all-reduce on RCCL) -- CU-free, so halo_hide can "
                          "run the interior band beside it")
     ap.add_argument("--delay-comm", default="",
-                    help="with --sim-world: AR_US,HALO_US[,copy] -- every all-reduce / halo (or all-gather) exchange "
+                    help="with --sim-world: AR_US,HALO_US[,copy|fat] -- every all-reduce / halo (or all-gather) exchange "
                          "of the rehearsed rank costs a device-side delay of that many microseconds (DelayComm) "
                          "instead of nothing (NullComm); 'copy': the halo is real copy-engine traffic of the "
-                         "layout's message sizes (a CU-free transport's timing)")
+                         "layout's message sizes (a CU-free transport's timing); 'fat': the delays spin with RCCL's "
+                         "~270 VGPRs per wave (they cannot start beside a resident kernel)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="timing rehearsal: run rank --sim-rank of a P-rank job alone on this GPU (its rows, "
                          "ghost layout, interior/boundary launches, graphs) with collectives that move nothing")
@@ -181,8 +182,8 @@ def _run_rank(args, out_fd) -> int:
     if sim:  # per-rank timing rehearsal (not a P-rank solve: see --sim-world)
         if args.delay_comm:
             f = args.delay_comm.split(",")
-            comm = mcg.native().DelayComm(args.sim_rank, args.sim_world, float(f[0]), float(f[1]), False,
-                                          len(f) > 2 and f[2] == "copy")
+            comm = mcg.native().DelayComm(args.sim_rank, args.sim_world, float(f[0]), float(f[1]), "fat" in f[2:],
+                                          "copy" in f[2:])
         else:
             comm = mcg.native().NullComm(args.sim_rank, args.sim_world)
 

@@ -165,6 +165,15 @@ def recipes(a) -> dict:
             ("v32_again", 400, bench(f"{c5} --steps 6 --warmup 2")),
         ] + counters("v32_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
           + counters("v32_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"),
+        # r4: the all-gather priced (DelayComm: 10 us all-reduce, 2330 us all-gather ~ 700 MB over xGMI) with
+        # the own-segment half swept while it is in flight (ag_overlap) vs after it; thin = a CU-light
+        # transport (copy engines), fat = RCCL's register footprint
+        "c5ag": [
+            ("ag_thin", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330")),
+            ("noag_thin", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 --set ag_overlap=0")),
+            ("ag_fat", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330,fat")),
+            ("ag_null", 400, bench(f"{c5} --steps 6 --warmup 2")),
+        ],
         "c5v32big": [
             ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2")),
         ],
@@ -263,6 +272,31 @@ def recipes(a) -> dict:
             for tag, kv in (("auto", ""), ("e13", "--set lean_depth=13 --set lean_bpc=5"),
                             ("e14", "--set lean_depth=14"))
         ] + stats("edge_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=13 --set lean_bpc=5"),
+        # r4: even / odd lean passes on their own geometry (lean_*_odd): packed edges at 5 waves / SIMD for
+        # the even passes, the odd ones (x stream paired in) at depth 4 or the default depth 3, 4 waves
+        "edge2": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'packed_edges or own_grid'"),
+        ] + [
+            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify {kv}"))
+            for rep in (1, 2)
+            for tag, kv in (("auto", ""), ("e14", "--set lean_depth=14"),
+                            ("mix14", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=14 --set lean_bpc_odd=4"),
+                            ("mix3", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=3 --set lean_bpc_odd=4"),
+                            ("mix4", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=4 --set lean_bpc_odd=3"))
+        ] + stats("e14_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=14")
+          + stats("auto_stats_4096", "--grid 4096 --steps 640 --warmup 64")
+          + stats("mix14_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=13 --set lean_bpc=5 "
+                                      "--set lean_depth_odd=14 --set lean_bpc_odd=4"),
+        # r4: tile values fp32 vs fp64 storage, interleaved, with DRAM / L2 counters of each
+        "c5ab": [
+            (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
+            for rep in (1, 2) for tag, kv in (("v64", ""), ("v32", "--set tile_vals32=1"))
+        ] + counters("v64_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
+          + counters("v64_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE")
+          + counters("v32_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1 --set tile_vals32=1",
+                     "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE")
+          + counters("v64_ta", "k_tiles", f"{C5SCR} --steps 2 --warmup 1",
+                     "TCC_EA0_RDREQ_sum TCC_REQ_sum GRBM_GUI_ACTIVE"),
         # r4: stream memory operations (write / wait value) around a NoCU copy, eager and captured
         "streamop": [
             ("probe", 240, f"{PY} -c 'import torch, json, cuda_mpi_parallel_amd as m; torch.cuda.init(); "

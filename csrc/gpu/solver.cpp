@@ -188,7 +188,9 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
   const int first = (k == 0 && !probing_) ? 1 : 0;
   const int check = (k >= 2 && !probing_) ? 1 : 0;  // the reference never tests r_0
   const TileRanges& tr = which == 1 ? tr_int_ : (which == 2 ? tr_bnd_ : tr_all_);
-  const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : g_all_);
+  // 2-D lean-only odd passes may run on a grid of their own (g_odd_, lean_bpc_odd)
+  const bool odd_grid = which == 0 && g_odd_ > 0 && (k & 1) != 0 && !final_mode;
+  const int grid = which == 1 ? g_int_ : (which == 2 ? g_bnd_ : (odd_grid ? g_odd_ : g_all_));
   double* part = partials_.get() + (which == 2 ? bnd_base_ : 0);
   if (grid == 0) return;
   kern::RedCtl rc;
@@ -199,7 +201,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     rc.l2s = red_l2s_;
     rc.top = red_l2s_;
     rc.base = which == 2 ? bnd_base_ : 0;
-    rc.ngroups = which == 0 ? red_groups_all_ : red_groups_split_;
+    rc.ngroups = which == 0 ? (odd_grid ? red_groups_odd_ : red_groups_all_) : red_groups_split_;
     rc.check = check;
     rc.first = first;
   }
@@ -241,7 +243,8 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     // passes 2 (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md);
     // the lean ones 3 as well (4096^2 8191-8225 vs 8064-8084 it/s, 16384^2 586.4 vs 584.9,
     // profiles/r3/lean/README.md)
-    const int depth = ((k & 1) == 0 && p3_ && !lean_only_) ? 2 : (lean_only_ && opt_.form.lean_depth > 0 ? opt_.form.lean_depth : 3);
+    const int ld = ((k & 1) != 0 && opt_.form.lean_depth_odd > 0) ? opt_.form.lean_depth_odd : opt_.form.lean_depth;
+    const int depth = ((k & 1) == 0 && p3_ && !lean_only_) ? 2 : (lean_only_ && ld > 0 ? ld : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
                       p3_, 3, lean_only_);
@@ -376,7 +379,7 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     return;
   }
   trace::Range tr_("mcg.iteration.single_reduction");
-  int np = g_all_;
+  int np = (g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_;
   const bool fr = fused_red_;
   if (hide_) {
     // halo_hide: the interior band reads no ghost line, so it runs while this iteration's ghosts land

@@ -750,10 +750,16 @@ void GpuCgSolver::setup() {
       }
       if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
     }
-    if (kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, ar3_ ? info_.ar3_kw : 0,
-                                  ar3_ ? carry_lo2_ : 0, s0_, 0, 0, ar3_ ? tr_all_.runs3 : 0) == 0) {
+    auto lean_ok = [&](int gg) {
+      return kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, gg, ar3_ ? info_.ar3_kw : 0,
+                                       ar3_ ? carry_lo2_ : 0, s0_, 0, 0, ar3_ ? tr_all_.runs3 : 0) == 0;
+    };
+    // the odd passes (x update paired in) on a grid of their own (lean_bpc_odd): both grids' runs must qualify
+    const int go = (!ar3_ && opt_.form.lean_bpc_odd > 0) ? ncu_ * opt_.form.lean_bpc_odd : g;
+    if (lean_ok(g) && (go == g || lean_ok(go))) {
       lean_only_ = true;
       g_all_ = g;
+      g_odd_ = go == g ? 0 : go;
     }
   }
   if (p3_ && diav3_ && ar3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
@@ -846,6 +852,7 @@ void GpuCgSolver::setup() {
   allocate_vectors_();
   g_b_ = kern::grid_for((n + 1) / 2, 256, 4);  // residual update / dot kernels: 1024 blocks (best measured)
   info_.grid_a = g_all_;
+  info_.grid_odd = g_odd_;
   info_.grid_b = g_b_;
   const bool split = split_ || hide_;
   fused_red_ = (opt_.recurrence == 1 && opt_.form.fused_reduce != 0) || opt_.recurrence == 2;
@@ -854,7 +861,7 @@ void GpuCgSolver::setup() {
   // (the extra blocks find no work in the grid-stride loops and contribute zero partials)
   if (split && fused_red_ && g_int_ > 0) g_int_ = groups(g_int_) * kern::kRedGroup;
   bnd_base_ = split ? g_int_ : 0;
-  const int np = std::max({g_all_, split ? g_int_ + g_bnd_ : 0, g_b_, 1});
+  const int np = std::max({g_all_, split ? g_int_ + g_bnd_ : 0, g_b_, g_odd_, 1});
   pstride_ = np + 64;
   partials_.allocate((size_t)pstride_ * (opt_.recurrence >= 1 ? 4 : 1), "partials");
   st_.allocate(1, "state");
@@ -864,7 +871,8 @@ void GpuCgSolver::setup() {
     red_groups_all_ = groups(g_all_);
     red_groups_split_ = split ? groups(g_int_) + groups(g_bnd_) : 0;
     red_groups_b_ = groups(g_b_);  // the pipelined update's grid
-    red_l2s_ = std::max({red_groups_all_, red_groups_split_, red_groups_b_, 1});
+    red_groups_odd_ = groups(g_odd_);
+    red_l2s_ = std::max({red_groups_all_, red_groups_split_, red_groups_b_, red_groups_odd_, 1});
     red_cnt_.allocate(red_l2s_ + 1, "partials");
     red_l2_.allocate((size_t)4 * red_l2s_, "partials");
     MCG_HIP(hipMemsetAsync(red_cnt_.get(), 0, red_cnt_.bytes(), s0_), "device memset failed");

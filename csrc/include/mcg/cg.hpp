@@ -64,10 +64,11 @@ struct PassForm {
   int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
   int tile_pace_slack = 1;   // tiles, tile_pace 2 / 4: a workgroup waits for all but this many eighths of its group
   int tile_prefetch = 0;     // tiles: each workgroup touches its share of the next segment before the pacing wait
-  int tile_vals32 = -1;      // tiles: values stored as fp32 (8 instead of 12 B per entry streamed) when every value
+  int tile_vals32 = 0;       // tiles: values stored as fp32 (8 instead of 12 B per entry streamed) when every value
                              // round-trips fp64 -> fp32 -> fp64 exactly, checked while the tiles are counted: the
-                             // same matrix, products and sums in fp64; -1 = auto (when exact on every rank), 0 = off,
-                             // 1 = required (an inexact value is an error)
+                             // same matrix, products and sums in fp64; -1 = auto (when exact on every rank), 0 = off
+                             // (the default: the scrambled config-5 share ran 18.1-18.4 vs 19.3 it/s with fp64
+                             // storage, profiles/r4/c5v32), 1 = required (an inexact value is an error)
   int tile_pace_sleep = 8;   // tiles: s_sleep units (64 clocks each) between two polls of a waiting workgroup
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
@@ -92,9 +93,12 @@ struct PassForm {
                              // values in scalar registers and no codes streamed (the 2-D three-term pass over runs
                              // of such lines; bitwise the same sums); -1 = auto (on), 0 = off
   int lean_depth = 0;        // 2-D lean-only passes: operand prefetch depth in lines (0 = auto: 3; 4 and 6 build with
-                             // 3 / 2 waves per SIMD for the registers)
+                             // 3 / 2 waves per SIMD for the registers; 13 / 14: packed slice edges at depth 3 with 5
+                             // waves per SIMD / depth 4 with 4, cg_carry_ar.hip EP)
   int lean_bpc = 0;          // 2-D lean-only passes: blocks per CU of the grid (0 = auto: the largest of 16 / 8 / 4
                              // whose runs keep >= 64 lines)
+  int lean_depth_odd = 0;    // ... the odd passes (x update paired in: one more stream) their own depth / grid; 0 = as
+  int lean_bpc_odd = 0;      // the even passes (the two grids each reduce their own block partials)
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
                              // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
                              // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)

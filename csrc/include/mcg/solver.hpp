@@ -43,6 +43,7 @@ struct SolverInfo {
   size_t device_bytes = 0;
   double bytes_per_iter_model = 0;  // modelled HBM bytes per iteration (this rank)
   int grid_a = 0, grid_b = 0;
+  int grid_odd = 0;  // 2-D lean-only odd passes on a grid of their own (CgOptions::form.lean_bpc_odd), else 0
   int64_t max_row_len = 0;
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
@@ -266,7 +267,7 @@ class GpuCgSolver {
   int bnd_base_ = 0;               // first partial slot of the boundary launch (a multiple of kRedGroup)
   bool fused_red_ = false;         // in-kernel reduction of the fused pass (CgOptions::fused_reduce)
   bool pmat_ = false;              // materialized-p split pass (CgOptions::pmat)
-  int red_groups_all_ = 0, red_groups_split_ = 0, red_groups_b_ = 0, red_l2s_ = 0;
+  int red_groups_all_ = 0, red_groups_split_ = 0, red_groups_b_ = 0, red_l2s_ = 0, red_groups_odd_ = 0;
   DeviceBuffer<unsigned> red_cnt_;  // group counters + top counter (zeroed at setup, reset by the kernels)
   DeviceBuffer<double> red_l2_;     // [4][red_l2s_] group sums
   DeviceBuffer<CgState> st_;
@@ -274,6 +275,7 @@ class GpuCgSolver {
   // launch geometry
   TileRanges tr_all_, tr_int_, tr_bnd_;
   int g_all_ = 1, g_int_ = 1, g_bnd_ = 1, g_b_ = 1;
+  int g_odd_ = 0;  // 2-D lean-only odd passes: their own grid (0 = g_all_)
   // graph of two iterations (even, odd)
   // [0]: one iteration pair, [1]: graph_iters iterations (when > 2)
   hipGraph_t graph_[2] = {nullptr, nullptr};

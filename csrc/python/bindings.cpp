@@ -221,6 +221,8 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(carry_vc)
       MCG_FORM_PROP(lean_depth)
       MCG_FORM_PROP(lean_bpc)
+      MCG_FORM_PROP(lean_depth_odd)
+      MCG_FORM_PROP(lean_bpc_odd)
       MCG_FORM_PROP(halo_hide)
       MCG_FORM_PROP(tile_pace_lag)
       MCG_FORM_PROP(tile_pace_slack)
@@ -500,6 +502,7 @@ PYBIND11_MODULE(_C, m) {
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
+        d["grid_odd"] = i.grid_odd;
         d["grid_b"] = i.grid_b;
         d["max_row_len"] = i.max_row_len;
         d["spmv_variant"] = i.spmv_variant;

@@ -336,16 +336,16 @@ def test_tiles_row_colliding_batches_run_to_run_bitwise(mcg):
 
 
 def test_tiles_fp32_exact_values_bitwise_and_auto(mcg):
-    """tile_vals32: the scrambled family's values (1 - k / 2^20 and integer diagonals) are all exact
-    fp32, so the tiles store them in 4 bytes by default (8 instead of 12 B per entry); the solve is
+    """tile_vals32 (auto, -1): the scrambled family's values (1 - k / 2^20 and integer diagonals) are all
+    exact fp32, so the tiles store them in 4 bytes (8 instead of 12 B per entry); the solve is
     bit for bit the fp64-storage solve (the same matrix, products and sums in fp64).  A user matrix
     with a value that is not an fp32 keeps fp64 storage, and requiring fp32 for it is an error."""
     import scipy.sparse as sp
 
     spec = mcg.make_problem("randspd", **SCR)
     kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=30, tile_seg_log2=12)
-    a = mcg.CGSolver(spec, tiles=1, **kw)
-    b = mcg.CGSolver(spec, tiles=1, tile_vals32=0, **kw)
+    a = mcg.CGSolver(spec, tiles=1, tile_vals32=-1, **kw)
+    b = mcg.CGSolver(spec, tiles=1, **kw)
     assert a.info["tile_vals32"] and not b.info["tile_vals32"]
     ra, rb = a.solve(), b.solve()
     assert ra["rnorm"] == rb["rnorm"]
@@ -357,7 +357,7 @@ def test_tiles_fp32_exact_values_bitwise_and_auto(mcg):
     T[3, 10] = T[10, 3] = -0.1  # not an fp32
     T[3, 3] = T[10, 10] = 2.6
     prob = mcg.csr_problem(T.tocsr(), b=np.ones(n))
-    u = mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tol=1e-10, tile_seg_log2=12)
+    u = mcg.CGSolver(prob, format="sell", recurrence=1, tiles=1, tol=1e-10, tile_seg_log2=12, tile_vals32=-1)
     assert u.info["tiles"] and not u.info["tile_vals32"]
     assert u.solve()["converged"]
     with pytest.raises(Exception, match="tile_vals32"):

@@ -495,3 +495,33 @@ def test_lean_packed_edges_bitwise(mcg, n, depth, bpc):
             outs.append((s.result(), s._s.x_local()))
         assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
         assert np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_lean_odd_passes_own_grid_bitwise(mcg):
+    """lean_bpc_odd / lean_depth_odd: the odd passes (x update paired in) on a grid and prefetch depth
+    of their own -- here the packed-edge kernels at 5 waves per SIMD for the even passes and depth 4
+    at 4 for the odd ones -- bit for bit the default kernels on the same two grids (each grid reduces
+    its own block partials, through the phase profile as well)."""
+    spec = mcg.make_problem("poisson2d", n=2048, rhs="random")
+    kw = dict(format="sellc8", recurrence=1, check_every=8, lean_bpc=5, lean_bpc_odd=4)
+    a = mcg.CGSolver(spec, **kw)
+    b = mcg.CGSolver(spec, lean_depth=13, lean_depth_odd=14, **kw)
+    for s in (a, b):
+        assert s.info["lean_only"] and s.info["grid_odd"] == s.info["grid_a"] * 4 // 5
+    for its in (21, 22):
+        outs = []
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+            outs.append((s.result(), s._s.x_local()))
+        assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
+        assert np.array_equal(outs[0][1], outs[1][1])
+    one = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=5)
+    one.reset()
+    one.run(22)
+    one.finalize()
+    assert abs(one.result()["rnorm"] - outs[0][0]["rnorm"]) <= 1e-12 * outs[0][0]["rnorm"]
+    b.reset()
+    ph = b._s.phase_profile(8)
+    assert ph["iteration"] > 0
