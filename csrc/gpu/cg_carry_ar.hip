@@ -492,6 +492,13 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             sum = fma(cp, upv, sum);
             return fma(V.v[4], upl, sum);
           };
+          // a first / last line of the other parity's runs (TileRanges::alt_chunk): r stored there too
+          const int32_t ach = tr.alt_chunk;
+          auto alt_edge = [&](int32_t m) {
+            if (ach <= 0) return false;
+            const int32_t l = (int32_t)l0 + m, md = l % ach;
+            return md == 0 || md == ach - 1 || l == (int32_t)nl - 1;
+          };
           auto epk = [&](const Edge& q) {
             if constexpr (EP) {
               const double v = q.r;
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1);
             const uint32_t ob = line_ofs(m);
             const double rr = fma(-b, o_pold, o_pk);
-            if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
+            if (m == 0 || m == n_run - 1 || alt_edge(m)) g_st_nt(rn_, ob + l8, rr);
             if (edge_lane) {
               const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
               g_st(ren, sb, rr);
@@ -2138,6 +2145,10 @@ int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl) {
     }
   }
   return best;
+}
+
+void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk) {
+  (void)carry_jobs(nw, ss, nl, 0, 0, runs, chunk);
 }
 
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,

@@ -244,6 +244,15 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     // the lean ones 3 as well (4096^2 8191-8225 vs 8064-8084 it/s, 16384^2 586.4 vs 584.9,
     // profiles/r3/lean/README.md)
     const int ld = ((k & 1) != 0 && opt_.form.lean_depth_odd > 0) ? opt_.form.lean_depth_odd : opt_.form.lean_depth;
+    if (g_odd_ > 0 && which == 0 && !final_mode) {
+      // the two parities' runs differ: each pass also stores r on the other decomposition's run ends
+      TileRanges ta = tr;
+      ta.alt_chunk = (k & 1) != 0 ? alt_chunk_even_ : alt_chunk_odd_;
+      kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, ld > 0 ? ld : 3, S, v, L_.own_off, ta,
+                        part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc, p3_, 3,
+                        lean_only_);
+      return;
+    }
     const int depth = ((k & 1) == 0 && p3_ && !lean_only_) ? 2 : (lean_only_ && ld > 0 ? ld : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,

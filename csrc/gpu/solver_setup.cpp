@@ -760,6 +760,13 @@ void GpuCgSolver::setup() {
       lean_only_ = true;
       g_all_ = g;
       g_odd_ = go == g ? 0 : go;
+      auto chunk_of = [&](int gg) {
+        int64_t runs = 0, chunk = 0;
+        kern::carry_jobs_host((int64_t)gg * 4, tr_all_.strip, nlines, runs, chunk);
+        return (int32_t)chunk;
+      };
+      alt_chunk_even_ = g_odd_ > 0 ? chunk_of(g) : 0;
+      alt_chunk_odd_ = g_odd_ > 0 ? chunk_of(go) : 0;
     }
   }
   if (p3_ && diav3_ && ar3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
@@ -774,6 +781,7 @@ void GpuCgSolver::setup() {
       if (l0 < nl && l1 - l0 < 3) all = false;
     }
     lean_only_ = all;
+    g_odd_ = 0;
   }
   if (p3_ && diav_ && !diav3_ && n > 0 && tr_all_.strip > 0 && opt_.form.dia_uniform != 0) {
     // diav: every run of >= 3 lines streams its coefficients in the lean loop (the same grids as the
@@ -802,6 +810,7 @@ void GpuCgSolver::setup() {
     if (g >= 1 && all_lean(g)) {
       lean_only_ = true;
       g_all_ = g;
+      g_odd_ = 0;
     }
   }
   info_.lean_only = lean_only_;

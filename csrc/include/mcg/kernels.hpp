@@ -69,6 +69,11 @@ struct TileRanges {
   // 3-D plane carry: runs of planes per job column (> 0: chosen at setup by carry3_runs, so the
   // jobs fill whole rounds of the launch's blocks); 0 = blocks / jobs-per-run (at least 1)
   int32_t runs3 = 0;
+  // 2-D lean three-term carry with the odd passes on a grid of their own (lean_bpc_odd): the other
+  // parity's run length in lines.  The next pass reads r_{k-1} on the line before / after each of ITS
+  // runs, which this pass stores only on its own runs' first / last lines, so it also stores r on the
+  // first / last line of every run of the other decomposition; 0 = both parities share the runs
+  int32_t alt_chunk = 0;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);
@@ -321,6 +326,9 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
 // The 3-D plane carry's run count (TileRanges::runs3) for `nb` blocks, `jpr` jobs per run and nl
 // planes: the R whose job rounds x (planes per run + the 3-plane prologue) is least (ties: fewer runs)
 int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl);
+// the 2-D carry's job decomposition of a launch of nw waves over nl lines of ss slices (every line in
+// one launch): runs per slice column and lines per run
+void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk);
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
                             int32_t ln, hipStream_t stream, int band = 0, int band_h = 0, int runs3 = 0);
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals), 5 SELL-64/diav (S.cvd / cve / cvs,

@@ -276,6 +276,7 @@ class GpuCgSolver {
   TileRanges tr_all_, tr_int_, tr_bnd_;
   int g_all_ = 1, g_int_ = 1, g_bnd_ = 1, g_b_ = 1;
   int g_odd_ = 0;  // 2-D lean-only odd passes: their own grid (0 = g_all_)
+  int32_t alt_chunk_even_ = 0, alt_chunk_odd_ = 0;  // ... run lengths (lines) of the even / odd decompositions
   // graph of two iterations (even, odd)
   // [0]: one iteration pair, [1]: graph_iters iterations (when > 2)
   hipGraph_t graph_[2] = {nullptr, nullptr};
