@@ -287,6 +287,14 @@ def recipes(a) -> dict:
           + stats("auto_stats_4096", "--grid 4096 --steps 640 --warmup 64")
           + stats("mix14_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=13 --set lean_bpc=5 "
                                       "--set lean_depth_odd=14 --set lean_bpc_odd=4"),
+        # r4: the auto mixed geometry at 4096^2 (packed edges, per-parity grids) vs the r3 lean default,
+        # interleaved repeats on one box
+        "mix": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'packed_edges or own_grid or lean_mix'"),
+        ] + [
+            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
+            for rep in (1, 2, 3) for tag, kv in (("mix", ""), ("r3", "--set lean_depth=3"))
+        ] + [("g16384", 200, bench("--phases 0"))],
         # r4: tile values fp32 vs fp64 storage, interleaved, with DRAM / L2 counters of each
         "c5ab": [
             (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
@@ -306,6 +314,7 @@ def recipes(a) -> dict:
         "peer": [
             ("check2", 180, f"{PY} -u bench/peer_halo_check.py --world 2"),
             ("check4", 180, f"{PY} -u bench/peer_halo_check.py --world 4 --n 512 --rounds 6"),
+            ("check4_ag", 180, f"{PY} -u bench/peer_halo_check.py --world 4 --problem scrambled --rounds 4"),
         ] + [
             (f"bench{w}_{t}", 300, f"{PY} -m torch.distributed.run --nnodes=1 --nproc-per-node {w} "
                                    f"--master-addr 127.0.0.1 --master-port {29600 + w} bench.py --gpus {w} "

@@ -243,7 +243,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     // passes 2 (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md);
     // the lean ones 3 as well (4096^2 8191-8225 vs 8064-8084 it/s, 16384^2 586.4 vs 584.9,
     // profiles/r3/lean/README.md)
-    const int ld = ((k & 1) != 0 && opt_.form.lean_depth_odd > 0) ? opt_.form.lean_depth_odd : opt_.form.lean_depth;
+    const int ld = (k & 1) != 0 ? lean_depth_odd_ : lean_depth_even_;
     if (g_odd_ > 0 && which == 0 && !final_mode) {
       // the two parities' runs differ: each pass also stores r on the other decomposition's run ends
       TileRanges ta = tr;

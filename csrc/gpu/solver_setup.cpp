@@ -733,6 +733,8 @@ void GpuCgSolver::setup() {
   // for; 3-D: LEAN); otherwise the generic kernels (no lean code: one kernel holding both measured
   // slower for each, profiles/r3/lean)
   lean_only_ = false;
+  lean_depth_even_ = opt_.form.lean_depth;
+  lean_depth_odd_ = opt_.form.lean_depth_odd > 0 ? opt_.form.lean_depth_odd : opt_.form.lean_depth;
   if (p3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0) {
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
     int g = g_all_;
@@ -741,21 +743,38 @@ void GpuCgSolver::setup() {
       // re-read their prologue lines too often): 16384^2 16 per CU, 585.8 vs 581 it/s at 8; 4096^2
       // 4 per CU, 8592-8655 vs 7911-8484 at 8; a P = 8 share of 16384^2 8 per CU, within noise of 4
       // (profiles/r3/lean)
+      int bpc_rule = 0;
       for (int bpc : {16, 8, 4}) {
         const int64_t waves = (int64_t)ncu_ * bpc * 4;  // 256-thread blocks
         if (nlines / std::max<int64_t>(1, waves / tr_all_.strip) >= 64) {
           g = ncu_ * bpc;
+          bpc_rule = bpc;
           break;
         }
       }
       if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
+      // the 4-blocks-per-CU grids (64-line runs: 4096^2, latency-bound passes): packed slice edges, the
+      // even passes at 5 waves per SIMD (depth 3), the odd ones at depth 4 with 4 (each on its own grid;
+      // 4096^2: 8441-8542 vs 8181-8188 it/s on one box, profiles/r4/edge2)
+      auto_mix_ = bpc_rule == 4 && opt_.form.lean_bpc <= 0 && opt_.form.lean_bpc_odd <= 0 && opt_.form.lean_depth <= 0 &&
+                  opt_.form.lean_depth_odd <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.form.halo_hide != 1;
     }
     auto lean_ok = [&](int gg) {
       return kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, gg, ar3_ ? info_.ar3_kw : 0,
                                        ar3_ ? carry_lo2_ : 0, s0_, 0, 0, ar3_ ? tr_all_.runs3 : 0) == 0;
     };
     // the odd passes (x update paired in) on a grid of their own (lean_bpc_odd): both grids' runs must qualify
-    const int go = (!ar3_ && opt_.form.lean_bpc_odd > 0) ? ncu_ * opt_.form.lean_bpc_odd : g;
+    int go = (!ar3_ && opt_.form.lean_bpc_odd > 0) ? ncu_ * opt_.form.lean_bpc_odd : g;
+    if (auto_mix_) {
+      if (lean_ok(ncu_ * 5) && lean_ok(ncu_ * 4)) {
+        g = ncu_ * 5;
+        go = ncu_ * 4;
+        lean_depth_even_ = 13;
+        lean_depth_odd_ = 14;
+      } else {
+        auto_mix_ = false;
+      }
+    }
     if (lean_ok(g) && (go == g || lean_ok(go))) {
       lean_only_ = true;
       g_all_ = g;
@@ -814,6 +833,7 @@ void GpuCgSolver::setup() {
     }
   }
   info_.lean_only = lean_only_;
+  info_.lean_mix = auto_mix_ && lean_only_ && g_odd_ > 0;
   // halo_hide: the lean 2-D pass split into the interior band (reads no ghost line; it runs while a
   // copy-engine halo lands) and the kHideLines lines at each end of the rank (after the halo)
   if (opt_.form.halo_hide == 1 && halo_ahead_ && comm_ != nullptr && comm_->halo_cu_free() && lean_only_ && ar_ && !ar3_ && p3_ &&

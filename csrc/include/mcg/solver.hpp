@@ -44,6 +44,7 @@ struct SolverInfo {
   double bytes_per_iter_model = 0;  // modelled HBM bytes per iteration (this rank)
   int grid_a = 0, grid_b = 0;
   int grid_odd = 0;  // 2-D lean-only odd passes on a grid of their own (CgOptions::form.lean_bpc_odd), else 0
+  bool lean_mix = false;  // ... chosen by the setup: packed edges, even passes 5 waves / SIMD, odd depth 4
   int64_t max_row_len = 0;
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
@@ -277,6 +278,8 @@ class GpuCgSolver {
   int g_all_ = 1, g_int_ = 1, g_bnd_ = 1, g_b_ = 1;
   int g_odd_ = 0;  // 2-D lean-only odd passes: their own grid (0 = g_all_)
   int32_t alt_chunk_even_ = 0, alt_chunk_odd_ = 0;  // ... run lengths (lines) of the even / odd decompositions
+  int lean_depth_even_ = 0, lean_depth_odd_ = 0;       // 2-D lean prefetch depth per parity (0 = 3; 13 / 14 packed edges)
+  bool auto_mix_ = false;                              // ... chosen by the setup (4-blocks-per-CU grids)
   // graph of two iterations (even, odd)
   // [0]: one iteration pair, [1]: graph_iters iterations (when > 2)
   hipGraph_t graph_[2] = {nullptr, nullptr};

@@ -503,6 +503,7 @@ PYBIND11_MODULE(_C, m) {
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
         d["grid_odd"] = i.grid_odd;
+        d["lean_mix"] = i.lean_mix;
         d["grid_b"] = i.grid_b;
         d["max_row_len"] = i.max_row_len;
         d["spmv_variant"] = i.spmv_variant;

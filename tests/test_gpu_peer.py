@@ -1,0 +1,56 @@
+"""The copy-engine halo transport (PeerHaloComm, csrc/gpu/peer_halo.cpp) across PROCESSES on one GPU:
+IPC-mapped peer buffers, hipMemcpyDeviceToDeviceNoCU pulls, stream write / wait-value flags.  The
+reference has no communication at all (CUDACG.cu:87, one device); this is the north star's halo and
+all-gather moved off the compute units."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(cmd, timeout=240):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
+
+
+def _port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,problem", [(2, "poisson2d"), (4, "scrambled")])
+def test_peer_halo_processes_pull_the_owners_rows(world, problem):
+    """P processes on device 0 exchange rank-tagged rows over the copy engines, several rounds with new
+    values each: every ghost row equals its owner's row -- the 2-D window halo (neighbour lines) and
+    the all-gather layout of the scrambled family (every peer's block, one copy stream per peer)."""
+    p = _run([sys.executable, "-u", "bench/peer_halo_check.py", "--world", str(world), "--problem", problem,
+              "--rounds", "4", "--port", str(_port())])
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["ok"] and all(r["mismatches"] == 0 for r in line["ranks"])
+    assert all(r["allgather"] == (problem == "scrambled") for r in line["ranks"])
+    assert all(r["recv_ranges"] >= (world - 1 if problem == "scrambled" else 1) for r in line["ranks"])
+
+
+def test_bench_sdma_halo_rehearsal_on_one_gpu():
+    """bench.py at P = 2 under torchrun on one GPU with the copy-engine halo (--halo-transport sdma):
+    the solver's halo goes through PeerHaloComm inside the 32-iteration graphs (flags replayed),
+    collectives of the all-reduce move nothing (rehearsal); every rank ok and latched together."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--rehearse-ranks", "--grid",
+           "1024", "--steps", "64", "--warmup", "8", "--phases", "0", "--watchdog", "60", "--halo-transport", "sdma"]
+    p = _run(cmd)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["check"]["ok"] and line["n_gpus"] == 2
+    assert line["config"]["halo_transport"].startswith("sdma")

@@ -525,3 +525,23 @@ def test_lean_odd_passes_own_grid_bitwise(mcg):
     b.reset()
     ph = b._s.phase_profile(8)
     assert ph["iteration"] > 0
+
+
+def test_lean_mix_auto_on_small_grids(mcg):
+    """The setup's geometry for 4-blocks-per-CU grids (64-line runs, e.g. 4096^2): packed slice edges,
+    the even passes on 5 blocks per CU, the odd passes on their own 4-per-CU grid at depth 4; the
+    solve tracks the explicitly configured default-kernel solve on the same two grids bit for bit.
+    A 16384-wide grid (16 blocks per CU) keeps one grid."""
+    spec = mcg.make_problem("poisson2d", n=4096, rhs="random")
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8)
+    assert a.info["lean_only"] and a.info["lean_mix"] and a.info["grid_odd"] == a.info["grid_a"] * 4 // 5
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=5, lean_bpc_odd=4)
+    assert not b.info["lean_mix"] and b.info["grid_odd"] == a.info["grid_odd"]
+    for s in (a, b):
+        s.reset()
+        s.run(15)
+        s.finalize()
+    assert a.result()["rnorm"] == b.result()["rnorm"]
+    assert np.array_equal(a._s.x_local(), b._s.x_local())
+    big = mcg.CGSolver(mcg.make_problem("poisson2d", n=8192), format="sellc8", recurrence=1)
+    assert big.info["lean_only"] and not big.info["lean_mix"] and big.info["grid_odd"] == 0
