@@ -173,6 +173,8 @@ def recipes(a) -> dict:
             ("noag_thin", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 --set ag_overlap=0")),
             ("ag_fat", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330,fat")),
             ("ag_null", 400, bench(f"{c5} --steps 6 --warmup 2")),
+            ("ag_copy", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,0,copy")),
+            ("noag_copy", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,0,copy --set ag_overlap=0")),
         ],
         "c5v32big": [
             ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2")),
@@ -336,6 +338,14 @@ def recipes(a) -> dict:
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),
+        ],
+        # how far rounding alone moves CG residual histories apart (CPU oracle, GPU two-reduction CSR,
+        # generic single-reduction d16, diav carry), constant vs variable coefficients
+        "vcdiv": [
+            ("coef1", 300, f"{PY} -u bench/vc_divergence.py --coef 1"),
+            ("coef0", 300, f"{PY} -u bench/vc_divergence.py --coef 0"),
+        ],
+        "vcb": [
             ("b16384", 300, bench("--coef 1 --steps 100 --warmup 10 --phases 0")),
             ("b16384_generic", 300, bench("--coef 1 --steps 50 --warmup 5 --phases 0 --set carry_vc=0")),
             ("b4096", 300, bench("--coef 1 --grid 4096 --steps 1000 --warmup 100 --phases 0")),
