@@ -577,7 +577,10 @@ void GpuCgSolver::setup() {
     // line-carry pass: whole 64-row slices per grid line (2-D) / plane (3-D), the stencil path's
     // format and layout; applies to a launch whose slices are one range of whole lines
     const int64_t gl = partition_granule(spec_);
-    const bool ok = opt_.recurrence == 1 && opt_.format == 1 && (d16_ || c8_) && opt_.form.interleave == 1 &&
+    // plain SELL-64 (int32 columns): a 3-D stencil whose +-plane offsets do not fit d16 and whose values
+    // overflow c8 (variable coefficients at N >= 182) -- only the diav plane carry below can take it
+    const bool plain3 = !d16_ && !c8_ && stencil_plane(spec_) > 0 && opt_.form.carry != 1;
+    const bool ok = opt_.recurrence == 1 && opt_.format == 1 && (d16_ || c8_ || plain3) && opt_.form.interleave == 1 &&
                     win_doubles_ == 0 && info_.max_row_len <= 8 &&
                     info_.spmv_param >= info_.max_row_len && info_.spmv_param >= 4 && gl > 1 && gl % 64 == 0 &&
                     n % gl == 0 && L_.row_begin % gl == 0 && !perm_.get();
@@ -641,9 +644,11 @@ void GpuCgSolver::setup() {
                 "carry_vc: needs a symmetric 2-D 5-point / 3-D 7-point stencil without a c8 dictionary, ap_recompute "
                 "on (3-D: p3 on, N a multiple of 64, ranks below 2^29 rows)");
       // auto: only the specialised pass (2-D stencils); with the slow path (3-D's +-N gathers) it
-      // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log)
-      if (opt_.form.carry == 1 || !carry_general_) carry_all_ = apply(tr_all_, g_all_);
-      if (split_ && (opt_.form.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
+      // measured slower than the generic pass (288 vs 311 it/s at 512^3, profiles/sweep_carry.log).
+      // Plain SELL-64 has no carry kernels of its own: only the diav conversion above makes it one
+      const bool carry_ok = !plain3 || diav_;
+      if (carry_ok && (opt_.form.carry == 1 || !carry_general_)) carry_all_ = apply(tr_all_, g_all_);
+      if (carry_ok && split_ && (opt_.form.carry == 1 || !carry_general_)) carry_int_ = apply(tr_int_, g_int_);
     }
     info_.carry = carry_all_ || carry_int_;
     // Ap recomputed instead of stored: the specialised 2-D pass over every owned line in one launch
@@ -689,6 +694,7 @@ void GpuCgSolver::setup() {
       if (diav3_) {  // back to the d16 pass with the general carry (the 3-D stencil without the dictionary)
         carry_general_ = true;
         carry_lo2_ = 0;
+        if (!d16_ && !c8_) carry_all_ = carry_int_ = info_.carry = false;  // plain SELL-64: the generic pass
       }
       diav_ = diav3_ = false;
       info_.dia_uniform = 0.0;
