@@ -129,7 +129,11 @@ def test_varcoef_local_ranks_agree_with_single_rank(mcg, world):
     assert all(r["ap_recompute"] for r in many["ranks"])
     r1, rp = one["ranks"][0]["rnorm"], many["ranks"][0]["rnorm"]
     assert abs(r1 - rp) <= 1e-12 * r1
-    np.testing.assert_allclose(many["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
+    # the ranks' dot products add their block partials in another order: on this ill-conditioned
+    # operator that rounding moves a few entries of x by ~1e-10 after 40 steps (measured 1.5e-10 at
+    # P = 2), norm-wise far less (test_varcoef_2000_iterations_track_cpu_oracle: the drift)
+    np.testing.assert_allclose(many["x"], one["x"], rtol=1e-9, atol=1e-12 * np.abs(one["x"]).max())
+    assert np.linalg.norm(many["x"] - one["x"]) <= 1e-11 * np.linalg.norm(one["x"])
 
 
 def _vc3(mcg, n=64, **kw):
