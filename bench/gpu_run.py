@@ -356,6 +356,12 @@ def recipes(a) -> dict:
                                         "--set carry_vc=0")),
         ] + counters("vc_dram", "k_cg_carry_ar", "--coef 1 --steps 8 --warmup 2")
           + counters("vc3_dram", "k_cg_carry_ar3", "--coef 1 --problem poisson3d --grid 512 --steps 8 --warmup 2"),
+        # r4: 3-D lean plane carry across sizes: below / past 2^29 rows (BIG: bases moved along the run)
+        "sizes3": [
+            (f"n{n}", 400, bench(f"--problem poisson3d --grid {n} --steps {st} --warmup 4 --phases 0 --no-verify"))
+            for n, st in ((512, 60), (640, 40), (768, 30), (800, 30), (832, 20), (1024, 12))
+        ] + [("n832_kw8", 400, bench("--problem poisson3d --grid 832 --steps 20 --warmup 4 --phases 0 --no-verify "
+                                     "--set carry3_kw=8"))],
         # r4: ranks past 2^29 rows on the lean carries (BIG kernels)
         "large": [
             ("pytest", 900, f"{PY} -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_large.py"),
