@@ -165,7 +165,7 @@ __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat,
   auto ld = [&](int64_t i) { return UNI ? uni_u64(dpat[i]) : dpat[i]; };
   WA = WB = WC = 0u;
   // 32-bit byte offsets: from kernel-wide bases (ext_len < 2^29), or past that (BIG kernels) from
-  // per-run bases (big = 1, the 2-D loop: lines -3 .. the run's end + 4 inside 4 GiB) or bases moved
+  // per-run bases (big = 1: lines / planes -3 .. the run's end + 4 inside 4 GiB) or bases moved
   // along the run (big = 2, the 3-D loop)
   if (dpat == nullptr || l1 - l0 < 3 || nl < 4) return false;
   if (ext_len >= ((int64_t)1 << 29) &&
@@ -1188,7 +1188,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
       constexpr int LD = 3, ED = 2, UNR = 6;
       uint32_t WA = 0, WB = 0, WC = 0;
       if constexpr (LEAN && !VC) {  // every run checked at setup (carry_lean_failures)
-        (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC, BIG ? 2 : 0);
+        (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC, BIG ? 1 : 0);
         __syncthreads();  // the previous job's last step has read its LDS slots
       }
       if constexpr (LEAN && VC) {
@@ -1450,8 +1450,10 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           const uint32_t l8 = (uint32_t)lane << 3;
           const uint32_t LOB = (uint32_t)LO << 3;                         // one plane of the vectors
           const uint32_t SB = (uint32_t)(2 * SS) << 3;                    // one plane of the edge arrays
-          // BIG: pointers re-based at plane mb (ext: plane mb - 3, x: plane mb) by rebase(); the
-          // 32-bit offsets are then (j - mb) planes from there.  !BIG: mb = 0, kernel-wide bases
+          // BIG: pointers based at the run's plane -3 (ext) / 0 (x) once (the setup keeps every run's
+          // planes -3 .. end + 4 within 4 GiB: carry3_runs max_chunk; a base moved along the run spilled
+          // 60 VGPRs and ran at half the rate); the 32-bit offsets are then planes from there.  !BIG:
+          // kernel-wide bases
           int32_t mb = 0;
           const double *po_ = po, *ro_ = ro, *apo_ = apo;
           double *pn_ = pn, *rn_ = rn, *x_ = x, *apw_ = apw;
@@ -1644,11 +1646,9 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           if (m_lo == 1) lstep(clamped, 0, vals(WA), VB, 1);
           m = m_lo;
           for (; m + UNR - 1 <= m_hi; m += UNR) {
-            rebase(m);
 #pragma unroll
             for (int u = 0; u < UNR; ++u) lstep(unclamped, m + u, VB, VB, 1);
           }
-          rebase(m);
           for (; m <= m_hi; ++m) lstep(unclamped, m, VB, VB, 1);
           if (m < n_run) {
             const VSet VL = vals(WC);
@@ -2126,18 +2126,19 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
     if (l0 >= l1) continue;
     uint32_t a, b, c;
     // past 2^29 the BIG kernels re-base: per run (2-D), along the run (3-D)
-    if (!lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c, kw == 0 ? 1 : 2)) ++f;
+    if (!lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c, 1)) ++f;
   }
   if (f) atomicAdd(fails, f);
 }
 
 }  // namespace
 
-int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl) {
+int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk) {
   if (nb <= 0 || jpr <= 0 || nl <= 0) return 1;
   int32_t best = 1;
   int64_t best_cost = INT64_MAX;
   for (int64_t r = 1; r <= 64 && (r == 1 || nl / r >= 4); ++r) {
+    if (max_chunk > 0 && (nl + r - 1) / r > max_chunk) continue;  // BIG: a run within 4 GiB of its base
     const int64_t rounds = (jpr * r + nb - 1) / nb, cost = rounds * ((nl + r - 1) / r + 3);
     if (cost < best_cost) {
       best_cost = cost;
@@ -2445,7 +2446,7 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
     MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
     return;
   }
-  const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: bases moved along the run
+  const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: per-run bases
 #define MCG_A3(QD, PAIR, KW, P3, ...)                                                                         \
   hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, stream, S, v, \
                      own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)

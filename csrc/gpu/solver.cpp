@@ -676,6 +676,9 @@ void GpuCgSolver::inject_fault_(int k) {
               : pmat_ ? r_.get()
               : opt_.form.interleave == 1 ? ra_[(k + 1) & 1].get() + 2 * L_.own_off  // .x of the first owned pair
                                      : ((opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get()) + L_.own_off;
+  // the three-term carries recover r from the two p's and read a stored r only past their runs' ends:
+  // poison p_{k-1}, which pass k reads everywhere
+  if (ar_ && p3_ && opt_.recurrence == 1) r = p_[(k + 1) & 1].get() + L_.own_off;
   MCG_HIP(hipMemcpyAsync(r, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
 }
 

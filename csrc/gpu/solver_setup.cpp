@@ -709,7 +709,9 @@ void GpuCgSolver::setup() {
     if (ar3_) {
       g_all_ = std::max(1, ncu_ * (diav3_ ? 8 : 16) / kw);
       const int64_t jpr = (int64_t)(carry_lo2_ / kw) * (carry_lo2_ / 64);
-      tr_all_.runs3 = opt_.form.carry3_runs < 0 ? kern::carry3_runs(g_all_, jpr, n / gl) : opt_.form.carry3_runs;
+      // past 2^29 rows the lean runs keep their planes -3 .. end + 4 within 4 GiB of a per-run base
+      const int64_t max_chunk = L_.ext_len >= ((int64_t)1 << 29) ? ((int64_t)1 << 32) / (gl * 8) - 8 : 0;
+      tr_all_.runs3 = opt_.form.carry3_runs < 0 ? kern::carry3_runs(g_all_, jpr, n / gl, max_chunk) : opt_.form.carry3_runs;
     }
     info_.ar3_kw = ar3_ ? kw : 0;
     info_.ar3_runs = ar3_ ? tr_all_.runs3 : 0;

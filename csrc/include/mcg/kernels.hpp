@@ -324,8 +324,10 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
 // blocks over ss * nl slices that do not qualify for the lean step (SellDev::dpat); 0 lets the
 // three-term passes launch their lean-only kernels (`lean`).  Synchronises the stream.
 // The 3-D plane carry's run count (TileRanges::runs3) for `nb` blocks, `jpr` jobs per run and nl
-// planes: the R whose job rounds x (planes per run + the 3-plane prologue) is least (ties: fewer runs)
-int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl);
+// planes: the R whose job rounds x (planes per run + the 3-plane prologue) is least (ties: fewer runs);
+// max_chunk > 0: only runs of at most that many planes (past 2^29 rows a lean run keeps its planes
+// within 4 GiB of its base)
+int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk = 0);
 // the 2-D carry's job decomposition of a launch of nw waves over nl lines of ss slices (every line in
 // one launch): runs per slice column and lines per run
 void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk);

@@ -91,7 +91,7 @@ def test_checkpoint_rejects_perturbed_user_matrix_or_rhs(mcg, tmp_path):
         mcg.CGSolver(mcg.csr_problem(T, b=b + 1.0), **kw).load_checkpoint(prefix)
 
 
-@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "csr"), (1, "sell16"), (2, "sell16")])
+@pytest.mark.parametrize("recurrence,fmt", [(0, "csr"), (1, "csr"), (1, "sell16"), (1, "sellc8"), (2, "sell16")])
 def test_fault_injection_latches_breakdown(mcg, recurrence, fmt):
     spec = mcg.make_problem("poisson2d", n=64)
     out = mcg.CGSolver(spec, recurrence=recurrence, format=fmt, inject_nan_at=5, check_every=4).solve()
