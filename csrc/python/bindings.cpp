@@ -726,7 +726,7 @@ PYBIND11_MODULE(_C, m) {
                            static_cast<hipMemcpyKind>(kind), as_stream(stream)), "memcpy async failed");
   }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("kind"), py::arg("stream"),
      "probe: hipMemcpyAsync of kind (3 = device to device, 1024 = device to device without compute units)");
-  k.def("carry3_runs", &kern::carry3_runs, py::arg("blocks"), py::arg("jobs_per_run"), py::arg("planes"),
+  k.def("carry3_runs", &kern::carry3_runs, py::arg("blocks"), py::arg("jobs_per_run"), py::arg("planes"), py::arg("max_chunk") = 0,
         "the 3-D plane carry's runs of planes per job column (setup's choice)");
   k.def("stream_destroy", [](uintptr_t st) { MCG_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(st)), "stream destroy failed"); });
   k.attr("TILE_ROWS") = kTileRows;
