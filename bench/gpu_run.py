@@ -297,6 +297,12 @@ def recipes(a) -> dict:
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
             for rep in (1, 2, 3) for tag, kv in (("mix", ""), ("r3", "--set lean_depth=3"))
         ] + [("g16384", 200, bench("--phases 0"))],
+        "mix2": [
+            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
+            for rep in (1, 2)
+            for tag, kv in (("mix", ""), ("e16", "--set lean_depth=16 --set lean_bpc=6 --set lean_depth_odd=14 "
+                                                  "--set lean_bpc_odd=4"))
+        ],
         # r4: tile values fp32 vs fp64 storage, interleaved, with DRAM / L2 counters of each
         "c5ab": [
             (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
