@@ -173,6 +173,9 @@ def recipes(a) -> dict:
             ("noag_thin", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 --set ag_overlap=0")),
             ("ag_fat", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330,fat")),
             ("ag_null", 400, bench(f"{c5} --steps 6 --warmup 2")),
+            ("ag_thin_eager", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 --no-graph")),
+            ("noag_thin_eager", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 --no-graph "
+                                           f"--set ag_overlap=0")),
             ("ag_copy", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,0,copy")),
             ("noag_copy", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,0,copy --set ag_overlap=0")),
         ],
