@@ -264,7 +264,11 @@ def test_local_ranks_halo_hide_copy_engine(mcg, problem, n, coef, world):
         outs[hh] = r
     one = C.run_local_ranks(spec.native(), _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1),
                             1, 30, True)
+    # the variable-coefficient operator is ~100x worse conditioned: the ranks' other partial-sum order
+    # moves a few entries of x by ~1e-11 (test_gpu_varcoef.py: the rounding drift)
+    rtol = 1e-9 if coef else 1e-12
     for hh in (0, 1):
         rp, r1 = outs[hh]["ranks"][0]["rnorm"], one["ranks"][0]["rnorm"]
         assert abs(rp - r1) <= 1e-12 * r1
-        np.testing.assert_allclose(outs[hh]["x"], one["x"], rtol=1e-12, atol=1e-14 * np.abs(one["x"]).max())
+        np.testing.assert_allclose(outs[hh]["x"], one["x"], rtol=rtol, atol=1e-14 * np.abs(one["x"]).max())
+        assert np.linalg.norm(outs[hh]["x"] - one["x"]) <= (1e-11 if coef else 1e-13) * np.linalg.norm(one["x"])
