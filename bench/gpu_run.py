@@ -300,6 +300,16 @@ def recipes(a) -> dict:
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
             for rep in (1, 2, 3) for tag, kv in (("mix", ""), ("r3", "--set lean_depth=3"))
         ] + [("g16384", 200, bench("--phases 0"))],
+        # a P = 8 rank's share of 16384^2 (2048 lines, 8 blocks per CU: the driver's N = 8 scaling
+        # point) and of 4096^2 (512 lines) with the packed-edge geometry
+        "simmix": [
+            (f"{tag}_{rep}", 200, bench(f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 {kv}"))
+            for rep in (1, 2)
+            for tag, kv in (("auto", ""), ("m10", "--set lean_depth=13 --set lean_bpc=10 --set lean_depth_odd=14 "
+                                                  "--set lean_bpc_odd=8"),
+                            ("m5", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=14 --set lean_bpc_odd=4"),
+                            ("e14", "--set lean_depth=14"))
+        ],
         "mix2": [
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
             for rep in (1, 2)
