@@ -77,3 +77,16 @@ def test_plane_carry_run_count_fills_rounds(mcg):
     rounds = -(-144 * r // 256)
     assert r > 1 and rounds * (-(-384 // r) + 3) < 384 + 3
     assert k.carry3_runs(256, 8, 64) <= 16  # runs keep >= 4 planes
+
+
+def test_plane_carry_runs_past_2_29_rows_stay_within_4_gib(mcg):
+    """Past 2^29 rows a lean plane-carry run keeps its planes -3 .. end + 4 within 4 GiB of one 64-bit
+    base (per-run bases; bases moved along the run spilled 60 VGPRs and ran at half rate): carry3_runs'
+    max_chunk caps the planes per run -- 1024^3 (8 MiB planes) at most 504, 832^3 at most 767."""
+    k = mcg.native().kernels
+    for n, cap in ((1024, (1 << 32) // (1024 * 1024 * 8) - 8), (832, (1 << 32) // (832 * 832 * 8) - 8)):
+        jpr = (n // 16) * (n // 64)  # jobs per run of the kw = 16 plane carry
+        r = k.carry3_runs(256, jpr, n, cap)
+        assert -(-n // r) <= cap, (n, r, cap)
+        assert k.carry3_runs(256, jpr, n) <= r  # the cap only ever adds runs
+    assert k.carry3_runs(256, 256, 512, 0) == k.carry3_runs(256, 256, 512)
