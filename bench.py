@@ -326,8 +326,9 @@ def _run_rank(args, out_fd) -> int:
                 # storage the timed pass streams (the carries read SELL-64/dia4 codes; their lean runs
                 # only the per-slice pattern words of uniform slices)
                 "format": (("sell64-dia4, uniform-slice patterns" if info.get("lean_only") else "sell64-dia4")
-                           if info.get("dia4") else info["format"] + (", fp32-exact values (8 B/entry)"
-                                                                      if info.get("tile_vals32") else "")),
+                           if info.get("dia4") else
+                           "sell64-diav (each row's own values streamed)" if info.get("diav") else
+                           info["format"] + (", fp32-exact values (8 B/entry)" if info.get("tile_vals32") else "")),
                 "recurrence": info["recurrence"],
                 "pass": pass_label(info, args.problem),
                 **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
