@@ -159,8 +159,8 @@ def test_library_default_is_the_cli_fast_path(mcg):
     s = mcg.CGSolver(mcg.make_problem("poisson2d", n=1024))
     i = s.info
     assert i["carry"] and i["ap_recompute"] and i["dia4"] and i["p3"] and i["lean_only"], i
-    out = mcg.solve("poisson2d", n=1024, tol=1e-6)
-    assert out["converged"]
+    out = mcg.solve("poisson2d", n=1024, tol=1e-6, maxit=20000)  # 1024^2 needs more than the reference's 2000
+    assert out["converged"] and out["rnorm"] <= 1e-6
     d = mcg.CGSolver(mcg.make_problem("demo"))
     assert d.info["recurrence"] == "two-reduction"
 
