@@ -335,21 +335,20 @@ def test_three_term_carry_refusal(mcg):
 @pytest.mark.parametrize("n,kw", [(64, 4), (128, 4), (128, 8), (128, 16)])
 def test_ap_recompute_3d_matches_store_form(mcg, n, kw):
     """3-D plane carry that recomputes Ap (SELL-64/dia4, +-N rows through LDS between the block's
-    kw waves, the outer lines' Ap stored): the same recurrence as the store-form plane carry.  With
-    kw = 4 the blocks, waves and rows are the store form's, so every bit agrees; other kw group the
-    dot-product partials differently (rounding only)."""
+    kw waves, the outer lines' Ap stored): the same recurrence as the store-form plane carry.  Its runs
+    of planes per job column are chosen to fill whole rounds of blocks (carry3_runs), so the
+    dot-product partials group differently from the store form's: the same iterations, rounding only
+    (kw = 4 agreed bit for bit while both used one run per column)."""
     spec = mcg.make_problem("poisson3d", n=n, rhs="random")
     a = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=1, carry3_kw=kw, p3=0, check_every=8)
     b = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=0, check_every=8)
     assert a.info["ap_recompute"] and a.info["dia4"] and a.info["ar3_kw"] == kw
     assert not b.info["ap_recompute"] and b.info["carry"]
     ra, rb = a.solve(), b.solve()
-    assert ra["converged"] and abs(ra["iterations"] - rb["iterations"]) <= (0 if kw == 4 else 1)
-    if kw == 4:
-        assert ra["rnorm"] == rb["rnorm"]
-        np.testing.assert_array_equal(ra["x_local"], rb["x_local"])
-    else:
-        np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-9, atol=1e-12)
+    assert ra["converged"] and abs(ra["iterations"] - rb["iterations"]) <= 1
+    if ra["iterations"] == rb["iterations"]:
+        assert abs(ra["rnorm"] - rb["rnorm"]) <= 1e-10 * rb["rnorm"]
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-9, atol=1e-12)
     for its in (23, 24):
         outs = []
         for s in (a, b):
