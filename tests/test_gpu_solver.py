@@ -357,12 +357,8 @@ def test_ap_recompute_3d_matches_store_form(mcg, n, kw):
             s.finalize()
             outs.append((s.result(), s._s.x_local()))
         assert outs[0][0]["iterations"] == its
-        if kw == 4:  # x is elementwise (same bits); ||r_m|| of the final pass sums rows in another grouping
-            assert abs(outs[0][0]["rnorm"] - outs[1][0]["rnorm"]) <= 1e-14 * outs[1][0]["rnorm"]
-            np.testing.assert_array_equal(outs[0][1], outs[1][1])
-        else:
-            assert abs(outs[0][0]["rnorm"] - outs[1][0]["rnorm"]) <= 1e-11 * outs[1][0]["rnorm"]
-            np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-10, atol=1e-13)
+        assert abs(outs[0][0]["rnorm"] - outs[1][0]["rnorm"]) <= 1e-11 * outs[1][0]["rnorm"]
+        np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-10, atol=1e-13)
     tr = a.true_residual_norm()
     assert abs(tr - outs[0][0]["rnorm"]) <= 1e-8 * tr
 
