@@ -68,6 +68,7 @@ def recipes(a) -> dict:
             ("bench_3d", 200, bench("--problem poisson3d --grid 512")),
         ],
         "tests": [("pytest_gpu", 900, f"{PYTEST} tests -m gpu")],
+        "fix3d": [("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'ap_recompute_3d'")],
         # the whole GPU suite without stopping at the first failure (every failure in one call)
         "suite": [("pytest_gpu", 1000, f"{PY} -u -m pytest -q --timeout 300 --timeout-method thread tests -m gpu")],
         "headline": [
