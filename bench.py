@@ -334,7 +334,7 @@ def _run_rank(args, out_fd) -> int:
                 **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
                     if info.get("allgather") else ("window, exchanged ahead || all-reduce" if info.get("halo_ahead")
                                                    else "window")} if (n_gpus > 1 or sim) else {}),
-                "hipgraph": use_graph and info.get("graph_fallbacks", 0) == 0,
+                "hipgraph": bool(info.get("graphs", use_graph)) and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
                 "comm": args.comm,

@@ -357,6 +357,15 @@ def recipes(a) -> dict:
             for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
                                 ("spin20_ahead", "10,20", ""), ("null", "0,0", ""))
         ],
+        # the same shares with eager launches (copy-engine copies captured in hipGraphs replay slowly)
+        "hide_eager": [
+            (f"{g}_{tag}", 200, bench(f"{'--grid ' + str(g) if g != 512 else '--problem poisson3d --grid 512'} "
+                                      f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 --no-graph "
+                                      f"--comm dual --delay-comm {dc} {hh}"))
+            for g in (16384, 4096)
+            for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
+                                ("spin20_ahead", "10,20", ""), ("null", "0,0", ""))
+        ],
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),

@@ -493,6 +493,11 @@ void GpuCgSolver::setup() {
     info_.ag_local_frac = sp[ns] > 0 ? (double)(64 * loc) / (double)sp[ns] : 0.0;
   }
   info_.ag_overlap = ag_overlap_;
+  // tiles with the all-gather overlap run eagerly: replayed from a hipGraph the all-gather branch did
+  // not start beside the own-segment half (a P = 8 share with a 2.3 ms all-gather: 18.6 it/s captured,
+  // 19.3 eager = the same as with no all-gather at all, profiles/r4/c5ag); at ~50 ms an iteration the
+  // launches cost nothing
+  if (ag_overlap_ && tiles_) opt_.use_graph = false;
 
   // ---- vectors ----
   b_.allocate(n, "b", 8);
@@ -889,6 +894,7 @@ void GpuCgSolver::setup() {
   allocate_vectors_();
   g_b_ = kern::grid_for((n + 1) / 2, 256, 4);  // residual update / dot kernels: 1024 blocks (best measured)
   info_.grid_a = g_all_;
+  info_.graphs = opt_.use_graph;
   info_.grid_odd = g_odd_;
   info_.grid_b = g_b_;
   const bool split = split_ || hide_;

@@ -69,6 +69,7 @@ struct SolverInfo {
                               // the all-reduce; one full pass per iteration (CgOptions::halo_ahead)
   double ag_local_frac = 0.0; // own-block slots / all slots (the part of the SpMV that hides the all-gather)
   int graph_fallbacks = 0;    // graph captures / launches that fell back to eager iterations
+  bool graphs = false;        // iterations replayed as hipGraphs (false: eager launches)
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool halo_hide = false;  // PassForm::halo_hide: the pass split around a copy-engine halo

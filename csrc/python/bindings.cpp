@@ -483,6 +483,7 @@ PYBIND11_MODULE(_C, m) {
         d["ap_recompute"] = i.ap_recompute;
         d["ag_local_frac"] = i.ag_local_frac;
         d["graph_fallbacks"] = i.graph_fallbacks;
+        d["graphs"] = i.graphs;
         d["xcd_map"] = i.xcd_map;
         d["dia4"] = i.dia4;
         d["diav"] = i.diav;
