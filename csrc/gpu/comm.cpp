@@ -2,6 +2,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include "mcg/check.hpp"
@@ -112,13 +113,14 @@ void DelayComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
                               const int* widths) {
   if (!L.has_halo()) return;
   if (copy_) {  // the messages' bytes through the copy engines (source: the rank's own first rows)
+    std::vector<CopyFan::Job> jobs;
     for (int v = 0; v < nvec; ++v) {
       const int64_t w = widths ? widths[v] : 1;
       for (const HaloRange& h : L.recvs)
-        MCG_HIP(hipMemcpyAsync(ext_vecs[v] + w * L.ext_index(h.gbegin), ext_vecs[v] + w * L.own_off,
-                               w * h.count * sizeof(double), hipMemcpyDeviceToDeviceNoCU, stream),
-                "halo copy failed");
+        jobs.push_back({ext_vecs[v] + w * L.ext_index(h.gbegin), ext_vecs[v] + w * L.own_off,
+                        (size_t)(w * h.count) * sizeof(double), nullptr, 0});
     }
+    fan_->run(stream, jobs);
     return;
   }
   if (halo_us_ > 0) kern::spin(nullptr, halo_us_, fat_, 1, stream);
@@ -147,6 +149,41 @@ void Comm::abort() {
   aborted_ = true;
   if (halo_ && halo_ != reduce_) (void)ncclCommAbort(halo_);
   if (reduce_) (void)ncclCommAbort(reduce_);
+}
+
+CopyFan::~CopyFan() {
+  for (hipStream_t st : st_) (void)hipStreamDestroy(st);
+  for (hipEvent_t ev : ev_) (void)hipEventDestroy(ev);
+  if (fork_) (void)hipEventDestroy(fork_);
+}
+
+void CopyFan::run(hipStream_t stream, const std::vector<Job>& jobs) {
+  auto issue = [](hipStream_t st, const Job& j) {
+    if (j.wait_flag != nullptr)
+      MCG_HIP(hipStreamWaitValue64(st, j.wait_flag, j.wait_value, hipStreamWaitValueEq, ~0ull), "copy fan: wait failed");
+    if (j.bytes > 0) MCG_HIP(hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToDeviceNoCU, st), "copy fan: copy failed");
+  };
+  if (jobs.size() <= 1) {
+    for (const Job& j : jobs) issue(stream, j);
+    return;
+  }
+  const size_t ns = std::min<size_t>(jobs.size(), kMaxStreams);
+  if (fork_ == nullptr) MCG_HIP(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "copy fan: event create failed");
+  while (st_.size() < ns) {
+    hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;
+    MCG_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "copy fan: stream create failed");
+    MCG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "copy fan: event create failed");
+    st_.push_back(st);
+    ev_.push_back(ev);
+  }
+  MCG_HIP(hipEventRecord(fork_, stream), "copy fan: event record failed");
+  for (size_t i = 0; i < ns; ++i) MCG_HIP(hipStreamWaitEvent(st_[i], fork_, 0), "copy fan: stream wait failed");
+  for (size_t j = 0; j < jobs.size(); ++j) issue(st_[j % ns], jobs[j]);
+  for (size_t i = 0; i < ns; ++i) {
+    MCG_HIP(hipEventRecord(ev_[i], st_[i]), "copy fan: event record failed");
+    MCG_HIP(hipStreamWaitEvent(stream, ev_[i], 0), "copy fan: stream wait failed");
+  }
 }
 
 }  // namespace mcg

@@ -63,9 +63,6 @@ PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int wo
 }
 
 PeerHaloComm::~PeerHaloComm() {
-  for (hipStream_t st : ag_streams_) (void)hipStreamDestroy(st);
-  for (hipEvent_t ev : ag_ev_) (void)hipEventDestroy(ev);
-  if (fork_ev_) (void)hipEventDestroy(fork_ev_);
   for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
   if (flags_) (void)hipFree(flags_);
 }
@@ -191,51 +188,28 @@ void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, 
     MCG_CHECK(it != bufs_.end(), "peer halo: vector not registered");
     idx[k] = (int)(it - bufs_.begin());
   }
-  // the all-gather layout pulls a whole block from every peer: one stream per peer, forked from and
-  // joined back to `stream` by events (captured as graph branches), so the copies can run on several
-  // copy engines at once instead of one after another on one queue
-  const bool fan = L.allgather && sources.size() > 1;
-  if (fan) {
-    if (ag_streams_.size() < sources.size()) {
-      if (fork_ev_ == nullptr)
-        MCG_HIP(hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming), "peer halo: event create failed");
-      while (ag_streams_.size() < sources.size()) {
-        hipStream_t st = nullptr;
-        hipEvent_t ev = nullptr;
-        MCG_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "peer halo: stream create failed");
-        MCG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "peer halo: event create failed");
-        ag_streams_.push_back(st);
-        ag_ev_.push_back(ev);
-      }
-    }
-    MCG_HIP(hipEventRecord(fork_ev_, stream), "peer halo: event record failed");
-  }
-  for (size_t j = 0; j < sources.size(); ++j) {
-    const int q = sources[j];
-    hipStream_t qs = stream;
-    if (fan) {
-      qs = ag_streams_[j];
-      MCG_HIP(hipStreamWaitEvent(qs, fork_ev_, 0), "peer halo: stream wait failed");
-    }
-    MCG_HIP(hipStreamWaitValue64(qs, flags_ + q, v, hipStreamWaitValueEq, ~0ull), "peer halo: wait failed");
+  // every pull (source peer x vector) on a copy stream of its own, each after its owner's ready flag;
+  // then, on `stream` (after all of them), the done flags that let each owner reuse its rows
+  std::vector<CopyFan::Job> jobs;
+  for (int q : sources) {
     // the owner's ext index of global row g: its own block starts at own_off(q) with row_begin(q);
     // ghost ranges come from its owned rows, located through the owner's registered layout numbers
+    bool any = false;
     for (const HaloRange& h : L.recvs) {
       if (h.peer != q) continue;
       for (int k = 0; k < nvec; ++k) {
         const int64_t w = widths ? widths[k] : 1;
         const int64_t src_row = peer_own_off_.at(q) + (h.gbegin - peer_row_begin_.at(q));
-        MCG_HIP(hipMemcpyAsync(ext_vecs[k] + w * L.ext_index(h.gbegin), peer_bufs_[q][idx[k]] + w * src_row,
-                               w * h.count * sizeof(double), hipMemcpyDeviceToDeviceNoCU, qs),
-                "peer halo: copy failed");
+        jobs.push_back({ext_vecs[k] + w * L.ext_index(h.gbegin), peer_bufs_[q][idx[k]] + w * src_row,
+                        (size_t)(w * h.count) * sizeof(double), flags_ + q, v});
+        any = true;
       }
     }
-    MCG_HIP(hipStreamWriteValue64(qs, peer_flags_[q] + world_ + rank_, v, 0), "peer halo: flag write failed");
-    if (fan) {
-      MCG_HIP(hipEventRecord(ag_ev_[j], qs), "peer halo: event record failed");
-      MCG_HIP(hipStreamWaitEvent(stream, ag_ev_[j], 0), "peer halo: stream wait failed");
-    }
+    if (!any) jobs.push_back({nullptr, nullptr, 0, flags_ + q, v});  // no rows from q: still wait for it
   }
+  fan_.run(stream, jobs);
+  for (int q : sources)
+    MCG_HIP(hipStreamWriteValue64(stream, peer_flags_[q] + world_ + rank_, v, 0), "peer halo: flag write failed");
 }
 
 }  // namespace mcg

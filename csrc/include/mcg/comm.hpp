@@ -45,6 +45,32 @@ int rccl_version();             // ncclGetVersion of the RCCL this process runs 
 std::string rccl_library();     // path of the shared object that provides it
 ncclUniqueId unique_id_from_bytes(const std::string& b);
 
+// Several copy-engine copies (hipMemcpyDeviceToDeviceNoCU) at once: each on a stream of its own (up
+// to kMaxStreams, then round robin), forked from and joined back to the caller's stream by events, so
+// a graph captures them as branches.  One queue runs its copies one after another; a halo of 2 peers x
+// 3 vectors of 128 KiB was 6 serial copies.  A job may first wait for a 64-bit flag (stream wait-value).
+class CopyFan {
+ public:
+  static constexpr int kMaxStreams = 16;
+  struct Job {
+    void* dst;
+    const void* src;
+    size_t bytes;
+    uint64_t* wait_flag;  // nullptr: no wait
+    uint64_t wait_value;
+  };
+  CopyFan() = default;
+  CopyFan(const CopyFan&) = delete;
+  CopyFan& operator=(const CopyFan&) = delete;
+  ~CopyFan();
+  void run(hipStream_t stream, const std::vector<Job>& jobs);
+
+ private:
+  std::vector<hipStream_t> st_;
+  std::vector<hipEvent_t> ev_;
+  hipEvent_t fork_ = nullptr;
+};
+
 class Communicator {
  public:
   virtual ~Communicator() = default;
@@ -142,7 +168,8 @@ class DelayComm final : public Communicator {
   // copied from this rank's own rows with hipMemcpyDeviceToDeviceNoCU: a timing stand-in for the
   // peer-to-peer copies, the ghosts get wrong values) instead of a spin
   DelayComm(int rank, int world, double allreduce_us, double halo_us, bool fat = false, bool copy_halo = false)
-      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us), fat_(fat), copy_(copy_halo) {}
+      : rank_(rank), world_(world), ar_us_(allreduce_us), halo_us_(halo_us), fat_(fat), copy_(copy_halo),
+        fan_(std::make_unique<CopyFan>()) {}
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   void allreduce_sum(double*, size_t, hipStream_t stream) override;
@@ -154,6 +181,7 @@ class DelayComm final : public Communicator {
   int rank_, world_;
   double ar_us_, halo_us_;
   bool fat_, copy_;
+  std::unique_ptr<CopyFan> fan_;  // copy mode: the messages' copies side by side
 };
 
 // CU-free halo between the GPUs of one node (or processes / threads sharing one GPU): every rank
@@ -167,8 +195,8 @@ class DelayComm final : public Communicator {
 //     for each rank q reading from me: wait done[q] == v(s - 1) (q copied my previous rows), then
 //       write v(s) into q's ready[me] (my rows of this exchange are final: the call follows my pass)
 //     for each rank q I read from: wait ready[q] == v(s), pull the ranges, write v(s) into q's done[me]
-// The all-gather ghost layout (unstructured sparsity) takes the same path: every peer's block is a
-// receive range, pulled on a stream of its own (several copy engines at once).
+// Every pull (peer x vector) runs on a stream of its own (CopyFan: several copy engines at once); the
+// all-gather ghost layout (unstructured sparsity) takes the same path, every peer's block a range.
 // The all-reduce goes to `inner` (RCCL, or NullComm in a one-GPU rehearsal).
 class PeerHaloComm final : public Communicator {
  public:
@@ -206,9 +234,7 @@ class PeerHaloComm final : public Communicator {
   int64_t own_off_ = 0, row_begin_ = 0;
   std::vector<int64_t> peer_own_off_, peer_row_begin_;
   std::vector<void*> opened_;                    // IPC mappings to close
-  std::vector<hipStream_t> ag_streams_;          // all-gather layout: one copy stream per source peer
-  std::vector<hipEvent_t> ag_ev_;
-  hipEvent_t fork_ev_ = nullptr;
+  CopyFan fan_;                                  // the pulls side by side (one stream per copy)
   long seq_ = 0;
   long cap_n_ = 0;  // exchanges recorded by the capture in progress
   // A captured exchange replays the flag values of its capture, which continues the 1/2 alternation
