@@ -366,6 +366,16 @@ def recipes(a) -> dict:
             for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
                                 ("spin20_ahead", "10,20", ""), ("null", "0,0", ""))
         ],
+        "fan": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_peer.py tests/test_gpu_multirank.py -k 'peer or halo_hide'"),
+            ("check4", 180, f"{PY} -u bench/peer_halo_check.py --world 4 --n 512 --rounds 6"),
+        ] + [
+            (f"{g}_{tag}_{gr}", 200, bench(f"--grid {g} --sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 "
+                                            f"--comm dual --delay-comm {dc} {hh} {'--no-graph' if gr == 'eager' else ''}"))
+            for g in (16384, 4096) for gr in ("graph", "eager")
+            for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
+                                ("null", "0,0", ""))
+        ],
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),
