@@ -163,7 +163,11 @@ void CopyFan::run(hipStream_t stream, const std::vector<Job>& jobs) {
       MCG_HIP(hipStreamWaitValue64(st, j.wait_flag, j.wait_value, hipStreamWaitValueEq, ~0ull), "copy fan: wait failed");
     if (j.bytes > 0) MCG_HIP(hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToDeviceNoCU, st), "copy fan: copy failed");
   };
-  if (jobs.size() <= 1) {
+  // one stream while a graph is being captured: the forked wait-value / NoCU-copy branches crashed the
+  // capture (bench --halo-transport sdma, SIGSEGV at P = 2), the serial form captures and replays
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  MCG_HIP(hipStreamIsCapturing(stream, &cs), "copy fan: capture query failed");
+  if (jobs.size() <= 1 || cs != hipStreamCaptureStatusNone) {
     for (const Job& j : jobs) issue(stream, j);
     return;
   }
