@@ -113,6 +113,9 @@ void DelayComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
                               const int* widths) {
   if (!L.has_halo()) return;
   if (copy_) {  // the messages' bytes through the copy engines (source: the rank's own first rows)
+    // the all-gather layout's blocks side by side (CopyFan); window halos' small copies in one queue:
+    // fanned out over streams they took longer (a P = 8 share of 16384^2: 0.507 vs 0.301 ms an
+    // iteration with halo_hide, profiles/r4/fan)
     std::vector<CopyFan::Job> jobs;
     for (int v = 0; v < nvec; ++v) {
       const int64_t w = widths ? widths[v] : 1;
@@ -120,7 +123,12 @@ void DelayComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
         jobs.push_back({ext_vecs[v] + w * L.ext_index(h.gbegin), ext_vecs[v] + w * L.own_off,
                         (size_t)(w * h.count) * sizeof(double), nullptr, 0});
     }
-    fan_->run(stream, jobs);
+    if (L.allgather) {
+      fan_->run(stream, jobs);
+    } else {
+      for (const CopyFan::Job& j : jobs)
+        MCG_HIP(hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToDeviceNoCU, stream), "halo copy failed");
+    }
     return;
   }
   if (halo_us_ > 0) kern::spin(nullptr, halo_us_, fat_, 1, stream);

@@ -188,8 +188,8 @@ void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, 
     MCG_CHECK(it != bufs_.end(), "peer halo: vector not registered");
     idx[k] = (int)(it - bufs_.begin());
   }
-  // every pull (source peer x vector) on a copy stream of its own, each after its owner's ready flag;
-  // then, on `stream` (after all of them), the done flags that let each owner reuse its rows
+  // every pull (source peer x vector) after its owner's ready flag -- the all-gather layout's blocks on
+  // copy streams of their own -- then, on `stream`, the done flags that let each owner reuse its rows
   std::vector<CopyFan::Job> jobs;
   for (int q : sources) {
     // the owner's ext index of global row g: its own block starts at own_off(q) with row_begin(q);
@@ -207,7 +207,17 @@ void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, 
     }
     if (!any) jobs.push_back({nullptr, nullptr, 0, flags_ + q, v});  // no rows from q: still wait for it
   }
-  fan_.run(stream, jobs);
+  if (L.allgather) {
+    fan_.run(stream, jobs);  // whole blocks from every peer: several copy engines at once
+  } else {
+    // a window halo's few small copies in one queue (fanned out over streams they took longer:
+    // profiles/r4/fan); each waits for its owner's flag first
+    for (const CopyFan::Job& j : jobs) {
+      MCG_HIP(hipStreamWaitValue64(stream, j.wait_flag, j.wait_value, hipStreamWaitValueEq, ~0ull), "peer halo: wait failed");
+      if (j.bytes > 0)
+        MCG_HIP(hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToDeviceNoCU, stream), "peer halo: copy failed");
+    }
+  }
   for (int q : sources)
     MCG_HIP(hipStreamWriteValue64(stream, peer_flags_[q] + world_ + rank_, v, 0), "peer halo: flag write failed");
 }

@@ -182,7 +182,7 @@ class DelayComm final : public Communicator {
   int rank_, world_;
   double ar_us_, halo_us_;
   bool fat_, copy_;
-  std::unique_ptr<CopyFan> fan_;  // copy mode: the messages' copies side by side
+  std::unique_ptr<CopyFan> fan_;  // copy mode, all-gather layout: the blocks' copies side by side
 };
 
 // CU-free halo between the GPUs of one node (or processes / threads sharing one GPU): every rank
@@ -196,8 +196,8 @@ class DelayComm final : public Communicator {
 //     for each rank q reading from me: wait done[q] == v(s - 1) (q copied my previous rows), then
 //       write v(s) into q's ready[me] (my rows of this exchange are final: the call follows my pass)
 //     for each rank q I read from: wait ready[q] == v(s), pull the ranges, write v(s) into q's done[me]
-// Every pull (peer x vector) runs on a stream of its own (CopyFan: several copy engines at once); the
-// all-gather ghost layout (unstructured sparsity) takes the same path, every peer's block a range.
+// The all-gather ghost layout (unstructured sparsity) takes the same path, every peer's block a range
+// pulled on a stream of its own (CopyFan: several copy engines at once).
 // The all-reduce goes to `inner` (RCCL, or NullComm in a one-GPU rehearsal).
 class PeerHaloComm final : public Communicator {
  public:
@@ -235,7 +235,7 @@ class PeerHaloComm final : public Communicator {
   int64_t own_off_ = 0, row_begin_ = 0;
   std::vector<int64_t> peer_own_off_, peer_row_begin_;
   std::vector<void*> opened_;                    // IPC mappings to close
-  CopyFan fan_;                                  // the pulls side by side (one stream per copy)
+  CopyFan fan_;                                  // the all-gather layout's pulls side by side
   long seq_ = 0;
   long cap_n_ = 0;  // exchanges recorded by the capture in progress
   // A captured exchange replays the flag values of its capture, which continues the 1/2 alternation
