@@ -316,8 +316,7 @@ def recipes(a) -> dict:
         "mix2": [
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
             for rep in (1, 2)
-            for tag, kv in (("mix", ""), ("m15", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=15 "
-                                                  "--set lean_bpc_odd=4"))
+            for tag, kv in (("mix", ""), ("r3", "--set lean_depth=3"))
         ],
         # r4: tile values fp32 vs fp64 storage, interleaved, with DRAM / L2 counters of each
         "c5ab": [

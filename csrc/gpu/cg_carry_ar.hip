@@ -2331,10 +2331,10 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
 #define MCG_LWE(QD, PAIR, W)                                                                                   \
   hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true>), dim3(grid), dim3(kBS), 0, stream, S, v, \
                      own_off, tr, partials, pstride, st, tol, first, check, rc)
-    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4, 15: QD 5 at 4, 16: QD 3 at 6 (even))
+    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4; measured and dropped: QD 5 at 4
+    // for the odd passes, the same rate, and QD 3 at 6 for the even ones, which spills in the loop:
+    // 4096^2 7200 vs 9470 it/s, profiles/r4/mix2)
     if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
-    else if (depth == 16 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 6); }
-    else if (depth == 15 && !big) { if (pair) MCG_LWE(5, true, 4); else MCG_LWE(5, false, 4); }
     else if (depth == 14 && !big) { if (pair) MCG_LWE(4, true, 4); else MCG_LWE(4, false, 4); }
     // deeper prefetch (lean_depth 4 / 6: fewer waves per SIMD, more lines in flight per wave; small grids)
     else if (depth >= 6 && depth < 13 && !big) { if (pair) MCG_LWD(6, true, 2); else MCG_LWD(6, false, 2); }
