@@ -313,6 +313,12 @@ def recipes(a) -> dict:
                             ("m5", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=14 --set lean_bpc_odd=4"),
                             ("e14", "--set lean_depth=14"))
         ],
+        # r4: the lean / generic split on a user matrix with a few changed rows
+        "lsplit": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean'"),
+            ("ab4096", 200, f"{PY} -u bench/lean_split_ab.py --n 4096 --steps 2000 --warmup 100"),
+            ("ab8192", 300, f"{PY} -u bench/lean_split_ab.py --n 8192 --steps 800 --warmup 50"),
+        ],
         "mix2": [
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
             for rep in (1, 2)

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""A/B of the lean / generic split on a user matrix that is a 2-D Laplacian except for a few rows.
+
+One changed diagonal entry leaves one slice of one run off the uniform pattern: without the split the
+whole pass drops to the generic three-term kernels (the round-3 cliff, profiles/r3/lean: 581 vs 515
+it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, same matrix and RHS:
+
+  uniform   the unperturbed Laplacian (every run lean; the ceiling)
+  generic   the perturbed matrix, lean_split = 0 (the pre-split dispatch)
+  split     the perturbed matrix, lean_split auto
+
+Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
+    python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _laplacian(n):
+    import scipy.sparse as sp
+    T = sp.diags([-1.0, 2.0, -1.0], [-1, 0, 1], shape=(n, n), format="csr")
+    I = sp.identity(n, format="csr")
+    return (sp.kron(I, T, format="csr") + sp.kron(T, I, format="csr")).tocsr()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--spots", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    a = ap.parse_args()
+    import numpy as np
+
+    import cuda_mpi_parallel_amd as mcg
+
+    A = _laplacian(a.n)
+    rng = np.random.default_rng(7)
+    spots = rng.integers(0, a.n * a.n, a.spots)
+    B = A.copy()
+    B.setdiag(B.diagonal() + 0.5 * np.isin(np.arange(a.n * a.n), spots))
+    out = {"n": a.n, "spots": a.spots, "steps": a.steps, "its": {}, "info": {}}
+    for name, M, kw in (("uniform", A, {}), ("generic", B, {"lean_split": 0}), ("split", B, {})):
+        p = mcg.csr_problem(M, rhs="random")
+        s = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=-1.0, maxit=a.steps + a.warmup, **kw)
+        s.reset()
+        s.run(a.warmup)
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.run(a.steps)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        out["its"][name] = round(a.steps / dt, 1)
+        out["info"][name] = {k: s.info.get(k) for k in ("lean_only", "lean_split", "dia_uniform", "lean_mix")}
+        del s, p
+        print(json.dumps({"arm": name, "it_s": out["its"][name]}), flush=True)
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

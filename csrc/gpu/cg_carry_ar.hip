@@ -365,7 +365,12 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       // the kernel has no generic step at all (one kernel with both measured slower for each)
       constexpr int LD = QD + 1;
       uint32_t WA, WB, WC;
-      (void)lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC, BIG ? 1 : 0);
+      // lean_split: both launches decide a run the same way (size mode 1 in both: it only differs from
+      // mode 0 past 2^29 rows, where the lean launch runs the BIG kernels)
+      const bool elig = lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC,
+                                            (BIG || tr.lean_split != 0) ? 1 : 0);
+      if (tr.lean_split == 1 && !elig) continue;  // the generic launch takes this run
+      if (tr.lean_split == 2 && elig) continue;   // the lean launch took it
       if constexpr (LEAN > 0) {
         struct VSet {
           double v[5];

@@ -221,7 +221,10 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
   }
   const SellDev S = sell_view();
   if (ar_) {
-    MCG_CHECK(which == 0 || hide_, "Ap-recomputing carry: one launch per iteration (halo_hide: two bands)");
+    MCG_CHECK(which == 0 || hide_ || lean_split_,
+              "Ap-recomputing carry: one launch per iteration (halo_hide: two bands; lean_split: lean + generic runs)");
+    // the launch runs the lean-only kernels: every run qualifies, or (lean_split) the lean half
+    const bool lean_launch = lean_only_ || (lean_split_ && which == 1);
     v.ra_old = nullptr;
     v.ra_new = nullptr;
     v.ap_old = apx_[(k + 1) & 1].get();
@@ -243,20 +246,20 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     // passes 2 (their chains of 3 registers are renamed by the 3-step unroll, profiles/r2s6_p3_16384.md);
     // the lean ones 3 as well (4096^2 8191-8225 vs 8064-8084 it/s, 16384^2 586.4 vs 584.9,
     // profiles/r3/lean/README.md)
-    const int ld = (k & 1) != 0 ? lean_depth_odd_ : lean_depth_even_;
+    const int ld = !lean_launch ? 0 : ((k & 1) != 0 ? lean_depth_odd_ : lean_depth_even_);
     if (g_odd_ > 0 && which == 0 && !final_mode) {
       // the two parities' runs differ: each pass also stores r on the other decomposition's run ends
       TileRanges ta = tr;
       ta.alt_chunk = (k & 1) != 0 ? alt_chunk_even_ : alt_chunk_odd_;
       kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, ld > 0 ? ld : 3, S, v, L_.own_off, ta,
                         part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc, p3_, 3,
-                        lean_only_);
+                        lean_launch);
       return;
     }
-    const int depth = ((k & 1) == 0 && p3_ && !lean_only_) ? 2 : (lean_only_ && ld > 0 ? ld : 3);
+    const int depth = ((k & 1) == 0 && p3_ && !lean_launch) ? 2 : (lean_launch && ld > 0 ? ld : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, depth, S, v,
                       L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
-                      p3_, 3, lean_only_);
+                      p3_, 3, lean_launch);
     return;
   }
   if (!final_mode && ((which == 0 && carry_all_) || (which == 1 && carry_int_))) {
@@ -382,6 +385,19 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
   if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
 }
 
+// one single-reduction pass over every owned row: one launch, or (lean_split) the lean kernels over
+// the runs that qualify and then the generic ones over the rest, whose last arriver finishes the
+// reduction.  Returns the number of block partials written.
+int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
+  if (!lean_split_) {
+    enqueue_f1_(k, 0, 0, fused_red);
+    return (g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_;
+  }
+  enqueue_f1_(k, 1, 0, fused_red);
+  enqueue_f1_(k, 2, 0, fused_red);
+  return g_int_ + g_bnd_;
+}
+
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
   if (pmat_) {
     enqueue_iteration_split_(k);
@@ -407,7 +423,7 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     halo_pending_ = true;
   } else if (halo_ahead_) {
     ensure_ghosts_(k);
-    enqueue_f1_(k, 0, 0, fr);  // every owned row in one pass (the line-carry pass at P > 1 too)
+    np = enqueue_pass_(k, fr);  // every owned row in one pass (the line-carry pass at P > 1 too)
     // the next iteration's ghosts are this pass's outputs, final now: exchange them on the side
     // stream while the all-reduce runs (the join sits in front of the next pass)
     MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
@@ -439,9 +455,9 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     }
   } else if (use_halo_) {
     enqueue_halo_f1_(k, s0_);
-    enqueue_f1_(k, 0, 0, fr);
+    np = enqueue_pass_(k, fr);
   } else {
-    enqueue_f1_(k, 0, 0, fr);
+    np = enqueue_pass_(k, fr);
   }
   CgState* st = st_.get();
   if (!fr) kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);

@@ -788,7 +788,29 @@ void GpuCgSolver::setup() {
         auto_mix_ = false;
       }
     }
-    if (lean_ok(g) && (go == g || lean_ok(go))) {
+    const bool lean_all = lean_ok(g) && (go == g || lean_ok(go));
+    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && g % kern::kRedGroup == 0 &&
+        opt_.form.lean_bpc_odd <= 0) {
+      // some runs do not qualify: split the pass by run -- the lean kernels over the runs that do, the
+      // generic ones over the rest, on the same grid (the same runs), when most runs qualify
+      auto_mix_ = false;
+      lean_depth_even_ = lean_depth_odd_ = 0;
+      int64_t runs = 0, chunk = 0;
+      kern::carry_jobs_host((int64_t)g * 4, tr_all_.strip, nlines, runs, chunk);
+      const int64_t jobs = runs * tr_all_.strip;
+      const int64_t fails = kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, 0, 0, s0_, 0, 0, 0);
+      if (jobs > 0 && (opt_.form.lean_split == 1 ? fails < jobs : 2 * fails < jobs)) {
+        lean_split_ = true;
+        g_all_ = g;
+        tr_int_ = tr_all_;
+        tr_int_.lean_split = 1;
+        tr_bnd_ = tr_all_;
+        tr_bnd_.lean_split = 2;
+        g_int_ = g_bnd_ = g;
+        info_.lean_split = 1.0 - (double)fails / (double)jobs;
+      }
+    }
+    if (lean_all) {
       lean_only_ = true;
       g_all_ = g;
       g_odd_ = go == g ? 0 : go;
@@ -900,7 +922,7 @@ void GpuCgSolver::setup() {
   info_.graphs = opt_.use_graph;
   info_.grid_odd = g_odd_;
   info_.grid_b = g_b_;
-  const bool split = split_ || hide_;
+  const bool split = split_ || hide_ || lean_split_;
   fused_red_ = (opt_.recurrence == 1 && opt_.form.fused_reduce != 0) || opt_.recurrence == 2;
   auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
   // the boundary launch's partials start on a reduction-group boundary: round the interior grid up

@@ -97,6 +97,10 @@ struct PassForm {
                              // waves per SIMD / depth 4 with 4, cg_carry_ar.hip EP)
   int lean_bpc = 0;          // 2-D lean-only passes: blocks per CU of the grid (0 = auto: the largest of 16 / 8 / 4
                              // whose runs keep >= 64 lines)
+  int lean_split = -1;       // 2-D three-term dia4 carry when some runs' slice patterns are not uniform (a user matrix
+                             // with a few odd rows): the lean kernels over the runs that qualify, the generic ones
+                             // over the rest, in two launches; -1 = auto (when most runs qualify), 0 = off (every run
+                             // on the generic kernels)
   int lean_depth_odd = 0;    // ... the odd passes (x update paired in: one more stream) their own depth / grid; 0 = as
   int lean_bpc_odd = 0;      // the even passes (the two grids each reduce their own block partials)
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging

@@ -74,6 +74,10 @@ struct TileRanges {
   // runs, which this pass stores only on its own runs' first / last lines, so it also stores r on the
   // first / last line of every run of the other decomposition; 0 = both parities share the runs
   int32_t alt_chunk = 0;
+  // 2-D three-term dia4 carry split by run eligibility (a matrix whose slice patterns are uniform only
+  // in places): 1 = this launch (the lean kernels) takes only the runs that qualify for the lean loop,
+  // 2 = this launch (the generic kernels, same grid) only the others; 0 = every run
+  int32_t lean_split = 0;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);

@@ -45,6 +45,7 @@ struct SolverInfo {
   int grid_a = 0, grid_b = 0;
   int grid_odd = 0;  // 2-D lean-only odd passes on a grid of their own (CgOptions::form.lean_bpc_odd), else 0
   bool lean_mix = false;  // ... chosen by the setup: packed edges, even passes 5 waves / SIMD, odd depth 4
+  double lean_split = 0.0;  // > 0: lean and generic launches split by run (the fraction of runs on the lean one)
   int64_t max_row_len = 0;
   int spmv_variant = 0, spmv_param = 0;
   int recurrence = 0;
@@ -130,6 +131,7 @@ class GpuCgSolver {
   void enqueue_halo_f1_(int k, hipStream_t s);            // ghosts iteration k of the single-reduction form reads
   void wait_bounded_(hipEvent_t ev);                       // poll wait with the optional watchdog
   void enqueue_iteration_f1_(int k);
+  int enqueue_pass_(int k, bool fused_red);  // the pass over every owned row (lean_split: two launches)
   void enqueue_iteration_split_(int k);                   // materialized-p split pass (pmat_)
   void enqueue_iteration_pipe_(int k);                    // pipelined CG (recurrence 2)
   void pick_pipe_order_();                                // pipelined CG: which fork branch goes first
@@ -159,6 +161,8 @@ class GpuCgSolver {
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
   bool hide_ = false;           // PassForm::halo_hide in effect: interior band || copy-engine halo, then the ends
+  bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
+                                // generic kernels over the rest (same grid; the second launch finishes the reduction)
   bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)

@@ -222,6 +222,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(lean_depth)
       MCG_FORM_PROP(lean_bpc)
       MCG_FORM_PROP(lean_depth_odd)
+      MCG_FORM_PROP(lean_split)
       MCG_FORM_PROP(lean_bpc_odd)
       MCG_FORM_PROP(halo_hide)
       MCG_FORM_PROP(tile_pace_lag)
@@ -505,6 +506,7 @@ PYBIND11_MODULE(_C, m) {
         d["grid_a"] = i.grid_a;
         d["grid_odd"] = i.grid_odd;
         d["lean_mix"] = i.lean_mix;
+        d["lean_split"] = i.lean_split;
         d["grid_b"] = i.grid_b;
         d["max_row_len"] = i.max_row_len;
         d["spmv_variant"] = i.spmv_variant;
