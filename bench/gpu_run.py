@@ -316,8 +316,12 @@ def recipes(a) -> dict:
         # r4: the lean / generic split on a user matrix with a few changed rows
         "lsplit": [
             ("pytest", 300, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean'"),
+        ],
+        "lsplit_ab": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean'"),
             ("ab4096", 200, f"{PY} -u bench/lean_split_ab.py --n 4096 --steps 2000 --warmup 100"),
             ("ab8192", 300, f"{PY} -u bench/lean_split_ab.py --n 8192 --steps 800 --warmup 50"),
+            ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 2"),
         ],
         "mix2": [
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))

@@ -7,7 +7,8 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
 
   uniform   the unperturbed Laplacian (every run lean; the ceiling)
   generic   the perturbed matrix, lean_split = 0 (the pre-split dispatch)
-  split     the perturbed matrix, lean_split auto
+  seq       the perturbed matrix, lean_split = 1, the generic launch after the lean one
+  side      the perturbed matrix, lean_split = 1, the generic launch on a side stream beside it
 
 Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
     python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400]
@@ -36,19 +37,29 @@ def main() -> int:
     ap.add_argument("--spots", type=int, default=3)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--reps", type=int, default=1)
     a = ap.parse_args()
     import numpy as np
 
     import cuda_mpi_parallel_amd as mcg
 
+    t0 = time.perf_counter()
     A = _laplacian(a.n)
+    print(json.dumps({"built": a.n, "nnz": int(A.nnz), "s": round(time.perf_counter() - t0, 1)}), flush=True)
     rng = np.random.default_rng(7)
     spots = rng.integers(0, a.n * a.n, a.spots)
-    B = A.copy()
-    B.setdiag(B.diagonal() + 0.5 * np.isin(np.arange(a.n * a.n), spots))
     out = {"n": a.n, "spots": a.spots, "steps": a.steps, "its": {}, "info": {}}
-    for name, M, kw in (("uniform", A, {}), ("generic", B, {"lean_split": 0}), ("split", B, {})):
-        p = mcg.csr_problem(M, rhs="random")
+    arms = [("uniform", {})] + [(f"generic_{i}", {"lean_split": 0}) for i in range(a.reps)]
+    arms += [(f"seq_{i}", {"lean_split": 1, "lean_split_side": 0}) for i in range(a.reps)]
+    arms += [(f"side_{i}", {"lean_split": 1}) for i in range(a.reps)]
+    for name, kw in arms:
+        if name != "uniform" and spots is not None:
+            # one matrix in memory (16384^2: 1.3 G nnz): the changed diagonal entries, in place
+            for r in spots:
+                lo, hi = A.indptr[r], A.indptr[r + 1]
+                A.data[lo + int(np.nonzero(A.indices[lo:hi] == r)[0][0])] += 0.5
+            spots = None
+        p = mcg.csr_problem(A, rhs="random")
         s = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=-1.0, maxit=a.steps + a.warmup, **kw)
         s.reset()
         s.run(a.warmup)

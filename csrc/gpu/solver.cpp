@@ -68,6 +68,9 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
     s0_ = Stream(true, 0);
   }
   s1_ = Stream(true, -1);  // comm stream at higher priority: halo kernels start first
+  s2_ = Stream(true, -1);  // lean_split: the generic runs' launch beside the lean one
+  ev_ls_[0] = Event(true);
+  ev_ls_[1] = Event(true);
   ev_r_ = Event(true);
   ev_h_ = Event(true);
   ev_t0_ = Event(true, true);
@@ -83,6 +86,7 @@ GpuCgSolver::~GpuCgSolver() {
   drop_graphs_();
   if (s0_.get()) (void)hipStreamSynchronize(s0_);
   if (s1_.get()) (void)hipStreamSynchronize(s1_);
+  if (s2_.get()) (void)hipStreamSynchronize(s2_);
 }
 
 void GpuCgSolver::reset() {
@@ -225,6 +229,8 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
               "Ap-recomputing carry: one launch per iteration (halo_hide: two bands; lean_split: lean + generic runs)");
     // the launch runs the lean-only kernels: every run qualifies, or (lean_split) the lean half
     const bool lean_launch = lean_only_ || (lean_split_ && which == 1);
+    // (lean_split: the generic launch runs on s2_, beside the lean one -- enqueue_pass_)
+    const hipStream_t ls = (lean_split_ && which == 2 && split_side_) ? (hipStream_t)s2_ : (hipStream_t)s0_;
     v.ra_old = nullptr;
     v.ra_new = nullptr;
     v.ap_old = apx_[(k + 1) & 1].get();
@@ -252,13 +258,13 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
       TileRanges ta = tr;
       ta.alt_chunk = (k & 1) != 0 ? alt_chunk_even_ : alt_chunk_odd_;
       kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, ld > 0 ? ld : 3, S, v, L_.own_off, ta,
-                        part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc, p3_, 3,
+                        part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, ls, rc, p3_, 3,
                         lean_launch);
       return;
     }
     const int depth = ((k & 1) == 0 && p3_ && !lean_launch) ? 2 : (lean_launch && ld > 0 ? ld : 3);
     kern::cg_carry_ar(dia4_.get() ? 4 : (cv_.get() ? 5 : 2), info_.spmv_param, depth, S, v,
-                      L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, s0_, rc,
+                      L_.own_off, tr, part, pstride_, grid, st_.get(), opt_.tol, first, check, k, final_mode, ls, rc,
                       p3_, 3, lean_launch);
     return;
   }
@@ -393,8 +399,21 @@ int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
     enqueue_f1_(k, 0, 0, fused_red);
     return (g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_;
   }
-  enqueue_f1_(k, 1, 0, fused_red);
+  if (!split_side_) {
+    enqueue_f1_(k, 1, 0, fused_red);
+    enqueue_f1_(k, 2, 0, fused_red);
+    return g_int_ + g_bnd_;
+  }
+  // the generic launch (few busy blocks: the runs that do not qualify) on the high-priority side
+  // stream s2_ first, then the lean one on s0_: the generic runs overlap the lean pass instead of
+  // following it.  The runs of one pass are independent (each reads the previous pass's vectors),
+  // and the last arriver of either launch finishes the fused reduction.
+  MCG_HIP(hipEventRecord(ev_ls_[0], s0_), "event record failed");
+  MCG_HIP(hipStreamWaitEvent(s2_, ev_ls_[0], 0), "stream wait failed");
   enqueue_f1_(k, 2, 0, fused_red);
+  MCG_HIP(hipEventRecord(ev_ls_[1], s2_), "event record failed");
+  enqueue_f1_(k, 1, 0, fused_red);
+  MCG_HIP(hipStreamWaitEvent(s0_, ev_ls_[1], 0), "stream wait failed");
   return g_int_ + g_bnd_;
 }
 

@@ -799,8 +799,13 @@ void GpuCgSolver::setup() {
       kern::carry_jobs_host((int64_t)g * 4, tr_all_.strip, nlines, runs, chunk);
       const int64_t jobs = runs * tr_all_.strip;
       const int64_t fails = kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, 0, 0, s0_, 0, 0, 0);
-      if (jobs > 0 && (opt_.form.lean_split == 1 ? fails < jobs : 2 * fails < jobs)) {
+      // auto: runs of >= 128 lines (each wave takes one run) -- 16384^2 (256-line runs) 548-557 it/s vs 514
+      // all-generic with 3 changed rows; the 64-line runs of 4096^2 / 8192^2 lose (the few generic runs
+      // sit on the critical path: 4855 vs 6816, 1819 vs 1938; profiles/r4/lsplit)
+      const bool want = opt_.form.lean_split == 1 || (2 * fails < jobs && chunk >= 128);
+      if (jobs > 0 && fails < jobs && want) {
         lean_split_ = true;
+        split_side_ = opt_.form.lean_split_side != 0;
         g_all_ = g;
         tr_int_ = tr_all_;
         tr_int_.lean_split = 1;

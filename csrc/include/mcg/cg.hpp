@@ -101,6 +101,7 @@ struct PassForm {
                              // with a few odd rows): the lean kernels over the runs that qualify, the generic ones
                              // over the rest, in two launches; -1 = auto (when most runs qualify), 0 = off (every run
                              // on the generic kernels)
+  int lean_split_side = 1;   // ... the generic launch on a side stream, concurrent with the lean one (0 = after it)
   int lean_depth_odd = 0;    // ... the odd passes (x update paired in: one more stream) their own depth / grid; 0 = as
   int lean_bpc_odd = 0;      // the even passes (the two grids each reduce their own block partials)
   int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging

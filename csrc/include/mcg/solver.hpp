@@ -161,6 +161,7 @@ class GpuCgSolver {
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
   bool hide_ = false;           // PassForm::halo_hide in effect: interior band || copy-engine halo, then the ends
+  bool split_side_ = true;     // lean_split: the generic launch on s2_, concurrent with the lean one
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
   bool ar_ = false;             // CgOptions::ap_recompute in effect
@@ -172,9 +173,9 @@ class GpuCgSolver {
   int ghosts_for_ = -1;         // halo_ahead: iteration whose ghosts are in place or in flight on s1_
   bool halo_pending_ = false;   // ... in flight: s0_ must wait for ev_h_ before reading them
 
-  Stream s0_, s1_;
+  Stream s0_, s1_, s2_;
   int ncu_ = 0;  // CUs of the device
-  Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2], ev_sync_[2];
+  Event ev_r_, ev_h_, ev_t0_, ev_t1_, ev_poll_[2], ev_sync_[2], ev_ls_[2];
   // matrix
   DeviceBuffer<int32_t> rp32_;
   DeviceBuffer<int64_t> rp64_;

@@ -223,6 +223,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(lean_bpc)
       MCG_FORM_PROP(lean_depth_odd)
       MCG_FORM_PROP(lean_split)
+      MCG_FORM_PROP(lean_split_side)
       MCG_FORM_PROP(lean_bpc_odd)
       MCG_FORM_PROP(halo_hide)
       MCG_FORM_PROP(tile_pace_lag)

@@ -211,8 +211,8 @@ def test_lean_runs_on_user_stencils(mcg, kind):
     keeps every slice uniform (one pattern, lean-only kernels); one changed row leaves one slice
     non-uniform, and a shift on every 7th grid line changes the pattern down every slice column --
     in both the setup check finds runs that do not qualify.  With lean_split = 0 the generic kernels
-    run every run and the solve is bit for bit the one with dia_uniform = 0; by default (lean_split
-    auto) the spot case splits the pass -- the lean kernels over the runs that qualify, the generic
+    run every run and the solve is bit for bit the one with dia_uniform = 0; with lean_split = 1
+    the spot case splits the pass -- the lean kernels over the runs that qualify, the generic
     ones over the rest -- and matches it to rounding (the block partials are summed in another
     order)."""
     n = 1024
@@ -228,7 +228,7 @@ def test_lean_runs_on_user_stencils(mcg, kind):
     p = mcg.csr_problem(A.tocsr(), rhs="random")
     a = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, lean_split=0)
     b = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, dia_uniform=0)
-    c = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8)
+    c = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, lean_split=1)
     assert a.info["dia4"] and a.info["p3"] and b.info["p3"] and c.info["p3"]
     assert a.info["lean_split"] == 0.0 and b.info["lean_split"] == 0.0
     if kind == "shift":
@@ -236,8 +236,11 @@ def test_lean_runs_on_user_stencils(mcg, kind):
         assert c.info["lean_only"] and c.info["lean_split"] == 0.0
     elif kind == "spot":
         assert a.info["dia_uniform"] < 1.0 and not a.info["lean_only"]
-        # one slice of one run does not qualify: every other run goes to the lean launch
+        # one slice of one run does not qualify: every other run goes to the lean launch (forced: auto
+        # splits only passes of >= 128-line runs, 1024^2 has shorter ones)
         assert not c.info["lean_only"] and c.info["lean_split"] > 0.99
+        auto = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8)
+        assert auto.info["lean_split"] == 0.0 and not auto.info["lean_only"]
     else:
         assert a.info["dia_uniform"] == 1.0 and not a.info["lean_only"]
     outs = []
@@ -261,22 +264,28 @@ def test_lean_runs_on_user_stencils(mcg, kind):
 def test_lean_split_converges_like_the_generic_pass(mcg):
     """lean_split to convergence on a user matrix with a few changed rows (spread over several
     runs): the same iteration count as the generic pass and the CPU oracle's solution."""
-    n = 512
+    n = 1024
     A = _poisson(n, 2).tolil()
     d = A.diagonal()
-    for r in (n * 17 + 3, n * 200 + 300, n * 401 + 77):
+    for r in (n * 17 + 3, n * 400 + 300, n * 801 + 77):
         d[r] += 0.75
     A.setdiag(d)
     p = mcg.csr_problem(A.tocsr(), rhs="random")
-    g = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=0, tol=1e-9, maxit=4000)
-    s = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=1, tol=1e-9, maxit=4000)
-    assert s.info["lean_split"] > 0.9 and not s.info["lean_only"]
-    og, os_ = g.solve(), s.solve()
-    assert og["converged"] and os_["converged"]
-    assert abs(og["iterations"] - os_["iterations"]) <= 1
-    np.testing.assert_allclose(os_["x_local"], og["x_local"], rtol=1e-7, atol=1e-10)
-    tg, ts = g.true_residual_norm(), s.true_residual_norm()
-    assert ts <= 2.0 * tg + 1e-12 and abs(ts - os_["rnorm"]) <= 1e-6 * ts + 1e-14
+    g = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=0, tol=1e-8, maxit=20000)
+    og = g.solve()
+    assert og["converged"]
+    tg = g.true_residual_norm()
+    for side in (1, 0):  # the generic launch beside the lean one (default) / after it
+        s = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=1, lean_split_side=side, tol=1e-8,
+                         maxit=20000)
+        assert s.info["lean_split"] > 0.9 and not s.info["lean_only"]
+        os_ = s.solve()
+        assert os_["converged"]
+        assert abs(og["iterations"] - os_["iterations"]) <= 1
+        np.testing.assert_allclose(os_["x_local"], og["x_local"], rtol=1e-7, atol=1e-10)
+        # the recurrence drifts from ||b - A x|| the same way in both (single-reduction, ~3000 iterations)
+        ts = s.true_residual_norm()
+        assert abs(ts - tg) <= 0.05 * tg
 
 
 def _nine_point(n=96, seed=3):
