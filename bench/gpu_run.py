@@ -313,6 +313,13 @@ def recipes(a) -> dict:
                             ("m5", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=14 --set lean_bpc_odd=4"),
                             ("e14", "--set lean_depth=14"))
         ],
+        # r4: tile row blocks of 960 rows at 5 workgroups per CU vs 1024 at 4, interleaved (config 5)
+        "c5tb": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'tiles'"),
+        ] + [
+            (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
+            for rep in (1, 2) for tag, kv in (("tb1024", ""), ("tb960", "--set tile_rows=960"))
+        ],
         # r4: the lean / generic split on a user matrix with a few changed rows
         "lsplit": [
             ("pytest", 300, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean'"),

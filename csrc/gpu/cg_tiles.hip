@@ -6,7 +6,7 @@
 // reference's cuSPARSE CSR SpMV, CUDACG.cu:288, has the same access pattern).  Gathers that hit
 // the L2 run 4-5x faster (bench/gather_probe.hip, profiles/r3_gather_probe.md).  So the columns
 // are cut into segments of S = 2^seg_shift doubles (default 2^19 = 4 MiB, one XCD's L2; CgOptions
-// tile_seg_log2), every wave owns kTileB = 1024 rows
+// tile_seg_log2), every wave owns kTileB = 1024 rows (tile_rows = 960: 5 workgroups per CU)
 // (their running sums live in LDS), and ALL waves sweep the segments in the same order: while the
 // chip works on segment g, the XCDs' L2s hold p[g S, (g + 1) S) and the gathers hit.
 //
@@ -49,7 +49,7 @@ constexpr int kTU = 8;                // entries per lane in flight (software-pi
 constexpr int kPaceSpins = 4000;      // ~1 ms of polling at most per segment step
 constexpr uint32_t kColMask = (1u << 22) - 1;
 
-// `live` (LDS, per workgroup): cleared after the first wait that times out -- the group is not
+// `live` (thread 0's, per workgroup): cleared after the first wait that times out -- the group is not
 // co-resident (another kernel holds CUs, or several ranks share the GPU), so this workgroup stops
 // waiting for the rest of the launch instead of paying the cap at every segment.
 //
@@ -126,12 +126,15 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // this rank's own block of p (they are final before the all-gather of p_k lands), the partial row
 // sums stored in Ap, no partials; 2 = the other segments, added to those sums, then the epilogue
 // (as k_split_spmv_aligned_part's halves)
-template <int MODE, bool V32, int PART = 0>
-__global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
+// TB: rows per block (kTileB: 32 KiB of row sums, 4 workgroups per CU; kTileB5: 30 KiB, built for 5,
+// which also caps the kernel at 96 VGPRs)
+template <int MODE, bool V32, int PART = 0, int TB = kTileB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == kTileB5 ? 5 : 1)))
+void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
-  __shared__ double acc[4][kTileB];
-  __shared__ int live;
+  __shared__ double acc[4][TB];
+  int live = 0;  // thread 0's (the only one that paces)
   if constexpr (MODE == 0) {
     const F1Scalars sc = f1_scalars(st, tol, first, check);
     if (st->done || sc.conv) {  // uniform over the grid: every workgroup leaves, no pacing
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
   for (int64_t rd = 0; rd < rounds; ++rd) {
     const int64_t b = wave + rd * nwaves;
     const bool active = b < T.nblocks;
-    for (int rr = lane; rr < kTileB; rr += 64) a[rr] = 0.0;
+    for (int rr = lane; rr < TB; rr += 64) a[rr] = 0.0;
     // tile g of block b = [tptr[b G + g], tptr[b G + g + 1])
     int64_t lo = 0, hi = 0;
     uint32_t q[kTU];
@@ -208,8 +211,8 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
       hi = hi_next;
     }
     if (active) {
-      const int64_t r0 = b * kTileB;
-      for (int rr = lane; rr < kTileB; rr += 64) {
+      const int64_t r0 = b * TB;
+      for (int rr = lane; rr < TB; rr += 64) {
         const int64_t i = r0 + rr;
         if (i >= T.n_rows) break;
         if constexpr (MODE == 0 && PART == 1) {
@@ -260,7 +263,7 @@ struct CsrSrc {  // a user matrix's rows on the device (local CSR, ext columns)
 // lane + 64, ... of the block in lockstep; the order of one LDS atomic's same-address lanes
 // (observed fixed, as above) orders a batch's appends.
 template <bool FILL, class V, class Src>
-__global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, int seg_shift, int64_t* __restrict__ tptr,
+__global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int tb, int G, int seg_shift, int64_t* __restrict__ tptr,
                                                     uint32_t* __restrict__ idx, V* __restrict__ vals,
                                                     unsigned long long* __restrict__ inexact) {
   extern __shared__ int cnt[];
@@ -270,8 +273,8 @@ __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, i
   __syncthreads();
   const uint32_t mask = (1u << seg_shift) - 1u;
   unsigned bad = 0;
-  for (int rr = lane; rr < kTileB; rr += 64) {
-    const int64_t i = b * kTileB + rr;
+  for (int rr = lane; rr < tb; rr += 64) {
+    const int64_t i = b * tb + rr;
     if (i >= n) break;
     src.row(i, [&](int64_t ec, double v) {
       const int g = (int)(ec >> seg_shift);
@@ -294,22 +297,23 @@ __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int G, i
 
 }  // namespace
 
-TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
+TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift, int tb) {
+  MCG_CHECK(tb == kTileB || tb == kTileB5, "tiles: rows per block are 1024 or 960");
   TilesGeometry t;
+  t.tb = tb;
   t.seg_shift = seg_shift;
-  t.nblocks = (n_rows + kTileB - 1) / kTileB;
+  t.nblocks = (n_rows + tb - 1) / tb;
   t.G = (int)std::max<int64_t>(1, (ext_len + ((int64_t)1 << seg_shift) - 1) >> seg_shift);
   return t;
 }
 
-int tiles_grid(int ncu) {
+int tiles_grid(int ncu, int tb) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_tiles<0, false>), 256, 0) !=
-          hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
+  const void* f = tb == kTileB5 ? reinterpret_cast<const void*>(&k_tiles<0, false, 0, kTileB5>)
+                                : reinterpret_cast<const void*>(&k_tiles<0, false>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   (void)hipGetLastError();
-  return std::min(per_cu, 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
+  return std::min(per_cu, tb == kTileB5 ? 5 : 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
 }
 
 namespace {
@@ -322,13 +326,13 @@ void tiles_build_impl(const Src& src, int64_t n, const TilesGeometry& geo, const
   const size_t lds = (size_t)geo.G * sizeof(int);
   const dim3 grid((unsigned)geo.nblocks);
   if (!fill)
-    hipLaunchKernelGGL((k_tiles_build<false, double, Src>), grid, dim3(64), lds, st, src, n, geo.G, geo.seg_shift,
+    hipLaunchKernelGGL((k_tiles_build<false, double, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
                        o.tptr, o.idx, nullptr, o.inexact);
   else if (o.vals32 != nullptr)
-    hipLaunchKernelGGL((k_tiles_build<true, float, Src>), grid, dim3(64), lds, st, src, n, geo.G, geo.seg_shift,
+    hipLaunchKernelGGL((k_tiles_build<true, float, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
                        o.tptr, o.idx, o.vals32, nullptr);
   else
-    hipLaunchKernelGGL((k_tiles_build<true, double, Src>), grid, dim3(64), lds, st, src, n, geo.G, geo.seg_shift,
+    hipLaunchKernelGGL((k_tiles_build<true, double, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
                        o.tptr, o.idx, o.vals, nullptr);
   MCG_HIP(hipGetLastError(), "kernel launch failed(tiles_build)");
 }
@@ -351,10 +355,17 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
   MCG_CHECK(part == 0 || (T.g_lo >= 0 && T.g_lo <= T.g_hi && T.g_hi <= T.G), "tiles: bad own-segment range");
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
+  MCG_CHECK(T.tb == kTileB || T.tb == kTileB5, "tiles: rows per block are 1024 or 960");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-#define MCG_TL(V32, PART)                                                                                             \
-  hipLaunchKernelGGL((k_tiles<0, V32, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
-                     pstride, st, tol, first, check, rc)
+#define MCG_TL(V32, PART)                                                                                         \
+  do {                                                                                                            \
+    if (T.tb == kTileB5)                                                                                          \
+      hipLaunchKernelGGL((k_tiles<0, V32, PART, kTileB5>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap,     \
+                         own_off, partials, pstride, st, tol, first, check, rc);                                  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((k_tiles<0, V32, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off,     \
+                         partials, pstride, st, tol, first, check, rc);                                           \
+  } while (0)
   const bool v32 = T.vals32 != nullptr;
   if (part == 1) { if (v32) MCG_TL(true, 1); else MCG_TL(false, 1); }
   else if (part == 2) { if (v32) MCG_TL(true, 2); else MCG_TL(false, 2); }
@@ -365,13 +376,14 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
 
 void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream) {
   if (grid <= 0 || T.nblocks == 0) return;
+  MCG_CHECK(T.tb == kTileB || T.tb == kTileB5, "tiles: rows per block are 1024 or 960");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-  if (T.vals32 != nullptr)
-    hipLaunchKernelGGL((k_tiles<1, true>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr,
-                       0.0, 0, 0, RedCtl());
-  else
-    hipLaunchKernelGGL((k_tiles<1, false>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr,
-                       0.0, 0, 0, RedCtl());
+#define MCG_TY(V32, TB)                                                                                          \
+  hipLaunchKernelGGL((k_tiles<1, V32, 0, TB>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, \
+                     nullptr, 0.0, 0, 0, RedCtl())
+  if (T.tb == kTileB5) { if (T.vals32 != nullptr) MCG_TY(true, kTileB5); else MCG_TY(false, kTileB5); }
+  else { if (T.vals32 != nullptr) MCG_TY(true, kTileB); else MCG_TY(false, kTileB); }
+#undef MCG_TY
   MCG_HIP(hipGetLastError(), "compute mv failed(y)");
 }
 

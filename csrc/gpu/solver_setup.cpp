@@ -259,7 +259,8 @@ void GpuCgSolver::setup() {
 
   size_t matrix_bytes = 0;
   if (tiles_) {
-    tgeo_ = kern::tiles_geometry(n, L_.ext_len, std::max(10, std::min(22, opt_.form.tile_seg_log2)));
+    tgeo_ = kern::tiles_geometry(n, L_.ext_len, std::max(10, std::min(22, opt_.form.tile_seg_log2)),
+                                 opt_.form.tile_rows == kern::kTileB5 ? kern::kTileB5 : kern::kTileB);
     MCG_CHECK(tgeo_.G <= kern::kTileMaxSegments, "tiles: too many column segments (raise tile_seg_log2)");
     tptr_.allocate(tgeo_.nblocks * tgeo_.G + 1, "A");
     MCG_HIP(hipMemsetAsync(tptr_.get(), 0, tptr_.bytes(), s0_), "device memset failed(A)");
@@ -554,7 +555,7 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (tiles_) {  // one launch over every row block: the resident workgroups (the pacing waits on each)
-    g_all_ = n > 0 ? kern::tiles_grid(ncu_) : 0;
+    g_all_ = n > 0 ? kern::tiles_grid(ncu_, tgeo_.tb) : 0;
     if (opt_.blocks_per_cu > 0) g_all_ = std::min(g_all_, ncu_ * opt_.blocks_per_cu);  // fewer waves: more rounds
     g_int_ = 0;
     g_bnd_ = g_all_;

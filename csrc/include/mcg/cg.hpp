@@ -57,6 +57,8 @@ struct PassForm {
   int tile_seg_log2 = 18;    // tiles: column segment = 2^k doubles (18: 2 MiB of p, half an XCD's L2; at a P = 8
                              // rank's share of the scrambled config 5 with step-flag pacing: 17 / 18 / 19 -> 18.5 /
                              // 19.3-19.5 / 17.5 it/s, profiles/r4/c5; r3's counter pacing peaked at 19: 14.0)
+  int tile_rows = 1024;      // tiles: rows per block, 1024 (4 workgroups per CU) or 960 (5 per CU, the kernel held
+                             // to 96 VGPRs)
   int tile_pace = 4;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
                              // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest);
                              // 3 / 4 = as 1 / 2, the waiters polling a step flag (8 replicas) instead of the arrival

@@ -385,10 +385,12 @@ void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, 
 // block at a time (sums in LDS) and all waves sweep the segments together (paced per segment), so
 // the gathers of p hit the L2.
 constexpr int kTileB = 1024;
+constexpr int kTileB5 = 960;  // tile_rows = 960: 30 KiB of row sums per workgroup, 5 workgroups per CU
 constexpr int kTileMaxSegments = 8192;  // LDS counters of the build kernels (32 KiB)
 constexpr int kTilePaceCnt = 8 * 64;     // pacing arrival counters: 8 groups, 256 B apart
 constexpr int kTilePaceWords = kTilePaceCnt + 8 * 8 * 64;  // + per group 8 replicas of its step flag, 256 B apart
 struct TilesGeometry {
+  int tb = kTileB;  // rows per block (kTileB or kTileB5)
   int64_t nblocks = 0;
   int G = 0;
   int seg_shift = 18;
@@ -401,6 +403,7 @@ struct TilesDev {
                                    // checked at build time; products and sums stay fp64): 8 instead of 12 B/entry
   int64_t n_rows = 0, nblocks = 0;
   int G = 0, seg_shift = 18;
+  int tb = kTileB;           // rows per block: kTileB (4 workgroups per CU) or kTileB5 (5)
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
   int pace_slack8 = 0;       // a workgroup waits for all but pace_slack8 / 8 of its group (0: all)
   int pace_flag = 0;         // 1: the arrival that completes a step publishes it in a step flag and the waiters
@@ -411,8 +414,8 @@ struct TilesDev {
   int64_t ext_len = 0;       // length of p (the last segment may be short)
   int g_lo = 0, g_hi = 0;    // the segments inside this rank's own block of p (all-gather overlap, part 1 / 2)
 };
-TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
-int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
+TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift, int tb = kTileB);
+int tiles_grid(int ncu, int tb = kTileB);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
 // count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0; *inexact += the
 // entries whose value is not exactly an fp32) then fill (into vals, or vals32 when vals is null)
 struct TilesOut {

@@ -239,6 +239,23 @@ def test_tiles_several_rounds_of_row_blocks(mcg):
     assert abs(a.true_residual_norm() - ra["rnorm"]) <= 1e-9 * ra["rnorm"]
 
 
+@pytest.mark.parametrize("v32", [0, 1])
+def test_tiles_960_row_blocks_match_1024(mcg, v32):
+    """tile_rows = 960 (5 workgroups per CU): every row's products are summed in the same order as
+    with 1024-row blocks (a row's entries of a segment stay in one lane's append order), so the true
+    SpMV is bit for bit the same; the dot products' block partials group differently."""
+    spec = mcg.make_problem("randspd", rows=1200000, band=4, density=0.5, scramble=1)
+    kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=12, tile_seg_log2=16, tile_vals32=v32)
+    a = mcg.CGSolver(spec, tile_rows=960, **kw)
+    b = mcg.CGSolver(spec, **kw)
+    assert a.info["tiles"] and b.info["tiles"]
+    assert a.info["grid_a"] * 4 == b.info["grid_a"] * 5
+    ra, rb = a.solve(), b.solve()
+    assert abs(ra["rnorm"] - rb["rnorm"]) <= 1e-13 * rb["rnorm"]
+    np.testing.assert_allclose(ra["x_local"], rb["x_local"], rtol=1e-13, atol=1e-15 * np.abs(rb["x_local"]).max())
+    assert abs(a.true_residual_norm() - ra["rnorm"]) <= 1e-9 * ra["rnorm"]
+
+
 def test_tiles_user_matrix_scattered(mcg):
     """A user CSR with scattered columns (random sparsity, strictly diagonally dominant) on the tiles
     SpMV (forced at P = 1; auto on the all-gather layout) matches the CPU reference solve."""
