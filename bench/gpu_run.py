@@ -320,6 +320,12 @@ def recipes(a) -> dict:
             (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
             for rep in (1, 2) for tag, kv in (("tb1024", ""), ("tb960", "--set tile_rows=960"))
         ],
+        "c5tu": [
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'tiles_same_recurrence or tiles_960'"),
+        ] + [
+            (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
+            for rep in (1, 2) for tag, kv in (("tu8", ""), ("tu12", "--set tile_unroll=12"))
+        ],
         # r4: the lean / generic split on a user matrix with a few changed rows
         "lsplit": [
             ("pytest", 300, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean'"),

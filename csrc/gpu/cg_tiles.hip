@@ -109,10 +109,10 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
 
 // one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once).  V32: the values
 // are stored as fp32 (exact, checked at build time) and widened here; everything after is fp64
-template <bool V32>
+template <bool V32, int TU = kTU>
 __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
 #pragma unroll
-  for (int u = 0; u < kTU; ++u) {
+  for (int u = 0; u < TU; ++u) {
     const int64_t e = k + u * 64;
     q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
     if constexpr (V32) v[u] = e < hi ? (double)__builtin_nontemporal_load(&T.vals32[e]) : 0.0;
@@ -128,8 +128,9 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // (as k_split_spmv_aligned_part's halves)
 // TB: rows per block (kTileB: 32 KiB of row sums, 4 workgroups per CU; kTileB5: 30 KiB, built for 5,
 // which also caps the kernel at 96 VGPRs)
-template <int MODE, bool V32, int PART = 0, int TB = kTileB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == kTileB5 ? 5 : 1)))
+// TU: entries per lane in flight (kTU; 12 = tile_unroll 12, at 4 workgroups per CU)
+template <int MODE, bool V32, int PART = 0, int TB = kTileB, int TU = kTU>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == kTileB5 ? 5 : (TU > kTU ? 4 : 1))))
 void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
@@ -162,30 +163,30 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
     for (int rr = lane; rr < TB; rr += 64) a[rr] = 0.0;
     // tile g of block b = [tptr[b G + g], tptr[b G + g + 1])
     int64_t lo = 0, hi = 0;
-    uint32_t q[kTU];
-    double v[kTU];
+    uint32_t q[TU];
+    double v[TU];
     if (active && ns > 0) {
       const int g0 = seg(0);
       lo = T.tptr[b * G + g0];
       hi = T.tptr[b * G + g0 + 1];
-      tile_batch_load<V32>(T, lo + lane, hi, q, v);
+      tile_batch_load<V32, TU>(T, lo + lane, hi, q, v);
     }
     for (int i = 0; i < ns; ++i, ++step) {
       const int g = seg(i);
       int64_t lo_next = hi, hi_next = hi;
       if (active) {
         const double* __restrict__ pg = p + ((int64_t)g << T.seg_shift);
-        for (int64_t k = lo + lane; k < hi; k += kTU * 64) {
-          uint32_t qn[kTU];
-          double vn[kTU], x[kTU];
-          tile_batch_load<V32>(T, k + kTU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
+        for (int64_t k = lo + lane; k < hi; k += TU * 64) {
+          uint32_t qn[TU];
+          double vn[TU], x[TU];
+          tile_batch_load<V32, TU>(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
 #pragma unroll
-          for (int u = 0; u < kTU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
+          for (int u = 0; u < TU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
 #pragma unroll
-          for (int u = 0; u < kTU; ++u)
+          for (int u = 0; u < TU; ++u)
             if (k + u * 64 < hi) atomicAdd(&a[q[u] >> 22], v[u] * x[u]);
 #pragma unroll
-          for (int u = 0; u < kTU; ++u) {
+          for (int u = 0; u < TU; ++u) {
             q[u] = qn[u];
             v[u] = vn[u];
           }
@@ -195,7 +196,7 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
           const int gn = seg(i + 1);
           lo_next = T.tptr[b * G + gn];
           hi_next = T.tptr[b * G + gn + 1];
-          tile_batch_load<V32>(T, lo_next + lane, hi_next, q, v);
+          tile_batch_load<V32, TU>(T, lo_next + lane, hi_next, q, v);
         }
       }
       const double* nxt = nullptr;  // the segment the group starts next (prefetched while it waits)
@@ -361,6 +362,9 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   do {                                                                                                            \
     if (T.tb == kTileB5)                                                                                          \
       hipLaunchKernelGGL((k_tiles<0, V32, PART, kTileB5>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap,     \
+                         own_off, partials, pstride, st, tol, first, check, rc);                                  \
+    else if (T.tu == 12)                                                                                          \
+      hipLaunchKernelGGL((k_tiles<0, V32, PART, kTileB, 12>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap,  \
                          own_off, partials, pstride, st, tol, first, check, rc);                                  \
     else                                                                                                          \
       hipLaunchKernelGGL((k_tiles<0, V32, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off,     \

@@ -59,6 +59,8 @@ struct PassForm {
                              // 19.3-19.5 / 17.5 it/s, profiles/r4/c5; r3's counter pacing peaked at 19: 14.0)
   int tile_rows = 1024;      // tiles: rows per block, 1024 (4 workgroups per CU) or 960 (5 per CU, the kernel held
                              // to 96 VGPRs: spills, 18.1-18.2 vs 19.4 it/s on config 5, profiles/r4/c5tb)
+  int tile_unroll = 8;       // tiles: entries per lane in flight, 8 or 12 (1024-row blocks; 12 spills at 4 waves per
+                             // SIMD: 18.9 vs 19.4 it/s on config 5, profiles/r4/c5tb)
   int tile_pace = 4;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
                              // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest);
                              // 3 / 4 = as 1 / 2, the waiters polling a step flag (8 replicas) instead of the arrival

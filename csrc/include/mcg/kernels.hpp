@@ -404,6 +404,7 @@ struct TilesDev {
   int64_t n_rows = 0, nblocks = 0;
   int G = 0, seg_shift = 18;
   int tb = kTileB;           // rows per block: kTileB (4 workgroups per CU) or kTileB5 (5)
+  int tu = 8;                // entries per lane in flight: 8 or 12 (kTileB only)
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
   int pace_slack8 = 0;       // a workgroup waits for all but pace_slack8 / 8 of its group (0: all)
   int pace_flag = 0;         // 1: the arrival that completes a step publishes it in a step flag and the waiters

@@ -221,6 +221,7 @@ class GpuCgSolver {
     t.G = tgeo_.G;
     t.seg_shift = tgeo_.seg_shift;
     t.tb = tgeo_.tb;
+    t.tu = opt_.form.tile_unroll == 12 ? 12 : 8;
     t.pace = opt_.form.tile_pace > 0 ? tpace_.get() : nullptr;
     t.pace_slack8 = (opt_.form.tile_pace == 2 || opt_.form.tile_pace == 4) ? std::max(0, std::min(7, opt_.form.tile_pace_slack)) : 0;
     t.pace_flag = opt_.form.tile_pace >= 3 ? 1 : 0;

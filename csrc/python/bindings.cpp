@@ -218,6 +218,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(tiles)
       MCG_FORM_PROP(tile_seg_log2)
       MCG_FORM_PROP(tile_rows)
+      MCG_FORM_PROP(tile_unroll)
       MCG_FORM_PROP(tile_pace)
       MCG_FORM_PROP(carry_vc)
       MCG_FORM_PROP(lean_depth)
