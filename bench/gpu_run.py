@@ -336,6 +336,15 @@ def recipes(a) -> dict:
             ("ab8192", 300, f"{PY} -u bench/lean_split_ab.py --n 8192 --steps 800 --warmup 50"),
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 2"),
         ],
+        # kernel trace of the split pass at 16384^2 (lean + generic launches per pass) and of the generic one
+        "lsplit_prof": [
+            ("side", 600, prof("lsplit_side", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "
+                                              "--arms side")),
+            ("side_md", 60, f"{PY} bench/prof_summary.py --stats {OUT}/lsplit_side --title 'lean_split side, 16384^2'"),
+            ("generic", 600, prof("lsplit_gen", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "
+                                                "--arms generic")),
+            ("generic_md", 60, f"{PY} bench/prof_summary.py --stats {OUT}/lsplit_gen --title 'lean_split=0, 16384^2'"),
+        ],
         "mix2": [
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
             for rep in (1, 2)

@@ -38,6 +38,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--arms", default="uniform,generic,seq,side", help="comma list of arms to run")
     a = ap.parse_args()
     import numpy as np
 
@@ -52,6 +53,8 @@ def main() -> int:
     arms = [("uniform", {})] + [(f"generic_{i}", {"lean_split": 0}) for i in range(a.reps)]
     arms += [(f"seq_{i}", {"lean_split": 1, "lean_split_side": 0}) for i in range(a.reps)]
     arms += [(f"side_{i}", {"lean_split": 1}) for i in range(a.reps)]
+    want = set(a.arms.split(","))
+    arms = [(nm, kw) for nm, kw in arms if nm.split("_")[0] in want]
     for name, kw in arms:
         if name != "uniform" and spots is not None:
             # one matrix in memory (16384^2: 1.3 G nnz): the changed diagonal entries, in place
