@@ -16,6 +16,7 @@ struct LocalRankResult {
   double true_rnorm = -1.0;
   bool ap_recompute = false;  // SolverInfo::ap_recompute of this rank
   bool lean_only = false;     // SolverInfo::lean_only of this rank
+  double lean_split = 0.0;    // SolverInfo::lean_split of this rank
   bool halo_hide = false;     // SolverInfo::halo_hide of this rank
   bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)
   bool ag_overlap = false;     // SolverInfo::ag_overlap (own-block SpMV half || all-gather)

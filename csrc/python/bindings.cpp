@@ -533,6 +533,7 @@ PYBIND11_MODULE(_C, m) {
       d["carry"] = rr.carry;
       d["ap_recompute"] = rr.ap_recompute;
       d["lean_only"] = rr.lean_only;
+      d["lean_split"] = rr.lean_split;
       d["halo_hide"] = rr.halo_hide;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;

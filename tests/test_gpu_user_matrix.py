@@ -288,6 +288,31 @@ def test_lean_split_converges_like_the_generic_pass(mcg):
         assert abs(ts - tg) <= 0.05 * tg
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_lean_split_local_ranks(mcg, world):
+    """lean_split at P = 2 / 4 (LocalComm, the ghost lines of the 2-D carry) on a user matrix with a
+    few changed rows: the same iterates as the generic pass (lean_split = 0) to rounding."""
+    n = 1024
+    A = _poisson(n, 2).tolil()
+    d = A.diagonal()
+    for r in (n * 100 + 5, n * 600 + 900):
+        d[r] += 0.5
+    A.setdiag(d)
+    p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
+    C = mcg.native()
+    outs = {}
+    for ls in (0, 1):
+        o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
+        o.lean_split = ls
+        outs[ls] = C.run_local_ranks(p.native(), o, world, 40, True)
+        # the ranks holding a changed row split their pass (ls = 1); the others stay lean-only
+        split = [rk["lean_split"] > 0 for rk in outs[ls]["ranks"]]
+        assert (any(split) if ls == 1 else not any(split)), outs[ls]["ranks"]
+    r0, r1 = outs[0]["ranks"][0]["rnorm"], outs[1]["ranks"][0]["rnorm"]
+    assert abs(r0 - r1) <= 1e-10 * r0
+    np.testing.assert_allclose(outs[1]["x"], outs[0]["x"], rtol=1e-10, atol=1e-12 * np.abs(outs[0]["x"]).max())
+
+
 def _nine_point(n=96, seed=3):
     """A variable-coefficient 9-point operator on an n x n grid (SPD: symmetric random off-diagonal
     weights, diagonal = sum |off| + 0.5): banded, every interior slice shares its 9 offsets, but no
