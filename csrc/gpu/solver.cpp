@@ -368,7 +368,7 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
     enqueue_split_spmv_(k, 1, fr);  // interior rows || ghosts of p_k on the side stream
     MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
     enqueue_split_spmv_(k, 2, fr);
-    np = g_int_ + g_bnd_;
+    np = bnd_base_ + g_bnd_;
   } else if (ag_overlap_) {
     // all-gather of p_k on the side stream || the own-block slots of every row (tiles: the segments
     // inside the own block); then the rest
@@ -379,13 +379,13 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
     enqueue_split_spmv_(k, 2, fr, 1);
     MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
     enqueue_split_spmv_(k, 2, fr, 2);
-    np = g_int_ + g_bnd_;
+    np = bnd_base_ + g_bnd_;
   } else {
     if (use_halo_) comm_->halo_exchange(L_, pv, 1, s0_);
     // all-gather layout: no interior rows (g_int_ = 0), every row in the boundary launch
     const bool split = use_halo_ && opt_.overlap;
     enqueue_split_spmv_(k, split ? 2 : 0, fr);
-    if (split) np = g_int_ + g_bnd_;
+    if (split) np = bnd_base_ + g_bnd_;
   }
   if (!fr) kern::cg_reduce_f1(partials_.get(), pstride_, np, st, 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
   if (use_comm_) comm_->allreduce_sum(st->red, 4, s0_);
@@ -402,7 +402,7 @@ int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
   if (!split_side_) {
     enqueue_f1_(k, 1, 0, fused_red);
     enqueue_f1_(k, 2, 0, fused_red);
-    return g_int_ + g_bnd_;
+    return bnd_base_ + g_bnd_;
   }
   // the generic launch (few busy blocks: the runs that do not qualify) on the high-priority side
   // stream s2_ first, then the lean one on s0_: the generic runs overlap the lean pass instead of
@@ -414,7 +414,7 @@ int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
   MCG_HIP(hipEventRecord(ev_ls_[1], s2_), "event record failed");
   enqueue_f1_(k, 1, 0, fused_red);
   MCG_HIP(hipStreamWaitEvent(s0_, ev_ls_[1], 0), "stream wait failed");
-  return g_int_ + g_bnd_;
+  return bnd_base_ + g_bnd_;
 }
 
 void GpuCgSolver::enqueue_iteration_f1_(int k) {
@@ -433,7 +433,7 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     enqueue_f1_(k, 1, 0, fr);
     ensure_ghosts_(k);
     enqueue_f1_(k, 2, 0, fr);
-    np = g_int_ + g_bnd_;
+    np = bnd_base_ + g_bnd_;
     MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
     MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
     enqueue_halo_f1_(k + 1, s1_);
@@ -461,7 +461,7 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
     enqueue_f1_(k, 1, 0, fr);  // interior rows || halo on the side stream
     MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
     enqueue_f1_(k, 2, 0, fr);  // boundary rows (its last arriver finishes the reduction)
-    np = g_int_ + g_bnd_;
+    np = bnd_base_ + g_bnd_;
     halo_ready_for_ = -1;
     if (prefetch_halo_) {
       // the next iteration's ghosts are this iteration's outputs, final now: exchange them while
@@ -582,7 +582,7 @@ void GpuCgSolver::enqueue_iteration_(int k) {
       enqueue_spmv_(k, 1, 0);
       MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
       enqueue_spmv_(k, 2, 0);
-      np = g_int_ + g_bnd_;
+      np = bnd_base_ + g_bnd_;
     } else {
       comm_->halo_exchange(L_, vecs, 2, s0_);
       enqueue_spmv_(k, 0, 0);

@@ -790,8 +790,7 @@ void GpuCgSolver::setup() {
       }
     }
     const bool lean_all = lean_ok(g) && (go == g || lean_ok(go));
-    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && g % kern::kRedGroup == 0 &&
-        opt_.form.lean_bpc_odd <= 0) {
+    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && opt_.form.lean_bpc_odd <= 0) {
       // some runs do not qualify: split the pass by run -- the lean kernels over the runs that do, the
       // generic ones over the rest, on the same grid (the same runs), when most runs qualify
       auto_mix_ = false;
@@ -933,9 +932,11 @@ void GpuCgSolver::setup() {
   auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
   // the boundary launch's partials start on a reduction-group boundary: round the interior grid up
   // (the extra blocks find no work in the grid-stride loops and contribute zero partials)
-  if (split && fused_red_ && g_int_ > 0) g_int_ = groups(g_int_) * kern::kRedGroup;
-  bnd_base_ = split ? g_int_ : 0;
-  const int np = std::max({g_all_, split ? g_int_ + g_bnd_ : 0, g_b_, g_odd_, 1});
+  // (lean_split: both launches keep the pass's grid -- the same runs -- and the boundary launch's
+  // partials start at the next group boundary instead; the slots between are never read)
+  if (split && fused_red_ && g_int_ > 0 && !lean_split_) g_int_ = groups(g_int_) * kern::kRedGroup;
+  bnd_base_ = split ? ((fused_red_ && g_int_ > 0) ? groups(g_int_) * kern::kRedGroup : g_int_) : 0;
+  const int np = std::max({g_all_, split ? bnd_base_ + g_bnd_ : 0, g_b_, g_odd_, 1});
   pstride_ = np + 64;
   partials_.allocate((size_t)pstride_ * (opt_.recurrence >= 1 ? 4 : 1), "partials");
   st_.allocate(1, "state");
