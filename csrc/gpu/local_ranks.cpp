@@ -75,6 +75,8 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         o.ap_recompute = s.info().ap_recompute;
         o.lean_only = s.info().lean_only;
         o.lean_split = s.info().lean_split;
+        o.p3 = s.info().p3;
+        o.dia_uniform = s.info().dia_uniform;
         o.halo_hide = s.info().halo_hide;
         o.ag_overlap = s.info().ag_overlap;
         o.ag_local_frac = s.info().ag_local_frac;

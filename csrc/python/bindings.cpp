@@ -534,6 +534,8 @@ PYBIND11_MODULE(_C, m) {
       d["ap_recompute"] = rr.ap_recompute;
       d["lean_only"] = rr.lean_only;
       d["lean_split"] = rr.lean_split;
+      d["p3"] = rr.p3;
+      d["dia_uniform"] = rr.dia_uniform;
       d["halo_hide"] = rr.halo_hide;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;

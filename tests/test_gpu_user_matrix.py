@@ -289,15 +289,17 @@ def test_lean_split_converges_like_the_generic_pass(mcg):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_lean_split_local_ranks_keeps_generic(mcg, world):
-    """At P = 2 / 4 (LocalComm) the setup does not take the lean / generic split (this round's known
-    limit: P = 1 only); a forced lean_split = 1 leaves every rank on the generic kernels, bit for bit
-    the lean_split = 0 solve."""
-    n = 1024
+def test_lean_split_off_at_local_ranks(mcg, world):
+    """lean_split is P = 1 only this round: at 4 LocalComm ranks (2048^2, changed rows on lines 100 and
+    1500) a split rank next to lean-only ones drifted from the generic iterates (4e-5 in 40
+    iterations; 2 ranks matched to 1e-10), so a forced lean_split = 1 leaves every rank that holds a
+    changed row on the generic kernels: bit for bit the lean_split = 0 solve."""
+    n = 2048
     A = _poisson(n, 2).tolil()
     d = A.diagonal()
-    for r in (n * 100 + 5, n * 600 + 900):
-        d[r] += 0.5
+    bad_lines = (100, 1500)
+    for ln in bad_lines:
+        d[n * ln + 7] += 0.5
     A.setdiag(d)
     p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
     C = mcg.native()
@@ -306,8 +308,8 @@ def test_lean_split_local_ranks_keeps_generic(mcg, world):
         o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
         o.lean_split = ls
         outs[ls] = C.run_local_ranks(p.native(), o, world, 40, True)
-        assert all(rk["lean_split"] == 0.0 and not rk["lean_only"] for rk in outs[ls]["ranks"])
-    assert outs[0]["ranks"][0]["rnorm"] == outs[1]["ranks"][0]["rnorm"]
+        assert all(rk["lean_split"] == 0.0 for rk in outs[ls]["ranks"])
+    assert [r["rnorm"] for r in outs[0]["ranks"]] == [r["rnorm"] for r in outs[1]["ranks"]]
     assert np.array_equal(outs[0]["x"], outs[1]["x"])
 
 
