@@ -792,7 +792,8 @@ void GpuCgSolver::setup() {
     const bool lean_all = lean_ok(g) && (go == g || lean_ok(go));
     // (P = 1 only: at 4 LocalComm ranks a split rank next to lean-only ones drifted from the generic
     // iterates by 4e-5 in 40 iterations -- a bug not found this round; 2 ranks matched to 1e-10)
-    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && !use_halo_ && opt_.form.lean_bpc_odd <= 0) {
+    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && (!use_halo_ || opt_.form.lean_split == 2) &&
+        opt_.form.lean_bpc_odd <= 0) {
       // some runs do not qualify: split the pass by run -- the lean kernels over the runs that do, the
       // generic ones over the rest, on the same grid (the same runs), when most runs qualify
       auto_mix_ = false;
@@ -804,7 +805,7 @@ void GpuCgSolver::setup() {
       // auto: runs of >= 128 lines (each wave takes one run) -- 16384^2 (256-line runs) 548-557 it/s vs 514
       // all-generic with 3 changed rows; the 64-line runs of 4096^2 / 8192^2 lose (the few generic runs
       // sit on the critical path: 4855 vs 6816, 1819 vs 1938; profiles/r4/lsplit)
-      const bool want = opt_.form.lean_split == 1 || (2 * fails < jobs && chunk >= 128);
+      const bool want = opt_.form.lean_split >= 1 || (2 * fails < jobs && chunk >= 128);
       if (jobs > 0 && fails < jobs && want) {
         lean_split_ = true;
         split_side_ = opt_.form.lean_split_side != 0;
