@@ -395,7 +395,12 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
 // the runs that qualify and then the generic ones over the rest, whose last arriver finishes the
 // reduction.  Returns the number of block partials written.
 int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
-  if (!lean_split_) {
+  // pass 0 (r_{-1} = b) runs the two-term generic kernel, which has no lean runs to leave to another
+  // launch: one launch over every run.  (Two launches there each computed every run, so a split rank's
+  // pass-0 sums came out doubled.  Harmless when every rank doubles -- alpha_0 and beta_0 are ratios of
+  // the sums -- but a split rank next to a lean-only one all-reduced 2x + y: the r4 P > 1 drift,
+  // profiles/r5/lsplit.)
+  if (!lean_split_ || k == 0) {
     enqueue_f1_(k, 0, 0, fused_red);
     return (g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_;
   }

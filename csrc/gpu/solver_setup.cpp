@@ -790,10 +790,9 @@ void GpuCgSolver::setup() {
       }
     }
     const bool lean_all = lean_ok(g) && (go == g || lean_ok(go));
-    // (P = 1 only: at 4 LocalComm ranks a split rank next to lean-only ones drifted from the generic
-    // iterates by 4e-5 in 40 iterations -- a bug not found this round; 2 ranks matched to 1e-10)
-    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && (!use_halo_ || opt_.form.lean_split == 2) &&
-        opt_.form.lean_bpc_odd <= 0) {
+    // (at P > 1 too since r5: the r4 drift of a split rank next to a lean-only one was pass 0 running
+    // on both launches, solver.cpp enqueue_pass_)
+    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && opt_.form.lean_bpc_odd <= 0) {
       // some runs do not qualify: split the pass by run -- the lean kernels over the runs that do, the
       // generic ones over the rest, on the same grid (the same runs), when most runs qualify
       auto_mix_ = false;

@@ -104,7 +104,7 @@ struct PassForm {
   int lean_split = -1;       // 2-D three-term dia4 carry when some runs' slice patterns are not uniform (a user matrix
                              // with a few odd rows): the lean kernels over the runs that qualify, the generic ones
                              // over the rest, in two launches; -1 = auto (when most runs qualify), 0 = off (every run
-                             // on the generic kernels), 1 = on, 2 = on with a halo too (P > 1: under investigation)
+                             // on the generic kernels), 1 = on
   int lean_split_side = 1;   // ... the generic launch on a side stream, concurrent with the lean one (0 = after it)
   int lean_depth_odd = 0;    // ... the odd passes (x update paired in: one more stream) their own depth / grid; 0 = as
   int lean_bpc_odd = 0;      // the even passes (the two grids each reduce their own block partials)

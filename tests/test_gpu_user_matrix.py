@@ -288,29 +288,40 @@ def test_lean_split_converges_like_the_generic_pass(mcg):
         assert abs(ts - tg) <= 0.05 * tg
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_lean_split_off_at_local_ranks(mcg, world):
-    """lean_split is P = 1 only this round: at 4 LocalComm ranks (2048^2, changed rows on lines 100 and
-    1500) a split rank next to lean-only ones drifted from the generic iterates (4e-5 in 40
-    iterations; 2 ranks matched to 1e-10), so a forced lean_split = 1 leaves every rank that holds a
-    changed row on the generic kernels: bit for bit the lean_split = 0 solve."""
+@pytest.mark.parametrize("world,lines", [(2, (1020,)), (4, (100, 1500))])
+def test_lean_split_mixed_ranks_match_one_rank(mcg, world, lines):
+    """lean_split at P > 1 with split ranks next to lean-only ones: at 2048^2 a
+    changed row on line 1020 splits rank 0 of 2 (its last run goes generic) while rank 1 stays
+    lean-only; rows on lines 100 and 1500 split ranks 0 and 2 of 4.  Round 4 saw a 0.11 / 4e-5 gap
+    after 40 iterations: pass 0 (the two-term generic kernel) ran on both of a split rank's launches,
+    doubling that rank's sums.  Now every arrangement matches the P = 1 generic solve to rounding."""
     n = 2048
     A = _poisson(n, 2).tolil()
     d = A.diagonal()
-    bad_lines = (100, 1500)
-    for ln in bad_lines:
+    for ln in lines:
         d[n * ln + 7] += 0.5
     A.setdiag(d)
     p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
     C = mcg.native()
-    outs = {}
-    for ls in (0, 1):
+
+    def run(w, ls, side=1, overlap=True):
         o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
         o.lean_split = ls
-        outs[ls] = C.run_local_ranks(p.native(), o, world, 40, True)
-        assert all(rk["lean_split"] == 0.0 for rk in outs[ls]["ranks"])
-    assert [r["rnorm"] for r in outs[0]["ranks"]] == [r["rnorm"] for r in outs[1]["ranks"]]
-    assert np.array_equal(outs[0]["x"], outs[1]["x"])
+        o.lean_split_side = side
+        o.overlap = overlap
+        return C.run_local_ranks(p.native(), o, w, 40, True)
+
+    one = run(1, 0)
+    r1 = one["ranks"][0]["rnorm"]
+    for ls, side, ov in ((1, 1, True), (1, 0, True), (1, 1, False), (0, 1, True)):
+        out = run(world, ls, side, ov)
+        split = [rk["lean_split"] > 0 for rk in out["ranks"]]
+        if ls == 1:
+            assert any(split) and not all(split), split  # split ranks next to lean-only ones
+            assert all(rk["lean_only"] for rk, sp_ in zip(out["ranks"], split) if not sp_)
+        rp = out["ranks"][0]["rnorm"]
+        assert abs(rp - r1) <= 1e-13 * r1, (ls, side, ov, rp, r1)
+        np.testing.assert_allclose(out["x"], one["x"], rtol=1e-11, atol=1e-13 * np.abs(one["x"]).max())
 
 
 def _nine_point(n=96, seed=3):
