@@ -109,6 +109,10 @@ def parse_args(argv=None):
                     help="sdma: the halo on copy engines (PeerHaloComm: the neighbours' buffers mapped through IPC, "
                          "flags by stream memory operations; all-reduce on RCCL) -- CU-free, so halo_hide can "
                          "run the interior band beside it")
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "ipc"],
+                    help="ipc: the 32-byte all-reduce through IPC-mapped mailboxes (PeerHaloComm + "
+                         "csrc/gpu/ipc_allreduce.hip, no RCCL; implies the peer-mapped halo).  With --rehearse-ranks "
+                         "the P processes on one GPU then run the real P-rank recurrence")
     ap.add_argument("--delay-comm", default="",
                     help="with --sim-world: AR_US,HALO_US[,copy|fat] -- every all-reduce / halo (or all-gather) exchange "
                          "of the rehearsed rank costs a device-side delay of that many microseconds (DelayComm) "
@@ -210,10 +214,12 @@ def _run_rank(args, out_fd) -> int:
             raise SystemExit(f"bench.py: unknown option {k!r}")
         setattr(opts, k, type(getattr(opts, k))(v))
     t_setup = time.perf_counter()
-    sdma = args.halo_transport == "sdma" and comm is not None and not sim
+    ipc_ar = args.allreduce == "ipc" and comm is not None and not sim
+    sdma = (args.halo_transport == "sdma" or ipc_ar) and comm is not None and not sim
     base_comm = comm  # RCCL's (or the rehearsal's) communicator: the count, the all-reduce
     if sdma:
-        comm = pdist.peer_halo(comm, env)
+        comm = pdist.peer_halo(comm, env, ipc_allreduce=ipc_ar)
+    real = not sim and (not rehearse or ipc_ar)  # a real P-rank solve (its residual must track)
     solver = (C.Solver(spec.native(), opts, args.sim_rank, args.sim_world, comm) if sim
               else C.Solver(spec.native(), opts, env.rank, env.world, comm))
     solver.setup()
@@ -264,7 +270,7 @@ def _run_rank(args, out_fd) -> int:
         extra["true_gap_rel"] = abs(tr - res["rnorm"]) / max(tr, 1e-300)
         extra["true_rel_to_b"] = tr / max(bnorm, 1e-300)
         tracks = abs(tr - res["rnorm"]) <= 1e-8 * max(tr, 1e-300) + 1e-12
-        ok = ok and (sim or rehearse or tracks or tr <= 1e-9 * bnorm)
+        ok = ok and (not real or tracks or tr <= 1e-9 * bnorm)
     info = solver.info
     # whole-job result: the slowest rank's clock, every rank ok and latched at the same count
     mine = {"dt": dt, "ok": bool(ok), "iterations": int(res["iterations"])}
@@ -295,6 +301,8 @@ def _run_rank(args, out_fd) -> int:
             "metric": METRIC if headline else (
                 "per-rank iterations/sec, timing rehearsal of rank %d of %d (collectives move nothing), %s"
                 % (args.sim_rank, args.sim_world, model) if sim else
+                "rehearsal: %d ranks on ONE GPU (IPC all-reduce + peer-mapped halo: the real %d-rank recurrence), %s"
+                % (env.world, env.world, model) if rehearse and ipc_ar else
                 "rehearsal: %d ranks on ONE GPU (collectives move nothing; rendezvous / barriers / aggregation real), %s"
                 % (env.world, model) if rehearse else "CG iterations/sec (whole node), %s" % model),
             "value": round(value, 4),
@@ -332,14 +340,17 @@ def _run_rank(args, out_fd) -> int:
                 "recurrence": info["recurrence"],
                 "pass": pass_label(info, args.problem),
                 **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
-                    if info.get("allgather") else ("window, exchanged ahead || all-reduce" if info.get("halo_ahead")
+                    if info.get("allgather") else ("window, read in-kernel from the neighbours' rows (halo_pull)"
+                                                   if info.get("halo_pull") else
+                                                   "window, exchanged ahead || all-reduce" if info.get("halo_ahead")
                                                    else "window")} if (n_gpus > 1 or sim) else {}),
                 "hipgraph": bool(info.get("graphs", use_graph)) and info.get("graph_fallbacks", 0) == 0,
                 "fused_reduce": info.get("fused_reduce", False),
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
                 "comm": args.comm,
-                **({"halo_transport": "sdma (copy engines, IPC)", "halo_hide": bool(info.get("halo_hide"))}
-                   if sdma else {}),
+                **({"halo_transport": ("in-kernel (the pass reads the IPC-mapped neighbour rows)" if info.get("halo_pull")
+                                       else "sdma (copy engines, IPC)"), "halo_hide": bool(info.get("halo_hide")),
+                    "allreduce": "ipc (mapped mailboxes)" if ipc_ar else "rccl"} if sdma else {}),
                 "launch": route,
                 **({"reserve_cus": opts.reserve_cus} if opts.reserve_cus else {}),
             },

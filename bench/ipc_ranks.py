@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""The real P-rank recurrence across PROCESSES on one GPU: P processes (gloo rendezvous for the IPC
+handle exchange) each run their rows of the CG solver with the IPC all-reduce (PeerHaloComm mailboxes,
+csrc/gpu/ipc_allreduce.hip) and the peer-mapped halo -- the in-kernel halo (halo_pull: the lean pass
+reads the neighbours' rows) or the copy-engine pulls (halo_pull 0) -- for a fixed iteration count, in
+32-iteration hipGraphs.  The parent then solves the same system with one rank and compares the
+residual norm and x.  The reference's two global reductions (CUDACG.cu:304, :328) are what the
+all-reduce carries; RCCL refuses two ranks on one GPU, so this is the only cross-process P-rank solve
+the one-GPU pool can run.  Prints one JSON line; exit 1 when a rank fails or the gap is too large.
+
+    python bench/ipc_ranks.py --world 2 [--problem poisson2d --n 1024 --iters 40 --halo-pull -1]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _opts(C, a):
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, check_every=1 << 30, format="sellc8", recurrence=1)
+    o.halo_pull = a.halo_pull
+    o.use_graph = not a.no_graph
+    o.watchdog_seconds = 120.0
+    return o
+
+
+def _spec(mcg, a):
+    return mcg.make_problem(a.problem, n=a.n, rhs="random", coef=a.coef).native()
+
+
+def rank_main(rank: int, a, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(a.world))
+    import torch
+    import torch.distributed as dist
+
+    import cuda_mpi_parallel_amd as mcg
+    from cuda_mpi_parallel_amd.parallel import dist as pdist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=a.world)
+    env = pdist.DistEnv(rank=rank, world=a.world, local_rank=0)
+    C = mcg.native()
+    comm = pdist.peer_halo(C.NullComm(rank, a.world), env, ipc_allreduce=True)
+    s = C.Solver(_spec(mcg, a), _opts(C, a), rank, a.world, comm)
+    s.setup()
+    pdist.attach_peer_halo(comm, env)
+    s.reset()
+    s.run_iterations(a.iters)
+    s.synchronize()
+    s.finalize()
+    res = s.result()
+    x = np.asarray(s.x_local())
+    tr = s.true_residual_norm()
+    info = s.info
+    q.put((rank, float(res["rnorm"]), int(res["iterations"]), x.tobytes(), float(tr),
+           bool(info.get("halo_pull")), bool(info.get("lean_only")), int(info.get("graph_fallbacks", 0)),
+           bool(info.get("graphs"))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--problem", choices=["poisson2d", "poisson3d"], default="poisson2d")
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--coef", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--halo-pull", type=int, default=-1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--tol", type=float, default=1e-13, help="relative gap allowed against one rank")
+    ap.add_argument("--port", type=int, default=29541)
+    ap.add_argument("--timeout", type=float, default=180.0)
+    a = ap.parse_args()
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=rank_main, args=(r, a, a.port, q)) for r in range(a.world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=a.timeout)
+    for p in procs:  # a rank stuck (its all-reduce times out on its own budget): end it
+        if p.is_alive():
+            p.kill()
+            p.join()
+    res = sorted(q.get(timeout=5) for _ in procs) if all(p.exitcode == 0 for p in procs) else []
+    out = {"world": a.world, "problem": a.problem, "n": a.n, "coef": a.coef, "iters": a.iters,
+           "halo_pull_opt": a.halo_pull, "graphs": not a.no_graph, "exitcodes": [p.exitcode for p in procs]}
+    ok = bool(res) and all(p.exitcode == 0 for p in procs)
+    if ok:
+        import cuda_mpi_parallel_amd as mcg
+
+        C = mcg.native()
+        one = C.run_local_ranks(_spec(mcg, a), _opts(C, a), 1, a.iters, True)
+        r1 = one["ranks"][0]["rnorm"]
+        x1 = np.asarray(one["x"])
+        xp = np.concatenate([np.frombuffer(r[3], dtype=np.float64) for r in res])
+        gap_r = max(abs(r[1] - r1) / r1 for r in res)
+        gap_x = float(np.linalg.norm(xp - x1) / np.linalg.norm(x1))
+        out.update(rnorm_1=r1, rnorm_p=res[0][1], gap_rnorm=gap_r, gap_x=gap_x,
+                   true_gap=max(abs(r[4] - r[1]) / r[4] for r in res),
+                   ranks=[{"rank": r[0], "iterations": r[2], "halo_pull": r[5], "lean_only": r[6],
+                           "graph_fallbacks": r[7], "graphs": r[8]} for r in res])
+        ok = (gap_r <= a.tol and gap_x <= 10 * a.tol and all(r[2] == a.iters for r in res)
+              and len({r[1] for r in res}) == 1)
+    out["ok"] = ok
+    print(json.dumps(out), flush=True)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -153,6 +153,47 @@ __device__ __forceinline__ void g_st_nt(double* base, uint32_t bo, double v) {
   if constexpr (MCG_NT_STORES) __builtin_nontemporal_store(v, (g_double*)((g_char*)(g_double*)base + bo));
   else *(g_double*)((g_char*)(g_double*)base + bo) = v;
 }
+// In-kernel halo (F1Vectors::pull_*): a neighbour's rows are loaded at system scope (sc0 sc1: past
+// this device's L2, so a line another device or process rewrote since is never served stale), and the
+// rank's own first / last line is stored the same way (written through to memory, where the
+// neighbour's next pass reads it once the all-reduce between the two passes has completed)
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ double ld_sys(const double* base, uint32_t bo) {
+  g_u64* p = (g_u64*)((g_char*)(g_double*)const_cast<double*>(base) + bo);
+  return __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+__device__ __forceinline__ void st_sys(double* base, uint32_t bo, double v) {
+  g_u64* p = (g_u64*)((g_char*)(g_double*)base + bo);
+  __hip_atomic_store(p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// a pulled ghost line's loads: side 0 = a local line, 1 / 2 = the lo / hi neighbour's rows
+struct PullBases {
+  const double *p[2], *ap[2];
+  int pub;
+  __device__ __forceinline__ void at(const F1Vectors& v, int64_t rb) {
+    for (int s = 0; s < 2; ++s) {
+      p[s] = v.pull_p[s] ? v.pull_p[s] + rb : nullptr;
+      ap[s] = v.pull_ap[s] ? v.pull_ap[s] + rb : nullptr;
+    }
+    pub = v.pull_pub;
+  }
+  // line l (rank-relative, wave-uniform) of a rank of nl lines
+  __device__ __forceinline__ int side(int64_t l, int64_t nl) const {
+    return (p[0] != nullptr && l == -1) ? 1 : ((p[1] != nullptr && l == nl) ? 2 : 0);
+  }
+  __device__ __forceinline__ double ld_p(int s, const double* local, uint32_t o) const {
+    return s == 0 ? g_ld(local, o) : ld_sys(p[s - 1], o);
+  }
+  __device__ __forceinline__ double ld_ap(int s, const double* local, uint32_t o) const {
+    return s == 0 ? g_ld(local, o) : ld_sys(ap[s - 1], o);
+  }
+  // the first / last line's p_k or Ap_k (CL steps only)
+  __device__ __forceinline__ void st_pub(bool boundary, double* base, uint32_t o, double v, bool nt) const {
+    if (pub && boundary) st_sys(base, o, v);
+    else if (nt) g_st_nt(base, o, v);
+    else g_st(base, o, v);
+  }
+};
 
 // Lean-run eligibility of one slice column's run [l0, l1) of a rank's nl lines (ss slices per
 // line): lines l0 - 1 .. l1 carry uniform patterns (one, B, for the inner lines; the rank's first
@@ -399,6 +440,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           double* __restrict__ x_ = x + xr;
           const double* __restrict__ apo_ = apx_o + rb;
           double* __restrict__ apn_ = apx_n + rb;
+          PullBases pl;  // in-kernel halo: the ghost lines from the neighbours' rows
+          pl.at(v, rb);
           const uint32_t ob0 = BIG ? 3u * ((uint32_t)LO << 3) : (uint32_t)e0 << 3;  // line 0 (ext layout)
           const uint32_t xb0 = BIG ? 0u : (uint32_t)i0 << 3;                         // line 0 of x
           const uint32_t cb0 = (uint32_t)(2 * (l0 * SS + col) - 1) << 3;  // edge arrays: 2 s - 1 of line 0
@@ -414,11 +457,14 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
           auto raw_at = [&](int32_t j) {
             Raw q;
-            const uint32_t o = line_ofs(jc(j)) + l8;
+            const int32_t jj = jc(j);
+            const uint32_t o = line_ofs(jj) + l8;
             q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
-            q.p = g_ld(po_, o);
+            q.p = pl.ld_p(pl.side(l0 + jj, nl), po_, o);
             return q;
           };
+          // a ghost line's Ap_{k-1}: the neighbour's stored first / last line
+          auto ap_gh = [&](int32_t j) { return pl.ld_ap(pl.side(l0 + j, nl), apo_, line_ofs(j) + l8); };
           // EP: lane roles (kernel comment) -- r: lanes 0 / 63, Ap: 15 / 48, p: 7 / 56; the other lanes
           // repeat lane 0's r load (the same address: no extra traffic).  Per lane a 64-bit base (reo,
           // eo or po_) and the byte offset of line 0 plus a per-line stride (SB, or LOB for p)
@@ -533,7 +579,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
             pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(e_p(edm1)), rm2.p, r0.p), rm1.r));
           } else if (is_ghost(-1)) {
-            pr_pk = fma(b, rm1.p, fma(na, g_ld(apo_, line_ofs(-1) + l8), rghost(-1, rm1)));
+            pr_pk = fma(b, rm1.p, fma(na, ap_gh(-1), rghost(-1, rm1)));
+            // pulled: this p_{k-1} is the next pass's p_{k-2} of the ghost line (rghost)
+            if (pl.p[0] != nullptr) g_st(const_cast<double*>(po_), line_ofs(-1) + l8, rm1.p);
           }
           double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
           {
@@ -556,8 +604,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
               pk1 = fma(b, q[0].p, rk1);
             } else if (CL && next == 2) {
-              rk1 = fma(na, g_ld(apo_, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
+              rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, q[0]));
               pk1 = fma(b, q[0].p, rk1);
+              if (pl.p[1] != nullptr) g_st(const_cast<double*>(po_), line_ofs(m + 1) + l8, q[0].p);
             }
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1);
             const uint32_t ob = line_ofs(m);
@@ -569,8 +618,10 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               g_st(en, sb, sum);
             }
             if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-            g_st_nt(pn_, ob + l8, o_pk);
-            if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apn_, ob + l8, sum);
+            const bool bnd = l0 + m == 0 || l0 + m == nl - 1;  // the halo's source lines
+            if constexpr (CL) pl.st_pub(bnd, pn_, ob + l8, o_pk, true);
+            else g_st_nt(pn_, ob + l8, o_pk);
+            if (CL && apx_n != nullptr && bnd) pl.st_pub(true, apn_, ob + l8, sum, false);
             s_pap = fma(o_pk, sum, s_pap);
             s_rap = fma(o_rk, sum, s_rap);
             s_apap = fma(sum, sum, s_apap);
@@ -646,6 +697,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       double* __restrict__ x_ = x + xr;
       const double* __restrict__ apo_ = apx_o + rb;
       double* __restrict__ apn_ = apx_n + rb;
+      PullBases pl;  // in-kernel halo (the dia4 lean loop's)
+      pl.at(v, rb);
       const int64_t kr = BIG ? (int64_t)i0 - 2 * (int64_t)LO : 0;  // lines -2 .. of the run: offsets >= 0
       const double* __restrict__ cvd_ = S.cvd + kr;
       const double* __restrict__ cve_ = S.cve + kr;
@@ -665,11 +718,13 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
       auto raw_at = [&](int32_t j) {
         Raw q;
-        const uint32_t o = line_ofs(jc(j)) + l8;
+        const int32_t jj = jc(j);
+        const uint32_t o = line_ofs(jj) + l8;
         q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
-        q.p = g_ld(po_, o);
+        q.p = pl.ld_p(pl.side(l0 + jj, nl), po_, o);
         return q;
       };
+      auto ap_gh = [&](int32_t j) { return pl.ld_ap(pl.side(l0 + j, nl), apo_, line_ofs(j) + l8); };
       auto edge_at = [&](int32_t j) {
         Edge q;
         const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
@@ -748,7 +803,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       if (l0 >= 1) {
         pr_pk = fma(b, rm1.p, fma(na, stencil_v(mkv(cm1, cm2.s), rm1.p, edm1.p, rm2.p, r0.p), rm1.r));
       } else if (is_ghost(-1)) {
-        pr_pk = fma(b, rm1.p, fma(na, g_ld(apo_, line_ofs(-1) + l8), rghost(-1, rm1)));
+        pr_pk = fma(b, rm1.p, fma(na, ap_gh(-1), rghost(-1, rm1)));
+        if (pl.p[0] != nullptr) g_st(const_cast<double*>(po_), line_ofs(-1) + l8, rm1.p);
       }
       VSet Vs = mkv(c0, cm1.s);  // line m
       double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
@@ -768,8 +824,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
           pk1 = fma(b, q[0].p, rk1);
         } else if (CL && next == 2) {
-          rk1 = fma(na, g_ld(apo_, line_ofs(m + 1) + l8), rghost(m + 1, q[0]));
+          rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, q[0]));
           pk1 = fma(b, q[0].p, rk1);
+          if (pl.p[1] != nullptr) g_st(const_cast<double*>(po_), line_ofs(m + 1) + l8, q[0].p);
         }
         const double sum = stencil_v(Vs, o_pk, o_epk, pr_pk, pk1);
         const uint32_t ob = line_ofs(m);
@@ -781,8 +838,10 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           g_st(en, sb, sum);
         }
         if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-        g_st_nt(pn_, ob + l8, o_pk);
-        if (CL && apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) g_st(apn_, ob + l8, sum);
+        const bool bnd = l0 + m == 0 || l0 + m == nl - 1;
+        if constexpr (CL) pl.st_pub(bnd, pn_, ob + l8, o_pk, true);
+        else g_st_nt(pn_, ob + l8, o_pk);
+        if (CL && apx_n != nullptr && bnd) pl.st_pub(true, apn_, ob + l8, sum, false);
         s_pap = fma(o_pk, sum, s_pap);
         s_rap = fma(o_rk, sum, s_rap);
         s_apap = fma(sum, sum, s_apap);
@@ -1231,13 +1290,16 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
         auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
         auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
         auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
+        PullBases pl;  // in-kernel halo (the 2-D lean loops')
+        pl.at(v, 0);
         auto raw_ld = [&](int32_t j, int32_t k) {
           Raw r;
           const uint32_t o = line_ofs(k) + l8;
           r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
-          r.p = g_ld(po, o);
+          r.p = pl.ld_p(pl.side(l0 + k, nl), po, o);
           return r;
         };
+        auto ap_gh = [&](int32_t j) { return pl.ld_ap(pl.side(l0 + j, nl), apo, line_ofs(j) + l8); };
         auto edge_ld = [&](int32_t j) {
           Edge r;
           const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
@@ -1338,7 +1400,8 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           const double t = stencil_v(mkv(cm1, cm2.t), rm1.p, edm1.p, rm2.p, r0.p, dn, up);
           pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
         } else if (is_ghost(-1)) {
-          pr_pk = pk_of(rghost(-1, rm1), g_ld(apo, line_ofs(-1) + l8), rm1.p);
+          pr_pk = pk_of(rghost(-1, rm1), ap_gh(-1), rm1.p);
+          if (pl.p[0] != nullptr) g_st(const_cast<double*>(po), line_ofs(-1) + l8, rm1.p);
         }
         VSet Vs = mkv(c0, cm1.t);  // plane m
         double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
@@ -1376,15 +1439,19 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
             pk1 = fma(b, qv[0].p, rk1);
           } else if (CL && next == 2) {
-            rk1 = fma(na, g_ld(apo, line_ofs(m + 1) + l8), rghost(m + 1, qv[0]));
+            rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, qv[0]));
             pk1 = fma(b, qv[0].p, rk1);
+            if (pl.p[1] != nullptr) g_st(const_cast<double*>(po), line_ofs(m + 1) + l8, qv[0].p);
           }
           double kdn, kup;
           nbr(par, 1, o_fpk, kdn, kup);
           const double sum = stencil_v(Vs, o_pk, o_epk, pr_pk, pk1, kdn, kup);
           if constexpr (PAIR) g_st_nt(x, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-          g_st_nt(pn, ob + l8, o_pk);
-          if (outer || (CL && gfull && (l0 + m == 0 || l0 + m == nl - 1))) g_st(apw, ob + l8, sum);
+          const bool bnd = CL && gfull && (l0 + m == 0 || l0 + m == nl - 1);  // the halo's source planes
+          if constexpr (CL) pl.st_pub(bnd, pn, ob + l8, o_pk, true);
+          else g_st_nt(pn, ob + l8, o_pk);
+          if (bnd) pl.st_pub(true, apw, ob + l8, sum, false);
+          else if (outer) g_st(apw, ob + l8, sum);
           if (edge_lane) {
             const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);
             g_st(ean, sb, sum);
@@ -1488,13 +1555,16 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           auto jc = [&](int32_t j) { return j < jlo ? jlo : (j > jhi ? jhi : j); };
           auto rc_ = [&](int32_t j) { return j < rlo ? rlo : (j > rhi ? rhi : j); };
           auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)(j - mb) * LOB; };
+          PullBases pl;  // in-kernel halo (the 2-D lean loops'; BIG: based like po_, at plane -3)
+          pl.at(v, BIG ? (int64_t)e0 - 3 * (int64_t)LO : 0);
           auto raw_ld = [&](int32_t j, int32_t k) {  // plane j's source, plane k's address
             Raw r;
             const uint32_t o = line_ofs(k) + l8;
             r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
-            r.p = g_ld(po_, o);
+            r.p = pl.ld_p(pl.side(l0 + k, nl), po_, o);
             return r;
           };
+          auto ap_gh = [&](int32_t j) { return pl.ld_ap(pl.side(l0 + j, nl), apo_, line_ofs(j) + l8); };
           auto edge_ld = [&](int32_t j) {  // plane j (clamped: compact index to the rank, row to ext)
             Edge r;
             const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
@@ -1568,7 +1638,8 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             const double t = stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p, dn, up);
             pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
           } else if (is_ghost(-1)) {
-            pr_pk = pk_of(rghost(-1, rm1), g_ld(apo_, line_ofs(-1) + l8), rm1.p);
+            pr_pk = pk_of(rghost(-1, rm1), ap_gh(-1), rm1.p);
+            if (pl.p[0] != nullptr) g_st(const_cast<double*>(po_), line_ofs(-1) + l8, rm1.p);
           }
           double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
           {
@@ -1605,15 +1676,19 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
               rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
               pk1 = fma(b, qv[0].p, rk1);
             } else if (CL && next == 2) {
-              rk1 = fma(na, g_ld(apo_, line_ofs(m + 1) + l8), rghost(m + 1, qv[0]));
+              rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, qv[0]));
               pk1 = fma(b, qv[0].p, rk1);
+              if (pl.p[1] != nullptr) g_st(const_cast<double*>(po_), line_ofs(m + 1) + l8, qv[0].p);
             }
             double kdn, kup;
             nbr(par, 1, o_fpk, kdn, kup);
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1, kdn, kup);
             if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)(m - mb) * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
-            g_st_nt(pn_, ob + l8, o_pk);
-            if (outer || (CL && gfull && (l0 + m == 0 || l0 + m == nl - 1))) g_st(apw_, ob + l8, sum);
+            const bool bnd = CL && gfull && (l0 + m == 0 || l0 + m == nl - 1);  // the halo's source planes
+            if constexpr (CL) pl.st_pub(bnd, pn_, ob + l8, o_pk, true);
+            else g_st_nt(pn_, ob + l8, o_pk);
+            if (bnd) pl.st_pub(true, apw_, ob + l8, sum, false);
+            else if (outer) g_st(apw_, ob + l8, sum);
             if (edge_lane) {
               const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
               g_st(ean, sb, sum);

@@ -46,6 +46,7 @@ LocalGroup::LocalGroup(int world, size_t max_allreduce) : world_(world), max_n_(
   mk(ev_post_);
   halo_vecs_.assign(world, nullptr);
   halo_layouts_.assign(world, nullptr);
+  reg_.assign(world, Reg{});
 }
 
 LocalGroup::~LocalGroup() {
@@ -96,6 +97,27 @@ void LocalComm::allreduce_sum(double* buf, size_t count, hipStream_t stream) {
                      buf, count);
   MCG_HIP(hipGetLastError(), "local allreduce failed");
   MCG_HIP(hipEventRecord(g.ev_done_[par][rank_], stream), "event record failed");
+}
+
+// the in-kernel halo's peer views: each rank's buffers as registered (one process, plain pointers).  A
+// solver asks for them at its first pulled pass, after every rank's setup registered (the all-reduces
+// of reset() are host barriers in between)
+void LocalComm::register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) {
+  LocalGroup& g = *group_;
+  std::lock_guard<std::mutex> lk(g.m_);
+  g.reg_[rank_] = LocalGroup::Reg{bufs, own_off, row_begin};
+}
+
+bool LocalComm::peer_view(int q, std::vector<double*>& bufs, int64_t& own_off, int64_t& row_begin) {
+  LocalGroup& g = *group_;
+  std::lock_guard<std::mutex> lk(g.m_);
+  MCG_CHECK(q >= 0 && q < g.world_, "local peer view: invalid rank");
+  const LocalGroup::Reg& r = g.reg_[q];
+  if (r.bufs.empty()) return false;
+  bufs = r.bufs;
+  own_off = r.own_off;
+  row_begin = r.row_begin;
+  return true;
 }
 
 void LocalComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,

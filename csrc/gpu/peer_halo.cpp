@@ -43,6 +43,27 @@ Entry make_entry(void* p) {
   MCG_HIP(hipIpcGetMemHandle(&e.handle, base), "peer halo: IPC handle failed");
   return e;
 }
+// a peer's allocation as this process addresses it: the same process (threads, or one rank) uses the
+// plain pointer (enabling peer access to another device), another process opens the IPC handle
+void* map_entry(const Entry& e, bool same_process, int64_t pdev, std::vector<void*>& opened) {
+  int dev = 0;
+  MCG_HIP(hipGetDevice(&dev), "get device failed");
+  if (same_process) {
+    if (pdev != dev) {
+      const hipError_t r = hipDeviceEnablePeerAccess((int)pdev, 0);
+      if (r != hipSuccess && r != hipErrorPeerAccessAlreadyEnabled) MCG_HIP(r, "peer halo: peer access failed");
+      (void)hipGetLastError();
+    }
+    return reinterpret_cast<void*>(e.ptr);
+  }
+  void* base = nullptr;
+  MCG_HIP(hipIpcOpenMemHandle(&base, e.handle, hipIpcMemLazyEnablePeerAccess), "peer halo: IPC open failed");
+  opened.push_back(base);
+  return static_cast<char*>(base) + e.offset;
+}
+size_t mailbox_bytes(int world) {
+  return (size_t)2 * world * kern::kIpcArMax * sizeof(double) + (size_t)(world + 1) * sizeof(unsigned long long);
+}
 }  // namespace
 
 PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int world)
@@ -60,11 +81,80 @@ PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int wo
   peer_flags_.assign(world, nullptr);
   peer_own_off_.assign(world, 0);
   peer_row_begin_.assign(world, 0);
+  // the IPC all-reduce's mailbox: uncached device memory (every access goes to memory, so a flag a peer
+  // wrote over the fabric is never served from a stale cache line), zeroed: call counters start at 0
+  MCG_CHECK(world <= kern::kIpcMaxRanks, "peer halo: too many ranks for the IPC all-reduce mailboxes");
+  const size_t mb_bytes = mailbox_bytes(world);
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&mbox_), mb_bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    MCG_HIP(hipMalloc(&mbox_, mb_bytes), "device malloc failed(ipc mailbox)");
+  }
+  MCG_HIP(hipMemset(mbox_, 0, mb_bytes), "device memset failed(ipc mailbox)");
+  MCG_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(unsigned long long),
+                        hipHostMallocMapped | hipHostMallocCoherent),
+          "host malloc failed(ipc all-reduce)");
+  *err_host_ = 0;
+  MCG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&mb_.err), err_host_, 0), "host pointer mapping failed");
+  mb_.rank = rank;
+  mb_.world = world;
 }
 
 PeerHaloComm::~PeerHaloComm() {
   for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
   if (flags_) (void)hipFree(flags_);
+  if (mbox_) (void)hipFree(mbox_);
+  if (err_host_) (void)hipHostFree(err_host_);
+}
+
+void PeerHaloComm::allreduce_sum(double* buf, size_t count, hipStream_t stream) {
+  if (!ipc_ar_) {
+    inner_->allreduce_sum(buf, count, stream);
+    return;
+  }
+  kern::ipc_allreduce(buf, (int)count, mb_, ar_budget_seconds, stream);
+}
+
+void PeerHaloComm::check_async() {
+  if (err_host_ != nullptr && __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0) {
+    fail("ipc all-reduce: a peer did not arrive", "waited " + std::to_string(ar_budget_seconds) + " s");
+  }
+  inner_->check_async();
+}
+
+std::string PeerHaloComm::mailbox_handle() const {
+  std::string s;
+  const uint64_t magic = kBlobMagic + 1;
+  const int64_t pid = (int64_t)getpid();
+  int dev = 0;
+  MCG_HIP(hipGetDevice(&dev), "get device failed");
+  const int64_t d64 = dev;
+  put(s, &magic, 8);
+  put(s, &pid, 8);
+  put(s, &d64, 8);
+  const Entry e = make_entry(mbox_);
+  put(s, &e, sizeof(Entry));
+  return s;
+}
+
+void PeerHaloComm::attach_mailbox(const std::vector<std::string>& all) {
+  MCG_CHECK((int)all.size() == world_, "ipc all-reduce: one mailbox handle per rank");
+  const int64_t me = (int64_t)getpid();
+  const size_t nslot = (size_t)2 * world_ * kern::kIpcArMax;
+  for (int q = 0; q < world_; ++q) {
+    double* mb = nullptr;
+    if (q == rank_) {
+      mb = mbox_;
+    } else {
+      size_t at = 0;
+      const std::string& s = all[q];
+      MCG_CHECK(get<uint64_t>(s, at) == kBlobMagic + 1, "ipc all-reduce: bad mailbox handle");
+      const int64_t pid = get<int64_t>(s, at), pdev = get<int64_t>(s, at);
+      mb = static_cast<double*>(map_entry(get<Entry>(s, at), pid == me, pdev, opened_));
+    }
+    mb_.slots[q] = mb;
+    mb_.flags[q] = reinterpret_cast<unsigned long long*>(mb + nslot);
+  }
+  ipc_ar_ = true;
 }
 
 void PeerHaloComm::register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) {
@@ -100,22 +190,7 @@ std::string PeerHaloComm::local_handles() const {
 void PeerHaloComm::attach(const std::vector<std::string>& all) {
   MCG_CHECK((int)all.size() == world_, "peer halo: one handle blob per rank");
   const int64_t me = (int64_t)getpid();
-  int dev = 0;
-  MCG_HIP(hipGetDevice(&dev), "get device failed");
-  auto map = [&](const Entry& e, int64_t pid, int64_t pdev) -> void* {
-    if (pid == me) {  // the same process (threads, or one rank): plain pointers, peer access if needed
-      if (pdev != dev) {
-        const hipError_t r = hipDeviceEnablePeerAccess((int)pdev, 0);
-        if (r != hipSuccess && r != hipErrorPeerAccessAlreadyEnabled) MCG_HIP(r, "peer halo: peer access failed");
-        (void)hipGetLastError();
-      }
-      return reinterpret_cast<void*>(e.ptr);
-    }
-    void* base = nullptr;
-    MCG_HIP(hipIpcOpenMemHandle(&base, e.handle, hipIpcMemLazyEnablePeerAccess), "peer halo: IPC open failed");
-    opened_.push_back(base);
-    return static_cast<char*>(base) + e.offset;
-  };
+  auto map = [&](const Entry& e, int64_t pid, int64_t pdev) { return map_entry(e, pid == me, pdev, opened_); };
   for (int q = 0; q < world_; ++q) {
     if (q == rank_) {
       peer_flags_[q] = flags_;
@@ -146,6 +221,15 @@ void PeerHaloComm::on_captured(bool kept) {
     return;
   }
   MCG_CHECK(n % 2 == 0, "peer halo: a graph must hold an even number of exchanges (its flag values replay)");
+}
+
+bool PeerHaloComm::peer_view(int q, std::vector<double*>& bufs, int64_t& own_off, int64_t& row_begin) {
+  MCG_CHECK(q >= 0 && q < world_, "peer halo: invalid rank");
+  if (!attached_) return false;
+  bufs = peer_bufs_[q];
+  own_off = peer_own_off_[q];
+  row_begin = peer_row_begin_[q];
+  return true;
 }
 
 std::vector<uintptr_t> PeerHaloComm::peer_buffers(int q) const {

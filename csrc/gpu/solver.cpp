@@ -152,6 +152,7 @@ void GpuCgSolver::reset() {
     opt_.tol = tol;
   }
   k_ = 0;
+  pull_from_ = 2;
   finalized_ = false;
   halo_ready_for_ = -1;
   ghosts_for_ = -1;
@@ -241,6 +242,17 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
       const int64_t ns2 = 2 * std::max<int64_t>((n + 63) / 64, 1);
       v.re_old = ape_[(k + 1) & 1].get() + ns2;
       v.re_new = ape_[k & 1].get() + ns2;
+    }
+    if (pull_ && !probing_ && !final_mode) {  // in-kernel halo (cg_carry_ar.hip PullBases)
+      v.pull_pub = 1;
+      if (k >= pull_from_) {
+        map_pull_();
+        const int pb = (k + 1) & 1;  // p_old / apx_old: the neighbours' pass k-1 outputs
+        for (int sd = 0; sd < 2; ++sd) {
+          v.pull_p[sd] = pull_p_[pb][sd];
+          v.pull_ap[sd] = pull_ap_[pb][sd];
+        }
+      }
     }
     if (ar3_) {
       kern::cg_carry_ar3(2, info_.ar3_kw, S, v, L_.own_off, tr,
@@ -430,7 +442,18 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
   trace::Range tr_("mcg.iteration.single_reduction");
   int np = (g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_;
   const bool fr = fused_red_;
-  if (hide_) {
+  if (pull_) {
+    // in-kernel halo: from pull_from_ on the pass reads its ghost lines from the neighbours' rows, so
+    // the iteration is the pass and the all-reduce; before that (and for finalize) the ghosts are
+    // exchanged in the serial order
+    if (k >= pull_from_) {
+      join_halo_();
+      ghosts_for_ = -1;
+    } else {
+      ensure_ghosts_(k);
+    }
+    np = enqueue_pass_(k, fr);
+  } else if (hide_) {
     // halo_hide: the interior band reads no ghost line, so it runs while this iteration's ghosts land
     // (copy engines: no CU is taken from the pass); then the lines at both ends of the rank, whose
     // last arriver finishes the reduction; then the next iteration's ghosts -- this pass's outputs,
@@ -604,6 +627,45 @@ void GpuCgSolver::enqueue_iteration_(int k) {
   if (use_comm_) comm_->allreduce_sum(&st->rr_new, 1, s0_);
 }
 
+// The in-kernel halo's pointers: for each p / apx buffer and side, the neighbour's buffer shifted so
+// that this rank's ext index of a ghost row addresses the owner's copy of the same global row.  With a
+// rehearsal communicator (no peers, no data moved) the rank's own first / last line stands in for the
+// neighbours' (timing only, like NullComm's collectives).
+void GpuCgSolver::map_pull_() {
+  if (pull_mapped_) return;
+  auto idx = [&](const double* b) {
+    auto it = std::find(halo_reg_.begin(), halo_reg_.end(), b);
+    MCG_CHECK(it != halo_reg_.end(), "in-kernel halo: buffer not registered");
+    return (size_t)(it - halo_reg_.begin());
+  };
+  const int64_t line = (int64_t)tr_all_.strip * 64;  // one grid line (2-D) / plane (3-D)
+  for (int sd = 0; sd < 2; ++sd) {
+    const HaloRange* h = nullptr;
+    for (const HaloRange& r : L_.recvs)
+      if (sd == 0 ? r.gbegin < L_.row_begin : r.gbegin >= L_.row_end) h = &r;
+    for (int b = 0; b < 2; ++b) pull_p_[b][sd] = pull_ap_[b][sd] = nullptr;
+    if (h == nullptr) continue;  // the first / last rank: no ghost on that side
+    MCG_CHECK(h->count == line && (sd == 0 ? h->gbegin + h->count == L_.row_begin : h->gbegin == L_.row_end),
+              "in-kernel halo: the ghosts must be one whole line / plane next to the rank's rows");
+    std::vector<double*> bufs;
+    int64_t q_own = 0, q_rb = 0, src = 0;
+    if (comm_->peer_view(h->peer, bufs, q_own, q_rb)) {
+      MCG_CHECK(bufs.size() == halo_reg_.size(), "in-kernel halo: ranks registered different buffer lists");
+      src = q_own + (h->gbegin - q_rb);  // the owner's ext index of the first ghost row
+    } else {
+      MCG_CHECK(!comm_->moves_data(), "in-kernel halo: the communicator cannot map the peers' buffers");
+      bufs = halo_reg_;  // rehearsal stand-in: this rank's own first / last line
+      src = L_.own_off + (sd == 0 ? 0 : L_.n_local() - line);
+    }
+    const int64_t shift = src - L_.ext_index(h->gbegin);
+    for (int b = 0; b < 2; ++b) {
+      pull_p_[b][sd] = bufs[idx(p_[b].get())] + shift;
+      pull_ap_[b][sd] = bufs[idx(apx_[b].get())] + shift;
+    }
+  }
+  pull_mapped_ = true;
+}
+
 void GpuCgSolver::join_halo_() {
   if (!halo_pending_) return;
   MCG_HIP(hipStreamWaitEvent(s0_, ev_h_, 0), "stream wait failed");
@@ -634,7 +696,7 @@ void GpuCgSolver::capture_pair_(int kind) {
   const int iters = kind == 0 ? 2 : opt_.form.graph_iters;
   // halo_ahead: a graph starts with its ghosts in place (joined before the launch) and ends by
   // joining the prefetch of its last iteration, so every replay sees the same host-side state
-  if (halo_ahead_) ensure_ghosts_(k_);
+  if (halo_ahead_ && !pull_) ensure_ghosts_(k_);
   MCG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "graph capture failed");
   try {
     for (int j = 0; j < iters; ++j) enqueue_iteration_(k_ + j);
@@ -648,7 +710,7 @@ void GpuCgSolver::capture_pair_(int kind) {
     halo_pending_ = false;
     throw;
   }
-  ghosts_for_ = halo_ahead_ ? k_ : -1;  // nothing captured has run yet
+  ghosts_for_ = (halo_ahead_ && !pull_) ? k_ : -1;  // nothing captured has run yet
   halo_pending_ = false;
   const hipError_t ec = hipStreamEndCapture(s, &graph_[kind]);
   if (comm_ != nullptr) comm_->on_captured(ec == hipSuccess);
@@ -660,7 +722,7 @@ void GpuCgSolver::run_iterations(int count) {
   MCG_CHECK(setup_done_, "solver not set up");
   const int glong = opt_.form.graph_iters > 2 ? opt_.form.graph_iters : 0;
   while (count > 0) {
-    if (opt_.use_graph && k_ >= 2 && (k_ % 2) == 0 && count >= 2) {
+    if (opt_.use_graph && k_ >= 2 && (k_ % 2) == 0 && count >= 2 && (!pull_ || k_ >= pull_from_)) {
       const int kind = glong && count >= glong ? 1 : 0;
       if (!graph_exec_[kind]) {
         try {
@@ -674,7 +736,7 @@ void GpuCgSolver::run_iterations(int count) {
           continue;
         }
       }
-      if (halo_ahead_) ensure_ghosts_(k_);
+      if (halo_ahead_ && !pull_) ensure_ghosts_(k_);
       const hipError_t le = (k_ == opt_.hooks.fail_graph_launch_at) ? hipErrorInvalidValue  // test hook
                                                               : hipGraphLaunch(graph_exec_[kind], s0_);
       if (le != hipSuccess) {
@@ -695,7 +757,7 @@ void GpuCgSolver::run_iterations(int count) {
       const int done = kind == 0 ? 2 : glong;
       k_ += done;
       count -= done;
-      if (halo_ahead_) ghosts_for_ = k_;  // prefetched by the graph's last iteration and joined
+      if (halo_ahead_ && !pull_) ghosts_for_ = k_;  // prefetched by the graph's last iteration and joined
     } else {
       if (k_ == opt_.hooks.inject_nan_at) inject_fault_(k_);
       enqueue_iteration_(k_);

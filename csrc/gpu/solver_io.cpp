@@ -106,6 +106,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   std::fclose(f);
   if (!ok) fail("checkpoint truncated", path);
   k_ = (int)h.k;
+  pull_from_ = k_ + 2;  // in-kernel halo: the first two iterations exchange (their p_{k-2} ghost rows)
   finalized_ = false;
   halo_ready_for_ = -1;
   ghosts_for_ = -1;
@@ -253,16 +254,18 @@ double GpuCgSolver::true_residual_norm() {
   trace::Range tr_("mcg.true_residual");
   synchronize();
   const int64_t n = L_.n_local();
-  DeviceBuffer<double> xe(L_.ext_len, "x", 8), y(n, "Ap", 8), out(1, "scalar");
+  // (a peer-mapping communicator moves registered buffers only: its x buffer, xt_)
+  DeviceBuffer<double> xtmp(xt_.get() ? 0 : L_.ext_len, "x", 8), y(n, "Ap", 8), out(1, "scalar");
+  double* xe = xt_.get() ? xt_.get() : xtmp.get();
   hipStream_t s = s0_;
-  MCG_HIP(hipMemsetAsync(xe.get(), 0, xe.bytes(), s), "device memset failed");
-  MCG_HIP(hipMemcpyAsync(xe.get() + L_.own_off, x_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
+  MCG_HIP(hipMemsetAsync(xe, 0, (size_t)L_.ext_len * sizeof(double), s), "device memset failed");
+  MCG_HIP(hipMemcpyAsync(xe + L_.own_off, x_.get(), n * sizeof(double), hipMemcpyDeviceToDevice, s),
           "vector copy failed(x)");
   if (use_halo_) {
-    double* v[1] = {xe.get()};
+    double* v[1] = {xe};
     comm_->halo_exchange(L_, v, 1, s);
   }
-  spmv_plain_(xe.get(), y.get(), s);
+  spmv_plain_(xe, y.get(), s);
   kern::xpby(b_.get(), -1.0, y.get(), n, s);  // y = b - A x
   kern::dot_partials(y.get(), y.get(), n, partials_.get(), g_b_, s);
   kern::sum_partials(partials_.get(), g_b_, out.get(), s);

@@ -911,6 +911,23 @@ void GpuCgSolver::setup() {
     }
   }
   info_.halo_hide = hide_;
+  // in-kernel halo: the lean carries read their ghost lines / planes from the neighbours' rows and store
+  // their own first / last ones write-through (cg_carry_ar.hip PullBases), so an iteration from 2 on is
+  // the pass + the all-reduce, no halo step.  The all-reduce orders the passes: a rank's pass k + 1
+  // starts after every rank's pass k has finished (its sums are in the all-reduce), which is all the
+  // pulled rows need -- p_{k-1} / Ap_{k-1} of the peer's first / last line sit in the buffers its pass k
+  // does not write, and its pass k + 1 rewrites them only after this rank's pass k has contributed.
+  // Every rank must take it (it decides the collectives of an iteration)
+  {
+    const bool can = use_halo_ && ar_ && p3_ && lean_only_ && !hide_ && !lean_split_ && !L_.allgather && !pmat_ &&
+                     opt_.recurrence == 1 && n > 0 && comm_ != nullptr &&
+                     (comm_->maps_peers() || (opt_.form.halo_pull == 1 && !comm_->moves_data()));
+    pull_ = opt_.form.halo_pull != 0 && can && (opt_.form.halo_pull == 1 || comm_->maps_peers());
+    if (use_comm_ && world_ > 1) pull_ = all_ranks_agree_(pull_);
+    MCG_CHECK(opt_.form.halo_pull != 1 || pull_,
+              "halo_pull needs the lean line / plane carry on every rank (P > 1, a communicator that maps its peers)");
+    info_.halo_pull = pull_;
+  }
   // the copy-engine halo replays slowly from a hipGraph (a P = 8 share of 16384^2 with halo_hide:
   // 0.393 ms an iteration captured, 0.301 eager, profiles/r4/hide): halo_hide iterates eagerly
   if (hide_) opt_.use_graph = false;
@@ -994,11 +1011,13 @@ void GpuCgSolver::setup() {
   // the vectors a halo may carry, final now (after the placement probe): for a transport that maps
   // its peers' buffers (PeerHaloComm); the same list, in the same order, on every rank
   if (comm_ != nullptr) {
-    std::vector<double*> hb;
-    for (DeviceBuffer<double>* b : {&r_, &r1_, &Ap_, &Ap1_, &p_[0], &p_[1], &ra_[0], &ra_[1], &apx_[0], &apx_[1], &w_, &xe_})
-      if (b->get() != nullptr) hb.push_back(b->get());
-    comm_->register_halo_buffers(hb, L_.own_off, L_.row_begin);
+    if (use_halo_ && comm_->maps_peers()) xt_.allocate(L_.ext_len, "x", 8);
+    halo_reg_.clear();
+    for (DeviceBuffer<double>* b : {&r_, &r1_, &Ap_, &Ap1_, &p_[0], &p_[1], &ra_[0], &ra_[1], &apx_[0], &apx_[1], &w_, &xe_, &xt_})
+      if (b->get() != nullptr) halo_reg_.push_back(b->get());
+    comm_->register_halo_buffers(halo_reg_, L_.own_off, L_.row_begin);
   }
+  pull_mapped_ = false;
   if (opt_.recurrence == 2) pick_pipe_order_();
   setup_done_ = true;
   setup_seconds_ = std::chrono::duration<double>(clk::now() - t0).count();

@@ -117,6 +117,13 @@ struct PassForm {
                              // engines): the pass runs as the interior band (no ghost read) while the ghosts
                              // arrive, then the band_h = 4 lines at each end of the rank; the halo of the next
                              // iteration is issued on the side stream right after that second launch. 1 = on
+  int halo_pull = -1;        // multi-rank lean carries (2-D line, 3-D plane): the in-kernel halo -- the waves that
+                             // read a ghost line load it straight from the neighbour's rows (peer-mapped: IPC or
+                             // another thread's pointers) and every pass stores its first / last line write-through,
+                             // so an iteration is the pass + the all-reduce, with no halo step (from iteration 2 on;
+                             // the first two exchange as before).  -1 = auto (when the communicator maps its peers:
+                             // Communicator::maps_peers), 0 = off, 1 = on (with a rehearsal communicator that moves no
+                             // data, the rank's own first / last line stands in for the neighbours': timing only)
   int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
                              // right after pass k wrote it (side stream, next to the all-reduce) and run one
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's

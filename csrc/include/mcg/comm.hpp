@@ -36,6 +36,7 @@
 #include <string>
 #include <vector>
 
+#include "mcg/kernels.hpp"
 #include "mcg/partition.hpp"
 
 namespace mcg {
@@ -97,11 +98,20 @@ class Communicator {
   // true: the halo moves its bytes with copy engines (no compute units), so it can run while a pass
   // holds every CU (CgOptions::form.halo_hide splits the pass around it)
   virtual bool halo_cu_free() const { return false; }
+  // true: peer_view() will give the peers' buffers once every rank has set up (and, for processes,
+  // attached): the solver may then read its ghost lines straight from them (PassForm::halo_pull)
+  virtual bool maps_peers() const { return false; }
   // the solver's halo-exchanged vectors (every rank registers the same list in the same order, once
   // its buffers are final): a transport that maps its peers' memory needs them
   // (own_off / row_begin: where this rank's owned rows start in those ext vectors, and their first
   // global row)
   virtual void register_halo_buffers(const std::vector<double*>&, int64_t /*own_off*/, int64_t /*row_begin*/) {}
+  // the in-kernel halo (GpuCgSolver pull_): rank q's registered buffers as this process addresses them
+  // (IPC-mapped, or plain pointers of another thread) and where its owned rows start in them; false:
+  // this transport cannot map its peers (RCCL alone, NullComm, DelayComm)
+  virtual bool peer_view(int /*q*/, std::vector<double*>& /*bufs*/, int64_t& /*own_off*/, int64_t& /*row_begin*/) {
+    return false;
+  }
   // a graph capture holding this communicator's operations has ended (the solver calls it after
   // hipStreamEndCapture; kept = false: the capture failed and its graph is dropped): a transport whose
   // captured operations replay fixed values checks / rewinds its sequence here
@@ -198,23 +208,28 @@ class DelayComm final : public Communicator {
 //     for each rank q I read from: wait ready[q] == v(s), pull the ranges, write v(s) into q's done[me]
 // The all-gather ghost layout (unstructured sparsity) takes the same path, every peer's block a range
 // pulled on a stream of its own (CopyFan: several copy engines at once).
-// The all-reduce goes to `inner` (RCCL, or NullComm in a one-GPU rehearsal).
+// The all-reduce goes to `inner` (RCCL, or NullComm in a one-GPU rehearsal), or, once
+// attach_mailbox() has mapped every rank's mailbox, to the IPC all-reduce (ipc_allreduce.hip: each
+// rank's sums written into every mailbox, a flag, a bounded wait, the slots summed in rank order) --
+// which needs no RCCL, so P processes on ONE GPU run the real P-rank recurrence.
 class PeerHaloComm final : public Communicator {
  public:
   PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int world);
   ~PeerHaloComm() override;
   int rank() const override { return rank_; }
   int world() const override { return world_; }
-  void allreduce_sum(double* buf, size_t count, hipStream_t stream) override { inner_->allreduce_sum(buf, count, stream); }
+  void allreduce_sum(double* buf, size_t count, hipStream_t stream) override;
   void halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
                      const int* widths = nullptr) override;
-  void check_async() override { inner_->check_async(); }
+  void check_async() override;
   bool graph_capturable() const override { return inner_->graph_capturable() && capturable_; }
-  bool moves_data() const override { return inner_->moves_data(); }
+  bool moves_data() const override { return ipc_ar_ || inner_->moves_data(); }
   void abort() override { inner_->abort(); }
   bool serialized() const override { return false; }  // the halo never enters the inner communicator
   bool halo_cu_free() const override { return true; }
+  bool maps_peers() const override { return true; }
   void register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) override;
+  bool peer_view(int q, std::vector<double*>& bufs, int64_t& own_off, int64_t& row_begin) override;
   void on_captured(bool kept) override;
   // this rank's IPC handles (flags + registered buffers) as bytes, for an out-of-band all-gather
   std::string local_handles() const;
@@ -224,6 +239,12 @@ class PeerHaloComm final : public Communicator {
   void set_capturable(bool c) { capturable_ = c; }
   // test hook: the registered buffer list (device pointers) of rank q as mapped here
   std::vector<uintptr_t> peer_buffers(int q) const;
+  // the IPC all-reduce: this rank's mailbox handle (allocated at construction) for an out-of-band
+  // all-gather, then every rank's, in rank order; from then on allreduce_sum runs through the mailboxes
+  std::string mailbox_handle() const;
+  void attach_mailbox(const std::vector<std::string>& all);
+  bool ipc_allreduce() const { return ipc_ar_; }
+  double ar_budget_seconds = 120.0;  // a peer that does not arrive for this long: error (check_async)
 
  private:
   std::shared_ptr<Communicator> inner_;
@@ -236,6 +257,10 @@ class PeerHaloComm final : public Communicator {
   std::vector<int64_t> peer_own_off_, peer_row_begin_;
   std::vector<void*> opened_;                    // IPC mappings to close
   CopyFan fan_;                                  // the all-gather layout's pulls side by side
+  double* mbox_ = nullptr;                       // uncached: [2][world][kIpcArMax] slots, then world + 1 u64 flags
+  unsigned long long* err_host_ = nullptr;       // pinned, device-mapped error word of the IPC all-reduce
+  kern::IpcMailboxes mb_;
+  bool ipc_ar_ = false;
   long seq_ = 0;
   long cap_n_ = 0;  // exchanges recorded by the capture in progress
   // A captured exchange replays the flag values of its capture, which continues the 1/2 alternation
@@ -265,6 +290,11 @@ class LocalGroup {
   std::vector<hipEvent_t> ev_copy_[2], ev_done_[2], ev_pre_, ev_post_;
   std::vector<double* const*> halo_vecs_;
   std::vector<const LocalLayout*> halo_layouts_;
+  struct Reg {  // register_halo_buffers() of each rank (the in-kernel halo's peer views)
+    std::vector<double*> bufs;
+    int64_t own_off = 0, row_begin = 0;
+  };
+  std::vector<Reg> reg_;
   std::mutex m_;
   std::condition_variable cv_;
   int count_ = 0, gen_ = 0;
@@ -280,6 +310,9 @@ class LocalComm final : public Communicator {
                      const int* widths = nullptr) override;
   bool graph_capturable() const override { return false; }
   bool halo_cu_free() const override { return true; }  // hipMemcpyDeviceToDeviceNoCU (SDMA engines)
+  bool maps_peers() const override { return true; }
+  void register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) override;
+  bool peer_view(int q, std::vector<double*>& bufs, int64_t& own_off, int64_t& row_begin) override;
 
  private:
   std::shared_ptr<LocalGroup> group_;

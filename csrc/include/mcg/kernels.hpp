@@ -258,6 +258,17 @@ struct F1Vectors {
   // the neighbouring waves read 16 contiguous bytes per slice instead of two scattered sectors
   const double* re_old = nullptr;
   double* re_new = nullptr;
+  // In-kernel halo (multi-rank lean carries; solver pull_): [0] the lo, [1] the hi ghost line / plane
+  // read straight from the neighbour's rows instead of this rank's ghost rows.  pull_p[s][e] for an
+  // ext index e of that ghost line is the owner's p_{k-1} of the same global row (a pointer into the
+  // neighbour's mapped buffer, shifted by the two layouts' offsets), pull_ap likewise its Ap_{k-1};
+  // nullptr: that side reads the local ghost rows a halo exchange filled.  The pass also copies the
+  // pulled p_{k-1} into its own ghost rows of p_old (the p_{k-2} the next pass recovers r from).
+  const double* pull_p[2] = {nullptr, nullptr};
+  const double* pull_ap[2] = {nullptr, nullptr};
+  // store the rank's first / last line's p_k and Ap_k write-through at system scope: the neighbours'
+  // next pass reads them over the fabric, ordered after this pass by the all-reduce between
+  int pull_pub = 0;
 };
 // In-kernel reduction of a fused pass's block partials (replaces the cg_reduce_f1 launch, so
 // one iteration is ONE kernel + the 32-B all-reduce).  Two-level last-arriver fan-in: each block
@@ -469,6 +480,18 @@ void axpy(double alpha, const double* x, double* y, int64_t n, hipStream_t strea
 void xpby(const double* x, double beta, double* y, int64_t n, hipStream_t stream);   // y = x + b y
 
 int grid_for(int64_t work_items, int block, int blocks_per_cu);
+
+// ---- IPC all-reduce (csrc/gpu/ipc_allreduce.hip): the CG scalars through peer-mapped mailboxes ----
+constexpr int kIpcArMax = 8;      // doubles per all-reduce
+constexpr int kIpcMaxRanks = 16;
+struct IpcMailboxes {
+  double* slots[kIpcMaxRanks] = {};               // rank q's mailbox as mapped here: [2 parities][world][kIpcArMax]
+  unsigned long long* flags[kIpcMaxRanks] = {};   // rank q's arrival flags [world], + its call counter [world]
+  unsigned long long* err = nullptr;              // host-mapped: 1 when a peer did not arrive within the budget
+  int rank = 0, world = 1;
+};
+// in-place sum of `count` doubles over the ranks, in rank order (the same bits everywhere); one wave
+void ipc_allreduce(double* buf, int count, const IpcMailboxes& mb, double budget_seconds, hipStream_t stream);
 
 // ---- probes (csrc/gpu/probe_kernels.hip) ----
 // `blocks` workgroups of 256 threads spinning for `microseconds` on the realtime clock; fat: ~270

@@ -74,6 +74,7 @@ struct SolverInfo {
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool halo_hide = false;  // PassForm::halo_hide: the pass split around a copy-engine halo
+  bool halo_pull = false;  // PassForm::halo_pull: the in-kernel halo (ghost lines read from the peers' rows)
   bool diav = false;
   double aligned_fill = 0.0;  // user matrices: SELL-64/aligned slots per nonzero of the per-slice offset unions     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
@@ -161,6 +162,13 @@ class GpuCgSolver {
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
   bool hide_ = false;           // PassForm::halo_hide in effect: interior band || copy-engine halo, then the ends
+  bool pull_ = false;           // PassForm::halo_pull in effect (in-kernel halo)
+  int pull_from_ = 2;           // ... first iteration that pulls (reset / resume + 2: the earlier ones exchange)
+  bool pull_mapped_ = false;    // ... pull_p_ / pull_ap_ resolved (map_pull_, at the first pulled pass)
+  const double* pull_p_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [p buffer][lo, hi side]
+  const double* pull_ap_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [apx buffer][lo, hi side]
+  std::vector<double*> halo_reg_;  // the buffers registered with the communicator (its peer_view order)
+  void map_pull_();
   bool split_side_ = true;     // lean_split: the generic launch on s2_, concurrent with the lean one
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
@@ -268,6 +276,8 @@ class GpuCgSolver {
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
   bool pipe_ar_first_ = false;
   DeviceBuffer<double> w_, z_, q_, xe_;  // pipelined CG: w = A r (ext), z = A s, q = A w, x in the ext layout
+  DeviceBuffer<double> xt_;  // x in the ext layout for true_residual_norm, registered with a peer-mapping
+                             // communicator (its halo can only move registered buffers)
   DeviceBuffer<double> ra_[2];     // interleaved {r, Ap} pairs by parity (2 * ext_len doubles each)
   DeviceBuffer<uint32_t> smeta_;  // Ap-recomputing carry: per-slice (first slot / 64 | width << 28)
   DeviceBuffer<double> ape_[2];    // Ap-recomputing carry: Ap of the slices' edge rows, by parity

@@ -228,6 +228,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(lean_split_side)
       MCG_FORM_PROP(lean_bpc_odd)
       MCG_FORM_PROP(halo_hide)
+      MCG_FORM_PROP(halo_pull)
       MCG_FORM_PROP(tile_pace_lag)
       MCG_FORM_PROP(tile_pace_slack)
       MCG_FORM_PROP(tile_pace_sleep)
@@ -385,6 +386,18 @@ PYBIND11_MODULE(_C, m) {
         c.attach(v);
       })
       .def_property_readonly("attached", &PeerHaloComm::attached)
+      .def("mailbox_handle", [](const PeerHaloComm& c) { return py::bytes(c.mailbox_handle()); })
+      .def("attach_mailbox", [](PeerHaloComm& c, const std::vector<py::bytes>& all) {
+        std::vector<std::string> v;
+        for (const py::bytes& b : all) v.push_back(std::string(b));
+        c.attach_mailbox(v);
+      }, "map every rank's IPC all-reduce mailbox; from then on the all-reduce runs through them")
+      .def_property_readonly("ipc_allreduce", &PeerHaloComm::ipc_allreduce)
+      .def_readwrite("ar_budget_seconds", &PeerHaloComm::ar_budget_seconds)
+      .def("allreduce_ptr", [](PeerHaloComm& c, uintptr_t buf, size_t count, uintptr_t stream) {
+        c.allreduce_sum(reinterpret_cast<double*>(buf), count, as_stream(stream));
+      }, "test hook: in-place sum all-reduce of `count` doubles at a device pointer")
+      .def("check_async", &PeerHaloComm::check_async)
       .def("set_capturable", &PeerHaloComm::set_capturable)
       .def("peer_buffers", &PeerHaloComm::peer_buffers)
       .def("register_halo_buffers", [](PeerHaloComm& c, const std::vector<uintptr_t>& bufs, int64_t own_off, int64_t row_begin) {
@@ -492,6 +505,7 @@ PYBIND11_MODULE(_C, m) {
         d["dia4"] = i.dia4;
         d["diav"] = i.diav;
         d["halo_hide"] = i.halo_hide;
+        d["halo_pull"] = i.halo_pull;
         d["aligned_fill"] = i.aligned_fill;
         d["p3"] = i.p3;
         d["dia_uniform"] = i.dia_uniform;
@@ -537,6 +551,7 @@ PYBIND11_MODULE(_C, m) {
       d["p3"] = rr.p3;
       d["dia_uniform"] = rr.dia_uniform;
       d["halo_hide"] = rr.halo_hide;
+      d["halo_pull"] = rr.halo_pull;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;
       py::dict ph;

@@ -64,11 +64,24 @@ def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "single"):
     return C.Comm(env.rank, env.world, *ids)
 
 
-def peer_halo(inner, env: DistEnv):
-    """Wrap a communicator so that the halo moves on copy engines (native ``PeerHaloComm``: the
-    ghost rows are pulled from the neighbours' buffers, mapped through IPC handles; the all-reduce
-    stays on ``inner``).  Call :func:`attach_peer_halo` after the solver's ``setup()``."""
-    return native().PeerHaloComm(inner, env.rank, env.world)
+def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False):
+    """Wrap a communicator so that the halo moves without RCCL (native ``PeerHaloComm``: the
+    neighbours' buffers mapped through IPC handles -- pulled by copy engines, or read by the lean
+    passes themselves, PassForm::halo_pull); the all-reduce stays on ``inner`` unless
+    ``ipc_allreduce``: then every rank's mailbox is mapped here (collective) and the all-reduce runs
+    through them (ipc_allreduce.hip) -- real P-rank sums with no RCCL, e.g. P processes on one GPU.
+    Call :func:`attach_peer_halo` after the solver's ``setup()``."""
+    comm = native().PeerHaloComm(inner, env.rank, env.world)
+    if ipc_allreduce:
+        mine = comm.mailbox_handle()
+        allb = [mine]
+        if env.world > 1:
+            if not dist.is_initialized():
+                raise RuntimeError("peer_halo(ipc_allreduce=True) needs torch.distributed initialised")
+            allb = [None] * env.world
+            dist.all_gather_object(allb, mine)
+        comm.attach_mailbox(allb)
+    return comm
 
 
 def attach_peer_halo(comm, env: DistEnv) -> None:

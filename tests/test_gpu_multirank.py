@@ -272,3 +272,67 @@ def test_local_ranks_halo_hide_copy_engine(mcg, problem, n, coef, world):
         assert abs(rp - r1) <= 1e-12 * r1
         np.testing.assert_allclose(outs[hh]["x"], one["x"], rtol=rtol, atol=1e-14 * np.abs(one["x"]).max())
         assert np.linalg.norm(outs[hh]["x"] - one["x"]) <= (1e-11 if coef else 1e-13) * np.linalg.norm(one["x"])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=2048)), ("poisson3d", dict(n=128)),
+                                         ("poisson2d", dict(n=1024, coef=1)), ("poisson3d", dict(n=128, coef=1))])
+def test_local_ranks_in_kernel_halo_bitwise(mcg, world, problem, kw):
+    """the in-kernel halo (halo_pull).  From iteration 2 on the lean carries read
+    their ghost lines / planes straight from the neighbours' rows (LocalComm: the other threads'
+    buffers) and store their own first / last ones write-through, with no halo step -- bit for bit
+    the serial path (halo exchanged before each pass) and the halo-ahead path, over 40 iterations."""
+    spec = mcg.make_problem(problem, rhs="random", **kw)
+    C = mcg.native()
+    outs = {}
+    for tag, hp, ov in (("pull", 1, False), ("serial", 0, False), ("ahead", 0, True), ("pull_ov", -1, True)):
+        o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8, overlap=ov)
+        o.halo_pull = hp
+        outs[tag] = C.run_local_ranks(spec.native(), o, world, 40, True)
+        assert all(q["halo_pull"] == (hp != 0) for q in outs[tag]["ranks"]), (tag, outs[tag]["ranks"])
+        assert all(q["lean_only"] for q in outs[tag]["ranks"]), tag
+    for tag in ("serial", "ahead", "pull_ov"):
+        assert [q["rnorm"] for q in outs[tag]["ranks"]] == [q["rnorm"] for q in outs["pull"]["ranks"]], tag
+        np.testing.assert_array_equal(outs[tag]["x"], outs["pull"]["x"])
+    assert all(abs(q["true_rnorm"] - q["rnorm"]) <= 1e-8 * q["true_rnorm"] for q in outs["pull"]["ranks"])
+
+
+@pytest.mark.parametrize("problem,n", [("poisson2d", 1024), ("poisson3d", 64)])
+def test_local_ranks_in_kernel_halo_converges(mcg, problem, n):
+    """The in-kernel halo to convergence at P = 4 against the CPU oracle (the reference's recurrence)."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    C = mcg.native()
+    o = _opts(mcg, format="sellc8", recurrence=-1, check_every=4)
+    out = C.run_local_ranks(spec.native(), o, 4, 0, True)
+    assert all(q["halo_pull"] for q in out["ranks"])
+    its = {q["iterations"] for q in out["ranks"]}
+    assert len(its) == 1, its
+    cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=1e-7))
+    assert abs(its.pop() - cpu["iterations"]) <= max(2, cpu["iterations"] // 100)
+    np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
+
+
+@pytest.mark.parametrize("problem,n", [("poisson2d", 512), ("poisson3d", 128)])
+def test_null_comm_in_kernel_halo_graph_equals_eager(mcg, problem, n):
+    """A P = 8 rank's share with the in-kernel halo forced on a NullComm (the rank's own first / last
+    line stands in for the neighbours'): the 32-iteration graphs replay the eager pulled passes bit for
+    bit, and a resumed count (graphs start only once pulling) keeps them equal."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    C = mcg.native()
+    xs, infos = [], []
+    for graph in (True, False):
+        o = C.CgOptions(tol=-1.0, maxit=1 << 30, check_every=1 << 30, format="sellc8", recurrence=1)
+        o.use_graph = graph
+        o.halo_pull = 1
+        s = C.Solver(spec.native(), o, 3, 8, C.NullComm(3, 8))
+        s.setup()
+        s.reset()
+        s.run_iterations(5)
+        s.run_iterations(70)
+        s.synchronize()
+        s.finalize()
+        xs.append(s.x_local())
+        infos.append(dict(s.info, **s.result()))
+    assert infos[0]["halo_pull"] and infos[0]["graph_fallbacks"] == 0 and infos[0]["graphs"]
+    assert infos[0]["iterations"] == infos[1]["iterations"] == 75
+    np.testing.assert_array_equal(xs[0], xs[1])

@@ -53,4 +53,35 @@ def test_bench_sdma_halo_rehearsal_on_one_gpu():
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["check"]["ok"] and line["n_gpus"] == 2
-    assert line["config"]["halo_transport"].startswith("sdma")
+    # the lean 2-D carry reads its ghost lines in-kernel from the mapped neighbour (halo_pull auto)
+    assert line["config"]["halo_transport"].startswith("in-kernel")
+
+
+@pytest.mark.parametrize("world,problem,n,pull,coef", [(2, "poisson2d", 1024, -1, 0), (4, "poisson2d", 1024, -1, 0),
+                                                       (2, "poisson2d", 1024, 0, 0), (4, "poisson3d", 128, -1, 0),
+                                                       (2, "poisson2d", 512, -1, 1)])
+def test_ipc_ranks_real_recurrence_matches_one_rank(world, problem, n, pull, coef):
+    """P processes on ONE GPU run the real P-rank recurrence -- the IPC all-reduce
+    (mailboxes mapped through IPC handles, rank-order sums) and the peer-mapped halo (the in-kernel
+    halo, or the copy-engine pulls with halo_pull 0), captured in 32-iteration graphs -- and agree with
+    one rank to <= 1e-13 over 40 iterations."""
+    p = _run([sys.executable, "-u", "bench/ipc_ranks.py", "--world", str(world), "--problem", problem, "--n", str(n),
+              "--halo-pull", str(pull), "--coef", str(coef), "--iters", "40", "--port", str(_port())], timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["ok"], line
+    assert all(r["halo_pull"] == (pull != 0) and r["graphs"] and r["graph_fallbacks"] == 0 for r in line["ranks"]), line
+    assert line["gap_rnorm"] <= 1e-13 and line["true_gap"] <= 1e-8, line
+
+
+def test_bench_ipc_allreduce_rehearsal_is_a_real_solve():
+    """bench.py --rehearse-ranks --allreduce ipc: the P-rank bench on one GPU with the IPC all-reduce is a
+    real solve, so its check requires the recurrence residual to track ||b - A x||."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--rehearse-ranks", "--grid",
+           "1024", "--steps", "64", "--warmup", "8", "--phases", "0", "--watchdog", "60", "--allreduce", "ipc"]
+    p = _run(cmd)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["check"]["ok"] and line["check"]["true_gap_rel"] <= 1e-8, line["check"]
+    assert line["config"]["allreduce"].startswith("ipc") and "real" in line["metric"]
