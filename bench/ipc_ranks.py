@@ -23,14 +23,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def _opts(C, a):
-    o = C.CgOptions(tol=-1.0, maxit=1 << 30, check_every=1 << 30, format="sellc8", recurrence=1)
+    o = C.CgOptions(tol=-1.0, maxit=1 << 30, check_every=1 << 30, format="sellc8", recurrence=a.recurrence)
     o.halo_pull = a.halo_pull
+    o.pipe_rr = a.pipe_rr
     o.use_graph = not a.no_graph
     o.watchdog_seconds = 120.0
     return o
 
 
 def _spec(mcg, a):
+    if a.problem == "scrambled":  # irregular: the all-gather layout, the split pass (single exchanged p)
+        return mcg.make_problem("randspd", rows=a.rows, band=16, density=0.5, scramble=1, rhs="random").native()
     return mcg.make_problem(a.problem, n=a.n, rhs="random", coef=a.coef).native()
 
 
@@ -68,8 +71,11 @@ def rank_main(rank: int, a, port: int, q) -> None:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
-    ap.add_argument("--problem", choices=["poisson2d", "poisson3d"], default="poisson2d")
+    ap.add_argument("--problem", choices=["poisson2d", "poisson3d", "scrambled"], default="poisson2d")
     ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--rows", type=int, default=200000, help="scrambled: global rows")
+    ap.add_argument("--recurrence", type=int, default=1, help="1 single-reduction, 2 pipelined")
+    ap.add_argument("--pipe-rr", type=int, default=0)
     ap.add_argument("--coef", type=int, default=0)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--halo-pull", type=int, default=-1)
@@ -93,6 +99,7 @@ def main() -> int:
             p.join()
     res = sorted(q.get(timeout=5) for _ in procs) if all(p.exitcode == 0 for p in procs) else []
     out = {"world": a.world, "problem": a.problem, "n": a.n, "coef": a.coef, "iters": a.iters,
+           "recurrence": a.recurrence, "pipe_rr": a.pipe_rr,
            "halo_pull_opt": a.halo_pull, "graphs": not a.no_graph, "exitcodes": [p.exitcode for p in procs]}
     ok = bool(res) and all(p.exitcode == 0 for p in procs)
     if ok:

@@ -116,12 +116,14 @@ void DelayComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
     // the all-gather layout's blocks side by side (CopyFan); window halos' small copies in one queue:
     // fanned out over streams they took longer (a P = 8 share of 16384^2: 0.507 vs 0.301 ms an
     // iteration with halo_hide, profiles/r4/fan)
+    // (a receive range longer than the rank's own rows -- the last rank of an all-gather layout, whose
+    // block is short -- copies only as many rows as it owns: the source stays inside its rows)
     std::vector<CopyFan::Job> jobs;
     for (int v = 0; v < nvec; ++v) {
       const int64_t w = widths ? widths[v] : 1;
       for (const HaloRange& h : L.recvs)
         jobs.push_back({ext_vecs[v] + w * L.ext_index(h.gbegin), ext_vecs[v] + w * L.own_off,
-                        (size_t)(w * h.count) * sizeof(double), nullptr, 0});
+                        (size_t)(w * std::min(h.count, L.n_local())) * sizeof(double), nullptr, 0});
     }
     if (L.allgather) {
       fan_->run(stream, jobs);

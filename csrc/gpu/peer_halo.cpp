@@ -232,6 +232,17 @@ bool PeerHaloComm::peer_view(int q, std::vector<double*>& bufs, int64_t& own_off
   return true;
 }
 
+// A single (not parity-alternating) exchanged buffer -- the pipelined pass's w, the split pass's p --
+// is rewritten by its owner's next update before the owner's next exchange, whose wait on the done
+// flags would come too late: the solver calls this first (torn ghost rows otherwise).
+// The readers' done flags of exchange seq_ carry v(seq_); the next exchange waits for the same value.
+void PeerHaloComm::halo_fence(hipStream_t stream) {
+  if (seq_ == 0 || last_readers_.empty()) return;
+  const uint64_t v = 1 + (uint64_t)(seq_ % 2);
+  for (int q : last_readers_)
+    MCG_HIP(hipStreamWaitValue64(stream, flags_ + world_ + q, v, hipStreamWaitValueEq, ~0ull), "peer halo: wait failed");
+}
+
 std::vector<uintptr_t> PeerHaloComm::peer_buffers(int q) const {
   std::vector<uintptr_t> v;
   for (double* p : peer_bufs_.at(q)) v.push_back(reinterpret_cast<uintptr_t>(p));
@@ -265,6 +276,7 @@ void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, 
             "peer halo: wait failed");
     MCG_HIP(hipStreamWriteValue64(stream, peer_flags_[q] + rank_, v, 0), "peer halo: flag write failed");
   }
+  last_readers_ = readers;
   // pull: the owner's rows for my ghost ranges, per vector, once the owner's rows are final
   std::vector<int> idx(nvec);
   for (int k = 0; k < nvec; ++k) {

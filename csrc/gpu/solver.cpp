@@ -368,6 +368,7 @@ void GpuCgSolver::enqueue_iteration_split_(int k) {
   const bool fr = fused_red_;
   CgState* st = st_.get();
   double* pv[1] = {p_[0].get()};
+  if (use_halo_) comm_->halo_fence(s0_);  // U_k rewrites p_k's rows, which readers of exchange k-1 may still pull
   // U_k: x, r_k, p_k of the owned rows
   kern::cg_split_update(x_.get(), r_.get(), Ap_.get(), p_[0].get() + L_.own_off, n, st, opt_.tol, k == 0 ? 1 : 0,
                         k >= 2 ? 1 : 0, 0, partials_.get(), pstride_, g_b_, s0_);
@@ -560,6 +561,7 @@ void GpuCgSolver::enqueue_iteration_pipe_(int k) {
   rc.check = k >= 1 ? 1 : 0;  // the reference never tests r_0
   rc.first = k == 0 ? 1 : 0;
   const int64_t o = L_.own_off;
+  if (use_halo_) comm_->halo_fence(s0_);  // the update rewrites w_, whose rows the readers may still pull
   kern::PipeVectors v{x_.get(), r_.get() + o, w_.get() + o, p_[0].get() + o, Ap_.get() + o, z_.get(), q_.get()};
   kern::cg_pipe_update(v, n, partials_.get(), pstride_, g_b_, st, opt_.tol, s0_, rc);
   const int rr = std::abs(opt_.pipe_rr);

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <limits>
 #include <thread>
+#include <unordered_set>
 
 #include "mcg/check.hpp"
 #include "mcg/trace.hpp"
@@ -195,16 +196,21 @@ void GpuCgSolver::setup() {
       const int64_t unnz = user.nnz();
       // a matrix with a one-byte (value, offset) dictionary streams 1 B per entry on c8 (sellc8): keep it
       bool small_dict = false;
-      if (c8_) {
-        std::vector<std::pair<double, int32_t>> seen;
+      if (c8_) {  // distinct (value bits, offset) pairs in a hash set, stopping at the 257th
+        struct PairHash {
+          size_t operator()(const std::pair<uint64_t, int32_t>& e) const {
+            return (size_t)(e.first * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)e.second);
+          }
+        };
+        std::unordered_set<std::pair<uint64_t, int32_t>, PairHash> seen;
+        seen.reserve(512);
         small_dict = true;
         for (int64_t i = 0; i < n && small_dict; ++i)
           for (int64_t k = user.rowptr[i]; k < user.rowptr[i + 1] && small_dict; ++k) {
-            const std::pair<double, int32_t> e(user.vals[k], (int32_t)(user.cols[k] - (L_.own_off + i)));
-            if (std::find(seen.begin(), seen.end(), e) == seen.end()) {
-              seen.push_back(e);
-              small_dict = seen.size() <= 256;
-            }
+            uint64_t vb = 0;
+            std::memcpy(&vb, &user.vals[k], sizeof(vb));
+            seen.emplace(vb, (int32_t)(user.cols[k] - (L_.own_off + i)));
+            small_dict = seen.size() <= 256;
           }
       }
       user_aligned_ = opt_.form.sell_aligned == 1 ||

@@ -92,6 +92,11 @@ class Communicator {
   virtual bool moves_data() const { return true; }
   // tear down outstanding collectives after a fatal error (watchdog)
   virtual void abort() {}
+  // the caller is about to overwrite, on `stream`, rows it sent in its last halo exchange: wait until
+  // every rank reading them has its copy.  A transport whose exchange returns before its readers have
+  // copied (PeerHaloComm: the readers pull later, on their own streams) waits here; RCCL's send/recv
+  // and LocalComm's copies complete in the exchange's stream order, so they have nothing to wait for
+  virtual void halo_fence(hipStream_t) {}
   // true: halo and all-reduce share one communicator, so the solver must issue them in one stream
   // order (no side-stream halo; CgOptions::overlap is forced off)
   virtual bool serialized() const { return false; }
@@ -231,6 +236,7 @@ class PeerHaloComm final : public Communicator {
   void register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) override;
   bool peer_view(int q, std::vector<double*>& bufs, int64_t& own_off, int64_t& row_begin) override;
   void on_captured(bool kept) override;
+  void halo_fence(hipStream_t stream) override;
   // this rank's IPC handles (flags + registered buffers) as bytes, for an out-of-band all-gather
   std::string local_handles() const;
   // every rank's local_handles(), in rank order: map the peers' buffers (same process: plain pointers)
@@ -262,6 +268,7 @@ class PeerHaloComm final : public Communicator {
   kern::IpcMailboxes mb_;
   bool ipc_ar_ = false;
   long seq_ = 0;
+  std::vector<int> last_readers_;  // the ranks that pull this rank's rows of exchange seq_
   long cap_n_ = 0;  // exchanges recorded by the capture in progress
   // A captured exchange replays the flag values of its capture, which continues the 1/2 alternation
   // only if every graph holds an even number of exchanges (the solver's graphs hold an even number

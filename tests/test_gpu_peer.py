@@ -74,6 +74,21 @@ def test_ipc_ranks_real_recurrence_matches_one_rank(world, problem, n, pull, coe
     assert line["gap_rnorm"] <= 1e-13 and line["true_gap"] <= 1e-8, line
 
 
+@pytest.mark.parametrize("problem,recurrence,pipe_rr", [("poisson2d", 2, 0), ("poisson2d", 2, 10), ("scrambled", 1, 0)])
+def test_ipc_ranks_single_buffer_exchanges(problem, recurrence, pipe_rr):
+    """the copy-engine halo on buffers that are NOT parity-alternating -- the pipelined pass's w
+    (rewritten by the update right after its exchange; with residual replacement also r, p, s) and the
+    split pass's p on the all-gather layout -- across processes, with the IPC all-reduce: the owner's
+    stream waits for its readers' done flags before rewriting (Communicator::halo_fence), so the
+    2-process solve matches one rank."""
+    p = _run([sys.executable, "-u", "bench/ipc_ranks.py", "--world", "2", "--problem", problem, "--n", "512",
+              "--recurrence", str(recurrence), "--pipe-rr", str(pipe_rr), "--iters", "60", "--tol", "1e-11",
+              "--port", str(_port())], timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["ok"] and not any(r["halo_pull"] for r in line["ranks"]), line
+
+
 def test_bench_ipc_allreduce_rehearsal_is_a_real_solve():
     """bench.py --rehearse-ranks --allreduce ipc: the P-rank bench on one GPU with the IPC all-reduce is a
     real solve, so its check requires the recurrence residual to track ||b - A x||."""
