@@ -94,7 +94,7 @@ def parse_args(argv=None):
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="SpMV grid; 0 = auto")
     ap.add_argument("--no-verify", action="store_true", help="skip the true-residual check ||b-Ax|| after the run")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
-                    help="experiment: set a native CgOptions field (e.g. tile_pace=2, placement_tries=1)")
+                    help="experiment: set a native CgOptions field (e.g. halo_pull=0, placement_tries=1)")
     ap.add_argument("--phases", type=int, default=10,
                     help="after the timed region: N more iterations with per-phase hipEvent timing (diagnostic, "
                          "reported under check.phase_us of rank 0 and check.phase_us_max over ranks; 0 = off)")
@@ -107,8 +107,8 @@ def parse_args(argv=None):
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
     ap.add_argument("--halo-transport", default="rccl", choices=["rccl", "sdma"],
                     help="sdma: the halo on copy engines (PeerHaloComm: the neighbours' buffers mapped through IPC, "
-                         "flags by stream memory operations; all-reduce on RCCL) -- CU-free, so halo_hide can "
-                         "run the interior band beside it")
+                         "flags by stream memory operations; all-reduce on RCCL); the lean carries read the mapped "
+                         "rows in-kernel instead (halo_pull)")
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "ipc"],
                     help="ipc: the 32-byte all-reduce through IPC-mapped mailboxes (PeerHaloComm + "
                          "csrc/gpu/ipc_allreduce.hip, no RCCL; implies the peer-mapped halo).  With --rehearse-ranks "
@@ -336,7 +336,7 @@ def _run_rank(args, out_fd) -> int:
                 "format": (("sell64-dia4, uniform-slice patterns" if info.get("lean_only") else "sell64-dia4")
                            if info.get("dia4") else
                            "sell64-diav (each row's own values streamed)" if info.get("diav") else
-                           info["format"] + (", fp32-exact values (8 B/entry)" if info.get("tile_vals32") else "")),
+                           info["format"]),
                 "recurrence": info["recurrence"],
                 "pass": pass_label(info, args.problem),
                 **({"ghosts": ("allgather || own-block SpMV half" if info.get("ag_overlap") else "allgather")
@@ -349,7 +349,7 @@ def _run_rank(args, out_fd) -> int:
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
                 "comm": args.comm,
                 **({"halo_transport": ("in-kernel (the pass reads the IPC-mapped neighbour rows)" if info.get("halo_pull")
-                                       else "sdma (copy engines, IPC)"), "halo_hide": bool(info.get("halo_hide")),
+                                       else "sdma (copy engines, IPC)"),
                     "allreduce": "ipc (mapped mailboxes)" if ipc_ar else "rccl"} if sdma else {}),
                 "launch": route,
                 **({"reserve_cus": opts.reserve_cus} if opts.reserve_cus else {}),

@@ -128,49 +128,21 @@ def recipes(a) -> dict:
             ("csr", 600, bench(f"{c5} --steps 5 --warmup 2 --format csr --set tiles=0")),
         ] + counters("c5_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
           + counters("c5_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"),
-        # tile pacing: counter polls vs step flags, segment size, slack, poll interval (r3_tiles_sweep.sh)
+        # tile segment size (r3_tiles_sweep.sh; the pacing variants were pruned in r5)
         "c5sweep": [
             (tag, 400, bench(f"{c5} --steps 6 --warmup 2 {sets(kv)}"))
-            for tag, kv in (("p2_s19", ["tile_pace=2", "tile_seg_log2=19"]),
-                            ("s18", ["tile_pace=4", "tile_seg_log2=18"]),
-                            ("s17", ["tile_pace=4", "tile_seg_log2=17"]),
-                            ("s19", ["tile_pace=4", "tile_seg_log2=19"]),
-                            ("s18_strict", ["tile_pace=3", "tile_seg_log2=18"]),
-                            ("s18_slack2", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_slack=2"]),
-                            ("s18_sleep2", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_sleep=2"]),
-                            ("s18_sleep4", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_sleep=4"]),
-                            ("s18_lag1", ["tile_pace=4", "tile_seg_log2=18", "tile_pace_lag=1"]),
-                            ("s18_again", ["tile_pace=4", "tile_seg_log2=18"]))
+            for tag, kv in (("s18", ["tile_seg_log2=18"]), ("s17", ["tile_seg_log2=17"]),
+                            ("s19", ["tile_seg_log2=19"]), ("s18_again", ["tile_seg_log2=18"]))
         ],
         # r4: the pacing beside other kernels (fat = RCCL's register footprint) and the collision test
         "useraligned": [
             ("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'aligned'"),
         ],
         "pacecorun": [
-            ("probe", 400, f"{PY} -u bench/pace_corun.py --set tile_pace=4 --set tile_seg_log2=18"),
+            ("probe", 400, f"{PY} -u bench/pace_corun.py --set tile_seg_log2=18"),
             ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'colliding or tiles'"),
         ],
         # r4: next-segment L2 prefetch during the pacing wait
-        "c5pf": [
-            (tag, 400, bench(f"{c5} --steps 6 --warmup 2 {sets(kv)}"))
-            for tag, kv in (("s18_pf", ["tile_pace=4", "tile_seg_log2=18", "tile_prefetch=1"]),
-                            ("s18", ["tile_pace=4", "tile_seg_log2=18"]),
-                            ("s19_pf", ["tile_pace=4", "tile_seg_log2=19", "tile_prefetch=1"]),
-                            ("s17_pf", ["tile_pace=4", "tile_seg_log2=17", "tile_prefetch=1"]),
-                            ("s18_pf_again", ["tile_pace=4", "tile_seg_log2=18", "tile_prefetch=1"]))
-        ],
-        # r4: tiles with fp32-exact values (8 B / entry) vs fp64 storage, the 101 GB share and the ~200 GB one
-        "c5v32": [
-            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'tiles'"),
-            ("v32", 400, bench(f"{c5} --steps 6 --warmup 2")),
-            ("v64", 400, bench(f"{c5} --steps 6 --warmup 2 --set tile_vals32=0")),
-            ("v32_priced", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330")),
-            ("v32_again", 400, bench(f"{c5} --steps 6 --warmup 2")),
-        ] + counters("v32_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
-          + counters("v32_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"),
-        # r4: the all-gather priced (DelayComm: 10 us all-reduce, 2330 us all-gather ~ 700 MB over xGMI) with
-        # the own-segment half swept while it is in flight (ag_overlap) vs after it; thin = a CU-light
-        # transport (copy engines), fat = RCCL's register footprint
         "c5ag": [
             ("ag_thin", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330")),
             ("noag_thin", 400, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 --set ag_overlap=0")),
@@ -187,10 +159,8 @@ def recipes(a) -> dict:
         ],
         # config 5 at ~200 GB per GPU and with the all-gather priced (DelayComm)
         "c5big": [
-            ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2 "
-                                    f"{sets(['tile_pace=4', 'tile_seg_log2=18'])}")),
-            ("share101_priced", 600, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330 "
-                                           f"{sets(['tile_pace=4', 'tile_seg_log2=18'])}")),
+            ("share200", 900, bench(f"{C5SCR.replace('--band 410', '--band 820')} --steps 4 --warmup 1 --phases 2")),
+            ("share101_priced", 600, bench(f"{c5} --steps 6 --warmup 2 --delay-comm 10,2330")),
         ],
         # config 5's other family: the wide multi-diagonal random SPD (SELL-64/aligned, all-gather overlap)
         "config5_wide": [
@@ -231,16 +201,12 @@ def recipes(a) -> dict:
                                  f"--graphs 1 --overlaps 1 --fat 1 --delays 10 --halo-us 30 --iters 640 "
                                  f"--reserve-cus 0,32 --halo-ahead 0,1") for gg in (16384, 4096)
         ],
-        # r4: the 3-D plane carry's runs per job column (carry3_runs) with CUs withheld, and a
+        # r4: the 3-D plane carry's runs per job column (kern::carry3_runs) with CUs withheld, and a
         # non-power-of-two grid whose jobs do not fill the blocks
         "runs3": [
             (f"p{g}_rc{rc}", 300, bench(f"--problem poisson3d --grid {g} --steps 64 --warmup 8 --phases 0 "
                                         f"--set reserve_cus={rc}"))
             for g in (512, 384) for rc in (0, 32)
-        ] + [
-            (f"p{g}_rc{rc}_r3rule", 300, bench(f"--problem poisson3d --grid {g} --steps 64 --warmup 8 --phases 0 "
-                                               f"--set reserve_cus={rc} --set carry3_runs=0"))
-            for g, rc in ((512, 32), (384, 0))
         ],
         # the distributed path at headline sizes as P in-process ranks on one GPU (r3_rehearse_lean.sh)
         "rehearse": [
@@ -256,77 +222,17 @@ def recipes(a) -> dict:
                               ("sim8", "--sim-world 8 --sim-rank 3 --steps 400 --warmup 40"))
         ],
         # 3-D block height (r3_kw_ab.sh) and setup placement probe depth (r3_placement_tries.sh)
-        "kwab": [(f"kw{kw}_{rep}", 300, bench(f"--problem poisson3d --grid 512 --steps 64 --warmup 8 "
-                                              f"--set carry3_kw={kw}")) for rep in (1, 2) for kw in (16, 8, 4)],
         "placement": [(f"t{t}_{rep}", 150, bench(f"--phases 0 --set placement_tries={t}"))
                       for rep in (1, 2) for t in (1, 3, 6)],
         # r4: 4096^2 (BASELINE config 2) lean-pass geometry: prefetch depth x blocks per CU
-        "p4096": [
-            (f"d{d}_b{b}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify "
-                                      f"--set lean_depth={d} --set lean_bpc={b}"))
-            for d in (3, 4, 6) for b in (2, 4, 8)
-        ] + [("auto_again", 200, bench("--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify"))],
-        # r4: packed slice edges (lean_depth 13: depth 3 at 5 waves / SIMD, 14: depth 4 at 4) at 4096^2
-        # and 16384^2 against the default lean kernels, interleaved
-        "edge": [
-            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'packed_edges'"),
-        ] + [
-            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify {kv}"))
-            for rep in (1, 2)
-            for tag, kv in (("auto", ""), ("e13", "--set lean_depth=13 --set lean_bpc=5"),
-                            ("e14", "--set lean_depth=14 --set lean_bpc=4"), ("d3b5", "--set lean_bpc=5"))
-        ] + [
-            (f"g16384_{tag}", 200, bench(f"--phases 0 --no-verify {kv}"))
-            for tag, kv in (("auto", ""), ("e13", "--set lean_depth=13 --set lean_bpc=5"),
-                            ("e14", "--set lean_depth=14"))
-        ] + stats("edge_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=13 --set lean_bpc=5"),
-        # r4: even / odd lean passes on their own geometry (lean_*_odd): packed edges at 5 waves / SIMD for
-        # the even passes, the odd ones (x stream paired in) at depth 4 or the default depth 3, 4 waves
-        "edge2": [
-            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'packed_edges or own_grid'"),
-        ] + [
-            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 --no-verify {kv}"))
-            for rep in (1, 2)
-            for tag, kv in (("auto", ""), ("e14", "--set lean_depth=14"),
-                            ("mix14", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=14 --set lean_bpc_odd=4"),
-                            ("mix3", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=3 --set lean_bpc_odd=4"),
-                            ("mix4", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=4 --set lean_bpc_odd=3"))
-        ] + stats("e14_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=14")
-          + stats("auto_stats_4096", "--grid 4096 --steps 640 --warmup 64")
-          + stats("mix14_stats_4096", "--grid 4096 --steps 640 --warmup 64 --set lean_depth=13 --set lean_bpc=5 "
-                                      "--set lean_depth_odd=14 --set lean_bpc_odd=4"),
-        # r4: the auto mixed geometry at 4096^2 (packed edges, per-parity grids) vs the r3 lean default,
-        # interleaved repeats on one box
         "mix": [
-            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'packed_edges or own_grid or lean_mix'"),
+            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_solver.py -k 'lean_mix'"),
         ] + [
             (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
-            for rep in (1, 2, 3) for tag, kv in (("mix", ""), ("r3", "--set lean_depth=3"))
+            for rep in (1, 2, 3) for tag, kv in (("mix", ""), ("r3", "--set lean_packed=0"))
         ] + [("g16384", 200, bench("--phases 0"))],
         # a P = 8 rank's share of 16384^2 (2048 lines, 8 blocks per CU: the driver's N = 8 scaling
         # point) and of 4096^2 (512 lines) with the packed-edge geometry
-        "simmix": [
-            (f"{tag}_{rep}", 200, bench(f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 {kv}"))
-            for rep in (1, 2)
-            for tag, kv in (("auto", ""), ("m10", "--set lean_depth=13 --set lean_bpc=10 --set lean_depth_odd=14 "
-                                                  "--set lean_bpc_odd=8"),
-                            ("m5", "--set lean_depth=13 --set lean_bpc=5 --set lean_depth_odd=14 --set lean_bpc_odd=4"),
-                            ("e14", "--set lean_depth=14"))
-        ],
-        # r4: tile row blocks of 960 rows at 5 workgroups per CU vs 1024 at 4, interleaved (config 5)
-        "c5tb": [
-            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'tiles'"),
-        ] + [
-            (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
-            for rep in (1, 2) for tag, kv in (("tb1024", ""), ("tb960", "--set tile_rows=960"))
-        ],
-        "c5tu": [
-            ("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k 'tiles_same_recurrence or tiles_960'"),
-        ] + [
-            (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
-            for rep in (1, 2) for tag, kv in (("tu8", ""), ("tu12", "--set tile_unroll=12"))
-        ],
-        # r4: the lean / generic split on a user matrix with a few changed rows
         "lsplit": [
             ("pytest", 300, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean'"),
         ],
@@ -345,22 +251,6 @@ def recipes(a) -> dict:
                                                 "--arms generic")),
             ("generic_md", 60, f"{PY} bench/prof_summary.py --stats {OUT}/lsplit_gen --title 'lean_split=0, 16384^2'"),
         ],
-        "mix2": [
-            (f"{tag}_{rep}", 200, bench(f"--grid 4096 --steps 2000 --warmup 100 --phases 0 {kv}"))
-            for rep in (1, 2)
-            for tag, kv in (("mix", ""), ("r3", "--set lean_depth=3"))
-        ],
-        # r4: tile values fp32 vs fp64 storage, interleaved, with DRAM / L2 counters of each
-        "c5ab": [
-            (f"{tag}_{rep}", 400, bench(f"{c5} --steps 6 --warmup 2 {kv}"))
-            for rep in (1, 2) for tag, kv in (("v64", ""), ("v32", "--set tile_vals32=1"))
-        ] + counters("v64_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
-          + counters("v64_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE")
-          + counters("v32_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1 --set tile_vals32=1",
-                     "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE")
-          + counters("v64_ta", "k_tiles", f"{C5SCR} --steps 2 --warmup 1",
-                     "TCC_EA0_RDREQ_sum TCC_REQ_sum GRBM_GUI_ACTIVE"),
-        # r4: stream memory operations (write / wait value) around a NoCU copy, eager and captured
         "streamop": [
             ("probe", 240, f"{PY} -c 'import torch, json, cuda_mpi_parallel_amd as m; torch.cuda.init(); "
                           f"print(json.dumps(dict(m.native().kernels.streamop_probe())))'"),
@@ -375,37 +265,6 @@ def recipes(a) -> dict:
                                    f"--master-addr 127.0.0.1 --master-port {29600 + w} bench.py --gpus {w} "
                                    f"--rehearse-ranks --steps 200 --warmup 20 --phases 0 --halo-transport {t}")
             for w in (2, 4) for t in ("rccl", "sdma")
-        ],
-        # r4: CU-free halo (copy engines) hidden behind the interior band of the pass (halo_hide), at
-        # P = 8 shares with a 10 us all-reduce; the halo as copy-engine traffic or as an RCCL-like spin
-        "hide": [
-            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_multirank.py -k 'halo_hide'"),
-        ] + [
-            (f"{g}_{tag}", 200, bench(f"{'--grid ' + str(g) if g != 512 else '--problem poisson3d --grid 512'} "
-                                      f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 "
-                                      f"--comm dual --delay-comm {dc} {hh}"))
-            for g in (16384, 4096)
-            for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
-                                ("spin20_ahead", "10,20", ""), ("null", "0,0", ""))
-        ],
-        # the same shares with eager launches (copy-engine copies captured in hipGraphs replay slowly)
-        "hide_eager": [
-            (f"{g}_{tag}", 200, bench(f"{'--grid ' + str(g) if g != 512 else '--problem poisson3d --grid 512'} "
-                                      f"--sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 --no-graph "
-                                      f"--comm dual --delay-comm {dc} {hh}"))
-            for g in (16384, 4096)
-            for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
-                                ("spin20_ahead", "10,20", ""), ("null", "0,0", ""))
-        ],
-        "fan": [
-            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_peer.py tests/test_gpu_multirank.py -k 'peer or halo_hide'"),
-            ("check4", 180, f"{PY} -u bench/peer_halo_check.py --world 4 --n 512 --rounds 6"),
-        ] + [
-            (f"{g}_{tag}_{gr}", 200, bench(f"--grid {g} --sim-world 8 --sim-rank 3 --steps 400 --warmup 40 --phases 0 "
-                                            f"--comm dual --delay-comm {dc} {hh} {'--no-graph' if gr == 'eager' else ''}"))
-            for g in (16384, 4096) for gr in ("graph", "eager")
-            for tag, dc, hh in (("copy_hide", "10,0,copy", "--set halo_hide=1"), ("copy_ahead", "10,0,copy", ""),
-                                ("null", "0,0", ""))
         ],
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
@@ -422,8 +281,6 @@ def recipes(a) -> dict:
             ("b16384_generic", 300, bench("--coef 1 --steps 50 --warmup 5 --phases 0 --set carry_vc=0")),
             ("b4096", 300, bench("--coef 1 --grid 4096 --steps 1000 --warmup 100 --phases 0")),
             ("b512", 300, bench("--coef 1 --problem poisson3d --grid 512 --steps 60 --warmup 6 --phases 0")),
-            ("b512_kw4", 300, bench("--coef 1 --problem poisson3d --grid 512 --steps 60 --warmup 6 --phases 0 "
-                                    "--set carry3_kw=4")),
             ("b512_generic", 300, bench("--coef 1 --problem poisson3d --grid 512 --steps 30 --warmup 3 --phases 0 "
                                         "--set carry_vc=0")),
         ] + counters("vc_dram", "k_cg_carry_ar", "--coef 1 --steps 8 --warmup 2")
@@ -432,8 +289,7 @@ def recipes(a) -> dict:
         "sizes3": [
             (f"n{n}", 400, bench(f"--problem poisson3d --grid {n} --steps {st} --warmup 4 --phases 0 --no-verify"))
             for n, st in ((512, 60), (640, 40), (768, 30), (800, 30), (832, 20), (1024, 12))
-        ] + [("n832_kw8", 400, bench("--problem poisson3d --grid 832 --steps 20 --warmup 4 --phases 0 --no-verify "
-                                     "--set carry3_kw=8"))],
+        ],
         # r4: ranks past 2^29 rows on the lean carries (BIG kernels)
         "large": [
             ("pytest", 900, f"{PY} -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_large.py"),

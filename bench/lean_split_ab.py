@@ -7,7 +7,6 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
 
   uniform   the unperturbed Laplacian (every run lean; the ceiling)
   generic   the perturbed matrix, lean_split = 0 (the pre-split dispatch)
-  seq       the perturbed matrix, lean_split = 1, the generic launch after the lean one
   side      the perturbed matrix, lean_split = 1, the generic launch on a side stream beside it
 
 Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
@@ -38,7 +37,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--reps", type=int, default=1)
-    ap.add_argument("--arms", default="uniform,generic,seq,side", help="comma list of arms to run")
+    ap.add_argument("--arms", default="uniform,generic,side", help="comma list of arms to run")
     a = ap.parse_args()
     import numpy as np
 
@@ -51,7 +50,6 @@ def main() -> int:
     spots = rng.integers(0, a.n * a.n, a.spots)
     out = {"n": a.n, "spots": a.spots, "steps": a.steps, "its": {}, "info": {}}
     arms = [("uniform", {})] + [(f"generic_{i}", {"lean_split": 0}) for i in range(a.reps)]
-    arms += [(f"seq_{i}", {"lean_split": 1, "lean_split_side": 0}) for i in range(a.reps)]
     arms += [(f"side_{i}", {"lean_split": 1}) for i in range(a.reps)]
     want = set(a.arms.split(","))
     arms = [(nm, kw) for nm, kw in arms if nm.split("_")[0] in want]

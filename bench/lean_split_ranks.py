@@ -1,6 +1,5 @@
-"""lean_split at P LocalComm ranks (forced, lean_split = 2) against the generic pass: relative rnorm
-gap after a fixed iteration count, with the generic launch beside (side 1) or after (side 0) the lean
-one.  One JSON line per arm.
+"""lean_split at P LocalComm ranks (forced, lean_split = 1) against the generic pass: relative rnorm
+gap after a fixed iteration count, with and without the halo overlap.  One JSON line per arm.
     python bench/lean_split_ranks.py [--n 2048] [--world 4] [--iters 40]
 """
 import argparse
@@ -31,17 +30,15 @@ A.setdiag(d)
 p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
 C = mcg.native()
 base = None
-for w, ls in ((1, 0), (1, 1), (2, 0), (2, 2)):
+for w, ls in ((1, 0), (1, 1), (2, 0), (2, 1)):
     o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
     o.lean_split = ls
     out = C.run_local_ranks(p.native(), o, w, a.iters, True)
     print(json.dumps({"arm": f"P{w}_ls{ls}", "rnorm": out["ranks"][0]["rnorm"],
                       "split": [rk["lean_split"] for rk in out["ranks"]]}), flush=True)
-for tag, ls, side, ov in (("generic", 0, 1, True), ("side", 2, 1, True), ("seq", 2, 0, True), ("side_noov", 2, 1, False),
-                          ("generic_noov", 0, 1, False)):
+for tag, ls, ov in (("generic", 0, True), ("split", 1, True), ("split_noov", 1, False), ("generic_noov", 0, False)):
     o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
     o.lean_split = ls
-    o.lean_split_side = side
     o.overlap = ov
     out = C.run_local_ranks(p.native(), o, a.world, a.iters, True)
     r = out["ranks"][0]["rnorm"]

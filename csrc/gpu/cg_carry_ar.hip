@@ -228,32 +228,18 @@ __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat,
 }
 
 // The 2-D carry's job decomposition: job -> (slice column, run of lines [l0, l1)) for a launch of nw
-// waves over nl lines of ss slices (TileRanges::band: the whole rank, the interior band, or the
-// band_h lines at each end).  Returns the number of jobs.
-__host__ __device__ __forceinline__ int64_t carry_jobs(int64_t nw, int64_t ss, int64_t nl, int band, int64_t h,
-                                                       int64_t& runs, int64_t& chunk) {
-  if (band == 2) {
-    runs = 2;
-    chunk = h;
-    return 2 * ss;
-  }
-  const int64_t lines = band == 1 ? nl - 2 * h : nl;
+// waves over nl lines of ss slices.  Returns the number of jobs.
+__host__ __device__ __forceinline__ int64_t carry_jobs(int64_t nw, int64_t ss, int64_t nl, int64_t& runs,
+                                                       int64_t& chunk) {
   runs = nw > ss ? nw / ss : 1;
-  chunk = (lines + runs - 1) / runs;
+  chunk = (nl + runs - 1) / runs;
   return ss * runs;
 }
-__host__ __device__ __forceinline__ void carry_run(int64_t job, int64_t ss, int64_t nl, int band, int64_t h,
-                                                   int64_t chunk, int64_t& col, int64_t& l0, int64_t& l1) {
+__host__ __device__ __forceinline__ void carry_run(int64_t job, int64_t ss, int64_t nl, int64_t chunk, int64_t& col,
+                                                   int64_t& l0, int64_t& l1) {
   col = job % ss;
-  const int64_t r = job / ss;
-  if (band == 2) {
-    l0 = r == 0 ? 0 : nl - h;
-    l1 = l0 + h;
-    return;
-  }
-  const int64_t lo = band == 1 ? h : 0, hi = band == 1 ? nl - h : nl;
-  l0 = lo + r * chunk;
-  l1 = l0 + chunk < hi ? l0 + chunk : hi;
+  l0 = (job / ss) * chunk;
+  l1 = l0 + chunk < nl ? l0 + chunk : nl;
 }
 
 // per-slice metadata for the carry's codes loads: first slot / 64 (28 bits) | width << 28
@@ -318,7 +304,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t gw = lb * kWaves + wv;
   int64_t runs, chunk;
-  const int64_t njobs = carry_jobs(nw, SS, nl, tr.band, tr.band_h, runs, chunk);
+  const int64_t njobs = carry_jobs(nw, SS, nl, runs, chunk);
   const int32_t ext32 = (int32_t)v.ext_len;
   constexpr bool ntl = false;  // plain loads (non-temporal measured slower: 281 vs 302 it/s 2-D)
   const double* __restrict__ eo = v.ape_old;
@@ -380,7 +366,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   };
   for (int64_t job = gw; job < njobs; job += nw) {
     int64_t col, l0, l1;
-    carry_run(job, SS, nl, tr.band, tr.band_h, chunk, col, l0, l1);
+    carry_run(job, SS, nl, chunk, col, l0, l1);
     if (l0 >= l1) continue;
     const int64_t sl0 = l0 * SS + col;
     const int32_t e0 = (int32_t)(own + sl0 * 64);
@@ -2179,12 +2165,12 @@ __global__ __launch_bounds__(256) void k_dia_runs(uint64_t* __restrict__ dpat, i
 // kw = 0, one wave per job; k_cg_carry_ar3: kw waves per job, their slice columns)
 __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
                                                     int64_t ext_len, int64_t grid, int kw, int64_t ln,
-                                                    int band, int64_t band_h, int runs3,
+                                                    int runs3,
                                                     unsigned long long* __restrict__ fails) {
   const int64_t waves = kw > 0 ? kw : 1;
   int64_t jobs, runs, chunk;
   if (kw == 0) {
-    jobs = carry_jobs(grid * kWaves, ss, nl, band, band_h, runs, chunk);
+    jobs = carry_jobs(grid * kWaves, ss, nl, runs, chunk);
   } else {
     const int64_t jpr = (ln / kw) * (ln / 64);
     runs = runs3 > 0 ? runs3 : (grid > jpr ? grid / jpr : 1);
@@ -2196,7 +2182,7 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
     const int64_t job = t / waves, wv = t % waves;
     int64_t col, l0, l1;
     if (kw == 0) {
-      carry_run(job, ss, nl, band, band_h, chunk, col, l0, l1);
+      carry_run(job, ss, nl, chunk, col, l0, l1);
     } else {
       const int64_t jpr = (ln / kw) * (ln / 64), G = ln / 64, q = job % jpr;
       col = ((q / G) * kw + wv) * G + q % G;
@@ -2229,18 +2215,18 @@ int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk) {
 }
 
 void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk) {
-  (void)carry_jobs(nw, ss, nl, 0, 0, runs, chunk);
+  (void)carry_jobs(nw, ss, nl, runs, chunk);
 }
 
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream, int band, int band_h, int runs3) {
+                            int32_t ln, hipStream_t stream, int runs3) {
   MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && (kw == 0 || (ln % 64 == 0 && ln % kw == 0)),
             "lean check: bad launch geometry");
   unsigned long long* f = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&f), sizeof(unsigned long long), stream), "device malloc failed(lean)");
   MCG_HIP(hipMemsetAsync(f, 0, sizeof(unsigned long long), stream), "device memset failed");
   hipLaunchKernelGGL(k_lean_check, dim3(64), dim3(256), 0, stream, dpat, ss, nl, ext_len, (int64_t)grid, kw,
-                     (int64_t)ln, band, (int64_t)band_h, runs3, f);
+                     (int64_t)ln, runs3, f);
   MCG_HIP(hipGetLastError(), "kernel launch failed(lean check)");
   unsigned long long h = 0;
   MCG_HIP(hipMemcpyAsync(&h, f, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
@@ -2365,8 +2351,6 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   if (tr.ntiles == 0 || grid == 0) return;
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0,
             "Ap-recomputing carry: one launch over the rank's whole grid lines");
-  MCG_CHECK(tr.band == 0 || (!final_mode && lean && tr.band_h >= 3 && 2 * tr.band_h + 3 <= tr.nt0 / tr.strip),
-            "Ap-recomputing carry: a line band needs the lean kernels and >= 3 lines per band");
   MCG_CHECK((cm == 2 || cm == 4 || cm == 5) && param >= 4 && param <= 5 && (cm == 5 || S.dict != nullptr),
             "Ap-recomputing carry: SELL-64/c8, /c4, /dia4 or /diav rows of at most 5 entries");
   MCG_CHECK(cm != 4 || (S.dia4 != nullptr && S.dvals != nullptr), "Ap-recomputing carry: dia4 codes missing");
@@ -2405,24 +2389,17 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
       hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
                          tr, partials, pstride, st, tol, first, check, rc);                                    \
   } while (0)
-#define MCG_LWD(QD, PAIR, W)                                                                                   \
-  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, tr, \
-                     partials, pstride, st, tol, first, check, rc)
 #define MCG_LWE(QD, PAIR, W)                                                                                   \
   hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true>), dim3(grid), dim3(kBS), 0, stream, S, v, \
                      own_off, tr, partials, pstride, st, tol, first, check, rc)
-    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4; measured and dropped: QD 5 at 4
-    // for the odd passes, the same rate, and QD 3 at 6 for the even ones, which spills in the loop:
-    // 4096^2 7200 vs 9470 it/s, profiles/r4/mix2)
+    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4, the setup's auto_mix_ for the
+    // 4-blocks-per-CU grids; measured and dropped: QD 5 at 4 for the odd passes, the same rate, and QD
+    // 3 at 6 for the even ones, which spills in the loop: 4096^2 7200 vs 9470 it/s, profiles/r4/mix2;
+    // r5 also dropped depth 2, 4 (3 waves per SIMD) and 6 (2): profiles/r3/lean, r4/mix)
     if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
     else if (depth == 14 && !big) { if (pair) MCG_LWE(4, true, 4); else MCG_LWE(4, false, 4); }
-    // deeper prefetch (lean_depth 4 / 6: fewer waves per SIMD, more lines in flight per wave; small grids)
-    else if (depth >= 6 && depth < 13 && !big) { if (pair) MCG_LWD(6, true, 2); else MCG_LWD(6, false, 2); }
-    else if (depth == 4 && !big) { if (pair) MCG_LWD(4, true, 3); else MCG_LWD(4, false, 3); }
-    else if (depth >= 3) { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
-    else { if (pair) MCG_LW(2, true); else MCG_LW(2, false); }
+    else { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
 #undef MCG_LWE
-#undef MCG_LWD
 #undef MCG_LW
     MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
     return;
@@ -2479,15 +2456,14 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
                   int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc, bool p3,
                   bool lean) {
   if (tr.ntiles == 0 || grid == 0) return;
-  MCG_CHECK(tr.band == 0, "3-D plane carry: no line bands");
   MCG_CHECK(tr.strip > 0 && tr.nt0 == tr.ntiles && tr.nt0 % tr.strip == 0 && tr.b0 == 0 && ln % 64 == 0 &&
-                (int64_t)ln * ln == (int64_t)tr.strip * 64 && (kw == 4 || kw == 8 || kw == 16) && ln % kw == 0,
-            "3-D Ap-recomputing carry: one launch over the rank's whole planes, N a multiple of 64 and of the block");
+                (int64_t)ln * ln == (int64_t)tr.strip * 64 && kw == (S.cvt != nullptr ? 8 : 16) && ln % kw == 0,
+            "3-D Ap-recomputing carry: one launch over the rank's whole planes, N a multiple of 64, blocks of 16 waves (diav: 8)");
   const bool vc = S.cvt != nullptr;  // SELL-64/diav 3-D
   MCG_CHECK(vc || (S.dia4 != nullptr && S.dvals != nullptr), "3-D Ap-recomputing carry: dia4 codes missing");
-  MCG_CHECK(!vc || (S.cvd && S.cve && S.cvs && (kw == 4 || kw == 8) && v.ext_len < ((int64_t)1 << 29) &&
+  MCG_CHECK(!vc || (S.cvd && S.cve && S.cvs && v.ext_len < ((int64_t)1 << 29) &&
                     (tr.nt0 * 64 + tr.strip * 64) < ((int64_t)1 << 29)),
-            "3-D diav carry: 4 / 8 waves per block, ranks below 2^29 rows");
+            "3-D diav carry: 8 waves per block, ranks below 2^29 rows");
   MCG_CHECK(v.ap_old != nullptr && v.ap_new != nullptr && v.r_old && v.p_old && v.r_new && v.p_new,
             "3-D Ap-recomputing carry: vectors missing");
   MCG_CHECK(rc.ngroups == 0 || (!final_mode && rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2),
@@ -2509,11 +2485,7 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
 #define MCG_A3V(PAIR, KW, P3, LEAN)                                                                            \
   hipLaunchKernelGGL((k_cg_carry_ar3<2, PAIR, KW, P3, LEAN, false, true>), dim3(grid), dim3(64 * KW), 0, stream, \
                      S, v, own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
-#define MCG_A3VK(PAIR, P3, LEAN)                     \
-  do {                                               \
-    if (kw == 4) MCG_A3V(PAIR, 4, P3, LEAN);         \
-    else MCG_A3V(PAIR, 8, P3, LEAN);                 \
-  } while (0)
+#define MCG_A3VK(PAIR, P3, LEAN) MCG_A3V(PAIR, 8, P3, LEAN)
 #define MCG_A3VP(PAIR)                                          \
   do {                                                          \
     if (p3 && !first && lean) MCG_A3VK(PAIR, true, true);       \
@@ -2539,12 +2511,7 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
     else if (p3 && !first) MCG_A3(QD, PAIR, KW, true);                \
     else MCG_A3(QD, PAIR, KW, false);                                 \
   } while (0)
-#define MCG_A3K(QD, PAIR)                       \
-  do {                                          \
-    if (kw == 4) MCG_A3P(QD, PAIR, 4);          \
-    else if (kw == 8) MCG_A3P(QD, PAIR, 8);     \
-    else MCG_A3P(QD, PAIR, 16);                 \
-  } while (0)
+#define MCG_A3K(QD, PAIR) MCG_A3P(QD, PAIR, 16)
   if (qd == 2) { if (pair) MCG_A3K(2, true); else MCG_A3K(2, false); }
   else { if (pair) MCG_A3K(3, true); else MCG_A3K(3, false); }
 #undef MCG_A3K

@@ -5,14 +5,13 @@
 // served at ~55 G requests/s whether p sits in the 256 MiB Infinity Cache or in HBM (the
 // reference's cuSPARSE CSR SpMV, CUDACG.cu:288, has the same access pattern).  Gathers that hit
 // the L2 run 4-5x faster (bench/gather_probe.hip, profiles/r3_gather_probe.md).  So the columns
-// are cut into segments of S = 2^seg_shift doubles (default 2^19 = 4 MiB, one XCD's L2; CgOptions
-// tile_seg_log2), every wave owns kTileB = 1024 rows (tile_rows = 960: 5 workgroups per CU)
-// (their running sums live in LDS), and ALL waves sweep the segments in the same order: while the
-// chip works on segment g, the XCDs' L2s hold p[g S, (g + 1) S) and the gathers hit.
+// are cut into segments of S = 2^seg_shift doubles (default 2^18 = 2 MiB, half an XCD's L2;
+// PassForm::tile_seg_log2), every wave owns kTileB = 1024 rows (their running sums live in LDS), and
+// ALL waves sweep the segments in the same order: while the chip works on segment g, the XCDs' L2s
+// hold p[g S, (g + 1) S) and the gathers hit.
 //
-// Storage (12 B per nonzero, like CSR; 8 B when every value is exactly an fp32, tile_vals32): tile
-// (b, g) = the nonzeros of row block b whose column is in segment g, a flat list of (row in block <<
-// 22 | column in segment) and the value;
+// Storage (12 B per nonzero, like CSR): tile (b, g) = the nonzeros of row block b whose column is in
+// segment g, a flat list of (row in block << 22 | column in segment) and the value;
 // tptr[b * G + g] .. tptr[b * G + g + 1].  A wave spreads its tile over its 64 lanes and adds every
 // product into the row's LDS slot (ds_add_f64); the wave owns those slots, so no other wave's adds
 // interleave with its own, batch after batch in program order.  Inside ONE batch two lanes can hold
@@ -25,10 +24,12 @@
 // ragged tile end is enough), the L2 then holds none of the segments in flight and the hit rate
 // falls from ~96 % to ~20 % (TCC counters, profiles/r3_gather_probe.md).  After each segment a
 // workgroup therefore adds to its group's arrival counter (group = blockIdx % 8, i.e. the XCD
-// under round-robin dispatch) and waits until the group has finished that segment (tile_pace 1:
-// every workgroup; 2, the default: all but 1/8 of them, so stragglers do not stall the rest).  The
-// wait is bounded (kPaceSpins polls): it paces, it never decides correctness, so a workgroup that
-// is not co-resident only costs time.
+// under round-robin dispatch) and waits until all but 1/8 of the group's workgroups have finished
+// that segment (stragglers do not stall the rest).  The wait is bounded (kPaceSpins polls): it
+// paces, it never decides correctness, so a workgroup that is not co-resident only costs time.
+// (r4 also measured, and r5 deleted: 960-row blocks for 5 workgroups per CU, 12 entries per lane in
+// flight, fp32 storage of exact values, a prefetch of the next segment, counter polling and waiting
+// for every workgroup -- each slower on config 5, profiles/r4/c5tb, c5v32, c5.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,76 +48,49 @@ namespace {
 constexpr int kTU = 8;                // entries per lane in flight (software-pipelined: the next batch's
                                       // indices / values load while this batch gathers)
 constexpr int kPaceSpins = 4000;      // ~1 ms of polling at most per segment step
+constexpr int kPaceSleep = 8;         // s_sleep units (64 clocks) between two polls of a waiting workgroup
 constexpr uint32_t kColMask = (1u << 22) - 1;
 
 // `live` (thread 0's, per workgroup): cleared after the first wait that times out -- the group is not
 // co-resident (another kernel holds CUs, or several ranks share the GPU), so this workgroup stops
 // waiting for the rest of the launch instead of paying the cap at every segment.
 //
-// Two ways to wait (TilesDev::pace_flag).  Counter polls: every waiter polls the group's arrival
-// counter.  Its line lives at the memory side (an atomic drops it from the L2), so ~128 pollers per
-// group keep one word busy and the arrivals queue behind the polls.  Step flags: the arrival whose
-// add completes step s (the counter's return value says so: the counter passes every integer once)
-// raises the group's step flag to s + 1 in 8 replicas on lines of their own; the waiters poll one
-// replica each with `sc1` loads, which the XCD's L2 serves until the flag changes.
-//
-// Prefetch (TilesDev::prefetch): before it waits, each workgroup touches its share of the NEXT
-// segment's lines (one double per 128-B line; the group's workgroups split the segment), so the
-// segment is in the XCD's L2 when the group starts it instead of every wave's first gathers
-// missing together.  The loaded values feed `pf`, which the kernel consumes once at its end.
-__device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live, const double* nxt, int64_t nlen,
-                                          double& pf) {
+// Step flags: the arrival whose add completes step s (the counter's return value says so: the counter
+// passes every integer once) raises the group's step flag to s + 1 in 8 replicas on lines of their
+// own; the waiters poll one replica each, which the XCD's L2 serves until the flag changes (polling
+// the arrival counter itself, whose line every arrival writes, queued the arrivals behind the polls:
+// 14.3 vs 17.5 it/s, profiles/r4/c5).
+__device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live) {
   __syncthreads();
-  if (nxt != nullptr && T.pace != nullptr) {
-    const int grp = blockIdx.x & 7;
-    const int64_t nwg = (gridDim.x - grp + 7) >> 3, wi = blockIdx.x >> 3;
-    const int64_t lines = (nlen + 15) >> 4, per = (lines + nwg - 1) / nwg;
-    const int64_t l0 = wi * per, l1 = l0 + per < lines ? l0 + per : lines;
-    for (int64_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) pf += nxt[l << 4];
-  }
   if (threadIdx.x == 0 && T.pace != nullptr && *live) {
     const int grp = blockIdx.x & 7;
     const unsigned nwg = (gridDim.x - grp + 7) >> 3;
-    const unsigned slack = (nwg * (unsigned)T.pace_slack8) >> 3;
+    const unsigned slack = nwg >> 3;  // all but 1/8 of the group
     unsigned* c = T.pace + grp * 64;  // one 256-B block per group
     const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // wait until the group finished segment step - lag (slack > 0: all but slack of its workgroups)
-    const int need = step + 1 - T.pace_lag;
+    unsigned* f = T.pace + kTilePaceCnt + grp * 8 * 64;
+    const unsigned done = old + 1 + slack;
+    if (done % nwg == 0)
+      for (int r = 0; r < 8; ++r) __hip_atomic_fetch_max(f + r * 64, done / nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned* fr = f + ((blockIdx.x >> 3) & 7) * 64;
+    const unsigned need = (unsigned)step + 1;  // the group has finished this segment
     int spin = 0;
-    const int cap = kPaceSpins * 8 / T.pace_sleep;  // ~1 ms whatever the poll interval
-    if (T.pace_flag) {
-      unsigned* f = T.pace + kTilePaceCnt + grp * 8 * 64;
-      const unsigned done = old + 1 + slack;
-      if (done % nwg == 0)
-        for (int r = 0; r < 8; ++r) __hip_atomic_fetch_max(f + r * 64, done / nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned* fr = f + ((blockIdx.x >> 3) & 7) * 64;
-      if (need > 0)
-        for (; spin < cap; ++spin) {
-          if (__hip_atomic_load(fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)need) break;
-          for (int z = 0; z < T.pace_sleep; ++z) __builtin_amdgcn_s_sleep(1);
-        }
-    } else if (need > 0) {
-      const unsigned target = (unsigned)need * nwg - slack;
-      for (; spin < cap; ++spin) {
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-        __builtin_amdgcn_s_sleep(8);
-      }
+    for (; spin < kPaceSpins; ++spin) {
+      if (__hip_atomic_load(fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+      for (int z = 0; z < kPaceSleep; ++z) __builtin_amdgcn_s_sleep(1);
     }
-    if (spin == cap) *live = 0;
+    if (spin == kPaceSpins) *live = 0;
   }
   __syncthreads();
 }
 
-// one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once).  V32: the values
-// are stored as fp32 (exact, checked at build time) and widened here; everything after is fp64
-template <bool V32, int TU = kTU>
+// one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
 __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
 #pragma unroll
-  for (int u = 0; u < TU; ++u) {
+  for (int u = 0; u < kTU; ++u) {
     const int64_t e = k + u * 64;
     q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
-    if constexpr (V32) v[u] = e < hi ? (double)__builtin_nontemporal_load(&T.vals32[e]) : 0.0;
-    else v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
+    v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
   }
 }
 
@@ -126,14 +100,12 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // this rank's own block of p (they are final before the all-gather of p_k lands), the partial row
 // sums stored in Ap, no partials; 2 = the other segments, added to those sums, then the epilogue
 // (as k_split_spmv_aligned_part's halves)
-// TB: rows per block (kTileB: 32 KiB of row sums, 4 workgroups per CU; kTileB5: 30 KiB, built for 5,
-// which also caps the kernel at 96 VGPRs)
-// TU: entries per lane in flight (kTU; 12 = tile_unroll 12, at 4 workgroups per CU)
-template <int MODE, bool V32, int PART = 0, int TB = kTileB, int TU = kTU>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == kTileB5 ? 5 : (TU > kTU ? 4 : 1))))
-void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
+// kTileB rows per block: 32 KiB of row sums, 4 workgroups per CU
+template <int MODE, int PART = 0>
+__global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
+  constexpr int TB = kTileB, TU = kTU;
   __shared__ double acc[4][TB];
   int live = 0;  // thread 0's (the only one that paces)
   if constexpr (MODE == 0) {
@@ -154,7 +126,6 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
   auto seg = [&](int i) { return PART == 0 ? i : (PART == 1 ? glo + i : (i < glo ? i : i - glo + ghi)); };
   double* a = acc[wv];
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
-  double pf = 0.0;  // prefetch sink
   int step = 0;
   if (threadIdx.x == 0) live = 1;
   for (int64_t rd = 0; rd < rounds; ++rd) {
@@ -169,7 +140,7 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
       const int g0 = seg(0);
       lo = T.tptr[b * G + g0];
       hi = T.tptr[b * G + g0 + 1];
-      tile_batch_load<V32, TU>(T, lo + lane, hi, q, v);
+      tile_batch_load(T, lo + lane, hi, q, v);
     }
     for (int i = 0; i < ns; ++i, ++step) {
       const int g = seg(i);
@@ -179,7 +150,7 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
         for (int64_t k = lo + lane; k < hi; k += TU * 64) {
           uint32_t qn[TU];
           double vn[TU], x[TU];
-          tile_batch_load<V32, TU>(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
+          tile_batch_load(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
 #pragma unroll
           for (int u = 0; u < TU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
 #pragma unroll
@@ -196,18 +167,10 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
           const int gn = seg(i + 1);
           lo_next = T.tptr[b * G + gn];
           hi_next = T.tptr[b * G + gn + 1];
-          tile_batch_load<V32, TU>(T, lo_next + lane, hi_next, q, v);
+          tile_batch_load(T, lo_next + lane, hi_next, q, v);
         }
       }
-      const double* nxt = nullptr;  // the segment the group starts next (prefetched while it waits)
-      int64_t nlen = 0;
-      if (T.prefetch && (i + 1 < ns || rd + 1 < rounds)) {
-        const int gn = seg(i + 1 < ns ? i + 1 : 0);
-        const int64_t s0 = (int64_t)gn << T.seg_shift;
-        nxt = p + s0;
-        nlen = ((int64_t)1 << T.seg_shift) < T.ext_len - s0 ? ((int64_t)1 << T.seg_shift) : T.ext_len - s0;
-      }
-      pace_step(T, step, &live, nxt, nlen, pf);
+      pace_step(T, step, &live);
       lo = lo_next;
       hi = hi_next;
     }
@@ -233,8 +196,6 @@ void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict_
     }
     __syncthreads();
   }
-  // keep the prefetch loads (a bit pattern no sum of finite values produces)
-  if (__double_as_longlong(pf) == (long long)0x7FF4DEAD0000BEEFll) Ap[0] = pf;
   if constexpr (MODE == 0 && PART != 1) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
@@ -258,22 +219,18 @@ struct CsrSrc {  // a user matrix's rows on the device (local CSR, ext columns)
   }
 };
 
-// FILL = false: tptr[b * G + g + 1] = entries of tile (b, g), and *inexact += the entries whose value
-// does not survive fp64 -> fp32 -> fp64 (the fp32 value storage is taken only when none does);
-// FILL = true: write the tiles (tptr = exclusive offsets; values as V).  Lanes take rows rr = lane,
-// lane + 64, ... of the block in lockstep; the order of one LDS atomic's same-address lanes
-// (observed fixed, as above) orders a batch's appends.
-template <bool FILL, class V, class Src>
+// FILL = false: tptr[b * G + g + 1] = entries of tile (b, g); FILL = true: write the tiles (tptr =
+// exclusive offsets).  Lanes take rows rr = lane, lane + 64, ... of the block in lockstep; the order
+// of one LDS atomic's same-address lanes (observed fixed, as above) orders a batch's appends.
+template <bool FILL, class Src>
 __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int tb, int G, int seg_shift, int64_t* __restrict__ tptr,
-                                                    uint32_t* __restrict__ idx, V* __restrict__ vals,
-                                                    unsigned long long* __restrict__ inexact) {
+                                                    uint32_t* __restrict__ idx, double* __restrict__ vals) {
   extern __shared__ int cnt[];
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
   for (int g = lane; g < G; g += 64) cnt[g] = 0;
   __syncthreads();
   const uint32_t mask = (1u << seg_shift) - 1u;
-  unsigned bad = 0;
   for (int rr = lane; rr < tb; rr += 64) {
     const int64_t i = b * tb + rr;
     if (i >= n) break;
@@ -283,23 +240,19 @@ __global__ __launch_bounds__(64) void k_tiles_build(Src src, int64_t n, int tb, 
       if constexpr (FILL) {
         const int64_t dst = tptr[b * G + g] + pos;
         idx[dst] = ((uint32_t)rr << 22) | ((uint32_t)ec & mask);
-        vals[dst] = (V)v;
-      } else {
-        bad += (double)(float)v != v;  // NaN counts as inexact too
+        vals[dst] = v;
       }
     });
   }
   __syncthreads();
-  if constexpr (!FILL) {
+  if constexpr (!FILL)
     for (int g = lane; g < G; g += 64) tptr[b * G + g + 1] = cnt[g];
-    if (inexact != nullptr && bad) atomicAdd(inexact, (unsigned long long)bad);
-  }
 }
 
 }  // namespace
 
-TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift, int tb) {
-  MCG_CHECK(tb == kTileB || tb == kTileB5, "tiles: rows per block are 1024 or 960");
+TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
+  const int tb = kTileB;
   TilesGeometry t;
   t.tb = tb;
   t.seg_shift = seg_shift;
@@ -308,13 +261,12 @@ TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift, int
   return t;
 }
 
-int tiles_grid(int ncu, int tb) {
+int tiles_grid(int ncu) {
   int per_cu = 0;
-  const void* f = tb == kTileB5 ? reinterpret_cast<const void*>(&k_tiles<0, false, 0, kTileB5>)
-                                : reinterpret_cast<const void*>(&k_tiles<0, false>);
+  const void* f = reinterpret_cast<const void*>(&k_tiles<0>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   (void)hipGetLastError();
-  return std::min(per_cu, tb == kTileB5 ? 5 : 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
+  return std::min(per_cu, 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
 }
 
 namespace {
@@ -322,19 +274,16 @@ template <class Src>
 void tiles_build_impl(const Src& src, int64_t n, const TilesGeometry& geo, const TilesOut& o, bool fill, hipStream_t st) {
   MCG_CHECK(geo.G <= kTileMaxSegments, "tiles: too many column segments for the LDS counters");
   MCG_CHECK(geo.seg_shift <= 22, "tiles: segments are at most 2^22 columns");
-  MCG_CHECK(!fill || (o.vals != nullptr) != (o.vals32 != nullptr), "tiles: fill needs exactly one value array");
+  MCG_CHECK(!fill || o.vals != nullptr, "tiles: fill needs the value array");
   if (geo.nblocks == 0) return;
   const size_t lds = (size_t)geo.G * sizeof(int);
   const dim3 grid((unsigned)geo.nblocks);
   if (!fill)
-    hipLaunchKernelGGL((k_tiles_build<false, double, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
-                       o.tptr, o.idx, nullptr, o.inexact);
-  else if (o.vals32 != nullptr)
-    hipLaunchKernelGGL((k_tiles_build<true, float, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
-                       o.tptr, o.idx, o.vals32, nullptr);
+    hipLaunchKernelGGL((k_tiles_build<false, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
+                       o.tptr, o.idx, nullptr);
   else
-    hipLaunchKernelGGL((k_tiles_build<true, double, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
-                       o.tptr, o.idx, o.vals, nullptr);
+    hipLaunchKernelGGL((k_tiles_build<true, Src>), grid, dim3(64), lds, st, src, n, geo.tb, geo.G, geo.seg_shift,
+                       o.tptr, o.idx, o.vals);
   MCG_HIP(hipGetLastError(), "kernel launch failed(tiles_build)");
 }
 }  // namespace
@@ -356,38 +305,24 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
   MCG_CHECK(part == 0 || (T.g_lo >= 0 && T.g_lo <= T.g_hi && T.g_hi <= T.G), "tiles: bad own-segment range");
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
-  MCG_CHECK(T.tb == kTileB || T.tb == kTileB5, "tiles: rows per block are 1024 or 960");
+  MCG_CHECK(T.tb == kTileB, "tiles: 1024 rows per block");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-#define MCG_TL(V32, PART)                                                                                         \
-  do {                                                                                                            \
-    if (T.tb == kTileB5)                                                                                          \
-      hipLaunchKernelGGL((k_tiles<0, V32, PART, kTileB5>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap,     \
-                         own_off, partials, pstride, st, tol, first, check, rc);                                  \
-    else if (T.tu == 12)                                                                                          \
-      hipLaunchKernelGGL((k_tiles<0, V32, PART, kTileB, 12>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap,  \
-                         own_off, partials, pstride, st, tol, first, check, rc);                                  \
-    else                                                                                                          \
-      hipLaunchKernelGGL((k_tiles<0, V32, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off,     \
-                         partials, pstride, st, tol, first, check, rc);                                           \
-  } while (0)
-  const bool v32 = T.vals32 != nullptr;
-  if (part == 1) { if (v32) MCG_TL(true, 1); else MCG_TL(false, 1); }
-  else if (part == 2) { if (v32) MCG_TL(true, 2); else MCG_TL(false, 2); }
-  else { if (v32) MCG_TL(true, 0); else MCG_TL(false, 0); }
+#define MCG_TL(PART)                                                                                              \
+  hipLaunchKernelGGL((k_tiles<0, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials,     \
+                     pstride, st, tol, first, check, rc)
+  if (part == 1) MCG_TL(1);
+  else if (part == 2) MCG_TL(2);
+  else MCG_TL(0);
 #undef MCG_TL
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
 
 void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream) {
   if (grid <= 0 || T.nblocks == 0) return;
-  MCG_CHECK(T.tb == kTileB || T.tb == kTileB5, "tiles: rows per block are 1024 or 960");
+  MCG_CHECK(T.tb == kTileB, "tiles: 1024 rows per block");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-#define MCG_TY(V32, TB)                                                                                          \
-  hipLaunchKernelGGL((k_tiles<1, V32, 0, TB>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, \
-                     nullptr, 0.0, 0, 0, RedCtl())
-  if (T.tb == kTileB5) { if (T.vals32 != nullptr) MCG_TY(true, kTileB5); else MCG_TY(false, kTileB5); }
-  else { if (T.vals32 != nullptr) MCG_TY(true, kTileB); else MCG_TY(false, kTileB); }
-#undef MCG_TY
+  hipLaunchKernelGGL((k_tiles<1>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr, 0.0, 0,
+                     0, RedCtl());
   MCG_HIP(hipGetLastError(), "compute mv failed(y)");
 }
 

@@ -115,7 +115,7 @@ void DelayComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int
   if (copy_) {  // the messages' bytes through the copy engines (source: the rank's own first rows)
     // the all-gather layout's blocks side by side (CopyFan); window halos' small copies in one queue:
     // fanned out over streams they took longer (a P = 8 share of 16384^2: 0.507 vs 0.301 ms an
-    // iteration with halo_hide, profiles/r4/fan)
+    // iteration, profiles/r4/fan)
     // (a receive range longer than the rank's own rows -- the last rank of an all-gather layout, whose
     // block is short -- copies only as many rows as it owns: the source stays inside its rows)
     std::vector<CopyFan::Job> jobs;

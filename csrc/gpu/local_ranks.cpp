@@ -77,7 +77,6 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         o.lean_split = s.info().lean_split;
         o.p3 = s.info().p3;
         o.dia_uniform = s.info().dia_uniform;
-        o.halo_hide = s.info().halo_hide;
         o.halo_pull = s.info().halo_pull;
         o.ag_overlap = s.info().ag_overlap;
         o.ag_local_frac = s.info().ag_local_frac;

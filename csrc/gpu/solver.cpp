@@ -44,7 +44,7 @@ GpuCgSolver::GpuCgSolver(const ProblemSpec& spec, const CgOptions& opt, int rank
   // one communicator for halo and all-reduce: every collective in one stream order on s0_
   if (use_comm_ && comm_->serialized()) opt_.overlap = false;
   if (use_comm_ && !comm_->graph_capturable()) opt_.use_graph = false;
-  MCG_CHECK(opt_.form.graph_iters >= 2 && opt_.form.graph_iters % 2 == 0, "graph_iters must be even and >= 2");
+  MCG_CHECK(opt_.graph_iters >= 2 && opt_.graph_iters % 2 == 0, "graph_iters must be even and >= 2");
   if (opt_.hooks.inject_nan_at >= 0) opt_.use_graph = false;  // the hook runs between eager iterations
   MCG_CHECK(opt_.recurrence >= -1 && opt_.recurrence <= 2, "recurrence must be -1 (auto), 0, 1 or 2 (pipelined)");
   // pipelined CG: a residual replacement every pipe_rr iterations is an eager step (no capture)
@@ -226,12 +226,11 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
   }
   const SellDev S = sell_view();
   if (ar_) {
-    MCG_CHECK(which == 0 || hide_ || lean_split_,
-              "Ap-recomputing carry: one launch per iteration (halo_hide: two bands; lean_split: lean + generic runs)");
+    MCG_CHECK(which == 0 || lean_split_, "Ap-recomputing carry: one launch per iteration (lean_split: lean + generic runs)");
     // the launch runs the lean-only kernels: every run qualifies, or (lean_split) the lean half
     const bool lean_launch = lean_only_ || (lean_split_ && which == 1);
     // (lean_split: the generic launch runs on s2_, beside the lean one -- enqueue_pass_)
-    const hipStream_t ls = (lean_split_ && which == 2 && split_side_) ? (hipStream_t)s2_ : (hipStream_t)s0_;
+    const hipStream_t ls = (lean_split_ && which == 2) ? (hipStream_t)s2_ : (hipStream_t)s0_;
     v.ra_old = nullptr;
     v.ra_new = nullptr;
     v.ap_old = apx_[(k + 1) & 1].get();
@@ -417,11 +416,6 @@ int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
     enqueue_f1_(k, 0, 0, fused_red);
     return (g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_;
   }
-  if (!split_side_) {
-    enqueue_f1_(k, 1, 0, fused_red);
-    enqueue_f1_(k, 2, 0, fused_red);
-    return bnd_base_ + g_bnd_;
-  }
   // the generic launch (few busy blocks: the runs that do not qualify) on the high-priority side
   // stream s2_ first, then the lean one on s0_: the generic runs overlap the lean pass instead of
   // following it.  The runs of one pass are independent (each reads the previous pass's vectors),
@@ -454,21 +448,6 @@ void GpuCgSolver::enqueue_iteration_f1_(int k) {
       ensure_ghosts_(k);
     }
     np = enqueue_pass_(k, fr);
-  } else if (hide_) {
-    // halo_hide: the interior band reads no ghost line, so it runs while this iteration's ghosts land
-    // (copy engines: no CU is taken from the pass); then the lines at both ends of the rank, whose
-    // last arriver finishes the reduction; then the next iteration's ghosts -- this pass's outputs,
-    // final now -- on the side stream next to the all-reduce and the next interior band
-    enqueue_f1_(k, 1, 0, fr);
-    ensure_ghosts_(k);
-    enqueue_f1_(k, 2, 0, fr);
-    np = bnd_base_ + g_bnd_;
-    MCG_HIP(hipEventRecord(ev_r_, s0_), "event record failed");
-    MCG_HIP(hipStreamWaitEvent(s1_, ev_r_, 0), "stream wait failed");
-    enqueue_halo_f1_(k + 1, s1_);
-    MCG_HIP(hipEventRecord(ev_h_, s1_), "event record failed");
-    ghosts_for_ = k + 1;
-    halo_pending_ = true;
   } else if (halo_ahead_) {
     ensure_ghosts_(k);
     np = enqueue_pass_(k, fr);  // every owned row in one pass (the line-carry pass at P > 1 too)
@@ -695,7 +674,7 @@ void GpuCgSolver::drop_graphs_() {
 // depend on k only through its parity (and k >= 2), so one capture replays for every even k_.
 void GpuCgSolver::capture_pair_(int kind) {
   hipStream_t s = s0_;
-  const int iters = kind == 0 ? 2 : opt_.form.graph_iters;
+  const int iters = kind == 0 ? 2 : opt_.graph_iters;
   // halo_ahead: a graph starts with its ghosts in place (joined before the launch) and ends by
   // joining the prefetch of its last iteration, so every replay sees the same host-side state
   if (halo_ahead_ && !pull_) ensure_ghosts_(k_);
@@ -722,7 +701,7 @@ void GpuCgSolver::capture_pair_(int kind) {
 
 void GpuCgSolver::run_iterations(int count) {
   MCG_CHECK(setup_done_, "solver not set up");
-  const int glong = opt_.form.graph_iters > 2 ? opt_.form.graph_iters : 0;
+  const int glong = opt_.graph_iters > 2 ? opt_.graph_iters : 0;
   while (count > 0) {
     if (opt_.use_graph && k_ >= 2 && (k_ % 2) == 0 && count >= 2 && (!pull_ || k_ >= pull_from_)) {
       const int kind = glong && count >= glong ? 1 : 0;

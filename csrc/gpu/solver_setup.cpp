@@ -265,8 +265,7 @@ void GpuCgSolver::setup() {
 
   size_t matrix_bytes = 0;
   if (tiles_) {
-    tgeo_ = kern::tiles_geometry(n, L_.ext_len, std::max(10, std::min(22, opt_.form.tile_seg_log2)),
-                                 opt_.form.tile_rows == kern::kTileB5 ? kern::kTileB5 : kern::kTileB);
+    tgeo_ = kern::tiles_geometry(n, L_.ext_len, std::max(10, std::min(22, opt_.form.tile_seg_log2)));
     MCG_CHECK(tgeo_.G <= kern::kTileMaxSegments, "tiles: too many column segments (raise tile_seg_log2)");
     tptr_.allocate(tgeo_.nblocks * tgeo_.G + 1, "A");
     MCG_HIP(hipMemsetAsync(tptr_.get(), 0, tptr_.bytes(), s0_), "device memset failed(A)");
@@ -283,26 +282,13 @@ void GpuCgSolver::setup() {
               "memcpy from host to device failed(A)");
     }
     const int64_t ntp = tgeo_.nblocks * tgeo_.G;
-    DeviceBuffer<unsigned long long> inexact(1, "A");
-    MCG_HIP(hipMemsetAsync(inexact.get(), 0, sizeof(unsigned long long), s0_), "device memset failed(A)");
     kern::TilesOut to;
     to.tptr = tptr_.get();
     to.idx = tidx_.get();
-    to.inexact = inexact.get();
     for (int fill = 0; fill < 2; ++fill) {
       if (fill) {
-        // values as fp32 when every value of every rank round-trips exactly (the same matrix bits; the
-        // products and sums stay fp64): 8 instead of 12 B per entry streamed
-        unsigned long long bad = 0;
-        MCG_HIP(hipMemcpy(&bad, inexact.get(), sizeof(bad), hipMemcpyDeviceToHost), "memcpy from device to host failed(A)");
-        bool v32 = opt_.form.tile_vals32 == 1 || (opt_.form.tile_vals32 < 0 && bad == 0);
-        MCG_CHECK(opt_.form.tile_vals32 != 1 || bad == 0, "tiles: tile_vals32=1 needs every value exactly representable in fp32");
-        if (opt_.form.tile_vals32 < 0 && use_comm_ && world_ > 1) v32 = all_ranks_agree_(v32);
-        if (v32) tvals32_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
-        else tvals_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
-        to.vals = v32 ? nullptr : tvals_.get();
-        to.vals32 = v32 ? tvals32_.get() : nullptr;
-        info_.tile_vals32 = v32;
+        tvals_.allocate(std::max<int64_t>(nnz, 1), "A", 64);
+        to.vals = tvals_.get();
       }
       if (is_user) kern::tiles_build_csr(rp64.get(), tc.get(), tv.get(), n, tgeo_, to, fill, s0_);
       else kern::tiles_build_gen(spec_, L_.row_begin, n, L_.col_lo, L_.pad, rp64.get(), tgeo_, to, fill, s0_);
@@ -320,7 +306,7 @@ void GpuCgSolver::setup() {
     c8_ = false;
     info_.format = 5;
     info_.sell_fill = 1.0;
-    matrix_bytes = (size_t)nnz * (info_.tile_vals32 ? 8 : 12) + tptr_.bytes();
+    matrix_bytes = (size_t)nnz * 12 + tptr_.bytes();
   } else if (opt_.format == 1) {
     // ---- SELL-64, generated directly (no CSR intermediate: peak memory = the SELL arrays) ----
     const int64_t ns = (n + 63) / 64;
@@ -561,7 +547,7 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (tiles_) {  // one launch over every row block: the resident workgroups (the pacing waits on each)
-    g_all_ = n > 0 ? kern::tiles_grid(ncu_, tgeo_.tb) : 0;
+    g_all_ = n > 0 ? kern::tiles_grid(ncu_) : 0;
     if (opt_.blocks_per_cu > 0) g_all_ = std::min(g_all_, ncu_ * opt_.blocks_per_cu);  // fewer waves: more rounds
     g_int_ = 0;
     g_bnd_ = g_all_;
@@ -607,7 +593,7 @@ void GpuCgSolver::setup() {
       auto apply = [&](TileRanges& t, int& grid) {
         if (t.ntiles == 0 || t.nt0 != t.ntiles || t.b0 % S != 0 || t.nt0 % S != 0 || t.nt0 / S < 2) return false;
         t.strip = (int32_t)S;
-        grid = ncu_ * (t.nt0 / S >= 4096 ? 8 : 4);
+        grid = ncu_ * (opt_.blocks_per_cu > 0 ? opt_.blocks_per_cu : (t.nt0 / S >= 4096 ? 8 : 4));
         return true;
       };
       // the specialised pass (no slow path) when every stored offset is carried: 0, +-1, +-one line
@@ -637,7 +623,7 @@ void GpuCgSolver::setup() {
       // 3-D 7-point with variable coefficients: SELL-64/diav 3-D (four arrays, one plane in front) on
       // the plane carry's three-term lean loop (32-bit byte offsets: ranks below 2^29 rows)
       const int64_t ln3 = stencil_line(spec_);
-      const int kwv = opt_.form.carry3_kw == 4 ? 4 : 8;
+      const int kwv = 8;  // the diav plane carry's blocks: 8 waves, 2 per SIMD
       if (!c8_ && !diav_ && stencil_plane(spec_) > 0 && ln3 >= 64 && ln3 % 64 == 0 && ln3 % kwv == 0 &&
           ln3 * ln3 == gl && info_.max_row_len <= 7 && opt_.form.carry_vc != 0 && opt_.form.ap_recompute != 0 &&
           opt_.form.p3 != 0 && !split_ && n > 0 && L_.ext_len < ((int64_t)1 << 29) && n + gl < ((int64_t)1 << 29)) {
@@ -668,12 +654,12 @@ void GpuCgSolver::setup() {
     // carry with +-N through LDS, on SELL-64/dia4 only
     const bool ar_any = opt_.form.ap_recompute != 0 && carry_all_ && !carry_general_ && (c8_ || diav_) && !split_ &&
                         tr_all_.b0 == 0 && tr_all_.strip > 0;
-    // 3-D diav: blocks of 8 (or 4) waves, 2 per SIMD (the streamed values need the registers)
-    const int kw = diav3_ ? (opt_.form.carry3_kw == 4 ? 4 : 8) : opt_.form.carry3_kw;
+    // blocks of 16 waves, 4 per SIMD (512^3: 714 vs 628 / 650-667 it/s at 4 / 8, profiles/r2_ar3_poisson512.md);
+    // 3-D diav: 8 waves, 2 per SIMD (the streamed values need the registers; 557 vs 493 at 4, profiles/r4/vc)
+    const int kw = diav3_ ? 8 : 16;
     const bool ar2 = ar_any && carry_lo2_ == 0 && info_.spmv_param <= 5;
     const bool ar3 = ar_any && carry_lo2_ > 0 && carry_lo2_ % 64 == 0 && info_.spmv_param <= 7 &&
-                     (opt_.form.carry_dia != 0 || diav3_) && (kw == 4 || kw == 8 || kw == 16) &&
-                     carry_lo2_ % kw == 0 && (int64_t)carry_lo2_ * carry_lo2_ == gl;
+                     (opt_.form.carry_dia != 0 || diav3_) && carry_lo2_ % kw == 0 && (int64_t)carry_lo2_ * carry_lo2_ == gl;
     MCG_CHECK(opt_.form.carry_dia != 1 || ar2 || ar3,
               "carry_dia needs the Ap-recomputing line / plane carry (ap_recompute)");
     if ((ar2 || ar3) && opt_.form.carry_dia != 0 && n > 0 && c8_) {  // SELL-64/dia4 from the c8 codes (replaces c4 + metadata)
@@ -713,7 +699,7 @@ void GpuCgSolver::setup() {
     }
     MCG_CHECK(opt_.form.ap_recompute != 1 || ar_,
               "ap_recompute needs the specialised line-carry pass over all lines (2-D: c8, <= 5 entries per row; "
-              "3-D: dia4, N a multiple of 64 and of carry3_kw)");
+              "3-D: dia4, N a multiple of 64)");
     // 4 waves per SIMD (one round of resident blocks; diav 3-D: 2).  Runs of planes per job column:
     // as many as make the jobs fill whole rounds of those blocks (a launch of 224 blocks over 256
     // jobs ran a second round for 32 of them: the 44 % that reserve_cus = 32 cost at 512^3,
@@ -723,7 +709,7 @@ void GpuCgSolver::setup() {
       const int64_t jpr = (int64_t)(carry_lo2_ / kw) * (carry_lo2_ / 64);
       // past 2^29 rows the lean runs keep their planes -3 .. end + 4 within 4 GiB of a per-run base
       const int64_t max_chunk = L_.ext_len >= ((int64_t)1 << 29) ? ((int64_t)1 << 32) / (gl * 8) - 8 : 0;
-      tr_all_.runs3 = opt_.form.carry3_runs < 0 ? kern::carry3_runs(g_all_, jpr, n / gl, max_chunk) : opt_.form.carry3_runs;
+      tr_all_.runs3 = kern::carry3_runs(g_all_, jpr, n / gl, max_chunk);
     }
     info_.ar3_kw = ar3_ ? kw : 0;
     info_.ar3_runs = ar3_ ? tr_all_.runs3 : 0;
@@ -753,8 +739,7 @@ void GpuCgSolver::setup() {
   // for; 3-D: LEAN); otherwise the generic kernels (no lean code: one kernel holding both measured
   // slower for each, profiles/r3/lean)
   lean_only_ = false;
-  lean_depth_even_ = opt_.form.lean_depth;
-  lean_depth_odd_ = opt_.form.lean_depth_odd > 0 ? opt_.form.lean_depth_odd : opt_.form.lean_depth;
+  lean_depth_even_ = lean_depth_odd_ = 0;  // 0 = the lean kernels' default depth (3)
   if (p3_ && dpat_.get() != nullptr && n > 0 && tr_all_.strip > 0) {
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
     int g = g_all_;
@@ -772,25 +757,24 @@ void GpuCgSolver::setup() {
           break;
         }
       }
-      if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
+      if (opt_.blocks_per_cu > 0) g = ncu_ * opt_.blocks_per_cu;  // fixed (tests: the generic pass's grid)
       // the 4-blocks-per-CU grids (64-line runs: 4096^2, latency-bound passes): packed slice edges, the
       // even passes at 5 waves per SIMD (depth 3), the odd ones at depth 4 with 4 (each on its own grid;
       // 4096^2: 8441-8542 vs 8181-8188 it/s on one box, profiles/r4/edge2)
-      auto_mix_ = bpc_rule == 4 && opt_.form.lean_bpc <= 0 && opt_.form.lean_bpc_odd <= 0 && opt_.form.lean_depth <= 0 &&
-                  opt_.form.lean_depth_odd <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.form.halo_hide != 1;
+      auto_mix_ = bpc_rule == 4 && opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29);
     }
     auto lean_ok = [&](int gg) {
       return kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, gg, ar3_ ? info_.ar3_kw : 0,
-                                       ar3_ ? carry_lo2_ : 0, s0_, 0, 0, ar3_ ? tr_all_.runs3 : 0) == 0;
+                                       ar3_ ? carry_lo2_ : 0, s0_, ar3_ ? tr_all_.runs3 : 0) == 0;
     };
-    // the odd passes (x update paired in) on a grid of their own (lean_bpc_odd): both grids' runs must qualify
-    int go = (!ar3_ && opt_.form.lean_bpc_odd > 0) ? ncu_ * opt_.form.lean_bpc_odd : g;
+    // the odd passes (x update paired in) on a grid of their own (auto_mix_): both grids' runs must qualify
+    int go = g;
     if (auto_mix_) {
       if (lean_ok(ncu_ * 5) && lean_ok(ncu_ * 4)) {
         g = ncu_ * 5;
         go = ncu_ * 4;
-        lean_depth_even_ = 13;
-        lean_depth_odd_ = 14;
+        lean_depth_even_ = opt_.hooks.lean_packed == 0 ? 0 : 13;
+        lean_depth_odd_ = opt_.hooks.lean_packed == 0 ? 0 : 14;
       } else {
         auto_mix_ = false;
       }
@@ -798,7 +782,7 @@ void GpuCgSolver::setup() {
     const bool lean_all = lean_ok(g) && (go == g || lean_ok(go));
     // (at P > 1 too since r5: the r4 drift of a split rank next to a lean-only one was pass 0 running
     // on both launches, solver.cpp enqueue_pass_)
-    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_ && opt_.form.lean_bpc_odd <= 0) {
+    if (!lean_all && !ar3_ && opt_.form.lean_split != 0 && !split_) {
       // some runs do not qualify: split the pass by run -- the lean kernels over the runs that do, the
       // generic ones over the rest, on the same grid (the same runs), when most runs qualify
       auto_mix_ = false;
@@ -806,14 +790,13 @@ void GpuCgSolver::setup() {
       int64_t runs = 0, chunk = 0;
       kern::carry_jobs_host((int64_t)g * 4, tr_all_.strip, nlines, runs, chunk);
       const int64_t jobs = runs * tr_all_.strip;
-      const int64_t fails = kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, 0, 0, s0_, 0, 0, 0);
+      const int64_t fails = kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, 0, 0, s0_, 0);
       // auto: runs of >= 128 lines (each wave takes one run) -- 16384^2 (256-line runs) 548-557 it/s vs 514
       // all-generic with 3 changed rows; the 64-line runs of 4096^2 / 8192^2 lose (the few generic runs
       // sit on the critical path: 4855 vs 6816, 1819 vs 1938; profiles/r4/lsplit)
       const bool want = opt_.form.lean_split >= 1 || (2 * fails < jobs && chunk >= 128);
       if (jobs > 0 && fails < jobs && want) {
         lean_split_ = true;
-        split_side_ = opt_.form.lean_split_side != 0;
         g_all_ = g;
         tr_int_ = tr_all_;
         tr_int_.lean_split = 1;
@@ -872,7 +855,7 @@ void GpuCgSolver::setup() {
         break;
       }
     if (g == 0) g = g_all_;
-    if (opt_.form.lean_bpc > 0) g = ncu_ * opt_.form.lean_bpc;
+    if (opt_.blocks_per_cu > 0) g = ncu_ * opt_.blocks_per_cu;
     for (int gg = g; gg >= 1 && !all_lean(gg); gg /= 2) g = gg / 2;
     if (g >= 1 && all_lean(g)) {
       lean_only_ = true;
@@ -881,42 +864,7 @@ void GpuCgSolver::setup() {
     }
   }
   info_.lean_only = lean_only_;
-  info_.lean_mix = auto_mix_ && lean_only_ && g_odd_ > 0;
-  // halo_hide: the lean 2-D pass split into the interior band (reads no ghost line; it runs while a
-  // copy-engine halo lands) and the kHideLines lines at each end of the rank (after the halo)
-  if (opt_.form.halo_hide == 1 && halo_ahead_ && comm_ != nullptr && comm_->halo_cu_free() && lean_only_ && ar_ && !ar3_ && p3_ &&
-      n > 0 && tr_all_.strip > 0) {
-    constexpr int kHideLines = 4;
-    const int64_t ss = tr_all_.strip, nlines = (n + 63) / 64 / ss;
-    TileRanges ti = tr_all_, tb = tr_all_;
-    ti.band = 1;
-    tb.band = 2;
-    ti.band_h = tb.band_h = kHideLines;
-    // band 1 on the full grid (rounded to whole reduction groups, as the split launches are below: the
-    // job decomposition depends on the grid), band 2 one wave per (end, slice column)
-    const int gi = (g_all_ + kern::kRedGroup - 1) / kern::kRedGroup * kern::kRedGroup;
-    const int gb = (int)((2 * ss + 3) / 4);
-    bool ok = nlines >= 2 * kHideLines + 3;
-    if (ok && dpat_.get() != nullptr)
-      ok = kern::carry_lean_failures(dpat_.get(), ss, nlines, L_.ext_len, gi, 0, 0, s0_, 1, kHideLines) == 0 &&
-           kern::carry_lean_failures(dpat_.get(), ss, nlines, L_.ext_len, gb, 0, 0, s0_, 2, kHideLines) == 0;
-    if (ok && diav_) {  // every interior-band run >= 3 lines
-      const int64_t nw = (int64_t)gi * 4, runs = nw > ss ? nw / ss : 1, lines = nlines - 2 * kHideLines;
-      const int64_t chunk = (lines + runs - 1) / runs;
-      for (int64_t r = 0; r < runs && ok; ++r) {
-        const int64_t a = r * chunk, b = std::min(lines, a + chunk);
-        if (a < lines && b - a < 3) ok = false;
-      }
-    }
-    if (ok) {
-      hide_ = true;
-      tr_int_ = ti;
-      tr_bnd_ = tb;
-      g_int_ = gi;
-      g_bnd_ = gb;
-    }
-  }
-  info_.halo_hide = hide_;
+  info_.lean_mix = auto_mix_ && lean_only_ && g_odd_ > 0 && opt_.hooks.lean_packed != 0;
   // in-kernel halo: the lean carries read their ghost lines / planes from the neighbours' rows and store
   // their own first / last ones write-through (cg_carry_ar.hip PullBases), so an iteration from 2 on is
   // the pass + the all-reduce, no halo step.  The all-reduce orders the passes: a rank's pass k + 1
@@ -925,7 +873,7 @@ void GpuCgSolver::setup() {
   // does not write, and its pass k + 1 rewrites them only after this rank's pass k has contributed.
   // Every rank must take it (it decides the collectives of an iteration)
   {
-    const bool can = use_halo_ && ar_ && p3_ && lean_only_ && !hide_ && !lean_split_ && !L_.allgather && !pmat_ &&
+    const bool can = use_halo_ && ar_ && p3_ && lean_only_ && !lean_split_ && !L_.allgather && !pmat_ &&
                      opt_.recurrence == 1 && n > 0 && comm_ != nullptr &&
                      (comm_->maps_peers() || (opt_.form.halo_pull == 1 && !comm_->moves_data()));
     pull_ = opt_.form.halo_pull != 0 && can && (opt_.form.halo_pull == 1 || comm_->maps_peers());
@@ -934,9 +882,6 @@ void GpuCgSolver::setup() {
               "halo_pull needs the lean line / plane carry on every rank (P > 1, a communicator that maps its peers)");
     info_.halo_pull = pull_;
   }
-  // the copy-engine halo replays slowly from a hipGraph (a P = 8 share of 16384^2 with halo_hide:
-  // 0.393 ms an iteration captured, 0.301 eager, profiles/r4/hide): halo_hide iterates eagerly
-  if (hide_) opt_.use_graph = false;
   if (ar_ && !info_.dia4 && !diav_ && n > 0) {
     const int64_t ns = (n + 63) / 64;
     int64_t slots = 0;
@@ -952,7 +897,7 @@ void GpuCgSolver::setup() {
   info_.graphs = opt_.use_graph;
   info_.grid_odd = g_odd_;
   info_.grid_b = g_b_;
-  const bool split = split_ || hide_ || lean_split_;
+  const bool split = split_ || lean_split_;
   fused_red_ = (opt_.recurrence == 1 && opt_.form.fused_reduce != 0) || opt_.recurrence == 2;
   auto groups = [](int g) { return (g + kern::kRedGroup - 1) / kern::kRedGroup; };
   // the boundary launch's partials start on a reduction-group boundary: round the interior grid up
@@ -1101,7 +1046,7 @@ void GpuCgSolver::allocate_vectors_() {
     return;
   }
   // with the placement probe, every vector gets room for leads up to kLeadCap (probe_placement_)
-  const size_t cap = opt_.form.placement_tries > 1 && opt_.form.placement_leads > 1 && opt_.recurrence == 1 ? kLeadCap : 0;
+  const size_t cap = opt_.placement_tries > 1 && opt_.placement_leads > 1 && opt_.recurrence == 1 ? kLeadCap : 0;
   x_.allocate(n, "x", 8, 0, cap);
   if (ar_) {  // r, p by parity (ext layout); Ap only for slice edges (+ first / last / ghost lines at P > 1)
     r_.allocate(L_.ext_len, "r", 8, 0, cap);
@@ -1145,12 +1090,12 @@ void GpuCgSolver::allocate_vectors_() {
 void GpuCgSolver::probe_placement_() {
   info_.placement_sets = 1;
   info_.placement_gain = 1.0;
-  if (opt_.form.placement_tries <= 1 || opt_.recurrence != 1 || pmat_) return;
+  if (opt_.placement_tries <= 1 || opt_.recurrence != 1 || pmat_) return;
   trace::Range tr_("mcg.placement");
   auto bufs = vectors_();
   size_t set_bytes = 0;
   for (auto* b : bufs) set_bytes += b->bytes();
-  const int leads = std::max(1, opt_.form.placement_leads);
+  const int leads = std::max(1, opt_.placement_leads);
   // start offset (doubles) of buffer i in lead trial t: trial 0 all zero, then pseudo-random
   // multiples of 4 KiB (0..7) + 1 MiB (0..3)
   auto lead_of = [&](int t, size_t i) -> size_t {
@@ -1204,7 +1149,7 @@ void GpuCgSolver::probe_placement_() {
   int best_t = 0;
   float best = probe_set(best_t);
   std::vector<std::vector<DeviceBuffer<double>>> held;
-  for (int t = 1; t < opt_.form.placement_tries; ++t) {
+  for (int t = 1; t < opt_.placement_tries; ++t) {
     size_t free_b = 0, total_b = 0;
     MCG_HIP(hipMemGetInfo(&free_b, &total_b), "device memory query failed");
     if (free_b < set_bytes + set_bytes / 4 + ((size_t)1 << 30)) break;

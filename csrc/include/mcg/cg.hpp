@@ -20,8 +20,6 @@ namespace mcg {
 // fastest form for the matrix, rank layout and recurrence); setting one forces a form on or off for
 // tests, sweeps and A/B measurements.  None changes the arithmetic of CG, only how a pass is built.
 struct PassForm {
-  int graph_iters = 32;      // iterations per graph launch (even, >= 2); the last < graph_iters run as pairs
-                             // (32 vs 2: 4096^2 4700 -> 5025 it/s, profiles/r1_graph_iters.log)
   int interleave = -1;       // single-reduction + SELL: {r, Ap} stored as 16-B pairs (one gather load); -1 = auto
   int pipeline = -1;         // single-reduction SELL d16/c8 + interleave, rows <= 8 nonzeros: software-pipelined
                              // pass (next slice's codes + own-row operands issued ahead); -1 = when applicable.
@@ -31,11 +29,6 @@ struct PassForm {
                              // per grid line / plane): line-carry pass — a wave walks down a column of slices and
                              // keeps the +-one-line and +-1 neighbours' p_k in registers.  -1 = auto: when every
                              // stored offset is carried (2-D stencils, c8); 1 = on (also with the slow path); 0 = off
-  int placement_tries = 6;   // single-reduction form: time the pass on this many physical placements of the vector
-                             // set at setup and keep the fastest (1 = off; profiles/r1_placement_probe.md)
-  int placement_leads = 16;  // ... times this many start offsets of the vectors inside their allocations
-                             // (16384^2: 3 x 8 -> 503-517 it/s, 6 x 8 -> 516-525, 6 x 16 -> 524-525;
-                             // profiles/r3_placement_depth.txt)
   int window = -1;           // single-reduction + SELL: p_k staged once per 1024-row chunk in an LDS window
                              // (long banded rows); -1 = auto (windows fit and mean row length >= 32)
   int pmat = -1;             // single-reduction form: materialized-p split pass (update kernel + SpMV gathering the
@@ -57,23 +50,8 @@ struct PassForm {
   int tile_seg_log2 = 18;    // tiles: column segment = 2^k doubles (18: 2 MiB of p, half an XCD's L2; at a P = 8
                              // rank's share of the scrambled config 5 with step-flag pacing: 17 / 18 / 19 -> 18.5 /
                              // 19.3-19.5 / 17.5 it/s, profiles/r4/c5; r3's counter pacing peaked at 19: 14.0)
-  int tile_rows = 1024;      // tiles: rows per block, 1024 (4 workgroups per CU) or 960 (5 per CU, the kernel held
-                             // to 96 VGPRs: spills, 18.1-18.2 vs 19.4 it/s on config 5, profiles/r4/c5tb)
-  int tile_unroll = 8;       // tiles: entries per lane in flight, 8 or 12 (1024-row blocks; 12 spills at 4 waves per
-                             // SIMD: 18.9 vs 19.4 it/s on config 5, profiles/r4/c5tb)
-  int tile_pace = 4;         // tiles: 0 = unpaced (7.5 it/s), 1 = every workgroup of a group finishes a segment
-                             // before any starts the next, 2 = all but 1/8 of them (stragglers do not stall the rest);
-                             // 3 / 4 = as 1 / 2, the waiters polling a step flag (8 replicas) instead of the arrival
-                             // counter, whose line every arrival writes (4: 17.5 vs 14.3 it/s for 2 at 2^19)
-  int tile_pace_lag = 0;     // tiles: segments a workgroup may run ahead of its group's completed ones
-  int tile_pace_slack = 1;   // tiles, tile_pace 2 / 4: a workgroup waits for all but this many eighths of its group
-  int tile_prefetch = 0;     // tiles: each workgroup touches its share of the next segment before the pacing wait
-  int tile_vals32 = 0;       // tiles: values stored as fp32 (8 instead of 12 B per entry streamed) when every value
-                             // round-trips fp64 -> fp32 -> fp64 exactly, checked while the tiles are counted: the
-                             // same matrix, products and sums in fp64; -1 = auto (when exact on every rank), 0 = off
-                             // (the default: the scrambled config-5 share ran 18.1-18.4 vs 19.3 it/s with fp64
-                             // storage, profiles/r4/c5v32), 1 = required (an inexact value is an error)
-  int tile_pace_sleep = 8;   // tiles: s_sleep units (64 clocks each) between two polls of a waiting workgroup
+                             // (r5 pruned the tile variants that measured slower: 960-row blocks, 12 entries per
+                             // lane, fp32 values, prefetch, the other pacing modes -- cg_tiles.hip header)
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off
@@ -96,27 +74,11 @@ struct PassForm {
   int dia_uniform = -1;      // dia4 carry: slices whose 64 rows share one value-index pattern take a lean loop with the
                              // values in scalar registers and no codes streamed (the 2-D three-term pass over runs
                              // of such lines; bitwise the same sums); -1 = auto (on), 0 = off
-  int lean_depth = 0;        // 2-D lean-only passes: operand prefetch depth in lines (0 = auto: 3; 4 and 6 build with
-                             // 3 / 2 waves per SIMD for the registers; 13 / 14: packed slice edges at depth 3 with 5
-                             // waves per SIMD / depth 4 with 4, cg_carry_ar.hip EP)
-  int lean_bpc = 0;          // 2-D lean-only passes: blocks per CU of the grid (0 = auto: the largest of 16 / 8 / 4
-                             // whose runs keep >= 64 lines)
   int lean_split = -1;       // 2-D three-term dia4 carry when some runs' slice patterns are not uniform (a user matrix
                              // with a few odd rows): the lean kernels over the runs that qualify, the generic ones
                              // over the rest, in two launches; -1 = auto (when most runs qualify), 0 = off (every run
-                             // on the generic kernels), 1 = on
-  int lean_split_side = 1;   // ... the generic launch on a side stream, concurrent with the lean one (0 = after it)
-  int lean_depth_odd = 0;    // ... the odd passes (x update paired in: one more stream) their own depth / grid; 0 = as
-  int lean_bpc_odd = 0;      // the even passes (the two grids each reduce their own block partials)
-  int carry3_kw = 16;        // 3-D Ap-recomputing plane carry: waves per block = consecutive grid lines exchanging
-                             // their +-N rows through LDS (4, 8 or 16; the outer two lines store Ap; 512^3: 628 /
-                             // 650-667 / 714 it/s, profiles/r2_ar3_poisson512.md)
-  int carry3_runs = -1;      // 3-D plane carry: runs of planes per job column (-1 auto: kern::carry3_runs, whole
-                             // rounds of blocks; 0 = blocks / jobs per run, the r3 rule; > 0 fixed)
-  int halo_hide = 0;         // 2-D lean line carry at P > 1 with a CU-free halo (Communicator::halo_cu_free: copy
-                             // engines): the pass runs as the interior band (no ghost read) while the ghosts
-                             // arrive, then the band_h = 4 lines at each end of the rank; the halo of the next
-                             // iteration is issued on the side stream right after that second launch. 1 = on
+                             // on the generic kernels), 1 = on; the generic launch runs on a side stream, concurrent with
+                             // the lean one (r4: 548-557 vs 523-525 it/s after it, profiles/r4/lsplit)
   int halo_pull = -1;        // multi-rank lean carries (2-D line, 3-D plane): the in-kernel halo -- the waves that
                              // read a ghost line load it straight from the neighbour's rows (peer-mapped: IPC or
                              // another thread's pointers) and every pass stores its first / last line write-through,
@@ -136,7 +98,16 @@ struct TestHooks {
   int fail_graph_launch_at = -1;  // test hook: report the graph launch at this iteration as failed (nothing enqueued)
   int force_idx64 = 0;       // test hook: int64 row pointers even when int32 would do
   int inject_nan_at = -1;    // fault-injection hook: poison r at this iteration (breakdown detection test)
+  int lean_packed = -1;      // test hook: 0 = the packed-edge geometry (solver_setup.cpp auto_mix_: even passes on 5,
+                             // odd ones on 4 blocks per CU) with the default lean kernels instead of the packed-edge
+                             // ones -- the bit-for-bit reference of those kernels
 };
+
+// Pass forms pruned in r5 (measured slower and kept opt-in until then): lean_depth 4 / 6 (fewer waves
+// per SIMD, deeper prefetch), lean_bpc / lean_bpc_odd / lean_depth_odd (now only the setup's rules:
+// the 4096^2-class grids still take the packed-edge kernels, solver_setup.cpp auto_mix_), lean_split_side
+// 0, carry3_kw 4 / 8 on dia4 and 4 on diav (16 / 8 kept), carry3_runs (auto only) and halo_hide (the
+// copy-engine halo split around the pass; superseded by halo_pull).  Their measurements stay in profiles/.
 
 struct CgOptions {
   int maxit = 2000;          // CUDACG.cu:244
@@ -147,7 +118,8 @@ struct CgOptions {
   bool use_graph = true;     // capture iteration pairs into a hipGraph
   bool force_comm = false;   // run RCCL collectives even with one rank
   int format = 0;            // 0 = CSR, 1 = SELL-64
-  int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps)
+  int blocks_per_cu = 0;     // SpMV grid (blocks per CU); 0 = auto (SELL 48, CSR 8: measured sweeps; the line
+                             // carries 16 / 8 / 4 by their run lengths, solver_setup.cpp)
   int spmv_variant = -1;     // CSR engine: 0 LDS-staged tiles, 1 direct, 2 CSR-vector, 4 row-length adaptive per
                              // tile (direct or 16 lanes per row); -1 = auto (1 when every row has <= 16 entries, else 4)
   int recurrence = 0;        // 0 = two-pass / two-reduction (reference order), 1 = single-reduction fused pass,
@@ -160,6 +132,13 @@ struct CgOptions {
   std::string checkpoint_path;  // per-rank file prefix ("<path>.rank<r>")
   double watchdog_seconds = 0.0;  // > 0: solve() fails (and aborts the communicator) if one poll interval
                                   // makes no progress for this long (bounded host wait)
+  int graph_iters = 32;      // iterations per graph launch (even, >= 2); the last < graph_iters run as pairs
+                             // (32 vs 2: 4096^2 4700 -> 5025 it/s, profiles/r1_graph_iters.log)
+  int placement_tries = 6;   // single-reduction form: time the pass on this many physical placements of the vector
+                             // set at setup and keep the fastest (1 = off; profiles/r1_placement_probe.md)
+  int placement_leads = 16;  // ... times this many start offsets of the vectors inside their allocations
+                             // (16384^2: 3 x 8 -> 503-517 it/s, 6 x 8 -> 516-525, 6 x 16 -> 524-525;
+                             // profiles/r3_placement_depth.txt)
   int reserve_cus = 0;       // CUs withheld from the compute stream (a CU-masked queue, the mask's top bits; 32 = one
                              // per shader engine) so a collective's ~270-VGPR kernels find a free CU beside the
                              // resident pass (profiles/r3_cumask_probe.md); the pass grids are sized for the CUs

@@ -101,7 +101,7 @@ class Communicator {
   // order (no side-stream halo; CgOptions::overlap is forced off)
   virtual bool serialized() const { return false; }
   // true: the halo moves its bytes with copy engines (no compute units), so it can run while a pass
-  // holds every CU (CgOptions::form.halo_hide splits the pass around it)
+  // holds every CU (r4's halo_hide split the pass around it; r5 removed that for the in-kernel halo)
   virtual bool halo_cu_free() const { return false; }
   // true: peer_view() will give the peers' buffers once every rank has set up (and, for processes,
   // attached): the solver may then read its ghost lines straight from them (PassForm::halo_pull)

@@ -62,10 +62,6 @@ struct TileRanges {
   // slices down the grid, so a row's +-N (next/previous line) neighbours are the wave's own
   // previous/next slices: cache hits instead of a second/third HBM read of the same vector rows.
   int32_t strip = 0;
-  // 2-D Ap-recomputing carry (halo_hide): band 1 = the runs of lines [band_h, lines - band_h) only
-  // (no ghost line is read), band 2 = the runs of the band_h lines at each end of the rank (the
-  // ghost-adjacent lines, after the halo lands); 0 = every line in one launch
-  int32_t band = 0, band_h = 0;
   // 3-D plane carry: runs of planes per job column (> 0: chosen at setup by carry3_runs, so the
   // jobs fill whole rounds of the launch's blocks); 0 = blocks / jobs-per-run (at least 1)
   int32_t runs3 = 0;
@@ -326,11 +322,11 @@ bool sell_to_diav(const SellDev& S, int64_t line, double* cv, hipStream_t stream
 // nslot 5 or 7); returns the number of uniform slices (synchronises the stream)
 int64_t dia_patterns(const uint8_t* dia4, const double* dvals, int64_t ns, int64_t ss, int nslot, uint64_t* dpat,
                      hipStream_t stream);
-// 3-D (7-pt) Ap-recomputing plane carry (SELL-64/dia4 with ln = N): blocks of kw (4 / 8 / 16) waves on
+// 3-D (7-pt) Ap-recomputing plane carry (SELL-64/dia4 with ln = N): blocks of kw = 16 waves on
 // kw consecutive grid lines of one x slice; v.ap_old / ap_new = ext-layout Ap (outer lines, slice
 // edge rows, and with gfull the first / last plane for the ghosts); grid = blocks (any count).
 // With S.cvt set (SELL-64/diav 3-D, variable coefficients) the per-row values are streamed instead
-// (kw 4 / 8, 2 waves per SIMD: the lean loop's coefficient chain needs up to 256 VGPRs)
+// (kw = 8, 2 waves per SIMD: the lean loop's coefficient chain needs up to 256 VGPRs)
 void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64_t own_off, const TileRanges& tr,
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
                   int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
@@ -347,7 +343,7 @@ int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk = 0);
 // one launch): runs per slice column and lines per run
 void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk);
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream, int band = 0, int band_h = 0, int runs3 = 0);
+                            int32_t ln, hipStream_t stream, int runs3 = 0);
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals), 5 SELL-64/diav (S.cvd / cve / cvs,
 // variable coefficients; lean runs stream them: every run of >= 3 lines).  p3 (dia4): three-term form --
 // r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p buffers, r stored only at the slices' edge rows
@@ -396,7 +392,6 @@ void cg_split_spmv(int fmt, int param, const CsrDev<IdxT>& A, const SellDev& S, 
 // block at a time (sums in LDS) and all waves sweep the segments together (paced per segment), so
 // the gathers of p hit the L2.
 constexpr int kTileB = 1024;
-constexpr int kTileB5 = 960;  // tile_rows = 960: 30 KiB of row sums per workgroup, 5 workgroups per CU
 constexpr int kTileMaxSegments = 8192;  // LDS counters of the build kernels (32 KiB)
 constexpr int kTilePaceCnt = 8 * 64;     // pacing arrival counters: 8 groups, 256 B apart
 constexpr int kTilePaceWords = kTilePaceCnt + 8 * 8 * 64;  // + per group 8 replicas of its step flag, 256 B apart
@@ -409,33 +404,21 @@ struct TilesGeometry {
 struct TilesDev {
   const int64_t* tptr = nullptr;  // nblocks * G + 1
   const uint32_t* idx = nullptr;
-  const double* vals = nullptr;    // fp64 values, or
-  const float* vals32 = nullptr;   // values stored as fp32 (every value round-trips fp64 -> fp32 -> fp64 exactly,
-                                   // checked at build time; products and sums stay fp64): 8 instead of 12 B/entry
+  const double* vals = nullptr;
   int64_t n_rows = 0, nblocks = 0;
   int G = 0, seg_shift = 18;
-  int tb = kTileB;           // rows per block: kTileB (4 workgroups per CU) or kTileB5 (5)
-  int tu = 8;                // entries per lane in flight: 8 or 12 (kTileB only)
+  int tb = kTileB;           // rows per block
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
-  int pace_slack8 = 0;       // a workgroup waits for all but pace_slack8 / 8 of its group (0: all)
-  int pace_flag = 0;         // 1: the arrival that completes a step publishes it in a step flag and the waiters
-                             // poll the flag (an L2-resident line) instead of the hot arrival counter
-  int pace_lag = 0;          // a workgroup may start segment s + pace_lag before its group finished segment s
-  int pace_sleep = 8;        // s_sleep units (64 clocks) between two polls
-  int prefetch = 0;          // 1: touch the next segment's lines before the pacing wait (kernel comment)
   int64_t ext_len = 0;       // length of p (the last segment may be short)
   int g_lo = 0, g_hi = 0;    // the segments inside this rank's own block of p (all-gather overlap, part 1 / 2)
 };
-TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift, int tb = kTileB);
-int tiles_grid(int ncu, int tb = kTileB);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
-// count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0; *inexact += the
-// entries whose value is not exactly an fp32) then fill (into vals, or vals32 when vals is null)
+TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
+int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
+// count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0) then fill
 struct TilesOut {
   int64_t* tptr = nullptr;
   uint32_t* idx = nullptr;
   double* vals = nullptr;
-  float* vals32 = nullptr;
-  unsigned long long* inexact = nullptr;  // count pass
 };
 void tiles_build_gen(const ProblemSpec& s, int64_t row_begin, int64_t n, int64_t col_lo, int64_t pad,
                      const int64_t* rp64, const TilesGeometry& geo, const TilesOut& out, bool fill, hipStream_t st);

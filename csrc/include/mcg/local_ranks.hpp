@@ -19,7 +19,6 @@ struct LocalRankResult {
   double lean_split = 0.0;    // SolverInfo::lean_split of this rank
   bool p3 = false;            // SolverInfo::p3 (three-term carry form)
   double dia_uniform = 0.0;   // SolverInfo::dia_uniform (fraction of uniform slices)
-  bool halo_hide = false;     // SolverInfo::halo_hide of this rank
   bool halo_pull = false;     // SolverInfo::halo_pull of this rank
   bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)
   bool ag_overlap = false;     // SolverInfo::ag_overlap (own-block SpMV half || all-gather)

@@ -60,7 +60,6 @@ struct SolverInfo {
   bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
   bool tiles = false;         // ... its SpMV on L2-segment COO tiles (CgOptions::tiles)
   int tile_segments = 0;      // column segments of the tiles (G)
-  bool tile_vals32 = false;   // ... the tiles' values stored as fp32 (every value exact; CgOptions::tile_vals32)
   int sigma = 0;              // SELL-C-sigma window (rows) of a user matrix; 0 = slices in row order
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
   bool allgather = false;     // ghosts refreshed by all-gather (unstructured sparsity)
@@ -73,7 +72,6 @@ struct SolverInfo {
   bool graphs = false;        // iterations replayed as hipGraphs (false: eager launches)
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
-  bool halo_hide = false;  // PassForm::halo_hide: the pass split around a copy-engine halo
   bool halo_pull = false;  // PassForm::halo_pull: the in-kernel halo (ghost lines read from the peers' rows)
   bool diav = false;
   double aligned_fill = 0.0;  // user matrices: SELL-64/aligned slots per nonzero of the per-slice offset unions     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
@@ -161,7 +159,6 @@ class GpuCgSolver {
   bool prefetch_halo_ = false;  // single-reduction form: next iteration's halo right after the boundary pass
   int halo_ready_for_ = -1;     // iteration whose halo is already enqueued on s1_ (ev_h_)
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
-  bool hide_ = false;           // PassForm::halo_hide in effect: interior band || copy-engine halo, then the ends
   bool pull_ = false;           // PassForm::halo_pull in effect (in-kernel halo)
   int pull_from_ = 2;           // ... first iteration that pulls (reset / resume + 2: the earlier ones exchange)
   bool pull_mapped_ = false;    // ... pull_p_ / pull_ap_ resolved (map_pull_, at the first pulled pass)
@@ -169,7 +166,6 @@ class GpuCgSolver {
   const double* pull_ap_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [apx buffer][lo, hi side]
   std::vector<double*> halo_reg_;  // the buffers registered with the communicator (its peer_view order)
   void map_pull_();
-  bool split_side_ = true;     // lean_split: the generic launch on s2_, concurrent with the lean one
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
   bool ar_ = false;             // CgOptions::ap_recompute in effect
@@ -215,7 +211,6 @@ class GpuCgSolver {
   DeviceBuffer<int64_t> tptr_;
   DeviceBuffer<uint32_t> tidx_;
   DeviceBuffer<double> tvals_;
-  DeviceBuffer<float> tvals32_;  // the values as fp32 when every one is exact (tile_vals32)
   DeviceBuffer<unsigned> tpace_;
   int tg_lo_ = 0, tg_hi_ = 0;  // the tile segments inside the own block of p (all-gather overlap)
   kern::TilesDev tiles_view() const {
@@ -223,19 +218,12 @@ class GpuCgSolver {
     t.tptr = tptr_.get();
     t.idx = tidx_.get();
     t.vals = tvals_.get();
-    t.vals32 = tvals32_.get();
     t.n_rows = L_.n_local();
     t.nblocks = tgeo_.nblocks;
     t.G = tgeo_.G;
     t.seg_shift = tgeo_.seg_shift;
     t.tb = tgeo_.tb;
-    t.tu = opt_.form.tile_unroll == 12 ? 12 : 8;
-    t.pace = opt_.form.tile_pace > 0 ? tpace_.get() : nullptr;
-    t.pace_slack8 = (opt_.form.tile_pace == 2 || opt_.form.tile_pace == 4) ? std::max(0, std::min(7, opt_.form.tile_pace_slack)) : 0;
-    t.pace_flag = opt_.form.tile_pace >= 3 ? 1 : 0;
-    t.pace_lag = std::max(0, opt_.form.tile_pace_lag);
-    t.pace_sleep = std::max(1, std::min(64, opt_.form.tile_pace_sleep));
-    t.prefetch = opt_.form.tile_prefetch > 0 ? 1 : 0;
+    t.pace = tpace_.get();
     t.ext_len = L_.ext_len;
     t.g_lo = tg_lo_;
     t.g_hi = tg_hi_;

@@ -212,29 +212,16 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(window)
       MCG_FORM_PROP(pipeline)
       MCG_FORM_PROP(carry)
-      MCG_FORM_PROP(placement_tries)
-      MCG_FORM_PROP(placement_leads)
       MCG_FORM_PROP(fused_reduce)
       MCG_FORM_PROP(tiles)
       MCG_FORM_PROP(tile_seg_log2)
-      MCG_FORM_PROP(tile_rows)
-      MCG_FORM_PROP(tile_unroll)
-      MCG_FORM_PROP(tile_pace)
       MCG_FORM_PROP(carry_vc)
-      MCG_FORM_PROP(lean_depth)
-      MCG_FORM_PROP(lean_bpc)
-      MCG_FORM_PROP(lean_depth_odd)
       MCG_FORM_PROP(lean_split)
-      MCG_FORM_PROP(lean_split_side)
-      MCG_FORM_PROP(lean_bpc_odd)
-      MCG_FORM_PROP(halo_hide)
       MCG_FORM_PROP(halo_pull)
-      MCG_FORM_PROP(tile_pace_lag)
-      MCG_FORM_PROP(tile_pace_slack)
-      MCG_FORM_PROP(tile_pace_sleep)
-      MCG_FORM_PROP(tile_vals32)
-      MCG_FORM_PROP(tile_prefetch)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
+      .def_readwrite("graph_iters", &CgOptions::graph_iters)
+      .def_readwrite("placement_tries", &CgOptions::placement_tries)
+      .def_readwrite("placement_leads", &CgOptions::placement_leads)
       .def_readwrite("halo_mode", &CgOptions::halo_mode)
       MCG_FORM_PROP(pmat)
       MCG_FORM_PROP(sell_sigma)
@@ -245,13 +232,12 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(carry_dia)
       MCG_FORM_PROP(p3)
       MCG_FORM_PROP(dia_uniform)
-      MCG_FORM_PROP(carry3_kw)
-      MCG_FORM_PROP(carry3_runs)
       MCG_HOOK_PROP(fail_graph_launch_at)
       .def_readwrite("checkpoint_every", &CgOptions::checkpoint_every)
       .def_readwrite("checkpoint_path", &CgOptions::checkpoint_path)
       MCG_HOOK_PROP(force_idx64)
       MCG_HOOK_PROP(inject_nan_at)
+      MCG_HOOK_PROP(lean_packed)
       .def_readwrite("spmv_variant", &CgOptions::spmv_variant)
       .def_readwrite("maxit", &CgOptions::maxit)
       .def_readwrite("tol", &CgOptions::tol)
@@ -261,7 +247,6 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("reserve_cus", &CgOptions::reserve_cus)
       .def_readwrite("overlap", &CgOptions::overlap)
       .def_readwrite("use_graph", &CgOptions::use_graph)
-      MCG_FORM_PROP(graph_iters)
       .def_readwrite("force_comm", &CgOptions::force_comm)
       .def_readwrite("format", &CgOptions::format)
       .def_readwrite("blocks_per_cu", &CgOptions::blocks_per_cu);
@@ -491,7 +476,6 @@ PYBIND11_MODULE(_C, m) {
         d["pmat"] = i.pmat;
         d["tiles"] = i.tiles;
         d["tile_segments"] = i.tile_segments;
-        d["tile_vals32"] = i.tile_vals32;
         d["sigma"] = i.sigma;
         d["sell_fill"] = i.sell_fill;
         d["allgather"] = i.allgather;
@@ -504,7 +488,6 @@ PYBIND11_MODULE(_C, m) {
         d["xcd_map"] = i.xcd_map;
         d["dia4"] = i.dia4;
         d["diav"] = i.diav;
-        d["halo_hide"] = i.halo_hide;
         d["halo_pull"] = i.halo_pull;
         d["aligned_fill"] = i.aligned_fill;
         d["p3"] = i.p3;
@@ -550,7 +533,6 @@ PYBIND11_MODULE(_C, m) {
       d["lean_split"] = rr.lean_split;
       d["p3"] = rr.p3;
       d["dia_uniform"] = rr.dia_uniform;
-      d["halo_hide"] = rr.halo_hide;
       d["halo_pull"] = rr.halo_pull;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;

@@ -30,7 +30,7 @@ def test_lean_carry_past_2_29_rows_matches_generic(mcg, problem, n):
     iters = 6
     # the 2-D lean grid on the generic kernels' grid (8 blocks per CU), so the block partials -- and
     # with them the dot products' rounding -- are the same and the comparison is bit for bit
-    kw = dict(lean_bpc=8) if problem == "poisson2d" else {}
+    kw = dict(blocks_per_cu=8) if problem == "poisson2d" else {}
     info_l, x_l = _run(mcg, spec, iters, **kw)
     assert info_l["lean_only"] and info_l["p3"] and info_l["ap_recompute"], info_l
     assert info_l["ext_len"] >= (1 << 29)

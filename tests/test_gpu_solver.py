@@ -295,17 +295,16 @@ def test_ap_recompute_bitwise_equal_to_stored_pairs(mcg, codes, n):
     assert a.true_residual_norm() == b.true_residual_norm()
 
 
-@pytest.mark.parametrize("problem,n,kw", [("poisson2d", 128, 0), ("poisson2d", 256, 0), ("poisson2d", 512, 0),
-                                          ("poisson3d", 64, 4), ("poisson3d", 128, 16)])
-def test_three_term_carry_tracks_two_term(mcg, problem, n, kw):
+@pytest.mark.parametrize("problem,n", [("poisson2d", 128), ("poisson2d", 256), ("poisson2d", 512),
+                                       ("poisson3d", 64), ("poisson3d", 128)])
+def test_three_term_carry_tracks_two_term(mcg, problem, n):
     """Three-term form of the dia4 line carry (r_{k-1} = p_{k-1} - beta p_{k-2} from the two stored p's,
     r kept only at slice edges and run outer lines): the same CG iterates up to rounding -- same
     iteration count (+-1), x and ||r|| to ~1e-9 -- against the two-term form, at convergence and at
     fixed odd / even counts (final pass, paired x updates); the recurrence residual tracks ||b - A x||."""
     spec = mcg.make_problem(problem, n=n, rhs="random")
-    k3 = dict(carry3_kw=kw) if kw else {}
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, p3=1, check_every=8, **k3)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, p3=0, check_every=8, **k3)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, p3=1, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, p3=0, check_every=8)
     assert a.info["p3"] and a.info["dia4"] and a.info["ap_recompute"] and not b.info["p3"]
     assert a.info["bytes_per_iter_model"] < b.info["bytes_per_iter_model"]
     ra, rb = a.solve(), b.solve()
@@ -332,17 +331,17 @@ def test_three_term_carry_refusal(mcg):
         mcg.CGSolver(mcg.make_problem("poisson2d", n=256), format="sellc8", recurrence=1, carry_dia=0, p3=1)
 
 
-@pytest.mark.parametrize("n,kw", [(64, 4), (128, 4), (128, 8), (128, 16)])
-def test_ap_recompute_3d_matches_store_form(mcg, n, kw):
+@pytest.mark.parametrize("n", [64, 128])
+def test_ap_recompute_3d_matches_store_form(mcg, n):
     """3-D plane carry that recomputes Ap (SELL-64/dia4, +-N rows through LDS between the block's
     kw waves, the outer lines' Ap stored): the same recurrence as the store-form plane carry.  Its runs
     of planes per job column are chosen to fill whole rounds of blocks (carry3_runs), so the
     dot-product partials group differently from the store form's: the same iterations, rounding only
-    (kw = 4 agreed bit for bit while both used one run per column)."""
+    (kw = 4, pruned in r5, agreed bit for bit while both used one run per column)."""
     spec = mcg.make_problem("poisson3d", n=n, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=1, carry3_kw=kw, p3=0, check_every=8)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=1, p3=0, check_every=8)
     b = mcg.CGSolver(spec, format="sellc8", recurrence=1, ap_recompute=0, check_every=8)
-    assert a.info["ap_recompute"] and a.info["dia4"] and a.info["ar3_kw"] == kw
+    assert a.info["ap_recompute"] and a.info["dia4"] and a.info["ar3_kw"] == 16
     assert not b.info["ap_recompute"] and b.info["carry"]
     ra, rb = a.solve(), b.solve()
     assert ra["converged"] and abs(ra["iterations"] - rb["iterations"]) <= 1
@@ -450,16 +449,16 @@ def test_dia_uniform_lean_runs_bitwise(mcg, n):
         assert np.array_equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("n,kw", [(128, 16), (128, 8), (128, 4), (256, 16)])
-def test_dia_uniform_lean_runs_bitwise_3d(mcg, n, kw):
+@pytest.mark.parametrize("n", [128, 256])
+def test_dia_uniform_lean_runs_bitwise_3d(mcg, n):
     """Lean runs of the 3-D three-term plane carry (per wave: the seven values in scalar registers,
     no codes streamed; the block takes them when every wave's run qualifies): x and ||r|| bit for
-    bit against dia_uniform = 0.  Runs of 8 / 4 planes at n = 128, 64 at n = 256, including the
+    bit against dia_uniform = 0.  Runs of a few planes at n = 128, 64 at n = 256, including the
     grid's first / last planes and the x / y boundary slices."""
     spec = mcg.make_problem("poisson3d", n=n, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, carry3_kw=kw)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, carry3_kw=kw, dia_uniform=0)
-    assert a.info["p3"] and a.info["ar3_kw"] == kw and a.info["dia_uniform"] > 0.99
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, dia_uniform=0)
+    assert a.info["p3"] and a.info["ar3_kw"] == 16 and a.info["dia_uniform"] > 0.99
     for its in (21, 22):
         outs = []
         for s in (a, b):
@@ -469,57 +468,6 @@ def test_dia_uniform_lean_runs_bitwise_3d(mcg, n, kw):
             outs.append((s.result(), s._s.x_local()))
         assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
         assert np.array_equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize("n,depth,bpc", [(1024, 13, 5), (2048, 13, 5), (2048, 14, 4), (1024, 14, 4)])
-def test_lean_packed_edges_bitwise(mcg, n, depth, bpc):
-    """Packed edges (lean_depth 13: prefetch depth 3 at 5 waves per SIMD; 14: depth 4 at 4): a
-    slice-edge lane's three neighbour values arrive in one load per line and move to lanes 0 / 63 by
-    DPP mirrors.  The same arithmetic in the same order, so x and ||r|| are bit for bit those of the
-    default lean kernels on the same grid (lean_bpc fixes the job decomposition for both)."""
-    spec = mcg.make_problem("poisson2d", n=n, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=bpc)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=bpc, lean_depth=depth)
-    assert a.info["lean_only"] and b.info["lean_only"] and a.info["grid_a"] == b.info["grid_a"]
-    for its in (37, 38):
-        outs = []
-        for s in (a, b):
-            s.reset()
-            s.run(its)
-            s.finalize()
-            outs.append((s.result(), s._s.x_local()))
-        assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
-        assert np.array_equal(outs[0][1], outs[1][1])
-
-
-def test_lean_odd_passes_own_grid_bitwise(mcg):
-    """lean_bpc_odd / lean_depth_odd: the odd passes (x update paired in) on a grid and prefetch depth
-    of their own -- here the packed-edge kernels at 5 waves per SIMD for the even passes and depth 4
-    at 4 for the odd ones -- bit for bit the default kernels on the same two grids (each grid reduces
-    its own block partials, through the phase profile as well)."""
-    spec = mcg.make_problem("poisson2d", n=2048, rhs="random")
-    kw = dict(format="sellc8", recurrence=1, check_every=8, lean_bpc=5, lean_bpc_odd=4)
-    a = mcg.CGSolver(spec, **kw)
-    b = mcg.CGSolver(spec, lean_depth=13, lean_depth_odd=14, **kw)
-    for s in (a, b):
-        assert s.info["lean_only"] and s.info["grid_odd"] == s.info["grid_a"] * 4 // 5
-    for its in (21, 22):
-        outs = []
-        for s in (a, b):
-            s.reset()
-            s.run(its)
-            s.finalize()
-            outs.append((s.result(), s._s.x_local()))
-        assert outs[0][0]["rnorm"] == outs[1][0]["rnorm"]
-        assert np.array_equal(outs[0][1], outs[1][1])
-    one = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=5)
-    one.reset()
-    one.run(22)
-    one.finalize()
-    assert abs(one.result()["rnorm"] - outs[0][0]["rnorm"]) <= 1e-12 * outs[0][0]["rnorm"]
-    b.reset()
-    ph = b._s.phase_profile(8)
-    assert ph["iteration"] > 0
 
 
 def test_lean_mix_auto_on_small_grids(mcg):
@@ -530,13 +478,17 @@ def test_lean_mix_auto_on_small_grids(mcg):
     spec = mcg.make_problem("poisson2d", n=4096, rhs="random")
     a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8)
     assert a.info["lean_only"] and a.info["lean_mix"] and a.info["grid_odd"] == a.info["grid_a"] * 4 // 5
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_bpc=5, lean_bpc_odd=4)
-    assert not b.info["lean_mix"] and b.info["grid_odd"] == a.info["grid_odd"]
-    for s in (a, b):
-        s.reset()
-        s.run(15)
-        s.finalize()
-    assert a.result()["rnorm"] == b.result()["rnorm"]
-    assert np.array_equal(a._s.x_local(), b._s.x_local())
+    # the same two grids with the default lean kernels (test hook): packed edges are bit for bit those
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, lean_packed=0)
+    assert not b.info["lean_mix"] and b.info["grid_odd"] == a.info["grid_odd"] and b.info["grid_a"] == a.info["grid_a"]
+    for its in (15, 38):
+        for s in (a, b):
+            s.reset()
+            s.run(its)
+            s.finalize()
+        assert a.result()["rnorm"] == b.result()["rnorm"]
+        assert np.array_equal(a._s.x_local(), b._s.x_local())
+    b.reset()
+    assert b._s.phase_profile(8)["iteration"] > 0
     big = mcg.CGSolver(mcg.make_problem("poisson2d", n=8192), format="sellc8", recurrence=1)
     assert big.info["lean_only"] and not big.info["lean_mix"] and big.info["grid_odd"] == 0

@@ -275,9 +275,8 @@ def test_lean_split_converges_like_the_generic_pass(mcg):
     og = g.solve()
     assert og["converged"]
     tg = g.true_residual_norm()
-    for side in (1, 0):  # the generic launch beside the lean one (default) / after it
-        s = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=1, lean_split_side=side, tol=1e-8,
-                         maxit=20000)
+    for graph in (True, False):
+        s = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=1, use_graph=graph, tol=1e-8, maxit=20000)
         assert s.info["lean_split"] > 0.9 and not s.info["lean_only"]
         os_ = s.solve()
         assert os_["converged"]
@@ -304,23 +303,22 @@ def test_lean_split_mixed_ranks_match_one_rank(mcg, world, lines):
     p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
     C = mcg.native()
 
-    def run(w, ls, side=1, overlap=True):
+    def run(w, ls, overlap=True):
         o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
         o.lean_split = ls
-        o.lean_split_side = side
         o.overlap = overlap
         return C.run_local_ranks(p.native(), o, w, 40, True)
 
     one = run(1, 0)
     r1 = one["ranks"][0]["rnorm"]
-    for ls, side, ov in ((1, 1, True), (1, 0, True), (1, 1, False), (0, 1, True)):
-        out = run(world, ls, side, ov)
+    for ls, ov in ((1, True), (1, False), (0, True)):
+        out = run(world, ls, ov)
         split = [rk["lean_split"] > 0 for rk in out["ranks"]]
         if ls == 1:
             assert any(split) and not all(split), split  # split ranks next to lean-only ones
             assert all(rk["lean_only"] for rk, sp_ in zip(out["ranks"], split) if not sp_)
         rp = out["ranks"][0]["rnorm"]
-        assert abs(rp - r1) <= 1e-13 * r1, (ls, side, ov, rp, r1)
+        assert abs(rp - r1) <= 1e-13 * r1, (ls, ov, rp, r1)
         np.testing.assert_allclose(out["x"], one["x"], rtol=1e-11, atol=1e-13 * np.abs(one["x"]).max())
 
 
