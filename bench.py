@@ -105,10 +105,11 @@ def parse_args(argv=None):
                          "communicators in flight at once)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL collectives also with one rank (1-rank communicator): the N > 1 code path")
-    ap.add_argument("--halo-transport", default="rccl", choices=["rccl", "sdma"],
-                    help="sdma: the halo on copy engines (PeerHaloComm: the neighbours' buffers mapped through IPC, "
-                         "flags by stream memory operations; all-reduce on RCCL); the lean carries read the mapped "
-                         "rows in-kernel instead (halo_pull)")
+    ap.add_argument("--halo-transport", default="auto", choices=["auto", "rccl", "sdma"],
+                    help="auto (N > 1): the neighbours' buffers mapped through IPC (PeerHaloComm) for the lean "
+                         "carries' in-kernel halo (halo_pull: checked at setup, off again if any rank cannot map or "
+                         "reads a wrong row), every remaining halo exchange and the all-reduce on RCCL; rccl: no "
+                         "mapping; sdma: the halo exchanges on copy engines (flags by stream memory operations)")
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "ipc"],
                     help="ipc: the 32-byte all-reduce through IPC-mapped mailboxes (PeerHaloComm + "
                          "csrc/gpu/ipc_allreduce.hip, no RCCL; implies the peer-mapped halo).  With --rehearse-ranks "
@@ -216,15 +217,18 @@ def _run_rank(args, out_fd) -> int:
     t_setup = time.perf_counter()
     ipc_ar = args.allreduce == "ipc" and comm is not None and not sim
     sdma = (args.halo_transport == "sdma" or ipc_ar) and comm is not None and not sim
+    # auto: the mapping for the in-kernel halo, the exchanges on the inner communicator (a rehearsal's
+    # inner moves nothing: there only the real P-rank form, ipc_ar, takes the copy-engine exchanges)
+    mapped = (sdma or args.halo_transport == "auto") and comm is not None and not sim and env.world > 1
     base_comm = comm  # RCCL's (or the rehearsal's) communicator: the count, the all-reduce
-    if sdma:
-        comm = pdist.peer_halo(comm, env, ipc_allreduce=ipc_ar)
+    if mapped:
+        comm = pdist.peer_halo(comm, env, ipc_allreduce=ipc_ar, halo_via_inner=not sdma)
     real = not sim and (not rehearse or ipc_ar)  # a real P-rank solve (its residual must track)
     solver = (C.Solver(spec.native(), opts, args.sim_rank, args.sim_world, comm) if sim
               else C.Solver(spec.native(), opts, env.rank, env.world, comm))
     solver.setup()
-    if sdma:
-        pdist.attach_peer_halo(comm, env)
+    if mapped:
+        pdist.attach_peer_halo(comm, env, tolerant=not sdma)
     solver.reset()
     setup_s = time.perf_counter() - t_setup
 
@@ -349,8 +353,8 @@ def _run_rank(args, out_fd) -> int:
                 "halo_overlap": (not args.no_overlap) and n_gpus > 1 and args.comm == "dual",
                 "comm": args.comm,
                 **({"halo_transport": ("in-kernel (the pass reads the IPC-mapped neighbour rows)" if info.get("halo_pull")
-                                       else "sdma (copy engines, IPC)"),
-                    "allreduce": "ipc (mapped mailboxes)" if ipc_ar else "rccl"} if sdma else {}),
+                                       else "sdma (copy engines, IPC)" if sdma else "rccl (mapping unused)"),
+                    "allreduce": "ipc (mapped mailboxes)" if ipc_ar else "rccl"} if mapped else {}),
                 "launch": route,
                 **({"reserve_cus": opts.reserve_cus} if opts.reserve_cus else {}),
             },

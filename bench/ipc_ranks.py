@@ -27,7 +27,7 @@ def _opts(C, a):
     o.halo_pull = a.halo_pull
     o.pipe_rr = a.pipe_rr
     o.use_graph = not a.no_graph
-    o.watchdog_seconds = 120.0
+    o.watchdog_seconds = 60.0
     return o
 
 
@@ -35,6 +35,12 @@ def _spec(mcg, a):
     if a.problem == "scrambled":  # irregular: the all-gather layout, the split pass (single exchanged p)
         return mcg.make_problem("randspd", rows=a.rows, band=16, density=0.5, scramble=1, rhs="random").native()
     return mcg.make_problem(a.problem, n=a.n, rhs="random", coef=a.coef).native()
+
+
+def log(rank, msg):
+    import time
+
+    print(f"[rank {rank}] {time.strftime('%X')} {msg}", file=sys.stderr, flush=True)
 
 
 def rank_main(rank: int, a, port: int, q) -> None:
@@ -50,16 +56,23 @@ def rank_main(rank: int, a, port: int, q) -> None:
     env = pdist.DistEnv(rank=rank, world=a.world, local_rank=0)
     C = mcg.native()
     comm = pdist.peer_halo(C.NullComm(rank, a.world), env, ipc_allreduce=True)
+    comm.ar_budget_seconds = a.budget
+    log(rank, "mailboxes mapped")
     s = C.Solver(_spec(mcg, a), _opts(C, a), rank, a.world, comm)
     s.setup()
+    log(rank, "setup done")
     pdist.attach_peer_halo(comm, env)
     s.reset()
+    log(rank, "reset done")
     s.run_iterations(a.iters)
     s.synchronize()
+    log(rank, "iterations done")
     s.finalize()
     res = s.result()
+    log(rank, "finalized")
     x = np.asarray(s.x_local())
     tr = s.true_residual_norm()
+    log(rank, "true residual done")
     info = s.info
     q.put((rank, float(res["rnorm"]), int(res["iterations"]), x.tobytes(), float(tr),
            bool(info.get("halo_pull")), bool(info.get("lean_only")), int(info.get("graph_fallbacks", 0)),
@@ -83,6 +96,7 @@ def main() -> int:
     ap.add_argument("--tol", type=float, default=1e-13, help="relative gap allowed against one rank")
     ap.add_argument("--port", type=int, default=29541)
     ap.add_argument("--timeout", type=float, default=180.0)
+    ap.add_argument("--budget", type=float, default=60.0, help="IPC all-reduce: seconds a peer may be late")
     a = ap.parse_args()
     import torch.multiprocessing as mp
 
@@ -91,13 +105,25 @@ def main() -> int:
     procs = [ctx.Process(target=rank_main, args=(r, a, a.port, q)) for r in range(a.world)]
     for p in procs:
         p.start()
+    import time
+
+    import queue
+
+    # read the results before joining: a child that put a large x on the queue exits only once the
+    # queue's feeder thread has handed it over
+    t_end = time.time() + a.timeout
+    res = []
+    try:
+        for _ in procs:
+            res.append(q.get(timeout=max(1.0, t_end - time.time())))
+    except queue.Empty:
+        res = []
     for p in procs:
-        p.join(timeout=a.timeout)
+        p.join(timeout=max(1.0, t_end - time.time()))
     for p in procs:  # a rank stuck (its all-reduce times out on its own budget): end it
         if p.is_alive():
             p.kill()
-            p.join()
-    res = sorted(q.get(timeout=5) for _ in procs) if all(p.exitcode == 0 for p in procs) else []
+    res = sorted(res) if len(res) == len(procs) and all(p.exitcode == 0 for p in procs) else []
     out = {"world": a.world, "problem": a.problem, "n": a.n, "coef": a.coef, "iters": a.iters,
            "recurrence": a.recurrence, "pipe_rr": a.pipe_rr,
            "halo_pull_opt": a.halo_pull, "graphs": not a.no_graph, "exitcodes": [p.exitcode for p in procs]}

@@ -242,6 +242,11 @@ __host__ __device__ __forceinline__ void carry_run(int64_t job, int64_t ss, int6
   l1 = l0 + chunk < nl ? l0 + chunk : nl;
 }
 
+__global__ __launch_bounds__(256) void k_pull_probe(const double* __restrict__ base, int64_t n, double* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = ld_sys(base + i, 0u);
+}
+
 // per-slice metadata for the carry's codes loads: first slot / 64 (28 bits) | width << 28
 __global__ void k_slice_meta(const int64_t* __restrict__ slice_ptr, int64_t ns, uint32_t* __restrict__ meta) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
@@ -2212,6 +2217,13 @@ int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk) {
     }
   }
   return best;
+}
+
+void pull_probe(const double* base, int64_t n, double* out, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pull_probe, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0, stream, base, n,
+                     out);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(pull probe)");
 }
 
 void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk) {

@@ -10,7 +10,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "mcg/check.hpp"
 #include "mcg/comm.hpp"
@@ -85,12 +87,16 @@ PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int wo
   // the IPC all-reduce's mailbox: uncached device memory (every access goes to memory, so a flag a peer
   // wrote over the fabric is never served from a stale cache line), zeroed: call counters start at 0
   MCG_CHECK(world <= kern::kIpcMaxRanks, "peer halo: too many ranks for the IPC all-reduce mailboxes");
+  // (MCG_IPC_MAILBOX=cached: plain hipMalloc memory, a diagnostic)
   const size_t mb_bytes = mailbox_bytes(world);
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&mbox_), mb_bytes, hipDeviceMallocUncached) != hipSuccess) {
+  const char* mk = std::getenv("MCG_IPC_MAILBOX");
+  const bool cached = mk != nullptr && std::string(mk) == "cached";
+  if (cached || hipExtMallocWithFlags(reinterpret_cast<void**>(&mbox_), mb_bytes, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();
     MCG_HIP(hipMalloc(&mbox_, mb_bytes), "device malloc failed(ipc mailbox)");
   }
   MCG_HIP(hipMemset(mbox_, 0, mb_bytes), "device memset failed(ipc mailbox)");
+  MCG_HIP(hipDeviceSynchronize(), "device synchronize failed(ipc mailbox)");  // zeroed before any peer maps it
   MCG_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(unsigned long long),
                         hipHostMallocMapped | hipHostMallocCoherent),
           "host malloc failed(ipc all-reduce)");
@@ -238,6 +244,10 @@ bool PeerHaloComm::peer_view(int q, std::vector<double*>& bufs, int64_t& own_off
 // flags would come too late: the solver calls this first (torn ghost rows otherwise).
 // The readers' done flags of exchange seq_ carry v(seq_); the next exchange waits for the same value.
 void PeerHaloComm::halo_fence(hipStream_t stream) {
+  if (halo_inner_) {
+    inner_->halo_fence(stream);
+    return;
+  }
   if (seq_ == 0 || last_readers_.empty()) return;
   const uint64_t v = 1 + (uint64_t)(seq_ % 2);
   for (int q : last_readers_)
@@ -253,6 +263,10 @@ std::vector<uintptr_t> PeerHaloComm::peer_buffers(int q) const {
 void PeerHaloComm::halo_exchange(const LocalLayout& L, double* const* ext_vecs, int nvec, hipStream_t stream,
                                  const int* widths) {
   if (!L.has_halo()) return;
+  if (halo_inner_) {
+    inner_->halo_exchange(L, ext_vecs, nvec, stream, widths);
+    return;
+  }
   for (int k = 0; k < nvec; ++k)  // a vector outside the iteration's set (true residual's temporary x)
     if (std::find(bufs_.begin(), bufs_.end(), ext_vecs[k]) == bufs_.end()) {
       inner_->halo_exchange(L, ext_vecs, nvec, stream, widths);

@@ -97,6 +97,7 @@ void GpuCgSolver::reset() {
   // a halo prefetched by the last iteration may still be sending / receiving rows of r, Ap and p
   // on s1_: order the memsets below after it (no write of s0_ may race the side stream's RCCL)
   join_halo_();
+  if (pull_ && !pull_checked_) verify_pull_();  // (writes the p / apx lines the memsets below clear)
   MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
   for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1], &w_, &z_, &q_})
     if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
@@ -245,7 +246,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     if (pull_ && !probing_ && !final_mode) {  // in-kernel halo (cg_carry_ar.hip PullBases)
       v.pull_pub = 1;
       if (k >= pull_from_) {
-        map_pull_();
+        MCG_CHECK(map_pull_(), "in-kernel halo: the peers' buffers are not mapped (attach the communicator)");
         const int pb = (k + 1) & 1;  // p_old / apx_old: the neighbours' pass k-1 outputs
         for (int sd = 0; sd < 2; ++sd) {
           v.pull_p[sd] = pull_p_[pb][sd];
@@ -612,8 +613,8 @@ void GpuCgSolver::enqueue_iteration_(int k) {
 // that this rank's ext index of a ghost row addresses the owner's copy of the same global row.  With a
 // rehearsal communicator (no peers, no data moved) the rank's own first / last line stands in for the
 // neighbours' (timing only, like NullComm's collectives).
-void GpuCgSolver::map_pull_() {
-  if (pull_mapped_) return;
+bool GpuCgSolver::map_pull_() {
+  if (pull_mapped_) return true;
   auto idx = [&](const double* b) {
     auto it = std::find(halo_reg_.begin(), halo_reg_.end(), b);
     MCG_CHECK(it != halo_reg_.end(), "in-kernel halo: buffer not registered");
@@ -633,10 +634,11 @@ void GpuCgSolver::map_pull_() {
     if (comm_->peer_view(h->peer, bufs, q_own, q_rb)) {
       MCG_CHECK(bufs.size() == halo_reg_.size(), "in-kernel halo: ranks registered different buffer lists");
       src = q_own + (h->gbegin - q_rb);  // the owner's ext index of the first ghost row
-    } else {
-      MCG_CHECK(!comm_->moves_data(), "in-kernel halo: the communicator cannot map the peers' buffers");
+    } else if (!comm_->moves_data()) {
       bufs = halo_reg_;  // rehearsal stand-in: this rank's own first / last line
       src = L_.own_off + (sd == 0 ? 0 : L_.n_local() - line);
+    } else {
+      return false;  // not mapped (a transport that was never attached, or whose mapping failed)
     }
     const int64_t shift = src - L_.ext_index(h->gbegin);
     for (int b = 0; b < 2; ++b) {
@@ -645,6 +647,55 @@ void GpuCgSolver::map_pull_() {
     }
   }
   pull_mapped_ = true;
+  return true;
+}
+
+// The in-kernel halo's check (the first reset, before the state is written; every rank takes part):
+// each rank writes a pattern of its global row numbers into its first / last line of both p and both
+// apx buffers, one all-reduce orders the ranks as the iterations will, and each rank reads its ghost
+// lines back through the pull pointers with the pass's loads.  A rank that cannot map its peers, or
+// reads a wrong value, turns it off on every rank: the halo is then exchanged, as before r5.  (A
+// rehearsal communicator moves no data: its stand-in pointers are only mapped.)
+void GpuCgSolver::verify_pull_() {
+  pull_checked_ = true;
+  const bool mapped = map_pull_();
+  bool ok = all_ranks_agree_(mapped);
+  if (ok && comm_->moves_data()) {
+    const int64_t line = (int64_t)tr_all_.strip * 64, n = L_.n_local();
+    DeviceBuffer<double>* bufs[4] = {&p_[0], &p_[1], &apx_[0], &apx_[1]};
+    std::vector<double> hv(line);
+    auto pattern = [&](int64_t g0, int i) {
+      for (int64_t t = 0; t < line; ++t) hv[t] = (double)(g0 + t) + 0.25 * i;
+    };
+    for (int i = 0; i < 4; ++i)
+      for (int e = 0; e < 2 && n >= line; ++e) {
+        const int64_t l0 = e == 0 ? 0 : n - line;
+        pattern(L_.row_begin + l0, i);
+        MCG_HIP(hipMemcpy(bufs[i]->get() + L_.own_off + l0, hv.data(), line * sizeof(double), hipMemcpyHostToDevice),
+                "memcpy from host to device failed(pull check)");
+      }
+    MCG_HIP(hipDeviceSynchronize(), "device synchronize failed(pull check)");
+    (void)all_ranks_agree_(true);  // every rank's pattern is in place (the order pass k -> pass k + 1 relies on)
+    DeviceBuffer<double> got(line, "pull check");
+    bool match = true;
+    for (int sd = 0; sd < 2; ++sd)
+      for (int i = 0; i < 4 && pull_p_[0][sd] != nullptr; ++i) {
+        const double* base = (i < 2 ? pull_p_[i & 1][sd] : pull_ap_[i & 1][sd]);
+        const int64_t g0 = sd == 0 ? L_.row_begin - line : L_.row_end;
+        kern::pull_probe(base + L_.ext_index(g0), line, got.get(), s0_);
+        MCG_HIP(hipMemcpyAsync(hv.data(), got.get(), line * sizeof(double), hipMemcpyDeviceToHost, s0_),
+                "memcpy from device to host failed(pull check)");
+        MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed(pull check)");
+        for (int64_t t = 0; t < line && match; ++t) match = hv[t] == (double)(g0 + t) + 0.25 * i;
+      }
+    ok = all_ranks_agree_(match);
+  }
+  if (!ok) {
+    if (rank_ == 0) std::fprintf(stderr, "[mcg] in-kernel halo check failed (peers not mapped, or a pulled row was wrong): "
+                                         "the halo is exchanged instead\n");
+    pull_ = false;
+    info_.halo_pull = false;
+  }
 }
 
 void GpuCgSolver::join_halo_() {

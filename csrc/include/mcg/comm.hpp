@@ -230,9 +230,15 @@ class PeerHaloComm final : public Communicator {
   bool graph_capturable() const override { return inner_->graph_capturable() && capturable_; }
   bool moves_data() const override { return ipc_ar_ || inner_->moves_data(); }
   void abort() override { inner_->abort(); }
-  bool serialized() const override { return false; }  // the halo never enters the inner communicator
-  bool halo_cu_free() const override { return true; }
+  // the copy-engine halo never enters the inner communicator; with halo_via_inner it is the inner's
+  bool serialized() const override { return halo_inner_ && inner_->serialized(); }
+  bool halo_cu_free() const override { return !halo_inner_; }
   bool maps_peers() const override { return true; }
+  // the mapping only (the in-kernel halo), the exchanges that remain (the first iterations, finalize,
+  // the true residual) on the inner communicator's halo -- RCCL's send/recv: the P > 1 default, where
+  // nothing but the pass's own pulled rows depends on the mapping
+  void set_halo_via_inner(bool v) { halo_inner_ = v; }
+  bool halo_via_inner() const { return halo_inner_; }
   void register_halo_buffers(const std::vector<double*>& bufs, int64_t own_off, int64_t row_begin) override;
   bool peer_view(int q, std::vector<double*>& bufs, int64_t& own_off, int64_t& row_begin) override;
   void on_captured(bool kept) override;
@@ -267,6 +273,7 @@ class PeerHaloComm final : public Communicator {
   unsigned long long* err_host_ = nullptr;       // pinned, device-mapped error word of the IPC all-reduce
   kern::IpcMailboxes mb_;
   bool ipc_ar_ = false;
+  bool halo_inner_ = false;
   long seq_ = 0;
   std::vector<int> last_readers_;  // the ranks that pull this rank's rows of exchange seq_
   long cap_n_ = 0;  // exchanges recorded by the capture in progress

@@ -342,6 +342,9 @@ int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk = 0);
 // the 2-D carry's job decomposition of a launch of nw waves over nl lines of ss slices (every line in
 // one launch): runs per slice column and lines per run
 void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk);
+// the in-kernel halo's setup check: out[i] = base[i] for i < n, loaded like the pass loads a pulled
+// ghost line (system scope)
+void pull_probe(const double* base, int64_t n, double* out, hipStream_t stream);
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
                             int32_t ln, hipStream_t stream, int runs3 = 0);
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals), 5 SELL-64/diav (S.cvd / cve / cvs,

@@ -161,11 +161,13 @@ class GpuCgSolver {
   bool halo_ahead_ = false;     // CgOptions::halo_ahead in effect
   bool pull_ = false;           // PassForm::halo_pull in effect (in-kernel halo)
   int pull_from_ = 2;           // ... first iteration that pulls (reset / resume + 2: the earlier ones exchange)
-  bool pull_mapped_ = false;    // ... pull_p_ / pull_ap_ resolved (map_pull_, at the first pulled pass)
+  bool pull_mapped_ = false;    // ... pull_p_ / pull_ap_ resolved (map_pull_)
+  bool pull_checked_ = false;   // ... verify_pull_ ran (the first reset)
   const double* pull_p_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [p buffer][lo, hi side]
   const double* pull_ap_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [apx buffer][lo, hi side]
   std::vector<double*> halo_reg_;  // the buffers registered with the communicator (its peer_view order)
-  void map_pull_();
+  bool map_pull_();     // false: a peer's buffers are not mapped here (not attached)
+  void verify_pull_();  // the first reset: every rank reads a pattern through the pull pointers, or pull_ goes off
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
   bool ar_ = false;             // CgOptions::ap_recompute in effect

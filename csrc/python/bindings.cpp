@@ -378,6 +378,7 @@ PYBIND11_MODULE(_C, m) {
         c.attach_mailbox(v);
       }, "map every rank's IPC all-reduce mailbox; from then on the all-reduce runs through them")
       .def_property_readonly("ipc_allreduce", &PeerHaloComm::ipc_allreduce)
+      .def_property("halo_via_inner", &PeerHaloComm::halo_via_inner, &PeerHaloComm::set_halo_via_inner)
       .def_readwrite("ar_budget_seconds", &PeerHaloComm::ar_budget_seconds)
       .def("allreduce_ptr", [](PeerHaloComm& c, uintptr_t buf, size_t count, uintptr_t stream) {
         c.allreduce_sum(reinterpret_cast<double*>(buf), count, as_stream(stream));

@@ -64,14 +64,17 @@ def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "single"):
     return C.Comm(env.rank, env.world, *ids)
 
 
-def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False):
+def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False, halo_via_inner: bool = False):
     """Wrap a communicator so that the halo moves without RCCL (native ``PeerHaloComm``: the
     neighbours' buffers mapped through IPC handles -- pulled by copy engines, or read by the lean
     passes themselves, PassForm::halo_pull); the all-reduce stays on ``inner`` unless
     ``ipc_allreduce``: then every rank's mailbox is mapped here (collective) and the all-reduce runs
     through them (ipc_allreduce.hip) -- real P-rank sums with no RCCL, e.g. P processes on one GPU.
-    Call :func:`attach_peer_halo` after the solver's ``setup()``."""
+    ``halo_via_inner``: only the mapping (the lean passes' in-kernel halo); every halo exchange that
+    remains goes to ``inner`` (RCCL's send/recv).  Call :func:`attach_peer_halo` after the solver's
+    ``setup()``."""
     comm = native().PeerHaloComm(inner, env.rank, env.world)
+    comm.halo_via_inner = halo_via_inner
     if ipc_allreduce:
         mine = comm.mailbox_handle()
         allb = [mine]
@@ -84,18 +87,31 @@ def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False):
     return comm
 
 
-def attach_peer_halo(comm, env: DistEnv) -> None:
+def attach_peer_halo(comm, env: DistEnv, tolerant: bool = False) -> bool:
     """Exchange every rank's IPC handles (registered by the solver's setup) over torch.distributed
-    and map the peers' halo buffers.  Collective: every rank calls it once, after ``setup()``."""
+    and map the peers' halo buffers.  Collective: every rank calls it once, after ``setup()``.
+    ``tolerant``: a rank whose mapping fails stays unattached instead of raising (the solver then
+    agrees with every rank, at its next reset, not to read peer rows: the in-kernel halo's check);
+    returns whether this rank attached."""
+    import sys
+
     mine = comm.local_handles()
     if env.world == 1:
-        comm.attach([mine])
-        return
-    if not dist.is_initialized():
-        raise RuntimeError("attach_peer_halo needs torch.distributed initialised")
-    allb = [None] * env.world
-    dist.all_gather_object(allb, mine)
-    comm.attach(allb)
+        allb = [mine]
+    else:
+        if not dist.is_initialized():
+            raise RuntimeError("attach_peer_halo needs torch.distributed initialised")
+        allb = [None] * env.world
+        dist.all_gather_object(allb, mine)
+    try:
+        comm.attach(allb)
+    except Exception as e:  # noqa: BLE001
+        if not tolerant:
+            raise
+        print(f"[mcg] rank {env.rank}: peer mapping failed ({e}); the halo stays on the inner communicator",
+              file=sys.stderr, flush=True)
+        return False
+    return True
 
 
 def set_device(env: DistEnv) -> int:

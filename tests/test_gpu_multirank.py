@@ -244,8 +244,8 @@ def test_local_ranks_lean_runs_bitwise(mcg, problem, n, world):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=2048)), ("poisson3d", dict(n=128)),
-                                         ("poisson2d", dict(n=1024, coef=1)), ("poisson3d", dict(n=128, coef=1))])
+@pytest.mark.parametrize("problem,kw", [("poisson2d", dict(n=4096)), ("poisson3d", dict(n=128)),
+                                         ("poisson2d", dict(n=2048, coef=1)), ("poisson3d", dict(n=128, coef=1))])
 def test_local_ranks_in_kernel_halo_bitwise(mcg, world, problem, kw):
     """the in-kernel halo (halo_pull).  From iteration 2 on the lean carries read
     their ghost lines / planes straight from the neighbours' rows (LocalComm: the other threads'

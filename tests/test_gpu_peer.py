@@ -48,18 +48,19 @@ def test_bench_sdma_halo_rehearsal_on_one_gpu():
     collectives of the all-reduce move nothing (rehearsal); every rank ok and latched together."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--rehearse-ranks", "--grid",
-           "1024", "--steps", "64", "--warmup", "8", "--phases", "0", "--watchdog", "60", "--halo-transport", "sdma"]
+           "2048", "--steps", "64", "--warmup", "8", "--phases", "0", "--watchdog", "60", "--halo-transport", "sdma"]
     p = _run(cmd)
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["check"]["ok"] and line["n_gpus"] == 2
-    # the lean 2-D carry reads its ghost lines in-kernel from the mapped neighbour (halo_pull auto)
-    assert line["config"]["halo_transport"].startswith("in-kernel")
+    # the lean 2-D carry (runs of >= 3 lines: 2048^2 at P = 2) reads its ghost lines in-kernel from the
+    # mapped neighbour (halo_pull auto)
+    assert line["config"]["halo_transport"].startswith("in-kernel") and line["check"]["lean_only"]
 
 
-@pytest.mark.parametrize("world,problem,n,pull,coef", [(2, "poisson2d", 1024, -1, 0), (4, "poisson2d", 1024, -1, 0),
-                                                       (2, "poisson2d", 1024, 0, 0), (4, "poisson3d", 128, -1, 0),
-                                                       (2, "poisson2d", 512, -1, 1)])
+@pytest.mark.parametrize("world,problem,n,pull,coef", [(2, "poisson2d", 2048, -1, 0), (4, "poisson2d", 2048, -1, 0),
+                                                       (2, "poisson2d", 2048, 0, 0), (4, "poisson3d", 128, -1, 0),
+                                                       (2, "poisson2d", 1024, -1, 1)])
 def test_ipc_ranks_real_recurrence_matches_one_rank(world, problem, n, pull, coef):
     """P processes on ONE GPU run the real P-rank recurrence -- the IPC all-reduce
     (mailboxes mapped through IPC handles, rank-order sums) and the peer-mapped halo (the in-kernel
@@ -94,7 +95,7 @@ def test_bench_ipc_allreduce_rehearsal_is_a_real_solve():
     real solve, so its check requires the recurrence residual to track ||b - A x||."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--rehearse-ranks", "--grid",
-           "1024", "--steps", "64", "--warmup", "8", "--phases", "0", "--watchdog", "60", "--allreduce", "ipc"]
+           "2048", "--steps", "64", "--warmup", "8", "--phases", "0", "--watchdog", "60", "--allreduce", "ipc"]
     p = _run(cmd)
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
