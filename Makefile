@@ -39,7 +39,7 @@ HOST_OBJ  := $(patsubst csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(GPU_CPP))
 CORE_OBJ  := $(HIP_OBJ) $(HOST_OBJ)
 HEADERS   := $(wildcard csrc/include/mcg/*.hpp) $(wildcard csrc/gpu/*.hpp)
 
-all: $(PYMOD) $(CLI) $(TESTBIN)
+all: $(PYMOD) $(CLI) $(TESTBIN) $(BUILD)/streamop_capture
 
 $(BUILD)/%.o: csrc/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)
@@ -72,6 +72,11 @@ $(TESTBIN): $(HOST_OBJ:$(BUILD)/gpu/%=) $(BUILD)/tests/test_host.o
 $(BUILD)/tests/test_host.o: tests/native/test_host.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+# repro of the stream memory operations / copy-engine copies under graph capture (bench/)
+$(BUILD)/streamop_capture: bench/streamop_capture.cpp
+	@mkdir -p $(BUILD)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 $< -o $@
 
 # host-only sanitizer build of the CPU reference path / partitioner / halo plan tests
 # (GPU sanitizers are not available on this pool: host code only)

@@ -695,6 +695,11 @@ void GpuCgSolver::verify_pull_() {
                                          "the halo is exchanged instead\n");
     pull_ = false;
     info_.halo_pull = false;
+    if (use_halo_ && !comm_->halo_capturable()) {
+      drop_graphs_();
+      opt_.use_graph = false;
+      info_.graphs = false;
+    }
   }
 }
 

@@ -882,6 +882,9 @@ void GpuCgSolver::setup() {
               "halo_pull needs the lean line / plane carry on every rank (P > 1, a communicator that maps its peers)");
     info_.halo_pull = pull_;
   }
+  // iterations that exchange a halo are captured only if the communicator's exchanges replay correctly
+  // (the in-kernel halo's graphs hold none)
+  if (use_halo_ && !pull_ && !comm_->halo_capturable()) opt_.use_graph = false;
   if (ar_ && !info_.dia4 && !diav_ && n > 0) {
     const int64_t ns = (n + 63) / 64;
     int64_t slots = 0;

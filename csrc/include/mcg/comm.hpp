@@ -88,6 +88,8 @@ class Communicator {
   virtual void check_async() {}
   // whether the solver may capture this communicator's calls into a hipGraph
   virtual bool graph_capturable() const { return true; }
+  // ... its halo exchanges too (the in-kernel halo's iterations hold none: only the all-reduce)
+  virtual bool halo_capturable() const { return graph_capturable(); }
   // false for NullComm (per-rank timing rehearsal): setup-time agreements take this rank's own value
   virtual bool moves_data() const { return true; }
   // tear down outstanding collectives after a fatal error (watchdog)
@@ -228,6 +230,10 @@ class PeerHaloComm final : public Communicator {
                      const int* widths = nullptr) override;
   void check_async() override;
   bool graph_capturable() const override { return inner_->graph_capturable() && capturable_; }
+  // the copy-engine exchange replays from a hipGraph without its order: a 2-process solve with the
+  // pulls captured drifts by 1.5e-2 in 40 iterations, eager it matches one rank to 1e-15
+  // (bench/ipc_ranks.py --halo-pull 0, profiles/r5/capture; bench/streamop_capture.cpp)
+  bool halo_capturable() const override { return graph_capturable() && (halo_inner_ ? inner_->halo_capturable() : false); }
   bool moves_data() const override { return ipc_ar_ || inner_->moves_data(); }
   void abort() override { inner_->abort(); }
   // the copy-engine halo never enters the inner communicator; with halo_via_inner it is the inner's

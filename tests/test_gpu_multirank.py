@@ -266,7 +266,7 @@ def test_local_ranks_in_kernel_halo_bitwise(mcg, world, problem, kw):
     assert all(abs(q["true_rnorm"] - q["rnorm"]) <= 1e-8 * q["true_rnorm"] for q in outs["pull"]["ranks"])
 
 
-@pytest.mark.parametrize("problem,n", [("poisson2d", 1024), ("poisson3d", 64)])
+@pytest.mark.parametrize("problem,n", [("poisson2d", 2048), ("poisson3d", 64)])
 def test_local_ranks_in_kernel_halo_converges(mcg, problem, n):
     """The in-kernel halo to convergence at P = 4 against the CPU oracle (the reference's recurrence)."""
     spec = mcg.make_problem(problem, n=n, rhs="random")
@@ -281,7 +281,7 @@ def test_local_ranks_in_kernel_halo_converges(mcg, problem, n):
     np.testing.assert_allclose(out["x"], cpu["x"], rtol=1e-6, atol=1e-6 * np.abs(cpu["x"]).max())
 
 
-@pytest.mark.parametrize("problem,n", [("poisson2d", 512), ("poisson3d", 128)])
+@pytest.mark.parametrize("problem,n", [("poisson2d", 4096), ("poisson3d", 128)])
 def test_null_comm_in_kernel_halo_graph_equals_eager(mcg, problem, n):
     """A P = 8 rank's share with the in-kernel halo forced on a NullComm (the rank's own first / last
     line stands in for the neighbours'): the 32-iteration graphs replay the eager pulled passes bit for
