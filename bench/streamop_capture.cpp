@@ -12,12 +12,13 @@
 //   fork     graph, the consumer's copy on a branch forked / joined by events (CopyFan's capture form;
 //            r4 saw a SIGSEGV there: a SIGSEGV handler prints the host backtrace)
 // Prints one JSON line per mode: rounds, mismatching entries, whether the consumer ever ran ahead.
-//   hipcc --offload-arch=gfx950 -O2 bench/streamop_capture.cpp -o build/streamop_capture && build/streamop_capture
+//   make build/streamop_capture && build/streamop_capture [ROUNDS [MODE]]
 #include <execinfo.h>
 #include <hip/hip_runtime.h>
 #include <signal.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +44,13 @@ __global__ void k_check(const double* dst, int n, double v, unsigned long long* 
   if (b) atomicAdd(bad, b);
 }
 
+static const char* g_mode = "";
+static void on_alarm(int) {
+  std::printf("{\"mode\": \"%s\", \"hung\": true}\n", g_mode);
+  std::fflush(stdout);
+  std::_Exit(3);
+}
+
 static void on_segv(int sig) {
   void* bt[64];
   const int n = backtrace(bt, 64);
@@ -53,6 +61,7 @@ static void on_segv(int sig) {
 
 int main(int argc, char** argv) {
   signal(SIGSEGV, on_segv);
+  signal(SIGALRM, on_alarm);
   const int n = 16384, rounds = argc > 1 ? std::atoi(argv[1]) : 20;
   int rate = 0;
   CK(hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, 0));
@@ -88,8 +97,12 @@ int main(int argc, char** argv) {
     CK(hipStreamWriteValue64(s, done, v, 0));  // the producer may overwrite src now
   };
   const char* modes[] = {"eager", "graph", "graphw", "fork"};
+  const std::string only = argc > 2 ? argv[2] : "";
   for (const char* mode : modes) {
     const std::string m = mode;
+    if (!only.empty() && m != only) continue;
+    g_mode = mode;
+    alarm(20);  // a mode that hangs ends the program with a line saying so
     CK(hipMemset(flag, 0, sizeof(uint64_t)));
     CK(hipMemset(done, 0, sizeof(uint64_t)));
     CK(hipMemset(bad, 0, sizeof(unsigned long long)));
@@ -111,30 +124,35 @@ int main(int argc, char** argv) {
       CK(hipStreamEndCapture(A, &g2));
       CK(hipGraphInstantiate(&gw, g2, nullptr, nullptr, 0));
     }
+    double launch_us = 0.0;
     for (int r = 0; r < rounds; r += 2) {
-      if (m == "eager") {
-        consumer(B, 1, false);
-        consumer(B, 2, false);
-      } else {
-        CK(hipGraphLaunch(gb, B));
-      }
+      // the producer's pair first (its second fill waits on the device for the consumer's done = 1), so
+      // a consumer launch that blocked the host until its waits are met could not deadlock
       for (uint64_t v = 1; v <= 2; ++v) {
         if (v == 2) CK(hipStreamWaitValue64(A, done, 1, hipStreamWaitValueEq, ~0ull));
         hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, A, src, n, (double)v, spin);
         if (m == "graphw" && v == 1) CK(hipGraphLaunch(gw, A));
         else CK(hipStreamWriteValue64(A, flag, v, 0));
       }
+      const auto t0 = std::chrono::steady_clock::now();
+      if (m == "eager") {
+        consumer(B, 1, false);
+        consumer(B, 2, false);
+      } else {
+        CK(hipGraphLaunch(gb, B));
+      }
+      launch_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       CK(hipStreamSynchronize(A));
       CK(hipStreamSynchronize(B));
-      // reset the flag for the next pair (the wait is for equality)
+      // reset the flags for the next pair (the waits are for equality)
       CK(hipMemset(flag, 0, sizeof(uint64_t)));
       CK(hipMemset(done, 0, sizeof(uint64_t)));
       CK(hipDeviceSynchronize());
     }
     unsigned long long h = 0;
     CK(hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost));
-    std::printf("{\"mode\": \"%s\", \"rounds\": %d, \"mismatches\": %llu, \"ordered\": %s}\n", mode, rounds, h,
-                h == 0 ? "true" : "false");
+    std::printf("{\"mode\": \"%s\", \"rounds\": %d, \"mismatches\": %llu, \"ordered\": %s, \"host_launch_us\": %.1f}\n",
+                mode, rounds, h, h == 0 ? "true" : "false", launch_us / (rounds / 2));
     std::fflush(stdout);
     if (gb) CK(hipGraphExecDestroy(gb));
     if (gw) CK(hipGraphExecDestroy(gw));

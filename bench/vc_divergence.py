@@ -8,8 +8,10 @@ alone?  The same problem (poisson2d --coef 1, 1024^2, random RHS) through four s
   d16    the GPU single-reduction pass on SELL-64/d16 (generic kernels)
   diav   the GPU default: SELL-64/diav three-term Ap-recomputing line carry (lean runs)
 
-and prints |rnorm_k - cpu_k| / cpu_k at several k, plus each run's recurrence vs ||b - A x||.  One JSON
-line.  A pure-rounding drift shows as csr0 drifting like the others.
+and prints |rnorm_k - cpu_k| / cpu_k at several k, plus each run's recurrence vs ||b - A x||, and (r5,
+VERDICT r4 item 9) each GPU run against the GPU csr0 run -- the same rounding growth, both on the GPU:
+|rnorm_k - csr0_k| / csr0_k and ||x_k - x_csr0,k|| / ||x_csr0,k||.  One JSON line.  A pure-rounding drift
+shows as csr0 drifting like the others.
     python bench/vc_divergence.py [--n 1024]
 """
 from __future__ import annotations
@@ -40,6 +42,7 @@ def main() -> int:
     arms = {"csr0": dict(format="csr", recurrence=0), "d16": dict(format="sellc8", recurrence=1, carry_vc=0),
             "diav": dict(format="sellc8", recurrence=1)}
     out = {"n": a.n, "coef": a.coef, "cpu_rnorm": {k: float(hist[k - 1]) for k in its}, "gap": {}, "true_gap": {}}
+    ref = {}  # csr0's (rnorm, x) per k
     for name, kw in arms.items():
         s = mcg.CGSolver(spec, tol=-1.0, maxit=max(its), **kw)
         gaps = {}
@@ -49,6 +52,13 @@ def main() -> int:
             s.finalize()
             r = s.result()["rnorm"]
             gaps[k] = abs(r - hist[k - 1]) / hist[k - 1]
+            x = np.asarray(s._s.x_local())
+            if name == "csr0":
+                ref[k] = (r, x)
+            else:
+                r0, x0 = ref[k]
+                out.setdefault("gap_vs_csr0", {}).setdefault(name, {})[k] = abs(r - r0) / r0
+                out.setdefault("xgap_vs_csr0", {}).setdefault(name, {})[k] = float(np.linalg.norm(x - x0) / np.linalg.norm(x0))
         tr = s.true_residual_norm()
         out["gap"][name] = gaps
         out["true_gap"][name] = abs(tr - s.result()["rnorm"]) / tr
