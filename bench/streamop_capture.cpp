@@ -7,10 +7,11 @@
 // dst that are not v and writes v into `done`, which the producer waits for before the next fill (the
 // ready / done pair of peer_halo.cpp).  Modes:
 //   eager    the consumer's operations enqueued per round
-//   graph    the consumer's two rounds (v = 1, 2) captured once into a graph and replayed per pair
-//   graphw   as graph, the producer's flag write captured too (its own graph)
+//   graph    the consumer's four operations of each round captured (one graph per round value)
 //   fork     graph, the consumer's copy on a branch forked / joined by events (CopyFan's capture form;
 //            r4 saw a SIGSEGV there: a SIGSEGV handler prints the host backtrace)
+//   g_wait / g_copy / g_check / g_write / g_copy_check   only those operations captured, the rest eager
+//            (which node kind breaks the ordering)
 // Prints one JSON line per mode: rounds, mismatching entries, whether the consumer ever ran ahead.
 //   make build/streamop_capture && build/streamop_capture [ROUNDS [MODE]]
 #include <execinfo.h>
@@ -82,48 +83,52 @@ int main(int argc, char** argv) {
   CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
 
-  auto consumer = [&](hipStream_t s, uint64_t v, bool forked) {
-    CK(hipStreamWaitValue64(s, flag, v, hipStreamWaitValueEq, ~0ull));
-    if (forked) {
-      CK(hipEventRecord(fork, s));
-      CK(hipStreamWaitEvent(C, fork, 0));
-      CK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDeviceNoCU, C));
-      CK(hipEventRecord(join, C));
-      CK(hipStreamWaitEvent(s, join, 0));
-    } else {
-      CK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDeviceNoCU, s));
+  // the consumer's four operations for round value v; `ops` selects which (bit 0 wait, 1 copy, 2 check,
+  // 3 done write)
+  auto consumer = [&](hipStream_t s, uint64_t v, unsigned ops, bool forked) {
+    if (ops & 1) CK(hipStreamWaitValue64(s, flag, v, hipStreamWaitValueEq, ~0ull));
+    if (ops & 2) {
+      if (forked) {
+        CK(hipEventRecord(fork, s));
+        CK(hipStreamWaitEvent(C, fork, 0));
+        CK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDeviceNoCU, C));
+        CK(hipEventRecord(join, C));
+        CK(hipStreamWaitEvent(s, join, 0));
+      } else {
+        CK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDeviceNoCU, s));
+      }
     }
-    hipLaunchKernelGGL(k_check, dim3(64), dim3(256), 0, s, dst, n, (double)v, bad);
-    CK(hipStreamWriteValue64(s, done, v, 0));  // the producer may overwrite src now
+    if (ops & 4) hipLaunchKernelGGL(k_check, dim3(64), dim3(256), 0, s, dst, n, (double)v, bad);
+    if (ops & 8) CK(hipStreamWriteValue64(s, done, v, 0));  // the producer may overwrite src now
   };
-  const char* modes[] = {"eager", "graph", "graphw", "fork"};
+  // mode -> the operations captured (one graph per round value; the others stay eager, in order)
+  struct Mode { const char* name; unsigned cap; bool forked; };
+  const Mode modes[] = {{"eager", 0, false}, {"graph", 15, false}, {"fork", 15, true}, {"g_wait", 1, false},
+                        {"g_copy", 2, false}, {"g_check", 4, false}, {"g_write", 8, false},
+                        {"g_copy_check", 6, false}};
   const std::string only = argc > 2 ? argv[2] : "";
-  for (const char* mode : modes) {
-    const std::string m = mode;
+  for (const Mode& md : modes) {
+    const std::string m = md.name;
     if (!only.empty() && m != only) continue;
-    g_mode = mode;
+    g_mode = md.name;
     alarm(20);  // a mode that hangs ends the program with a line saying so
     CK(hipMemset(flag, 0, sizeof(uint64_t)));
     CK(hipMemset(done, 0, sizeof(uint64_t)));
     CK(hipMemset(bad, 0, sizeof(unsigned long long)));
     CK(hipMemset(src, 0, n * sizeof(double)));
     CK(hipDeviceSynchronize());
-    hipGraphExec_t gb = nullptr, gw = nullptr;
-    hipGraph_t g = nullptr;
-    if (m != "eager") {  // the consumer's pair (v = 1, 2)
-      CK(hipStreamBeginCapture(B, hipStreamCaptureModeThreadLocal));
-      consumer(B, 1, m == "fork");
-      consumer(B, 2, m == "fork");
-      CK(hipStreamEndCapture(B, &g));
-      CK(hipGraphInstantiate(&gb, g, nullptr, nullptr, 0));
+    hipGraphExec_t gx[3] = {nullptr, nullptr, nullptr};
+    if (md.cap) {
+      for (uint64_t v = 1; v <= 2; ++v) {
+        hipGraph_t g = nullptr;
+        CK(hipStreamBeginCapture(B, hipStreamCaptureModeThreadLocal));
+        consumer(B, v, md.cap, md.forked);
+        CK(hipStreamEndCapture(B, &g));
+        CK(hipGraphInstantiate(&gx[v], g, nullptr, nullptr, 0));
+      }
     }
-    if (m == "graphw") {  // the producer's flag writes captured too (the kernels stay eager)
-      hipGraph_t g2 = nullptr;
-      CK(hipStreamBeginCapture(A, hipStreamCaptureModeThreadLocal));
-      CK(hipStreamWriteValue64(A, flag, 1, 0));
-      CK(hipStreamEndCapture(A, &g2));
-      CK(hipGraphInstantiate(&gw, g2, nullptr, nullptr, 0));
-    }
+    const unsigned low = md.cap & (~md.cap + 1);  // first captured op
+    const unsigned pre = md.cap ? low - 1 : 15, post = md.cap ? (15 & ~(pre | md.cap)) : 0;
     double launch_us = 0.0;
     for (int r = 0; r < rounds; r += 2) {
       // the producer's pair first (its second fill waits on the device for the consumer's done = 1), so
@@ -131,15 +136,13 @@ int main(int argc, char** argv) {
       for (uint64_t v = 1; v <= 2; ++v) {
         if (v == 2) CK(hipStreamWaitValue64(A, done, 1, hipStreamWaitValueEq, ~0ull));
         hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, A, src, n, (double)v, spin);
-        if (m == "graphw" && v == 1) CK(hipGraphLaunch(gw, A));
-        else CK(hipStreamWriteValue64(A, flag, v, 0));
+        CK(hipStreamWriteValue64(A, flag, v, 0));
       }
       const auto t0 = std::chrono::steady_clock::now();
-      if (m == "eager") {
-        consumer(B, 1, false);
-        consumer(B, 2, false);
-      } else {
-        CK(hipGraphLaunch(gb, B));
+      for (uint64_t v = 1; v <= 2; ++v) {
+        consumer(B, v, pre, false);
+        if (md.cap) CK(hipGraphLaunch(gx[v], B));
+        consumer(B, v, post, false);
       }
       launch_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       CK(hipStreamSynchronize(A));
@@ -149,13 +152,14 @@ int main(int argc, char** argv) {
       CK(hipMemset(done, 0, sizeof(uint64_t)));
       CK(hipDeviceSynchronize());
     }
+    alarm(0);
     unsigned long long h = 0;
     CK(hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost));
-    std::printf("{\"mode\": \"%s\", \"rounds\": %d, \"mismatches\": %llu, \"ordered\": %s, \"host_launch_us\": %.1f}\n",
-                mode, rounds, h, h == 0 ? "true" : "false", launch_us / (rounds / 2));
+    std::printf("{\"mode\": \"%s\", \"captured_ops\": %u, \"rounds\": %d, \"mismatches\": %llu, \"ordered\": %s, \"host_launch_us\": %.1f}\n",
+                md.name, md.cap, rounds, h, h == 0 ? "true" : "false", launch_us / (rounds / 2));
     std::fflush(stdout);
-    if (gb) CK(hipGraphExecDestroy(gb));
-    if (gw) CK(hipGraphExecDestroy(gw));
+    for (hipGraphExec_t e : gx)
+      if (e) CK(hipGraphExecDestroy(e));
   }
   return 0;
 }

@@ -173,10 +173,18 @@ void CopyFan::run(hipStream_t stream, const std::vector<Job>& jobs) {
       MCG_HIP(hipStreamWaitValue64(st, j.wait_flag, j.wait_value, hipStreamWaitValueEq, ~0ull), "copy fan: wait failed");
     if (j.bytes > 0) MCG_HIP(hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToDeviceNoCU, st), "copy fan: copy failed");
   };
-  // one stream while a graph is being captured: the forked wait-value / NoCU-copy branches crashed the
-  // capture (bench --halo-transport sdma, SIGSEGV at P = 2), the serial form captures and replays
+  // never inside a graph capture: captured stream memory operations do not keep their order on this
+  // stack (ROCm 7.2, gfx950).  bench/streamop_capture.cpp isolates it: a captured hipStreamWaitValue64
+  // node never completes, a captured hipStreamWriteValue64 node never lands (the producer waiting for it
+  // hangs), while the same operations enqueued eagerly order correctly and captured NoCU copies /
+  // kernels alone replay fine (profiles/r5/capture/streamop_capture.jsonl).  r4's "SIGSEGV at P = 2"
+  // with forked branches and the wrong results of the serial captured form were both this: a solver
+  // whose halo runs through these flags is not captured (PeerHaloComm::halo_capturable is false for the
+  // copy-engine halo, so the solver stays eager there; the in-kernel halo needs no flags and captures).
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   MCG_HIP(hipStreamIsCapturing(stream, &cs), "copy fan: capture query failed");
+  MCG_CHECK(cs == hipStreamCaptureStatusNone || !std::any_of(jobs.begin(), jobs.end(), [](const Job& j) { return j.wait_flag != nullptr; }),
+            "copy fan: flag-ordered copies cannot be captured (bench/streamop_capture.cpp)");
   if (jobs.size() <= 1 || cs != hipStreamCaptureStatusNone) {
     for (const Job& j : jobs) issue(stream, j);
     return;

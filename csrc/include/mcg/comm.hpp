@@ -50,7 +50,8 @@ ncclUniqueId unique_id_from_bytes(const std::string& b);
 // to kMaxStreams, then round robin), forked from and joined back to the caller's stream by events, so
 // a graph captures them as branches.  One queue runs its copies one after another; a halo of 2 peers x
 // 3 vectors of 128 KiB was 6 serial copies.  A job may first wait for a 64-bit flag (stream wait-value).
-// Inside a graph capture the copies stay on the caller's stream (the branches crashed the capture).
+// Inside a graph capture (flag-free jobs only: captured wait / write-value nodes do not order on this
+// stack, bench/streamop_capture.cpp) the copies stay on the caller's stream.
 class CopyFan {
  public:
   static constexpr int kMaxStreams = 16;

@@ -118,6 +118,39 @@ def test_varcoef_2000_iterations_track_cpu_oracle(mcg):
     assert abs(tr - out["rnorm"]) <= 1e-9 * tr, (tr, out["rnorm"])
 
 
+def test_varcoef_2000_iterations_track_gpu_two_reduction_csr(mcg):
+    """the diav carry against the GPU two-reduction CSR pass (the reference's own
+    algorithm, CUDACG.cu:269-352, on the GPU) over the reference's 2000 iterations -- both runs round on
+    the GPU, so this pins the carry to the algorithm's own rounding growth.  Tolerances from the
+    measured gaps (bench/vc_divergence.py --coef 1, profiles/r5/vc/vcdiv_coef1.json, bitwise the r4
+    numbers): ||x_diav - x_csr0|| / ||x_csr0|| = 1.3e-3 at k = 300 (the drift's peak; the generic d16
+    pass: 1.3e-3 too) and 1.2e-5 at 2000 (d16: 1.2e-5); |rnorm gap| 1.4e-2 at 2000 (the CPU oracle vs
+    csr0: 3.0e-2).  Asserted at ~4x: 5e-3 / 5e-5 / 0.06, and <= 1e-12 at k = 20."""
+    spec = _vc(mcg, 1024)
+    runs = {}
+    for name, kw in (("csr0", dict(format="csr", recurrence=0)), ("diav", dict(format="sellc8", recurrence=1))):
+        s = mcg.CGSolver(spec, tol=-1.0, maxit=2000, **kw)
+        if name == "diav":
+            assert s.info["diav"] and s.info["lean_only"], s.info
+        else:
+            assert s.info["recurrence"] == "two-reduction", s.info
+        got = {}
+        for k in (20, 300, 2000):
+            s.reset()
+            s.run(k)
+            s.finalize()
+            got[k] = (s.result()["rnorm"], np.asarray(s._s.x_local()))
+        runs[name] = (got, s.true_residual_norm())
+    (g0, t0), (g1, t1) = runs["csr0"], runs["diav"]
+    for k, rtol, xtol in ((20, 1e-12, 1e-12), (300, 0.06, 5e-3), (2000, 0.06, 5e-5)):
+        (r0, x0), (r1, x1) = g0[k], g1[k]
+        assert abs(r1 - r0) <= rtol * r0, (k, r1, r0)
+        xg = np.linalg.norm(x1 - x0) / np.linalg.norm(x0)
+        assert xg <= xtol, (k, xg)
+    # each recurrence tracks its own ||b - A x|| at 2000
+    assert abs(t1 - g1[2000][0]) <= 1e-9 * t1 and abs(t0 - g0[2000][0]) <= 1e-9 * t0
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_varcoef_local_ranks_agree_with_single_rank(mcg, world):
     """P ranks (LocalComm) on the diav carry: ghost lines' north coefficients from the rank's own rows."""
