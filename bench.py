@@ -366,6 +366,7 @@ def _run_rank(args, out_fd) -> int:
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
                       "placement_lead_trial": info.get("placement_lead_trial"),
                       "dia_uniform": round(info.get("dia_uniform", 0.0), 4), "lean_only": info.get("lean_only", False),
+                      "halo_pull": info.get("halo_pull", False),
                       **({"ag_local_frac": round(info["ag_local_frac"], 4)} if info.get("ag_overlap") else {}),
                       "model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
                       "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3),

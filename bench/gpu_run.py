@@ -46,6 +46,9 @@ def recipes(a) -> dict:
     g = a.grid
     c5 = f"{C5SCR} --phases 0 --no-verify"
     dram = "TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum GRBM_GUI_ACTIVE"
+    WAVES = ("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY "
+             "SQ_WAIT_INST_ANY SQ_INSTS_LDS")
+    S8 = "--sim-world 8 --sim-rank 3 --set halo_pull=1"
 
     def stats(tag, args):  # kernel trace + stats of one bench run, summarised to markdown
         return [(tag, 300, prof(tag, f"{PY} {ROOT}/bench.py --phases 0 {args}")),
@@ -113,9 +116,7 @@ def recipes(a) -> dict:
                 + counters("dram_512", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2")
                 + counters("dram_4096", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8"),
         # issue-side counters of one grid's pass (--grid)
-        "waves": counters(f"waves_{g}", "k_cg_carry_ar", f"--grid {g} --steps 8 --warmup 2",
-                          "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY "
-                          "SQ_WAIT_INST_ANY SQ_INSTS_LDS"),
+        "waves": counters(f"waves_{g}", "k_cg_carry_ar", f"--grid {g} --steps 8 --warmup 2", WAVES),
         # kernel trace + per-iteration kernel count / gaps of one grid (--grid)
         "trace": [
             ("trace", 300, prof(f"prof{g}", f"{PY} {ROOT}/bench.py --grid {g} --steps 64 --warmup 8 --phases 0 "
@@ -266,6 +267,15 @@ def recipes(a) -> dict:
                                    f"--rehearse-ranks --steps 200 --warmup 20 --phases 0 --halo-transport {t}")
             for w in (2, 4) for t in ("rccl", "sdma")
         ],
+        # r5: a P = 8 rank's share of 16384^2 and 512^3 (the in-kernel halo's pass, NullComm):
+        # kernel trace, DRAM bytes and issue counters of the pass
+        "share8": stats("share8_2d", f"{S8} --steps 256 --warmup 32")
+                  + stats("share8_3d", f"--problem poisson3d --grid 512 {S8} --steps 256 --warmup 32")
+                  + counters("share8_2d_dram", "k_cg_carry_ar", f"{S8} --steps 32 --warmup 4")
+                  + counters("share8_3d_dram", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4")
+                  + counters("share8_2d_waves", "k_cg_carry_ar", f"{S8} --steps 32 --warmup 4", WAVES)
+                  + counters("p1_2d_waves", "k_cg_carry_ar", "--steps 8 --warmup 2", WAVES)
+                  + counters("p1_2d_dram", "k_cg_carry_ar", "--steps 8 --warmup 2"),
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),
