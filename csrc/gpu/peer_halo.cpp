@@ -5,7 +5,7 @@
 // The reference has no communication at all (CUDACG.cu is one process on device 0, :87); this is
 // the north star's halo (the SpMV reads neighbours' p, CUDACG.cu:288), moved off the
 // compute units so it can run beside the resident pass; the lean carries instead read these mapped rows
-// themselves (PassForm::halo_pull, cg_carry_ar.hip PullBases) and the copies serve the other passes.
+// themselves (PassForm::halo_pull, carry_common.hpp PullBases) and the copies serve the other passes.
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 

@@ -243,7 +243,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
       v.re_old = ape_[(k + 1) & 1].get() + ns2;
       v.re_new = ape_[k & 1].get() + ns2;
     }
-    if (pull_ && !probing_ && !final_mode) {  // in-kernel halo (cg_carry_ar.hip PullBases)
+    if (pull_ && !probing_ && !final_mode) {  // in-kernel halo (carry_common.hpp PullBases)
       v.pull_pub = 1;
       if (k >= pull_from_) {
         MCG_CHECK(map_pull_(), "in-kernel halo: the peers' buffers are not mapped (attach the communicator)");

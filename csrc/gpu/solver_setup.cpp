@@ -866,7 +866,7 @@ void GpuCgSolver::setup() {
   info_.lean_only = lean_only_;
   info_.lean_mix = auto_mix_ && lean_only_ && g_odd_ > 0 && opt_.hooks.lean_packed != 0;
   // in-kernel halo: the lean carries read their ghost lines / planes from the neighbours' rows and store
-  // their own first / last ones write-through (cg_carry_ar.hip PullBases), so an iteration from 2 on is
+  // their own first / last ones write-through (carry_common.hpp PullBases), so an iteration from 2 on is
   // the pass + the all-reduce, no halo step.  The all-reduce orders the passes: a rank's pass k + 1
   // starts after every rank's pass k has finished (its sums are in the all-reduce), which is all the
   // pulled rows need -- p_{k-1} / Ap_{k-1} of the peer's first / last line sit in the buffers its pass k
