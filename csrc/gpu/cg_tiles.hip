@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "mcg/check.hpp"
 #include "mcg/kernels.hpp"
@@ -85,10 +86,16 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
 }
 
 // one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
+template <int ABL = 0>
 __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
 #pragma unroll
   for (int u = 0; u < kTU; ++u) {
     const int64_t e = k + u * 64;
+    if constexpr ((ABL & 8) != 0) {
+      q[u] = (uint32_t)e & 1023u;
+      v[u] = 1.0;
+      continue;
+    }
     q[u] = e < hi ? __builtin_nontemporal_load(&T.idx[e]) : 0u;
     v[u] = e < hi ? __builtin_nontemporal_load(&T.vals[e]) : 0.0;
   }
@@ -101,7 +108,9 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // sums stored in Ap, no partials; 2 = the other segments, added to those sums, then the epilogue
 // (as k_split_spmv_aligned_part's halves)
 // kTileB rows per block: 32 KiB of row sums, 4 workgroups per CU
-template <int MODE, int PART = 0>
+// ABL (diagnostic ablations, MCG_TILES_ABLATE, results wrong), bits: 1 = no LDS adds (the products summed in
+// a register), 2 = no gathers (the values themselves added), 4 = no pacing, 8 = no tile loads
+template <int MODE, int PART = 0, int ABL = 0>
 __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
       const int g0 = seg(0);
       lo = T.tptr[b * G + g0];
       hi = T.tptr[b * G + g0 + 1];
-      tile_batch_load(T, lo + lane, hi, q, v);
+      tile_batch_load<ABL>(T, lo + lane, hi, q, v);
     }
     for (int i = 0; i < ns; ++i, ++step) {
       const int g = seg(i);
@@ -150,12 +159,17 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
         for (int64_t k = lo + lane; k < hi; k += TU * 64) {
           uint32_t qn[TU];
           double vn[TU], x[TU];
-          tile_batch_load(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
+          tile_batch_load<ABL>(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
 #pragma unroll
-          for (int u = 0; u < TU; ++u) x[u] = k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0;
+          for (int u = 0; u < TU; ++u) x[u] = (ABL & 2) ? 1.0 : (k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0);
+          if constexpr ((ABL & 1) != 0) {
 #pragma unroll
-          for (int u = 0; u < TU; ++u)
-            if (k + u * 64 < hi) atomicAdd(&a[q[u] >> 22], v[u] * x[u]);
+            for (int u = 0; u < TU; ++u) s_rr = fma(v[u], x[u], s_rr);
+          } else {
+#pragma unroll
+            for (int u = 0; u < TU; ++u)
+              if (k + u * 64 < hi) atomicAdd(&a[q[u] >> 22], v[u] * x[u]);
+          }
 #pragma unroll
           for (int u = 0; u < TU; ++u) {
             q[u] = qn[u];
@@ -167,10 +181,10 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
           const int gn = seg(i + 1);
           lo_next = T.tptr[b * G + gn];
           hi_next = T.tptr[b * G + gn + 1];
-          tile_batch_load(T, lo_next + lane, hi_next, q, v);
+          tile_batch_load<ABL>(T, lo_next + lane, hi_next, q, v);
         }
       }
-      pace_step(T, step, &live);
+      if constexpr ((ABL & 4) == 0) pace_step(T, step, &live);
       lo = lo_next;
       hi = hi_next;
     }
@@ -307,12 +321,25 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
   MCG_CHECK(T.tb == kTileB, "tiles: 1024 rows per block");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-#define MCG_TL(PART)                                                                                              \
-  hipLaunchKernelGGL((k_tiles<0, PART>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials,     \
+#define MCG_TL(PART, ABL)                                                                                         \
+  hipLaunchKernelGGL((k_tiles<0, PART, ABL>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
                      pstride, st, tol, first, check, rc)
-  if (part == 1) MCG_TL(1);
-  else if (part == 2) MCG_TL(2);
-  else MCG_TL(0);
+  static const int ablate = [] {
+    const char* e = std::getenv("MCG_TILES_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+#define MCG_TLA(PART)                   \
+  do {                                  \
+    if (ablate == 3) MCG_TL(PART, 3);   \
+    else if (ablate == 4) MCG_TL(PART, 4); \
+    else if (ablate == 7) MCG_TL(PART, 7); \
+    else if (ablate == 15) MCG_TL(PART, 15); \
+    else MCG_TL(PART, 0);               \
+  } while (0)
+  if (part == 1) MCG_TLA(1);
+  else if (part == 2) MCG_TLA(2);
+  else MCG_TLA(0);
+#undef MCG_TLA
 #undef MCG_TL
   MCG_HIP(hipGetLastError(), "compute mv failed(Ap)");
 }
@@ -321,8 +348,22 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
   if (grid <= 0 || T.nblocks == 0) return;
   MCG_CHECK(T.tb == kTileB, "tiles: 1024 rows per block");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-  hipLaunchKernelGGL((k_tiles<1>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr, 0.0, 0,
-                     0, RedCtl());
+  static const int ablate = [] {
+    const char* e = std::getenv("MCG_TILES_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+#define MCG_T1(ABL)                                                                                                 \
+  hipLaunchKernelGGL((k_tiles<1, 0, ABL>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr, \
+                     0.0, 0, 0, RedCtl())
+  if (ablate == 1) MCG_T1(1);
+  else if (ablate == 2) MCG_T1(2);
+  else if (ablate == 3) MCG_T1(3);
+  else if (ablate == 4) MCG_T1(4);
+  else if (ablate == 7) MCG_T1(7);
+  else if (ablate == 11) MCG_T1(11);
+  else if (ablate == 15) MCG_T1(15);
+  else MCG_T1(0);
+#undef MCG_T1
   MCG_HIP(hipGetLastError(), "compute mv failed(y)");
 }
 
