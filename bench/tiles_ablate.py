@@ -32,7 +32,7 @@ def main() -> int:
     torch.cuda.init()
     C = mcg.native()
     spec = mcg.make_problem("randspd", rows=a.rows, band=a.band, density=1.0, scramble=1, rhs="random")
-    o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, format="sellc8")
+    o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, format="sellc8", recurrence=-1)
     for kv in a.set:
         k, v = kv.split("=", 1)
         setattr(o, k, type(getattr(o, k))(v))

@@ -34,7 +34,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "mcg/check.hpp"
 #include "mcg/kernels.hpp"
@@ -84,6 +86,10 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
   }
   __syncthreads();
 }
+
+// ABL bit 16 (diagnostic): per-workgroup wall-clock ticks spent waiting at the pacing steps and in total
+constexpr int kTileDiagMax = 4096;
+__device__ unsigned long long g_tile_diag[2 * kTileDiagMax];
 
 // one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
 template <int ABL = 0>
@@ -137,6 +143,8 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
   int step = 0;
   if (threadIdx.x == 0) live = 1;
+  unsigned long long t_wait = 0;
+  const unsigned long long t_start = (ABL & 16) ? wall_clock64() : 0ull;
   for (int64_t rd = 0; rd < rounds; ++rd) {
     const int64_t b = wave + rd * nwaves;
     const bool active = b < T.nblocks;
@@ -184,7 +192,13 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
           tile_batch_load<ABL>(T, lo_next + lane, hi_next, q, v);
         }
       }
-      if constexpr ((ABL & 4) == 0) pace_step(T, step, &live);
+      if constexpr ((ABL & 16) != 0) {
+        const unsigned long long w0 = wall_clock64();
+        pace_step(T, step, &live);
+        t_wait += wall_clock64() - w0;
+      } else if constexpr ((ABL & 4) == 0) {
+        pace_step(T, step, &live);
+      }
       lo = lo_next;
       hi = hi_next;
     }
@@ -209,6 +223,12 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
       }
     }
     __syncthreads();
+  }
+  if constexpr ((ABL & 16) != 0) {
+    if (threadIdx.x == 0 && blockIdx.x < kTileDiagMax) {
+      g_tile_diag[2 * blockIdx.x] = t_wait;
+      g_tile_diag[2 * blockIdx.x + 1] = wall_clock64() - t_start;
+    }
   }
   if constexpr (MODE == 0 && PART != 1) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
@@ -362,8 +382,24 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
   else if (ablate == 7) MCG_T1(7);
   else if (ablate == 11) MCG_T1(11);
   else if (ablate == 15) MCG_T1(15);
+  else if (ablate == 16) MCG_T1(16);
   else MCG_T1(0);
 #undef MCG_T1
+  if (ablate == 16) {  // diagnostic: the pacing waits' share of each workgroup's time
+    std::vector<unsigned long long> d(2 * kTileDiagMax);
+    MCG_HIP(hipStreamSynchronize(stream), "tiles diag sync failed");
+    MCG_HIP(hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_tile_diag), d.size() * sizeof(unsigned long long)), "tiles diag copy failed");
+    const int nb = std::min(grid, kTileDiagMax);
+    double w = 0, t = 0, tmax = 0, tmin = 1e300;
+    for (int i = 0; i < nb; ++i) {
+      w += (double)d[2 * i];
+      t += (double)d[2 * i + 1];
+      tmax = std::max(tmax, (double)d[2 * i + 1]);
+      tmin = std::min(tmin, (double)d[2 * i + 1]);
+    }
+    std::fprintf(stderr, "{\"tiles_diag\": {\"workgroups\": %d, \"wait_frac\": %.4f, \"mean_ticks\": %.0f, \"min_ticks\": %.0f, \"max_ticks\": %.0f}}\n",
+                 nb, t > 0 ? w / t : 0.0, t / nb, tmin, tmax);
+  }
   MCG_HIP(hipGetLastError(), "compute mv failed(y)");
 }
 
