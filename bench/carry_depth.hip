@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -77,12 +78,15 @@ __global__ __launch_bounds__(256) void k_step(const double* __restrict__ pa, dou
     const int64_t es = 2 * cols;  // one line of the edge arrays
     const double* ex = ea + l0 * es + 2 * col + (lane == 63);
     double* ey = eb + l0 * es + 2 * col + (lane == 63);
+    // the neighbouring slices' edge rows (inside the array: the first / last column reads its own row)
+    const int nbo = lane == 0 ? (col == 0 ? 0 : -1) : (col == cols - 1 ? 0 : 1);
     double qa[D], qb[D], qe[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       qa[d] = a[d * line_len];
       qb[d] = b[d * line_len];
-      if constexpr (PIECES & 1) qe[d] = edge ? ex[d * es] : 0.0;
+      if constexpr (PIECES & 16) qe[d] = edge ? a[d * line_len + nbo] : 0.0;
+      else if constexpr (PIECES & 1) qe[d] = edge ? ex[d * es] : 0.0;
     }
     int64_t m = 0;
     const int64_t n = l1 - l0 - D;
@@ -91,7 +95,8 @@ __global__ __launch_bounds__(256) void k_step(const double* __restrict__ pa, dou
       for (int u = 0; u < D; ++u) {
         const double na = a[(m + u + D) * line_len], nb = b[(m + u + D) * line_len];
         double ne = 0.0;
-        if constexpr (PIECES & 1) ne = edge ? ex[(m + u + D) * es] : 0.0;
+        if constexpr (PIECES & 16) ne = edge ? a[(m + u + D) * line_len + nbo] : 0.0;
+        else if constexpr (PIECES & 1) ne = edge ? ex[(m + u + D) * es] : 0.0;
         double v = qa[u] + 0.5 * qb[u];
         if constexpr (PIECES & 2) {
           const double up = __shfl_down(qa[u], 1), dn = __shfl_up(qa[u], 1);
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(256) void k_step(const double* __restrict__ pa, dou
           if constexpr ((PIECES & 4) == 0) {  // the lean kernel's layout: r / Ap of the slice's two edge rows
             if (edge) {                       // in two compact arrays, 2 doubles per slice (16 B partial sectors)
               ey[(m + u) * es] = v;
-              ey[(m + u) * es + es / 2] = v;
+              if constexpr ((PIECES & 32) == 0) ey[(m + u) * es + es / 2] = v;  // 32: only one of them
             }
           } else if constexpr ((PIECES & 8) == 0) {  // merged: [r_lo, ap_lo, r_hi, ap_hi] = one 32-B sector per
             if (edge) {                               // slice and line, written whole by one store instruction
@@ -180,8 +185,10 @@ __global__ __launch_bounds__(256) void k_glds(const double* __restrict__ pa, dou
   }
 }
 
-int main() {
-  const int64_t line_len = 4096, lines = 4096, n = line_len * lines;
+int main(int argc, char** argv) {
+  // argv[1]: grid edge (default 4096); argv[2] == "steps": only the lean-step piece variants
+  const int64_t line_len = argc > 1 ? std::atoi(argv[1]) : 4096, lines = line_len, n = line_len * lines;
+  const bool steps_only = argc > 2 && argv[2][0] == 's';
   double *a, *b;
   CK(hipMalloc(&a, n * 8));
   CK(hipMalloc(&b, n * 8 + 4096));
@@ -214,6 +221,7 @@ int main() {
     return 0;
   };
   for (int wps : {4, 5, 8}) {
+    if (steps_only) break;
     if (run("reg D=3", k_reg<3>, wps, 0)) return 1;
     if (run("reg D=4", k_reg<4>, wps, 0)) return 1;
     if (run("reg D=6", k_reg<6>, wps, 0)) return 1;
@@ -252,11 +260,16 @@ int main() {
     if (runs_("step D=3 edges+arithmetic", k_step<3, 3>, wps)) return 1;
     if (runs_("step D=6 edges+arithmetic", k_step<6, 3>, wps)) return 1;
     if (runs_("step D=3 edge loads, no stores", k_step<3, 13>, wps)) return 1;
+    if (runs_("step D=3 edges+arith, one store", k_step<3, 32 | 2 | 1>, wps)) return 1;
+    if (runs_("step D=3 neighbour-row loads, no stores", k_step<3, 16 | 8 | 4 | 1>, wps)) return 1;
+    if (runs_("step D=3 neighbour-row loads+arith, no stores", k_step<3, 16 | 8 | 4 | 2 | 1>, wps)) return 1;
+    if (runs_("step D=4 neighbour-row loads+arith, no stores", k_step<4, 16 | 8 | 4 | 2 | 1>, wps)) return 1;
     if (runs_("step D=3 edges, merged 32-B sectors", k_step<3, 5>, wps)) return 1;
     if (runs_("step D=3 edges+arith, merged", k_step<3, 7>, wps)) return 1;
     if (runs_("step D=6 edges+arith, merged", k_step<6, 7>, wps)) return 1;
   }
   for (int wps : {4, 5}) {
+    if (steps_only) break;
     if (run("glds R=4", k_glds<4>, wps, 4 * 4 * 1024)) return 1;
     if (run("glds R=6", k_glds<6>, wps, 4 * 6 * 1024)) return 1;
     if (run("glds R=8", k_glds<8>, wps, 4 * 8 * 1024)) return 1;

@@ -217,9 +217,11 @@ __global__ __launch_bounds__(kBS) void k_ar_final(SellDev S, F1Vectors v, int64_
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   if (done || sc.conv) {
     const int64_t m = done ? (done == 1 ? st->conv_iter : -1) : k - 1;
-    if (m >= 2 && (m & 1) == 0)
+    if (m >= 2 && (m & 1) == 0) {
+      const double* pf = v.p_fix3[0] != nullptr ? v.p_fix3[(m - 1) % 3] : v.p_fix;  // p_{m-1}
       for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        v.x[i] = fma(ap, v.p_fix[own + i], v.x[i]);
+        v.x[i] = fma(ap, pf[own + i], v.x[i]);
+    }
     return;
   }
   const bool pair = (k & 1) && k >= 3;

@@ -228,7 +228,33 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
   if (f) atomicAdd(fails, f);
 }
 
+// dia_lines_uniform: slices whose masked pattern word differs from their line's first slice
+__global__ __launch_bounds__(256) void k_lines_uniform(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
+                                                       unsigned long long* __restrict__ bad) {
+  const uint32_t mask = ~(3u << 28);
+  unsigned long long b = 0;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ss * nl; s += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = (uint32_t)dpat[s], w0 = (uint32_t)dpat[(s / ss) * ss];
+    b += ((w >> 31) == 0u || (w & mask) != (w0 & mask)) ? 1u : 0u;
+  }
+  if (b) atomicAdd(bad, b);
+}
+
 }  // namespace
+
+bool dia_lines_uniform(const uint64_t* dpat, int64_t ss, int64_t nl, hipStream_t stream) {
+  if (dpat == nullptr || ss <= 0 || nl <= 0) return false;
+  unsigned long long* f = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&f), sizeof(unsigned long long), stream), "device malloc failed(lines)");
+  MCG_HIP(hipMemsetAsync(f, 0, sizeof(unsigned long long), stream), "device memset failed");
+  hipLaunchKernelGGL(k_lines_uniform, dim3(grid_for(ss * nl, 256, 4)), dim3(256), 0, stream, dpat, ss, nl, f);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(lines uniform)");
+  unsigned long long h = 1;
+  MCG_HIP(hipMemcpyAsync(&h, f, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(lines uniform)");
+  (void)hipFreeAsync(f, stream);
+  return h == 0;
+}
 
 int32_t carry3_runs(int64_t nb, int64_t jpr, int64_t nl, int64_t max_chunk) {
   if (nb <= 0 || jpr <= 0 || nl <= 0) return 1;

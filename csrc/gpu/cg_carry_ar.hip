@@ -52,7 +52,14 @@ namespace {
 // lane 0's and lanes 63 / 48 / 56 lane 63's, and move to lanes 0 / 63 by row_mirror /
 // row_half_mirror DPP (one move serves both ends).  A line in flight then holds 2 instead of 6
 // VGPRs of edges, which buys a wave per SIMD (LEAN 5) or a line of prefetch depth
-template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false>
+// T3 (lean dia4 kernels, F1Vectors::p_m2): three p buffers -- p_k goes to a buffer this pass does not
+// read, so p_{k-2} stays intact all pass.  r is recovered from p_{k-1}, p_{k-2} on every line (no
+// stored r at run ends), and the neighbouring slices' edge rows are recomputed from their p_{k-1},
+// p_{k-2} (the owner's stencil in the owner's fma order: the same bits it stored) instead of read from
+// compact edge arrays: no edge-array loads or stores at all (bench/carry_depth.hip: the pattern with
+// the edge stores 77 us at 4096^2, with neighbour-row loads instead 58; profiles/r5/depth)
+template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false,
+          bool T3 = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
@@ -218,6 +225,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           double* __restrict__ pn_ = pn + rb;
           double* __restrict__ rn_ = rn + rb;
           double* __restrict__ x_ = x + xr;
+          const double* __restrict__ pm2_ = (T3 ? v.p_m2 : (const double*)pn) + rb;  // T3: p_{k-2}, read-only
           const double* __restrict__ apo_ = apx_o + rb;
           double* __restrict__ apn_ = apx_n + rb;
           PullBases pl;  // in-kernel halo: the ghost lines from the neighbours' rows
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             Raw q;
             const int32_t jj = jc(j);
             const uint32_t o = line_ofs(jj) + l8;
-            q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
+            q.r = T3 ? g_ld(pm2_, o) : g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
             q.p = pl.ld_p(pl.side(l0 + jj, nl), po_, o);
             return q;
           };
@@ -261,8 +269,41 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const uint32_t o = eoff0 + (uint32_t)(erole == 2 ? jp : jr) * estr;
             return *(const g_double*)((const g_char*)(const g_double*)ebase + o);
           };
+          // T3 edges: the neighbouring slice's edge row (nb: row -1 / 64) and the row beyond it (nb2: -2 /
+          // 65) of line j -- per lane a byte offset from the line start and a base.  EP: lanes 0 / 63 p_{k-2}
+          // (nb), 15 / 48 p_{k-1} (nb2), 7 / 56 p_{k-1} (nb) (the other lanes repeat lane 0's / 63's
+          // load); otherwise every lane loads the three for its own -1 / +1 side.  A slice that starts /
+          // ends a grid line reads its own row (the value meets a zero coefficient).
+          const bool er3 = EP ? eright : hi;
+          const bool erz3 = er3 ? z63 : z0;
+          const int32_t eo_nb = er3 ? 504 + (erz3 ? 0 : 8) : (erz3 ? 0 : -8);
+          const int32_t eo_nb2 = er3 ? 504 + (erz3 ? 0 : 16) : (erz3 ? 0 : -16);
+          const int32_t eo_ep = erole == 1 ? eo_nb2 : eo_nb;
+          const char* ebase3 = (const char*)(erole == 0 ? pm2_ : po_);
+          auto t3_at = [&](int32_t j, int32_t off, const double* base, bool pulled_p) {
+            const int32_t jj = jc(j);
+            const uint32_t o = (uint32_t)((int32_t)line_ofs(jj) + off);
+            return pulled_p ? pl.ld_p(pl.side(l0 + jj, nl), base, o) : g_ld(base, o);
+          };
+          auto edge3 = [&](int32_t j, bool un) {
+            Edge q;
+            if constexpr (EP) {
+              const int32_t jj = un ? j : jc(j);
+              const uint32_t o = (uint32_t)((int32_t)line_ofs(jj) + eo_ep);
+              const int sd = un ? -1 : pl.side(l0 + jj, nl);
+              if (sd >= 0 && erole != 0) q.r = pl.ld_p(sd, po_, o);  // a pulled ghost line's p_{k-1}
+              else q.r = *(const g_double*)((const g_char*)(const g_double*)ebase3 + o);
+              q.a = q.p = 0.0;
+            } else {
+              q.r = t3_at(un ? j : j, eo_nb - (hi ? 504 : 0) + (int32_t)l8, pm2_, false);
+              q.a = t3_at(j, eo_nb2 - (hi ? 504 : 0) + (int32_t)l8, po_, true);
+              q.p = t3_at(j, eo_nb - (hi ? 504 : 0) + (int32_t)l8, po_, true);
+            }
+            return q;
+          };
           auto edge_at = [&](int32_t j) {
             Edge q;
+            if constexpr (T3) return edge3(j, false);
             if constexpr (EP) {
               q.r = edge_pk_ld(rc_(j), jc(j));
               q.a = q.p = 0.0;
@@ -275,17 +316,18 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             return q;
           };
           // a ghost line's r_{k-1} (step()'s rghost): from the halo's p_{k-2} in p_new's ghost rows
-          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn_, line_ofs(j) + l8), q.p); };
+          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(T3 ? pm2_ : (const double*)pn_, line_ofs(j) + l8), q.p); };
           auto is_ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
           auto raw_un = [&](int32_t j) {  // a line of the run or below it, inside the rank
             Raw q;
             const uint32_t o = line_ofs(j) + l8;
-            q.r = g_ld(j < n_run ? (const double*)pn_ : ro_, o);
+            q.r = g_ld(T3 ? pm2_ : (j < n_run ? (const double*)pn_ : ro_), o);
             q.p = g_ld(po_, o);
             return q;
           };
           auto edge_un = [&](int32_t j) {
             Edge q;
+            if constexpr (T3) return edge3(j, true);
             if constexpr (EP) {
               q.r = edge_pk_ld(j, j);
               q.a = q.p = 0.0;
@@ -340,6 +382,30 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               return fma(b, q.p, fma(na, q.a, q.r));
             }
           };
+          // T3: the neighbouring edge row's p_k, recomputed as its owner computed it (the owner's stencil
+          // over its p_{k-1}: lines j - 1 / j + 1 (prev / next), its inner neighbour nb2, itself, and the
+          // row across the slice edge -- this lane's own p_{k-1}, `own`; coefficients V of line j)
+          auto epk3 = [&](double prev, const Edge& q, double next, double own, const VSet& V) {
+            const double p1 = e_p(q);
+            double p1b, p2;
+            if constexpr (EP) {
+              const double v = q.r;
+              const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x140, 0xf, 0xf, false);  // row_mirror
+              const int hi2 = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x140, 0xf, 0xf, false);
+              p1b = __hiloint2double(hi2, lo);
+              p2 = v;
+            } else {
+              p1b = q.a;
+              p2 = q.r;
+            }
+            const double dnv = hi ? own : p1b, upv = hi ? p1b : own;
+            double t = fma(V.v[0], prev, 0.0);
+            t = fma(V.v[1], dnv, t);
+            t = fma(V.v[2], p1, t);
+            t = fma(V.v[3], upv, t);
+            t = fma(V.v[4], next, t);
+            return fma(b, p1, fma(na, t, fma(nbp, p2, p1)));
+          };
           // prologue (step()'s): lines -2 .. LD - 1
           const Raw rm2 = raw_at(-2), rm1 = raw_at(-1), r0 = raw_at(0);
           Raw q[LD - 1];  // lines m + 1 .. m + LD - 1
@@ -357,7 +423,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
           double pr_pk = 0.0;  // p_k of line -1: owned, a ghost, or none
           if (l0 >= 1) {
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
-            pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(e_p(edm1)), rm2.p, r0.p), rm1.r));
+            pr_pk = fma(b, rm1.p, fma(na, stencil_u(Vm, rm1.p, ez(e_p(edm1)), rm2.p, r0.p), T3 ? fma(nbp, rm1.r, rm1.p) : rm1.r));
           } else if (is_ghost(-1)) {
             pr_pk = fma(b, rm1.p, fma(na, ap_gh(-1), rghost(-1, rm1)));
             // pulled: this p_{k-1} is the next pass's p_{k-2} of the ghost line (rghost)
@@ -369,7 +435,14 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             o_rk = fma(na, stencil_u(V0, r0.p, ez(e_p(ed0)), rm1.p, q[0].p), fma(nbp, r0.r, r0.p));
             o_pk = fma(b, r0.p, o_rk);
           }
-          double o_epk = epk(ed0);
+          double o_epk, ep_prev = 0.0;  // T3: p_{k-1} of the neighbouring edge row, line m (carried)
+          if constexpr (T3) {
+            const VSet V0 = l0 == 0 ? vals(WA) : VB;
+            o_epk = epk3(e_p(edm1), ed0, e_p(e[0]), r0.p, V0);
+            ep_prev = e_p(ed0);
+          } else {
+            o_epk = epk(ed0);
+          }
           // step m: Ap_{k-1} of line m + 1 (next: 1 owned, values Vt; 2 a ghost line; 0 none) and
           // Ap_k of line m (values Vs)
           auto lstep = [&](auto clc, int32_t m, const VSet& Vs, const VSet& Vt, int next) __attribute__((always_inline)) {
@@ -381,7 +454,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             double rk1 = 0.0, pk1 = 0.0;
             if (next == 1) {
               const double t = stencil_u(Vt, q[0].p, ez(e_p(e[0])), o_pold, q[1].p);
-              rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
+              rk1 = fma(na, t, (T3 || m + 1 < n_run) ? fma(nbp, q[0].r, q[0].p) : q[0].r);
               pk1 = fma(b, q[0].p, rk1);
             } else if (CL && next == 2) {
               rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, q[0]));
@@ -391,11 +464,13 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             const double sum = stencil_u(Vs, o_pk, o_epk, pr_pk, pk1);
             const uint32_t ob = line_ofs(m);
             const double rr = fma(-b, o_pold, o_pk);
-            if (m == 0 || m == n_run - 1 || alt_edge(m)) g_st_nt(rn_, ob + l8, rr);
-            if (edge_lane) {
-              const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
-              g_st(ren, sb, rr);
-              g_st(en, sb, sum);
+            if constexpr (!T3) {  // T3: nobody reads a stored r or edge row
+              if (m == 0 || m == n_run - 1 || alt_edge(m)) g_st_nt(rn_, ob + l8, rr);
+              if (edge_lane) {
+                const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
+                g_st(ren, sb, rr);
+                g_st(en, sb, sum);
+              }
             }
             if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
             const bool bnd = l0 + m == 0 || l0 + m == nl - 1;  // the halo's source lines
@@ -411,7 +486,15 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
             o_rk = rk1;
             o_pold = q[0].p;
             o_pm2 = q[0].r;
-            o_epk = epk(e[0]);
+            if constexpr (T3) {
+              if (next == 1) {
+                const double ep0 = e_p(e[0]);
+                o_epk = epk3(ep_prev, e[0], e_p(e[1]), q[0].p, Vt);
+                ep_prev = ep0;
+              }
+            } else {
+              o_epk = epk(e[0]);
+            }
 #pragma unroll
             for (int d = 0; d + 1 < LD - 1; ++d) {
               q[d] = q[d + 1];
@@ -910,18 +993,31 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: per-run 64-bit bases
   MCG_CHECK(v.ext_len < ((int64_t)1 << 31), "Ap-recomputing carry: a rank's vectors must stay below 2^31 rows");
   if (cm == 4 && p3k && lean && S.dpat != nullptr) {  // lean-only kernels (4 waves per SIMD)
+    const bool t3 = v.p_m2 != nullptr;  // three p buffers (kernel comment)
 #define MCG_LW(QD, PAIR)                                                                                       \
   do {                                                                                                         \
-    if (big)                                                                                                   \
+    if (big && t3)                                                                                             \
+      hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4, true, false, true>), dim3(grid), dim3(kBS), 0, stream, \
+                         S, v, own_off, tr, partials, pstride, st, tol, first, check, rc);                     \
+    else if (big)                                                                                              \
       hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4, true>), dim3(grid), dim3(kBS), 0, stream, S, v, \
                          own_off, tr, partials, pstride, st, tol, first, check, rc);                           \
+    else if (t3)                                                                                               \
+      hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4, false, false, true>), dim3(grid), dim3(kBS), 0, stream, \
+                         S, v, own_off, tr, partials, pstride, st, tol, first, check, rc);                     \
     else                                                                                                       \
       hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, 4>), dim3(grid), dim3(kBS), 0, stream, S, v, own_off, \
                          tr, partials, pstride, st, tol, first, check, rc);                                    \
   } while (0)
 #define MCG_LWE(QD, PAIR, W)                                                                                   \
-  hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true>), dim3(grid), dim3(kBS), 0, stream, S, v, \
-                     own_off, tr, partials, pstride, st, tol, first, check, rc)
+  do {                                                                                                         \
+    if (t3)                                                                                                    \
+      hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true, true>), dim3(grid), dim3(kBS), 0, stream, \
+                         S, v, own_off, tr, partials, pstride, st, tol, first, check, rc);                     \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true>), dim3(grid), dim3(kBS), 0, stream, S, \
+                         v, own_off, tr, partials, pstride, st, tol, first, check, rc);                        \
+  } while (0)
     // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4, the setup's auto_mix_ for the
     // 4-blocks-per-CU grids; measured and dropped: QD 5 at 4 for the odd passes, the same rate, and QD
     // 3 at 6 for the even ones, which spills in the loop: 4096^2 7200 vs 9470 it/s, profiles/r4/mix2;

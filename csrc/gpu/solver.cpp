@@ -103,6 +103,7 @@ void GpuCgSolver::reset() {
     if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
   MCG_HIP(hipMemsetAsync(p_[0].get(), 0, p_[0].bytes(), s), "device memset failed(p)");
   MCG_HIP(hipMemsetAsync(p_[1].get(), 0, p_[1].bytes(), s), "device memset failed(p)");
+  if (p_[2].bytes()) MCG_HIP(hipMemsetAsync(p_[2].get(), 0, p_[2].bytes(), s), "device memset failed(p)");
   // r = b  (CUDACG.cu:248; x0 = 0 so r0 = b - A x0 = b, and p0 = r0 is formed by K_A at k = 0)
   MCG_HIP(hipMemsetAsync(st_.get(), 0, sizeof(CgState), s), "device memset failed");
   if (opt_.recurrence == 2) {
@@ -217,9 +218,13 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
   DeviceBuffer<double>& r_old = odd ? r_ : r1_;
   DeviceBuffer<double>& ap_new = odd ? Ap1_ : Ap_;
   DeviceBuffer<double>& ap_old = odd ? Ap_ : Ap1_;
-  kern::F1Vectors v{r_old.get(), ap_old.get(), p_[(k + 1) & 1].get(), r_new.get(), ap_new.get(), p_[k & 1].get(),
-                    x_.get()};
+  kern::F1Vectors v{r_old.get(), ap_old.get(), pbuf_(k - 1), r_new.get(), ap_new.get(), pbuf_(k), x_.get()};
   v.p_fix = p_[1].get();
+  if (p3buf_) {  // three p buffers: p_k to a buffer this pass does not read (final mode reads p_{m-2} there)
+    v.p_m2 = pbuf_(k - 2);
+    if (final_mode) v.p_new = pbuf_(k - 2);
+    for (int b = 0; b < 3; ++b) v.p_fix3[b] = p_[b].get();
+  }
   v.ext_len = L_.ext_len;
   if (opt_.form.interleave == 1) {
     v.ra_old = reinterpret_cast<const double2*>(ra_[(k + 1) & 1].get());
@@ -249,7 +254,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
         MCG_CHECK(map_pull_(), "in-kernel halo: the peers' buffers are not mapped (attach the communicator)");
         const int pb = (k + 1) & 1;  // p_old / apx_old: the neighbours' pass k-1 outputs
         for (int sd = 0; sd < 2; ++sd) {
-          v.pull_p[sd] = pull_p_[pb][sd];
+          v.pull_p[sd] = pull_p_[pidx_(k - 1)][sd];
           v.pull_ap[sd] = pull_ap_[pb][sd];
         }
       }
@@ -306,13 +311,13 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
 void GpuCgSolver::enqueue_halo_f1_(int k, hipStream_t s) {
   // ghosts read by iteration k: {r, Ap} (or r and Ap) and p of iteration k-1 (parity (k+1)&1)
   const bool odd = (k & 1) != 0;
-  double* vecs[3] = {(odd ? r_ : r1_).get(), (odd ? Ap_ : Ap1_).get(), p_[(k + 1) & 1].get()};
+  double* vecs[3] = {(odd ? r_ : r1_).get(), (odd ? Ap_ : Ap1_).get(), pbuf_(k - 1)};
   int nv = 3;
   static const int widths[2] = {2, 1};
   const int* w = nullptr;
   if (opt_.form.interleave == 1) {
     vecs[0] = ra_[(k + 1) & 1].get();
-    vecs[1] = p_[(k + 1) & 1].get();
+    vecs[1] = pbuf_(k - 1);
     nv = 2;
     w = widths;
   }
@@ -625,7 +630,8 @@ bool GpuCgSolver::map_pull_() {
     const HaloRange* h = nullptr;
     for (const HaloRange& r : L_.recvs)
       if (sd == 0 ? r.gbegin < L_.row_begin : r.gbegin >= L_.row_end) h = &r;
-    for (int b = 0; b < 2; ++b) pull_p_[b][sd] = pull_ap_[b][sd] = nullptr;
+    for (int b = 0; b < 3; ++b) pull_p_[b][sd] = nullptr;
+    for (int b = 0; b < 2; ++b) pull_ap_[b][sd] = nullptr;
     if (h == nullptr) continue;  // the first / last rank: no ghost on that side
     MCG_CHECK(h->count == line && (sd == 0 ? h->gbegin + h->count == L_.row_begin : h->gbegin == L_.row_end),
               "in-kernel halo: the ghosts must be one whole line / plane next to the rank's rows");
@@ -641,10 +647,9 @@ bool GpuCgSolver::map_pull_() {
       return false;  // not mapped (a transport that was never attached, or whose mapping failed)
     }
     const int64_t shift = src - L_.ext_index(h->gbegin);
-    for (int b = 0; b < 2; ++b) {
-      pull_p_[b][sd] = bufs[idx(p_[b].get())] + shift;
-      pull_ap_[b][sd] = bufs[idx(apx_[b].get())] + shift;
-    }
+    for (int b = 0; b < 3; ++b)
+      if (p_[b].bytes()) pull_p_[b][sd] = bufs[idx(p_[b].get())] + shift;
+    for (int b = 0; b < 2; ++b) pull_ap_[b][sd] = bufs[idx(apx_[b].get())] + shift;
   }
   pull_mapped_ = true;
   return true;
@@ -662,12 +667,13 @@ void GpuCgSolver::verify_pull_() {
   bool ok = all_ranks_agree_(mapped);
   if (ok && comm_->moves_data()) {
     const int64_t line = (int64_t)tr_all_.strip * 64, n = L_.n_local();
-    DeviceBuffer<double>* bufs[4] = {&p_[0], &p_[1], &apx_[0], &apx_[1]};
+    DeviceBuffer<double>* bufs[5] = {&p_[0], &p_[1], &apx_[0], &apx_[1], &p_[2]};
+    const int nb = p_[2].bytes() ? 5 : 4;
     std::vector<double> hv(line);
     auto pattern = [&](int64_t g0, int i) {
       for (int64_t t = 0; t < line; ++t) hv[t] = (double)(g0 + t) + 0.25 * i;
     };
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < nb; ++i)
       for (int e = 0; e < 2 && n >= line; ++e) {
         const int64_t l0 = e == 0 ? 0 : n - line;
         pattern(L_.row_begin + l0, i);
@@ -679,8 +685,8 @@ void GpuCgSolver::verify_pull_() {
     DeviceBuffer<double> got(line, "pull check");
     bool match = true;
     for (int sd = 0; sd < 2; ++sd)
-      for (int i = 0; i < 4 && pull_p_[0][sd] != nullptr; ++i) {
-        const double* base = (i < 2 ? pull_p_[i & 1][sd] : pull_ap_[i & 1][sd]);
+      for (int i = 0; i < nb && pull_p_[0][sd] != nullptr; ++i) {
+        const double* base = i == 4 ? pull_p_[2][sd] : (i < 2 ? pull_p_[i & 1][sd] : pull_ap_[i & 1][sd]);
         const int64_t g0 = sd == 0 ? L_.row_begin - line : L_.row_end;
         kern::pull_probe(base + L_.ext_index(g0), line, got.get(), s0_);
         MCG_HIP(hipMemcpyAsync(hv.data(), got.get(), line * sizeof(double), hipMemcpyDeviceToHost, s0_),
@@ -718,17 +724,19 @@ void GpuCgSolver::ensure_ghosts_(int k) {
 }
 
 void GpuCgSolver::drop_graphs_() {
-  for (int g = 0; g < 2; ++g) {
-    if (graph_exec_[g]) (void)hipGraphExecDestroy(graph_exec_[g]);
-    if (graph_[g]) (void)hipGraphDestroy(graph_[g]);
-    graph_exec_[g] = nullptr;
-    graph_[g] = nullptr;
-  }
+  for (int g = 0; g < 2; ++g)
+    for (int ph = 0; ph < 3; ++ph) {
+      if (graph_exec_[g][ph]) (void)hipGraphExecDestroy(graph_exec_[g][ph]);
+      if (graph_[g][ph]) (void)hipGraphDestroy(graph_[g][ph]);
+      graph_exec_[g][ph] = nullptr;
+      graph_[g][ph] = nullptr;
+    }
 }
 
 // Captures 2 (kind 0) or graph_iters (kind 1) iterations starting at an even k_.  The passes
-// depend on k only through its parity (and k >= 2), so one capture replays for every even k_.
-void GpuCgSolver::capture_pair_(int kind) {
+// depend on k only through its parity (and k >= 2) -- with three p buffers also through k mod 3, the
+// phase: one capture per (kind, phase) replays for every such k_.
+void GpuCgSolver::capture_pair_(int kind, int phase) {
   hipStream_t s = s0_;
   const int iters = kind == 0 ? 2 : opt_.graph_iters;
   // halo_ahead: a graph starts with its ghosts in place (joined before the launch) and ends by
@@ -749,10 +757,11 @@ void GpuCgSolver::capture_pair_(int kind) {
   }
   ghosts_for_ = (halo_ahead_ && !pull_) ? k_ : -1;  // nothing captured has run yet
   halo_pending_ = false;
-  const hipError_t ec = hipStreamEndCapture(s, &graph_[kind]);
+  const hipError_t ec = hipStreamEndCapture(s, &graph_[kind][phase]);
   if (comm_ != nullptr) comm_->on_captured(ec == hipSuccess);
   MCG_HIP(ec, "graph capture failed");
-  MCG_HIP(hipGraphInstantiate(&graph_exec_[kind], graph_[kind], nullptr, nullptr, 0), "graph instantiate failed");
+  MCG_HIP(hipGraphInstantiate(&graph_exec_[kind][phase], graph_[kind][phase], nullptr, nullptr, 0),
+          "graph instantiate failed");
 }
 
 void GpuCgSolver::run_iterations(int count) {
@@ -761,9 +770,10 @@ void GpuCgSolver::run_iterations(int count) {
   while (count > 0) {
     if (opt_.use_graph && k_ >= 2 && (k_ % 2) == 0 && count >= 2 && (!pull_ || k_ >= pull_from_)) {
       const int kind = glong && count >= glong ? 1 : 0;
-      if (!graph_exec_[kind]) {
+      const int phase = p3buf_ ? k_ % 3 : 0;
+      if (!graph_exec_[kind][phase]) {
         try {
-          capture_pair_(kind);
+          capture_pair_(kind, phase);
         } catch (const Error& e) {
           std::fprintf(stderr, "[mcg] graph capture unavailable (%s: %s); running eagerly\n", e.what(),
                        e.detail().c_str());
@@ -775,7 +785,7 @@ void GpuCgSolver::run_iterations(int count) {
       }
       if (halo_ahead_ && !pull_) ensure_ghosts_(k_);
       const hipError_t le = (k_ == opt_.hooks.fail_graph_launch_at) ? hipErrorInvalidValue  // test hook
-                                                              : hipGraphLaunch(graph_exec_[kind], s0_);
+                                                              : hipGraphLaunch(graph_exec_[kind][phase], s0_);
       if (le != hipSuccess) {
         (void)hipGetLastError();
         // Only errors that hipGraphLaunch reports while validating its arguments, before it enqueues
@@ -817,7 +827,7 @@ void GpuCgSolver::inject_fault_(int k) {
                                      : ((opt_.recurrence == 1 && (k & 1) == 0) ? r1_.get() : r_.get()) + L_.own_off;
   // the three-term carries recover r from the two p's and read a stored r only past their runs' ends:
   // poison p_{k-1}, which pass k reads everywhere
-  if (ar_ && p3_ && opt_.recurrence == 1) r = p_[(k + 1) & 1].get() + L_.own_off;
+  if (ar_ && p3_ && opt_.recurrence == 1) r = pbuf_(k - 1) + L_.own_off;
   MCG_HIP(hipMemcpyAsync(r, &nan, sizeof(double), hipMemcpyHostToDevice, s0_), "fault injection failed");
 }
 

@@ -46,7 +46,7 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
   h.world = world_;
   h.recurrence = opt_.recurrence;
   h.format = info_.format;
-  h.pass_form = (ar_ ? 1 : 0) | (p3_ ? 2 : 0);
+  h.pass_form = (ar_ ? 1 : 0) | (p3_ ? 2 : 0) | (p3buf_ ? 4 : 0);
   h.n_local = L_.n_local();
   h.ext_len = L_.ext_len;
   h.row_begin = L_.row_begin;
@@ -67,7 +67,7 @@ void GpuCgSolver::save_checkpoint(const std::string& prefix) {
   };
   dump(st_.get(), sizeof(CgState));
   for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1], &ape_[0], &ape_[1],
-                                  &apx_[0], &apx_[1], &w_, &z_, &q_})
+                                  &apx_[0], &apx_[1], &w_, &z_, &q_, &p_[2]})
     dump(b->get(), b->bytes());
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) fail("checkpoint write failed", path);
@@ -84,7 +84,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   CkptHeader h{};
   bool ok = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, kCkptMagic, 8) == 0;
   ok = ok && h.rank == rank_ && h.world == world_ && h.recurrence == opt_.recurrence && h.format == info_.format &&
-       h.pass_form == ((ar_ ? 1 : 0) | (p3_ ? 2 : 0)) &&
+       h.pass_form == ((ar_ ? 1 : 0) | (p3_ ? 2 : 0) | (p3buf_ ? 4 : 0)) &&
        h.n_local == L_.n_local() && h.ext_len == L_.ext_len && h.row_begin == L_.row_begin &&
        h.n_global == L_.n_global && h.seed == spec_.seed && h.kind == (int32_t)spec_.kind &&
        h.rhs == (int32_t)spec_.rhs && h.nnz_local == info_.nnz_local && h.fingerprint == fingerprint();
@@ -101,7 +101,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   };
   load(st_.get(), sizeof(CgState));
   for (DeviceBuffer<double>* b : {&x_, &r_, &r1_, &p_[0], &p_[1], &Ap_, &Ap1_, &ra_[0], &ra_[1], &ape_[0], &ape_[1],
-                                  &apx_[0], &apx_[1], &w_, &z_, &q_})
+                                  &apx_[0], &apx_[1], &w_, &z_, &q_, &p_[2]})
     load(b->get(), b->bytes());
   std::fclose(f);
   if (!ok) fail("checkpoint truncated", path);

@@ -865,6 +865,17 @@ void GpuCgSolver::setup() {
   }
   info_.lean_only = lean_only_;
   info_.lean_mix = auto_mix_ && lean_only_ && g_odd_ > 0 && opt_.hooks.lean_packed != 0;
+  // three p buffers (PassForm::p3buf, cg_carry_ar.hip T3): the 2-D lean three-term dia4 carry, when every
+  // line's slices share one value pattern (a slice recomputes its neighbours' edge rows with its own
+  // values).  Every rank the same (the in-kernel halo maps the same buffer list on every rank)
+  p3buf_ = false;
+  if (opt_.form.p3buf != 0 && ar_ && !ar3_ && p3_ && lean_only_ && !lean_split_ && info_.dia4 && !diav_ &&
+      dpat_.get() != nullptr && opt_.recurrence == 1 && n > 0 && tr_all_.strip > 0)
+    p3buf_ = kern::dia_lines_uniform(dpat_.get(), tr_all_.strip, (n + 63) / 64 / tr_all_.strip, s0_);
+  if (use_comm_ && world_ > 1) p3buf_ = all_ranks_agree_(p3buf_);
+  MCG_CHECK(opt_.form.p3buf != 1 || p3buf_,
+            "p3buf needs the 2-D lean three-term dia4 carry with one value pattern per line on every rank");
+  info_.p3buf = p3buf_;
   // in-kernel halo: the lean carries read their ghost lines / planes from the neighbours' rows and store
   // their own first / last ones write-through (carry_common.hpp PullBases), so an iteration from 2 on is
   // the pass + the all-reduce, no halo step.  The all-reduce orders the passes: a rank's pass k + 1
@@ -967,7 +978,8 @@ void GpuCgSolver::setup() {
   if (comm_ != nullptr) {
     if (use_halo_ && comm_->maps_peers()) xt_.allocate(L_.ext_len, "x", 8);
     halo_reg_.clear();
-    for (DeviceBuffer<double>* b : {&r_, &r1_, &Ap_, &Ap1_, &p_[0], &p_[1], &ra_[0], &ra_[1], &apx_[0], &apx_[1], &w_, &xe_, &xt_})
+    for (DeviceBuffer<double>* b : {&r_, &r1_, &Ap_, &Ap1_, &p_[0], &p_[1], &ra_[0], &ra_[1], &apx_[0], &apx_[1], &w_, &xe_, &xt_,
+                                    &p_[2]})
       if (b->get() != nullptr) halo_reg_.push_back(b->get());
     comm_->register_halo_buffers(halo_reg_, L_.own_off, L_.row_begin);
   }
@@ -1025,7 +1037,7 @@ bool GpuCgSolver::all_ranks_agree_(bool mine) {
 
 std::vector<DeviceBuffer<double>*> GpuCgSolver::vectors_() {
   return {&x_, &r_, &r1_, &Ap_, &Ap1_, &ra_[0], &ra_[1], &p_[0], &p_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1],
-          &w_, &z_, &q_};
+          &w_, &z_, &q_, &p_[2]};
 }
 
 void GpuCgSolver::allocate_vectors_() {
@@ -1079,6 +1091,7 @@ void GpuCgSolver::allocate_vectors_() {
   }
   p_[0].allocate(L_.ext_len, "p", 8, 0, cap);
   p_[1].allocate(L_.ext_len, "p", 8, 0, cap);
+  if (p3buf_) p_[2].allocate(L_.ext_len, "p", 8, 0, cap);
 }
 
 // Physical placement of the vector streams.  The same stream kernel on the same sizes runs at

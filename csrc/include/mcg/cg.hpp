@@ -86,6 +86,10 @@ struct PassForm {
                              // the first two exchange as before).  -1 = auto (when the communicator maps its peers:
                              // Communicator::maps_peers), 0 = off, 1 = on (with a rehearsal communicator that moves no
                              // data, the rank's own first / last line stands in for the neighbours': timing only)
+  int p3buf = -1;            // 2-D lean three-term dia4 carry (every run lean, every line's slices one value
+                             // pattern): three p buffers -- p_k written to one this pass does not read, so r is
+                             // recovered from p_{k-1} / p_{k-2} everywhere and the neighbouring slices' edge rows
+                             // recomputed: no compact edge arrays, no stored r (bitwise the same sums); -1 = auto, 0 = off
   int halo_ahead = -1;       // multi-rank stencils, single-reduction pass: exchange the halo iteration k+1 reads
                              // right after pass k wrote it (side stream, next to the all-reduce) and run one
                              // full pass per iteration instead of interior || halo then boundary.  RCCL's

@@ -265,6 +265,12 @@ struct F1Vectors {
   // store the rank's first / last line's p_k and Ap_k write-through at system scope: the neighbours'
   // next pass reads them over the fabric, ordered after this pass by the all-reduce between
   int pull_pub = 0;
+  // Three p buffers (solver p3buf_, the 2-D lean three-term carry, cg_carry_ar.hip T3): p_new is a buffer
+  // this pass does not read, p_m2 = p_{k-2} (read-only); nullptr: two buffers, p_new holds p_{k-2} on
+  // entry and is overwritten in place.  p_fix3[j % 3] = p_j's buffer (final mode's catch-up of a latched
+  // even m reads p_{m-1}, m known on the device only)
+  const double* p_m2 = nullptr;
+  const double* p_fix3[3] = {nullptr, nullptr, nullptr};
 };
 // In-kernel reduction of a fused pass's block partials (replaces the cg_reduce_f1 launch, so
 // one iteration is ONE kernel + the 32-B all-reduce).  Two-level last-arriver fan-in: each block
@@ -331,6 +337,10 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
                   int32_t ln, bool gfull, double* partials, int pstride, int grid, CgState* st, double tol,
                   int first, int check, int k, int final_mode, hipStream_t stream, const RedCtl& rc = RedCtl(),
                   bool p3 = false, bool lean = false);
+// True when every line's uniform slices share one value pattern (the pattern words of dia_patterns equal
+// up to the line-start / line-end flags, bits 28 / 29): the three-buffer lean carry recomputes a slice's
+// neighbours' edge rows with its own values (cg_carry_ar.hip T3)
+bool dia_lines_uniform(const uint64_t* dpat, int64_t ss, int64_t nl, hipStream_t stream);
 // Runs of a line (kw = 0, 2-D) / plane (kw = waves per block, 3-D, ln = N) carry launch of `grid`
 // blocks over ss * nl slices that do not qualify for the lean step (SellDev::dpat); 0 lets the
 // three-term passes launch their lean-only kernels (`lean`).  Synchronises the stream.

@@ -73,6 +73,7 @@ struct SolverInfo {
   bool xcd_map = false;  // XCD-aware contiguous slice regions (auto for the 3-D stencil's generic pass)
   bool dia4 = false;     // SELL-64/dia4 storage for the Ap-recomputing line-carry pass (CgOptions::carry_dia)
   bool halo_pull = false;  // PassForm::halo_pull: the in-kernel halo (ghost lines read from the peers' rows)
+  bool p3buf = false;      // PassForm::p3buf: three p buffers, no compact edge arrays (cg_carry_ar.hip T3)
   bool diav = false;
   double aligned_fill = 0.0;  // user matrices: SELL-64/aligned slots per nonzero of the per-slice offset unions     // SELL-64/diav: the line carry streams per-row coefficients (variable-coefficient stencils)
   bool p3 = false;       // ... in its three-term form (CgOptions::p3)
@@ -136,7 +137,7 @@ class GpuCgSolver {
   void pick_pipe_order_();                                // pipelined CG: which fork branch goes first
   void spmv_plain_(const double* x_ext, double* y, hipStream_t s);  // y = A x, the format's plain SpMV
   void enqueue_split_spmv_(int k, int which, bool fused_red, int part = 0);  // part: cg_split_spmv
-  void capture_pair_(int kind);
+  void capture_pair_(int kind, int phase);
   void join_halo_();            // s0_ waits for a halo in flight on s1_
   void ensure_ghosts_(int k);   // ghosts of iteration k in place on s0_ (joins a prefetch or exchanges now)
   void inject_fault_(int k);
@@ -163,7 +164,7 @@ class GpuCgSolver {
   int pull_from_ = 2;           // ... first iteration that pulls (reset / resume + 2: the earlier ones exchange)
   bool pull_mapped_ = false;    // ... pull_p_ / pull_ap_ resolved (map_pull_)
   bool pull_checked_ = false;   // ... verify_pull_ ran (the first reset)
-  const double* pull_p_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [p buffer][lo, hi side]
+  const double* pull_p_[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};  // [p buffer][lo, hi side]
   const double* pull_ap_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [apx buffer][lo, hi side]
   std::vector<double*> halo_reg_;  // the buffers registered with the communicator (its peer_view order)
   bool map_pull_();     // false: a peer's buffers are not mapped here (not attached)
@@ -262,7 +263,10 @@ class GpuCgSolver {
     return s;
   }
   // vectors
-  DeviceBuffer<double> x_, r_, p_[2], Ap_, b_, partials_;
+  DeviceBuffer<double> x_, r_, p_[3], Ap_, b_, partials_;  // p_[2]: the third p buffer (p3buf_)
+  bool p3buf_ = false;  // PassForm::p3buf: p_j in p_[j mod 3] (else p_[j & 1])
+  int pidx_(int j) const { return p3buf_ ? ((j % 3) + 3) % 3 : (j & 1); }
+  double* pbuf_(int j) { return p_[pidx_(j)].get(); }
   DeviceBuffer<double> r1_, Ap1_;  // second parity buffers of the single-reduction recurrence
   bool pipe_ar_first_ = false;
   DeviceBuffer<double> w_, z_, q_, xe_;  // pipelined CG: w = A r (ext), z = A s, q = A w, x in the ext layout
@@ -290,8 +294,9 @@ class GpuCgSolver {
   bool auto_mix_ = false;                              // ... chosen by the setup (4-blocks-per-CU grids)
   // graph of two iterations (even, odd)
   // [0]: one iteration pair, [1]: graph_iters iterations (when > 2)
-  hipGraph_t graph_[2] = {nullptr, nullptr};
-  hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
+  // [kind][phase]: with three p buffers (p3buf_) a captured run of iterations depends on k mod 3 too
+  hipGraph_t graph_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+  hipGraphExec_t graph_exec_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
   void drop_graphs_();
   double setup_seconds_ = 0.0;
   uint64_t fingerprint_ = 0;  // problem_fingerprint(spec_), recorded in checkpoints (computed on first use:

@@ -218,6 +218,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(carry_vc)
       MCG_FORM_PROP(lean_split)
       MCG_FORM_PROP(halo_pull)
+      MCG_FORM_PROP(p3buf)
       .def_readwrite("pipe_rr", &CgOptions::pipe_rr)
       .def_readwrite("graph_iters", &CgOptions::graph_iters)
       .def_readwrite("placement_tries", &CgOptions::placement_tries)
@@ -490,6 +491,7 @@ PYBIND11_MODULE(_C, m) {
         d["dia4"] = i.dia4;
         d["diav"] = i.diav;
         d["halo_pull"] = i.halo_pull;
+        d["p3buf"] = i.p3buf;
         d["aligned_fill"] = i.aligned_fill;
         d["p3"] = i.p3;
         d["dia_uniform"] = i.dia_uniform;

@@ -266,6 +266,24 @@ def test_local_ranks_in_kernel_halo_bitwise(mcg, world, problem, kw):
     assert all(abs(q["true_rnorm"] - q["rnorm"]) <= 1e-8 * q["true_rnorm"] for q in outs["pull"]["ranks"])
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_local_ranks_p3buf_bitwise(mcg, world):
+    """Three p buffers at P > 1 (the ghost lines' p_{k-2} in the third buffer's ghost rows, pulled or
+    exchanged): bit for bit the two-buffer lean pass, with the in-kernel halo and with the halo
+    exchanged, over 40 iterations."""
+    spec = mcg.make_problem("poisson2d", n=4096, rhs="random")
+    C = mcg.native()
+    for hp in (1, 0):
+        outs = {}
+        for pb in (1, 0):
+            o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8, overlap=False)
+            o.halo_pull = hp
+            o.p3buf = pb
+            outs[pb] = C.run_local_ranks(spec.native(), o, world, 40, True)
+        assert [q["rnorm"] for q in outs[1]["ranks"]] == [q["rnorm"] for q in outs[0]["ranks"]], hp
+        np.testing.assert_array_equal(outs[1]["x"], outs[0]["x"])
+
+
 @pytest.mark.parametrize("problem,n", [("poisson2d", 2048), ("poisson3d", 64)])
 def test_local_ranks_in_kernel_halo_converges(mcg, problem, n):
     """The in-kernel halo to convergence at P = 4 against the CPU oracle (the reference's recurrence)."""

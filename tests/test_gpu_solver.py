@@ -492,3 +492,41 @@ def test_lean_mix_auto_on_small_grids(mcg):
     assert b._s.phase_profile(8)["iteration"] > 0
     big = mcg.CGSolver(mcg.make_problem("poisson2d", n=8192), format="sellc8", recurrence=1)
     assert big.info["lean_only"] and not big.info["lean_mix"] and big.info["grid_odd"] == 0
+
+
+@pytest.mark.parametrize("n", [1024, 4096])
+@pytest.mark.parametrize("graph", [True, False])
+def test_p3buf_bitwise_equal_to_two_buffer_lean(mcg, n, graph):
+    """Three p buffers (PassForm::p3buf, cg_carry_ar.hip T3): p_k goes to a buffer the pass does not
+    read, r is recovered from p_{k-1} / p_{k-2} on every line and the neighbouring slices' edge rows
+    are recomputed instead of read from compact edge arrays -- the same sums in the same order, so bit
+    for bit the two-buffer lean pass.  41 iterations (an odd count: the final pass's x catch-up), in
+    graphs (captures keyed by k mod 3) and eagerly; 4096^2 takes the packed-edge kernels."""
+    spec = mcg.make_problem("poisson2d", n=n, rhs="random")
+    outs = {}
+    for pb in (1, 0):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=41, p3buf=pb, use_graph=graph)
+        assert s.info["p3buf"] == (pb == 1) and s.info["lean_only"], s.info
+        outs[pb] = (s.solve(), s.true_residual_norm())
+    (a, ta), (b, tb) = outs[1], outs[0]
+    assert a["rnorm"] == b["rnorm"] and a["iterations"] == b["iterations"] == 41
+    np.testing.assert_array_equal(a["x_local"], b["x_local"])
+    assert ta == tb
+
+
+def test_p3buf_default_converges_like_the_cpu_oracle(mcg):
+    """The default 2-D path takes the three buffers, converges in the oracle's iteration count and
+    latches the same x as the two-buffer form (convergence after an even and an odd pass)."""
+    C = mcg.native()
+    for n in (1024, 768):
+        spec = mcg.make_problem("poisson2d", n=n, rhs="random")
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, rtol=1e-8, maxit=20000)
+        assert s.info["p3buf"], s.info
+        out = s.solve()
+        ref = mcg.CGSolver(spec, format="sellc8", recurrence=-1, rtol=1e-8, maxit=20000, p3buf=0).solve()
+        assert out["converged"] and out["iterations"] == ref["iterations"], (out["iterations"], ref["iterations"])
+        np.testing.assert_array_equal(out["x_local"], ref["x_local"])
+        co = C.CgOptions(maxit=20000)
+        co.rtol = 1e-8
+        cpu = C.cpu_cg(spec.native(), co)
+        assert abs(out["iterations"] - cpu["iterations"]) <= max(2, cpu["iterations"] // 200)
