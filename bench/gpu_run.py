@@ -276,6 +276,13 @@ def recipes(a) -> dict:
                   + counters("share8_2d_waves", "k_cg_carry_ar", f"{S8} --steps 32 --warmup 4", WAVES)
                   + counters("p1_2d_waves", "k_cg_carry_ar", "--steps 8 --warmup 2", WAVES)
                   + counters("p1_2d_dram", "k_cg_carry_ar", "--steps 8 --warmup 2"),
+        # r5: three p buffers (the lean 2-D carry without compact edge arrays) against two, kernel stats + DRAM
+        "p3buf": stats("p3_16384", "--steps 64 --warmup 8") + stats("p2_16384", "--steps 64 --warmup 8 --set p3buf=0")
+                 + stats("p3_4096", "--grid 4096 --steps 640 --warmup 64")
+                 + stats("p2_4096", "--grid 4096 --steps 640 --warmup 64 --set p3buf=0")
+                 + counters("p3_16384_dram", "k_cg_carry_ar", "--steps 8 --warmup 2")
+                 + counters("p3_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8")
+                 + counters("p2_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8 --set p3buf=0"),
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),
