@@ -1023,6 +1023,7 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     // 3 at 6 for the even ones, which spills in the loop: 4096^2 7200 vs 9470 it/s, profiles/r4/mix2;
     // r5 also dropped depth 2, 4 (3 waves per SIMD) and 6 (2): profiles/r3/lean, r4/mix)
     if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
+    else if (depth == 15 && !big && !pair) MCG_LWE(3, false, 6);  // experiment: 6 waves per SIMD
     else if (depth == 14 && !big) { if (pair) MCG_LWE(4, true, 4); else MCG_LWE(4, false, 4); }
     else { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
 #undef MCG_LWE

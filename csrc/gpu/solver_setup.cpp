@@ -4,6 +4,7 @@
 #include "mcg/solver.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -758,10 +759,14 @@ void GpuCgSolver::setup() {
         }
       }
       if (opt_.blocks_per_cu > 0) g = ncu_ * opt_.blocks_per_cu;  // fixed (tests: the generic pass's grid)
-      // the 4-blocks-per-CU grids (64-line runs: 4096^2, latency-bound passes): packed slice edges, the
-      // even passes at 5 waves per SIMD (depth 3), the odd ones at depth 4 with 4 (each on its own grid;
-      // 4096^2: 8441-8542 vs 8181-8188 it/s on one box, profiles/r4/edge2)
-      auto_mix_ = bpc_rule == 4 && opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29);
+      // packed slice edges, the even passes on 5 or 6 blocks per CU (depth 3), the odd ones at depth 4 on
+      // 4 (each on its own grid): r4 took it on the 4-blocks-per-CU grids (64-line runs: 4096^2 8441-8542
+      // vs 8181-8188 it/s, profiles/r4/edge2); with three p buffers (p3buf) on every size below 2^29
+      // rows: 16384^2 642-648 vs 612-615 on one grid of 16 per CU, a P = 8 share 4720 vs 4489, and 6 per
+      // CU for the even passes where their runs keep >= 64 lines (the share 4826; 4096^2, 43-line runs:
+      // 8346-8442 vs 8872-8982 at 5), profiles/r5/mix
+      (void)bpc_rule;
+      auto_mix_ = opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29);
     }
     auto lean_ok = [&](int gg) {
       return kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, gg, ar3_ ? info_.ar3_kw : 0,
@@ -770,10 +775,12 @@ void GpuCgSolver::setup() {
     // the odd passes (x update paired in) on a grid of their own (auto_mix_): both grids' runs must qualify
     int go = g;
     if (auto_mix_) {
-      if (lean_ok(ncu_ * 5) && lean_ok(ncu_ * 4)) {
-        g = ncu_ * 5;
+      const int64_t runs6 = std::max<int64_t>(1, (int64_t)ncu_ * 6 * 4 / tr_all_.strip);
+      const int we = nlines / runs6 >= 64 ? 6 : 5;
+      if (lean_ok(ncu_ * we) && lean_ok(ncu_ * 4)) {
+        g = ncu_ * we;
         go = ncu_ * 4;
-        lean_depth_even_ = opt_.hooks.lean_packed == 0 ? 0 : 13;
+        lean_depth_even_ = opt_.hooks.lean_packed == 0 ? 0 : (we == 6 ? 15 : 13);
         lean_depth_odd_ = opt_.hooks.lean_packed == 0 ? 0 : 14;
       } else {
         auto_mix_ = false;

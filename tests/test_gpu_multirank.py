@@ -231,12 +231,13 @@ def test_local_ranks_default_serial_order_matches_single_rank(mcg, world, proble
 def test_local_ranks_lean_runs_bitwise(mcg, problem, n, world):
     """With ghost lines (P > 1) the lean runs of the three-term dia4 carry take the runs clear of the
     rank's outer lines; every rank's x and the iteration count are bit for bit those of
-    dia_uniform = 0 (the generic step for every run)."""
+    dia_uniform = 0 (the generic step for every run), on one grid (4 blocks per CU: the auto lean grids
+    differ from the generic pass's, and the block partials' order with them)."""
     spec = mcg.make_problem(problem, n=n, rhs="random")
     C = mcg.native()
     outs = []
     for du in (-1, 0):
-        o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8)
+        o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8, blocks_per_cu=4)
         o.dia_uniform = du
         outs.append(C.run_local_ranks(spec.native(), o, world, 30, True))
     assert [r["rnorm"] for r in outs[0]["ranks"]] == [r["rnorm"] for r in outs[1]["ranks"]]

@@ -430,11 +430,12 @@ def test_dia_uniform_lean_runs_bitwise(mcg, n):
     """Lean runs of the three-term 2-D dia4 carry (runs whose slices all carry one uniform value
     pattern: values in scalar registers, no codes streamed) compute exactly what the generic step
     computes: x and ||r|| bit for bit against dia_uniform = 0, at odd and even iteration counts
-    (paired x update) and at convergence.  At these sizes the auto grid gives runs of 4 / 16 lines,
+    (paired x update) and at convergence.  Both on one grid of 4 blocks per CU (the auto lean grids
+    differ from the generic pass's, and the block partials' order with them): runs of 4 / 16 lines,
     so most runs are lean (l0 >= 2, l1 <= lines - 4)."""
     spec = mcg.make_problem("poisson2d", n=n, rhs="random")
-    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8)
-    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, dia_uniform=0)
+    a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, blocks_per_cu=4)
+    b = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8, dia_uniform=0, blocks_per_cu=4)
     assert a.info["p3"] and a.info["dia4"] and b.info["p3"]
     assert a.info["dia_uniform"] > 0.9 and b.info["dia_uniform"] == 0.0
     assert a.info["bytes_per_iter_model"] < b.info["bytes_per_iter_model"]
@@ -471,10 +472,10 @@ def test_dia_uniform_lean_runs_bitwise_3d(mcg, n):
 
 
 def test_lean_mix_auto_on_small_grids(mcg):
-    """The setup's geometry for 4-blocks-per-CU grids (64-line runs, e.g. 4096^2): packed slice edges,
-    the even passes on 5 blocks per CU, the odd passes on their own 4-per-CU grid at depth 4; the
-    solve tracks the explicitly configured default-kernel solve on the same two grids bit for bit.
-    A 16384-wide grid (16 blocks per CU) keeps one grid."""
+    """The setup's 2-D lean geometry (r5: every size below 2^29 rows): packed slice edges, the even
+    passes on 5 blocks per CU (6 where their runs keep >= 64 lines), the odd passes on their own
+    4-per-CU grid at depth 4; the solve tracks the explicitly configured default-kernel solve on the
+    same two grids bit for bit.  8192^2 takes 6 per CU for the even passes."""
     spec = mcg.make_problem("poisson2d", n=4096, rhs="random")
     a = mcg.CGSolver(spec, format="sellc8", recurrence=1, check_every=8)
     assert a.info["lean_only"] and a.info["lean_mix"] and a.info["grid_odd"] == a.info["grid_a"] * 4 // 5
@@ -491,7 +492,8 @@ def test_lean_mix_auto_on_small_grids(mcg):
     b.reset()
     assert b._s.phase_profile(8)["iteration"] > 0
     big = mcg.CGSolver(mcg.make_problem("poisson2d", n=8192), format="sellc8", recurrence=1)
-    assert big.info["lean_only"] and not big.info["lean_mix"] and big.info["grid_odd"] == 0
+    assert big.info["lean_only"] and big.info["lean_mix"] and big.info["grid_odd"] * 6 == big.info["grid_a"] * 4
+    assert a.info["grid_odd"] * 5 == a.info["grid_a"] * 4
 
 
 @pytest.mark.parametrize("n", [1024, 4096])

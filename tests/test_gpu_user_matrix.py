@@ -226,9 +226,10 @@ def test_lean_runs_on_user_stencils(mcg, kind):
         d = d + 0.25 * (((np.arange(n * n) // n) % 7) == 3)
     A.setdiag(d)
     p = mcg.csr_problem(A.tocsr(), rhs="random")
-    a = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, lean_split=0)
-    b = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, dia_uniform=0)
-    c = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, lean_split=1)
+    # one grid for all three (the auto lean grids differ from the generic pass's: 4 blocks per CU)
+    a = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, lean_split=0, blocks_per_cu=4)
+    b = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, dia_uniform=0, blocks_per_cu=4)
+    c = mcg.CGSolver(p, format="sellc8", recurrence=1, check_every=8, lean_split=1, blocks_per_cu=4)
     assert a.info["dia4"] and a.info["p3"] and b.info["p3"] and c.info["p3"]
     assert a.info["lean_split"] == 0.0 and b.info["lean_split"] == 0.0
     if kind == "shift":
