@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -1018,12 +1019,13 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
       hipLaunchKernelGGL((k_cg_carry_ar<4, 5, QD, PAIR, true, 1, W, false, true>), dim3(grid), dim3(kBS), 0, stream, S, \
                          v, own_off, tr, partials, pstride, st, tol, first, check, rc);                        \
   } while (0)
-    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 14: QD 4 at 4, the setup's auto_mix_ for the
-    // 4-blocks-per-CU grids; measured and dropped: QD 5 at 4 for the odd passes, the same rate, and QD
-    // 3 at 6 for the even ones, which spills in the loop: 4096^2 7200 vs 9470 it/s, profiles/r4/mix2;
-    // r5 also dropped depth 2, 4 (3 waves per SIMD) and 6 (2): profiles/r3/lean, r4/mix)
+    // packed edges (depth 13: QD 3 at 5 waves per SIMD, 15: QD 3 at 6 (even passes whose runs keep >= 64
+    // lines; with three p buffers 80 VGPRs: r4's two-buffer kernel spilled there), 14: QD 4 at 4 (odd), the
+    // setup's auto_mix_; measured and dropped: QD 5 at 4 for the odd passes, the same rate; r5: QD 4 for
+    // the even ones at 5 / 6 (16384^2 644.6 / 620.1 vs 646.0, profiles/r5/mix/qd4); r5 also dropped depth
+    // 2, 4 (3 waves per SIMD) and 6 (2): profiles/r3/lean, r4/mix)
     if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
-    else if (depth == 15 && !big && !pair) MCG_LWE(3, false, 6);  // experiment: 6 waves per SIMD
+    else if (depth == 15 && !big && !pair) MCG_LWE(3, false, 6);  // even passes at 6 waves per SIMD
     else if (depth == 14 && !big) { if (pair) MCG_LWE(4, true, 4); else MCG_LWE(4, false, 4); }
     else { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
 #undef MCG_LWE
