@@ -247,7 +247,9 @@ struct F1Vectors {
   int64_t ext_len = 0;  // ext-layout length of r / Ap / p (bounds of the line-carry pass's edge loads)
   // Ap-recomputing carry (cg_carry_ar.hip): Ap of each slice's two edge rows (lanes 0 / 63),
   // 2 doubles per owned slice, iteration k-1 / k; r_old/new, p_old/new as above, ap_old/new the
-  // ext-layout Ap of the rank's first / last line and of its ghost lines (multi-rank, else null)
+  // ext-layout Ap of the rank's first / last line and of its ghost lines (multi-rank, else null).
+  // The three-buffer lean passes (p_m2 below) neither read nor write the compact arrays (only pass 0,
+  // the two-term kernel, still writes them)
   const double* ape_old = nullptr;
   double* ape_new = nullptr;
   // ... its three-term form: r of the same edge rows, same compact layout (2 doubles per slice), so
