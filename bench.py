@@ -364,6 +364,9 @@ def _run_rank(args, out_fd) -> int:
                       "graph_fallbacks": info.get("graph_fallbacks", 0),
                       "setup_s": round(setup_s, 3), "placement_sets": info.get("placement_sets"),
                       "placement_gain": round(info.get("placement_gain", 1.0), 4),
+                      # the probe's spread: two passes' time on its best and worst placement (setup)
+                      "placement_best_ms": round(info.get("placement_best_ms", 0.0), 4),
+                      "placement_worst_ms": round(info.get("placement_worst_ms", 0.0), 4),
                       "placement_lead_trial": info.get("placement_lead_trial"),
                       "dia_uniform": round(info.get("dia_uniform", 0.0), 4), "lean_only": info.get("lean_only", False),
                       "halo_pull": info.get("halo_pull", False),

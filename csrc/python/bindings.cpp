@@ -502,6 +502,7 @@ PYBIND11_MODULE(_C, m) {
         d["placement_sets"] = i.placement_sets;
         d["placement_gain"] = i.placement_gain;
         d["placement_best_ms"] = i.placement_best_ms;
+        d["placement_worst_ms"] = i.placement_worst_ms;
         d["placement_lead_trial"] = i.placement_lead_trial;
         d["placement_peak_bytes"] = i.placement_peak_bytes;
         d["device_bytes"] = i.device_bytes;
