@@ -48,8 +48,10 @@ namespace {
 
 #include "f1_common.hpp"
 
-constexpr int kTU = 8;                // entries per lane in flight (software-pipelined: the next batch's
-                                      // indices / values load while this batch gathers)
+constexpr int kTU = 10;               // entries per lane in flight (software-pipelined: the next batch's
+                                      // indices / values load while this batch gathers); config 5's tiles
+                                      // (~1790 entries) take 3 batches of 640 instead of 4 of 512.  The
+                                      // order of the adds is the same for any kTU (ascending entry index)
 constexpr int kPaceSpins = 4000;      // ~1 ms of polling at most per segment step
 constexpr int kPaceSleep = 8;         // s_sleep units (64 clocks) between two polls of a waiting workgroup
 constexpr uint32_t kColMask = (1u << 22) - 1;
@@ -63,7 +65,7 @@ constexpr uint32_t kColMask = (1u << 22) - 1;
 // own; the waiters poll one replica each, which the XCD's L2 serves until the flag changes (polling
 // the arrival counter itself, whose line every arrival writes, queued the arrivals behind the polls:
 // 14.3 vs 17.5 it/s, profiles/r4/c5).
-__device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live) {
+__device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live, int* behind) {
   __syncthreads();
   if (threadIdx.x == 0 && T.pace != nullptr && *live) {
     const int grp = blockIdx.x & 7;
@@ -83,19 +85,27 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
       for (int z = 0; z < kPaceSleep; ++z) __builtin_amdgcn_s_sleep(1);
     }
     if (spin == kPaceSpins) *live = 0;
+    *behind = spin == 0;  // arrived after the group had moved on: a straggler
   }
   __syncthreads();
+  // A straggler's waves issue first during the next segment.  The wave arbiter favours older waves,
+  // so on every CU the last-dispatched of its four workgroups fell behind at every step and the
+  // others waited for it: 31 % of each workgroup's time at the pacing steps, bimodal within each CU
+  // (profiles/r5/c5/README.md).  Feedback priority: 20.4-20.5 vs 19.5-19.6 it/s (with 10 entries per
+  // lane); a static priority by dispatch order 19.6.
+  if (*behind) __builtin_amdgcn_s_setprio(3);
+  else __builtin_amdgcn_s_setprio(0);
 }
 
 // ABL bit 16 (diagnostic): per-workgroup wall-clock ticks spent waiting at the pacing steps and in total
 constexpr int kTileDiagMax = 4096;
-__device__ unsigned long long g_tile_diag[2 * kTileDiagMax];
+__device__ unsigned long long g_tile_diag[3 * kTileDiagMax];
 
 // one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
-template <int ABL = 0>
+template <int ABL = 0, int TU = kTU>
 __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
 #pragma unroll
-  for (int u = 0; u < kTU; ++u) {
+  for (int u = 0; u < TU; ++u) {
     const int64_t e = k + u * 64;
     if constexpr ((ABL & 8) != 0) {
       q[u] = (uint32_t)e & 1023u;
@@ -115,13 +125,15 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // (as k_split_spmv_aligned_part's halves)
 // kTileB rows per block: 32 KiB of row sums, 4 workgroups per CU
 // ABL (diagnostic ablations, MCG_TILES_ABLATE, results wrong), bits: 1 = no LDS adds (the products summed in
-// a register), 2 = no gathers (the values themselves added), 4 = no pacing, 8 = no tile loads
+// a register), 2 = no gathers (the values themselves added), 4 = no pacing, 8 = no tile loads, 32 = every
+// segment's gathers from segment 0 (always L2-hot)
 template <int MODE, int PART = 0, int ABL = 0>
-__global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
   constexpr int TB = kTileB, TU = kTU;
   __shared__ double acc[4][TB];
+  __shared__ int s_behind;
   int live = 0;  // thread 0's (the only one that paces)
   if constexpr (MODE == 0) {
     const F1Scalars sc = f1_scalars(st, tol, first, check);
@@ -142,7 +154,10 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
   double* a = acc[wv];
   double s_pap = 0.0, s_rap = 0.0, s_apap = 0.0, s_rr = 0.0;
   int step = 0;
-  if (threadIdx.x == 0) live = 1;
+  if (threadIdx.x == 0) {
+    live = 1;
+    s_behind = 0;
+  }
   unsigned long long t_wait = 0;
   const unsigned long long t_start = (ABL & 16) ? wall_clock64() : 0ull;
   for (int64_t rd = 0; rd < rounds; ++rd) {
@@ -157,17 +172,17 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
       const int g0 = seg(0);
       lo = T.tptr[b * G + g0];
       hi = T.tptr[b * G + g0 + 1];
-      tile_batch_load<ABL>(T, lo + lane, hi, q, v);
+      tile_batch_load<ABL, TU>(T, lo + lane, hi, q, v);
     }
     for (int i = 0; i < ns; ++i, ++step) {
       const int g = seg(i);
       int64_t lo_next = hi, hi_next = hi;
       if (active) {
-        const double* __restrict__ pg = p + ((int64_t)g << T.seg_shift);
+        const double* __restrict__ pg = p + ((ABL & 32) ? 0 : ((int64_t)g << T.seg_shift));
         for (int64_t k = lo + lane; k < hi; k += TU * 64) {
           uint32_t qn[TU];
           double vn[TU], x[TU];
-          tile_batch_load<ABL>(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
+          tile_batch_load<ABL, TU>(T, k + TU * 64, hi, qn, vn);  // next batch in flight during this one's gathers
 #pragma unroll
           for (int u = 0; u < TU; ++u) x[u] = (ABL & 2) ? 1.0 : (k + u * 64 < hi ? pg[q[u] & kColMask] : 0.0);
           if constexpr ((ABL & 1) != 0) {
@@ -189,15 +204,15 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
           const int gn = seg(i + 1);
           lo_next = T.tptr[b * G + gn];
           hi_next = T.tptr[b * G + gn + 1];
-          tile_batch_load<ABL>(T, lo_next + lane, hi_next, q, v);
+          tile_batch_load<ABL, TU>(T, lo_next + lane, hi_next, q, v);
         }
       }
       if constexpr ((ABL & 16) != 0) {
         const unsigned long long w0 = wall_clock64();
-        pace_step(T, step, &live);
+        pace_step(T, step, &live, &s_behind);
         t_wait += wall_clock64() - w0;
       } else if constexpr ((ABL & 4) == 0) {
-        pace_step(T, step, &live);
+        pace_step(T, step, &live, &s_behind);
       }
       lo = lo_next;
       hi = hi_next;
@@ -224,10 +239,16 @@ __global__ __launch_bounds__(256) void k_tiles(TilesDev T, const double* __restr
     }
     __syncthreads();
   }
+  if constexpr (MODE == 1 && (ABL & 1) != 0) {
+    if (s_rr == 1.2345e-300) Ap[0] = s_rr;  // keeps the gathers of the no-LDS-add ablation live
+  }
   if constexpr ((ABL & 16) != 0) {
     if (threadIdx.x == 0 && blockIdx.x < kTileDiagMax) {
       g_tile_diag[2 * blockIdx.x] = t_wait;
       g_tile_diag[2 * blockIdx.x + 1] = wall_clock64() - t_start;
+      // where the workgroup ran: HW_ID (cu / sh / se) and XCC_ID
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+      g_tile_diag[2 * kTileDiagMax + blockIdx.x] = ((unsigned long long)xcc << 32) | hw;
     }
   }
   if constexpr (MODE == 0 && PART != 1) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
@@ -383,10 +404,12 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
   else if (ablate == 11) MCG_T1(11);
   else if (ablate == 15) MCG_T1(15);
   else if (ablate == 16) MCG_T1(16);
+  else if (ablate == 32) MCG_T1(32);
+  else if (ablate == 36) MCG_T1(36);
   else MCG_T1(0);
 #undef MCG_T1
   if (ablate == 16) {  // diagnostic: the pacing waits' share of each workgroup's time
-    std::vector<unsigned long long> d(2 * kTileDiagMax);
+    std::vector<unsigned long long> d(3 * kTileDiagMax);
     MCG_HIP(hipStreamSynchronize(stream), "tiles diag sync failed");
     MCG_HIP(hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_tile_diag), d.size() * sizeof(unsigned long long)), "tiles diag copy failed");
     const int nb = std::min(grid, kTileDiagMax);
@@ -399,6 +422,15 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
     }
     std::fprintf(stderr, "{\"tiles_diag\": {\"workgroups\": %d, \"wait_frac\": %.4f, \"mean_ticks\": %.0f, \"min_ticks\": %.0f, \"max_ticks\": %.0f}}\n",
                  nb, t > 0 ? w / t : 0.0, t / nb, tmin, tmax);
+    if (const char* fn = std::getenv("MCG_TILES_DIAG_FILE")) {  // one line per workgroup: block wait total hw_id xcc
+      if (FILE* fo = std::fopen(fn, "w")) {
+        for (int i = 0; i < nb; ++i) {
+          const unsigned long long h = d[2 * kTileDiagMax + i];
+          std::fprintf(fo, "%d %llu %llu %u %u\n", i, d[2 * i], d[2 * i + 1], (unsigned)(h & 0xffffffffu), (unsigned)(h >> 32));
+        }
+        std::fclose(fo);
+      }
+    }
   }
   MCG_HIP(hipGetLastError(), "compute mv failed(y)");
 }
