@@ -48,10 +48,6 @@ namespace {
 
 #include "f1_common.hpp"
 
-constexpr int kTU = 10;               // entries per lane in flight (software-pipelined: the next batch's
-                                      // indices / values load while this batch gathers); config 5's tiles
-                                      // (~1790 entries) take 3 batches of 640 instead of 4 of 512.  The
-                                      // order of the adds is the same for any kTU (ascending entry index)
 constexpr int kPaceSpins = 4000;      // ~1 ms of polling at most per segment step
 constexpr int kPaceSleep = 8;         // s_sleep units (64 clocks) between two polls of a waiting workgroup
 constexpr uint32_t kColMask = (1u << 22) - 1;
@@ -65,6 +61,7 @@ constexpr uint32_t kColMask = (1u << 22) - 1;
 // own; the waiters poll one replica each, which the XCD's L2 serves until the flag changes (polling
 // the arrival counter itself, whose line every arrival writes, queued the arrivals behind the polls:
 // 14.3 vs 17.5 it/s, profiles/r4/c5).
+template <bool PRIO = true>
 __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live, int* behind) {
   __syncthreads();
   if (threadIdx.x == 0 && T.pace != nullptr && *live) {
@@ -92,9 +89,11 @@ __device__ __forceinline__ void pace_step(const TilesDev& T, int step, int* live
   // so on every CU the last-dispatched of its four workgroups fell behind at every step and the
   // others waited for it: 31 % of each workgroup's time at the pacing steps, bimodal within each CU
   // (profiles/r5/c5/README.md).  Feedback priority: 20.4-20.5 vs 19.5-19.6 it/s (with 10 entries per
-  // lane); a static priority by dispatch order 19.6.
-  if (*behind) __builtin_amdgcn_s_setprio(3);
-  else __builtin_amdgcn_s_setprio(0);
+  // lane); a static priority by dispatch order 19.6, three levels by arrival order 20.4-20.5.  Only
+  // with 10 entries per lane: the 201 GB share's 8-per-lane tiles ran 9.17-9.24 with it, 9.51-9.53
+  // without (profiles/r5/c5/prio/ab.md).
+  if (PRIO && *behind) __builtin_amdgcn_s_setprio(3);
+  else if (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // ABL bit 16 (diagnostic): per-workgroup wall-clock ticks spent waiting at the pacing steps and in total
@@ -102,7 +101,7 @@ constexpr int kTileDiagMax = 4096;
 __device__ unsigned long long g_tile_diag[3 * kTileDiagMax];
 
 // one batch of a tile: entries e = k + u * 64 < hi (non-temporal: streamed once)
-template <int ABL = 0, int TU = kTU>
+template <int ABL, int TU>
 __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, int64_t hi, uint32_t* q, double* v) {
 #pragma unroll
   for (int u = 0; u < TU; ++u) {
@@ -126,12 +125,15 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // kTileB rows per block: 32 KiB of row sums, 4 workgroups per CU
 // ABL (diagnostic ablations, MCG_TILES_ABLATE, results wrong), bits: 1 = no LDS adds (the products summed in
 // a register), 2 = no gathers (the values themselves added), 4 = no pacing, 8 = no tile loads, 32 = every
-// segment's gathers from segment 0 (always L2-hot)
-template <int MODE, int PART = 0, int ABL = 0>
+// segment's gathers from segment 0 (always L2-hot), 64 = no straggler priority
+// TU: entries per lane in flight, 8 or 10 (TilesDev::tu; software-pipelined: the next batch's indices and
+// values load while this batch gathers).  The order of the adds is the same for either (ascending entry
+// index), so the results are too.
+template <int MODE, int PART = 0, int ABL = 0, int TU = 10>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
-  constexpr int TB = kTileB, TU = kTU;
+  constexpr int TB = kTileB;
   __shared__ double acc[4][TB];
   __shared__ int s_behind;
   int live = 0;  // thread 0's (the only one that paces)
@@ -209,10 +211,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
       if constexpr ((ABL & 16) != 0) {
         const unsigned long long w0 = wall_clock64();
-        pace_step(T, step, &live, &s_behind);
+        pace_step<TU == 10 && (ABL & 64) == 0>(T, step, &live, &s_behind);
         t_wait += wall_clock64() - w0;
       } else if constexpr ((ABL & 4) == 0) {
-        pace_step(T, step, &live, &s_behind);
+        pace_step<TU == 10 && (ABL & 64) == 0>(T, step, &live, &s_behind);
       }
       lo = lo_next;
       hi = hi_next;
@@ -318,7 +320,7 @@ TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
 
 int tiles_grid(int ncu) {
   int per_cu = 0;
-  const void* f = reinterpret_cast<const void*>(&k_tiles<0>);
+  const void* f = reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   (void)hipGetLastError();
   return std::min(per_cu, 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
@@ -360,11 +362,17 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(rc.ngroups == 0 || (rc.base % kRedGroup == 0 && rc.cnt && rc.lvl2), "in-kernel reduction: bad control block");
   MCG_CHECK(part == 0 || (T.g_lo >= 0 && T.g_lo <= T.g_hi && T.g_hi <= T.G), "tiles: bad own-segment range");
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
-  MCG_CHECK(T.tb == kTileB, "tiles: 1024 rows per block");
+  MCG_CHECK(T.tb == kTileB && (T.tu == 8 || T.tu == 10), "tiles: 1024 rows per block, 8 or 10 entries per lane");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-#define MCG_TL(PART, ABL)                                                                                         \
-  hipLaunchKernelGGL((k_tiles<0, PART, ABL>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
-                     pstride, st, tol, first, check, rc)
+#define MCG_TL(PART, ABL)                                                                                              \
+  do {                                                                                                                 \
+    if (T.tu == 10)                                                                                                    \
+      hipLaunchKernelGGL((k_tiles<0, PART, ABL, 10>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
+                         pstride, st, tol, first, check, rc);                                                          \
+    else                                                                                                               \
+      hipLaunchKernelGGL((k_tiles<0, PART, ABL, 8>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
+                         pstride, st, tol, first, check, rc);                                                          \
+  } while (0)
   static const int ablate = [] {
     const char* e = std::getenv("MCG_TILES_ABLATE");
     return e ? std::atoi(e) : 0;
@@ -375,6 +383,7 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
     else if (ablate == 4) MCG_TL(PART, 4); \
     else if (ablate == 7) MCG_TL(PART, 7); \
     else if (ablate == 15) MCG_TL(PART, 15); \
+    else if (ablate == 64) MCG_TL(PART, 64); \
     else MCG_TL(PART, 0);               \
   } while (0)
   if (part == 1) MCG_TLA(1);
@@ -387,28 +396,32 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
 
 void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hipStream_t stream) {
   if (grid <= 0 || T.nblocks == 0) return;
-  MCG_CHECK(T.tb == kTileB, "tiles: 1024 rows per block");
+  MCG_CHECK(T.tb == kTileB && (T.tu == 8 || T.tu == 10), "tiles: 1024 rows per block, 8 or 10 entries per lane");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
   static const int ablate = [] {
     const char* e = std::getenv("MCG_TILES_ABLATE");
     return e ? std::atoi(e) : 0;
   }();
-#define MCG_T1(ABL)                                                                                                 \
-  hipLaunchKernelGGL((k_tiles<1, 0, ABL>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, nullptr, \
-                     0.0, 0, 0, RedCtl())
+#define MCG_T1(ABL)                                                                                                    \
+  do {                                                                                                                 \
+    if (T.tu == 10)                                                                                                    \
+      hipLaunchKernelGGL((k_tiles<1, 0, ABL, 10>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, \
+                         nullptr, 0.0, 0, 0, RedCtl());                                                                \
+    else                                                                                                               \
+      hipLaunchKernelGGL((k_tiles<1, 0, ABL, 8>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0,  \
+                         nullptr, 0.0, 0, 0, RedCtl());                                                                \
+  } while (0)
   if (ablate == 1) MCG_T1(1);
   else if (ablate == 2) MCG_T1(2);
   else if (ablate == 3) MCG_T1(3);
   else if (ablate == 4) MCG_T1(4);
   else if (ablate == 7) MCG_T1(7);
-  else if (ablate == 11) MCG_T1(11);
   else if (ablate == 15) MCG_T1(15);
   else if (ablate == 16) MCG_T1(16);
   else if (ablate == 32) MCG_T1(32);
-  else if (ablate == 36) MCG_T1(36);
   else MCG_T1(0);
 #undef MCG_T1
-  if (ablate == 16) {  // diagnostic: the pacing waits' share of each workgroup's time
+  if (ablate & 16) {  // diagnostic: the pacing waits' share of each workgroup's time
     std::vector<unsigned long long> d(3 * kTileDiagMax);
     MCG_HIP(hipStreamSynchronize(stream), "tiles diag sync failed");
     MCG_HIP(hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_tile_diag), d.size() * sizeof(unsigned long long)), "tiles diag copy failed");

@@ -15,6 +15,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <vector>
 
@@ -426,7 +427,18 @@ struct TilesDev {
   unsigned* pace = nullptr;  // kTilePaceWords, zeroed by the launchers; nullptr = unpaced
   int64_t ext_len = 0;       // length of p (the last segment may be short)
   int g_lo = 0, g_hi = 0;    // the segments inside this rank's own block of p (all-gather overlap, part 1 / 2)
+  int tu = 10;               // entries per lane in flight, 8 or 10 (tiles_tu)
 };
+// entries per lane in flight for tiles of mean size m: 8 or 10, whichever fills the batches of 64 x TU
+// entries better (config 5's ~1790-entry tiles: 3 batches of 640 rather than 4 of 512; the 201 GB
+// share's ~3580: 7 of 512 rather than 6 of 640)
+inline int tiles_tu(double m) {
+  auto fill = [m](int tu) {
+    const double b = 64.0 * tu;
+    return m <= 0.0 ? 1.0 : m / (std::ceil(m / b) * b);
+  };
+  return fill(10) > fill(8) ? 10 : 8;
+}
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
 int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
 // count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0) then fill

@@ -230,6 +230,8 @@ class GpuCgSolver {
     t.ext_len = L_.ext_len;
     t.g_lo = tg_lo_;
     t.g_hi = tg_hi_;
+    const double ntiles = (double)tgeo_.nblocks * (double)tgeo_.G;
+    t.tu = kern::tiles_tu(ntiles > 0 ? (double)tidx_.size() / ntiles : 0.0);
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)
