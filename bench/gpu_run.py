@@ -283,6 +283,12 @@ def recipes(a) -> dict:
                  + counters("p3_16384_dram", "k_cg_carry_ar", "--steps 8 --warmup 2")
                  + counters("p3_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8")
                  + counters("p2_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8 --set p3buf=0"),
+        # the final r5 tree: kernel stats and DRAM counters of the headline, 4096^2 and 512^3 passes
+        "final": stats("f_16384", "--steps 64 --warmup 8") + stats("f_4096", "--grid 4096 --steps 640 --warmup 64")
+                 + stats("f_512c", "--problem poisson3d --grid 512 --steps 64 --warmup 8")
+                 + counters("f_16384_dram", "k_cg_carry_ar", "--steps 8 --warmup 2")
+                 + counters("f_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8")
+                 + counters("f_512c_dram", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2"),
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),
