@@ -443,6 +443,7 @@ void GpuCgSolver::setup() {
   MCG_CHECK(!tiles_ || pmat_ || opt_.recurrence == 2, "tiles need the split pass on every rank");
   info_.tiles = tiles_;
   info_.tile_segments = tiles_ ? tgeo_.G : 0;
+  info_.tiles_tu = tiles_ ? tiles_view().tu : 0;
   if (pmat_) {
     opt_.form.interleave = 0;
     info_.interleave = false;

@@ -23,6 +23,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <memory>
 #include <vector>
 
@@ -59,6 +60,7 @@ struct SolverInfo {
   bool fused_reduce = false;  // the pass reduces its own block partials (one kernel per iteration)
   bool pmat = false;          // materialized-p split pass (irregular-sparsity path)
   bool tiles = false;         // ... its SpMV on L2-segment COO tiles (CgOptions::tiles)
+  int tiles_tu = 0;           // ... entries per lane in flight (kern::tiles_tu; 0 = no tiles)
   int tile_segments = 0;      // column segments of the tiles (G)
   int sigma = 0;              // SELL-C-sigma window (rows) of a user matrix; 0 = slices in row order
   double sell_fill = 1.0;     // stored SELL slots / nonzeros (padding overhead)
@@ -232,6 +234,7 @@ class GpuCgSolver {
     t.g_hi = tg_hi_;
     const double ntiles = (double)tgeo_.nblocks * (double)tgeo_.G;
     t.tu = kern::tiles_tu(ntiles > 0 ? (double)tidx_.size() / ntiles : 0.0);
+    if (const char* e = std::getenv("MCG_TILES_TU")) t.tu = std::atoi(e) == 8 ? 8 : 10;  // test override
     return t;
   }
   DeviceBuffer<int32_t> win_;  // per-chunk [lo, hi) ext-column windows (windowed pass)

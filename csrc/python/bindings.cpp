@@ -477,6 +477,7 @@ PYBIND11_MODULE(_C, m) {
         d["fused_reduce"] = i.fused_reduce;
         d["pmat"] = i.pmat;
         d["tiles"] = i.tiles;
+        d["tiles_tu"] = i.tiles_tu;
         d["tile_segments"] = i.tile_segments;
         d["sigma"] = i.sigma;
         d["sell_fill"] = i.sell_fill;

@@ -224,6 +224,31 @@ def test_tiles_same_recurrence_as_sell_split_and_deterministic(mcg):
     np.testing.assert_array_equal(c["x_local"], a["x_local"])
 
 
+def test_tiles_lane_depth_bitwise_and_chosen_by_tile_size(mcg, monkeypatch):
+    """8 or 10 entries per lane in flight (kern::tiles_tu, MCG_TILES_TU overrides it): every row's
+    adds run in ascending entry order either way, so the solves are bitwise equal; the default picks
+    the depth whose batches of 64 x TU entries the mean tile fills better."""
+    spec = mcg.make_problem("randspd", **SCR)
+    kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=30, tile_seg_log2=12, tiles=1)
+    out = {}
+    for tu in (8, 10):
+        monkeypatch.setenv("MCG_TILES_TU", str(tu))
+        s = mcg.CGSolver(spec, **kw)
+        assert s.info["tiles"] and s.info["tiles_tu"] == tu
+        out[tu] = s.solve()
+    assert out[8]["rnorm"] == out[10]["rnorm"]
+    np.testing.assert_array_equal(out[8]["x_local"], out[10]["x_local"])
+    monkeypatch.delenv("MCG_TILES_TU")
+    s = mcg.CGSolver(spec, **kw)
+    m = s.info["nnz_local"] / (s.info["tile_segments"] * -(-s.info["n_local"] // 1024))
+
+    def fill(tu):
+        b = 64 * tu
+        return m / (-(-m // b) * b)
+
+    assert s.info["tiles_tu"] == (10 if fill(10) > fill(8) else 8)
+
+
 def test_tiles_several_rounds_of_row_blocks(mcg):
     """More row blocks than waves (blocks_per_cu = 1: 1024 waves, 1.2 M rows = 1172 blocks): the
     waves take a second round of blocks; the same row sums as the full grid (only the dot products'
