@@ -1135,11 +1135,18 @@ void GpuCgSolver::probe_placement_() {
       if (bufs[i]->get()) bufs[i]->relead(lead_of(t, i));
   };
   auto time_pairs = [&]() {
-    // k = 0, 1: both parities, no convergence test (check = 0), so every launch does its work
+    // both parities, no convergence test (check = 0), so every launch does its work; three p buffers:
+    // all six (parity, buffer rotation) combinations -- one rotation of the odd pass ran 15 % slower
+    // than the other two on one box's allocation (2072 vs 1790 us, profiles/r5/final_prof), which
+    // k = 2, 3 never time; probing all six: 651.5-652.2 vs 649.2-651.9 it/s (profiles/r5/probe6)
     MCG_HIP(hipEventRecord(ev_t0_, s0_), "event record failed");
-    for (int r = 0; r < 2; ++r) {
-      enqueue_f1_(2, 0, 0);
-      enqueue_f1_(3, 0, 0);
+    if (p3buf_) {
+      for (int k = 2; k < 8; ++k) enqueue_f1_(k, 0, 0);
+    } else {
+      for (int r = 0; r < 2; ++r) {
+        enqueue_f1_(2, 0, 0);
+        enqueue_f1_(3, 0, 0);
+      }
     }
     MCG_HIP(hipEventRecord(ev_t1_, s0_), "event record failed");
     MCG_HIP(hipEventSynchronize(ev_t1_), "event synchronize failed");
