@@ -64,7 +64,7 @@ __device__ __forceinline__ void ar3_finish(double a0, double a1, double a2, doub
 // from kernel-wide bases, so the lean loop re-bases its ext / x pointers every unrolled step group
 // VC: SELL-64/diav 3-D (variable coefficients, S.cvd / cve / cvs / cvt) instead of dia4 codes; the
 // lean loop carries the streamed values per lane, so these kernels run 2 waves per SIMD (256 VGPRs)
-template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false, bool BIG = false, bool VC = false>
+template <int QD, bool PAIR, int KW, bool P3, bool LEAN = false, bool BIG = false, bool VC = false, bool T3 = false>
 __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S, F1Vectors v, int64_t own,
                                                                           TileRanges tr, int32_t LN, int gfull,
                                                                           double* __restrict__ partials, int pstride,
@@ -72,6 +72,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
                                                                           int check, RedCtl rc) {
   static_assert(KW >= 2 && QD >= 2, "3-D carry: >= 2 waves per block, operands >= 2 planes ahead");
   static_assert(!(VC && BIG), "3-D diav: 32-bit byte offsets (ranks below 2^29 rows)");
+  static_assert(!T3 || (P3 && LEAN && !BIG && !VC), "3-D three p buffers: the dia4 lean kernels below 2^29 rows");
   constexpr int U = 7;
   using Co = ArCodes<VC ? 6 : 4, U>;
   __shared__ double s_val[16];
@@ -457,6 +458,9 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           int32_t mb = 0;
           const double *po_ = po, *ro_ = ro, *apo_ = apo;
           double *pn_ = pn, *rn_ = rn, *x_ = x, *apw_ = apw;
+          // T3 (three p buffers, not BIG): p_{k-2} read-only in its own buffer, so r_{k-1} is recovered from
+          // p_{k-1} / p_{k-2} on every plane, outer line and edge row -- no r stored anywhere
+          const double* __restrict__ pm2_ = T3 ? v.p_m2 : (const double*)pn;
           auto rebase = [&](int32_t m) {
             if constexpr (BIG) {
               mb = m;
@@ -488,7 +492,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           auto raw_ld = [&](int32_t j, int32_t k) {  // plane j's source, plane k's address
             Raw r;
             const uint32_t o = line_ofs(k) + l8;
-            r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
+            r.r = T3 ? g_ld(pm2_, o) : g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
             r.p = pl.ld_p(pl.side(l0 + k, nl), po_, o);
             return r;
           };
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           auto edge_ld = [&](int32_t j) {  // plane j (clamped: compact index to the rank, row to ext)
             Edge r;
             const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
-            r.r = g_ld(reo, c);
+            r.r = T3 ? g_ld(pm2_, line_ofs(jc(j)) - 8u + op) : g_ld(reo, c);  // T3: the row's p_{k-2}
             r.a = g_ld(eao, c);
             r.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
             return r;
@@ -504,18 +508,18 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           auto edge_un = [&](int32_t j) {
             Edge r;
             const uint32_t c = cb0 + (uint32_t)j * SB + oc;
-            r.r = g_ld(reo, c);
+            r.r = T3 ? g_ld(pm2_, line_ofs(j) - 8u + op) : g_ld(reo, c);
             r.a = g_ld(eao, c);
             r.p = g_ld(po_, line_ofs(j) - 8u + op);
             return r;
           };
-          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn_, line_ofs(j) + l8), q.p); };
+          auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(T3 ? pm2_ : (const double*)pn_, line_ofs(j) + l8), q.p); };
           auto is_ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
           auto far_ld = [&](int32_t k) {
             Far f{0.0, 0.0, 0.0};
             if (outer) {
               const uint32_t o = line_ofs(k) + l8 + fob;
-              f.r = g_ld(ro_, o);
+              f.r = g_ld(T3 ? pm2_ : ro_, o);
               f.p = g_ld(po_, o);
               f.a = g_ld(apo_, o);
             }
@@ -538,7 +542,9 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             sum = fma(V.v[5], upn, sum);
             return fma(V.v[6], upl, sum);
           };
-          auto epk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
+          // T3: the loaded r is p_{k-2}; recovered at the use, not at the (early) load
+          auto rv = [&](double r, double p) { return T3 ? fma(nbp, r, p) : r; };
+          auto epk = [&](const Edge& e) { return pk_of(rv(e.r, e.p), e.a, e.p); };
           // prologue (the generic one's): planes -2 .. LD - 1
           const Raw rm2 = raw_ld(-2, jc(-2)), rm1 = raw_ld(-1, jc(-1)), r0 = raw_ld(0, 0);
           Raw qv[LD - 1];  // planes m + 1 .. m + LD - 1
@@ -564,7 +570,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             nbr(1, 0, fm1.p, dn, up);
             const VSet Vm = l0 == 1 ? vals(WA) : VB;
             const double t = stencil_u(Vm, rm1.p, ez(edm1.p), rm2.p, r0.p, dn, up);
-            pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+            pr_pk = fma(b, rm1.p, fma(na, t, rv(rm1.r, rm1.p)));
           } else if (is_ghost(-1)) {
             pr_pk = pk_of(rghost(-1, rm1), ap_gh(-1), rm1.p);
             if (pl.p[0] != nullptr) g_st(const_cast<double*>(po_), line_ofs(-1) + l8, rm1.p);
@@ -579,15 +585,17 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             o_pk = fma(b, r0.p, o_rk);
           }
           double o_epk = epk(ed0);
-          double o_fpk = pk_of(f0.r, f0.a, f0.p);
+          double o_fpk = pk_of(rv(f0.r, f0.p), f0.a, f0.p);
           // next: 1 plane m + 1 owned (values Vt), 2 a ghost plane, 0 none
           auto lstep = [&](auto clc, int32_t m, const VSet& Vs, const VSet& Vt, int next) __attribute__((always_inline)) {
             constexpr bool CL = decltype(clc)::value;
             const int par = m & 1;
             const uint32_t ob = line_ofs(m);
             const double rr = fma(-b, o_pold, o_pk);
-            if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
-            else if (outer) g_st(rn_, ob + l8, rr);
+            if constexpr (!T3) {
+              if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
+              else if (outer) g_st(rn_, ob + l8, rr);
+            }
             const int32_t kn = CL ? jc(m + LD) : m + LD;
             const Raw qn = raw_ld(m + LD, kn);
             const Edge en2 = CL ? edge_ld(m + ED) : edge_un(m + ED);
@@ -601,7 +609,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
               double dn, up;
               nbr(par, 0, fv[0].p, dn, up);
               const double t = stencil_u(Vt, qv[0].p, ez(ev[0].p), o_pold, qv[1].p, dn, up);
-              rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
+              rk1 = fma(na, t, (T3 || m + 1 < n_run) ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
               pk1 = fma(b, qv[0].p, rk1);
             } else if (CL && next == 2) {
               rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, qv[0]));
@@ -620,7 +628,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             if (edge_lane) {
               const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);  // 2 s, 2 s + 1
               g_st(ean, sb, sum);
-              g_st(ren, sb, rr);
+              if constexpr (!T3) g_st(ren, sb, rr);
             }
             s_pap = fma(o_pk, sum, s_pap);
             s_rap = fma(o_rk, sum, s_rap);
@@ -632,7 +640,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             o_pold = qv[0].p;
             o_pm2 = qv[0].r;
             o_epk = epk(ev[0]);
-            o_fpk = pk_of(fv[0].r, fv[0].a, fv[0].p);
+            o_fpk = pk_of(rv(fv[0].r, fv[0].p), fv[0].a, fv[0].p);
 #pragma unroll
             for (int d = 0; d + 1 < LD - 1; ++d) qv[d] = qv[d + 1];
 #pragma unroll
@@ -921,12 +929,15 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
     return;
   }
   const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: per-run bases
+  const bool t3 = v.p_m2 != nullptr;                  // three p buffers (kernel comment)
+  MCG_CHECK(!t3 || (!big && lean && S.dpat != nullptr), "3-D three p buffers: lean dia4 kernels below 2^29 rows");
 #define MCG_A3(QD, PAIR, KW, P3, ...)                                                                         \
   hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, stream, S, v, \
                      own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
 #define MCG_A3P(QD, PAIR, KW)                                         \
   do {                                                                \
     if (p3 && !first && lean && S.dpat != nullptr && big) MCG_A3(QD, PAIR, KW, true, true, true); \
+    else if (p3 && !first && lean && S.dpat != nullptr && t3) MCG_A3(QD, PAIR, KW, true, true, false, false, true); \
     else if (p3 && !first && lean && S.dpat != nullptr) MCG_A3(QD, PAIR, KW, true, true); \
     else if (p3 && !first) MCG_A3(QD, PAIR, KW, true);                \
     else MCG_A3(QD, PAIR, KW, false);                                 \

@@ -269,19 +269,19 @@ def test_local_ranks_in_kernel_halo_bitwise(mcg, world, problem, kw):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_local_ranks_p3buf_bitwise(mcg, world):
-    """Three p buffers at P > 1 (the ghost lines' p_{k-2} in the third buffer's ghost rows, pulled or
-    exchanged): bit for bit the two-buffer lean pass, with the in-kernel halo and with the halo
-    exchanged, over 40 iterations."""
-    spec = mcg.make_problem("poisson2d", n=4096, rhs="random")
+    """Three p buffers at P > 1 (the ghost lines' / planes' p_{k-2} in the third buffer's ghost rows,
+    pulled or exchanged): bit for bit the two-buffer lean pass, 2-D and 3-D, with the in-kernel halo
+    and with the halo exchanged, over 40 iterations."""
     C = mcg.native()
-    for hp in (1, 0):
+    for prob, n, hp in (("poisson2d", 4096, 1), ("poisson2d", 4096, 0), ("poisson3d", 128, 1), ("poisson3d", 128, 0)):
+        spec = mcg.make_problem(prob, n=n, rhs="random")
         outs = {}
         for pb in (1, 0):
             o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8, overlap=False)
             o.halo_pull = hp
             o.p3buf = pb
             outs[pb] = C.run_local_ranks(spec.native(), o, world, 40, True)
-        assert [q["rnorm"] for q in outs[1]["ranks"]] == [q["rnorm"] for q in outs[0]["ranks"]], hp
+        assert [q["rnorm"] for q in outs[1]["ranks"]] == [q["rnorm"] for q in outs[0]["ranks"]], (prob, hp)
         np.testing.assert_array_equal(outs[1]["x"], outs[0]["x"])
 
 

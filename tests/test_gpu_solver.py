@@ -516,6 +516,37 @@ def test_p3buf_bitwise_equal_to_two_buffer_lean(mcg, n, graph):
     assert ta == tb
 
 
+@pytest.mark.parametrize("n", [128, 256])
+@pytest.mark.parametrize("graph", [True, False])
+def test_p3buf_3d_bitwise_equal_to_two_buffer_lean(mcg, n, graph):
+    """3-D three p buffers (cg_carry_ar3.hip T3): r recovered from p_{k-1} / p_{k-2} on every plane,
+    the blocks' outer lines and the slices' edge rows, none stored -- the same operands in the same
+    fma order as the stored r, so bit for bit the two-buffer lean plane carry; 41 iterations."""
+    spec = mcg.make_problem("poisson3d", n=n, rhs="random")
+    outs = {}
+    for pb in (1, 0):
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=41, p3buf=pb, use_graph=graph)
+        assert s.info["p3buf"] == (pb == 1) and s.info["lean_only"], s.info
+        outs[pb] = (s.solve(), s.true_residual_norm())
+    (a, ta), (b, tb) = outs[1], outs[0]
+    assert a["rnorm"] == b["rnorm"] and a["iterations"] == b["iterations"] == 41
+    np.testing.assert_array_equal(a["x_local"], b["x_local"])
+    assert ta == tb
+
+
+def test_p3buf_3d_default_converges_like_the_two_buffer_form(mcg):
+    """The default 3-D path takes the three buffers and converges to the same x, in the same
+    iteration count, as the two-buffer form (latched after an even or an odd pass)."""
+    for n in (128, 192):  # the 3-D carry: N a multiple of 64
+        spec = mcg.make_problem("poisson3d", n=n, rhs="random")
+        s = mcg.CGSolver(spec, format="sellc8", recurrence=-1, rtol=1e-8, maxit=20000)
+        assert s.info["p3buf"], s.info
+        out = s.solve()
+        ref = mcg.CGSolver(spec, format="sellc8", recurrence=-1, rtol=1e-8, maxit=20000, p3buf=0).solve()
+        assert out["converged"] and out["iterations"] == ref["iterations"]
+        np.testing.assert_array_equal(out["x_local"], ref["x_local"])
+
+
 def test_p3buf_default_converges_like_the_cpu_oracle(mcg):
     """The default 2-D path takes the three buffers, converges in the oracle's iteration count and
     latches the same x as the two-buffer form (convergence after an even and an odd pass)."""
