@@ -283,6 +283,15 @@ def recipes(a) -> dict:
                  + counters("p3_16384_dram", "k_cg_carry_ar", "--steps 8 --warmup 2")
                  + counters("p3_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8")
                  + counters("p2_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8 --set p3buf=0"),
+        # r5: the 3-D lean plane carry on three p buffers against two: A/B, kernel stats, DRAM, priced shares
+        "p3buf3d": [(f"{t}{i}", 300, bench(f"--problem poisson3d --grid 512 --phases 0{a}"))
+                    for i in (1, 2) for t, a in (("ab3", ""), ("ab2", " --set p3buf=0"))]
+                   + stats("p3_512", "--problem poisson3d --grid 512 --steps 64 --warmup 8")
+                   + counters("p3_512_dram", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2")
+                   + counters("p2_512_dram", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2 --set p3buf=0")
+                   + [(f"priced512_{w}", 200, f"{PY} bench/pipe_latency.py --problem poisson3d --grid 512 --world {w} "
+                                              f"--rank {3 if w > 2 else 1} --recurrences 1 --graphs 1 --overlaps 1,0 "
+                                              f"--delays 0,10,20 --halo-us 10 --iters 320") for w in (2, 4, 8)],
         # the final r5 tree: kernel stats and DRAM counters of the headline, 4096^2 and 512^3 passes
         "final": stats("f_16384", "--steps 64 --warmup 8") + stats("f_4096", "--grid 4096 --steps 640 --warmup 64")
                  + stats("f_512c", "--problem poisson3d --grid 512 --steps 64 --warmup 8")
