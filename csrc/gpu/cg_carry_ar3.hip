@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
                                                                           int check, RedCtl rc) {
   static_assert(KW >= 2 && QD >= 2, "3-D carry: >= 2 waves per block, operands >= 2 planes ahead");
   static_assert(!(VC && BIG), "3-D diav: 32-bit byte offsets (ranks below 2^29 rows)");
-  static_assert(!T3 || (P3 && LEAN && !BIG && !VC), "3-D three p buffers: the dia4 lean kernels below 2^29 rows");
+  static_assert(!T3 || (P3 && LEAN && !BIG), "3-D three p buffers: the lean kernels below 2^29 rows");
   constexpr int U = 7;
   using Co = ArCodes<VC ? 6 : 4, U>;
   __shared__ double s_val[16];
@@ -221,10 +221,13 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
         auto line_ofs = [&](int32_t j) { return ob0 + (uint32_t)j * LOB; };
         PullBases pl;  // in-kernel halo (the 2-D lean loops')
         pl.at(v, 0);
+        // T3: p_{k-2} read-only in its own buffer; r_{k-1} recovered everywhere (the dia4 loop below)
+        const double* __restrict__ pm2 = T3 ? v.p_m2 : (const double*)pn;
+        auto rv = [&](double r, double p) { return T3 ? fma(nbp, r, p) : r; };
         auto raw_ld = [&](int32_t j, int32_t k) {
           Raw r;
           const uint32_t o = line_ofs(k) + l8;
-          r.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
+          r.r = T3 ? g_ld(pm2, o) : g_ld((j >= 0 && j < n_run) ? (const double*)pn : ro, o);
           r.p = pl.ld_p(pl.side(l0 + k, nl), po, o);
           return r;
         };
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
         auto edge_ld = [&](int32_t j) {
           Edge r;
           const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
-          r.r = g_ld(reo, c);
+          r.r = T3 ? g_ld(pm2, line_ofs(jc(j)) - 8u + op) : g_ld(reo, c);
           r.a = g_ld(eao, c);
           r.p = g_ld(po, line_ofs(jc(j)) - 8u + op);
           return r;
@@ -240,18 +243,18 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
         auto edge_un = [&](int32_t j) {
           Edge r;
           const uint32_t c = cb0 + (uint32_t)j * SB + oc;
-          r.r = g_ld(reo, c);
+          r.r = T3 ? g_ld(pm2, line_ofs(j) - 8u + op) : g_ld(reo, c);
           r.a = g_ld(eao, c);
           r.p = g_ld(po, line_ofs(j) - 8u + op);
           return r;
         };
-        auto rghost = [&](int32_t j, const Raw& qq) { return fma(nbp, g_ld(pn, line_ofs(j) + l8), qq.p); };
+        auto rghost = [&](int32_t j, const Raw& qq) { return fma(nbp, g_ld(T3 ? pm2 : (const double*)pn, line_ofs(j) + l8), qq.p); };
         auto is_ghost = [&](int32_t j) { return gfull && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
         auto far_ld = [&](int32_t k) {
           Far f{0.0, 0.0, 0.0};
           if (outer) {
             const uint32_t o = line_ofs(k) + l8 + fob;
-            f.r = g_ld(ro, o);
+            f.r = g_ld(T3 ? pm2 : ro, o);
             f.p = g_ld(po, o);
             f.a = g_ld(apo, o);
           }
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           sum = fma(V.v[5], upn, sum);
           return fma(V.v[6], upl, sum);
         };
-        auto epk = [&](const Edge& e) { return pk_of(e.r, e.a, e.p); };
+        auto epk = [&](const Edge& e) { return pk_of(rv(e.r, e.p), e.a, e.p); };
         const Raw rm2 = raw_ld(-2, jc(-2)), rm1 = raw_ld(-1, jc(-1)), r0 = raw_ld(0, 0);
         Raw qv[LD - 1];
 #pragma unroll
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           double dn, up;
           nbr(1, 0, fm1.p, dn, up);
           const double t = stencil_v(mkv(cm1, cm2.t), rm1.p, edm1.p, rm2.p, r0.p, dn, up);
-          pr_pk = fma(b, rm1.p, fma(na, t, rm1.r));
+          pr_pk = fma(b, rm1.p, fma(na, t, rv(rm1.r, rm1.p)));
         } else if (is_ghost(-1)) {
           pr_pk = pk_of(rghost(-1, rm1), ap_gh(-1), rm1.p);
           if (pl.p[0] != nullptr) g_st(const_cast<double*>(po), line_ofs(-1) + l8, rm1.p);
@@ -342,15 +345,17 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           o_pk = fma(b, r0.p, o_rk);
         }
         double o_epk = epk(ed0);
-        double o_fpk = pk_of(f0.r, f0.a, f0.p);
+        double o_fpk = pk_of(rv(f0.r, f0.p), f0.a, f0.p);
         // next: 1 plane m + 1 owned, 2 a ghost plane, 0 none
         auto lstep = [&](auto clc, int32_t m, int next) __attribute__((always_inline)) {
           constexpr bool CL = decltype(clc)::value;
           const int par = m & 1;
           const uint32_t ob = line_ofs(m);
           const double rr = fma(-b, o_pold, o_pk);
-          if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
-          else if (outer) g_st(rn, ob + l8, rr);
+          if constexpr (!T3) {
+            if (m == 0 || m == n_run - 1) g_st_nt(rn, ob + l8, rr);
+            else if (outer) g_st(rn, ob + l8, rr);
+          }
           const Raw qn = raw_ld(m + LD, CL ? jc(m + LD) : m + LD);
           const Edge en2 = CL ? edge_ld(m + ED) : edge_un(m + ED);
           const Far fn = far_ld(CL ? jc(m + ED) : m + ED);
@@ -365,7 +370,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
             double dn, up;
             nbr(par, 0, fv[0].p, dn, up);
             const double t = stencil_v(Vt, qv[0].p, ev[0].p, o_pold, qv[1].p, dn, up);
-            rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
+            rk1 = fma(na, t, (T3 || m + 1 < n_run) ? fma(nbp, qv[0].r, qv[0].p) : qv[0].r);
             pk1 = fma(b, qv[0].p, rk1);
           } else if (CL && next == 2) {
             rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, qv[0]));
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           if (edge_lane) {
             const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);
             g_st(ean, sb, sum);
-            g_st(ren, sb, rr);
+            if constexpr (!T3) g_st(ren, sb, rr);
           }
           s_pap = fma(o_pk, sum, s_pap);
           s_rap = fma(o_rk, sum, s_rap);
@@ -396,7 +401,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           o_pold = qv[0].p;
           o_pm2 = qv[0].r;
           o_epk = epk(ev[0]);
-          o_fpk = pk_of(fv[0].r, fv[0].a, fv[0].p);
+          o_fpk = pk_of(rv(fv[0].r, fv[0].p), fv[0].a, fv[0].p);
           Vs = Vt;
           cq = cn;
 #pragma unroll
@@ -909,14 +914,16 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
   const bool pair = (k & 1) != 0;
   const int qd = depth >= 3 ? 3 : 2;
   const int g = gfull ? 1 : 0;
+  MCG_CHECK(v.p_m2 == nullptr || (lean && p3 && v.ext_len < ((int64_t)1 << 29)), "3-D three p buffers: lean kernels below 2^29 rows");
   if (vc) {
-#define MCG_A3V(PAIR, KW, P3, LEAN)                                                                            \
-  hipLaunchKernelGGL((k_cg_carry_ar3<2, PAIR, KW, P3, LEAN, false, true>), dim3(grid), dim3(64 * KW), 0, stream, \
-                     S, v, own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
-#define MCG_A3VK(PAIR, P3, LEAN) MCG_A3V(PAIR, 8, P3, LEAN)
+#define MCG_A3V(PAIR, KW, P3, LEAN, ...)                                                                       \
+  hipLaunchKernelGGL((k_cg_carry_ar3<2, PAIR, KW, P3, LEAN, false, true, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, \
+                     stream, S, v, own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
+#define MCG_A3VK(PAIR, P3, LEAN, ...) MCG_A3V(PAIR, 8, P3, LEAN, ##__VA_ARGS__)
 #define MCG_A3VP(PAIR)                                          \
   do {                                                          \
-    if (p3 && !first && lean) MCG_A3VK(PAIR, true, true);       \
+    if (p3 && !first && lean && v.p_m2) MCG_A3VK(PAIR, true, true, true); \
+    else if (p3 && !first && lean) MCG_A3VK(PAIR, true, true);  \
     else if (p3 && !first) MCG_A3VK(PAIR, true, false);         \
     else MCG_A3VK(PAIR, false, false);                          \
   } while (0)

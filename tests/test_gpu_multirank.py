@@ -273,8 +273,9 @@ def test_local_ranks_p3buf_bitwise(mcg, world):
     pulled or exchanged): bit for bit the two-buffer lean pass, 2-D and 3-D, with the in-kernel halo
     and with the halo exchanged, over 40 iterations."""
     C = mcg.native()
-    for prob, n, hp in (("poisson2d", 4096, 1), ("poisson2d", 4096, 0), ("poisson3d", 128, 1), ("poisson3d", 128, 0)):
-        spec = mcg.make_problem(prob, n=n, rhs="random")
+    for prob, n, hp, coef in (("poisson2d", 4096, 1, 0), ("poisson2d", 4096, 0, 0), ("poisson3d", 128, 1, 0),
+                              ("poisson3d", 128, 0, 0), ("poisson3d", 128, 1, 1)):
+        spec = mcg.make_problem(prob, n=n, rhs="random", coef=coef)
         outs = {}
         for pb in (1, 0):
             o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8, overlap=False)

@@ -516,13 +516,14 @@ def test_p3buf_bitwise_equal_to_two_buffer_lean(mcg, n, graph):
     assert ta == tb
 
 
-@pytest.mark.parametrize("n", [128, 256])
+@pytest.mark.parametrize("n,coef", [(128, 0), (256, 0), (128, 1)])
 @pytest.mark.parametrize("graph", [True, False])
-def test_p3buf_3d_bitwise_equal_to_two_buffer_lean(mcg, n, graph):
-    """3-D three p buffers (cg_carry_ar3.hip T3): r recovered from p_{k-1} / p_{k-2} on every plane,
-    the blocks' outer lines and the slices' edge rows, none stored -- the same operands in the same
-    fma order as the stored r, so bit for bit the two-buffer lean plane carry; 41 iterations."""
-    spec = mcg.make_problem("poisson3d", n=n, rhs="random")
+def test_p3buf_3d_bitwise_equal_to_two_buffer_lean(mcg, n, coef, graph):
+    """3-D three p buffers (cg_carry_ar3.hip T3, dia4 and the variable-coefficient diav kernels): r
+    recovered from p_{k-1} / p_{k-2} on every plane, the blocks' outer lines and the slices' edge rows,
+    none stored -- the same operands in the same fma order as the stored r, so bit for bit the
+    two-buffer lean plane carry; 41 iterations."""
+    spec = mcg.make_problem("poisson3d", n=n, rhs="random", coef=coef)
     outs = {}
     for pb in (1, 0):
         s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=41, p3buf=pb, use_graph=graph)
