@@ -53,12 +53,13 @@ namespace {
 // lane 0's and lanes 63 / 48 / 56 lane 63's, and move to lanes 0 / 63 by row_mirror /
 // row_half_mirror DPP (one move serves both ends).  A line in flight then holds 2 instead of 6
 // VGPRs of edges, which buys a wave per SIMD (LEAN 5) or a line of prefetch depth
-// T3 (lean dia4 kernels, F1Vectors::p_m2): three p buffers -- p_k goes to a buffer this pass does not
+// T3 (lean dia4 / diav kernels, F1Vectors::p_m2): three p buffers -- p_k goes to a buffer this pass does not
 // read, so p_{k-2} stays intact all pass.  r is recovered from p_{k-1}, p_{k-2} on every line (no
 // stored r at run ends), and the neighbouring slices' edge rows are recomputed from their p_{k-1},
 // p_{k-2} (the owner's stencil in the owner's fma order: the same bits it stored) instead of read from
 // compact edge arrays: no edge-array loads or stores at all (bench/carry_depth.hip: the pattern with
-// the edge stores 77 us at 4096^2, with neighbour-row loads instead 58; profiles/r5/depth)
+// the edge stores 77 us at 4096^2, with neighbour-row loads instead 58; profiles/r5/depth).  The diav
+// loop (CM 5) recovers r the same way but still stores and reads its edge rows' Ap (per-row values)
 template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false,
           bool T3 = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
@@ -563,6 +564,10 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       double* __restrict__ apn_ = apx_n + rb;
       PullBases pl;  // in-kernel halo (the dia4 lean loop's)
       pl.at(v, rb);
+      // T3 (three p buffers, not BIG): p_{k-2} read-only in its own buffer, r_{k-1} recovered from p_{k-1} /
+      // p_{k-2} on every line and edge row (no r stored); the edge rows' Ap still stored (compact arrays)
+      const double* __restrict__ pm2_ = T3 ? v.p_m2 + rb : (const double*)pn_;
+      auto rv = [&](double r, double p) { return T3 ? fma(nbp, r, p) : r; };
       const int64_t kr = BIG ? (int64_t)i0 - 2 * (int64_t)LO : 0;  // lines -2 .. of the run: offsets >= 0
       const double* __restrict__ cvd_ = S.cvd + kr;
       const double* __restrict__ cve_ = S.cve + kr;
@@ -584,7 +589,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         Raw q;
         const int32_t jj = jc(j);
         const uint32_t o = line_ofs(jj) + l8;
-        q.r = g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
+        q.r = T3 ? g_ld(pm2_, o) : g_ld((j >= 0 && j < n_run) ? (const double*)pn_ : ro_, o);
         q.p = pl.ld_p(pl.side(l0 + jj, nl), po_, o);
         return q;
       };
@@ -592,7 +597,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       auto edge_at = [&](int32_t j) {
         Edge q;
         const uint32_t c = cb0 + (uint32_t)rc_(j) * SB + oc;
-        q.r = g_ld(reo, c);
+        q.r = T3 ? g_ld(pm2_, line_ofs(jc(j)) - 8u + op) : g_ld(reo, c);
         q.a = g_ld(eo, c);
         q.p = g_ld(po_, line_ofs(jc(j)) - 8u + op);
         return q;
@@ -608,19 +613,19 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         c.ee = g_ld(cve_, o >= 8u ? o - 8u : o);
         return c;
       };
-      auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(pn_, line_ofs(j) + l8), q.p); };
+      auto rghost = [&](int32_t j, const Raw& q) { return fma(nbp, g_ld(T3 ? pm2_ : (const double*)pn_, line_ofs(j) + l8), q.p); };
       auto is_ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jlo && j <= jhi; };
       auto raw_un = [&](int32_t j) {
         Raw q;
         const uint32_t o = line_ofs(j) + l8;
-        q.r = g_ld(j < n_run ? (const double*)pn_ : ro_, o);
+        q.r = T3 ? g_ld(pm2_, o) : g_ld(j < n_run ? (const double*)pn_ : ro_, o);
         q.p = g_ld(po_, o);
         return q;
       };
       auto edge_un = [&](int32_t j) {
         Edge q;
         const uint32_t c = cb0 + (uint32_t)j * SB + oc;
-        q.r = g_ld(reo, c);
+        q.r = T3 ? g_ld(pm2_, line_ofs(j) - 8u + op) : g_ld(reo, c);
         q.a = g_ld(eo, c);
         q.p = g_ld(po_, line_ofs(j) - 8u + op);
         return q;
@@ -647,7 +652,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         sum = fma(V.v[3], upv, sum);
         return fma(V.v[4], upl, sum);
       };
-      auto epk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };
+      auto epk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, rv(q.r, q.p))); };
       const Raw rm2 = raw_at(-2), rm1 = raw_at(-1), r0 = raw_at(0);
       Raw q[LD - 1];
 #pragma unroll
@@ -665,7 +670,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       for (int d = 0; d < LD - 1; ++d) cq[d] = coef_ld(coef_ofs(kc(1 + d)));
       double pr_pk = 0.0;
       if (l0 >= 1) {
-        pr_pk = fma(b, rm1.p, fma(na, stencil_v(mkv(cm1, cm2.s), rm1.p, edm1.p, rm2.p, r0.p), rm1.r));
+        pr_pk = fma(b, rm1.p, fma(na, stencil_v(mkv(cm1, cm2.s), rm1.p, edm1.p, rm2.p, r0.p), rv(rm1.r, rm1.p)));
       } else if (is_ghost(-1)) {
         pr_pk = fma(b, rm1.p, fma(na, ap_gh(-1), rghost(-1, rm1)));
         if (pl.p[0] != nullptr) g_st(const_cast<double*>(po_), line_ofs(-1) + l8, rm1.p);
@@ -685,7 +690,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         double rk1 = 0.0, pk1 = 0.0;
         if (next == 1) {
           const double t = stencil_v(Vt, q[0].p, e[0].p, o_pold, q[1].p);
-          rk1 = fma(na, t, m + 1 < n_run ? fma(nbp, q[0].r, q[0].p) : q[0].r);
+          rk1 = fma(na, t, (T3 || m + 1 < n_run) ? fma(nbp, q[0].r, q[0].p) : q[0].r);
           pk1 = fma(b, q[0].p, rk1);
         } else if (CL && next == 2) {
           rk1 = fma(na, ap_gh(m + 1), rghost(m + 1, q[0]));
@@ -695,10 +700,12 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         const double sum = stencil_v(Vs, o_pk, o_epk, pr_pk, pk1);
         const uint32_t ob = line_ofs(m);
         const double rr = fma(-b, o_pold, o_pk);
-        if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
+        if constexpr (!T3) {
+          if (m == 0 || m == n_run - 1) g_st_nt(rn_, ob + l8, rr);
+        }
         if (edge_lane) {
           const uint32_t sb = cb0 + (uint32_t)m * SB + (hi ? 16u : 8u);
-          g_st(ren, sb, rr);
+          if constexpr (!T3) g_st(ren, sb, rr);
           g_st(en, sb, sum);
         }
         if constexpr (PAIR) g_st_nt(x_, xb0 + (uint32_t)m * LOB + l8, fma(a, o_pold, fma(ap, o_pm2, xs[0])));
@@ -1036,13 +1043,17 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   if (cm == 5 && p3k && lean) {  // diav lean-only kernels: the streamed coefficients need more VGPRs
 #define MCG_LV(QD, PAIR)                                                                                        \
   do {                                                                                                          \
-    if (big)                                                                                                    \
+    if (v.p_m2 != nullptr)                                                                                      \
+      hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV, false, false, true>), dim3(grid), dim3(kBS), 0, \
+                         stream, S, v, own_off, tr, partials, pstride, st, tol, first, check, rc);              \
+    else if (big)                                                                                               \
       hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV, true>), dim3(grid), dim3(kBS), 0, stream, S, \
                          v, own_off, tr, partials, pstride, st, tol, first, check, rc);                         \
     else                                                                                                        \
       hipLaunchKernelGGL((k_cg_carry_ar<5, 5, QD, PAIR, true, 1, kLeanV>), dim3(grid), dim3(kBS), 0, stream, S, v, \
                          own_off, tr, partials, pstride, st, tol, first, check, rc);                            \
   } while (0)
+    MCG_CHECK(v.p_m2 == nullptr || !big, "diav carry, three p buffers: ranks below 2^29 rows");
     if (depth >= 3) { if (pair) MCG_LV(3, true); else MCG_LV(3, false); }
     else { if (pair) MCG_LV(2, true); else MCG_LV(2, false); }
 #undef MCG_LV

@@ -884,6 +884,7 @@ void GpuCgSolver::setup() {
     if (ar3_) p3buf_ = L_.ext_len < ((int64_t)1 << 29) && (diav3_ || (info_.dia4 && dpat_.get() != nullptr));
     else if (info_.dia4 && !diav_ && dpat_.get() != nullptr)
       p3buf_ = kern::dia_lines_uniform(dpat_.get(), tr_all_.strip, (n + 63) / 64 / tr_all_.strip, s0_);
+    else if (diav_) p3buf_ = L_.ext_len < ((int64_t)1 << 29);  // 2-D diav: r recovered, edge rows' Ap stored
   }
   if (use_comm_ && world_ > 1) p3buf_ = all_ranks_agree_(p3buf_);
   MCG_CHECK(opt_.form.p3buf != 1 || p3buf_,

@@ -274,7 +274,7 @@ def test_local_ranks_p3buf_bitwise(mcg, world):
     and with the halo exchanged, over 40 iterations."""
     C = mcg.native()
     for prob, n, hp, coef in (("poisson2d", 4096, 1, 0), ("poisson2d", 4096, 0, 0), ("poisson3d", 128, 1, 0),
-                              ("poisson3d", 128, 0, 0), ("poisson3d", 128, 1, 1)):
+                              ("poisson3d", 128, 0, 0), ("poisson3d", 128, 1, 1), ("poisson2d", 2048, 1, 1)):
         spec = mcg.make_problem(prob, n=n, rhs="random", coef=coef)
         outs = {}
         for pb in (1, 0):

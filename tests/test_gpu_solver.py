@@ -496,15 +496,16 @@ def test_lean_mix_auto_on_small_grids(mcg):
     assert a.info["grid_odd"] * 5 == a.info["grid_a"] * 4
 
 
-@pytest.mark.parametrize("n", [1024, 4096])
+@pytest.mark.parametrize("n,coef", [(1024, 0), (4096, 0), (1024, 1)])
 @pytest.mark.parametrize("graph", [True, False])
-def test_p3buf_bitwise_equal_to_two_buffer_lean(mcg, n, graph):
+def test_p3buf_bitwise_equal_to_two_buffer_lean(mcg, n, coef, graph):
     """Three p buffers (PassForm::p3buf, cg_carry_ar.hip T3): p_k goes to a buffer the pass does not
     read, r is recovered from p_{k-1} / p_{k-2} on every line and the neighbouring slices' edge rows
     are recomputed instead of read from compact edge arrays -- the same sums in the same order, so bit
     for bit the two-buffer lean pass.  41 iterations (an odd count: the final pass's x catch-up), in
-    graphs (captures keyed by k mod 3) and eagerly; 4096^2 takes the packed-edge kernels."""
-    spec = mcg.make_problem("poisson2d", n=n, rhs="random")
+    graphs (captures keyed by k mod 3) and eagerly; 4096^2 takes the packed-edge kernels; coef = 1:
+    the diav loop (r recovered, the edge rows' Ap still in compact arrays)."""
+    spec = mcg.make_problem("poisson2d", n=n, rhs="random", coef=coef)
     outs = {}
     for pb in (1, 0):
         s = mcg.CGSolver(spec, format="sellc8", recurrence=1, tol=-1.0, maxit=41, p3buf=pb, use_graph=graph)
