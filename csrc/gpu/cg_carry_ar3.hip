@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
                                                                           int check, RedCtl rc) {
   static_assert(KW >= 2 && QD >= 2, "3-D carry: >= 2 waves per block, operands >= 2 planes ahead");
   static_assert(!(VC && BIG), "3-D diav: 32-bit byte offsets (ranks below 2^29 rows)");
-  static_assert(!T3 || (P3 && LEAN && !BIG), "3-D three p buffers: the lean kernels below 2^29 rows");
+  static_assert(!T3 || (P3 && LEAN), "3-D three p buffers: the lean kernels");
   constexpr int U = 7;
   using Co = ArCodes<VC ? 6 : 4, U>;
   __shared__ double s_val[16];
@@ -463,13 +463,14 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           int32_t mb = 0;
           const double *po_ = po, *ro_ = ro, *apo_ = apo;
           double *pn_ = pn, *rn_ = rn, *x_ = x, *apw_ = apw;
-          // T3 (three p buffers, not BIG): p_{k-2} read-only in its own buffer, so r_{k-1} is recovered from
+          // T3 (three p buffers): p_{k-2} read-only in its own buffer, so r_{k-1} is recovered from
           // p_{k-1} / p_{k-2} on every plane, outer line and edge row -- no r stored anywhere
-          const double* __restrict__ pm2_ = T3 ? v.p_m2 : (const double*)pn;
+          const double* pm2_ = T3 ? v.p_m2 : (const double*)pn;
           auto rebase = [&](int32_t m) {
             if constexpr (BIG) {
               mb = m;
               const int64_t eb = (int64_t)e0 + (int64_t)(m - 3) * LO, xb = (int64_t)i0 + (int64_t)m * LO;
+              if constexpr (T3) pm2_ = v.p_m2 + eb;
               po_ = po + eb;
               ro_ = ro + eb;
               apo_ = apo + eb;
@@ -914,7 +915,7 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
   const bool pair = (k & 1) != 0;
   const int qd = depth >= 3 ? 3 : 2;
   const int g = gfull ? 1 : 0;
-  MCG_CHECK(v.p_m2 == nullptr || (lean && p3 && v.ext_len < ((int64_t)1 << 29)), "3-D three p buffers: lean kernels below 2^29 rows");
+  MCG_CHECK(v.p_m2 == nullptr || (lean && p3), "3-D three p buffers: lean kernels");
   if (vc) {
 #define MCG_A3V(PAIR, KW, P3, LEAN, ...)                                                                       \
   hipLaunchKernelGGL((k_cg_carry_ar3<2, PAIR, KW, P3, LEAN, false, true, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, \
@@ -937,13 +938,14 @@ void cg_carry_ar3(int depth, int kw, const SellDev& S, const F1Vectors& v, int64
   }
   const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: per-run bases
   const bool t3 = v.p_m2 != nullptr;                  // three p buffers (kernel comment)
-  MCG_CHECK(!t3 || (!big && lean && S.dpat != nullptr), "3-D three p buffers: lean dia4 kernels below 2^29 rows");
+  MCG_CHECK(!t3 || (lean && S.dpat != nullptr), "3-D three p buffers: lean dia4 kernels");
 #define MCG_A3(QD, PAIR, KW, P3, ...)                                                                         \
   hipLaunchKernelGGL((k_cg_carry_ar3<QD, PAIR, KW, P3, ##__VA_ARGS__>), dim3(grid), dim3(64 * KW), 0, stream, S, v, \
                      own_off, tr, ln, g, partials, pstride, st, tol, first, check, rc)
 #define MCG_A3P(QD, PAIR, KW)                                         \
   do {                                                                \
-    if (p3 && !first && lean && S.dpat != nullptr && big) MCG_A3(QD, PAIR, KW, true, true, true); \
+    if (p3 && !first && lean && S.dpat != nullptr && big && t3) MCG_A3(QD, PAIR, KW, true, true, true, false, true); \
+    else if (p3 && !first && lean && S.dpat != nullptr && big) MCG_A3(QD, PAIR, KW, true, true, true); \
     else if (p3 && !first && lean && S.dpat != nullptr && t3) MCG_A3(QD, PAIR, KW, true, true, false, false, true); \
     else if (p3 && !first && lean && S.dpat != nullptr) MCG_A3(QD, PAIR, KW, true, true); \
     else if (p3 && !first) MCG_A3(QD, PAIR, KW, true);                \

@@ -875,13 +875,13 @@ void GpuCgSolver::setup() {
   info_.lean_mix = auto_mix_ && lean_only_ && g_odd_ > 0 && opt_.hooks.lean_packed != 0;
   // three p buffers (PassForm::p3buf, T3 in cg_carry_ar.hip / cg_carry_ar3.hip): the lean three-term dia4
   // carries.  2-D: when every line's slices share one value pattern (a slice recomputes its
-  // neighbours' edge rows with its own values).  3-D (dia4 and diav): below 2^29 rows (no per-run
-  // bases); r recovered everywhere, the outer lines' and edge rows' Ap still stored.  Every rank the same (the in-kernel
+  // neighbours' edge rows with its own values); 2-D diav: r recovered, the edge rows' Ap stored.  3-D
+  // (dia4 and diav): r recovered everywhere, the outer lines' and edge rows' Ap still stored.  Every rank the same (the in-kernel
   // halo maps the same buffer list on every rank)
   p3buf_ = false;
   if (opt_.form.p3buf != 0 && ar_ && p3_ && lean_only_ && !lean_split_ && opt_.recurrence == 1 && n > 0 &&
       tr_all_.strip > 0) {
-    if (ar3_) p3buf_ = L_.ext_len < ((int64_t)1 << 29) && (diav3_ || (info_.dia4 && dpat_.get() != nullptr));
+    if (ar3_) p3buf_ = diav3_ || (info_.dia4 && dpat_.get() != nullptr);  // (diav: below 2^29 rows anyway)
     else if (info_.dia4 && !diav_ && dpat_.get() != nullptr)
       p3buf_ = kern::dia_lines_uniform(dpat_.get(), tr_all_.strip, (n + 63) / 64 / tr_all_.strip, s0_);
     else if (diav_) p3buf_ = L_.ext_len < ((int64_t)1 << 29);  // 2-D diav: r recovered, edge rows' Ap stored
