@@ -55,6 +55,8 @@ def pass_label(info, problem):
             kind += ", Ap recomputed"
         if info.get("lean_only"):
             kind += ", lean runs (values in scalar registers, no codes streamed)"
+        if info.get("p3buf"):
+            kind += ", three p buffers (no r stored)"
         if info.get("lean_mix"):
             kind += ", packed slice edges (even passes 5 waves/SIMD, odd passes depth 4 on their own grid)"
         return kind
