@@ -292,6 +292,11 @@ def recipes(a) -> dict:
                    + [(f"priced512_{w}", 200, f"{PY} bench/pipe_latency.py --problem poisson3d --grid 512 --world {w} "
                                               f"--rank {3 if w > 2 else 1} --recurrences 1 --graphs 1 --overlaps 1,0 "
                                               f"--delays 0,10,20 --halo-us 10 --iters 320") for w in (2, 4, 8)],
+        # the 3-D P = 8 share on three p buffers: kernel stats and DRAM counters
+        "share3d": stats("s3d", f"--problem poisson3d --grid 512 {S8} --steps 256 --warmup 32")
+                   + counters("s3d_dram", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4")
+                   + counters("s3d_waves", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4", WAVES)
+                   + counters("p1_3d_waves", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2", WAVES),
         # the final r5 tree: kernel stats and DRAM counters of the headline, 4096^2 and 512^3 passes
         "final": stats("f_16384", "--steps 64 --warmup 8") + stats("f_4096", "--grid 4096 --steps 640 --warmup 64")
                  + stats("f_512c", "--problem poisson3d --grid 512 --steps 64 --warmup 8")
