@@ -58,7 +58,7 @@ def pass_label(info, problem):
         if info.get("p3buf"):
             kind += ", three p buffers (no r stored)"
         if info.get("lean_mix"):
-            kind += ", packed slice edges (even passes 5 waves/SIMD, odd passes depth 4 on their own grid)"
+            kind += ", packed slice edges (even passes 5-6 waves/SIMD, odd passes depth 4 on their own grid)"
         return kind
     if info.get("pmat"):
         return "split (materialized p)"
