@@ -36,6 +36,24 @@ def test_checkpoint_resume_matches_uninterrupted(mcg, tmp_path, recurrence, pipe
     np.testing.assert_array_equal(out["x_local"], full["x_local"])
 
 
+@pytest.mark.parametrize("problem,n,every", [("poisson2d", 1024, 50), ("poisson3d", 128, 50)])
+def test_checkpoint_resume_three_p_buffers(mcg, tmp_path, problem, n, every):
+    """Three p buffers (p_j in p_[j mod 3]): a checkpoint taken at an iteration that is not a multiple of
+    3 (the buffer rotation mid-cycle) resumes bitwise equal to the uninterrupted solve, 2-D and 3-D."""
+    spec = mcg.make_problem(problem, n=n, rhs="random")
+    kw = dict(format="sellc8", recurrence=1, check_every=8, maxit=400)
+    full = mcg.CGSolver(spec, **kw).solve()
+    prefix = str(tmp_path / "ck")
+    a = mcg.CGSolver(spec, checkpoint_every=every, checkpoint_path=prefix, **dict(kw, maxit=2 * every + 7))
+    assert a.info["p3buf"], a.info
+    a.solve()
+    b = mcg.CGSolver(spec, **kw)
+    b.load_checkpoint(prefix)
+    out = b.solve(resume=True)
+    assert out["iterations"] == full["iterations"] and out["rnorm"] == full["rnorm"]
+    np.testing.assert_array_equal(out["x_local"], full["x_local"])
+
+
 @pytest.mark.parametrize("p3", [0, 1])
 def test_checkpoint_resume_default_stencil_path(mcg, tmp_path, p3):
     """The default stencil path (dia4 line carry, Ap recomputed; p3 = three-term form, whose r lives
