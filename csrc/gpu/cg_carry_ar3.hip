@@ -90,7 +90,10 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
   // three-term form (P3, as in k_cg_carry_ar): r_{k-1} = p_{k-1} - b_prev p_{k-2} on the run's own
   // planes; r stored (as that recovered value) only where another wave reads it: the block's outer
   // lines, the slices' edge rows and the run's first / last plane (the halo's source at P > 1);
-  // pass 0 runs the two-term kernel (see k_cg_carry_ar)
+  // pass 0 runs the two-term kernel (see k_cg_carry_ar).  T3 (lean kernels, three p buffers:
+  // F1Vectors::p_m2): p_{k-2} is never overwritten during the pass, so every one of those readers
+  // recovers r from p_{k-1} / p_{k-2} itself and no r is stored at all (512^3: 1103 vs 1010 it/s,
+  // profiles/r5/p3buf3d)
   constexpr bool rfull = !P3;
   const double nbp = P3 ? -st->b_prev : 0.0;
   const double* __restrict__ ro = v.r_old;
