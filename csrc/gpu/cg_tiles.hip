@@ -364,27 +364,23 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
   MCG_CHECK(T.tb == kTileB && (T.tu == 8 || T.tu == 10), "tiles: 1024 rows per block, 8 or 10 entries per lane");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
-#define MCG_TL(PART, ABL)                                                                                              \
-  do {                                                                                                                 \
-    if (T.tu == 10)                                                                                                    \
-      hipLaunchKernelGGL((k_tiles<0, PART, ABL, 10>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
-                         pstride, st, tol, first, check, rc);                                                          \
-    else                                                                                                               \
-      hipLaunchKernelGGL((k_tiles<0, PART, ABL, 8>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
-                         pstride, st, tol, first, check, rc);                                                          \
-  } while (0)
+#define MCG_TL(PART, ABL, TU)                                                                                          \
+  hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
+                     pstride, st, tol, first, check, rc)
   static const int ablate = [] {
     const char* e = std::getenv("MCG_TILES_ABLATE");
     return e ? std::atoi(e) : 0;
   }();
-#define MCG_TLA(PART)                   \
-  do {                                  \
-    if (ablate == 3) MCG_TL(PART, 3);   \
-    else if (ablate == 4) MCG_TL(PART, 4); \
-    else if (ablate == 7) MCG_TL(PART, 7); \
-    else if (ablate == 15) MCG_TL(PART, 15); \
-    else if (ablate == 64) MCG_TL(PART, 64); \
-    else MCG_TL(PART, 0);               \
+  // the ablations (diagnostic, results wrong) run the 10-per-lane kernels only
+#define MCG_TLA(PART)                          \
+  do {                                         \
+    if (ablate == 3) MCG_TL(PART, 3, 10);      \
+    else if (ablate == 4) MCG_TL(PART, 4, 10); \
+    else if (ablate == 7) MCG_TL(PART, 7, 10); \
+    else if (ablate == 15) MCG_TL(PART, 15, 10); \
+    else if (ablate == 64) MCG_TL(PART, 64, 10); \
+    else if (T.tu == 10) MCG_TL(PART, 0, 10);  \
+    else MCG_TL(PART, 0, 8);                   \
   } while (0)
   if (part == 1) MCG_TLA(1);
   else if (part == 2) MCG_TLA(2);
@@ -402,24 +398,19 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
     const char* e = std::getenv("MCG_TILES_ABLATE");
     return e ? std::atoi(e) : 0;
   }();
-#define MCG_T1(ABL)                                                                                                    \
-  do {                                                                                                                 \
-    if (T.tu == 10)                                                                                                    \
-      hipLaunchKernelGGL((k_tiles<1, 0, ABL, 10>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0, \
-                         nullptr, 0.0, 0, 0, RedCtl());                                                                \
-    else                                                                                                               \
-      hipLaunchKernelGGL((k_tiles<1, 0, ABL, 8>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0,  \
-                         nullptr, 0.0, 0, 0, RedCtl());                                                                \
-  } while (0)
-  if (ablate == 1) MCG_T1(1);
-  else if (ablate == 2) MCG_T1(2);
-  else if (ablate == 3) MCG_T1(3);
-  else if (ablate == 4) MCG_T1(4);
-  else if (ablate == 7) MCG_T1(7);
-  else if (ablate == 15) MCG_T1(15);
-  else if (ablate == 16) MCG_T1(16);
-  else if (ablate == 32) MCG_T1(32);
-  else MCG_T1(0);
+#define MCG_T1(ABL, TU)                                                                                                \
+  hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0,  \
+                     nullptr, 0.0, 0, 0, RedCtl())
+  if (ablate == 1) MCG_T1(1, 10);
+  else if (ablate == 2) MCG_T1(2, 10);
+  else if (ablate == 3) MCG_T1(3, 10);
+  else if (ablate == 4) MCG_T1(4, 10);
+  else if (ablate == 7) MCG_T1(7, 10);
+  else if (ablate == 15) MCG_T1(15, 10);
+  else if (ablate == 16) MCG_T1(16, 10);
+  else if (ablate == 32) MCG_T1(32, 10);
+  else if (T.tu == 10) MCG_T1(0, 10);
+  else MCG_T1(0, 8);
 #undef MCG_T1
   if (ablate & 16) {  // diagnostic: the pacing waits' share of each workgroup's time
     std::vector<unsigned long long> d(3 * kTileDiagMax);
