@@ -297,6 +297,10 @@ def recipes(a) -> dict:
                    + counters("s3d_dram", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4")
                    + counters("s3d_waves", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4", WAVES)
                    + counters("p1_3d_waves", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2", WAVES),
+        # config 5 tiles on the final r5 tree (straggler priority, 10 per lane): L2 and DRAM counters
+        "c5final": counters("c5f_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE")
+                   + counters("c5f_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
+                   + counters("c5f_req", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_REQ_sum TCC_READ_sum GRBM_GUI_ACTIVE"),
         # the final r5 tree: kernel stats and DRAM counters of the headline, 4096^2 and 512^3 passes
         "final": stats("f_16384", "--steps 64 --warmup 8") + stats("f_4096", "--grid 4096 --steps 640 --warmup 64")
                  + stats("f_512c", "--problem poisson3d --grid 512 --steps 64 --warmup 8")
