@@ -297,6 +297,9 @@ def recipes(a) -> dict:
                    + counters("s3d_dram", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4")
                    + counters("s3d_waves", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4", WAVES)
                    + counters("p1_3d_waves", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2", WAVES),
+        # variable coefficients on three p buffers: DRAM counters (2-D and 3-D diav lean carries)
+        "vcp3": counters("vc2_dram", "k_cg_carry_ar", "--coef 1 --steps 8 --warmup 2")
+                + counters("vc3_dram", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --coef 1 --steps 8 --warmup 2"),
         # config 5 tiles on the final r5 tree (straggler priority, 10 per lane): L2 and DRAM counters
         "c5final": counters("c5f_l2", "k_tiles", f"{C5SCR} --steps 2 --warmup 1", "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE")
                    + counters("c5f_dram", "k_tiles", f"{C5SCR} --steps 2 --warmup 1")
