@@ -297,6 +297,10 @@ def recipes(a) -> dict:
                    + counters("s3d_dram", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4")
                    + counters("s3d_waves", "k_cg_carry_ar3", f"--problem poisson3d --grid 512 {S8} --steps 32 --warmup 4", WAVES)
                    + counters("p1_3d_waves", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2", WAVES),
+        # the headline's priced P-rank shares on the final r5 tree
+        "priced16k": [(f"p16k_{w}", 200, f"{PY} bench/pipe_latency.py --grid 16384 --world {w} --rank {3 if w > 2 else 1} "
+                                         f"--recurrences 1 --graphs 1 --overlaps 1,0 --delays 0,10,20 --halo-us 10 --iters 320")
+                      for w in (2, 4, 8)] + [("p16k_1", 200, bench("--phases 0"))],
         # variable coefficients on three p buffers: DRAM counters (2-D and 3-D diav lean carries)
         "vcp3": counters("vc2_dram", "k_cg_carry_ar", "--coef 1 --steps 8 --warmup 2")
                 + counters("vc3_dram", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --coef 1 --steps 8 --warmup 2"),
