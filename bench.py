@@ -5,9 +5,12 @@ Metric and config come from BASELINE.json: one linear system (n = 268,435,456
 rows, nnz = 1,342,111,744) solved jointly by N GPUs of one node (strong
 scaling: total work fixed), matrix 1-D row-partitioned, generated on device
 (synthetic — no dataset exists for this), random RHS.  A "step" is one full CG
-iteration: fused SpMV + pAp all-reduce + residual update + r.r all-reduce, halo
-exchange when N > 1.  tol is disabled so every timed step does real work; the
-device-side iteration counter is checked after the run.
+iteration: one single-reduction pass (SpMV with Ap recomputed, the x / r / p updates
+and the four dot products, reduced inside the kernel) + ONE 32-byte all-reduce of
+those dot products, and at N > 1 the ghost lines (read by the pass from the
+neighbours' rows, or exchanged before it: the transport probe picks at setup).
+tol is disabled so every timed step does real work; the device-side iteration
+counter is checked after the run.
 
   python bench.py                      # N=1
   python bench.py --gpus 8             # starts 8 ranks itself (one process per GPU, RCCL)
@@ -67,6 +70,27 @@ def pass_label(info, problem):
     return "generic"
 
 
+def probe_report(info, probed_ar):
+    """The solver's setup-time transport probe (GpuCgSolver::probe_transport_): mean microseconds per
+    iteration over the ranks of each arm it ran, what it checked, and the transports it kept."""
+    r = {"iters_timed": info.get("probe_iters", 0)}
+    if info.get("probe_pull_us"):
+        r["pull_us"] = round(info["probe_pull_us"], 2)
+    if info.get("probe_xchg_us"):
+        r["rccl_halo_us"] = round(info["probe_xchg_us"], 2)
+    if info.get("probe_pull_us") and info.get("probe_xchg_us"):
+        r["pull_bitwise"] = bool(info.get("probe_pull_bitwise"))
+    if probed_ar:
+        # the first all-reduce's time = the chosen halo's arm (it ran with RCCL's all-reduce)
+        r["rccl_ar_us"] = round(info["probe_pull_us"] if info.get("halo_pull") else info["probe_xchg_us"], 2)
+        r["ipc_ar_us"] = round(info.get("probe_alt_us", 0.0), 2)
+        r["ipc_ar_close"] = bool(info.get("probe_alt_close"))
+        if info.get("probe_alt_timeout"):
+            r["ipc_ar_timeout"] = True
+    r["chosen"] = ("pull" if info.get("halo_pull") else "exchange") + "+" + ("ipc" if info.get("alt_allreduce") else "rccl")
+    return r
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -112,10 +136,12 @@ def parse_args(argv=None):
                          "carries' in-kernel halo (halo_pull: checked at setup, off again if any rank cannot map or "
                          "reads a wrong row), every remaining halo exchange and the all-reduce on RCCL; rccl: no "
                          "mapping; sdma: the halo exchanges on copy engines (flags by stream memory operations)")
-    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "ipc"],
-                    help="ipc: the 32-byte all-reduce through IPC-mapped mailboxes (PeerHaloComm + "
-                         "csrc/gpu/ipc_allreduce.hip, no RCCL; implies the peer-mapped halo).  With --rehearse-ranks "
-                         "the P processes on one GPU then run the real P-rank recurrence")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="auto (N > 1 on N GPUs): every rank's IPC all-reduce mailbox mapped next to RCCL, and the "
+                         "solver's transport probe times both at setup and keeps the faster correct one (check."
+                         "transport_probe); rccl: RCCL only; ipc: the 32-byte all-reduce through IPC-mapped mailboxes "
+                         "(PeerHaloComm + csrc/gpu/ipc_allreduce.hip, no RCCL; implies the peer-mapped halo).  With "
+                         "--rehearse-ranks the P processes on one GPU then run the real P-rank recurrence")
     ap.add_argument("--delay-comm", default="",
                     help="with --sim-world: AR_US,HALO_US[,copy|fat] -- every all-reduce / halo (or all-gather) exchange "
                          "of the rehearsed rank costs a device-side delay of that many microseconds (DelayComm) "
@@ -222,9 +248,14 @@ def _run_rank(args, out_fd) -> int:
     # auto: the mapping for the in-kernel halo, the exchanges on the inner communicator (a rehearsal's
     # inner moves nothing: there only the real P-rank form, ipc_ar, takes the copy-engine exchanges)
     mapped = (sdma or args.halo_transport == "auto") and comm is not None and not sim and env.world > 1
+    # --allreduce auto: the IPC mailboxes mapped but not selected, so the solver's transport probe (first
+    # reset) times them against RCCL's all-reduce and keeps the faster one that reproduces RCCL's sums
+    probe_ar = args.allreduce == "auto" and mapped and not rehearse
     base_comm = comm  # RCCL's (or the rehearsal's) communicator: the count, the all-reduce
     if mapped:
-        comm = pdist.peer_halo(comm, env, ipc_allreduce=ipc_ar, halo_via_inner=not sdma)
+        comm = pdist.peer_halo(comm, env, ipc_allreduce=ipc_ar or probe_ar, halo_via_inner=not sdma, tolerant=probe_ar)
+        if probe_ar:
+            comm.ipc_allreduce = False
     real = not sim and (not rehearse or ipc_ar)  # a real P-rank solve (its residual must track)
     solver = (C.Solver(spec.native(), opts, args.sim_rank, args.sim_world, comm) if sim
               else C.Solver(spec.native(), opts, env.rank, env.world, comm))
@@ -356,7 +387,8 @@ def _run_rank(args, out_fd) -> int:
                 "comm": args.comm,
                 **({"halo_transport": ("in-kernel (the pass reads the IPC-mapped neighbour rows)" if info.get("halo_pull")
                                        else "sdma (copy engines, IPC)" if sdma else "rccl (mapping unused)"),
-                    "allreduce": "ipc (mapped mailboxes)" if ipc_ar else "rccl"} if mapped else {}),
+                    "allreduce": "ipc (mapped mailboxes)" if (ipc_ar or info.get("alt_allreduce")) else "rccl"}
+                   if mapped else {}),
                 "launch": route,
                 **({"reserve_cus": opts.reserve_cus} if opts.reserve_cus else {}),
             },
@@ -372,6 +404,7 @@ def _run_rank(args, out_fd) -> int:
                       "placement_lead_trial": info.get("placement_lead_trial"),
                       "dia_uniform": round(info.get("dia_uniform", 0.0), 4), "lean_only": info.get("lean_only", False),
                       "halo_pull": info.get("halo_pull", False),
+                      **({"transport_probe": probe_report(info, probe_ar)} if info.get("probe_ran") else {}),
                       **({"ag_local_frac": round(info["ag_local_frac"], 4)} if info.get("ag_overlap") else {}),
                       "model_gb_per_iter_rank0": round(info["bytes_per_iter_model"] / 1e9, 3),
                       "model_tb_per_s_rank0": round(info["bytes_per_iter_model"] * value / 1e12, 3),

@@ -25,6 +25,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def _opts(C, a):
     o = C.CgOptions(tol=-1.0, maxit=1 << 30, check_every=1 << 30, format="sellc8", recurrence=a.recurrence)
     o.halo_pull = a.halo_pull
+    # the transport probe (first reset) runs the pulled and the exchanged arm; which it keeps is pinned
+    # here (by default the pull, as before the probe) so the test knows the path
+    o.probe_pick_halo = a.probe_pick
     o.pipe_rr = a.pipe_rr
     o.use_graph = not a.no_graph
     o.watchdog_seconds = 60.0
@@ -76,7 +79,8 @@ def rank_main(rank: int, a, port: int, q) -> None:
     info = s.info
     q.put((rank, float(res["rnorm"]), int(res["iterations"]), x.tobytes(), float(tr),
            bool(info.get("halo_pull")), bool(info.get("lean_only")), int(info.get("graph_fallbacks", 0)),
-           bool(info.get("graphs"))))
+           bool(info.get("graphs")), {k: info.get(k) for k in ("probe_ran", "probe_pull_us", "probe_xchg_us",
+                                                                 "probe_pull_bitwise", "probe_iters")}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -92,6 +96,8 @@ def main() -> int:
     ap.add_argument("--coef", type=int, default=0)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--halo-pull", type=int, default=-1)
+    ap.add_argument("--probe-pick", type=int, default=1, help="transport probe: keep the pull (1) / exchange (0) / "
+                                                              "the faster (-1)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--tol", type=float, default=1e-13, help="relative gap allowed against one rank")
     ap.add_argument("--port", type=int, default=29541)
@@ -141,7 +147,7 @@ def main() -> int:
         out.update(rnorm_1=r1, rnorm_p=res[0][1], gap_rnorm=gap_r, gap_x=gap_x,
                    true_gap=max(abs(r[4] - r[1]) / r[4] for r in res),
                    ranks=[{"rank": r[0], "iterations": r[2], "halo_pull": r[5], "lean_only": r[6],
-                           "graph_fallbacks": r[7], "graphs": r[8]} for r in res])
+                           "graph_fallbacks": r[7], "graphs": r[8], **r[9]} for r in res])
         ok = (gap_r <= a.tol and gap_x <= 10 * a.tol and all(r[2] == a.iters for r in res)
               and len({r[1] for r in res}) == 1)
     out["ok"] = ok

@@ -18,10 +18,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def us_per_iter(C, spec, recurrence, delay, fat, graph, overlap, world, rank, iters, fmt, pipe_rr=0, halo_us=0.0,
-                reserve_cus=0, halo_ahead=-1):
+                reserve_cus=0, halo_ahead=-1, halo_pull=-1, pull_proxy=0):
     o = C.CgOptions(maxit=1 << 30, tol=-1.0, check_every=1 << 30, overlap=overlap, use_graph=graph, format=fmt,
                     recurrence=recurrence)
     o.pipe_rr = pipe_rr
+    o.halo_pull = halo_pull  # 1: the in-kernel halo on this rehearsal (no halo step; own lines or host memory)
+    o.pull_proxy = pull_proxy
     o.reserve_cus = reserve_cus
     o.halo_ahead = halo_ahead
     comm = C.DelayComm(rank, world, delay, halo_us, fat)
@@ -60,6 +62,12 @@ def main():
     ap.add_argument("--halo-us", type=float, default=0.0, help="device-side delay of each halo exchange")
     ap.add_argument("--reserve-cus", default="0", help="CgOptions.reserve_cus values (CU-masked compute stream)")
     ap.add_argument("--halo-ahead", default="-1", help="PassForm.halo_ahead values (0: interior || halo split)")
+    ap.add_argument("--halo-pull", type=int, default=-1,
+                    help="PassForm.halo_pull: 1 = the in-kernel halo (the pass reads the ghost lines itself, no halo "
+                         "step; the rehearsal's stand-in rows), 0 = exchanged, -1 = auto (a DelayComm maps no peers: "
+                         "exchanged)")
+    ap.add_argument("--pull-proxy", type=int, default=0, help="with --halo-pull 1: 1 = the ghost lines in pinned host "
+                                                              "memory (PCIe: a slow remote)")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime initialised as in the other tools)
 
@@ -73,13 +81,14 @@ def main():
                                                         ints(a.fat), [float(v) for v in a.delays.split(",")],
                                                         ints(a.reserve_cus), ints(a.halo_ahead)):
         us, info = us_per_iter(C, spec, rec, d, bool(fat), bool(g), bool(ov), a.world, a.rank, a.iters, a.format,
-                               a.pipe_rr if rec == 2 else 0, a.halo_us, rc, ha)
+                               a.pipe_rr if rec == 2 else 0, a.halo_us, rc, ha, a.halo_pull, a.pull_proxy)
         print(json.dumps({"recurrence": info["recurrence"], "graph": g, "overlap": ov, "fat": fat, "delay_us": d,
                           "us_per_iter": round(us, 2), "graph_fallbacks": info.get("graph_fallbacks"),
                           "pipe_rr": info.get("pipe_rr"), "ar_first": info.get("pipe_ar_first"),
                           "t_spmv": round(info.get("pipe_spmv_us", 0), 1), "t_ar": round(info.get("pipe_allreduce_us", 0), 1), "format": info["format"], "carry": info.get("carry"), "pmat": info.get("pmat"),
                           "problem": a.problem, "world": a.world, "rank": a.rank, "halo_us": a.halo_us,
                           "reserve_cus": rc, "halo_ahead": ha, "halo_ahead_on": info.get("halo_ahead"),
+                          "halo_pull": info.get("halo_pull"), "pull_proxy": a.pull_proxy,
                           "grid": a.grid}),
               flush=True)
 

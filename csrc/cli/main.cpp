@@ -22,8 +22,17 @@
 //   --fused-reduce auto|on|off  --watchdog SECONDS  --reserve-cus K
 //   --checkpoint PREFIX  --checkpoint-every K  --resume PREFIX  --inject-nan-at K
 //   --print-x auto|yes|no  --report text|json  --verify
+//   --halo-transport auto|rccl  --allreduce auto|rccl|ipc  --transport-probe auto|off  --rehearse-ranks
 // Multi-GPU runs use one host thread per GPU inside this process (no MPI in
-// this image); the two RCCL unique ids are shared in memory.
+// this image); the two RCCL unique ids are shared in memory.  At P > 1 each rank's
+// communicator is wrapped in a PeerHaloComm that maps the other threads' halo
+// buffers as plain pointers (peer access enabled), so the lean carries read their
+// ghost lines from the neighbours' rows (halo_pull), and every rank's IPC
+// all-reduce mailbox is mapped next to RCCL; the solver's transport probe picks
+// the halo and the all-reduce at the first reset (--halo-transport rccl /
+// --allreduce rccl: RCCL only).  --rehearse-ranks runs the P rank threads on
+// GPU 0 with an in-process communicator (LocalComm) under the same wrapping: the
+// real P-rank recurrence on one GPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -66,6 +75,9 @@ struct Args {
   bool format_set = false, recurrence_set = false;
   std::string resume;  // checkpoint prefix to resume from
   bool comm_single = true;  // --comm single (default): one RCCL communicator, collectives in one stream order
+  std::string halo_transport = "auto";  // auto: peers mapped (in-kernel halo) | rccl
+  std::string allreduce = "auto";       // auto: IPC mailboxes mapped, the probe decides | rccl | ipc
+  bool rehearse = false;                // every rank thread on GPU 0 over LocalComm (one-GPU rehearsal)
   std::string matrix, rhs_file;  // user matrix (Matrix Market) and its right-hand side
   std::shared_ptr<HostMatrix> mat;
 };
@@ -137,6 +149,16 @@ Args parse(int argc, char** argv) {
       if (v != "single" && v != "dual") usage_error("--comm " + v);
       a.comm_single = v == "single";
     }
+    else if (f == "--halo-transport") {
+      a.halo_transport = need(i);
+      if (a.halo_transport != "auto" && a.halo_transport != "rccl") usage_error("--halo-transport " + a.halo_transport);
+    }
+    else if (f == "--allreduce") {
+      a.allreduce = need(i);
+      if (a.allreduce != "auto" && a.allreduce != "rccl" && a.allreduce != "ipc") usage_error("--allreduce " + a.allreduce);
+    }
+    else if (f == "--transport-probe") a.opt.transport_probe = tri(need(i), "--transport-probe") == 0 ? 0 : -1;
+    else if (f == "--rehearse-ranks") a.rehearse = true;
     else if (f == "--blocks-per-cu") a.opt.blocks_per_cu = std::stoi(need(i));
     else if (f == "--spmv-variant") a.opt.spmv_variant = std::stoi(need(i));
     else if (f == "--checkpoint") a.opt.checkpoint_path = need(i);
@@ -164,6 +186,7 @@ Args parse(int argc, char** argv) {
       std::exit(0);
     } else usage_error(f);
   }
+  if (a.halo_transport == "rccl") a.opt.form.halo_pull = 0;  // no mapped peers: every ghost line exchanged
   if (!a.matrix.empty()) a.spec.kind = ProblemKind::Csr;
   if (a.spec.kind == ProblemKind::Csr) {
     if (a.matrix.empty()) usage_error("--problem csr needs --matrix FILE");
@@ -246,14 +269,26 @@ struct CommRegistry {
 };
 CommRegistry g_comms;
 
+// Handle blobs of the rank threads (PeerHaloComm's local_handles / mailbox_handle), shared in memory:
+// each thread deposits its own, a barrier, then every thread maps the others' (plain pointers).
+struct Blobs {
+  std::vector<std::string> halo, mailbox;
+  explicit Blobs(int world) : halo(world), mailbox(world) {}
+};
+
 void run_rank(const Args& a, int rank, int world, const std::string& id_red, const std::string& id_halo,
-              Barrier& bar, bool want_x, RankOut& out) {
+              Barrier& bar, Blobs& blobs, const std::shared_ptr<LocalGroup>& group, bool want_x, RankOut& out) {
   try {
-    if (hipSetDevice(rank) != hipSuccess) fail("Device Set failed");  // CUDACG.cu:87-91
-    std::unique_ptr<Comm> comm;
-    if (world > 1 || a.opt.force_comm)
+    if (hipSetDevice(group ? 0 : rank) != hipSuccess) fail("Device Set failed");  // CUDACG.cu:87-91
+    std::shared_ptr<Comm> comm;
+    std::shared_ptr<Communicator> inner;
+    if (group) {
+      inner = std::make_shared<LocalComm>(group, rank);  // --rehearse-ranks: the rank threads share GPU 0
+    } else if (world > 1 || a.opt.force_comm) {
       comm.reset(a.comm_single ? new Comm(rank, world, unique_id_from_bytes(id_red))
                                : new Comm(rank, world, unique_id_from_bytes(id_red), unique_id_from_bytes(id_halo)));
+      inner = comm;
+    }
     if (comm) g_comms.add(comm.get());
     struct Unreg {
       Comm* c;
@@ -262,19 +297,63 @@ void run_rank(const Args& a, int rank, int world, const std::string& id_red, con
       }
     } unreg{comm.get()};
     struct AbortOnThrow {  // runs during unwinding, before `comm` is destroyed
-      bool armed = true;
+      const std::shared_ptr<LocalGroup>* g;
       ~AbortOnThrow() {
-        if (armed && std::uncaught_exceptions() > 0) g_comms.abort_all();
+        if (std::uncaught_exceptions() > 0) {
+          g_comms.abort_all();
+          if (*g) (*g)->abort();
+        }
       }
-    } guard;
+    } guard{&group};
+    // P > 1: the neighbours' halo buffers mapped (the in-kernel halo), every remaining exchange and, unless
+    // the probe picks the IPC mailboxes, the all-reduce on the inner communicator
+    std::shared_ptr<PeerHaloComm> peer;
+    if (inner && world > 1 && a.halo_transport == "auto") {
+      peer = std::make_shared<PeerHaloComm>(inner, rank, world);
+      peer->set_halo_via_inner(true);
+      // IPC all-reduce mailboxes: real GPUs only (rank threads sharing one GPU could queue one rank's
+      // spinning all-reduce in front of another's pass)
+      if (a.allreduce == "ipc" || (a.allreduce == "auto" && !group)) {
+        const bool tolerant = a.allreduce == "auto";  // the probe's option: a rank that cannot map stays out
+        try {
+          blobs.mailbox[rank] = peer->mailbox_handle();
+        } catch (const Error& e) {
+          if (!tolerant) throw;
+          std::fprintf(stderr, "[mcg] rank %d: IPC all-reduce mailbox unavailable (%s)\n", rank, e.what());
+        }
+        bar.wait();
+        const bool all = std::all_of(blobs.mailbox.begin(), blobs.mailbox.end(), [](const std::string& b) { return !b.empty(); });
+        try {
+          if (!all) fail("ipc all-reduce: a rank could not export its mailbox");
+          peer->attach_mailbox(blobs.mailbox);
+        } catch (const Error& e) {
+          if (!tolerant) throw;
+          std::fprintf(stderr, "[mcg] rank %d: IPC all-reduce mailboxes not mapped (%s)\n", rank, e.what());
+        }
+        if (tolerant) peer->use_alt_allreduce(false);  // the transport probe decides
+      }
+    }
+    Communicator* c = peer ? (Communicator*)peer.get() : inner.get();
     CgOptions opt = a.opt;
     if (a.fixed_iters > 0) { opt.tol = -1.0; opt.maxit = a.fixed_iters; }
-    GpuCgSolver solver(a.spec, opt, rank, world, comm.get());
+    GpuCgSolver solver(a.spec, opt, rank, world, c);
     solver.setup();
+    if (peer) {  // map the other threads' registered buffers; a rank that cannot stays unattached and the
+                 // solver's check at the first reset turns the pull off on every rank
+      blobs.halo[rank] = peer->local_handles();
+      bar.wait();
+      try {
+        peer->attach(blobs.halo);
+      } catch (const Error& e) {
+        std::fprintf(stderr, "[mcg] rank %d: peer mapping failed (%s: %s); the halo stays on the inner communicator\n",
+                     rank, e.what(), e.detail().c_str());
+      }
+    }
     out.info = solver.info();
     out.row_begin = solver.layout().row_begin;
     if (a.fixed_iters > 0) {
       solver.reset();
+      out.info = solver.info();  // (the transport probe's choices)
       solver.run_iterations(a.warmup);
       solver.synchronize();
       bar.wait();
@@ -294,6 +373,7 @@ void run_rank(const Args& a, int rank, int world, const std::string& id_red, con
     }
     if (a.verify) out.true_rnorm = solver.true_residual_norm();
     if (want_x) out.x = solver.x_local();
+    out.info = solver.info();
   } catch (const Error& e) {
     out.error = e.what();
     out.detail = e.detail();
@@ -334,18 +414,21 @@ int main(int argc, char** argv) {
     } else {
       int ndev = 0;
       if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) fail("Device Set failed", "no HIP device");
-      if (a.gpus < 1 || a.gpus > ndev) fail("Device Set failed", "requested more GPUs than present");
+      if (a.gpus < 1 || (a.gpus > ndev && !a.rehearse)) fail("Device Set failed", "requested more GPUs than present");
       std::string id_red, id_halo;
-      if (a.gpus > 1 || a.opt.force_comm) {
+      if ((a.gpus > 1 || a.opt.force_comm) && !a.rehearse) {
         id_red = unique_id_bytes();
         id_halo = unique_id_bytes();
       }
+      std::shared_ptr<LocalGroup> group;
+      if (a.rehearse && a.gpus > 1) group = std::make_shared<LocalGroup>(a.gpus);
       Barrier bar(a.gpus);
+      Blobs blobs(a.gpus);
       std::vector<RankOut> outs(a.gpus);
       std::vector<std::thread> ts;
       for (int r = 0; r < a.gpus; ++r)
         ts.emplace_back(run_rank, std::cref(a), r, a.gpus, std::cref(id_red), std::cref(id_halo), std::ref(bar),
-                        want_x, std::ref(outs[r]));
+                        std::ref(blobs), std::cref(group), want_x, std::ref(outs[r]));
       for (auto& t : ts) t.join();
       for (auto& o : outs)
         if (!o.error.empty()) fail(o.error, o.detail);
@@ -376,7 +459,22 @@ int main(int argc, char** argv) {
     std::string per_rank = "[";
     for (size_t r = 0; r < rank_bytes.size(); ++r) per_rank += (r ? ", " : "") + std::to_string(rank_bytes[r]);
     per_rank += "]";
-    std::printf("{\"problem\": \"%s\", \"n\": %lld, \"nnz_rank0\": %lld, \"ranks\": %d, \"device\": \"%s\", "
+    // the P > 1 transports in effect and, if it ran, the transport probe's arms (mean us per iteration)
+    char probe[512] = "null";
+    if (info.probe_ran)
+      std::snprintf(probe, sizeof probe,
+                    "{\"pull_us\": %.3f, \"rccl_halo_us\": %.3f, \"ipc_ar_us\": %.3f, \"pull_bitwise\": %s, "
+                    "\"ipc_ar_close\": %s, \"iters_timed\": %d, \"chosen\": \"%s+%s\"}",
+                    info.probe_pull_us, info.probe_xchg_us, info.probe_alt_us, info.probe_pull_bitwise ? "true" : "false",
+                    info.probe_alt_close ? "true" : "false", info.probe_iters, info.halo_pull ? "pull" : "exchange",
+                    info.alt_allreduce ? "ipc" : "rccl");
+    std::printf("{\"halo_pull\": %s, \"halo_transport\": \"%s\", \"allreduce\": \"%s\", \"transport_probe\": %s, "
+                "\"rehearse_ranks\": %s, ",
+                info.halo_pull ? "true" : "false",
+                world < 2 || a.cpu ? "none" : info.halo_pull ? "in-kernel" : (a.rehearse ? "local" : "rccl"),
+                world < 2 || a.cpu ? "none" : info.alt_allreduce ? "ipc" : (a.rehearse ? "local" : "rccl"), probe,
+                a.rehearse ? "true" : "false");
+    std::printf("\"problem\": \"%s\", \"n\": %lld, \"nnz_rank0\": %lld, \"ranks\": %d, \"device\": \"%s\", "
                 "\"format\": \"%s\", \"iterations\": %d, \"converged\": %s, \"breakdown\": %s, \"rnorm\": %.6e, "
                 "\"true_rnorm\": %.6e, \"setup_s\": %.6f, \"solve_s\": %.6f, \"it_per_s\": %.3f, "
                 "\"device_bytes_rank0\": %zu, \"device_bytes_per_rank\": %s, \"rccl_version\": %d, "

@@ -129,6 +129,21 @@ __device__ __forceinline__ void st_sys(double* base, uint32_t bo, double v) {
   g_u64* p = (g_u64*)((g_char*)(g_double*)base + bo);
   __hip_atomic_store(p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+#ifndef MCG_PULL_FENCE
+#define MCG_PULL_FENCE 1
+#endif
+// The in-kernel halo's memory-model argument.  Rank B's pass k stores its first / last line (p_k,
+// Ap_k) with relaxed system-scope stores (st_sys: sc0 sc1, written through past B's L2 to its HBM),
+// and the wave that stored them ends its run with a system-scope release (release(): the stores are
+// complete -- acknowledged by the memory that serves remote readers -- before anything the wave does
+// later, its end included).  B's kernel end precedes B's all-reduce of pass k in stream order; rank
+// A's pass k + 1 follows A's all-reduce of pass k, which cannot complete before B contributed
+// (RCCL: the data dependence of the sum; the IPC all-reduce: B's flag, stored after its own release).
+// So A's pass k + 1, whose system-scope loads (ld_sys: past A's caches, over xGMI) read B's lines of
+// pass k (p_{k-1} / Ap_{k-1} of pass k + 1), sees them; B's pass k + 1 rewrites the other p / apx
+// buffers, never the ones A reads in pass k + 1, and rewrites these only in pass k + 2, after A's pass
+// k + 1 has contributed to the next all-reduce.  The transport probe re-checks the whole chain on the
+// job's fabric at setup (the pulled iterations must reproduce the exchanged ones bit for bit).
 // a pulled ghost line's loads: side 0 = a local line, 1 / 2 = the lo / hi neighbour's rows
 struct PullBases {
   const double *p[2], *ap[2];
@@ -155,6 +170,13 @@ struct PullBases {
     if (pub && boundary) st_sys(base, o, v);
     else if (nt) g_st_nt(base, o, v);
     else g_st(base, o, v);
+  }
+  // the end of a run [l0, l1) that published the rank's first / last line: a system-scope release (the
+  // argument above); one per publishing wave
+  __device__ __forceinline__ void release(int64_t l0, int64_t l1, int64_t nl) const {
+    if constexpr (MCG_PULL_FENCE) {
+      if (pub && (l0 == 0 || l1 == nl)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
   }
 };
 

@@ -530,6 +530,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
               lstep(clamped, m, lastl ? VL : VB, nextc ? VL : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
+          pl.release(l0, l1, nl);
         }
         continue;
       }
@@ -752,6 +753,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         const bool lastl = l0 + m == nl - 1;
         lstep(clamped, m, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
       }
+      pl.release(l0, l1, nl);
       continue;
     }
     if constexpr (LEAN == 0) {

@@ -436,6 +436,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
           const bool lastl = l0 + m == nl - 1;
           lstep(clamped, m, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
         }
+        pl.release(l0, l1, nl);
         continue;
       }
       if constexpr (LEAN && !VC) {
@@ -683,6 +684,7 @@ __global__ __launch_bounds__(64 * KW, VC ? 2 : 4) void k_cg_carry_ar3(SellDev S,
               lstep(clamped, m, lastl ? VL : VB, nextc ? VL : VB, !lastl ? 1 : (is_ghost(m + 1) ? 2 : 0));
             }
           }
+          pl.release(l0, l1, nl);
         }
         continue;
       }

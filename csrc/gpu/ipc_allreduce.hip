@@ -9,9 +9,9 @@
 //      included), at system scope (write-through);
 //   2. after a barrier and a system-scope release fence, raises its flag in every mailbox: flag[rank]
 //      = the call's sequence number;
-//   3. waits (bounded by a wall-clock budget; a peer that never arrives sets the error word and the
-//      kernel ends) until every rank's flag in its own mailbox has reached the sequence number, then
-//      acquires;
+//   3. waits (bounded by a wall-clock budget; a peer that never arrives sets the error word, the sums
+//      come out NaN and the kernel ends) until every rank's flag in its own mailbox has reached the
+//      sequence number, then acquires;
 //   4. sums the slots in rank order (the same bits on every rank) into `buf`.
 // The sequence number is a device counter (mailbox flag[world]), so a hipGraph replays the kernel
 // correctly.  Slots alternate by the call's parity: a rank reaches call s + 2 only after every rank
@@ -43,6 +43,10 @@ __global__ __launch_bounds__(64) void k_ipc_allreduce(double* __restrict__ buf, 
   unsigned long long seq = 0;
   if (t == 0) seq = my_flags[P] + 1;  // this rank's call counter (only this kernel writes it)
   seq = __shfl(seq, 0, 64);
+  if (seq >> 63) {  // an earlier call gave up waiting (the sticky bit below): fail at once, no waiting
+    if (t < count) buf[t] = __builtin_nan("");
+    return;
+  }
   const int par = (int)(seq & 1);
   for (int e = t; e < P * count; e += 64) {
     const int q = e / count, i = e % count;
@@ -64,8 +68,19 @@ __global__ __launch_bounds__(64) void k_ipc_allreduce(double* __restrict__ buf, 
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  __syncthreads();
-  if (!ok) st_sys64(mb.err, 1ull);
+  // a peer that did not arrive: the error word for the host, NaN sums so the solver's breakdown latch
+  // stops every later iteration at once, and the call counter not advanced but marked failed (the
+  // mailboxes are out of step: the run ends, or the transport probe drops them; every later call
+  // returns NaN at once instead of waiting out its budget again)
+  const bool all_ok = __syncthreads_and(ok) != 0;
+  if (!all_ok) {
+    if (t == 0) {
+      st_sys64(mb.err, 1ull);
+      my_flags[P] = (seq - 1) | (1ull << 63);  // sticky: every later call fails at once
+    }
+    if (t < count) buf[t] = __builtin_nan("");
+    return;
+  }
   if (t < count) {
     const double* mine = mb.slots[me] + (size_t)(par * P) * kIpcArMax + t;
     double s = 0.0;

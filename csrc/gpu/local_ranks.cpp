@@ -80,6 +80,10 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         o.halo_pull = s.info().halo_pull;
         o.ag_overlap = s.info().ag_overlap;
         o.ag_local_frac = s.info().ag_local_frac;
+        o.probe_ran = s.info().probe_ran;
+        o.probe_pull_bitwise = s.info().probe_pull_bitwise;
+        o.probe_pull_us = s.info().probe_pull_us;
+        o.probe_xchg_us = s.info().probe_xchg_us;
         if (verify) o.true_rnorm = s.true_residual_norm();
       } catch (const Error& e) {
         o.error = std::string(e.what()) + ": " + e.detail();

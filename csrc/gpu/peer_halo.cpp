@@ -10,8 +10,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <random>
 #include <string>
 
 #include "mcg/check.hpp"
@@ -64,6 +66,17 @@ void* map_entry(const Entry& e, bool same_process, int64_t pdev, std::vector<voi
   opened.push_back(base);
   return static_cast<char*>(base) + e.offset;
 }
+// who made a handle blob: a per-process random token, not the pid (with a PID namespace per rank two
+// processes can share a pid, and a foreign pointer taken for a local one would fault the first pull)
+int64_t process_token() {
+  static const int64_t tok = [] {
+    std::random_device rd;
+    const uint64_t t = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    return (int64_t)((((uint64_t)rd() << 32) ^ rd() ^ (t * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)getpid() << 17)) |
+                     1ull);
+  }();
+  return tok;
+}
 size_t mailbox_bytes(int world) {
   return (size_t)2 * world * kern::kIpcArMax * sizeof(double) + (size_t)(world + 1) * sizeof(unsigned long long);
 }
@@ -84,15 +97,23 @@ PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int wo
   peer_flags_.assign(world, nullptr);
   peer_own_off_.assign(world, 0);
   peer_row_begin_.assign(world, 0);
-  // the IPC all-reduce's mailbox: uncached device memory (every access goes to memory, so a flag a peer
-  // wrote over the fabric is never served from a stale cache line), zeroed: call counters start at 0
-  MCG_CHECK(world <= kern::kIpcMaxRanks, "peer halo: too many ranks for the IPC all-reduce mailboxes");
+  mb_.rank = rank;
+  mb_.world = world;
+}
+
+// The IPC all-reduce's mailbox, allocated on first use (only a run that asks for the IPC all-reduce
+// maps mailboxes): uncached device memory (every access goes to memory, so a flag a peer wrote over
+// the fabric is never served from a stale cache line), zeroed: call counters start at 0
+void PeerHaloComm::ensure_mailbox_() {
+  if (mbox_ != nullptr) return;
+  MCG_CHECK(world_ <= kern::kIpcMaxRanks, "peer halo: too many ranks for the IPC all-reduce mailboxes");
   // (MCG_IPC_MAILBOX=cached: plain hipMalloc memory, a diagnostic)
-  const size_t mb_bytes = mailbox_bytes(world);
+  const size_t mb_bytes = mailbox_bytes(world_);
   const char* mk = std::getenv("MCG_IPC_MAILBOX");
   const bool cached = mk != nullptr && std::string(mk) == "cached";
   if (cached || hipExtMallocWithFlags(reinterpret_cast<void**>(&mbox_), mb_bytes, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();
+    mbox_ = nullptr;
     MCG_HIP(hipMalloc(&mbox_, mb_bytes), "device malloc failed(ipc mailbox)");
   }
   MCG_HIP(hipMemset(mbox_, 0, mb_bytes), "device memset failed(ipc mailbox)");
@@ -102,8 +123,6 @@ PeerHaloComm::PeerHaloComm(std::shared_ptr<Communicator> inner, int rank, int wo
           "host malloc failed(ipc all-reduce)");
   *err_host_ = 0;
   MCG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&mb_.err), err_host_, 0), "host pointer mapping failed");
-  mb_.rank = rank;
-  mb_.world = world;
 }
 
 PeerHaloComm::~PeerHaloComm() {
@@ -122,16 +141,23 @@ void PeerHaloComm::allreduce_sum(double* buf, size_t count, hipStream_t stream) 
 }
 
 void PeerHaloComm::check_async() {
-  if (err_host_ != nullptr && __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0) {
+  if (ipc_ar_ && err_host_ != nullptr && __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0) {
     fail("ipc all-reduce: a peer did not arrive", "waited " + std::to_string(ar_budget_seconds) + " s");
   }
   inner_->check_async();
 }
 
-std::string PeerHaloComm::mailbox_handle() const {
+bool PeerHaloComm::alt_allreduce_timed_out() {
+  if (err_host_ == nullptr || __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) == 0) return false;
+  __atomic_store_n(err_host_, 0ull, __ATOMIC_RELEASE);
+  return true;
+}
+
+std::string PeerHaloComm::mailbox_handle() {
+  ensure_mailbox_();
   std::string s;
   const uint64_t magic = kBlobMagic + 1;
-  const int64_t pid = (int64_t)getpid();
+  const int64_t pid = process_token();
   int dev = 0;
   MCG_HIP(hipGetDevice(&dev), "get device failed");
   const int64_t d64 = dev;
@@ -145,7 +171,8 @@ std::string PeerHaloComm::mailbox_handle() const {
 
 void PeerHaloComm::attach_mailbox(const std::vector<std::string>& all) {
   MCG_CHECK((int)all.size() == world_, "ipc all-reduce: one mailbox handle per rank");
-  const int64_t me = (int64_t)getpid();
+  ensure_mailbox_();
+  const int64_t me = process_token();
   const size_t nslot = (size_t)2 * world_ * kern::kIpcArMax;
   for (int q = 0; q < world_; ++q) {
     double* mb = nullptr;
@@ -161,6 +188,7 @@ void PeerHaloComm::attach_mailbox(const std::vector<std::string>& all) {
     mb_.slots[q] = mb;
     mb_.flags[q] = reinterpret_cast<unsigned long long*>(mb + nslot);
   }
+  mb_attached_ = true;
   ipc_ar_ = true;
 }
 
@@ -174,7 +202,7 @@ void PeerHaloComm::register_halo_buffers(const std::vector<double*>& bufs, int64
 std::string PeerHaloComm::local_handles() const {
   std::string s;
   const uint64_t magic = kBlobMagic;
-  const int64_t pid = (int64_t)getpid(), nb = (int64_t)bufs_.size();
+  const int64_t pid = process_token(), nb = (int64_t)bufs_.size();
   int dev = 0;
   MCG_HIP(hipGetDevice(&dev), "get device failed");
   const int64_t d64 = dev;
@@ -196,7 +224,7 @@ std::string PeerHaloComm::local_handles() const {
 
 void PeerHaloComm::attach(const std::vector<std::string>& all) {
   MCG_CHECK((int)all.size() == world_, "peer halo: one handle blob per rank");
-  const int64_t me = (int64_t)getpid();
+  const int64_t me = process_token();
   auto map = [&](const Entry& e, int64_t pid, int64_t pdev) { return map_entry(e, pid == me, pdev, opened_); };
   for (int q = 0; q < world_; ++q) {
     if (q == rank_) {

@@ -87,17 +87,30 @@ GpuCgSolver::~GpuCgSolver() {
   if (s0_.get()) (void)hipStreamSynchronize(s0_);
   if (s1_.get()) (void)hipStreamSynchronize(s1_);
   if (s2_.get()) (void)hipStreamSynchronize(s2_);
+  if (pull_host_) (void)hipHostFree(pull_host_);
 }
 
 void GpuCgSolver::reset() {
   trace::Range tr_("mcg.reset");
   MCG_CHECK(setup_done_, "solver not set up");
-  const int64_t n = L_.n_local();
-  hipStream_t s = s0_;
   // a halo prefetched by the last iteration may still be sending / receiving rows of r, Ap and p
   // on s1_: order the memsets below after it (no write of s0_ may race the side stream's RCCL)
   join_halo_();
-  if (pull_ && !pull_checked_) verify_pull_();  // (writes the p / apx lines the memsets below clear)
+  first_reset_checks_();  // (writes the p / apx lines and the state that reset_state_ clears)
+  reset_state_();
+}
+
+void GpuCgSolver::first_reset_checks_() {
+  if (pull_ && !pull_checked_) verify_pull_();
+  if (!probed_) {
+    probed_ = true;
+    probe_transport_();
+  }
+}
+
+void GpuCgSolver::reset_state_() {
+  const int64_t n = L_.n_local();
+  hipStream_t s = s0_;
   MCG_HIP(hipMemsetAsync(x_.get(), 0, x_.bytes(), s), "device memset failed(x)");
   for (DeviceBuffer<double>* v : {&Ap_, &r_, &ra_[0], &ra_[1], &ape_[0], &ape_[1], &apx_[0], &apx_[1], &w_, &z_, &q_})
     if (v->bytes()) MCG_HIP(hipMemsetAsync(v->get(), 0, v->bytes(), s), "device memset failed(r)");
@@ -618,11 +631,17 @@ void GpuCgSolver::enqueue_iteration_(int k) {
 // that this rank's ext index of a ghost row addresses the owner's copy of the same global row.  With a
 // rehearsal communicator (no peers, no data moved) the rank's own first / last line stands in for the
 // neighbours' (timing only, like NullComm's collectives).
+// A layout or registration mismatch returns false like a missing mapping (verify_pull_ then turns the
+// pull off on every rank through its agreement instead of one rank throwing before it).
 bool GpuCgSolver::map_pull_() {
   if (pull_mapped_) return true;
+  bool bad = false;
   auto idx = [&](const double* b) {
     auto it = std::find(halo_reg_.begin(), halo_reg_.end(), b);
-    MCG_CHECK(it != halo_reg_.end(), "in-kernel halo: buffer not registered");
+    if (it == halo_reg_.end()) {
+      bad = true;
+      return (size_t)0;
+    }
     return (size_t)(it - halo_reg_.begin());
   };
   const int64_t line = (int64_t)tr_all_.strip * 64;  // one grid line (2-D) / plane (3-D)
@@ -633,13 +652,27 @@ bool GpuCgSolver::map_pull_() {
     for (int b = 0; b < 3; ++b) pull_p_[b][sd] = nullptr;
     for (int b = 0; b < 2; ++b) pull_ap_[b][sd] = nullptr;
     if (h == nullptr) continue;  // the first / last rank: no ghost on that side
-    MCG_CHECK(h->count == line && (sd == 0 ? h->gbegin + h->count == L_.row_begin : h->gbegin == L_.row_end),
-              "in-kernel halo: the ghosts must be one whole line / plane next to the rank's rows");
+    // the ghosts must be one whole line / plane next to the rank's rows
+    if (h->count != line || !(sd == 0 ? h->gbegin + h->count == L_.row_begin : h->gbegin == L_.row_end)) return false;
     std::vector<double*> bufs;
     int64_t q_own = 0, q_rb = 0, src = 0;
     if (comm_->peer_view(h->peer, bufs, q_own, q_rb)) {
-      MCG_CHECK(bufs.size() == halo_reg_.size(), "in-kernel halo: ranks registered different buffer lists");
+      if (bufs.size() != halo_reg_.size()) return false;  // the ranks registered different buffer lists
       src = q_own + (h->gbegin - q_rb);  // the owner's ext index of the first ghost row
+    } else if (!comm_->moves_data() && opt_.hooks.pull_proxy == 1) {
+      // rehearsal stand-in over PCIe: every pulled buffer's ghost line in pinned, coherent host memory
+      // (5 buffers x 2 sides x one line), read by the pass's system-scope loads like a remote peer's rows
+      if (pull_host_ == nullptr) {
+        MCG_HIP(hipHostMalloc(reinterpret_cast<void**>(&pull_host_), (size_t)10 * line * sizeof(double),
+                              hipHostMallocMapped | hipHostMallocCoherent),
+                "host malloc failed(pull proxy)");
+        std::memset(pull_host_, 0, (size_t)10 * line * sizeof(double));
+      }
+      const int64_t g0 = L_.ext_index(h->gbegin);
+      for (int b = 0; b < 3; ++b)
+        pull_p_[b][sd] = p_[b].bytes() ? pull_host_ + (int64_t)(5 * sd + b) * line - g0 : nullptr;
+      for (int b = 0; b < 2; ++b) pull_ap_[b][sd] = pull_host_ + (int64_t)(5 * sd + 3 + b) * line - g0;
+      continue;
     } else if (!comm_->moves_data()) {
       bufs = halo_reg_;  // rehearsal stand-in: this rank's own first / last line
       src = L_.own_off + (sd == 0 ? 0 : L_.n_local() - line);
@@ -650,6 +683,7 @@ bool GpuCgSolver::map_pull_() {
     for (int b = 0; b < 3; ++b)
       if (p_[b].bytes()) pull_p_[b][sd] = bufs[idx(p_[b].get())] + shift;
     for (int b = 0; b < 2; ++b) pull_ap_[b][sd] = bufs[idx(apx_[b].get())] + shift;
+    if (bad) return false;  // a buffer the pass pulls was never registered
   }
   pull_mapped_ = true;
   return true;
@@ -707,6 +741,150 @@ void GpuCgSolver::verify_pull_() {
       info_.graphs = false;
     }
   }
+}
+
+// Sum of n host doubles over the ranks (setup only: a device bounce through the communicator's
+// all-reduce, then a sync).  Every rank gets the same bits, so a decision made from them is agreed.
+void GpuCgSolver::allreduce_host_(double* v, int n) {
+  if (!use_comm_ || !comm_->moves_data()) return;
+  DeviceBuffer<double> d(n, "state");
+  MCG_HIP(hipMemcpyAsync(d.get(), v, n * sizeof(double), hipMemcpyHostToDevice, s0_), "memcpy from host to device failed");
+  comm_->allreduce_sum(d.get(), n, s0_);
+  MCG_HIP(hipMemcpyAsync(v, d.get(), n * sizeof(double), hipMemcpyDeviceToHost, s0_), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
+}
+
+namespace {
+// the scalars of a run (every one the iterations wrote: equal bits = the same recurrence)
+bool states_equal(const CgState& a, const CgState& b) {
+  auto eq = [](double x, double y) { return std::memcmp(&x, &y, sizeof(double)) == 0; };
+  bool ok = eq(a.rr_new, b.rr_new) && eq(a.rho, b.rho) && eq(a.pAp, b.pAp) && eq(a.a_prev, b.a_prev) &&
+            eq(a.b_prev, b.b_prev) && a.iter == b.iter && a.done == b.done && a.breakdown == b.breakdown;
+  for (int i = 0; i < 4; ++i) ok = ok && eq(a.red[i], b.red[i]);
+  return ok;
+}
+bool states_close(const CgState& a, const CgState& b, double rel) {
+  auto cl = [&](double x, double y) {
+    if (std::isnan(x) || std::isnan(y)) return std::isnan(x) && std::isnan(y);
+    return std::fabs(x - y) <= rel * std::max(std::fabs(x), std::fabs(y)) + 1e-300;
+  };
+  bool ok = cl(a.rr_new, b.rr_new) && cl(a.rho, b.rho) && cl(a.pAp, b.pAp) && a.iter == b.iter && a.done == b.done &&
+            a.breakdown == b.breakdown;
+  for (int i = 0; i < 4; ++i) ok = ok && cl(a.red[i], b.red[i]);
+  return ok;
+}
+}  // namespace
+
+// The transport probe (P > 1, the first reset, after verify_pull_): which halo and all-reduce the
+// iterations use is chosen on the fabric the job runs on, from the same iterations timed both ways.
+//   halo (halo_pull auto and verified): 2 + C untimed and C timed iterations from the same start with
+//     the ghost lines pulled by the pass (PullBases) and with them exchanged before it (the
+//     communicator's halo: RCCL's send/recv); C = the graph iterations of every replayed phase.  The
+//     pulled run must end with the exchanged run's scalars bit for bit on every rank -- the real
+//     test of the pull's ordering (a pass's write-through boundary stores -> kernel end -> the
+//     all-reduce -> the neighbour's next pass), which verify_pull_'s memcpy'd pattern cannot be.
+//   all-reduce (a mapped but unselected alternative, PeerHaloComm's IPC mailboxes): the same with the
+//     halo chosen, its bounded wait cut to 10 s; it must match the first all-reduce's run to 1e-6
+//     (the sums' order differs, RCCL's from rank order) with no time-out.
+// Each rank's times and verdicts are summed over the ranks (one all-reduce on the first transport),
+// so every rank takes the same choice from the mean times; info_.probe_* report them.  The state the
+// arms leave is thrown away: reset_state_() follows.  Reference: the reduction sites CUDACG.cu:304,328
+// and the SpMV's read of the neighbours' p, :288, which these transports carry.
+void GpuCgSolver::probe_transport_() {
+  info_.alt_allreduce = use_comm_ && comm_->alt_allreduce_in_use();
+  if (!use_comm_ || world_ < 2 || !comm_->moves_data() || opt_.transport_probe == 0 || opt_.hooks.inject_nan_at >= 0)
+    return;
+  const bool halo_choice = pull_ && opt_.form.halo_pull == -1;  // (pull_ is agreed: the same on every rank)
+  // the alternative all-reduce only if every rank mapped every mailbox (a rank whose mapping failed
+  // must not leave the others running an arm it cannot)
+  const bool ar_choice = all_ranks_agree_(comm_->alt_allreduce_ready() && !comm_->alt_allreduce_in_use());
+  if (!halo_choice && !ar_choice) return;
+  trace::Range tr_("mcg.transport_probe");
+  const double tol0 = opt_.tol, rtol0 = opt_.rtol;
+  const bool graph0 = opt_.use_graph;
+  opt_.tol = -1.0;  // every probe iteration does its work (kernels take tol by value: fresh captures below)
+  opt_.rtol = 0.0;
+  const int cyc = graph0 ? (p3buf_ ? 3 : 1) * opt_.graph_iters : 16;
+  struct Arm {
+    double us = 0.0;
+    CgState st{};
+    bool timeout = false;
+  };
+  auto run_arm = [&](bool pull, bool alt) {
+    Arm a;
+    drop_graphs_();
+    pull_ = pull;
+    comm_->use_alt_allreduce(alt);
+    opt_.use_graph = graph0 && (pull || !use_halo_ || comm_->halo_capturable());
+    reset_state_();
+    run_iterations(2 + cyc);  // captures every graph the timed iterations replay
+    MCG_HIP(hipEventRecord(ev_t0_, s0_), "event record failed");
+    run_iterations(cyc);
+    MCG_HIP(hipEventRecord(ev_t1_, s0_), "event record failed");
+    if (alt) {  // (not synchronize(): its async check would throw on the time-out this arm may report)
+      MCG_HIP(hipStreamSynchronize(s1_), "device synchronize failed");
+      MCG_HIP(hipStreamSynchronize(s0_), "device synchronize failed");
+    } else {
+      synchronize();
+    }
+    float ms = 0.f;
+    MCG_HIP(hipEventElapsedTime(&ms, ev_t0_, ev_t1_), "event elapsed time failed");
+    a.us = 1e3 * (double)ms / cyc;
+    MCG_HIP(hipMemcpy(&a.st, st_.get(), sizeof(CgState), hipMemcpyDeviceToHost), "memcpy from device to host failed(state)");
+    if (alt) a.timeout = comm_->alt_allreduce_timed_out();
+    comm_->use_alt_allreduce(false);
+    return a;
+  };
+  info_.probe_ran = true;
+  info_.probe_iters = cyc;
+  const bool pull0 = pull_;  // without a halo choice: the configured halo (forced pull, or exchanged)
+  bool pull = pull0;
+  Arm best;
+  {
+    const Arm x = run_arm(halo_choice ? false : pull0, false);
+    Arm p;
+    if (halo_choice) p = run_arm(true, false);
+    double v[3] = {x.us, halo_choice ? p.us : 0.0, halo_choice && !states_equal(p.st, x.st) ? 1.0 : 0.0};
+    allreduce_host_(v, 3);
+    if (halo_choice) {
+      info_.probe_xchg_us = v[0] / world_;
+      info_.probe_pull_us = v[1] / world_;
+      info_.probe_pull_bitwise = v[2] == 0.0;
+      pull = info_.probe_pull_bitwise && (opt_.hooks.probe_pick_halo >= 0 ? opt_.hooks.probe_pick_halo == 1
+                                                                         : info_.probe_pull_us <= info_.probe_xchg_us);
+      if (!info_.probe_pull_bitwise && rank_ == 0)
+        std::fprintf(stderr, "[mcg] transport probe: the pulled run did not reproduce the exchanged one: the halo is exchanged\n");
+    } else {
+      (pull0 ? info_.probe_pull_us : info_.probe_xchg_us) = v[0] / world_;
+    }
+    best = pull && halo_choice ? p : x;
+    best.us = pull ? info_.probe_pull_us : info_.probe_xchg_us;
+  }
+  bool alt = false;
+  if (ar_choice) {
+    comm_->set_alt_allreduce_budget(10.0);
+    const Arm a = run_arm(pull, true);
+    double v[3] = {a.us, a.timeout ? 1.0 : 0.0, states_close(a.st, best.st, 1e-6) ? 0.0 : 1.0};
+    allreduce_host_(v, 3);
+    comm_->set_alt_allreduce_budget(120.0);
+    info_.probe_alt_us = v[0] / world_;
+    info_.probe_alt_timeout = v[1] != 0.0;
+    info_.probe_alt_close = v[1] == 0.0 && v[2] == 0.0;
+    alt = info_.probe_alt_close &&
+          (opt_.hooks.probe_pick_ar >= 0 ? opt_.hooks.probe_pick_ar == 1 : info_.probe_alt_us < best.us);
+    if (!info_.probe_alt_close && rank_ == 0)
+      std::fprintf(stderr, "[mcg] transport probe: the alternative all-reduce %s: the first one is kept\n",
+                   info_.probe_alt_timeout ? "timed out" : "did not reproduce the first one's sums");
+  }
+  drop_graphs_();
+  pull_ = pull;
+  info_.halo_pull = pull_;
+  comm_->use_alt_allreduce(alt);
+  info_.alt_allreduce = alt;
+  opt_.tol = tol0;
+  opt_.rtol = rtol0;
+  opt_.use_graph = graph0 && (pull_ || !use_halo_ || comm_->halo_capturable());
+  info_.graphs = opt_.use_graph;
 }
 
 void GpuCgSolver::join_halo_() {

@@ -78,6 +78,7 @@ void GpuCgSolver::load_checkpoint(const std::string& prefix) {
   // nothing of an earlier solve may still run on either stream (a pending halo writes ghost rows)
   synchronize();
   join_halo_();
+  first_reset_checks_();  // (a resume without a reset: the in-kernel halo's check and the transport probe first)
   const std::string path = prefix + ".rank" + std::to_string(rank_);
   std::FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) fail("checkpoint read failed", path);

@@ -102,6 +102,12 @@ struct TestHooks {
   int fail_graph_launch_at = -1;  // test hook: report the graph launch at this iteration as failed (nothing enqueued)
   int force_idx64 = 0;       // test hook: int64 row pointers even when int32 would do
   int inject_nan_at = -1;    // fault-injection hook: poison r at this iteration (breakdown detection test)
+  int pull_proxy = 0;        // rehearsal (a communicator that moves no data) with halo_pull 1: the pulled ghost lines
+                             // read 0 = this rank's own first / last line (local HBM), 1 = pinned host memory over
+                             // PCIe (a slow remote: an upper bound on what the pull costs over the fabric)
+  int probe_pick_halo = -1;  // test hook: the transport probe runs every arm but keeps the pulled (1) / exchanged (0)
+                             // halo whatever the times (a pulled run that did not match the exchanged one still loses)
+  int probe_pick_ar = -1;    // test hook: ... keeps the alternative (1) / the first (0) all-reduce (a failed one loses)
   int lean_packed = -1;      // test hook: 0 = the packed-edge geometry (solver_setup.cpp auto_mix_: even passes on 5,
                              // odd ones on 4 blocks per CU) with the default lean kernels instead of the packed-edge
                              // ones -- the bit-for-bit reference of those kernels
@@ -143,6 +149,12 @@ struct CgOptions {
   int placement_leads = 16;  // ... times this many start offsets of the vectors inside their allocations
                              // (16384^2: 3 x 8 -> 503-517 it/s, 6 x 8 -> 516-525, 6 x 16 -> 524-525;
                              // profiles/r3_placement_depth.txt)
+  int transport_probe = -1;  // P > 1, at the first reset: the transport probe (GpuCgSolver::probe_transport_) runs the
+                             // same iterations from the same start with the ghost lines pulled (halo_pull auto) and
+                             // exchanged, then with the alternative all-reduce (a PeerHaloComm whose IPC mailboxes are
+                             // mapped but not selected) against the first, and keeps the fastest correct arm: the
+                             // pulled run must reproduce the exchanged one bit for bit, the IPC sums the RCCL ones to
+                             // rounding.  -1 = auto (on when there is a choice), 0 = off (the configured transport)
   int reserve_cus = 0;       // CUs withheld from the compute stream (a CU-masked queue, the mask's top bits; 32 = one
                              // per shader engine) so a collective's ~270-VGPR kernels find a free CU beside the
                              // resident pass (profiles/r3_cumask_probe.md); the pass grids are sized for the CUs

@@ -124,6 +124,16 @@ class Communicator {
   // hipStreamEndCapture; kept = false: the capture failed and its graph is dropped): a transport whose
   // captured operations replay fixed values checks / rewinds its sequence here
   virtual void on_captured(bool /*kept*/) {}
+  // A second all-reduce transport the solver's transport probe (GpuCgSolver::probe_transport_) may time
+  // against the first at setup: PeerHaloComm's IPC mailboxes, once every rank's is mapped, next to an
+  // inner communicator that moves data.  ready: both exist; use: route allreduce_sum to it (true) or to
+  // the first (false); timed_out: its bounded wait gave up since the last call (the error is cleared);
+  // budget: seconds that wait may last before it gives up
+  virtual bool alt_allreduce_ready() const { return false; }
+  virtual void use_alt_allreduce(bool) {}
+  virtual bool alt_allreduce_in_use() const { return false; }
+  virtual bool alt_allreduce_timed_out() { return false; }
+  virtual void set_alt_allreduce_budget(double) {}
 };
 
 class Comm final : public Communicator {
@@ -258,12 +268,18 @@ class PeerHaloComm final : public Communicator {
   void set_capturable(bool c) { capturable_ = c; }
   // test hook: the registered buffer list (device pointers) of rank q as mapped here
   std::vector<uintptr_t> peer_buffers(int q) const;
-  // the IPC all-reduce: this rank's mailbox handle (allocated at construction) for an out-of-band
-  // all-gather, then every rank's, in rank order; from then on allreduce_sum runs through the mailboxes
-  std::string mailbox_handle() const;
+  // the IPC all-reduce: this rank's mailbox handle (the mailbox is allocated on this first use) for an
+  // out-of-band all-gather, then every rank's, in rank order; from then on allreduce_sum runs through the
+  // mailboxes (use_alt_allreduce(false) routes it back to the inner communicator)
+  std::string mailbox_handle();
   void attach_mailbox(const std::vector<std::string>& all);
   bool ipc_allreduce() const { return ipc_ar_; }
   double ar_budget_seconds = 120.0;  // a peer that does not arrive for this long: error (check_async)
+  bool alt_allreduce_ready() const override { return mb_attached_ && inner_->moves_data(); }
+  void use_alt_allreduce(bool on) override { ipc_ar_ = on && mb_attached_; }
+  bool alt_allreduce_in_use() const override { return ipc_ar_; }
+  bool alt_allreduce_timed_out() override;
+  void set_alt_allreduce_budget(double s) override { ar_budget_seconds = s; }
 
  private:
   std::shared_ptr<Communicator> inner_;
@@ -279,7 +295,9 @@ class PeerHaloComm final : public Communicator {
   double* mbox_ = nullptr;                       // uncached: [2][world][kIpcArMax] slots, then world + 1 u64 flags
   unsigned long long* err_host_ = nullptr;       // pinned, device-mapped error word of the IPC all-reduce
   kern::IpcMailboxes mb_;
-  bool ipc_ar_ = false;
+  void ensure_mailbox_();
+  bool mb_attached_ = false;  // every rank's mailbox mapped (attach_mailbox)
+  bool ipc_ar_ = false;       // ... and the all-reduce runs through them
   bool halo_inner_ = false;
   long seq_ = 0;
   std::vector<int> last_readers_;  // the ranks that pull this rank's rows of exchange seq_

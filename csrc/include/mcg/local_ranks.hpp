@@ -23,6 +23,8 @@ struct LocalRankResult {
   bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)
   bool ag_overlap = false;     // SolverInfo::ag_overlap (own-block SpMV half || all-gather)
   double ag_local_frac = 0.0;  // SolverInfo::ag_local_frac
+  bool probe_ran = false, probe_pull_bitwise = false;  // SolverInfo's transport probe
+  double probe_pull_us = 0.0, probe_xchg_us = 0.0;
   std::vector<std::pair<std::string, double>> phases;  // phase_profile (mean us) when asked for
   std::string error;
 };

@@ -89,6 +89,16 @@ struct SolverInfo {
   double placement_best_ms = 0.0, placement_worst_ms = 0.0;  // two even/odd pass pairs
   int placement_lead_trial = 0;  // start-offset trial kept (0 = allocation starts)
   size_t placement_peak_bytes = 0;  // extra device bytes held while the probe compared vector sets
+  // the transport probe (GpuCgSolver::probe_transport_; P > 1, the first reset): microseconds per iteration,
+  // the mean over the ranks, of each arm it ran (0: not run) -- pulled / exchanged ghost lines with the first
+  // all-reduce, the alternative (IPC) all-reduce with the halo chosen -- and what it found
+  bool probe_ran = false;
+  double probe_pull_us = 0.0, probe_xchg_us = 0.0, probe_alt_us = 0.0;
+  int probe_iters = 0;             // timed iterations per arm (after 2 + as many untimed)
+  bool probe_pull_bitwise = false; // the pulled run reproduced the exchanged one bit for bit on every rank
+  bool probe_alt_close = false;    // the alternative all-reduce's run matched the first's to 1e-6, no time-out
+  bool probe_alt_timeout = false;  // ... its bounded wait gave up on some rank
+  bool alt_allreduce = false;      // the all-reduce runs on the alternative transport (IPC mailboxes)
 };
 
 class GpuCgSolver {
@@ -169,8 +179,14 @@ class GpuCgSolver {
   const double* pull_p_[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};  // [p buffer][lo, hi side]
   const double* pull_ap_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [apx buffer][lo, hi side]
   std::vector<double*> halo_reg_;  // the buffers registered with the communicator (its peer_view order)
-  bool map_pull_();     // false: a peer's buffers are not mapped here (not attached)
+  double* pull_host_ = nullptr;    // TestHooks::pull_proxy 1: the stand-in ghost lines in pinned host memory
+  bool map_pull_();     // false: a peer's buffers are not mapped here (not attached), or their layout differs
   void verify_pull_();  // the first reset: every rank reads a pattern through the pull pointers, or pull_ goes off
+  void first_reset_checks_();  // verify_pull_ + probe_transport_, once (the first reset or checkpoint load)
+  void probe_transport_();     // P > 1: time (and check) the halo / all-reduce transports, keep the best
+  void reset_state_();         // reset()'s state: x = 0, r = b, p = 0, scalars, k = 0
+  void allreduce_host_(double* v, int n);  // setup-time sum of n host doubles over the ranks
+  bool probed_ = false;
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
   bool ar_ = false;             // CgOptions::ap_recompute in effect

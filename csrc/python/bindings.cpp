@@ -239,6 +239,10 @@ PYBIND11_MODULE(_C, m) {
       MCG_HOOK_PROP(force_idx64)
       MCG_HOOK_PROP(inject_nan_at)
       MCG_HOOK_PROP(lean_packed)
+      MCG_HOOK_PROP(pull_proxy)
+      MCG_HOOK_PROP(probe_pick_halo)
+      MCG_HOOK_PROP(probe_pick_ar)
+      .def_readwrite("transport_probe", &CgOptions::transport_probe)
       .def_readwrite("spmv_variant", &CgOptions::spmv_variant)
       .def_readwrite("maxit", &CgOptions::maxit)
       .def_readwrite("tol", &CgOptions::tol)
@@ -372,13 +376,15 @@ PYBIND11_MODULE(_C, m) {
         c.attach(v);
       })
       .def_property_readonly("attached", &PeerHaloComm::attached)
-      .def("mailbox_handle", [](const PeerHaloComm& c) { return py::bytes(c.mailbox_handle()); })
+      .def("mailbox_handle", [](PeerHaloComm& c) { return py::bytes(c.mailbox_handle()); })
       .def("attach_mailbox", [](PeerHaloComm& c, const std::vector<py::bytes>& all) {
         std::vector<std::string> v;
         for (const py::bytes& b : all) v.push_back(std::string(b));
         c.attach_mailbox(v);
       }, "map every rank's IPC all-reduce mailbox; from then on the all-reduce runs through them")
-      .def_property_readonly("ipc_allreduce", &PeerHaloComm::ipc_allreduce)
+      .def_property("ipc_allreduce", &PeerHaloComm::ipc_allreduce, &PeerHaloComm::use_alt_allreduce,
+                    "the all-reduce runs through the mapped mailboxes (settable once attach_mailbox ran; the "
+                    "solver's transport probe may change it at the first reset)")
       .def_property("halo_via_inner", &PeerHaloComm::halo_via_inner, &PeerHaloComm::set_halo_via_inner)
       .def_readwrite("ar_budget_seconds", &PeerHaloComm::ar_budget_seconds)
       .def("allreduce_ptr", [](PeerHaloComm& c, uintptr_t buf, size_t count, uintptr_t stream) {
@@ -506,6 +512,15 @@ PYBIND11_MODULE(_C, m) {
         d["placement_worst_ms"] = i.placement_worst_ms;
         d["placement_lead_trial"] = i.placement_lead_trial;
         d["placement_peak_bytes"] = i.placement_peak_bytes;
+        d["probe_ran"] = i.probe_ran;
+        d["probe_pull_us"] = i.probe_pull_us;
+        d["probe_xchg_us"] = i.probe_xchg_us;
+        d["probe_alt_us"] = i.probe_alt_us;
+        d["probe_iters"] = i.probe_iters;
+        d["probe_pull_bitwise"] = i.probe_pull_bitwise;
+        d["probe_alt_close"] = i.probe_alt_close;
+        d["probe_alt_timeout"] = i.probe_alt_timeout;
+        d["alt_allreduce"] = i.alt_allreduce;
         d["device_bytes"] = i.device_bytes;
         d["bytes_per_iter_model"] = i.bytes_per_iter_model;
         d["grid_a"] = i.grid_a;
@@ -541,6 +556,10 @@ PYBIND11_MODULE(_C, m) {
       d["halo_pull"] = rr.halo_pull;
       d["ag_overlap"] = rr.ag_overlap;
       d["ag_local_frac"] = rr.ag_local_frac;
+      d["probe_ran"] = rr.probe_ran;
+      d["probe_pull_bitwise"] = rr.probe_pull_bitwise;
+      d["probe_pull_us"] = rr.probe_pull_us;
+      d["probe_xchg_us"] = rr.probe_xchg_us;
       py::dict ph;
       for (auto& kv : rr.phases) ph[py::str(kv.first)] = kv.second;
       d["phases"] = ph;

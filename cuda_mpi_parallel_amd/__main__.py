@@ -18,11 +18,13 @@ import time
 from .cli_spec import FLAGS, recurrence, tri
 from .utils import format_x
 
-SWITCHES = {"--no-overlap", "--no-graph", "--force-comm", "--verify"}
+SWITCHES = {"--no-overlap", "--no-graph", "--force-comm", "--verify", "--rehearse-ranks"}
 CHOICES = {"--problem": ["demo", "poisson2d", "poisson3d", "randspd", "csr", "random-spd", "random"],
            "--rhs": ["reference", "random", "ones"], "--device": ["gpu", "cpu"],
            "--format": ["csr", "sell", "sell16", "sellc8"], "--print-x": ["auto", "yes", "no"],
-           "--report": ["text", "json"], "--comm": ["dual", "single"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"]}
+           "--report": ["text", "json"], "--comm": ["dual", "single"], "--halo-mode": ["auto", "window", "allgather", "-1", "0", "1"],
+           "--halo-transport": ["auto", "rccl"], "--allreduce": ["auto", "rccl", "ipc"],
+           "--transport-probe": ["auto", "off", "on", "-1", "0", "1"]}
 INTS = {"--n", "--rows", "--band", "--spread", "--scramble", "--coef", "--seed", "--gpus", "--sim-ranks", "--maxit", "--check-every",
         "--fixed-iters", "--warmup", "--blocks-per-cu", "--spmv-variant", "--checkpoint-every", "--inject-nan-at",
         "--pipe-rr", "--reserve-cus"}
@@ -33,7 +35,7 @@ DEFAULTS = {"--problem": "demo", "--seed": 1234, "--device": "gpu", "--gpus": No
             "--pmat": "auto", "--fused-reduce": "auto", "--halo-mode": "auto", "--blocks-per-cu": 0,
             "--spmv-variant": -1, "--checkpoint": "", "--checkpoint-every": 0, "--resume": "", "--inject-nan-at": -1,
             "--print-x": "auto", "--report": "text", "--comm": "single", "--pipe-rr": 0,
-            "--reserve-cus": 0}
+            "--reserve-cus": 0, "--halo-transport": "auto", "--allreduce": "auto", "--transport-probe": "auto"}
 
 
 def _parser() -> argparse.ArgumentParser:
@@ -98,7 +100,7 @@ def main(argv=None) -> int:
     if args.device == "gpu":
         from .parallel import launch
 
-        rc = launch.launch_or_none(args.gpus, argv, module="cuda_mpi_parallel_amd")
+        rc = launch.launch_or_none(args.gpus, argv, module="cuda_mpi_parallel_amd", share_device=args.rehearse_ranks)
         if rc is not None:
             return rc
     try:
@@ -143,7 +145,9 @@ def _run(args) -> int:
                          pmat=tri(args.pmat), fused_reduce=tri(args.fused_reduce), halo_mode=_halo(args.halo_mode),
                          rtol=args.rtol, pipe_rr=args.pipe_rr, checkpoint_every=args.checkpoint_every, checkpoint_path=args.checkpoint,
                          inject_nan_at=args.inject_nan_at, watchdog_seconds=args.watchdog,
-                         reserve_cus=args.reserve_cus)
+                         reserve_cus=args.reserve_cus, halo_transport=args.halo_transport, allreduce=args.allreduce,
+                         rehearse_ranks=args.rehearse_ranks,
+                         transport_probe=0 if tri(args.transport_probe) == 0 else -1)
         if fixed:
             import torch.distributed as dist
 
@@ -188,7 +192,7 @@ def _run(args) -> int:
                 "iterations": res["iterations"], "converged": res["converged"], "breakdown": res["breakdown"],
                 "rnorm": res["rnorm"], "true_rnorm": true_rnorm, "setup_s": res.get("setup_seconds"),
                 "solve_s": res["solve_seconds"], "it_per_s": res["iters_per_second"],
-                "device_bytes_rank0": info.get("device_bytes", 0)}) + "\n")
+                "device_bytes_rank0": info.get("device_bytes", 0), **_transport_report(info, world, args)}) + "\n")
         elif not want_x or n > 3:
             sys.stderr.write("[mcg] problem=%s n=%d ranks=%d iterations=%d converged=%d rnorm=%.3e solve=%.4fs "
                              "(%.2f it/s)\n" % (spec.problem, n, world, res["iterations"], int(res["converged"]),
@@ -197,6 +201,24 @@ def _run(args) -> int:
         sys.stdout.write("".join(out))
         sys.stdout.flush()
     return 0
+
+
+def _transport_report(info, world, args) -> dict:
+    """The P > 1 transports in effect (the keys bin/mcg-cg --report json prints too)."""
+    gpu = args.device == "gpu" and world > 1
+    probe = None
+    if info.get("probe_ran"):
+        probe = {"pull_us": info["probe_pull_us"], "rccl_halo_us": info["probe_xchg_us"],
+                 "ipc_ar_us": info["probe_alt_us"], "pull_bitwise": info["probe_pull_bitwise"],
+                 "ipc_ar_close": info["probe_alt_close"], "iters_timed": info["probe_iters"],
+                 "chosen": ("pull" if info.get("halo_pull") else "exchange") + "+"
+                           + ("ipc" if info.get("alt_allreduce") else "rccl")}
+    rehearse = bool(args.rehearse_ranks)
+    return {"halo_pull": bool(info.get("halo_pull", False)),
+            "halo_transport": "none" if not gpu else "in-kernel" if info.get("halo_pull") else
+                              ("sdma" if rehearse else "rccl"),
+            "allreduce": "none" if not gpu else "ipc" if (info.get("alt_allreduce") or rehearse) else "rccl",
+            "transport_probe": probe, "rehearse_ranks": rehearse}
 
 
 def _halo(v: str) -> int:

@@ -56,6 +56,13 @@ FLAGS = [
     ("--blocks-per-cu", "0", "SpMV grid, blocks per CU (0 = auto)"),
     ("--reserve-cus", "0", "CUs withheld from the compute stream (32 = one per shader engine) so collectives start beside the pass"),
     ("--spmv-variant", "-1", "CSR engine: 0 LDS tiles, 1 direct, 2 CSR-vector, 3 direct nt, 4 row-length adaptive; -1 auto"),
+    # P > 1 transports (the solver's transport probe picks at the first reset)
+    ("--halo-transport", "auto", "auto: the neighbours' halo buffers mapped (the lean carries read their ghost lines "
+                                 "in-kernel) | rccl: RCCL's send/recv only"),
+    ("--allreduce", "auto", "auto: IPC mailboxes mapped next to RCCL, the probe keeps the faster correct one | rccl | ipc"),
+    ("--transport-probe", "auto", "auto | off: time the pulled vs exchanged halo and the two all-reduces at setup"),
+    ("--rehearse-ranks", None, "--gpus P ranks all on GPU 0, the real P-rank recurrence (native: threads over an "
+                               "in-process communicator; python: processes over IPC mailboxes and copy engines)"),
     # aux subsystems
     ("--checkpoint", None, "PREFIX of per-rank checkpoint files"),
     ("--checkpoint-every", "0", "write a checkpoint every ~K iterations"),

@@ -64,7 +64,8 @@ def bootstrap_comm(env: DistEnv, force: bool = False, mode: str = "single"):
     return C.Comm(env.rank, env.world, *ids)
 
 
-def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False, halo_via_inner: bool = False):
+def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False, halo_via_inner: bool = False,
+              tolerant: bool = False):
     """Wrap a communicator so that the halo moves without RCCL (native ``PeerHaloComm``: the
     neighbours' buffers mapped through IPC handles -- pulled by copy engines, or read by the lean
     passes themselves, PassForm::halo_pull); the all-reduce stays on ``inner`` unless
@@ -72,18 +73,36 @@ def peer_halo(inner, env: DistEnv, ipc_allreduce: bool = False, halo_via_inner: 
     through them (ipc_allreduce.hip) -- real P-rank sums with no RCCL, e.g. P processes on one GPU.
     ``halo_via_inner``: only the mapping (the lean passes' in-kernel halo); every halo exchange that
     remains goes to ``inner`` (RCCL's send/recv).  Call :func:`attach_peer_halo` after the solver's
-    ``setup()``."""
+    ``setup()``.  ``tolerant``: a rank that cannot allocate, export or map the mailboxes leaves them
+    unmapped instead of raising (every rank then skips them: the solver's transport probe agrees on it,
+    and the all-reduce stays on ``inner``)."""
+    import sys
+
     comm = native().PeerHaloComm(inner, env.rank, env.world)
     comm.halo_via_inner = halo_via_inner
     if ipc_allreduce:
-        mine = comm.mailbox_handle()
+        try:
+            mine = comm.mailbox_handle()
+        except Exception as e:  # noqa: BLE001
+            if not tolerant:
+                raise
+            print(f"[mcg] rank {env.rank}: IPC all-reduce mailbox unavailable ({e})", file=sys.stderr, flush=True)
+            mine = b""
         allb = [mine]
         if env.world > 1:
             if not dist.is_initialized():
                 raise RuntimeError("peer_halo(ipc_allreduce=True) needs torch.distributed initialised")
             allb = [None] * env.world
             dist.all_gather_object(allb, mine)
-        comm.attach_mailbox(allb)
+        if all(allb):
+            try:
+                comm.attach_mailbox(allb)
+            except Exception as e:  # noqa: BLE001
+                if not tolerant:
+                    raise
+                print(f"[mcg] rank {env.rank}: IPC all-reduce mailboxes not mapped ({e})", file=sys.stderr, flush=True)
+        elif not tolerant:
+            raise RuntimeError("a rank could not export its IPC all-reduce mailbox")
     return comm
 
 

@@ -47,23 +47,53 @@ class CGSolver:
     def __init__(self, spec: ProblemSpec, maxit: int = 2000, tol: float = 1e-7, check_every: int = 32,
                  overlap: bool = True, use_graph: bool = True, format: str = "auto", force_comm: bool = False,
                  blocks_per_cu: int = 0, env: Optional[_dist.DistEnv] = None, comm=None, comm_mode: str = "single",
-                 **tuning):
+                 halo_transport: str = "auto", allreduce: str = "auto", rehearse_ranks: bool = False, **tuning):
+        """``halo_transport`` / ``allreduce`` (P > 1, a communicator built here): "auto" maps the
+        neighbours' halo buffers (the lean carries' in-kernel halo) and every rank's IPC all-reduce
+        mailbox next to RCCL, and the solver's transport probe keeps the fastest correct pair at the
+        first reset; "rccl" keeps RCCL only; ``allreduce="ipc"`` forces the mailboxes.
+        ``rehearse_ranks``: the P processes share GPU 0 (collectives: IPC mailboxes and copy engines,
+        no RCCL) -- the real P-rank recurrence on one GPU, as ``bench.py --rehearse-ranks --allreduce ipc``."""
         if format == "auto":
             demo = getattr(spec, "problem", "") == "demo"
             format = "csr" if demo else "sellc8"
             if not demo:
                 tuning.setdefault("recurrence", -1)
+        if halo_transport not in ("auto", "rccl") or allreduce not in ("auto", "rccl", "ipc"):
+            raise ValueError(f"halo_transport auto|rccl, allreduce auto|rccl|ipc; got {halo_transport!r}, {allreduce!r}")
         self.spec = spec
         self.env = env or _dist.dist_env()
-        _dist.set_device(self.env)
+        rehearse = rehearse_ranks and self.env.world > 1
+        if rehearse:
+            import torch
+
+            torch.cuda.set_device(0)
+        else:
+            _dist.set_device(self.env)
+        peer = False
         if comm is None and (self.env.world > 1 or force_comm):
             _dist.init_process_group(self.env)
-            comm = _dist.bootstrap_comm(self.env, force=force_comm, mode=comm_mode)
+            if rehearse:  # every rank on GPU 0: the IPC all-reduce and the copy-engine halo (RCCL refuses)
+                comm = _dist.peer_halo(native().NullComm(self.env.rank, self.env.world), self.env, ipc_allreduce=True)
+                peer = True
+            else:
+                comm = _dist.bootstrap_comm(self.env, force=force_comm, mode=comm_mode)
+                if self.env.world > 1 and halo_transport == "auto":
+                    probe_ar = allreduce == "auto"
+                    comm = _dist.peer_halo(comm, self.env, ipc_allreduce=probe_ar or allreduce == "ipc",
+                                           halo_via_inner=True, tolerant=probe_ar)
+                    if probe_ar:
+                        comm.ipc_allreduce = False  # the transport probe decides
+                    peer = True
         self.comm = comm
+        if halo_transport == "rccl":
+            tuning.setdefault("halo_pull", 0)  # no mapped peers: every ghost line exchanged
         self.opts = _opts(maxit, tol, check_every=check_every, overlap=overlap, use_graph=use_graph,
                           force_comm=force_comm, format=format, blocks_per_cu=blocks_per_cu, **tuning)
         self._s = native().Solver(spec.native(), self.opts, self.env.rank, self.env.world, comm)
         self._s.setup()
+        if peer:  # map the peers' registered halo buffers (collective; the first reset checks the mapping)
+            _dist.attach_peer_halo(comm, self.env, tolerant=not rehearse)
 
     # --- solve to tolerance (reference semantics) ---
     def solve(self, resume: bool = False) -> Dict:

@@ -258,8 +258,13 @@ def test_local_ranks_in_kernel_halo_bitwise(mcg, world, problem, kw):
     for tag, hp, ov in (("pull", 1, False), ("serial", 0, False), ("ahead", 0, True), ("pull_ov", -1, True)):
         o = _opts(mcg, tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1, check_every=8, overlap=ov)
         o.halo_pull = hp
+        o.probe_pick_halo = 1  # auto: the transport probe runs both arms, keeps the pull if it reproduced the exchange
         outs[tag] = C.run_local_ranks(spec.native(), o, world, 40, True)
         assert all(q["halo_pull"] == (hp != 0) for q in outs[tag]["ranks"]), (tag, outs[tag]["ranks"])
+        assert all(q["probe_ran"] == (hp == -1) for q in outs[tag]["ranks"]), tag
+        if hp == -1:
+            assert all(q["probe_pull_bitwise"] and q["probe_pull_us"] > 0 and q["probe_xchg_us"] > 0
+                       for q in outs[tag]["ranks"]), outs[tag]["ranks"]
         assert all(q["lean_only"] for q in outs[tag]["ranks"]), tag
     for tag in ("serial", "ahead", "pull_ov"):
         assert [q["rnorm"] for q in outs[tag]["ranks"]] == [q["rnorm"] for q in outs["pull"]["ranks"]], tag
@@ -292,8 +297,9 @@ def test_local_ranks_in_kernel_halo_converges(mcg, problem, n):
     spec = mcg.make_problem(problem, n=n, rhs="random")
     C = mcg.native()
     o = _opts(mcg, format="sellc8", recurrence=-1, check_every=4)
+    o.probe_pick_halo = 1  # (the probe's timing would pick either on threads sharing one GPU)
     out = C.run_local_ranks(spec.native(), o, 4, 0, True)
-    assert all(q["halo_pull"] for q in out["ranks"])
+    assert all(q["halo_pull"] and q["probe_pull_bitwise"] for q in out["ranks"])
     its = {q["iterations"] for q in out["ranks"]}
     assert len(its) == 1, its
     cpu = C.cpu_cg(spec.native(), C.CgOptions(maxit=2000, tol=1e-7))

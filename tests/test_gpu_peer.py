@@ -78,6 +78,26 @@ def test_ipc_ranks_real_recurrence_matches_one_rank(world, problem, n, pull, coe
     assert line["gap_rnorm"] <= 1e-13 and line["true_gap"] <= 1e-8, line
 
 
+@pytest.mark.parametrize("problem,n,pick", [("poisson2d", 2048, 0), ("poisson2d", 2048, 1), ("poisson3d", 128, 0),
+                                            ("poisson2d", 2048, -1)])
+def test_ipc_ranks_transport_probe_arms(problem, n, pick):
+    """the transport probe at the first reset of a real 2-process solve on one GPU (IPC
+    all-reduce, peer-mapped buffers) runs the pulled and the exchanged arm, finds the pulled one bit for
+    bit the exchanged one, and keeps what it is told (or the faster: -1) on both ranks alike; the kept
+    transport then runs the solve, which matches one rank -- the choice is numerically neutral."""
+    p = _run([sys.executable, "-u", "bench/ipc_ranks.py", "--world", "2", "--problem", problem, "--n", str(n),
+              "--probe-pick", str(pick), "--iters", "40", "--port", str(_port())], timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["ok"] and line["gap_rnorm"] <= 1e-13, line
+    rk = line["ranks"]
+    assert all(r["probe_ran"] and r["probe_pull_bitwise"] and r["probe_pull_us"] > 0 and r["probe_xchg_us"] > 0
+               for r in rk), rk
+    assert len({r["halo_pull"] for r in rk}) == 1 and (pick < 0 or rk[0]["halo_pull"] == bool(pick)), rk
+    # the arms' times are the mean over the ranks: the same numbers on every rank
+    assert len({(r["probe_pull_us"], r["probe_xchg_us"]) for r in rk}) == 1, rk
+
+
 @pytest.mark.parametrize("problem,recurrence,pipe_rr", [("poisson2d", 2, 0), ("poisson2d", 2, 10), ("scrambled", 1, 0)])
 def test_ipc_ranks_single_buffer_exchanges(problem, recurrence, pipe_rr):
     """the copy-engine halo on buffers that are NOT parity-alternating -- the pipelined pass's w

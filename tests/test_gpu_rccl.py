@@ -131,6 +131,52 @@ def test_bench_matches_single_gpu_fixed_iterations(world):
 
 
 @needs2
+@pytest.mark.parametrize("world", WORLDS)
+def test_bench_default_transport_probed_and_matches_one_gpu(world):
+    """the default P > 1 path at a lean size, and which transport it took.  The
+    transport probe must have run on the real fabric, found the pulled run bit for bit the exchanged
+    one and the IPC all-reduce's sums RCCL's to rounding, and kept the faster of each (its choice is in
+    the JSON); the fixed-iteration residual matches one GPU.  With the probe off the verified pull
+    runs (the r5 default), with --halo-transport rccl the exchange: both match as well."""
+    args = ["--grid", "2048", "--steps", "60", "--warmup", "4", "--phases", "0", "--watchdog", "120"]
+    out = {}
+    for tag, extra in (("one", ["--gpus", "1"]), ("auto", ["--gpus", str(world)]),
+                       ("noprobe", ["--gpus", str(world), "--set", "transport_probe=0"]),
+                       ("rccl", ["--gpus", str(world), "--halo-transport", "rccl", "--allreduce", "rccl"])):
+        p = _run([sys.executable, "bench.py"] + extra + args)
+        assert p.returncode == 0, (tag, p.stdout + p.stderr)
+        out[tag] = json.loads(p.stdout.strip().splitlines()[-1])
+        assert out[tag]["check"]["ok"] and out[tag]["check"]["graph_fallbacks"] == 0, (tag, out[tag]["check"])
+    pr = out["auto"]["check"]["transport_probe"]
+    assert pr["pull_bitwise"] and pr["ipc_ar_close"] and not pr.get("ipc_ar_timeout"), pr
+    assert out["auto"]["check"]["halo_pull"] == pr["chosen"].startswith("pull")
+    assert out["auto"]["config"]["allreduce"].startswith("ipc") == pr["chosen"].endswith("ipc")
+    assert out["noprobe"]["check"]["halo_pull"] and "transport_probe" not in out["noprobe"]["check"]
+    assert out["noprobe"]["config"]["halo_transport"].startswith("in-kernel")
+    assert not out["rccl"]["check"]["halo_pull"]
+    r1 = out["one"]["check"]["rnorm"]
+    for tag in ("auto", "noprobe", "rccl"):
+        assert abs(out[tag]["check"]["rnorm"] - r1) <= 1e-12 * r1, (tag, out[tag]["check"]["rnorm"], r1)
+
+
+@needs2
+@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("problem", [["--problem", "poisson2d", "--n", "2048"], ["--problem", "poisson3d", "--n", "128"]])
+def test_native_cli_threads_default_path_reports_transport(mcg, world, problem):
+    """bin/mcg-cg --gpus P: each rank thread maps its neighbours' buffers (plain pointers, peer access)
+    and every rank's IPC mailbox; the probe's choice is reported and the solve matches one GPU."""
+    fixed = ["--fixed-iters", "40", "--report", "json", "--print-x", "no", "--watchdog", "120"]
+    one = json.loads(_run([mcg.cli_path()] + problem + fixed).stdout.splitlines()[-2])
+    p = _run([mcg.cli_path(), "--gpus", str(world)] + problem + fixed)
+    assert p.returncode == 0, p.stdout + p.stderr
+    rep = json.loads(p.stdout.splitlines()[-2])
+    pr = rep["transport_probe"]
+    assert pr is not None and pr["pull_bitwise"] and pr["ipc_ar_close"], rep
+    assert rep["halo_pull"] == pr["chosen"].startswith("pull") and rep["halo_transport"] in ("in-kernel", "rccl")
+    assert abs(rep["rnorm"] - one["rnorm"]) <= 1e-12 * one["rnorm"]
+
+
+@needs2
 @pytest.mark.parametrize("world", WORLDS[:1])
 def test_python_cli_processes(mcg, world):
     args = PROBLEMS["poisson2d"]
