@@ -39,7 +39,7 @@ HOST_OBJ  := $(patsubst csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC) $(GPU_CPP))
 CORE_OBJ  := $(HIP_OBJ) $(HOST_OBJ)
 HEADERS   := $(wildcard csrc/include/mcg/*.hpp) $(wildcard csrc/gpu/*.hpp)
 
-all: $(PYMOD) $(CLI) $(TESTBIN) $(BUILD)/streamop_capture
+all: $(PYMOD) $(CLI) $(TESTBIN) $(BUILD)/streamop_capture $(BUILD)/persist_probe
 
 $(BUILD)/%.o: csrc/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)
@@ -77,6 +77,11 @@ $(BUILD)/tests/test_host.o: tests/native/test_host.cpp $(HEADERS)
 $(BUILD)/streamop_capture: bench/streamop_capture.cpp
 	@mkdir -p $(BUILD)
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 $< -o $@
+
+# grid barrier between resident passes vs the kernel boundary (bench/)
+$(BUILD)/persist_probe: bench/persist_probe.hip
+	@mkdir -p $(BUILD)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 $< -o $@
 
 # host-only sanitizer build of the CPU reference path / partitioner / halo plan tests
 # (GPU sanitizers are not available on this pool: host code only)

@@ -344,6 +344,49 @@ def recipes(a) -> dict:
             ("b32768", 600, bench("--grid 32768 --steps 40 --warmup 4 --phases 0")),
             ("b1024", 600, bench("--problem poisson3d --grid 1024 --steps 40 --warmup 4 --phases 0")),
         ],
+        # the round-end set the driver runs (r5's tools/steps/r5final.txt): smoke, the three stencil
+        # headlines, config 5's share, the whole GPU suite
+        "roundend": [
+            ("smoke", 300, f"{PY} -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"),
+            ("bench", 300, bench()),
+            ("bench3", 300, bench("--problem poisson3d --grid 512")),
+            ("bench4k", 300, bench("--grid 4096 --steps 2000 --warmup 200")),
+            ("c5", 400, bench(f"{C5SCR} --phases 0 --steps 10 --warmup 3")),
+            ("suite", 1100, f"{PY} -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread"),
+        ],
+        # r6: the transport probe and both CLIs' P > 1 path, rehearsed on one GPU
+        "transport": [
+            ("pytest", 900, f"{PYTEST} -v tests/test_gpu_transport.py tests/test_gpu_peer.py"),
+            ("multirank", 900, f"{PYTEST} tests/test_gpu_multirank.py tests/test_gpu_user_matrix.py "
+                               f"-k 'in_kernel_halo or p3buf or lean_split'"),
+        ],
+        # r6: the system-scope release after a wave publishes a rank-end line, A/B on the P = 8 shares
+        # (the variant without it: make BUILD=exp_x/nofence/build EXTRA_HIPFLAGS=-DMCG_PULL_FENCE=0
+        # PYMOD=exp_x/nofence/cuda_mpi_parallel_amd/_C<ext> next to a copy of the package, run through
+        # exp_x/nofence/run_bench.py)
+        "fence_ab": [
+            (f"{tag}{pr}_{rep}", 200, f"{PY} -u {script} {args} {S8} --steps 2000 --warmup 200 --phases 0")
+            for rep in ("a", "b") for pr, args in (("2d", ""), ("3d", "--problem poisson3d --grid 512"))
+            for tag, script in (("fence", "bench.py"), ("nofence", "exp_x/nofence/run_bench.py"))
+        ],
+        # r6: the pulled ghost lines served from pinned host memory (PCIe, a slow
+        # remote) on the P = 8 shares, next to the local stand-in; NullComm and a 10 us all-reduce
+        "pull_proxy": [
+            (f"{src}{pr}{tag}", 200, bench(f"{args} {S8} --set pull_proxy={px} {dc} --steps 2000 --warmup 200 "
+                                           f"--phases 0"))
+            for pr, args in (("2d", ""), ("3d", "--problem poisson3d --grid 512"))
+            for src, px in (("host", 1), ("local", 0)) for tag, dc in (("", ""), ("_d10", "--delay-comm 10,0"))
+        ],
+        # r6: a grid barrier between resident passes against the kernel boundary
+        "persist": [("probe", 240, "build/persist_probe")],  # (make builds it)
+        # r6: the priced shares with the in-kernel halo forced on, and the kernel trace
+        # of the DelayComm overlap=1 anomaly (D = 10 us slower than 20 us)
+        "priced_pull": [(f"p16k_{w}", 300, f"{PY} bench/pipe_latency.py --grid 16384 --world {w} --rank {3 if w > 2 else 1} "
+                                           f"--recurrences 1 --graphs 1 --overlaps 0 --delays 0,10,20 --halo-pull 1 "
+                                           f"--iters 320") for w in (2, 4, 8)],
+        "anomaly": [("trace", 400, prof("anom", f"{PY} {ROOT}/bench/pipe_latency.py --grid 16384 --world 8 --rank 3 "
+                                                f"--delays 10,20 --recurrences 1 --graphs 1 --overlaps 1 --halo-us 10 "
+                                                f"--iters 320", fmt=""))],
     }
 
 

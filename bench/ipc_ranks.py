@@ -28,8 +28,10 @@ def _opts(C, a):
     # the transport probe (first reset) runs the pulled and the exchanged arm; which it keeps is pinned
     # here (by default the pull, as before the probe) so the test knows the path
     o.probe_pick_halo = a.probe_pick
+    o.transport_probe = a.transport_probe
     o.pipe_rr = a.pipe_rr
     o.use_graph = not a.no_graph
+    o.overlap = bool(a.overlap)
     o.watchdog_seconds = 60.0
     return o
 
@@ -99,6 +101,8 @@ def main() -> int:
     ap.add_argument("--probe-pick", type=int, default=1, help="transport probe: keep the pull (1) / exchange (0) / "
                                                               "the faster (-1)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--transport-probe", type=int, default=-1, help="0: no transport probe at the first reset")
+    ap.add_argument("--overlap", type=int, default=1, help="0: the halo in the pass's stream order (no halo_ahead)")
     ap.add_argument("--tol", type=float, default=1e-13, help="relative gap allowed against one rank")
     ap.add_argument("--port", type=int, default=29541)
     ap.add_argument("--timeout", type=float, default=180.0)

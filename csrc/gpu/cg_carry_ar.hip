@@ -770,10 +770,25 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     // P3: lines of this run take p_{k-2} (their r is recovered at use), others the stored r; the
     // pointer is chosen before the load (wave-uniform), the recovery selected after it arrives
     auto inrun = [&](int32_t j) { return !rfull && j >= 0 && j < n_run; };
+    // in-kernel halo (lean_split ranks: the generic runs that hold a rank-end line): a ghost line's
+    // p_{k-1} and Ap_{k-1} from the neighbour's rows, the rank's first / last line published
+    // write-through, as in the lean loops (PullBases)
+    PullBases pl;
+    pl.at(v, 0);
+    auto gside = [&](int32_t j) { return pl.side(l0 + (j < jmin ? jmin : (j > jmax ? jmax : j)), nl); };
     auto load_raw = [&](int32_t j, Raw& q) {
       const int32_t e = ebase(j) + lane;
       q.r = ld_once((inrun(j) ? (const double*)pn : ro) + e, ntl);
-      q.p = ld_once(po + e, ntl);
+      const int sd = gside(j);
+      q.p = sd != 0 ? ld_sys(pl.p[sd - 1] + e, 0u) : ld_once(po + e, ntl);
+    };
+    // a pulled ghost line's p_{k-1} kept in this rank's ghost rows: the next pass's p_{k-2} there (rghost)
+    auto keep_ghost_p = [&](int32_t j, const Raw& q) {
+      if (gside(j) != 0) const_cast<double*>(po)[ebase(j) + lane] = q.p;
+    };
+    auto ghost_ap = [&](int32_t j) {
+      const int sd = gside(j);
+      return sd != 0 ? ld_sys(pl.ap[sd - 1] + (ebase(j) + lane), 0u) : apx_o[ebase(j) + lane];
     };
     auto rof = [&](int32_t j, const Raw& q) { return inrun(j) ? fma(nbp, q.r, q.p) : q.r; };
     auto load_edge = [&](int32_t j, Edge& q) {
@@ -866,8 +881,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       const double t = stencil(cm1, rm1.p, edge_p(edm1), rm2.p, r0.p);
       pr_pk = fma(b, rm1.p, fma(na, t, rof(-1, rm1)));
     } else if (ghost(-1)) {
-      const double t = apx_o[ebase(-1) + lane];
+      const double t = ghost_ap(-1);
       pr_pk = fma(b, rm1.p, fma(na, t, rghost(-1, rm1)));
+      keep_ghost_p(-1, rm1);
     }
     double o_pold = r0.p, o_pm2 = r0.r, o_rk, o_pk;
     {
@@ -899,9 +915,10 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         rk1 = fma(na, t, rof(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
       } else if (ghost(m + 1)) {
-        const double t = apx_o[ebase(m + 1) + lane];
+        const double t = ghost_ap(m + 1);
         rk1 = fma(na, t, rghost(m + 1, rq[0]));
         pk1 = fma(b, rq[0].p, rk1);
+        keep_ghost_p(m + 1, rq[0]);
       }
       // 3. Ap_k of line m, stores, partials
       const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1);
@@ -920,9 +937,14 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         if (ren != nullptr && (lane == 0 || lane == 63)) ren[2 * s + (lane == 63 ? 1 : 0)] = o_rk;
       }
       if constexpr (PAIR) st_stream(&(x + i0 + m * LO)[lane], fma(a, o_pold, fma(ap, P3 ? o_pm2 : x0.pkm2, x0.xo)));
-      st_stream(&(pn + eb)[lane], o_pk);
+      const bool bnd = l0 + m == 0 || l0 + m == nl - 1;  // the halo's source lines
+      if (pl.pub && bnd) st_sys(pn + eb, (uint32_t)lane << 3, o_pk);
+      else st_stream(&(pn + eb)[lane], o_pk);
       if (lane == 0 || lane == 63) en[2 * s + (lane == 63 ? 1 : 0)] = sum;
-      if (apx_n != nullptr && (l0 + m == 0 || l0 + m == nl - 1)) apx_n[eb + lane] = sum;
+      if (apx_n != nullptr && bnd) {
+        if (pl.pub) st_sys(apx_n + eb, (uint32_t)lane << 3, sum);
+        else apx_n[eb + lane] = sum;
+      }
       s_pap = fma(o_pk, sum, s_pap);
       s_rap = fma(o_rk, sum, s_rap);
       s_apap = fma(sum, sum, s_apap);
@@ -959,6 +981,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       }
     }
     for (; m < n_run; ++m) step(m);
+    pl.release(l0, l1, nl);
     }  // !LEAN
   }
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);

@@ -814,7 +814,8 @@ void GpuCgSolver::probe_transport_() {
     Arm a;
     drop_graphs_();
     pull_ = pull;
-    comm_->use_alt_allreduce(alt);
+    // (only a probed alternative is switched: a rehearsal's IPC all-reduce is its first and only one)
+    if (ar_choice) comm_->use_alt_allreduce(alt);
     opt_.use_graph = graph0 && (pull || !use_halo_ || comm_->halo_capturable());
     reset_state_();
     run_iterations(2 + cyc);  // captures every graph the timed iterations replay
@@ -832,7 +833,7 @@ void GpuCgSolver::probe_transport_() {
     a.us = 1e3 * (double)ms / cyc;
     MCG_HIP(hipMemcpy(&a.st, st_.get(), sizeof(CgState), hipMemcpyDeviceToHost), "memcpy from device to host failed(state)");
     if (alt) a.timeout = comm_->alt_allreduce_timed_out();
-    comm_->use_alt_allreduce(false);
+    if (ar_choice) comm_->use_alt_allreduce(false);
     return a;
   };
   info_.probe_ran = true;
@@ -879,8 +880,8 @@ void GpuCgSolver::probe_transport_() {
   drop_graphs_();
   pull_ = pull;
   info_.halo_pull = pull_;
-  comm_->use_alt_allreduce(alt);
-  info_.alt_allreduce = alt;
+  if (ar_choice) comm_->use_alt_allreduce(alt);
+  info_.alt_allreduce = comm_->alt_allreduce_in_use();
   opt_.tol = tol0;
   opt_.rtol = rtol0;
   opt_.use_graph = graph0 && (pull_ || !use_halo_ || comm_->halo_capturable());

@@ -898,7 +898,8 @@ void GpuCgSolver::setup() {
   // does not write, and its pass k + 1 rewrites them only after this rank's pass k has contributed.
   // Every rank must take it (it decides the collectives of an iteration)
   {
-    const bool can = use_halo_ && ar_ && p3_ && lean_only_ && !lean_split_ && !L_.allgather && !pmat_ &&
+    // (lean_split ranks too: their generic launch pulls and publishes like the lean one, cg_carry_ar.hip)
+    const bool can = use_halo_ && ar_ && p3_ && (lean_only_ || lean_split_) && !L_.allgather && !pmat_ &&
                      opt_.recurrence == 1 && n > 0 && comm_ != nullptr &&
                      (comm_->maps_peers() || (opt_.form.halo_pull == 1 && !comm_->moves_data()));
     pull_ = opt_.form.halo_pull != 0 && can && (opt_.form.halo_pull == 1 || comm_->maps_peers());

@@ -304,22 +304,27 @@ def test_lean_split_mixed_ranks_match_one_rank(mcg, world, lines):
     p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
     C = mcg.native()
 
-    def run(w, ls, overlap=True):
+    def run(w, ls, overlap=True, hp=-1):
         o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
         o.lean_split = ls
         o.overlap = overlap
+        o.halo_pull = hp
         return C.run_local_ranks(p.native(), o, w, 40, True)
 
     one = run(1, 0)
     r1 = one["ranks"][0]["rnorm"]
-    for ls, ov in ((1, True), (1, False), (0, True)):
-        out = run(world, ls, ov)
+    # r6: the split ranks read their ghost lines in-kernel too (halo_pull 1: the
+    # generic launch's runs pull and publish their rank-end lines like the lean launch's)
+    for ls, ov, hp in ((1, True, -1), (1, False, -1), (0, True, -1), (1, False, 1), (1, False, 0)):
+        out = run(world, ls, ov, hp)
         split = [rk["lean_split"] > 0 for rk in out["ranks"]]
         if ls == 1:
             assert any(split) and not all(split), split  # split ranks next to lean-only ones
             assert all(rk["lean_only"] for rk, sp_ in zip(out["ranks"], split) if not sp_)
+        if hp >= 0:
+            assert all(rk["halo_pull"] == (hp == 1) for rk in out["ranks"]), out["ranks"]
         rp = out["ranks"][0]["rnorm"]
-        assert abs(rp - r1) <= 1e-13 * r1, (ls, ov, rp, r1)
+        assert abs(rp - r1) <= 1e-13 * r1, (ls, ov, hp, rp, r1)
         np.testing.assert_allclose(out["x"], one["x"], rtol=1e-11, atol=1e-13 * np.abs(one["x"]).max())
 
 
