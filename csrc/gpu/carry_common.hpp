@@ -129,14 +129,20 @@ __device__ __forceinline__ void st_sys(double* base, uint32_t bo, double v) {
   g_u64* p = (g_u64*)((g_char*)(g_double*)base + bo);
   __hip_atomic_store(p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// MCG_PULL_FENCE: how a publishing wave ends its run.  1 (default): it waits for its stores
+// (s_waitcnt vmcnt(0)) -- they are write-through, so acknowledged means in the memory the
+// neighbours read; 2: a full system-scope release fence (buffer_wbl2 sc0 sc1 + the wait), which also
+// writes back every dirty line of the XCD's L2 -- measured 29-30 % slower on the P = 8 shares
+// (16384^2: 3432-3437 vs 4634-4869 it/s, 512^3: 5040-5124 vs 7169-7241, profiles/r6/fence/); 0: nothing
 #ifndef MCG_PULL_FENCE
 #define MCG_PULL_FENCE 1
 #endif
 // The in-kernel halo's memory-model argument.  Rank B's pass k stores its first / last line (p_k,
 // Ap_k) with relaxed system-scope stores (st_sys: sc0 sc1, written through past B's L2 to its HBM),
-// and the wave that stored them ends its run with a system-scope release (release(): the stores are
-// complete -- acknowledged by the memory that serves remote readers -- before anything the wave does
-// later, its end included).  B's kernel end precedes B's all-reduce of pass k in stream order; rank
+// and the wave that stored them ends its run waiting for them (release(): the stores are complete --
+// acknowledged by the memory that serves remote readers -- before anything the wave does later, its
+// end included; a system-scope release fence would add only the write-back of the L2's OTHER dirty
+// lines, which no neighbour reads, and costs 29 % of the pass).  B's kernel end precedes B's all-reduce of pass k in stream order; rank
 // A's pass k + 1 follows A's all-reduce of pass k, which cannot complete before B contributed
 // (RCCL: the data dependence of the sum; the IPC all-reduce: B's flag, stored after its own release).
 // So A's pass k + 1, whose system-scope loads (ld_sys: past A's caches, over xGMI) read B's lines of
@@ -171,10 +177,12 @@ struct PullBases {
     else if (nt) g_st_nt(base, o, v);
     else g_st(base, o, v);
   }
-  // the end of a run [l0, l1) that published the rank's first / last line: a system-scope release (the
-  // argument above); one per publishing wave
+  // the end of a run [l0, l1) that published the rank's first / last line (the argument above); one
+  // per publishing wave
   __device__ __forceinline__ void release(int64_t l0, int64_t l1, int64_t nl) const {
-    if constexpr (MCG_PULL_FENCE) {
+    if constexpr (MCG_PULL_FENCE == 1) {
+      if (pub && (l0 == 0 || l1 == nl)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (MCG_PULL_FENCE == 2) {
       if (pub && (l0 == 0 || l1 == nl)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
   }

@@ -129,24 +129,27 @@ __device__ __forceinline__ void tile_batch_load(const TilesDev& T, int64_t k, in
 // TU: entries per lane in flight, 8 or 10 (TilesDev::tu; software-pipelined: the next batch's indices and
 // values load while this batch gathers).  The order of the adds is the same for either (ascending entry
 // index), so the results are too.
-template <int MODE, int PART = 0, int ABL = 0, int TU = 10>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
+// W: waves per workgroup -- 4 (four workgroups per CU, the default) or 16 (one per CU: the pacing
+// step's barrier then holds waves of one age, so no CU has a youngest workgroup to fall behind;
+// PassForm::tile_waves, an experiment: profiles/r6/c5)
+template <int MODE, int PART = 0, int ABL = 0, int TU = 10, int W = 4>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_tiles(TilesDev T, const double* __restrict__ p, const double* __restrict__ r,
                                                double* __restrict__ Ap, int64_t own, double* __restrict__ partials,
                                                int pstride, CgState* st, double tol, int first, int check, RedCtl rc) {
   constexpr int TB = kTileB;
-  __shared__ double acc[4][TB];
+  __shared__ double acc[W][TB];
   __shared__ int s_behind;
   int live = 0;  // thread 0's (the only one that paces)
   if constexpr (MODE == 0) {
     const F1Scalars sc = f1_scalars(st, tol, first, check);
     if (st->done || sc.conv) {  // uniform over the grid: every workgroup leaves, no pacing
-      if constexpr (PART != 1) f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
+      if constexpr (PART != 1) f1_finish<W>(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
       return;
     }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
-  const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t nwaves = (int64_t)gridDim.x * W;
+  const int64_t wave = (int64_t)blockIdx.x * W + wv;
   const int64_t rounds = (T.nblocks + nwaves - 1) / nwaves;
   const int G = T.G;
   // the segments this launch sweeps, in order: seg(0 .. ns - 1)
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       g_tile_diag[2 * kTileDiagMax + blockIdx.x] = ((unsigned long long)xcc << 32) | hw;
     }
   }
-  if constexpr (MODE == 0 && PART != 1) f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+  if constexpr (MODE == 0 && PART != 1) f1_finish<W>(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
 }
 
 // ---- setup: count / fill one row block per 64-thread workgroup (LDS counters per segment) ----
@@ -318,12 +321,15 @@ TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
   return t;
 }
 
-int tiles_grid(int ncu) {
+int tiles_grid(int ncu, int ww) {
+  MCG_CHECK(ww == 4 || ww == 16, "tiles: 4 or 16 waves per workgroup");
   int per_cu = 0;
-  const void* f = reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10>);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  const void* f = ww == 16 ? reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10, 16>)
+                           : reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, ww * 64, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   (void)hipGetLastError();
-  return std::min(per_cu, 4) * std::max(1, ncu);  // every workgroup resident on the solver's CUs (pacing waits on them)
+  // every workgroup resident on the solver's CUs (pacing waits on them): 16 waves per CU either way
+  return std::min(per_cu, 16 / ww) * std::max(1, ncu);
 }
 
 namespace {
@@ -363,10 +369,17 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(part == 0 || (T.g_lo >= 0 && T.g_lo <= T.g_hi && T.g_hi <= T.G), "tiles: bad own-segment range");
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
   MCG_CHECK(T.tb == kTileB && (T.tu == 8 || T.tu == 10), "tiles: 1024 rows per block, 8 or 10 entries per lane");
+  MCG_CHECK(T.ww == 4 || T.ww == 16, "tiles: 4 or 16 waves per workgroup");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
 #define MCG_TL(PART, ABL, TU)                                                                                          \
-  hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off, partials, \
-                     pstride, st, tol, first, check, rc)
+  do {                                                                                                                 \
+    if (T.ww == 16 && ABL == 0)                                                                                        \
+      hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU, 16>), dim3(grid), dim3(1024), 0, stream, T, p_ext, r, Ap, own_off,  \
+                         partials, pstride, st, tol, first, check, rc);                                               \
+    else                                                                                                               \
+      hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off,      \
+                         partials, pstride, st, tol, first, check, rc);                                               \
+  } while (0)
   static const int ablate = [] {
     const char* e = std::getenv("MCG_TILES_ABLATE");
     return e ? std::atoi(e) : 0;
@@ -399,8 +412,14 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
     return e ? std::atoi(e) : 0;
   }();
 #define MCG_T1(ABL, TU)                                                                                                \
-  hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, 0,  \
-                     nullptr, 0.0, 0, 0, RedCtl())
+  do {                                                                                                                 \
+    if (T.ww == 16 && ABL == 0)                                                                                        \
+      hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU, 16>), dim3(grid), dim3(1024), 0, stream, T, x_ext, nullptr, y, 0,      \
+                         nullptr, 0, nullptr, 0.0, 0, 0, RedCtl());                                                   \
+    else                                                                                                               \
+      hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, \
+                         0, nullptr, 0.0, 0, 0, RedCtl());                                                            \
+  } while (0)
   if (ablate == 1) MCG_T1(1, 10);
   else if (ablate == 2) MCG_T1(2, 10);
   else if (ablate == 3) MCG_T1(3, 10);

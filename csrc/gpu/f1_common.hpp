@@ -40,9 +40,10 @@ __device__ __forceinline__ double ld_wt(const double* p) {
 
 // four fixed-order block partials -> partials[q * pstride + blockIdx.x] (write-through when an
 // in-kernel reduction reads them)
+template <int NW = kWaves>  // waves per block (the tiles' 16-wave workgroups: 16)
 __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, double a3, double* __restrict__ out,
                                                int pstride, bool wt = false) {
-  __shared__ double sh[4][kWaves];
+  __shared__ double sh[4][NW];
   a0 = eng::wave_sum(a0);
   a1 = eng::wave_sum(a1);
   a2 = eng::wave_sum(a2);
@@ -58,7 +59,7 @@ __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, 
   if (threadIdx.x < 4) {
     double s = 0.0;
 #pragma unroll
-    for (int k = 0; k < kWaves; ++k) s += sh[threadIdx.x][k];
+    for (int k = 0; k < NW; ++k) s += sh[threadIdx.x][k];
     if (wt) st_wt(&out[threadIdx.x * pstride + blockIdx.x], s);
     else out[threadIdx.x * pstride + blockIdx.x] = s;
   }
@@ -162,9 +163,10 @@ __device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc,
 }
 
 // end of a fused pass: block partials, then (rc on) the in-kernel reduction
+template <int NW = kWaves>
 __device__ __forceinline__ void f1_finish(double a0, double a1, double a2, double a3, double* __restrict__ out,
                                           int pstride, const RedCtl& rc, CgState* st, double tol) {
-  block_partial4(a0, a1, a2, a3, out, pstride, rc.ngroups > 0);
+  block_partial4<NW>(a0, a1, a2, a3, out, pstride, rc.ngroups > 0);
   if (rc.ngroups > 0) f1_reduce_tail(out, pstride, rc, st, tol);
 }
 

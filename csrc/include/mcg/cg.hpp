@@ -52,6 +52,8 @@ struct PassForm {
                              // 19.3-19.5 / 17.5 it/s, profiles/r4/c5; r3's counter pacing peaked at 19: 14.0)
                              // (r5 pruned the tile variants that measured slower: 960-row blocks, 12 entries per
                              // lane, fp32 values, prefetch, the other pacing modes -- cg_tiles.hip header)
+  int tile_waves = -1;       // tiles: waves per workgroup, 4 (four workgroups per CU) or 16 (one per CU, so the
+                             // pacing barrier holds waves of one age); -1 = auto (4)
   int fused_reduce = -1;     // single-reduction form: sum the pass's block partials inside the pass (last-arriver
                              // fan-in, kernels.hpp RedCtl) instead of a separate single-block reduce launch, so an
                              // iteration is one kernel (+ the all-reduce); -1 = auto (on), 0 = off

@@ -428,6 +428,7 @@ struct TilesDev {
   int64_t ext_len = 0;       // length of p (the last segment may be short)
   int g_lo = 0, g_hi = 0;    // the segments inside this rank's own block of p (all-gather overlap, part 1 / 2)
   int tu = 10;               // entries per lane in flight, 8 or 10 (tiles_tu)
+  int ww = 4;                // waves per workgroup: 4 (four workgroups per CU) or 16 (one per CU; PassForm::tile_waves)
 };
 // entries per lane in flight for tiles of mean size m: 8 or 10, whichever fills the batches of 64 x TU
 // entries better (config 5's ~1790-entry tiles: 3 batches of 640 rather than 4 of 512; the 201 GB
@@ -440,7 +441,8 @@ inline int tiles_tu(double m) {
   return fill(10) > fill(8) ? 10 : 8;
 }
 TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift);
-int tiles_grid(int ncu);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every workgroup)
+int tiles_grid(int ncu, int ww = 4);  // workgroups of the SpMV on ncu CUs: the resident count (pacing waits on every
+                                      // workgroup); ww = waves per workgroup (4 or 16)
 // count (fill = false: tptr[b * G + g + 1] = tile sizes; scan them, tptr[0] = 0) then fill
 struct TilesOut {
   int64_t* tptr = nullptr;

@@ -228,6 +228,7 @@ class GpuCgSolver {
   bool c8_ = false;
   // L2-segment COO tiles (cg_tiles.hip): tile pointers, packed (row, column) indices, values, pacing
   bool tiles_ = false;
+  int tile_ww_ = 4;  // PassForm::tile_waves in effect
   kern::TilesGeometry tgeo_;
   DeviceBuffer<int64_t> tptr_;
   DeviceBuffer<uint32_t> tidx_;
@@ -250,6 +251,7 @@ class GpuCgSolver {
     t.g_hi = tg_hi_;
     const double ntiles = (double)tgeo_.nblocks * (double)tgeo_.G;
     t.tu = kern::tiles_tu(ntiles > 0 ? (double)tidx_.size() / ntiles : 0.0);
+    t.ww = tile_ww_;
     if (const char* e = std::getenv("MCG_TILES_TU")) t.tu = std::atoi(e) == 8 ? 8 : 10;  // test override
     return t;
   }

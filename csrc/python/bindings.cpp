@@ -215,6 +215,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_FORM_PROP(fused_reduce)
       MCG_FORM_PROP(tiles)
       MCG_FORM_PROP(tile_seg_log2)
+      MCG_FORM_PROP(tile_waves)
       MCG_FORM_PROP(carry_vc)
       MCG_FORM_PROP(lean_split)
       MCG_FORM_PROP(halo_pull)
