@@ -171,7 +171,8 @@ def test_native_cli_threads_default_path_reports_transport(mcg, world, problem):
     assert p.returncode == 0, p.stdout + p.stderr
     rep = json.loads(p.stdout.splitlines()[-2])
     pr = rep["transport_probe"]
-    assert pr is not None and pr["pull_bitwise"] and pr["ipc_ar_close"], rep
+    # (the halo arms run where every rank's pass is the lean carry: not on 16-plane ranks of 128^3 at P = 8)
+    assert pr is not None and (pr["pull_us"] == 0 or pr["pull_bitwise"]) and pr["ipc_ar_close"], rep
     assert rep["halo_pull"] == pr["chosen"].startswith("pull") and rep["halo_transport"] in ("in-kernel", "rccl")
     assert abs(rep["rnorm"] - one["rnorm"]) <= 1e-12 * one["rnorm"]
 
