@@ -792,7 +792,9 @@ bool states_close(const CgState& a, const CgState& b, double rel) {
 // and the SpMV's read of the neighbours' p, :288, which these transports carry.
 void GpuCgSolver::probe_transport_() {
   info_.alt_allreduce = use_comm_ && comm_->alt_allreduce_in_use();
-  if (!use_comm_ || world_ < 2 || !comm_->moves_data() || opt_.transport_probe == 0 || opt_.hooks.inject_nan_at >= 0)
+  // (not with a fault-injection hook armed: its iteration count refers to the real run)
+  if (!use_comm_ || world_ < 2 || !comm_->moves_data() || opt_.transport_probe == 0 || opt_.hooks.inject_nan_at >= 0 ||
+      opt_.hooks.fail_graph_launch_at >= 0)
     return;
   const bool halo_choice = pull_ && opt_.form.halo_pull == -1;  // (pull_ is agreed: the same on every rank)
   // the alternative all-reduce only if every rank mapped every mailbox (a rank whose mapping failed
