@@ -78,14 +78,15 @@ def test_ipc_ranks_real_recurrence_matches_one_rank(world, problem, n, pull, coe
     assert line["gap_rnorm"] <= 1e-13 and line["true_gap"] <= 1e-8, line
 
 
-@pytest.mark.parametrize("problem,n,pick", [("poisson2d", 2048, 0), ("poisson2d", 2048, 1), ("poisson3d", 128, 0),
-                                            ("poisson2d", 2048, -1)])
-def test_ipc_ranks_transport_probe_arms(problem, n, pick):
+@pytest.mark.parametrize("world,problem,n,pick", [(2, "poisson2d", 2048, 0), (2, "poisson2d", 2048, 1),
+                                                  (2, "poisson3d", 128, 0), (2, "poisson2d", 2048, -1),
+                                                  (8, "poisson2d", 2048, -1)])
+def test_ipc_ranks_transport_probe_arms(world, problem, n, pick):
     """the transport probe at the first reset of a real 2-process solve on one GPU (IPC
     all-reduce, peer-mapped buffers) runs the pulled and the exchanged arm, finds the pulled one bit for
     bit the exchanged one, and keeps what it is told (or the faster: -1) on both ranks alike; the kept
     transport then runs the solve, which matches one rank -- the choice is numerically neutral."""
-    p = _run([sys.executable, "-u", "bench/ipc_ranks.py", "--world", "2", "--problem", problem, "--n", str(n),
+    p = _run([sys.executable, "-u", "bench/ipc_ranks.py", "--world", str(world), "--problem", problem, "--n", str(n),
               "--probe-pick", str(pick), "--iters", "40", "--port", str(_port())], timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])

@@ -34,13 +34,17 @@ def _report(p):
 FIXED = ["--fixed-iters", "40", "--report", "json", "--print-x", "no", "--watchdog", "120"]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("problem", [["--problem", "poisson2d", "--n", "2048"], ["--problem", "poisson3d", "--n", "128"]])
 def test_native_cli_rehearsed_ranks_pull_and_match_one_rank(mcg, world, problem):
     one = _report(_run([mcg.cli_path()] + problem + FIXED))
     rep = _report(_run([mcg.cli_path(), "--gpus", str(world), "--rehearse-ranks"] + problem + FIXED))
     assert rep["ranks"] == world and rep["rehearse_ranks"]
     pr = rep["transport_probe"]
+    if pr is None:  # the pull was no candidate (a 3-D rank of 16 planes may be too short for the lean runs)
+        assert problem[1] == "poisson3d" and world == 8 and not rep["halo_pull"], rep
+        assert abs(rep["rnorm"] - one["rnorm"]) <= 1e-13 * one["rnorm"]
+        return
     # the probe ran both halo arms on the mapped buffers and the pulled run reproduced the exchanged one
     assert pr is not None and pr["pull_bitwise"] and pr["pull_us"] > 0 and pr["rccl_halo_us"] > 0, rep
     assert rep["halo_pull"] == (pr["pull_us"] <= pr["rccl_halo_us"]) == pr["chosen"].startswith("pull"), rep
