@@ -80,7 +80,7 @@ def test_ipc_ranks_real_recurrence_matches_one_rank(world, problem, n, pull, coe
 
 @pytest.mark.parametrize("world,problem,n,pick", [(2, "poisson2d", 2048, 0), (2, "poisson2d", 2048, 1),
                                                   (2, "poisson3d", 128, 0), (2, "poisson2d", 2048, -1),
-                                                  (8, "poisson2d", 2048, -1)])
+                                                  (8, "poisson2d", 4096, -1)])
 def test_ipc_ranks_transport_probe_arms(world, problem, n, pick):
     """the transport probe at the first reset of a real 2-process solve on one GPU (IPC
     all-reduce, peer-mapped buffers) runs the pulled and the exchanged arm, finds the pulled one bit for

@@ -133,12 +133,14 @@ def test_bench_matches_single_gpu_fixed_iterations(world):
 @needs2
 @pytest.mark.parametrize("world", WORLDS)
 def test_bench_default_transport_probed_and_matches_one_gpu(world):
-    """the default P > 1 path at a lean size, and which transport it took.  The
-    transport probe must have run on the real fabric, found the pulled run bit for bit the exchanged
-    one and the IPC all-reduce's sums RCCL's to rounding, and kept the faster of each (its choice is in
-    the JSON); the fixed-iteration residual matches one GPU.  With the probe off the verified pull
-    runs (the r5 default), with --halo-transport rccl the exchange: both match as well."""
-    args = ["--grid", "2048", "--steps", "60", "--warmup", "4", "--phases", "0", "--watchdog", "120"]
+    """the default P > 1 path at a lean size (4096^2: 512 lines a rank at P = 8),
+    and which transport it took.  The transport probe must have run on the real fabric, found the
+    pulled run bit for bit the exchanged one and the IPC all-reduce's sums RCCL's to rounding, and kept
+    the faster of each (its choice is in the JSON); the fixed-iteration residual matches one GPU.  With
+    the probe off the verified pull runs (the r5 default), with --halo-transport rccl the exchange: both
+    match as well."""
+    # 4096^2: 512 lines a rank at P = 8, long enough runs for the lean carry (and so for the pull)
+    args = ["--grid", "4096", "--steps", "60", "--warmup", "4", "--phases", "0", "--watchdog", "120"]
     out = {}
     for tag, extra in (("one", ["--gpus", "1"]), ("auto", ["--gpus", str(world)]),
                        ("noprobe", ["--gpus", str(world), "--set", "transport_probe=0"]),
@@ -161,7 +163,7 @@ def test_bench_default_transport_probed_and_matches_one_gpu(world):
 
 @needs2
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("problem", [["--problem", "poisson2d", "--n", "2048"], ["--problem", "poisson3d", "--n", "128"]])
+@pytest.mark.parametrize("problem", [["--problem", "poisson2d", "--n", "4096"], ["--problem", "poisson3d", "--n", "128"]])
 def test_native_cli_threads_default_path_reports_transport(mcg, world, problem):
     """bin/mcg-cg --gpus P: each rank thread maps its neighbours' buffers (plain pointers, peer access)
     and every rank's IPC mailbox; the probe's choice is reported and the solve matches one GPU."""
