@@ -865,11 +865,12 @@ void GpuCgSolver::probe_transport_() {
   }
   bool alt = false;
   if (ar_choice) {
-    comm_->set_alt_allreduce_budget(10.0);
+    const double budget0 = comm_->alt_allreduce_budget();
+    comm_->set_alt_allreduce_budget(std::min(budget0, 10.0));
     const Arm a = run_arm(pull, true);
     double v[3] = {a.us, a.timeout ? 1.0 : 0.0, states_close(a.st, best.st, 1e-6) ? 0.0 : 1.0};
     allreduce_host_(v, 3);
-    comm_->set_alt_allreduce_budget(120.0);
+    comm_->set_alt_allreduce_budget(budget0);
     info_.probe_alt_us = v[0] / world_;
     info_.probe_alt_timeout = v[1] != 0.0;
     info_.probe_alt_close = v[1] == 0.0 && v[2] == 0.0;

@@ -134,6 +134,7 @@ class Communicator {
   virtual bool alt_allreduce_in_use() const { return false; }
   virtual bool alt_allreduce_timed_out() { return false; }
   virtual void set_alt_allreduce_budget(double) {}
+  virtual double alt_allreduce_budget() const { return 0.0; }
 };
 
 class Comm final : public Communicator {
@@ -280,6 +281,7 @@ class PeerHaloComm final : public Communicator {
   bool alt_allreduce_in_use() const override { return ipc_ar_; }
   bool alt_allreduce_timed_out() override;
   void set_alt_allreduce_budget(double s) override { ar_budget_seconds = s; }
+  double alt_allreduce_budget() const override { return ar_budget_seconds; }
 
  private:
   std::shared_ptr<Communicator> inner_;
