@@ -314,6 +314,30 @@ def recipes(a) -> dict:
                  + counters("f_16384_dram", "k_cg_carry_ar", "--steps 8 --warmup 2")
                  + counters("f_4096_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8")
                  + counters("f_512c_dram", "k_cg_carry_ar3", "--problem poisson3d --grid 512 --steps 8 --warmup 2"),
+        # r6: the 2-D carries read one 128-B line per slice and pass above the byte model -- the slice-edge
+        # rows of neighbouring columns held by other workgroups?  A/B against the diagnostic build whose
+        # workgroups' waves take columns SS / 4 apart (every edge between workgroups): var/colx, built with
+        # cp -r cuda_mpi_parallel_amd var/colx/ (minus _C*.so); make BUILD=var/colx/build
+        # EXTRA_HIPFLAGS=-DMCG_COLMAP_SPREAD PYMOD=var/colx/cuda_mpi_parallel_amd/_C<ext> <that PYMOD>, and a
+        # var/colx/run_bench.py that puts var/colx first on sys.path and runs bench.py (profiles/r6/colmap)
+        "colmap": [
+            ("base", 300, bench("--phases 0 --steps 200 --warmup 20")),
+            ("spread", 300, f"{PY} var/colx/run_bench.py --phases 0 --steps 200 --warmup 20"),
+        ] + counters("base_dram", "k_cg_carry_ar", "--steps 8 --warmup 2") + [
+            ("spread_dram", 300, prof("spread_dram", f"{PY} {ROOT}/var/colx/run_bench.py --phases 0 --no-verify --steps 8 "
+                                                     f"--warmup 2", dram)),
+            ("spread_dram_txt", 60, f"{PY} bench/pmc_csv.py {OUT}/spread_dram k_cg_carry_ar"),
+        ] + counters("base4k_dram", "k_cg_carry_ar", "--grid 4096 --steps 64 --warmup 8"),
+        # r6: wider workgroups for the packed-edge three-buffer kernels (PassForm::lean_waves), bitwise test
+        # then interleaved A/B at 16384^2 / 8192^2 / 4096^2 and the DRAM counters of the widest
+        "leanww": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_solver.py -k 'lean_waves or p3buf_bitwise'"),
+        ] + [
+            (f"w{ww}_{g}_{rep}", 200, bench(f"--grid {g} --phases 0 --set lean_waves={ww} "
+                                            + ("--steps 2000 --warmup 200" if g == 4096 else "--steps 300 --warmup 30")))
+            for rep in ("a", "b") for g in (16384, 8192, 4096) for ww in (4, 8, 16)
+        ] + counters("w16_dram", "k_cg_carry_ar", "--steps 8 --warmup 2 --set lean_waves=16")
+          + counters("w8_dram", "k_cg_carry_ar", "--steps 8 --warmup 2 --set lean_waves=8"),
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),

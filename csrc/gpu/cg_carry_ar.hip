@@ -105,7 +105,15 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;  // XCD-aware (k_cg_f1_carry)
   const int64_t nw = nb * kWaves;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t gw = lb * kWaves + wv;
+  int64_t gw = lb * kWaves + wv;
+#if defined(MCG_COLMAP_SPREAD)
+  // diagnostic build (profiles/r6/colmap): a block's waves take columns SS / kWaves apart, so every slice
+  // edge lies between two blocks (the default: a block's waves take kWaves adjacent columns)
+  if (SS % kWaves == 0 && gw < (nw / SS) * SS) {
+    const int64_t w = gw % SS, q = w / kWaves, u = w % kWaves;
+    gw = gw - w + u * (SS / kWaves) + q;
+  }
+#endif
   int64_t runs, chunk;
   const int64_t njobs = carry_jobs(nw, SS, nl, runs, chunk);
   const int32_t ext32 = (int32_t)v.ext_len;
