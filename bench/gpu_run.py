@@ -338,6 +338,26 @@ def recipes(a) -> dict:
             for rep in ("a", "b") for g in (16384, 8192, 4096) for ww in (4, 8, 16)
         ] + counters("w16_dram", "k_cg_carry_ar", "--steps 8 --warmup 2 --set lean_waves=16")
           + counters("w8_dram", "k_cg_carry_ar", "--steps 8 --warmup 2 --set lean_waves=8"),
+        # r6: per-wave timing of one even and one odd 2-D pass (var/diag: the build with -DMCG_CARRY_DIAG,
+        # made like var/colx above), eager; bench/wave_spread.py summarises
+        "wavediag": [
+            (f"d{g}", 300, f"env MCG_CARRY_DIAG_FILE={OUT}/diag{g} MCG_CARRY_DIAG_AT={at} {PY} var/diag/run_bench.py "
+                           f"--grid {g} --no-graph --phases 0 --steps {st} --warmup 20")
+            for g, at, st in ((4096, 1500, 2000), (16384, 300, 400))
+        ],
+        # r6: issue priority by a workgroup's arrival rank on its CU (var/ageprio: -DMCG_CARRY_AGEPRIO from
+        # profiles/r6/waves/ageprio_and_diag.patch, reverted), A/B interleaved, and the per-wave timings with
+        # it (var/agediag) next to the default's (var/diag: -DMCG_CARRY_DIAG, in the tree)
+        "ageprio": [
+            (f"{tag}_{g}_{rep}", 200, f"{PY} {script} --grid {g} --phases 0 "
+                                      + ("--steps 2000 --warmup 200" if g == 4096 else "--steps 300 --warmup 30"))
+            for rep in ("a", "b") for g in (16384, 8192, 4096)
+            for tag, script in (("base", "bench.py"), ("prio", "var/ageprio/run_bench.py"))
+        ] + [
+            (f"{tag}{g}", 300, f"env MCG_CARRY_DIAG_FILE={OUT}/{tag}{g} MCG_CARRY_DIAG_AT={at} {PY} var/{tag}/run_bench.py "
+                               f"--grid {g} --no-graph --phases 0 --steps {st} --warmup 20")
+            for tag in ("diag", "agediag") for g, at, st in ((4096, 1500, 2000), (16384, 300, 400))
+        ],
         # r4: variable-coefficient stencils on the line carry (SELL-64/diav)
         "vc": [
             ("pytest", 600, f"{PY} -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_varcoef.py"),

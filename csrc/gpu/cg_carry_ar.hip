@@ -30,7 +30,9 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -60,6 +62,13 @@ namespace {
 // compact edge arrays: no edge-array loads or stores at all (bench/carry_depth.hip: the pattern with
 // the edge stores 77 us at 4096^2, with neighbour-row loads instead 58; profiles/r5/depth).  The diav
 // loop (CM 5) recovers r the same way but still stores and reads its edge rows' Ap (per-row values)
+#if defined(MCG_CARRY_DIAG)
+// diagnostic build (profiles/r6/waves): per wave of one launch -- entry, end of its jobs, end of the
+// reduction (wall clock, 100 MHz) and where it ran (XCC_ID << 32 | HW_ID)
+constexpr int kCarryDiagMax = 8192;
+__device__ unsigned long long g_carry_diag[4 * kCarryDiagMax];
+#endif
+
 template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false,
           bool T3 = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
@@ -67,6 +76,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
                                                      double tol, int first, int check, RedCtl rc) {
   __shared__ double2 s_dict[CM >= 4 ? 1 : 256];
   __shared__ double s_val[16];  // dia4 values
+#if defined(MCG_CARRY_DIAG)
+  const unsigned long long t_in = wall_clock64();
+#endif
   const F1Scalars sc = f1_scalars(st, tol, first, check);
   if (st->done || sc.conv) {
     f1_finish(0.0, 0.0, 0.0, 0.0, partials, pstride, rc, st, tol);
@@ -992,7 +1004,20 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     pl.release(l0, l1, nl);
     }  // !LEAN
   }
+#if defined(MCG_CARRY_DIAG)
+  const unsigned long long t_work = wall_clock64();
+#endif
   f1_finish(s_pap, s_rap, s_apap, s_rr, partials, pstride, rc, st, tol);
+#if defined(MCG_CARRY_DIAG)
+  const int64_t dw = blk * kWaves + (threadIdx.x >> 6);
+  if (lane == 0 && dw < kCarryDiagMax) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    g_carry_diag[4 * dw] = t_in;
+    g_carry_diag[4 * dw + 1] = t_work;
+    g_carry_diag[4 * dw + 2] = wall_clock64();
+    g_carry_diag[4 * dw + 3] = ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 
@@ -1032,6 +1057,32 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
   }
   const bool pair = (k & 1) != 0;
   const bool big = v.ext_len >= ((int64_t)1 << 29);  // lean kernels: per-run 64-bit bases
+#if defined(MCG_CARRY_DIAG)
+  // diagnostic build: after the launches numbered MCG_CARRY_DIAG_AT and the next one (eager runs), the
+  // per-wave records into MCG_CARRY_DIAG_FILE.<launch>
+  struct DiagDump {
+    hipStream_t s;
+    int grid;
+    ~DiagDump() {
+      static int launch = 0;
+      static const int at = std::getenv("MCG_CARRY_DIAG_AT") ? std::atoi(std::getenv("MCG_CARRY_DIAG_AT")) : -1;
+      const char* fn = std::getenv("MCG_CARRY_DIAG_FILE");
+      const int me = launch++;
+      if (fn == nullptr || at < 0 || (me != at && me != at + 1)) return;
+      std::vector<unsigned long long> d(4 * kCarryDiagMax);
+      if (hipStreamSynchronize(s) != hipSuccess) return;
+      if (hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_carry_diag), d.size() * sizeof(unsigned long long)) != hipSuccess) return;
+      const std::string path = std::string(fn) + "." + std::to_string(me);
+      if (FILE* fo = std::fopen(path.c_str(), "w")) {
+        const int nw = std::min(grid * kWaves, kCarryDiagMax);
+        for (int w = 0; w < nw; ++w)
+          std::fprintf(fo, "%d %d %llu %llu %llu %u %u\n", w / kWaves, w % kWaves, d[4 * w], d[4 * w + 1], d[4 * w + 2],
+                       (unsigned)(d[4 * w + 3] & 0xffffffffu), (unsigned)(d[4 * w + 3] >> 32));
+        std::fclose(fo);
+      }
+    }
+  } diag_dump{stream, grid};
+#endif
   MCG_CHECK(v.ext_len < ((int64_t)1 << 31), "Ap-recomputing carry: a rank's vectors must stay below 2^31 rows");
   if (cm == 4 && p3k && lean && S.dpat != nullptr) {  // lean-only kernels (4 waves per SIMD)
     const bool t3 = v.p_m2 != nullptr;  // three p buffers (kernel comment)
