@@ -243,6 +243,23 @@ def recipes(a) -> dict:
             ("ab8192", 300, f"{PY} -u bench/lean_split_ab.py --n 8192 --steps 800 --warmup 50"),
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 2"),
         ],
+        # r6: split ranks on three p buffers -- the bitwise tests, then the A/B (side = three buffers, two = r5)
+        "lsplit3": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean_split'"),
+            ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 3 "
+                             "--arms uniform,side,two"),
+            ("ab4096", 300, f"{PY} -u bench/lean_split_ab.py --n 4096 --steps 2000 --warmup 100 --reps 2 "
+                            "--arms uniform,generic,side,two"),
+        ],
+        "lsplit3b": [
+            ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 3 --arms side,two"),
+            ("t3", 600, prof("lsplit_t3", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "
+                                          "--arms side")),
+            ("t3_md", 60, f"{PY} bench/prof_summary.py --stats {OUT}/lsplit_t3 --title 'lean_split, three p buffers, 16384^2'"),
+            ("two", 600, prof("lsplit_two", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "
+                                            "--arms two")),
+            ("two_md", 60, f"{PY} bench/prof_summary.py --stats {OUT}/lsplit_two --title 'lean_split, two p buffers, 16384^2'"),
+        ],
         # kernel trace of the split pass at 16384^2 (lean + generic launches per pass) and of the generic one
         "lsplit_prof": [
             ("side", 600, prof("lsplit_side", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "

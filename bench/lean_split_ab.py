@@ -7,7 +7,9 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
 
   uniform   the unperturbed Laplacian (every run lean; the ceiling)
   generic   the perturbed matrix, lean_split = 0 (the pre-split dispatch)
-  side      the perturbed matrix, lean_split = 1, the generic launch on a side stream beside it
+  side      the perturbed matrix, lean_split = 1, the generic launch on a side stream beside it (r6: three
+            p buffers when the split allows them, the default)
+  two       the same with two p buffers (p3buf = 0: the r5 split)
 
 Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
     python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400]
@@ -37,7 +39,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--reps", type=int, default=1)
-    ap.add_argument("--arms", default="uniform,generic,side", help="comma list of arms to run")
+    ap.add_argument("--arms", default="uniform,generic,side,two", help="comma list of arms to run")
     a = ap.parse_args()
     import numpy as np
 
@@ -51,6 +53,7 @@ def main() -> int:
     out = {"n": a.n, "spots": a.spots, "steps": a.steps, "its": {}, "info": {}}
     arms = [("uniform", {})] + [(f"generic_{i}", {"lean_split": 0}) for i in range(a.reps)]
     arms += [(f"side_{i}", {"lean_split": 1}) for i in range(a.reps)]
+    arms += [(f"two_{i}", {"lean_split": 1, "p3buf": 0}) for i in range(a.reps)]
     want = set(a.arms.split(","))
     arms = [(nm, kw) for nm, kw in arms if nm.split("_")[0] in want]
     for name, kw in arms:
@@ -70,7 +73,7 @@ def main() -> int:
         s.synchronize()
         dt = time.perf_counter() - t0
         out["its"][name] = round(a.steps / dt, 1)
-        out["info"][name] = {k: s.info.get(k) for k in ("lean_only", "lean_split", "dia_uniform", "lean_mix")}
+        out["info"][name] = {k: s.info.get(k) for k in ("lean_only", "lean_split", "dia_uniform", "lean_mix", "p3buf")}
         del s, p
         print(json.dumps({"arm": name, "it_s": out["its"][name]}), flush=True)
     print(json.dumps(out), flush=True)

@@ -192,10 +192,12 @@ struct PullBases {
 // line): lines l0 - 1 .. l1 carry uniform patterns (one, B, for the inner lines; the rank's first
 // / last line their own, A / C, with B's slice-edge bits), and a column at a grid line's start /
 // end has the absent edge entry.  UNI: the caller is a wave (one run; values made wave-uniform).
+// nbr (three p buffers on a split rank, T3): the neighbouring columns' slices on those lines carry the
+// same value pattern too -- a three-buffer lean run recomputes their edge rows with its own line's values
 template <bool UNI>
 __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat, int64_t l0, int64_t l1, int64_t nl,
                                               int64_t ss, int64_t col, int64_t ext_len, uint32_t& WA, uint32_t& WB,
-                                              uint32_t& WC, int big = 0) {
+                                              uint32_t& WC, int big = 0, bool nbr = false) {
   auto ld = [&](int64_t i) { return UNI ? uni_u64(dpat[i]) : dpat[i]; };
   WA = WB = WC = 0u;
   // 32-bit byte offsets: from kernel-wide bases (ext_len < 2^29), or past that (BIG kernels) from
@@ -217,7 +219,19 @@ __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat,
     WC = (uint32_t)ld((nl - 1) * ss + col);
     go = go && (WC >> 31) != 0u && ((WC ^ WB) & (3u << 28)) == 0u;
   }
-  return go && (col != 0 || ((WB >> 28) & 1u)) && (col != ss - 1 || ((WB >> 29) & 1u));
+  go = go && (col != 0 || ((WB >> 28) & 1u)) && (col != ss - 1 || ((WB >> 29) & 1u));
+  if (nbr && go) {
+    const uint32_t m = ~(3u << 28);  // uniform flag and values; the slice-edge bits are the column's own
+    for (int d = -1; d <= 1; d += 2) {
+      const int64_t c = col + d;
+      if (c < 0 || c >= ss) continue;
+      const uint64_t wn = ld(ia * ss + c);
+      go = go && ((((uint32_t)wn ^ WB) & m) == 0u) && (int64_t)(wn >> 32) >= ib - ia + 1;
+      if (l0 <= 1) go = go && ((((uint32_t)ld(c) ^ WA) & m) == 0u);
+      if (l1 >= nl - 1) go = go && ((((uint32_t)ld((nl - 1) * ss + c) ^ WC) & m) == 0u);
+    }
+  }
+  return go;
 }
 
 // The 2-D carry's job decomposition: job -> (slice column, run of lines [l0, l1)) for a launch of nw

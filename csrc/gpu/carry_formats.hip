@@ -196,8 +196,8 @@ __global__ __launch_bounds__(256) void k_dia_runs(uint64_t* __restrict__ dpat, i
 // kw = 0, one wave per job; k_cg_carry_ar3: kw waves per job, their slice columns)
 __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
                                                     int64_t ext_len, int64_t grid, int kw, int64_t ln,
-                                                    int runs3,
-                                                    unsigned long long* __restrict__ fails) {
+                                                    int runs3, bool nbr,
+                                                    unsigned long long* __restrict__ fails, uint8_t* __restrict__ flags) {
   const int64_t waves = kw > 0 ? kw : 1;
   int64_t jobs, runs, chunk;
   if (kw == 0) {
@@ -223,7 +223,9 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
     if (l0 >= l1) continue;
     uint32_t a, b, c;
     // past 2^29 the BIG kernels re-base: per run (2-D), along the run (3-D)
-    if (!lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c, 1)) ++f;
+    const bool ok = lean_eligible<false>(dpat, l0, l1, nl, ss, col, ext_len, a, b, c, 1, nbr);
+    if (!ok) ++f;
+    if (flags != nullptr && kw == 0) flags[job] = ok ? 0 : 1;
   }
   if (f) atomicAdd(fails, f);
 }
@@ -283,19 +285,36 @@ void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t&
 }
 
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream, int runs3) {
+                            int32_t ln, hipStream_t stream, int runs3, bool nbr, std::vector<int32_t>* failed) {
   MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && (kw == 0 || (ln % 64 == 0 && ln % kw == 0)),
             "lean check: bad launch geometry");
   unsigned long long* f = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&f), sizeof(unsigned long long), stream), "device malloc failed(lean)");
   MCG_HIP(hipMemsetAsync(f, 0, sizeof(unsigned long long), stream), "device memset failed");
+  int64_t njobs = 0, runs = 0, chunk = 0;
+  uint8_t* fl = nullptr;
+  if (failed != nullptr) {
+    MCG_CHECK(kw == 0, "lean check: the failing-job list is for the 2-D carry");
+    njobs = carry_jobs((int64_t)grid * kWaves, ss, nl, runs, chunk);
+    MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&fl), (size_t)std::max<int64_t>(njobs, 1), stream),
+            "device malloc failed(lean)");
+  }
   hipLaunchKernelGGL(k_lean_check, dim3(64), dim3(256), 0, stream, dpat, ss, nl, ext_len, (int64_t)grid, kw,
-                     (int64_t)ln, runs3, f);
+                     (int64_t)ln, runs3, nbr, f, fl);
   MCG_HIP(hipGetLastError(), "kernel launch failed(lean check)");
   unsigned long long h = 0;
   MCG_HIP(hipMemcpyAsync(&h, f, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  std::vector<uint8_t> hf((size_t)njobs);
+  if (fl != nullptr && njobs > 0)
+    MCG_HIP(hipMemcpyAsync(hf.data(), fl, (size_t)njobs, hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
   MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(lean check)");
   (void)hipFreeAsync(f, stream);
+  if (fl != nullptr) (void)hipFreeAsync(fl, stream);
+  if (failed != nullptr) {
+    failed->clear();
+    for (int64_t j = 0; j < njobs; ++j)
+      if (hf[(size_t)j]) failed->push_back((int32_t)j);
+  }
   return (int64_t)h;
 }
 

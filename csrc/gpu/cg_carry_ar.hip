@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   // slice's edge row, ape), p -- loaded by those two lanes only; other lanes' values are unused
   struct Edge {
     double r, a, p;
+    uint32_t c;  // T3, generic step: the neighbouring edge row's dia4 codes
   };
   struct XP {
     double pkm2, xo;
@@ -187,9 +188,20 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       return sum;
     }
   };
-  for (int64_t job = gw; job < njobs; job += nw) {
+  // T3 generic launch of a split rank (TileRanges::gen_pieces / gen_list): the listed generic runs of the lean
+  // launch's decomposition, each in K pieces on K waves
+  const bool listed = T3 && tr.lean_split == 2 && tr.gen_list != nullptr;
+  const int64_t K = (T3 && tr.lean_split == 2 && tr.gen_pieces > 1) ? tr.gen_pieces : 1;
+  const int64_t cchunk = listed ? (int64_t)tr.gen_chunk : chunk;
+  for (int64_t job = gw; job < (listed ? (int64_t)tr.ngen : njobs) * K; job += nw) {
     int64_t col, l0, l1;
-    carry_run(job, SS, nl, chunk, col, l0, l1);
+    carry_run(listed ? (int64_t)tr.gen_list[job / K] : job / K, SS, nl, cchunk, col, l0, l1);
+    const int64_t L0 = l0, L1 = l1;  // the run the lean launch decides on
+    if (K > 1) {
+      const int64_t pc = (L1 - L0 + K - 1) / K;
+      l0 = L0 + (job % K) * pc;
+      l1 = l0 + pc < L1 ? l0 + pc : L1;
+    }
     if (l0 >= l1) continue;
     const int64_t sl0 = l0 * SS + col;
     const int32_t e0 = (int32_t)(own + sl0 * 64);
@@ -217,8 +229,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       uint32_t WA, WB, WC;
       // lean_split: both launches decide a run the same way (size mode 1 in both: it only differs from
       // mode 0 past 2^29 rows, where the lean launch runs the BIG kernels)
-      const bool elig = lean_eligible<true>(S.dpat, l0, l1, nl, SS, col, v.ext_len, WA, WB, WC,
-                                            (BIG || tr.lean_split != 0) ? 1 : 0);
+      // (T3 on a split rank: also the neighbouring columns' patterns, whose edge rows the lean run recomputes)
+      const bool elig = lean_eligible<true>(S.dpat, L0, L1, nl, SS, col, v.ext_len, WA, WB, WC,
+                                            (BIG || tr.lean_split != 0) ? 1 : 0, T3 && tr.lean_split != 0);
       if (tr.lean_split == 1 && !elig) continue;  // the generic launch takes this run
       if (tr.lean_split == 2 && elig) continue;   // the lean launch took it
       if constexpr (LEAN > 0) {
@@ -796,9 +809,13 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     PullBases pl;
     pl.at(v, 0);
     auto gside = [&](int32_t j) { return pl.side(l0 + (j < jmin ? jmin : (j > jmax ? jmax : j)), nl); };
+    // T3 (three p buffers, a split rank's generic runs): p_{k-2} read-only in its own buffer on every line,
+    // r_{k-1} recovered everywhere (no stored r); the neighbouring slices' edge rows recomputed from their
+    // codes and p's (load_edge / edge_pk3) -- no compact edge arrays, as in the lean T3 loop
+    const double* __restrict__ pm2 = T3 ? v.p_m2 : (const double*)pn;
     auto load_raw = [&](int32_t j, Raw& q) {
       const int32_t e = ebase(j) + lane;
-      q.r = ld_once((inrun(j) ? (const double*)pn : ro) + e, ntl);
+      q.r = ld_once((T3 ? pm2 : (inrun(j) ? (const double*)pn : ro)) + e, ntl);
       const int sd = gside(j);
       q.p = sd != 0 ? ld_sys(pl.p[sd - 1] + e, 0u) : ld_once(po + e, ntl);
     };
@@ -810,10 +827,29 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       const int sd = gside(j);
       return sd != 0 ? ld_sys(pl.ap[sd - 1] + (ebase(j) + lane), 0u) : apx_o[ebase(j) + lane];
     };
-    auto rof = [&](int32_t j, const Raw& q) { return inrun(j) ? fma(nbp, q.r, q.p) : q.r; };
+    auto rof = [&](int32_t j, const Raw& q) { return (T3 || inrun(j)) ? fma(nbp, q.r, q.p) : q.r; };
     auto load_edge = [&](int32_t j, Edge& q) {
       const int32_t e = ebase(j);
       const int64_t s = oline(j) * SS + col;
+      if constexpr (T3) {
+        // the neighbouring edge row (row -1 / 64 of the slice: lane 63 of slice s - 1 / lane 0 of s + 1) and
+        // the row beyond it (-2 / 65): their p_{k-1} (a pulled ghost line's from the neighbour's rows), the
+        // edge row's p_{k-2} and its codes; edge_pk3 recomputes its p_k in its owner's fma order
+        if (lane == 0 || lane == 63) {
+          const bool hi = lane == 63;
+          const int32_t row = hi ? (e + 64 < ext32 ? e + 64 : ext32 - 1) : (e >= 1 ? e - 1 : 0);
+          const int32_t row2 = hi ? (row + 1 < ext32 ? row + 1 : ext32 - 1) : (row >= 1 ? row - 1 : 0);
+          const int sd = gside(j);
+          q.p = sd != 0 ? ld_sys(pl.p[sd - 1] + row, 0u) : po[row];
+          q.a = sd != 0 ? ld_sys(pl.p[sd - 1] + row2, 0u) : po[row2];
+          q.r = pm2[row];
+          const int64_t sn = hi ? (s + 1 < nsl ? s + 1 : nsl - 1) : (s >= 1 ? s - 1 : 0);
+          ArCodes<4, 5> ce;
+          ar_load_dia<5>(S.dia4 + sn * 160, hi ? 0 : 63, ce);
+          q.c = ce.pk[0];
+        }
+        return;
+      }
       if constexpr (P3 && MCG_EDGE_BRANCHLESS) {
         // every lane loads (lanes 1-62 at lane 0's addresses, the same cache lines): selects instead
         // of exec-mask branches around the two edge lanes
@@ -864,12 +900,25 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     };
     auto edge_p = [&](const Edge& q) { return q.p; };
     auto edge_pk = [&](const Edge& q) { return fma(b, q.p, fma(na, q.a, q.r)); };  // p_k of the edge row
+    // T3: the edge row's p_k from its p_{k-1} on lines j - 1 / j + 1 (prev / next), the row beyond it (q.a),
+    // itself, this lane's own p_{k-1} (own) and its codes -- the owner's stencil (canonical slot order)
+    auto edge_pk3 = [&](double prev, const Edge& q, double next, double own) {
+      const bool hi = lane == 63;
+      const double g[5] = {prev, hi ? own : q.a, q.p, hi ? q.a : own, next};
+      double t = 0.0;
+#pragma unroll
+      for (int u = 0; u < 5; ++u) t = fma(s_val[(q.c >> (4 * u)) & 15u], g[u], t);
+      return fma(b, q.p, fma(na, t, fma(nbp, q.r, q.p)));
+    };
     // ghost line: Ap_{k-1} exchanged by the halo (multi-rank only)
     auto ghost = [&](int32_t j) { return apx_o != nullptr && (l0 + j == -1 || l0 + j == nl) && j >= jmin && j <= jmax; };
     // r_{k-1} of a ghost line (P > 1).  P3: recovered like an own line -- no wave writes the ghost
     // rows, and the halo delivered p_{k-2} into p_new's ghost rows two iterations ago -- so the halo
     // carries {Ap, p} and not r (one extra load, at a run's outer step only)
-    auto rghost = [&](int32_t j, const Raw& q) { return P3 && !first ? fma(nbp, pn[ebase(j) + lane], q.p) : q.r; };
+    auto rghost = [&](int32_t j, const Raw& q) {
+      if constexpr (T3) return fma(nbp, q.r, q.p);  // q.r: p_{k-2} of the ghost rows (load_raw)
+      return P3 && !first ? fma(nbp, pn[ebase(j) + lane], q.p) : q.r;
+    };
 
     // prologue: p_k of lines -1 and 0, r_k of line 0; operands of lines 1 .. QD, codes of 0, 1
     Raw rm2, rm1, r0, rq[QD];
@@ -911,7 +960,13 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       o_rk = fma(na, t, rof(0, r0));
       o_pk = fma(b, r0.p, o_rk);
     }
-    double o_epk = edge_pk(ed0);
+    double o_epk, ep_m = 0.0;  // T3: p_{k-1} of the neighbouring edge row, line m (carried)
+    if constexpr (T3) {
+      o_epk = edge_pk3(edm1.p, ed0, ed1.p, r0.p);
+      ep_m = ed0.p;
+    } else {
+      o_epk = edge_pk(ed0);
+    }
     // one line step; the rotation at its end is register renaming once the driver below unrolls
     // the steps by the rotation period (a rolled loop pays ~30 64-bit moves per step)
     auto step = [&](int32_t m) {
@@ -944,7 +999,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       const double sum = stencil(c0, o_pk, o_epk, pr_pk, pk1);
       const int32_t eb = e0 + m * LO;
       const int64_t s = (l0 + m) * SS + col;
-      if constexpr (P3) {
+      if constexpr (T3) {
+        // nobody reads a stored r or edge row
+      } else if constexpr (P3) {
         // r_k only where another wave (edge rows: compact, next to their Ap; the run's outer
         // lines) or rank reads it, and as the value the next pass recovers from the stored p's,
         // fma(-b, p_{k-1}, p_k): every reader of a row's r_k -- owner, neighbouring wave,
@@ -960,7 +1017,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       const bool bnd = l0 + m == 0 || l0 + m == nl - 1;  // the halo's source lines
       if (pl.pub && bnd) st_sys(pn + eb, (uint32_t)lane << 3, o_pk);
       else st_stream(&(pn + eb)[lane], o_pk);
-      if (lane == 0 || lane == 63) en[2 * s + (lane == 63 ? 1 : 0)] = sum;
+      if constexpr (!T3)
+        if (lane == 0 || lane == 63) en[2 * s + (lane == 63 ? 1 : 0)] = sum;
       if (apx_n != nullptr && bnd) {
         if (pl.pub) st_sys(apx_n + eb, (uint32_t)lane << 3, sum);
         else apx_n[eb + lane] = sum;
@@ -973,9 +1031,15 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       pr_pk = o_pk;
       o_pk = pk1;
       o_rk = rk1;
+      if constexpr (T3) {
+        if constexpr (E3) o_epk = edge_pk3(ep_m, ed1, ed2p.p, rq[0].p);
+        else o_epk = edge_pk3(ep_m, ed1, ed2.p, rq[0].p);
+        ep_m = ed1.p;
+      } else {
+        o_epk = edge_pk(ed1);
+      }
       o_pold = rq[0].p;
       o_pm2 = rq[0].r;
-      o_epk = edge_pk(ed1);
       if constexpr (E3) {
         ed1 = ed2p;
         ed2p = ed2;
@@ -1166,7 +1230,13 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     if (qd == 2) MCG_AP(CM, U, 2);            \
     else MCG_AP(CM, U, 3);                    \
   } while (0)
-  if (cm == 4) MCG_AQ(4, 5);
+  if (cm == 4 && p3k && v.p_m2 != nullptr) {
+    // three p buffers on a split rank's generic runs (T3: no stored r or edge rows)
+    // (the even passes rolled at depth 3: the 3-step unroll at depth 2 spills 13 VGPRs with the recomputed edges;
+    // also every run of a one-launch pass -- the setup's placement probe)
+    if (pair) MCG_A(4, 5, 3, true, true, 1, 0, false, false, true);
+    else MCG_A(4, 5, 3, false, true, 1, 0, false, false, true);
+  } else if (cm == 4) MCG_AQ(4, 5);
   else if (cm == 5) MCG_AQ(5, 5);
   else { if (param == 4) MCG_AQ(2, 4); else MCG_AQ(2, 5); }
 #undef MCG_AQ

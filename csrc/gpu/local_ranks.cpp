@@ -76,6 +76,7 @@ LocalRunResult run_local_ranks(const ProblemSpec& spec, const CgOptions& opt, in
         o.lean_only = s.info().lean_only;
         o.lean_split = s.info().lean_split;
         o.p3 = s.info().p3;
+        o.p3buf = s.info().p3buf;
         o.dia_uniform = s.info().dia_uniform;
         o.halo_pull = s.info().halo_pull;
         o.ag_overlap = s.info().ag_overlap;

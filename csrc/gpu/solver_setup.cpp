@@ -806,6 +806,14 @@ void GpuCgSolver::setup() {
       // all-generic with 3 changed rows; the 64-line runs of 4096^2 / 8192^2 lose (the few generic runs
       // sit on the critical path: 4855 vs 6816, 1819 vs 1938; profiles/r4/lsplit)
       const bool want = opt_.form.lean_split >= 1 || (2 * fails < jobs && chunk >= 128);
+      // three p buffers on a split rank (T3 kernels): a lean run also needs its neighbouring columns'
+      // patterns (it recomputes their edge rows), so fewer runs qualify; taken when the same rule holds
+      split_t3_lean_ = -1.0;
+      if (opt_.form.p3buf != 0 && opt_.recurrence == 1 && info_.dia4 && !diav_) {
+        const int64_t fn = kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g, 0, 0, s0_, 0, true);
+        if (fn < jobs && (opt_.form.lean_split >= 1 || (2 * fn < jobs && chunk >= 128)))
+          split_t3_lean_ = 1.0 - (double)fn / (double)jobs;
+      }
       if (jobs > 0 && fails < jobs && want) {
         lean_split_ = true;
         g_all_ = g;
@@ -889,7 +897,32 @@ void GpuCgSolver::setup() {
       p3buf_ = kern::dia_lines_uniform(dpat_.get(), tr_all_.strip, (n + 63) / 64 / tr_all_.strip, s0_);
     else if (diav_) p3buf_ = L_.ext_len < ((int64_t)1 << 29);  // 2-D diav: r recovered, edge rows' Ap stored
   }
+  // a split rank (r6): the lean T3 runs whose neighbouring columns match, the generic T3 kernels (edge rows
+  // recomputed from their codes) over the rest
+  if (opt_.form.p3buf != 0 && ar_ && p3_ && lean_split_ && split_t3_lean_ >= 0.0 && opt_.recurrence == 1 && n > 0)
+    p3buf_ = true;
   if (use_comm_ && world_ > 1) p3buf_ = all_ranks_agree_(p3buf_);
+  if (p3buf_ && lean_split_) {
+    // the generic launch over just the generic runs (ascending job order: fixed partial slots), each in
+    // pieces of >= 32 lines, one wave a piece: a small grid beside the lean launch
+    info_.lean_split = split_t3_lean_;
+    const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
+    int64_t runs = 0, chunk = 0;
+    kern::carry_jobs_host((int64_t)g_int_ * 4, tr_all_.strip, nlines, runs, chunk);
+    std::vector<int32_t> gen;
+    (void)kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g_int_, 0, 0, s0_, 0, true, &gen);
+    const int32_t pieces = opt_.hooks.gen_pieces > 0 ? opt_.hooks.gen_pieces
+                                                     : (int32_t)std::min<int64_t>(16, std::max<int64_t>(1, chunk / 32));
+    gen_list_.allocate(std::max<size_t>(gen.size(), 1), "generic runs");
+    if (!gen.empty())
+      MCG_HIP(hipMemcpy(gen_list_.get(), gen.data(), gen.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+              "memcpy from host to device failed(generic runs)");
+    tr_bnd_.gen_list = gen_list_.get();
+    tr_bnd_.ngen = (int32_t)gen.size();
+    tr_bnd_.gen_chunk = (int32_t)chunk;
+    tr_bnd_.gen_pieces = pieces;
+    g_bnd_ = (int)std::max<int64_t>(1, ((int64_t)gen.size() * pieces + 3) / 4);
+  }
   MCG_CHECK(opt_.form.p3buf != 1 || p3buf_,
             "p3buf needs the lean three-term dia4 carry (2-D: one value pattern per line; 3-D: below 2^29 rows) on every rank");
   info_.p3buf = p3buf_;

@@ -75,6 +75,15 @@ struct TileRanges {
   // in places): 1 = this launch (the lean kernels) takes only the runs that qualify for the lean loop,
   // 2 = this launch (the generic kernels, same grid) only the others; 0 = every run
   int32_t lean_split = 0;
+  // lean_split 2 with three p buffers (T3): each generic run in this many pieces, one wave each -- a T3 run
+  // needs nothing stored by its neighbours, so it splits at any line, and the generic runs' single waves
+  // were the split pass's critical path; 0 / 1 = whole runs.  gen_list (ngen entries, ascending): the
+  // generic runs' job indices in the lean launch's decomposition (gen_chunk lines per run), so the generic
+  // launch is a small grid over just those pieces
+  int32_t gen_pieces = 0;
+  int32_t ngen = 0;
+  int32_t gen_chunk = 0;
+  const int32_t* gen_list = nullptr;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);
@@ -359,7 +368,9 @@ void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t&
 // ghost line (system scope)
 void pull_probe(const double* base, int64_t n, double* out, hipStream_t stream);
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
-                            int32_t ln, hipStream_t stream, int runs3 = 0);
+                            int32_t ln, hipStream_t stream, int runs3 = 0,
+                            bool nbr = false,  // nbr: lean_eligible's neighbour check (split ranks, three p buffers)
+                            std::vector<int32_t>* failed = nullptr);  // 2-D: the failing jobs, ascending
 // cm: 2 SELL-64/c8, 3 SELL-64/c4, 4 SELL-64/dia4 (S.dia4 / S.dvals), 5 SELL-64/diav (S.cvd / cve / cvs,
 // variable coefficients; lean runs stream them: every run of >= 3 lines).  p3 (dia4): three-term form --
 // r_{k-1} = p_{k-1} - b_prev p_{k-2} from the two p buffers, r stored only at the slices' edge rows

@@ -18,6 +18,7 @@ struct LocalRankResult {
   bool lean_only = false;     // SolverInfo::lean_only of this rank
   double lean_split = 0.0;    // SolverInfo::lean_split of this rank
   bool p3 = false;            // SolverInfo::p3 (three-term carry form)
+  bool p3buf = false;         // SolverInfo::p3buf (three p buffers)
   double dia_uniform = 0.0;   // SolverInfo::dia_uniform (fraction of uniform slices)
   bool halo_pull = false;     // SolverInfo::halo_pull of this rank
   bool carry = false;  // SolverInfo::carry of this rank (the line-carry pass ran on its interior)

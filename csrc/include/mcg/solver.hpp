@@ -189,6 +189,8 @@ class GpuCgSolver {
   bool probed_ = false;
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
+  double split_t3_lean_ = -1.0;  // ... with three p buffers (runs whose neighbouring columns match too): the lean
+                                 // share of the runs, -1 = not applicable
   bool ar_ = false;             // CgOptions::ap_recompute in effect
   bool ar3_ = false;            // ... the 3-D plane carry (cg_carry_ar3)
   bool p3_ = false;             // ... the 2-D carry's three-term form (CgOptions::p3)
@@ -218,6 +220,7 @@ class GpuCgSolver {
   bool diav3_ = false;
   DeviceBuffer<double> dvals_;    // ... its value table (16 doubles)
   DeviceBuffer<uint64_t> dpat_;   // ... its uniform-slice patterns and run lengths (SellDev::dpat)
+  DeviceBuffer<int32_t> gen_list_;  // a split rank on three p buffers: its generic runs (TileRanges::gen_list)
   DeviceBuffer<int32_t> perm_;    // SELL-C-sigma slot -> local row (user matrices)
   DeviceBuffer<int32_t> soffs_;   // SELL-64/aligned per-slot column offsets
   bool aligned_ = false;

@@ -240,6 +240,7 @@ PYBIND11_MODULE(_C, m) {
       MCG_HOOK_PROP(force_idx64)
       MCG_HOOK_PROP(inject_nan_at)
       MCG_HOOK_PROP(lean_packed)
+      MCG_HOOK_PROP(gen_pieces)
       MCG_HOOK_PROP(pull_proxy)
       MCG_HOOK_PROP(probe_pick_halo)
       MCG_HOOK_PROP(probe_pick_ar)
@@ -553,6 +554,7 @@ PYBIND11_MODULE(_C, m) {
       d["lean_only"] = rr.lean_only;
       d["lean_split"] = rr.lean_split;
       d["p3"] = rr.p3;
+      d["p3buf"] = rr.p3buf;
       d["dia_uniform"] = rr.dia_uniform;
       d["halo_pull"] = rr.halo_pull;
       d["ag_overlap"] = rr.ag_overlap;

@@ -328,6 +328,55 @@ def test_lean_split_mixed_ranks_match_one_rank(mcg, world, lines):
         np.testing.assert_allclose(out["x"], one["x"], rtol=1e-11, atol=1e-13 * np.abs(one["x"]).max())
 
 
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_lean_split_three_buffers_match_two_buffers(mcg, world):
+    """Split ranks on three p buffers: the lean runs take the T3 kernels when their
+    neighbouring columns carry the same pattern (they recompute those columns' edge rows), the generic
+    runs the T3 generic step -- p_{k-2} read-only, r recovered everywhere, the neighbouring edge rows'
+    p_k recomputed from their codes in their owners' fma order, no stored r or compact edge arrays.  The
+    changed rows include a slice's last row and a slice's first row, so the generic runs recompute edge
+    rows whose coefficients differ from their line's.  The runs next to an odd column go generic here (in
+    the two-buffer split they stay lean), so the block partials are grouped differently: the same solve
+    to rounding, at P = 1, 2, 4 (LocalComm; P > 1 with the in-kernel halo and with exchanges), and bit for
+    bit graph = eager, 41 iterations."""
+    n = 2048
+    A = _poisson(n, 2).tolil()
+    d = A.diagonal()
+    for row in (n * 100 + 7, n * 1020 + 3 * 64 + 63, n * 1500 + 4 * 64):
+        d[row] += 0.5
+    A.setdiag(d)
+    p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
+    C = mcg.native()
+
+    def run(pb, hp=-1, graph=True, pieces=-1):
+        o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
+        o.lean_split = 1
+        o.p3buf = pb
+        o.halo_pull = hp
+        o.use_graph = graph
+        o.gen_pieces = pieces
+        return C.run_local_ranks(p.native(), o, world, 41, True)
+
+    for hp in ((-1,) if world == 1 else (1, 0)):
+        two, three, eager = run(0, hp), run(-1, hp), run(-1, hp, False)
+        assert not any(rk["p3buf"] for rk in two["ranks"])
+        assert all(rk["p3buf"] for rk in three["ranks"]), three["ranks"]
+        assert any(0.0 < rk["lean_split"] < 1.0 for rk in three["ranks"]), [rk["lean_split"] for rk in three["ranks"]]
+        if hp >= 0:
+            assert all(rk["halo_pull"] == (hp == 1) for rk in three["ranks"])
+        for a, b, c in zip(three["ranks"], two["ranks"], eager["ranks"]):
+            assert a["iterations"] == b["iterations"] == c["iterations"] == 41
+            assert abs(a["rnorm"] - b["rnorm"]) <= 1e-13 * b["rnorm"], (hp, a["rnorm"], b["rnorm"])
+            assert a["rnorm"] == c["rnorm"]
+        np.testing.assert_allclose(three["x"], two["x"], rtol=1e-11, atol=1e-13 * np.abs(two["x"]).max())
+        np.testing.assert_array_equal(three["x"], eager["x"])
+        # the generic runs in 5 pieces on 5 waves each (TileRanges::gen_pieces; 2048^2's runs are whole)
+        cut = run(-1, hp, pieces=5)
+        for a, b in zip(cut["ranks"], two["ranks"]):
+            assert abs(a["rnorm"] - b["rnorm"]) <= 1e-13 * b["rnorm"], (hp, a["rnorm"], b["rnorm"])
+        np.testing.assert_allclose(cut["x"], two["x"], rtol=1e-11, atol=1e-13 * np.abs(two["x"]).max())
+
+
 def _nine_point(n=96, seed=3):
     """A variable-coefficient 9-point operator on an n x n grid (SPD: symmetric random off-diagonal
     weights, diagonal = sum |off| + 0.5): banded, every interior slice shares its 9 offsets, but no
