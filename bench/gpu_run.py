@@ -260,6 +260,11 @@ def recipes(a) -> dict:
                                             "--arms two")),
             ("two_md", 60, f"{PY} bench/prof_summary.py --stats {OUT}/lsplit_two --title 'lean_split, two p buffers, 16384^2'"),
         ],
+        # r6: config-5 tiles in two 8-wave workgroups per CU (tile_waves 8) against four 4-wave ones, interleaved
+        "c5w8": [("pytest", 300, f"{PYTEST} -v tests/test_gpu_irregular.py -k wide_workgroups")] + [
+            (f"w{ww}_{rep}", 400, bench(f"{C5SCR} --phases 0 --steps 10 --warmup 3 --set tile_waves={ww}"))
+            for rep in ("a", "b") for ww in (4, 8)
+        ],
         # kernel trace of the split pass at 16384^2 (lean + generic launches per pass) and of the generic one
         "lsplit_prof": [
             ("side", 600, prof("lsplit_side", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "

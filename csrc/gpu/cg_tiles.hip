@@ -322,10 +322,11 @@ TilesGeometry tiles_geometry(int64_t n_rows, int64_t ext_len, int seg_shift) {
 }
 
 int tiles_grid(int ncu, int ww) {
-  MCG_CHECK(ww == 4 || ww == 16, "tiles: 4 or 16 waves per workgroup");
+  MCG_CHECK(ww == 4 || ww == 8 || ww == 16, "tiles: 4, 8 or 16 waves per workgroup");
   int per_cu = 0;
   const void* f = ww == 16 ? reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10, 16>)
-                           : reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10>);
+                  : ww == 8 ? reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10, 8>)
+                            : reinterpret_cast<const void*>(&k_tiles<0, 0, 0, 10>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, ww * 64, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   (void)hipGetLastError();
   // every workgroup resident on the solver's CUs (pacing waits on them): 16 waves per CU either way
@@ -369,12 +370,15 @@ void cg_split_spmv_tiles(const TilesDev& T, const double* p_ext, const double* r
   MCG_CHECK(part == 0 || (T.g_lo >= 0 && T.g_lo <= T.g_hi && T.g_hi <= T.G), "tiles: bad own-segment range");
   MCG_CHECK(part != 1 || rc.ngroups == 0, "tiles: the own-segment half writes no partials");
   MCG_CHECK(T.tb == kTileB && (T.tu == 8 || T.tu == 10), "tiles: 1024 rows per block, 8 or 10 entries per lane");
-  MCG_CHECK(T.ww == 4 || T.ww == 16, "tiles: 4 or 16 waves per workgroup");
+  MCG_CHECK(T.ww == 4 || T.ww == 8 || T.ww == 16, "tiles: 4, 8 or 16 waves per workgroup");
   if (T.pace) MCG_HIP(hipMemsetAsync(T.pace, 0, kTilePaceWords * sizeof(unsigned), stream), "device memset failed");
 #define MCG_TL(PART, ABL, TU)                                                                                          \
   do {                                                                                                                 \
     if (T.ww == 16 && ABL == 0)                                                                                        \
       hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU, 16>), dim3(grid), dim3(1024), 0, stream, T, p_ext, r, Ap, own_off,  \
+                         partials, pstride, st, tol, first, check, rc);                                               \
+    else if (T.ww == 8 && ABL == 0)                                                                                    \
+      hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU, 8>), dim3(grid), dim3(512), 0, stream, T, p_ext, r, Ap, own_off,    \
                          partials, pstride, st, tol, first, check, rc);                                               \
     else                                                                                                               \
       hipLaunchKernelGGL((k_tiles<0, PART, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, p_ext, r, Ap, own_off,      \
@@ -415,6 +419,9 @@ void spmv_tiles(const TilesDev& T, const double* x_ext, double* y, int grid, hip
   do {                                                                                                                 \
     if (T.ww == 16 && ABL == 0)                                                                                        \
       hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU, 16>), dim3(grid), dim3(1024), 0, stream, T, x_ext, nullptr, y, 0,      \
+                         nullptr, 0, nullptr, 0.0, 0, 0, RedCtl());                                                   \
+    else if (T.ww == 8 && ABL == 0)                                                                                    \
+      hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU, 8>), dim3(grid), dim3(512), 0, stream, T, x_ext, nullptr, y, 0,        \
                          nullptr, 0, nullptr, 0.0, 0, 0, RedCtl());                                                   \
     else                                                                                                               \
       hipLaunchKernelGGL((k_tiles<1, 0, ABL, TU>), dim3(grid), dim3(256), 0, stream, T, x_ext, nullptr, y, 0, nullptr, \

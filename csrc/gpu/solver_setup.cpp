@@ -549,9 +549,10 @@ void GpuCgSolver::setup() {
     g_bnd_ = grid_a(tr_bnd_);
   }
   if (tiles_) {  // one launch over every row block: the resident workgroups (the pacing waits on each)
-    tile_ww_ = opt_.form.tile_waves == 16 ? 16 : 4;
-    MCG_CHECK(opt_.form.tile_waves == -1 || opt_.form.tile_waves == 4 || opt_.form.tile_waves == 16,
-              "tile_waves: 4 or 16 waves per workgroup");
+    tile_ww_ = (opt_.form.tile_waves == 16 || opt_.form.tile_waves == 8) ? opt_.form.tile_waves : 4;
+    MCG_CHECK(opt_.form.tile_waves == -1 || opt_.form.tile_waves == 4 || opt_.form.tile_waves == 8 ||
+                  opt_.form.tile_waves == 16,
+              "tile_waves: 4, 8 or 16 waves per workgroup");
     g_all_ = n > 0 ? kern::tiles_grid(ncu_, tile_ww_) : 0;
     if (opt_.blocks_per_cu > 0) g_all_ = std::min(g_all_, ncu_ * opt_.blocks_per_cu);  // fewer waves: more rounds
     g_int_ = 0;

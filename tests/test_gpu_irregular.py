@@ -387,21 +387,22 @@ def test_tiles_all_gather_overlap_halves_match(mcg, world):
     assert all(r["true_rnorm"] < 1e-6 for r in on["ranks"])
 
 
-def test_tiles_sixteen_wave_workgroups_same_row_sums(mcg):
-    """PassForm::tile_waves = 16 (one 1024-thread workgroup per CU, pacing barrier over waves of one
-    age): every row's sum is added in the same order as with four 4-wave workgroups (its wave owns it),
-    so the iterates agree to the rounding of the dot products' block partials (grouped over 16 waves
-    instead of 4); graph = eager bit for bit and the true residual tracks."""
+@pytest.mark.parametrize("ww", [8, 16])
+def test_tiles_wide_workgroups_same_row_sums(mcg, ww):
+    """PassForm::tile_waves = 16 / 8 (one 1024- or two 512-thread workgroups per CU, the pacing barrier
+    over waves of one age): every row's sum is added in the same order as with four 4-wave workgroups
+    (its wave owns it), so the iterates agree to the rounding of the dot products' block partials
+    (grouped over 16 / 8 waves instead of 4); graph = eager bit for bit and the true residual tracks."""
     spec = mcg.make_problem("randspd", **SCR)
     kw = dict(format="sell", recurrence=1, tol=-1.0, maxit=40, tile_seg_log2=12, tiles=1)
     a = mcg.CGSolver(spec, **kw).solve()
-    s = mcg.CGSolver(spec, tile_waves=16, **kw)
+    s = mcg.CGSolver(spec, tile_waves=ww, **kw)
     assert s.info["tiles"]
     b = s.solve()
     assert a["iterations"] == b["iterations"] == 40
     assert abs(a["rnorm"] - b["rnorm"]) <= 1e-12 * a["rnorm"]
     np.testing.assert_allclose(b["x_local"], a["x_local"], rtol=1e-12, atol=1e-14 * np.abs(a["x_local"]).max())
-    c = mcg.CGSolver(spec, tile_waves=16, use_graph=False, **kw).solve()
+    c = mcg.CGSolver(spec, tile_waves=ww, use_graph=False, **kw).solve()
     assert c["rnorm"] == b["rnorm"]
     np.testing.assert_array_equal(c["x_local"], b["x_local"])
     tr = s.true_residual_norm()
