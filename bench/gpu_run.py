@@ -247,7 +247,7 @@ def recipes(a) -> dict:
         "lsplit3": [
             ("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean_split'"),
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 3 "
-                             "--arms uniform,side,two"),
+                             "--arms uniform,side,two,sideplain"),
             ("ab4096", 300, f"{PY} -u bench/lean_split_ab.py --n 4096 --steps 2000 --warmup 100 --reps 2 "
                             "--arms uniform,generic,side,two"),
         ],

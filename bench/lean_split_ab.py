@@ -10,6 +10,7 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
   side      the perturbed matrix, lean_split = 1, the generic launch on a side stream beside it (r6: three
             p buffers when the split allows them, the default)
   two       the same with two p buffers (p3buf = 0: the r5 split)
+  sideplain three p buffers on the split's r4 geometry (one grid by the runs' length, no packed edges)
 
 Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
     python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400]
@@ -54,6 +55,7 @@ def main() -> int:
     arms = [("uniform", {})] + [(f"generic_{i}", {"lean_split": 0}) for i in range(a.reps)]
     arms += [(f"side_{i}", {"lean_split": 1}) for i in range(a.reps)]
     arms += [(f"two_{i}", {"lean_split": 1, "p3buf": 0}) for i in range(a.reps)]
+    arms += [(f"sideplain_{i}", {"lean_split": 1, "lean_packed": 0}) for i in range(a.reps)]
     want = set(a.arms.split(","))
     arms = [(nm, kw) for nm, kw in arms if nm.split("_")[0] in want]
     for name, kw in arms:

@@ -906,7 +906,12 @@ void GpuCgSolver::setup() {
   if (p3buf_ && lean_split_) {
     // the generic launch over just the generic runs (ascending job order: fixed partial slots), each in
     // pieces of >= 32 lines, one wave a piece: a small grid beside the lean launch
-    info_.lean_split = split_t3_lean_;
+    // the lean launch on the packed-edge kernels (EP, depth 4 at 4 waves per SIMD) over 4 blocks per CU for
+    // both parities -- the lean-only odd passes' geometry; one grid, so one generic list serves both
+    if (opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.hooks.lean_packed != 0) {
+      g_int_ = ncu_ * 4;
+      lean_depth_even_ = lean_depth_odd_ = 14;
+    }
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
     int64_t runs = 0, chunk = 0;
     kern::carry_jobs_host((int64_t)g_int_ * 4, tr_all_.strip, nlines, runs, chunk);
@@ -923,6 +928,7 @@ void GpuCgSolver::setup() {
     tr_bnd_.gen_chunk = (int32_t)chunk;
     tr_bnd_.gen_pieces = pieces;
     g_bnd_ = (int)std::max<int64_t>(1, ((int64_t)gen.size() * pieces + 3) / 4);
+    info_.lean_split = runs * tr_all_.strip > 0 ? 1.0 - (double)gen.size() / (double)(runs * tr_all_.strip) : 0.0;
   }
   MCG_CHECK(opt_.form.p3buf != 1 || p3buf_,
             "p3buf needs the lean three-term dia4 carry (2-D: one value pattern per line; 3-D: below 2^29 rows) on every rank");
