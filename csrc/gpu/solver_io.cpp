@@ -202,7 +202,8 @@ std::vector<std::pair<std::string, double>> GpuCgSolver::phase_profile(int iters
       MCG_HIP(hipEventRecord(e[2].get(), s0_), "event record failed");
     }
     MCG_HIP(hipEventRecord(e[3].get(), s0_), "event record failed");
-    const int np = split ? g_int_ + g_bnd_ : ((g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_);
+    // (split: the boundary launch's partials from bnd_base_; the slots between are never written, zero)
+    const int np = split ? bnd_base_ + g_bnd_ : ((g_odd_ > 0 && (k & 1) != 0) ? g_odd_ : g_all_);
     kern::cg_reduce_f1(partials_.get(), pstride_, np, st_.get(), 0, k >= 2 ? 1 : 0, k == 0 ? 1 : 0, opt_.tol, s0_);
     MCG_HIP(hipEventRecord(e[4].get(), s0_), "event record failed");
     if (use_comm_) comm_->allreduce_sum(st_.get()->red, 4, s0_);
