@@ -265,6 +265,14 @@ def recipes(a) -> dict:
             (f"w{ww}_{rep}", 400, bench(f"{C5SCR} --phases 0 --steps 10 --warmup 3 --set tile_waves={ww}"))
             for rep in ("a", "b") for ww in (4, 8)
         ],
+        # r6: plain (MALL-allocating) stores for the vectors a pass writes, against non-temporal ones, by size
+        # (var/tstore: -DMCG_NT_STORES=0, built like var/colx)
+        "tstore": [
+            (f"{tag}_{g}_{rep}", 200, f"{PY} {script} --grid {g} --phases 0 "
+                                      + ("--steps 2000 --warmup 200" if g <= 4096 else "--steps 300 --warmup 30"))
+            for rep in ("a", "b") for g in (4096, 8192, 16384)
+            for tag, script in (("nt", "bench.py"), ("plain", "var/tstore/run_bench.py"))
+        ],
         # kernel trace of the split pass at 16384^2 (lean + generic launches per pass) and of the generic one
         "lsplit_prof": [
             ("side", 600, prof("lsplit_side", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "
