@@ -251,6 +251,12 @@ def recipes(a) -> dict:
             ("ab4096", 300, f"{PY} -u bench/lean_split_ab.py --n 4096 --steps 2000 --warmup 100 --reps 2 "
                             "--arms uniform,generic,side,two"),
         ],
+        # ... a P = 8 rank's share (rank 5 holds two of the three changed rows), NullComm, in-kernel halo
+        "lsplit3s8": [
+            ("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean_split'"),
+            ("s8", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 2000 --warmup 200 --reps 2 "
+                        "--arms uniform,side,serial,two --sim-world 8 --sim-rank 5"),
+        ],
         "lsplit3b": [
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 3 --arms side,two"),
             ("t3", 600, prof("lsplit_t3", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 100 --warmup 10 "

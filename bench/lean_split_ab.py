@@ -11,9 +11,14 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
             p buffers when the split allows them, the default)
   two       the same with two p buffers (p3buf = 0: the r5 split)
   sideplain three p buffers on the split's r4 geometry (one grid by the runs' length, no packed edges)
+  rsv8/32   side with 8 / 32 CUs withheld from the lean launch's stream (the generic launch's side stream
+            keeps them: its pieces start at once instead of after the lean launch's workgroups)
+  serial    side with the generic launch ahead of the lean one on one stream
 
 Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
-    python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400]
+    python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400] [--sim-world 8 --sim-rank 3]
+--sim-world P --sim-rank r: rank r's share of a P-rank job alone on the GPU (collectives that move nothing,
+the in-kernel halo on, as bench.py --sim-world ... --set halo_pull=1).
 """
 from __future__ import annotations
 
@@ -41,6 +46,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--arms", default="uniform,generic,side,two", help="comma list of arms to run")
+    ap.add_argument("--sim-world", type=int, default=0)
+    ap.add_argument("--sim-rank", type=int, default=0)
     a = ap.parse_args()
     import numpy as np
 
@@ -51,11 +58,13 @@ def main() -> int:
     print(json.dumps({"built": a.n, "nnz": int(A.nnz), "s": round(time.perf_counter() - t0, 1)}), flush=True)
     rng = np.random.default_rng(7)
     spots = rng.integers(0, a.n * a.n, a.spots)
-    out = {"n": a.n, "spots": a.spots, "steps": a.steps, "its": {}, "info": {}}
+    out = {"n": a.n, "spots": a.spots, "steps": a.steps, "its": {}, "info": {}, "sim": [a.sim_rank, a.sim_world]}
     arms = [("uniform", {})] + [(f"generic_{i}", {"lean_split": 0}) for i in range(a.reps)]
     arms += [(f"side_{i}", {"lean_split": 1}) for i in range(a.reps)]
     arms += [(f"two_{i}", {"lean_split": 1, "p3buf": 0}) for i in range(a.reps)]
     arms += [(f"sideplain_{i}", {"lean_split": 1, "lean_packed": 0}) for i in range(a.reps)]
+    arms += [(f"rsv{c}_{i}", {"lean_split": 1, "reserve_cus": c}) for i in range(a.reps) for c in (8, 32)]
+    arms += [(f"serial_{i}", {"lean_split": 1, "split_serial": 1}) for i in range(a.reps)]
     want = set(a.arms.split(","))
     arms = [(nm, kw) for nm, kw in arms if nm.split("_")[0] in want]
     for name, kw in arms:
@@ -66,7 +75,16 @@ def main() -> int:
                 A.data[lo + int(np.nonzero(A.indices[lo:hi] == r)[0][0])] += 0.5
             spots = None
         p = mcg.csr_problem(A, rhs="random")
-        s = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=-1.0, maxit=a.steps + a.warmup, **kw)
+        if a.sim_world > 1:
+            from cuda_mpi_parallel_amd.solver import _opts
+
+            C = mcg.native()
+            o = _opts(maxit=a.steps + a.warmup, tol=-1.0, format="sellc8", recurrence=1, halo_pull=1, **kw)
+            s = mcg.CGSolver.__new__(mcg.CGSolver)  # the rank's share on a NullComm, as bench.py --sim-world
+            s._s = C.Solver(p.native(), o, a.sim_rank, a.sim_world, C.NullComm(a.sim_rank, a.sim_world))
+            s._s.setup()
+        else:
+            s = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=-1.0, maxit=a.steps + a.warmup, **kw)
         s.reset()
         s.run(a.warmup)
         s.synchronize()

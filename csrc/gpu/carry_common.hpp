@@ -234,6 +234,58 @@ __device__ __forceinline__ bool lean_eligible(const uint64_t* __restrict__ dpat,
   return go;
 }
 
+// A split rank on three p buffers (TileRanges::sub_ranges): the next lean sub-range [a, b) of the run [L0, L1)
+// at or after line `from` -- the stretch from `from` over which lines a - 1 .. b carry one pattern in this
+// column and its neighbours (lean_eligible with nbr, WA / WB / WC set), at least 3 lines; false when none is
+// left.  A T3 run needs nothing stored by its neighbours, so the lean launch takes every such stretch and
+// the generic launch only the lines around the odd slices (split_generic_ranges lists them: the same walk).
+template <bool UNI>
+__device__ __forceinline__ bool next_lean_range(const uint64_t* __restrict__ dpat, int64_t from, int64_t L1, int64_t nl,
+                                                int64_t ss, int64_t col, int64_t ext_len, int64_t& a, int64_t& b,
+                                                uint32_t& WA, uint32_t& WB, uint32_t& WC) {
+  auto ld = [&](int64_t i) { return UNI ? uni_u64(dpat[i]) : dpat[i]; };
+  const uint32_t vm = ~(3u << 28);  // uniform flag and values (the slice-edge bits are each column's own)
+  for (int64_t x = from; x + 3 <= L1;) {
+    // lines ia .. ia + len - 1 identical in each of the three columns (k_dia_runs' counts)
+    const int64_t ia = x - 1 > 1 ? x - 1 : 1;
+    int64_t len = INT64_MAX;
+    uint32_t w0 = 0u;
+    int bad = 0;  // 1: a non-uniform slice on line ia, 2: the columns' patterns differ there
+    for (int d = -1; d <= 1 && bad == 0; ++d) {
+      const int64_t c = col + d;
+      if (c < 0 || c >= ss) continue;
+      const uint64_t wn = ld(ia * ss + c);
+      if (((uint32_t)wn >> 31) == 0u) bad = 1;
+      else if (w0 != 0u && (((uint32_t)wn ^ w0) & vm) != 0u) bad = 2;
+      w0 = (uint32_t)wn;
+      len = (int64_t)(wn >> 32) < len ? (int64_t)(wn >> 32) : len;
+    }
+    if (bad == 1) {  // the next candidate starts past that line
+      x = ia + 2;
+      continue;
+    }
+    if (bad == 2) {  // they differ all along the shortest stretch
+      x = ia + len + 1;
+      continue;
+    }
+    const int64_t y = ia + len - 1 >= nl - 2 ? L1 : (ia + len - 1 < L1 ? ia + len - 1 : L1);
+    if (y - x >= 3 && lean_eligible<UNI>(dpat, x, y, nl, ss, col, ext_len, WA, WB, WC, 1, true)) {
+      a = x;
+      b = y;
+      return true;
+    }
+    // the rank's last line (pattern C) may be what fails: the stretch short of it
+    const int64_t y2 = y < nl - 2 ? y : nl - 2;
+    if (y2 - x >= 3 && y2 != y && lean_eligible<UNI>(dpat, x, y2, nl, ss, col, ext_len, WA, WB, WC, 1, true)) {
+      a = x;
+      b = y2;
+      return true;
+    }
+    ++x;  // (the rank's first line, pattern A, for x <= 1)
+  }
+  return false;
+}
+
 // The 2-D carry's job decomposition: job -> (slice column, run of lines [l0, l1)) for a launch of nw
 // waves over nl lines of ss slices.  Returns the number of jobs.
 __host__ __device__ __forceinline__ int64_t carry_jobs(int64_t nw, int64_t ss, int64_t nl, int64_t& runs,

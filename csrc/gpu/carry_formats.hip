@@ -8,6 +8,7 @@
 #include <climits>
 #include <cmath>
 #include <type_traits>
+#include <array>
 #include <vector>
 
 #include "mcg/check.hpp"
@@ -230,6 +231,36 @@ __global__ __launch_bounds__(256) void k_lean_check(const uint64_t* __restrict__
   if (f) atomicAdd(fails, f);
 }
 
+// split_generic_ranges: one thread per job of the lean launch; the lines its lean stretches leave
+// (next_lean_range, the walk the lean kernel makes) as ranges of at most maxlen lines
+__global__ __launch_bounds__(256) void k_split_ranges(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
+                                                      int64_t ext_len, int64_t grid, int maxlen, int cap,
+                                                      unsigned* __restrict__ cnt, int32_t* __restrict__ out) {
+  int64_t runs, chunk;
+  const int64_t jobs = carry_jobs(grid * kWaves, ss, nl, runs, chunk);
+  for (int64_t job = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; job < jobs; job += (int64_t)gridDim.x * blockDim.x) {
+    int64_t col, L0, L1;
+    carry_run(job, ss, nl, chunk, col, L0, L1);
+    auto emit = [&](int64_t a, int64_t b) {
+      for (int64_t x = a; x < b; x += maxlen) {
+        const unsigned i = atomicAdd(cnt, 1u);
+        if ((int)i < cap) {
+          out[3 * i] = (int32_t)col;
+          out[3 * i + 1] = (int32_t)x;
+          out[3 * i + 2] = (int32_t)(x + maxlen < b ? x + maxlen : b);
+        }
+      }
+    };
+    int64_t from = L0, a = 0, b = 0;
+    uint32_t wa, wb, wc;
+    while (from < L1 && next_lean_range<false>(dpat, from, L1, nl, ss, col, ext_len, a, b, wa, wb, wc)) {
+      emit(from, a);
+      from = b;
+    }
+    emit(from, L1);
+  }
+}
+
 // dia_lines_uniform: slices whose masked pattern word differs from their line's first slice
 __global__ __launch_bounds__(256) void k_lines_uniform(const uint64_t* __restrict__ dpat, int64_t ss, int64_t nl,
                                                        unsigned long long* __restrict__ bad) {
@@ -282,6 +313,44 @@ void pull_probe(const double* base, int64_t n, double* out, hipStream_t stream) 
 
 void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t& chunk) {
   (void)carry_jobs(nw, ss, nl, runs, chunk);
+}
+
+bool split_generic_ranges(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int maxlen,
+                          std::vector<int32_t>& ranges, hipStream_t stream) {
+  MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && maxlen > 0, "split ranges: bad geometry");
+  int64_t runs = 0, chunk = 0;
+  const int64_t jobs = carry_jobs((int64_t)grid * kWaves, ss, nl, runs, chunk);
+  const int cap = (int)std::min<int64_t>(1 << 22, 4 * jobs + 1024);
+  unsigned* cnt = nullptr;
+  int32_t* out = nullptr;
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned), stream), "device malloc failed(ranges)");
+  MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&out), (size_t)cap * 3 * sizeof(int32_t), stream), "device malloc failed(ranges)");
+  MCG_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned), stream), "device memset failed");
+  hipLaunchKernelGGL(k_split_ranges, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((jobs + 255) / 256, 1024))),
+                     dim3(256), 0, stream, dpat, ss, nl, ext_len, (int64_t)grid, maxlen, cap, cnt, out);
+  MCG_HIP(hipGetLastError(), "kernel launch failed(split ranges)");
+  unsigned h = 0;
+  MCG_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, stream), "memcpy from device to host failed");
+  MCG_HIP(hipStreamSynchronize(stream), "device synchronize failed(split ranges)");
+  const bool ok = (int64_t)h <= cap;
+  ranges.assign((size_t)(ok ? h : 0) * 3, 0);
+  if (ok && h > 0) {
+    MCG_HIP(hipMemcpy(ranges.data(), out, ranges.size() * sizeof(int32_t), hipMemcpyDeviceToHost),
+            "memcpy from device to host failed(ranges)");
+    // a fixed order (the atomic append's is not): by first line, then column -- the generic launch's waves
+    // and so its partial slots take the ranges in this order
+    std::vector<std::array<int32_t, 3>> t(h);
+    for (size_t i = 0; i < h; ++i) t[i] = {ranges[3 * i + 1], ranges[3 * i], ranges[3 * i + 2]};
+    std::sort(t.begin(), t.end());
+    for (size_t i = 0; i < h; ++i) {
+      ranges[3 * i] = t[i][1];
+      ranges[3 * i + 1] = t[i][0];
+      ranges[3 * i + 2] = t[i][2];
+    }
+  }
+  (void)hipFreeAsync(cnt, stream);
+  (void)hipFreeAsync(out, stream);
+  return ok;
 }
 
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,

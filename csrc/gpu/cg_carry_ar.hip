@@ -190,17 +190,27 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   };
   // T3 generic launch of a split rank (TileRanges::gen_pieces / gen_list): the listed generic runs of the lean
   // launch's decomposition, each in K pieces on K waves
-  const bool listed = T3 && tr.lean_split == 2 && tr.gen_list != nullptr;
-  const int64_t K = (T3 && tr.lean_split == 2 && tr.gen_pieces > 1) ? tr.gen_pieces : 1;
-  const int64_t cchunk = listed ? (int64_t)tr.gen_chunk : chunk;
-  for (int64_t job = gw; job < (listed ? (int64_t)tr.ngen : njobs) * K; job += nw) {
-    int64_t col, l0, l1;
-    carry_run(listed ? (int64_t)tr.gen_list[job / K] : job / K, SS, nl, cchunk, col, l0, l1);
-    const int64_t L0 = l0, L1 = l1;  // the run the lean launch decides on
-    if (K > 1) {
-      const int64_t pc = (L1 - L0 + K - 1) / K;
-      l0 = L0 + (job % K) * pc;
-      l1 = l0 + pc < L1 ? l0 + pc : L1;
+  // a split rank on three p buffers (TileRanges::sub_ranges): the lean launch takes every lean stretch of its
+  // runs (next_lean_range), the generic launch the listed ranges left between them (col, first, end line)
+  const bool listed = T3 && tr.lean_split == 2 && tr.sub_ranges != 0 && tr.gen_list != nullptr;
+  const bool subr = T3 && tr.lean_split == 1 && tr.sub_ranges != 0;
+  for (int64_t job = gw; job < (listed ? (int64_t)tr.ngen : njobs); job += nw) {
+    int64_t col, L0, L1;
+    if (listed) {
+      col = tr.gen_list[3 * job];
+      L0 = tr.gen_list[3 * job + 1];
+      L1 = tr.gen_list[3 * job + 2];
+    } else {
+      carry_run(job, SS, nl, chunk, col, L0, L1);
+    }
+    uint32_t sWA = 0u, sWB = 0u, sWC = 0u;
+    for (int64_t from = L0, more = 1; more;) {
+    int64_t l0 = L0, l1 = L1;
+    if (subr) {
+      if (!next_lean_range<true>(S.dpat, from, L1, nl, SS, col, v.ext_len, l0, l1, sWA, sWB, sWC)) break;
+      from = l1;
+    } else {
+      more = 0;
     }
     if (l0 >= l1) continue;
     const int64_t sl0 = l0 * SS + col;
@@ -229,9 +239,17 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       uint32_t WA, WB, WC;
       // lean_split: both launches decide a run the same way (size mode 1 in both: it only differs from
       // mode 0 past 2^29 rows, where the lean launch runs the BIG kernels)
-      // (T3 on a split rank: also the neighbouring columns' patterns, whose edge rows the lean run recomputes)
-      const bool elig = lean_eligible<true>(S.dpat, L0, L1, nl, SS, col, v.ext_len, WA, WB, WC,
-                                            (BIG || tr.lean_split != 0) ? 1 : 0, T3 && tr.lean_split != 0);
+      // (T3 on a split rank: also the neighbouring columns' patterns, whose edge rows the lean run recomputes;
+      // with sub-ranges the lean stretch is eligible by construction and a listed range is generic)
+      const bool elig = subr ? true
+                             : (listed ? false
+                                       : lean_eligible<true>(S.dpat, L0, L1, nl, SS, col, v.ext_len, WA, WB, WC,
+                                                             (BIG || tr.lean_split != 0) ? 1 : 0, T3 && tr.lean_split != 0));
+      if (subr) {
+        WA = sWA;
+        WB = sWB;
+        WC = sWC;
+      }
       if (tr.lean_split == 1 && !elig) continue;  // the generic launch takes this run
       if (tr.lean_split == 2 && elig) continue;   // the lean launch took it
       if constexpr (LEAN > 0) {
@@ -1067,6 +1085,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
     for (; m < n_run; ++m) step(m);
     pl.release(l0, l1, nl);
     }  // !LEAN
+    }  // sub-ranges
   }
 #if defined(MCG_CARRY_DIAG)
   const unsigned long long t_work = wall_clock64();

@@ -249,7 +249,7 @@ void GpuCgSolver::enqueue_f1_(int k, int which, int final_mode, bool fused_red) 
     // the launch runs the lean-only kernels: every run qualifies, or (lean_split) the lean half
     const bool lean_launch = lean_only_ || (lean_split_ && which == 1);
     // (lean_split: the generic launch runs on s2_, beside the lean one -- enqueue_pass_)
-    const hipStream_t ls = (lean_split_ && which == 2) ? (hipStream_t)s2_ : (hipStream_t)s0_;
+    const hipStream_t ls = (lean_split_ && which == 2 && opt_.hooks.split_serial <= 0) ? (hipStream_t)s2_ : (hipStream_t)s0_;
     v.ra_old = nullptr;
     v.ra_new = nullptr;
     v.ap_old = apx_[(k + 1) & 1].get();
@@ -439,6 +439,11 @@ int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
   // stream s2_ first, then the lean one on s0_: the generic runs overlap the lean pass instead of
   // following it.  The runs of one pass are independent (each reads the previous pass's vectors),
   // and the last arriver of either launch finishes the fused reduction.
+  if (opt_.hooks.split_serial > 0) {  // experiment: the generic launch ahead of the lean one, one stream
+    enqueue_f1_(k, 2, 0, fused_red);
+    enqueue_f1_(k, 1, 0, fused_red);
+    return bnd_base_ + g_bnd_;
+  }
   MCG_HIP(hipEventRecord(ev_ls_[0], s0_), "event record failed");
   MCG_HIP(hipStreamWaitEvent(s2_, ev_ls_[0], 0), "stream wait failed");
   enqueue_f1_(k, 2, 0, fused_red);

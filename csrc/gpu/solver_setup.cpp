@@ -904,31 +904,31 @@ void GpuCgSolver::setup() {
     p3buf_ = true;
   if (use_comm_ && world_ > 1) p3buf_ = all_ranks_agree_(p3buf_);
   if (p3buf_ && lean_split_) {
-    // the generic launch over just the generic runs (ascending job order: fixed partial slots), each in
-    // pieces of >= 32 lines, one wave a piece: a small grid beside the lean launch
     // the lean launch on the packed-edge kernels (EP, depth 4 at 4 waves per SIMD) over 4 blocks per CU for
     // both parities -- the lean-only odd passes' geometry; one grid, so one generic list serves both
     if (opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.hooks.lean_packed != 0) {
       g_int_ = ncu_ * 4;
       lean_depth_even_ = lean_depth_odd_ = 14;
     }
+    // the lean launch takes every lean stretch of its runs, the generic launch only the lines around the odd
+    // slices: a listed range (at most 32 lines) per wave, a small grid beside the lean launch
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
-    int64_t runs = 0, chunk = 0;
-    kern::carry_jobs_host((int64_t)g_int_ * 4, tr_all_.strip, nlines, runs, chunk);
-    std::vector<int32_t> gen;
-    (void)kern::carry_lean_failures(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g_int_, 0, 0, s0_, 0, true, &gen);
-    const int32_t pieces = opt_.hooks.gen_pieces > 0 ? opt_.hooks.gen_pieces
-                                                     : (int32_t)std::min<int64_t>(16, std::max<int64_t>(1, chunk / 32));
-    gen_list_.allocate(std::max<size_t>(gen.size(), 1), "generic runs");
-    if (!gen.empty())
-      MCG_HIP(hipMemcpy(gen_list_.get(), gen.data(), gen.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+    const int maxlen = opt_.hooks.gen_piece_lines > 0 ? opt_.hooks.gen_piece_lines : 32;
+    std::vector<int32_t> rng;
+    MCG_CHECK(kern::split_generic_ranges(dpat_.get(), tr_all_.strip, nlines, L_.ext_len, g_int_, maxlen, rng, s0_),
+              "lean split: too many generic ranges");
+    const int64_t ngen = (int64_t)rng.size() / 3;
+    gen_list_.allocate(std::max<size_t>(rng.size(), 3), "generic runs");
+    if (ngen > 0)
+      MCG_HIP(hipMemcpy(gen_list_.get(), rng.data(), rng.size() * sizeof(int32_t), hipMemcpyHostToDevice),
               "memcpy from host to device failed(generic runs)");
+    tr_int_.sub_ranges = tr_bnd_.sub_ranges = 1;
     tr_bnd_.gen_list = gen_list_.get();
-    tr_bnd_.ngen = (int32_t)gen.size();
-    tr_bnd_.gen_chunk = (int32_t)chunk;
-    tr_bnd_.gen_pieces = pieces;
-    g_bnd_ = (int)std::max<int64_t>(1, ((int64_t)gen.size() * pieces + 3) / 4);
-    info_.lean_split = runs * tr_all_.strip > 0 ? 1.0 - (double)gen.size() / (double)(runs * tr_all_.strip) : 0.0;
+    tr_bnd_.ngen = (int32_t)ngen;
+    g_bnd_ = (int)std::max<int64_t>(1, (ngen + 3) / 4);
+    int64_t glines = 0;
+    for (int64_t q = 0; q < ngen; ++q) glines += rng[3 * q + 2] - rng[3 * q + 1];
+    info_.lean_split = 1.0 - (double)glines / (double)std::max<int64_t>(1, nlines * tr_all_.strip);
   }
   MCG_CHECK(opt_.form.p3buf != 1 || p3buf_,
             "p3buf needs the lean three-term dia4 carry (2-D: one value pattern per line; 3-D: below 2^29 rows) on every rank");

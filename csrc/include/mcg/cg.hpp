@@ -113,8 +113,10 @@ struct TestHooks {
   int lean_packed = -1;      // test hook: 0 = the packed-edge geometry (solver_setup.cpp auto_mix_: even passes on 5,
                              // odd ones on 4 blocks per CU) with the default lean kernels instead of the packed-edge
                              // ones -- the bit-for-bit reference of those kernels
-  int gen_pieces = -1;       // test hook: a split rank's generic runs on three p buffers in this many pieces
-                             // (TileRanges::gen_pieces; -1 = the setup's rule, pieces of >= 32 lines)
+  int split_serial = -1;     // experiment: a split pass's generic launch ahead of the lean one on one stream (1)
+                             // instead of beside it on the side stream
+  int gen_piece_lines = -1;  // test hook: a split rank's generic ranges on three p buffers cut into pieces of at
+                             // most this many lines (TileRanges::gen_list; -1 = 32)
 };
 
 // Pass forms pruned in r5 (measured slower and kept opt-in until then): lean_depth 4 / 6 (fewer waves

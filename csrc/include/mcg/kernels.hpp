@@ -75,14 +75,13 @@ struct TileRanges {
   // in places): 1 = this launch (the lean kernels) takes only the runs that qualify for the lean loop,
   // 2 = this launch (the generic kernels, same grid) only the others; 0 = every run
   int32_t lean_split = 0;
-  // lean_split 2 with three p buffers (T3): each generic run in this many pieces, one wave each -- a T3 run
-  // needs nothing stored by its neighbours, so it splits at any line, and the generic runs' single waves
-  // were the split pass's critical path; 0 / 1 = whole runs.  gen_list (ngen entries, ascending): the
-  // generic runs' job indices in the lean launch's decomposition (gen_chunk lines per run), so the generic
-  // launch is a small grid over just those pieces
-  int32_t gen_pieces = 0;
+  // a split rank on three p buffers (T3): a T3 run needs nothing stored by its neighbours, so it splits at
+  // any line.  sub_ranges != 0: the lean launch (lean_split 1) takes every lean stretch of its runs
+  // (next_lean_range) and the generic launch (lean_split 2) only the ranges listed in gen_list (ngen
+  // triples: slice column, first line, end line; ascending, pieces of at most 32 lines) -- a small grid,
+  // one wave a range, where whole generic runs on single waves had been the split pass's critical path
+  int32_t sub_ranges = 0;
   int32_t ngen = 0;
-  int32_t gen_chunk = 0;
   const int32_t* gen_list = nullptr;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
@@ -367,6 +366,10 @@ void carry_jobs_host(int64_t nw, int64_t ss, int64_t nl, int64_t& runs, int64_t&
 // the in-kernel halo's setup check: out[i] = base[i] for i < n, loaded like the pass loads a pulled
 // ghost line (system scope)
 void pull_probe(const double* base, int64_t n, double* out, hipStream_t stream);
+// a split rank on three p buffers: the ranges (slice column, first line, end line; at most maxlen lines, in a
+// fixed order) the lean stretches of the lean launch's runs leave to the generic launch; false on overflow
+bool split_generic_ranges(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int maxlen,
+                          std::vector<int32_t>& ranges, hipStream_t stream);
 int64_t carry_lean_failures(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t ext_len, int grid, int kw,
                             int32_t ln, hipStream_t stream, int runs3 = 0,
                             bool nbr = false,  // nbr: lean_eligible's neighbour check (split ranks, three p buffers)

@@ -240,7 +240,8 @@ PYBIND11_MODULE(_C, m) {
       MCG_HOOK_PROP(force_idx64)
       MCG_HOOK_PROP(inject_nan_at)
       MCG_HOOK_PROP(lean_packed)
-      MCG_HOOK_PROP(gen_pieces)
+      MCG_HOOK_PROP(gen_piece_lines)
+      MCG_HOOK_PROP(split_serial)
       MCG_HOOK_PROP(pull_proxy)
       MCG_HOOK_PROP(probe_pick_halo)
       MCG_HOOK_PROP(probe_pick_ar)

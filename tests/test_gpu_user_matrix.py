@@ -330,15 +330,16 @@ def test_lean_split_mixed_ranks_match_one_rank(mcg, world, lines):
 
 @pytest.mark.parametrize("world", [1, 2, 4])
 def test_lean_split_three_buffers_match_two_buffers(mcg, world):
-    """Split ranks on three p buffers: the lean runs take the T3 kernels when their
-    neighbouring columns carry the same pattern (they recompute those columns' edge rows), the generic
-    runs the T3 generic step -- p_{k-2} read-only, r recovered everywhere, the neighbouring edge rows'
-    p_k recomputed from their codes in their owners' fma order, no stored r or compact edge arrays.  The
-    changed rows include a slice's last row and a slice's first row, so the generic runs recompute edge
-    rows whose coefficients differ from their line's.  The runs next to an odd column go generic here (in
-    the two-buffer split they stay lean), so the block partials are grouped differently: the same solve
-    to rounding, at P = 1, 2, 4 (LocalComm; P > 1 with the in-kernel halo and with exchanges), and bit for
-    bit graph = eager, 41 iterations."""
+    """Split ranks on three p buffers: the lean launch takes every stretch of a run whose
+    lines carry one pattern in its column and the neighbouring ones (the T3 lean loop recomputes those
+    columns' edge rows), the generic launch only the listed ranges left around the odd slices -- the T3
+    generic step: p_{k-2} read-only, r recovered everywhere, the neighbouring edge rows' p_k recomputed
+    from their codes in their owners' fma order, no stored r or compact edge arrays.  The changed rows
+    include a slice's last row and a slice's first row, so the generic ranges recompute edge rows whose
+    coefficients differ from their line's.  Lines are assigned to the launches differently from the
+    two-buffer split, so the block partials group differently: the same solve to rounding, at P = 1, 2, 4
+    (LocalComm; P > 1 with the in-kernel halo and with exchanges), bit for bit graph = eager, and with
+    the generic ranges cut into one-line pieces; 41 iterations."""
     n = 2048
     A = _poisson(n, 2).tolil()
     d = A.diagonal()
@@ -348,13 +349,13 @@ def test_lean_split_three_buffers_match_two_buffers(mcg, world):
     p = mcg.csr_problem(A.tocsr(), b=np.ones(n * n))
     C = mcg.native()
 
-    def run(pb, hp=-1, graph=True, pieces=-1):
+    def run(pb, hp=-1, graph=True, lines=-1):
         o = C.CgOptions(tol=-1.0, maxit=1 << 30, format="sellc8", recurrence=1)
         o.lean_split = 1
         o.p3buf = pb
         o.halo_pull = hp
         o.use_graph = graph
-        o.gen_pieces = pieces
+        o.gen_piece_lines = lines
         return C.run_local_ranks(p.native(), o, world, 41, True)
 
     for hp in ((-1,) if world == 1 else (1, 0)):
@@ -370,8 +371,8 @@ def test_lean_split_three_buffers_match_two_buffers(mcg, world):
             assert a["rnorm"] == c["rnorm"]
         np.testing.assert_allclose(three["x"], two["x"], rtol=1e-11, atol=1e-13 * np.abs(two["x"]).max())
         np.testing.assert_array_equal(three["x"], eager["x"])
-        # the generic runs in 5 pieces on 5 waves each (TileRanges::gen_pieces; 2048^2's runs are whole)
-        cut = run(-1, hp, pieces=5)
+        # the generic ranges cut into pieces of one line, one wave each (TileRanges::gen_list)
+        cut = run(-1, hp, lines=1)
         for a, b in zip(cut["ranks"], two["ranks"]):
             assert abs(a["rnorm"] - b["rnorm"]) <= 1e-13 * b["rnorm"], (hp, a["rnorm"], b["rnorm"])
         np.testing.assert_allclose(cut["x"], two["x"], rtol=1e-11, atol=1e-13 * np.abs(two["x"]).max())
