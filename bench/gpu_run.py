@@ -255,7 +255,9 @@ def recipes(a) -> dict:
         "lsplit3s8": [
             ("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean_split'"),
             ("s8", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 2000 --warmup 200 --reps 2 "
-                        "--arms uniform,side,serial,two --sim-world 8 --sim-rank 5"),
+                        "--arms uniform,side,serial,stream,two --sim-world 8 --sim-rank 5"),
+            ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 2 "
+                             "--arms uniform,side,stream,two"),
         ],
         "lsplit3b": [
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 3 --arms side,two"),
@@ -278,6 +280,11 @@ def recipes(a) -> dict:
                                       + ("--steps 2000 --warmup 200" if g <= 4096 else "--steps 300 --warmup 30"))
             for rep in ("a", "b") for g in (4096, 8192, 16384)
             for tag, script in (("nt", "bench.py"), ("plain", "var/tstore/run_bench.py"))
+        ],
+        # kernel trace of the split share with the generic launch ahead on one stream (per-call durations)
+        "lsplit3tr": [
+            ("tr", 600, prof("lsplit_ser", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 "
+                                          "--arms serial --sim-world 8 --sim-rank 5")),
         ],
         # kernel trace of the split pass at 16384^2 (lean + generic launches per pass) and of the generic one
         "lsplit_prof": [

@@ -14,6 +14,8 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
   rsv8/32   side with 8 / 32 CUs withheld from the lean launch's stream (the generic launch's side stream
             keeps them: its pieces start at once instead of after the lean launch's workgroups)
   serial    side with the generic launch ahead of the lean one on one stream
+  stream    side with the generic launch beside the lean one on the side stream (r6's first form; the
+            default since is one combined launch, the generic ranges' workgroups first)
 
 Prints one JSON line with it/s per arm (fixed iteration count, untimed warmup).
     python bench/lean_split_ab.py [--n 8192] [--spots 3] [--steps 400] [--sim-world 8 --sim-rank 3]
@@ -65,6 +67,7 @@ def main() -> int:
     arms += [(f"sideplain_{i}", {"lean_split": 1, "lean_packed": 0}) for i in range(a.reps)]
     arms += [(f"rsv{c}_{i}", {"lean_split": 1, "reserve_cus": c}) for i in range(a.reps) for c in (8, 32)]
     arms += [(f"serial_{i}", {"lean_split": 1, "split_serial": 1}) for i in range(a.reps)]
+    arms += [(f"stream_{i}", {"lean_split": 1, "split_serial": 0}) for i in range(a.reps)]
     want = set(a.arms.split(","))
     arms = [(nm, kw) for nm, kw in arms if nm.split("_")[0] in want]
     for name, kw in arms:

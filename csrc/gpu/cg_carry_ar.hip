@@ -69,8 +69,10 @@ constexpr int kCarryDiagMax = 8192;
 __device__ unsigned long long g_carry_diag[4 * kCarryDiagMax];
 #endif
 
+// COMBO (T3 lean kernels of a split rank, TileRanges::gen_blocks): the first gen_blocks workgroups run the
+// generic step over the listed ranges, the rest the lean launch -- one launch, no side stream
 template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false,
-          bool T3 = false>
+          bool T3 = false, bool COMBO = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
                                                      double* __restrict__ partials, int pstride, CgState* st,
                                                      double tol, int first, int check, RedCtl rc) {
@@ -113,7 +115,11 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   const int32_t LO = (int32_t)(SS * 64);  // one line
   const int64_t nl = tr.nt0 / SS;         // the rank's lines (the launch covers them all)
   const int64_t nsl = tr.nt0;             // the rank's slices
-  const int64_t nb = gridDim.x, blk = blockIdx.x;
+  // COMBO: workgroups [0, gen_blocks) take the listed generic ranges (gen_blocks a multiple of 8, so the
+  // lean workgroups keep their XCDs), the others the lean launch's jobs
+  const int64_t gb = COMBO ? (int64_t)tr.gen_blocks : 0;
+  const bool gblk = COMBO && (int64_t)blockIdx.x < gb;
+  const int64_t nb = gblk ? gb : gridDim.x - gb, blk = gblk ? blockIdx.x : blockIdx.x - gb;
   const int64_t lb = (nb % 8 == 0) ? (blk % 8) * (nb / 8) + blk / 8 : blk;  // XCD-aware (k_cg_f1_carry)
   const int64_t nw = nb * kWaves;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -192,8 +198,8 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   // launch's decomposition, each in K pieces on K waves
   // a split rank on three p buffers (TileRanges::sub_ranges): the lean launch takes every lean stretch of its
   // runs (next_lean_range), the generic launch the listed ranges left between them (col, first, end line)
-  const bool listed = T3 && tr.lean_split == 2 && tr.sub_ranges != 0 && tr.gen_list != nullptr;
-  const bool subr = T3 && tr.lean_split == 1 && tr.sub_ranges != 0;
+  const bool listed = gblk || (T3 && tr.lean_split == 2 && tr.sub_ranges != 0 && tr.gen_list != nullptr);
+  const bool subr = T3 && tr.lean_split == 1 && tr.sub_ranges != 0 && !gblk;
   for (int64_t job = gw; job < (listed ? (int64_t)tr.ngen : njobs); job += nw) {
     int64_t col, L0, L1;
     if (listed) {
@@ -250,9 +256,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
         WB = sWB;
         WC = sWC;
       }
-      if (tr.lean_split == 1 && !elig) continue;  // the generic launch takes this run
-      if (tr.lean_split == 2 && elig) continue;   // the lean launch took it
-      if constexpr (LEAN > 0) {
+      if (tr.lean_split == 1 && !elig && !gblk) continue;  // the generic launch takes this run
+      if (tr.lean_split == 2 && elig) continue;            // the lean launch took it
+      if (LEAN > 0 && !gblk) {
         struct VSet {
           double v[5];
         };
@@ -807,7 +813,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       pl.release(l0, l1, nl);
       continue;
     }
-    if constexpr (LEAN == 0) {
+    if (LEAN == 0 || gblk) {
     // lines j (relative to l0) inside the ext vectors: [jmin, jmax]; loads clamp to them (values
     // of lines that do not exist are never multiplied: the matrix has no entry for them)
     const int32_t jmax = (ext32 - 64 - e0) / LO;
@@ -1200,6 +1206,17 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     // 2, 4 (3 waves per SIMD) and 6 (2): profiles/r3/lean, r4/mix)
     if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
     else if (depth == 15 && !big && !pair) MCG_LWE(3, false, 6);  // even passes at 6 waves per SIMD
+    else if (depth == 14 && !big && t3 && tr.gen_blocks > 0) {
+      // a split rank's combined launch (COMBO): the generic ranges' workgroups ahead of the lean ones
+      MCG_CHECK(tr.gen_blocks % 8 == 0 && grid > tr.gen_blocks && tr.gen_list != nullptr,
+                "lean split: the combined launch's generic workgroups");
+      if (pair)
+        hipLaunchKernelGGL((k_cg_carry_ar<4, 5, 4, true, true, 1, 4, false, true, true, true>), dim3(grid), dim3(kBS), 0,
+                           stream, S, v, own_off, tr, partials, pstride, st, tol, first, check, rc);
+      else
+        hipLaunchKernelGGL((k_cg_carry_ar<4, 5, 4, false, true, 1, 4, false, true, true, true>), dim3(grid), dim3(kBS), 0,
+                           stream, S, v, own_off, tr, partials, pstride, st, tol, first, check, rc);
+    }
     else if (depth == 14 && !big) { if (pair) MCG_LWE(4, true, 4); else MCG_LWE(4, false, 4); }
     else { if (pair) MCG_LW(3, true); else MCG_LW(3, false); }
 #undef MCG_LWE

@@ -439,7 +439,11 @@ int GpuCgSolver::enqueue_pass_(int k, bool fused_red) {
   // stream s2_ first, then the lean one on s0_: the generic runs overlap the lean pass instead of
   // following it.  The runs of one pass are independent (each reads the previous pass's vectors),
   // and the last arriver of either launch finishes the fused reduction.
-  if (opt_.hooks.split_serial > 0) {  // experiment: the generic launch ahead of the lean one, one stream
+  if (combo_) {  // one combined launch: the generic ranges' workgroups, then the lean ones (setup)
+    enqueue_f1_(k, 1, 0, fused_red);
+    return bnd_base_ + g_bnd_;
+  }
+  if (opt_.hooks.split_serial > 0) {  // the generic launch ahead of the lean one, one stream
     enqueue_f1_(k, 2, 0, fused_red);
     enqueue_f1_(k, 1, 0, fused_red);
     return bnd_base_ + g_bnd_;

@@ -906,7 +906,8 @@ void GpuCgSolver::setup() {
   if (p3buf_ && lean_split_) {
     // the lean launch on the packed-edge kernels (EP, depth 4 at 4 waves per SIMD) over 4 blocks per CU for
     // both parities -- the lean-only odd passes' geometry; one grid, so one generic list serves both
-    if (opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.hooks.lean_packed != 0) {
+    const bool packed = opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.hooks.lean_packed != 0;
+    if (packed) {
       g_int_ = ncu_ * 4;
       lean_depth_even_ = lean_depth_odd_ = 14;
     }
@@ -923,9 +924,18 @@ void GpuCgSolver::setup() {
       MCG_HIP(hipMemcpy(gen_list_.get(), rng.data(), rng.size() * sizeof(int32_t), hipMemcpyHostToDevice),
               "memcpy from host to device failed(generic runs)");
     tr_int_.sub_ranges = tr_bnd_.sub_ranges = 1;
-    tr_bnd_.gen_list = gen_list_.get();
-    tr_bnd_.ngen = (int32_t)ngen;
+    tr_bnd_.gen_list = tr_int_.gen_list = gen_list_.get();
+    tr_bnd_.ngen = tr_int_.ngen = (int32_t)ngen;
     g_bnd_ = (int)std::max<int64_t>(1, (ngen + 3) / 4);
+    // default: one combined launch, the generic ranges' workgroups first (a second launch on the side stream
+    // ran beside the lean one only when the graph put its branch on another hardware queue; on one stream
+    // it added its whole ~22 us, profiles/r6/lsplit3); split_serial 0 / 1 keeps the two launches
+    combo_ = packed && ngen > 0 && opt_.hooks.split_serial < 0;
+    if (combo_) {
+      tr_int_.gen_blocks = (int32_t)(((ngen + 3) / 4 + 7) / 8 * 8);
+      g_int_ += tr_int_.gen_blocks;
+      g_bnd_ = 0;
+    }
     int64_t glines = 0;
     for (int64_t q = 0; q < ngen; ++q) glines += rng[3 * q + 2] - rng[3 * q + 1];
     info_.lean_split = 1.0 - (double)glines / (double)std::max<int64_t>(1, nlines * tr_all_.strip);

@@ -113,8 +113,9 @@ struct TestHooks {
   int lean_packed = -1;      // test hook: 0 = the packed-edge geometry (solver_setup.cpp auto_mix_: even passes on 5,
                              // odd ones on 4 blocks per CU) with the default lean kernels instead of the packed-edge
                              // ones -- the bit-for-bit reference of those kernels
-  int split_serial = -1;     // experiment: a split pass's generic launch ahead of the lean one on one stream (1)
-                             // instead of beside it on the side stream
+  int split_serial = -1;     // a split rank on three p buffers: -1 = one combined launch (generic ranges' workgroups
+                             // first), 0 = the generic launch beside the lean one on the side stream, 1 = ahead of
+                             // it on one stream
   int gen_piece_lines = -1;  // test hook: a split rank's generic ranges on three p buffers cut into pieces of at
                              // most this many lines (TileRanges::gen_list; -1 = 32)
 };

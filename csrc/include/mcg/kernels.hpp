@@ -83,6 +83,9 @@ struct TileRanges {
   int32_t sub_ranges = 0;
   int32_t ngen = 0;
   const int32_t* gen_list = nullptr;
+  // lean_split 1 with sub_ranges: > 0 = one combined launch -- its first gen_blocks workgroups (a multiple of 8)
+  // run the generic step over gen_list, the rest the lean stretches (no second launch, no side stream)
+  int32_t gen_blocks = 0;
 };
 // `tile` = rows per tile (kTileRows for CSR row tiles, 1 for SELL slice units)
 TileRanges make_tiles(int64_t b0, int64_t e0, int64_t b1 = 0, int64_t e1 = 0, int64_t tile = kTileRows);

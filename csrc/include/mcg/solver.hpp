@@ -189,6 +189,7 @@ class GpuCgSolver {
   bool probed_ = false;
   bool lean_split_ = false;     // 2-D three-term dia4 carry: the lean kernels over the runs that qualify, then the
                                 // generic kernels over the rest (same grid; the second launch finishes the reduction)
+  bool combo_ = false;           // ... and one combined launch (TileRanges::gen_blocks)
   double split_t3_lean_ = -1.0;  // ... with three p buffers (runs whose neighbouring columns match too): the lean
                                  // share of the runs, -1 = not applicable
   bool ar_ = false;             // CgOptions::ap_recompute in effect
