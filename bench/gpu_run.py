@@ -258,6 +258,8 @@ def recipes(a) -> dict:
                         "--arms uniform,side,serial,stream,two --sim-world 8 --sim-rank 5"),
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 2 "
                              "--arms uniform,side,stream,two"),
+            ("b16384", 200, bench("--phases 0")),
+            ("b4096", 200, bench("--grid 4096 --steps 2000 --warmup 200 --phases 0")),
         ],
         "lsplit3b": [
             ("ab16384", 900, f"{PY} -u bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 --reps 3 --arms side,two"),

@@ -10,7 +10,7 @@ it/s at 16384^2); with it (lean_split, the default) only that run does.  Arms, s
   side      the perturbed matrix, lean_split = 1, the generic launch on a side stream beside it (r6: three
             p buffers when the split allows them, the default)
   two       the same with two p buffers (p3buf = 0: the r5 split)
-  sideplain three p buffers on the split's r4 geometry (one grid by the runs' length, no packed edges)
+  sideplain the split's r4 geometry (one grid by the runs' length, no packed edges: two p buffers since late r6)
   rsv8/32   side with 8 / 32 CUs withheld from the lean launch's stream (the generic launch's side stream
             keeps them: its pieces start at once instead of after the lean launch's workgroups)
   serial    side with the generic launch ahead of the lean one on one stream

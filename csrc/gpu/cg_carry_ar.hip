@@ -69,8 +69,9 @@ constexpr int kCarryDiagMax = 8192;
 __device__ unsigned long long g_carry_diag[4 * kCarryDiagMax];
 #endif
 
-// COMBO (T3 lean kernels of a split rank, TileRanges::gen_blocks): the first gen_blocks workgroups run the
-// generic step over the listed ranges, the rest the lean launch -- one launch, no side stream
+// COMBO (the T3 lean kernels of a split rank's lean launch): the lean stretches of every run
+// (TileRanges::sub_ranges), and with gen_blocks > 0 the first gen_blocks workgroups run the generic step over
+// the listed ranges -- one launch, no side stream
 template <int CM, int U, int QD, bool PAIR, bool P3, int UN = 1, int LEAN = 0, bool BIG = false, bool EP = false,
           bool T3 = false, bool COMBO = false>
 __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(SellDev S, F1Vectors v, int64_t own, TileRanges tr,
@@ -198,8 +199,9 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
   // launch's decomposition, each in K pieces on K waves
   // a split rank on three p buffers (TileRanges::sub_ranges): the lean launch takes every lean stretch of its
   // runs (next_lean_range), the generic launch the listed ranges left between them (col, first, end line)
-  const bool listed = gblk || (T3 && tr.lean_split == 2 && tr.sub_ranges != 0 && tr.gen_list != nullptr);
-  const bool subr = T3 && tr.lean_split == 1 && tr.sub_ranges != 0 && !gblk;
+  // (compile-time false outside the split kernels: the lean-only kernels keep their register allocation)
+  const bool listed = gblk || (LEAN == 0 && T3 && tr.lean_split == 2 && tr.sub_ranges != 0 && tr.gen_list != nullptr);
+  const bool subr = COMBO && T3 && tr.lean_split == 1 && tr.sub_ranges != 0 && !gblk;
   for (int64_t job = gw; job < (listed ? (int64_t)tr.ngen : njobs); job += nw) {
     int64_t col, L0, L1;
     if (listed) {
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kBS, (LEAN > 0 ? LEAN : 4)) void k_cg_carry_ar(Sell
       const bool elig = subr ? true
                              : (listed ? false
                                        : lean_eligible<true>(S.dpat, L0, L1, nl, SS, col, v.ext_len, WA, WB, WC,
-                                                             (BIG || tr.lean_split != 0) ? 1 : 0, T3 && tr.lean_split != 0));
+                                                             (BIG || tr.lean_split != 0) ? 1 : 0, COMBO && tr.lean_split != 0));
       if (subr) {
         WA = sWA;
         WB = sWB;
@@ -1206,9 +1208,10 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
     // 2, 4 (3 waves per SIMD) and 6 (2): profiles/r3/lean, r4/mix)
     if (depth == 13 && !big) { if (pair) MCG_LWE(3, true, 5); else MCG_LWE(3, false, 5); }
     else if (depth == 15 && !big && !pair) MCG_LWE(3, false, 6);  // even passes at 6 waves per SIMD
-    else if (depth == 14 && !big && t3 && tr.gen_blocks > 0) {
-      // a split rank's combined launch (COMBO): the generic ranges' workgroups ahead of the lean ones
-      MCG_CHECK(tr.gen_blocks % 8 == 0 && grid > tr.gen_blocks && tr.gen_list != nullptr,
+    else if (depth == 14 && !big && t3 && tr.sub_ranges != 0) {
+      // a split rank's lean launch (COMBO): the lean stretches, and (gen_blocks > 0) the generic ranges'
+      // workgroups ahead of the lean ones in the same launch
+      MCG_CHECK(tr.gen_blocks % 8 == 0 && grid > tr.gen_blocks && (tr.gen_blocks == 0 || tr.gen_list != nullptr),
                 "lean split: the combined launch's generic workgroups");
       if (pair)
         hipLaunchKernelGGL((k_cg_carry_ar<4, 5, 4, true, true, 1, 4, false, true, true, true>), dim3(grid), dim3(kBS), 0,

@@ -900,17 +900,16 @@ void GpuCgSolver::setup() {
   }
   // a split rank (r6): the lean T3 runs whose neighbouring columns match, the generic T3 kernels (edge rows
   // recomputed from their codes) over the rest
-  if (opt_.form.p3buf != 0 && ar_ && p3_ && lean_split_ && split_t3_lean_ >= 0.0 && opt_.recurrence == 1 && n > 0)
+  // (on the packed-edge geometry only: its lean launch is the split kernel, COMBO, that takes the lean stretches)
+  if (opt_.form.p3buf != 0 && ar_ && p3_ && lean_split_ && split_t3_lean_ >= 0.0 && opt_.recurrence == 1 && n > 0 &&
+      opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.hooks.lean_packed != 0)
     p3buf_ = true;
   if (use_comm_ && world_ > 1) p3buf_ = all_ranks_agree_(p3buf_);
   if (p3buf_ && lean_split_) {
     // the lean launch on the packed-edge kernels (EP, depth 4 at 4 waves per SIMD) over 4 blocks per CU for
     // both parities -- the lean-only odd passes' geometry; one grid, so one generic list serves both
-    const bool packed = opt_.blocks_per_cu <= 0 && L_.ext_len < ((int64_t)1 << 29) && opt_.hooks.lean_packed != 0;
-    if (packed) {
-      g_int_ = ncu_ * 4;
-      lean_depth_even_ = lean_depth_odd_ = 14;
-    }
+    g_int_ = ncu_ * 4;  // (the packed-edge geometry: the p3buf condition above)
+    lean_depth_even_ = lean_depth_odd_ = 14;
     // the lean launch takes every lean stretch of its runs, the generic launch only the lines around the odd
     // slices: a listed range (at most 32 lines) per wave, a small grid beside the lean launch
     const int64_t nlines = (n + 63) / 64 / tr_all_.strip;
@@ -930,7 +929,7 @@ void GpuCgSolver::setup() {
     // default: one combined launch, the generic ranges' workgroups first (a second launch on the side stream
     // ran beside the lean one only when the graph put its branch on another hardware queue; on one stream
     // it added its whole ~22 us, profiles/r6/lsplit3); split_serial 0 / 1 keeps the two launches
-    combo_ = packed && ngen > 0 && opt_.hooks.split_serial < 0;
+    combo_ = ngen > 0 && opt_.hooks.split_serial < 0;
     if (combo_) {
       tr_int_.gen_blocks = (int32_t)(((ngen + 3) / 4 + 7) / 8 * 8);
       g_int_ += tr_int_.gen_blocks;
