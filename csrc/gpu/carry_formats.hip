@@ -320,7 +320,11 @@ bool split_generic_ranges(const uint64_t* dpat, int64_t ss, int64_t nl, int64_t 
   MCG_CHECK(dpat != nullptr && ss > 0 && nl > 0 && grid > 0 && maxlen > 0, "split ranges: bad geometry");
   int64_t runs = 0, chunk = 0;
   const int64_t jobs = carry_jobs((int64_t)grid * kWaves, ss, nl, runs, chunk);
-  const int cap = (int)std::min<int64_t>(1 << 22, 4 * jobs + 1024);
+  // never overflows: lean stretches are >= 3 lines, so a run of L lines leaves at most L / 4 + 1 gaps, and
+  // cutting them at maxlen lines adds at most L / maxlen pieces
+  const int64_t cap64 = nl * ss / 4 + nl * ss / maxlen + jobs + 1024;
+  MCG_CHECK(cap64 < ((int64_t)1 << 29), "split ranges: too many slices");
+  const int cap = (int)cap64;
   unsigned* cnt = nullptr;
   int32_t* out = nullptr;
   MCG_HIP(hipMallocAsync(reinterpret_cast<void**>(&cnt), sizeof(unsigned), stream), "device malloc failed(ranges)");
