@@ -283,6 +283,13 @@ def recipes(a) -> dict:
             for rep in ("a", "b") for g in (4096, 8192, 16384)
             for tag, script in (("nt", "bench.py"), ("plain", "var/tstore/run_bench.py"))
         ],
+        # r6: the combined split on short runs (4096^2 / 8192^2: 64-line runs, where the auto rule kept the
+        # generic kernels), forced against the generic fallback and the uniform matrix
+        "lsplit3short": [("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean_split'")] + [
+            (f"ab{n}", 600, f"{PY} -u bench/lean_split_ab.py --n {n} --steps {st} --warmup {st // 10} --reps 2 "
+                            "--arms uniform,generic,side")
+            for n, st in ((4096, 2000), (8192, 800))
+        ],
         # kernel trace of the split share with the generic launch ahead on one stream (per-call durations)
         "lsplit3tr": [
             ("tr", 600, prof("lsplit_ser", f"{PY} {ROOT}/bench/lean_split_ab.py --n 16384 --steps 300 --warmup 20 "

@@ -288,6 +288,26 @@ def test_lean_split_converges_like_the_generic_pass(mcg):
         assert abs(ts - tg) <= 0.05 * tg
 
 
+def test_lean_split_auto_on_short_runs_takes_three_buffers(mcg):
+    """Auto (r6): with three p buffers the split pays on short runs too (the lean launch takes the lean
+    stretches, its first workgroups the ~3 lines around each odd slice), so a 1024^2 user matrix with a
+    few changed rows -- 64-line runs, which the two-buffer rule left on the generic kernels -- takes it,
+    and converges like the generic pass."""
+    n = 1024
+    A = _poisson(n, 2).tolil()
+    d = A.diagonal()
+    for r in (n * 17 + 3, n * 400 + 300, n * 801 + 77):
+        d[r] += 0.75
+    A.setdiag(d)
+    p = mcg.csr_problem(A.tocsr(), rhs="random")
+    s = mcg.CGSolver(p, format="sellc8", recurrence=1, tol=1e-8, maxit=20000)
+    assert s.info["lean_split"] > 0.99 and s.info["p3buf"] and not s.info["lean_only"], s.info
+    og = mcg.CGSolver(p, format="sellc8", recurrence=1, lean_split=0, tol=1e-8, maxit=20000).solve()
+    os_ = s.solve()
+    assert os_["converged"] and abs(og["iterations"] - os_["iterations"]) <= 1
+    np.testing.assert_allclose(os_["x_local"], og["x_local"], rtol=1e-7, atol=1e-10)
+
+
 @pytest.mark.parametrize("world,lines", [(2, (1020,)), (4, (100, 1500))])
 def test_lean_split_mixed_ranks_match_one_rank(mcg, world, lines):
     """lean_split at P > 1 with split ranks next to lean-only ones: at 2048^2 a
