@@ -1164,6 +1164,12 @@ void cg_carry_ar(int cm, int param, int depth, const SellDev& S, const F1Vectors
       if (hipStreamSynchronize(s) != hipSuccess) return;
       if (hipMemcpyFromSymbol(d.data(), HIP_SYMBOL(g_carry_diag), d.size() * sizeof(unsigned long long)) != hipSuccess) return;
       const std::string path = std::string(fn) + "." + std::to_string(me);
+      unsigned long long rd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      (void)hipMemcpyFromSymbol(rd, HIP_SYMBOL(g_red_diag), sizeof(rd));
+      if (FILE* fr = std::fopen((path + ".red").c_str(), "w")) {  // the reduction tail's steps (f1_common.hpp)
+        for (int i = 0; i < 8; ++i) std::fprintf(fr, "%llu\n", rd[i]);
+        std::fclose(fr);
+      }
       if (FILE* fo = std::fopen(path.c_str(), "w")) {
         const int nw = std::min(grid * kWaves, kCarryDiagMax);
         for (int w = 0; w < nw; ++w)

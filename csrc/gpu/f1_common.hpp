@@ -117,17 +117,30 @@ __device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int 
 // compiler barrier, so no load of the hand-off can be hoisted above the atomic it depends on.  An
 // agent release fence on every block's add (buffer_wbl2, ~1.7 us a block) would order nothing the
 // write-through path has not ordered already.
+#if defined(MCG_CARRY_DIAG)
+// diagnostic build: the grid's last arriver's wall clock at each step of the reduction tail (profiles/r6/waves)
+__device__ unsigned long long g_red_diag[8];
+#define MCG_RED_T(i) (t_red[i] = wall_clock64())
+#else
+#define MCG_RED_T(i) ((void)0)
+#endif
 template <int NV, typename Book>
 __device__ __forceinline__ void last_arriver_reduce(const double* out, int pstride, const RedCtl& rc, Book&& book) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
+#if defined(MCG_CARRY_DIAG)
+  unsigned long long t_red[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  MCG_RED_T(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MCG_RED_T(1);
   const int g = (rc.base + (int)blockIdx.x) / kRedGroup;
   const int g0 = g * kRedGroup - rc.base;  // the group's first slot, relative to `out`
   const int gsize = min(kRedGroup, (int)gridDim.x - g0);
   unsigned old = 0;
   if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __shfl(old, 0, 64);
+  MCG_RED_T(2);
   if (old != (unsigned)(gsize - 1)) return;
   asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -136,13 +149,16 @@ __device__ __forceinline__ void last_arriver_reduce(const double* out, int pstri
   for (int q = 0; q < NV; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
 #pragma unroll
   for (int q = 0; q < NV; ++q) v[q] = eng::wave_sum(v[q]);
+  MCG_RED_T(3);
   if (lane == 0) {
 #pragma unroll
     for (int q = 0; q < NV; ++q) st_wt(&rc.lvl2[q * rc.l2s + g], v[q]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MCG_RED_T(4);
   if (lane == 0) old = __hip_atomic_fetch_add((gu32*)&rc.cnt[rc.top], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __shfl(old, 0, 64);
+  MCG_RED_T(5);
   if (old != (unsigned)(rc.ngroups - 1)) return;
   asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[rc.top], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -155,7 +171,13 @@ __device__ __forceinline__ void last_arriver_reduce(const double* out, int pstri
   }
 #pragma unroll
   for (int q = 0; q < NV; ++q) t[q] = eng::wave_sum(t[q]);
+  MCG_RED_T(6);
   if (lane == 0) book(t);
+#if defined(MCG_CARRY_DIAG)
+  MCG_RED_T(7);
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) g_red_diag[i] = t_red[i];
+#endif
 }
 
 __device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
