@@ -283,6 +283,15 @@ def recipes(a) -> dict:
             for rep in ("a", "b") for g in (4096, 8192, 16384)
             for tag, script in (("nt", "bench.py"), ("plain", "var/tstore/run_bench.py"))
         ],
+        # r6: the reduction's CgState snapshot loaded in the group winners (f1_common.hpp book_snap) against
+        # the tree before it (var/old: the previous commit's package and extension, built like var/colx)
+        "bsnap": [("pytest", 600, f"{PYTEST} tests/test_gpu_fused_reduce.py tests/test_gpu_solver.py")] + [
+            (f"{tag}_{g}_{rep}", 200, f"{PY} {script} --grid {g} --phases 0 "
+                                      + ("--steps 2000 --warmup 200" if g <= 4096 else "--steps 300 --warmup 30"))
+            for rep in ("a", "b", "c") for g in (4096, 8192, 16384)
+            for tag, script in (("snap", "bench.py"), ("old", "var/old/run_bench.py"))
+        ] + [(f"{tag}_512_{rep}", 200, f"{PY} {script} --problem poisson3d --grid 512 --phases 0")
+             for rep in ("a", "b") for tag, script in (("snap", "bench.py"), ("old", "var/old/run_bench.py"))],
         # r6: the combined split on short runs (4096^2 / 8192^2: 64-line runs, where the auto rule kept the
         # generic kernels), forced against the generic fallback and the uniform matrix
         "lsplit3short": [("pytest", 600, f"{PYTEST} -v tests/test_gpu_user_matrix.py -k 'lean_split'")] + [

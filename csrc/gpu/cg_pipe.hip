@@ -85,7 +85,8 @@ __device__ __forceinline__ void pipe_bookkeep(CgState* st, const double* tot, in
 
 // the in-kernel two-level reduction of f1_common.hpp with the pipelined bookkeeping
 __device__ __noinline__ void pipe_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
-  last_arriver_reduce<2>(out, pstride, rc, [&](const double* t) { pipe_bookkeep(st, t, rc.check, rc.first, tol); });
+  last_arriver_reduce<2>(
+      out, pstride, rc, [] { return 0; }, [&](const double* t, int) { pipe_bookkeep(st, t, rc.check, rc.first, tol); });
 }
 
 __global__ __launch_bounds__(kBS) void k_pipe_update(PipeVectors v, int64_t n, double* __restrict__ partials,

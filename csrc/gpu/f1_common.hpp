@@ -65,19 +65,53 @@ __device__ __forceinline__ void block_partial4(double a0, double a1, double a2, 
   }
 }
 
+// The CgState fields the bookkeeping reads.  Nothing writes them inside a pass before its grid's
+// last arriver does, so the in-kernel reduction loads them early, in every group winner, under the
+// round trips that follow (profiles/r6/waves: ~1 us of dependent misses a pass when loaded last).
+struct BookSnap {
+  double red[4];
+  int iter, done, clamps;
+};
+__device__ __forceinline__ BookSnap book_snap(const CgState* st) {
+  BookSnap s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s.red[q] = st->red[q];
+  s.iter = st->iter;
+  s.done = st->done;
+  s.clamps = st->clamps;
+  return s;
+}
+// the snapshot is the same in every lane: held in SGPRs across the reduction's round trips
+__device__ __forceinline__ double rfl_d(double x) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(x)));
+}
+__device__ __forceinline__ BookSnap rfl(const BookSnap& s) {
+  BookSnap u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) u.red[q] = rfl_d(s.red[q]);
+  u.iter = __builtin_amdgcn_readfirstlane(s.iter);
+  u.done = __builtin_amdgcn_readfirstlane(s.done);
+  u.clamps = __builtin_amdgcn_readfirstlane(s.clamps);
+  return u;
+}
+__device__ __forceinline__ int rfl(int x) { return x; }
+
 // CgState update from a fused pass's sums tot[4] (local; the all-reduce that follows makes them
 // global): the convergence / breakdown latch on the previous pass's GLOBAL r.r, a_prev, the new
-// sums, the iteration count.  cg_reduce_f1 mode 0 and the in-kernel reduction share this code.
-__device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int check, int first, double tol) {
+// sums, the iteration count.  cg_reduce_f1 mode 0 and the in-kernel reduction share this code;
+// s = book_snap(st) taken any time after the pass's start.
+__device__ __forceinline__ void f1_bookkeep(CgState* st, const BookSnap& s, const double* tot, int check, int first,
+                                            double tol) {
   auto zero = [&] {
     for (int q = 0; q < 4; ++q) st->red[q] = 0.0;
   };
-  if (st->done) { zero(); return; }
-  const double rr_prev = st->red[3];
+  if (s.done) { zero(); return; }
+  const double rr_prev = s.red[3];
   if (check && sqrt(rr_prev) < tol) {
     st->done = 1;
     st->converged = 1;
-    st->conv_iter = st->iter - 1;
+    st->conv_iter = s.iter - 1;
     st->rr_final = rr_prev;
     zero();
     return;
@@ -85,24 +119,27 @@ __device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int 
   if (check && !isfinite(rr_prev)) {
     st->done = 3;
     st->breakdown = 1;
-    st->conv_iter = st->iter - 1;
+    st->conv_iter = s.iter - 1;
     st->rr_final = rr_prev;
     zero();
     return;
   }
   // alpha of the pass whose (global) sums are being replaced — the pass after next pairs it
   // into its x update; same division as f1_scalars so the bits agree
-  st->a_prev = first ? 0.0 : st->red[3] / st->red[0];
+  st->a_prev = first ? 0.0 : s.red[3] / s.red[0];
   st->b_prev = 0.0;
   if (!first) {  // the clamp in f1_scalars, re-evaluated on the same global sums: count when it fired
-    const double a = st->red[3] / st->red[0];
-    const double est = fma(a * a, st->red[2], fma(-2.0 * a, st->red[1], st->red[3]));
-    if (!(est > 0.0)) st->clamps += 1;
-    st->b_prev = (est > 0.0 ? est : 0.0) / st->red[3];  // f1_scalars' beta, same operations: same bits
+    const double a = s.red[3] / s.red[0];
+    const double est = fma(a * a, s.red[2], fma(-2.0 * a, s.red[1], s.red[3]));
+    if (!(est > 0.0)) st->clamps = s.clamps + 1;
+    st->b_prev = (est > 0.0 ? est : 0.0) / s.red[3];  // f1_scalars' beta, same operations: same bits
   }
   for (int q = 0; q < 4; ++q) st->red[q] = tot[q];
   st->rr_new = tot[3];
-  st->iter += 1;
+  st->iter = s.iter + 1;
+}
+__device__ __forceinline__ void f1_bookkeep(CgState* st, const double* tot, int check, int first, double tol) {
+  f1_bookkeep(st, book_snap(st), tot, check, first, tol);
 }
 
 // In-kernel two-level last-arriver reduction (kernels.hpp RedCtl) of NV block sums, then
@@ -124,8 +161,9 @@ __device__ unsigned long long g_red_diag[8];
 #else
 #define MCG_RED_T(i) ((void)0)
 #endif
-template <int NV, typename Book>
-__device__ __forceinline__ void last_arriver_reduce(const double* out, int pstride, const RedCtl& rc, Book&& book) {
+template <int NV, typename Pre, typename Book>
+__device__ __forceinline__ void last_arriver_reduce(const double* out, int pstride, const RedCtl& rc, Pre&& pre,
+                                                    Book&& book) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
 #if defined(MCG_CARRY_DIAG)
@@ -144,9 +182,11 @@ __device__ __forceinline__ void last_arriver_reduce(const double* out, int pstri
   if (old != (unsigned)(gsize - 1)) return;
   asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_store((gu32*)&rc.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto snap = pre();  // issued ahead of the group's loads: its latency hides under theirs
   double v[NV];
 #pragma unroll
   for (int q = 0; q < NV; ++q) v[q] = lane < gsize ? ld_wt(&out[q * pstride + g0 + lane]) : 0.0;
+  snap = rfl(snap);  // arrives with the group's loads; into SGPRs before the sums' VGPR peak
 #pragma unroll
   for (int q = 0; q < NV; ++q) v[q] = eng::wave_sum(v[q]);
   MCG_RED_T(3);
@@ -172,7 +212,7 @@ __device__ __forceinline__ void last_arriver_reduce(const double* out, int pstri
 #pragma unroll
   for (int q = 0; q < NV; ++q) t[q] = eng::wave_sum(t[q]);
   MCG_RED_T(6);
-  if (lane == 0) book(t);
+  if (lane == 0) book(t, snap);
 #if defined(MCG_CARRY_DIAG)
   MCG_RED_T(7);
   if (lane == 0)
@@ -181,7 +221,9 @@ __device__ __forceinline__ void last_arriver_reduce(const double* out, int pstri
 }
 
 __device__ __noinline__ void f1_reduce_tail(double* out, int pstride, RedCtl rc, CgState* st, double tol) {
-  last_arriver_reduce<4>(out, pstride, rc, [&](const double* t) { f1_bookkeep(st, t, rc.check, rc.first, tol); });
+  last_arriver_reduce<4>(
+      out, pstride, rc, [&] { return book_snap(st); },
+      [&](const double* t, const BookSnap& s) { f1_bookkeep(st, s, t, rc.check, rc.first, tol); });
 }
 
 // end of a fused pass: block partials, then (rc on) the in-kernel reduction
